@@ -1,0 +1,85 @@
+"""ctypes binding of liborbx.so (include/orbx.h).
+
+The product path has exactly one implementation: the HIP library built from
+ar_orbslam2_amd/csrc for gfx950.  If the library is missing this module raises — there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "liborbx.so")
+
+KEYPOINT_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+     ("octave", "<i4"), ("class_id", "<i4")])
+
+ERRORS = {-1: "ORBX_EINVAL", -2: "ORBX_ENOMEM", -3: "ORBX_EDEVICE", -4: "ORBX_ECAPACITY",
+          -5: "ORBX_EUNSUPPORTED"}
+
+EXPORTS = [
+    "orbx_extractor_create", "orbx_extractor_destroy", "orbx_extractor_tables", "orbx_extract",
+    "orbx_extractor_pyramid", "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_capacity",
+    "orbx_plan_extract", "orbx_plan_outputs", "orbx_plan_sync", "orbx_plan_stream",
+    "orbx_plan_profile", "orbx_plan_profile_read", "orbx_descriptor_distance",
+    "orbx_search_by_bow_kf_f", "orbx_search_by_bow_kf_kf", "orbx_search_for_triangulation",
+    "orbx_epipole", "orbx_feature_vector",
+]
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, fn, rc):
+        super().__init__(f"{fn} failed: {ERRORS.get(rc, rc)}")
+        self.rc = rc
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class FeatVec(C.Structure):
+    _fields_ = [("n_nodes", C.c_int32), ("node_ids", C.c_void_p), ("node_offsets", C.c_void_p),
+                ("node_feats", C.c_void_p)]
+
+
+class BowSide(C.Structure):
+    _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("angle", C.c_void_p),
+                ("valid", C.c_void_p), ("fv", FeatVec)]
+
+
+class TriSide(C.Structure):
+    _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("keys_un", C.c_void_p),
+                ("u_right", C.c_void_p), ("has_mp", C.c_void_p), ("fv", FeatVec),
+                ("scale_factors", C.c_void_p), ("level_sigma2", C.c_void_p),
+                ("nlevels", C.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load liborbx.so; raises if the HIP library has not been built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (hipcc, gfx950). There is no CPU fallback.")
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orbx_plan_stream.restype = C.c_void_p
+    return _lib
+
+
+def check(fn, rc):
+    if rc != 0:
+        raise OrbxError(fn, rc)
+    return rc
+
+
+def ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)

@@ -1,0 +1,122 @@
+// orbx_api.hip — the drop-in C ABI around a plan: ORBextractor semantics for one host image
+// (ORB_SLAM2/src/ORBextractor.cc:404-460, 985-1045; ORB_SLAM2/include/ORBextractor.h:52-88).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "orbx_internal.h"
+
+using namespace orbx;
+
+extern "C" int orbx_plan_level_dims(const orbx_plan* P, int level, int* w, int* h);
+extern "C" int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out,
+                                        int64_t stride);
+
+struct orbx_extractor {
+  orbx_params params{};
+  Geometry tables;  // scale / sigma / features-per-level (no image size)
+  int device = 0;
+  orbx_plan* plan = nullptr;
+  int pw = 0, ph = 0;
+  uint8_t* d_img = nullptr;
+  bool has_run = false;
+};
+
+extern "C" {
+
+int orbx_extractor_create(const orbx_params* params, int hip_device, orbx_extractor** out) {
+  if (!params || !out || params->nlevels < 1 || params->nlevels > kMaxLevels ||
+      params->nfeatures < 0 || !(params->scale_factor > 0))
+    return ORBX_EINVAL;
+  orbx_extractor* ex = new (std::nothrow) orbx_extractor();
+  if (!ex) return ORBX_ENOMEM;
+  ex->params = *params;
+  ex->device = hip_device;
+  build_tables(*params, &ex->tables);
+  *out = ex;
+  return ORBX_OK;
+}
+
+int orbx_extractor_destroy(orbx_extractor* ex) {
+  if (!ex) return ORBX_OK;
+  if (ex->plan) orbx_plan_destroy(ex->plan);
+  if (ex->d_img) hipFree(ex->d_img);
+  delete ex;
+  return ORBX_OK;
+}
+
+int orbx_extractor_tables(const orbx_extractor* ex, int32_t* nlevels, float* scale_factors,
+                          float* inv_scale_factors, float* level_sigma2, float* inv_level_sigma2,
+                          int32_t* features_per_level) {
+  if (!ex) return ORBX_EINVAL;
+  const Geometry& g = ex->tables;
+  if (nlevels) *nlevels = g.nlevels;
+  for (int l = 0; l < g.nlevels; l++) {
+    if (scale_factors) scale_factors[l] = g.scale[l];
+    if (inv_scale_factors) inv_scale_factors[l] = g.inv_scale[l];
+    if (level_sigma2) level_sigma2[l] = g.sigma2[l];
+    if (inv_level_sigma2) inv_level_sigma2[l] = g.inv_sigma2[l];
+    if (features_per_level) features_per_level[l] = g.feats[l];
+  }
+  return ORBX_OK;
+}
+
+int orbx_extract(orbx_extractor* ex, const uint8_t* img, int32_t w, int32_t h, int64_t stride,
+                 orbx_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out) {
+  if (!ex || !n_out) return ORBX_EINVAL;
+  if (w <= 0 || h <= 0) {  // operator() returns early on an empty image (:987-988)
+    *n_out = -1;
+    return ORBX_OK;
+  }
+  if (!img || stride < w || cap < 0 || (cap > 0 && (!kps || !desc))) return ORBX_EINVAL;
+  ORBX_HIP(hipSetDevice(ex->device));
+  if (!ex->plan || ex->pw != w || ex->ph != h) {
+    if (ex->plan) orbx_plan_destroy(ex->plan);
+    ex->plan = nullptr;
+    if (ex->d_img) hipFree(ex->d_img);
+    ex->d_img = nullptr;
+    int rc = orbx_plan_create(&ex->params, w, h, 1, ex->device, &ex->plan);
+    if (rc != ORBX_OK) return rc;
+    ORBX_HIP(hipMalloc(&ex->d_img, (size_t)w * h));
+    ex->pw = w;
+    ex->ph = h;
+  }
+  hipStream_t s = (hipStream_t)orbx_plan_stream(ex->plan);
+  ORBX_HIP(hipMemcpy2DAsync(ex->d_img, w, img, stride, w, h, hipMemcpyHostToDevice, s));
+  int rc = orbx_plan_extract(ex->plan, ex->d_img, 1);
+  if (rc != ORBX_OK) return rc;
+  orbx_keypoint* d_kps;
+  uint8_t* d_desc;
+  int32_t* d_counts;
+  orbx_plan_outputs(ex->plan, &d_kps, &d_desc, &d_counts);
+  int32_t n = 0;
+  ORBX_HIP(hipMemcpyAsync(&n, d_counts, 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  ex->has_run = true;
+  *n_out = n;
+  if (n > cap) return ORBX_ECAPACITY;
+  if (n > 0) {
+    ORBX_HIP(hipMemcpyAsync(kps, d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(desc, d_desc, (size_t)32 * n, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+  }
+  return ORBX_OK;
+}
+
+int orbx_extractor_pyramid(orbx_extractor* ex, int32_t level, uint8_t* out, int64_t stride,
+                           int32_t* w, int32_t* h) {
+  if (!ex || !ex->plan || !ex->has_run) return ORBX_EINVAL;
+  int lw = 0, lh = 0;
+  int rc = orbx_plan_level_dims(ex->plan, level, &lw, &lh);
+  if (rc != ORBX_OK) return rc;
+  if (w) *w = lw;
+  if (h) *h = lh;
+  if (!out) return ORBX_OK;
+  if (stride < lw) return ORBX_EINVAL;
+  return orbx_plan_level_download(ex->plan, 0, level, out, stride);
+}
+
+}  // extern "C"

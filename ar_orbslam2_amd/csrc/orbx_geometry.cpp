@@ -1,0 +1,212 @@
+// orbx_geometry.cpp — host-side tables of a plan.  Every float expression below is evaluated
+// with the reference's types (ORB_SLAM2/src/ORBextractor.cc) and without contraction, so the
+// GPU path sees exactly the level sizes, cell grid, resize coefficients and octree frame the
+// reference computes.
+#include <math.h>
+
+#include <algorithm>
+#include <cstdio>
+
+#include "orbx_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace orbx {
+
+static inline int cv_round(double v) { return (int)nearbyint(v); }  // cvRound: half-even
+
+int report_hip(hipError_t e, const char* what) {
+  fprintf(stderr, "[orbx] HIP error %d (%s) at %s\n", (int)e, hipGetErrorString(e), what);
+  return ORBX_EDEVICE;
+}
+
+// ORBextractor::ORBextractor (ORBextractor.cc:404-460)
+void build_tables(const orbx_params& p, Geometry* g) {
+  const int L = p.nlevels;
+  const double sf = (double)p.scale_factor;  // member `double scaleFactor` (ORBextractor.h:104)
+  g->nlevels = L;
+  g->scale[0] = 1.0f;
+  g->sigma2[0] = 1.0f;
+  for (int i = 1; i < L; i++) {
+    g->scale[i] = (float)((double)g->scale[i - 1] * sf);
+    g->sigma2[i] = g->scale[i] * g->scale[i];
+  }
+  for (int i = 0; i < L; i++) {
+    g->inv_scale[i] = 1.0f / g->scale[i];
+    g->inv_sigma2[i] = 1.0f / g->sigma2[i];
+  }
+  const float factor = (float)(1.0f / sf);
+  float nDesired =
+      (float)p.nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)L));
+  int sum = 0;
+  for (int l = 0; l < L - 1; l++) {
+    g->feats[l] = cv_round(nDesired);
+    sum += g->feats[l];
+    nDesired *= factor;
+  }
+  g->feats[L - 1] = std::max(p.nfeatures - sum, 0);
+  // umax (ORBextractor.cc:445-459)
+  const int vmax = (int)floor(kHalfPatch * sqrtf(2.f) / 2 + 1);
+  const int vmin = (int)ceil(kHalfPatch * sqrtf(2.f) / 2);
+  const double hp2 = kHalfPatch * kHalfPatch;
+  int v, v0;
+  for (v = 0; v <= vmax; ++v) g->umax[v] = cv_round(sqrt(hp2 - v * v));
+  for (v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+    while (g->umax[v0] == g->umax[v0 + 1]) ++v0;
+    g->umax[v] = v0;
+    ++v0;
+  }
+}
+
+// cv::resize INTER_LINEAR coefficient tables (OpenCV 2.4 imgwarp.cpp).
+static void resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom* L) {
+  const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+  const double sx = 1. / inv_sx, sy = 1. / inv_sy;
+  L->coef_x = (int)g->xofs.size();
+  L->coef_y = (int)g->yofs.size();
+  int xmax = dw;
+  for (int dx = 0; dx < dw; dx++) {
+    float fx = (float)((dx + 0.5) * sx - 0.5);
+    int x0 = (int)floorf(fx);
+    fx -= x0;
+    if (x0 < 0) fx = 0, x0 = 0;
+    if (x0 + 1 >= sw) {
+      xmax = std::min(xmax, dx);
+      if (x0 >= sw - 1) fx = 0, x0 = sw - 1;
+    }
+    g->xofs.push_back(x0);
+    const float c0 = 1.f - fx, c1 = fx;
+    g->xa.push_back((int16_t)std::min(32767, std::max(-32768, cv_round(c0 * 2048))));
+    g->xa.push_back((int16_t)std::min(32767, std::max(-32768, cv_round(c1 * 2048))));
+  }
+  for (int dy = 0; dy < dh; dy++) {
+    float fy = (float)((dy + 0.5) * sy - 0.5);
+    const int y0 = (int)floorf(fy);
+    fy -= y0;
+    g->yofs.push_back(y0);
+    const float c0 = 1.f - fy, c1 = fy;
+    g->yb.push_back((int16_t)std::min(32767, std::max(-32768, cv_round(c0 * 2048))));
+    g->yb.push_back((int16_t)std::min(32767, std::max(-32768, cv_round(c1 * 2048))));
+  }
+  L->xmax = xmax;
+  int xs = 0;  // VResizeLinearVec_32s8u: 16-wide while x <= W-16, 4-wide while x < W-4
+  while (xs <= dw - 16) xs += 16;
+  while (xs < dw - 4) xs += 4;
+  L->vxs = xs;
+}
+
+int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string* why) {
+  if (p.nlevels < 1 || p.nlevels > kMaxLevels || p.nfeatures < 0 || !(p.scale_factor > 0)) {
+    if (why) *why = "bad params";
+    return ORBX_EINVAL;
+  }
+  build_tables(p, g);
+  g->w = w;
+  g->h = h;
+  g->ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
+  g->min_th = std::min(std::max(p.min_th_fast, 0), 255);
+  g->cells.clear();
+  g->xofs.clear();
+  g->yofs.clear();
+  g->xa.clear();
+  g->yb.clear();
+  int64_t pyr = 0;
+  int cand = 0, kp = 0, ncmax = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelGeom& L = g->lv[l];
+    L = LevelGeom{};
+    // ComputePyramid (ORBextractor.cc:1049-1051)
+    L.w = cv_round((float)w * g->inv_scale[l]);
+    L.h = cv_round((float)h * g->inv_scale[l]);
+    if (L.w < 1 || L.h < 1) {
+      if (why) *why = "empty pyramid level";
+      return ORBX_EUNSUPPORTED;
+    }
+    if (l > 0) {
+      const LevelGeom& P = g->lv[l - 1];
+      // cv::resize switches INTER_LINEAR to INTER_AREA at an exact 2x2 decimation; not
+      // implemented (the reference configurations use scaleFactor 1.2).
+      const double sx = 1. / ((double)L.w / P.w), sy = 1. / ((double)L.h / P.h);
+      if (fabs(sx - 2) < 2.2e-16 && fabs(sy - 2) < 2.2e-16) {
+        if (why) *why = "exact 2x decimation (INTER_AREA path)";
+        return ORBX_EUNSUPPORTED;
+      }
+      resize_tables(P.w, P.h, L.w, L.h, g, &L);
+      L.pyr_off = pyr;
+      pyr += ((int64_t)L.w * L.h + 255) / 256 * 256;
+    }
+    L.bxs = (L.w / 4) * 4;
+    L.scale = g->scale[l];
+    L.size = (float)(int)(kPatch * g->scale[l]);
+    L.nfeat = g->feats[l];
+    // ComputeKeyPointsOctTree cell grid (ORBextractor.cc:742-796)
+    const int minB = kEdge - 3;
+    const int maxBX = L.w - kEdge + 3, maxBY = L.h - kEdge + 3;
+    const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+    const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+    L.cell_begin = (int)g->cells.size();
+    L.cand_off = cand;
+    if (nCols > 0 && nRows > 0) {
+      const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+      for (int i = 0; i < nRows; i++) {
+        const float iniY = (float)(minB + i * hCell);
+        float maxY = iniY + hCell + 6;
+        if (iniY >= maxBY - 3) continue;
+        if (maxY > maxBY) maxY = (float)maxBY;
+        for (int j = 0; j < nCols; j++) {
+          const float iniX = (float)(minB + j * wCell);
+          float maxX = iniX + wCell + 6;
+          if (iniX >= maxBX - 6) continue;
+          if (maxX > maxBX) maxX = (float)maxBX;
+          CellGeom c{};
+          c.x0 = (int16_t)(int)iniX;
+          c.y0 = (int16_t)(int)iniY;
+          c.x1 = (int16_t)(int)maxX;
+          c.y1 = (int16_t)(int)maxY;
+          c.offx = (int16_t)(j * wCell);
+          c.offy = (int16_t)(i * hCell);
+          c.level = (int16_t)l;
+          const int dc = c.x1 - c.x0 - 6, dr = c.y1 - c.y0 - 6;
+          // strict 8-neighbour NMS survivors form an independent set of the king graph
+          c.slot_cap = (dc > 0 && dr > 0) ? ((dc + 1) / 2) * ((dr + 1) / 2) : 0;
+          c.slot_off = cand;
+          cand += c.slot_cap;
+          g->cells.push_back(c);
+        }
+      }
+      // DistributeOctTree frame (ORBextractor.cc:530-532)
+      L.W = maxBX - minB;
+      L.H = maxBY - minB;
+      L.nini = (int)roundf(static_cast<float>(L.W) / L.H);
+      if (L.nini < 1 || L.nini > kMaxIni) {
+        if (why) *why = "octree initial column count out of range (extreme aspect ratio)";
+        return ORBX_EUNSUPPORTED;
+      }
+      L.hx = static_cast<float>(L.W) / L.nini;
+      for (int i = 0; i <= L.nini; i++) L.ini_x[i] = (int)(L.hx * static_cast<float>(i));
+      if (L.W >= 4096 || L.H >= 4096) {
+        if (why) *why = "level too large for 12-bit key packing";
+        return ORBX_EUNSUPPORTED;
+      }
+    }
+    L.ncells = (int)g->cells.size() - L.cell_begin;
+    L.cand_cap = cand - L.cand_off;
+    ncmax = std::max(ncmax, L.ncells);
+    L.node_cap = L.ncells ? std::max(L.nfeat + 3, 4 * L.nini + 4) : 1;
+    L.kp_off = kp;
+    L.kp_cap = L.node_cap;
+    kp += L.kp_cap;
+    g->node_cap_max = std::max(g->node_cap_max, L.node_cap);
+  }
+  if (cand >= (1 << 24)) {
+    if (why) *why = "candidate capacity exceeds 2^24";
+    return ORBX_EUNSUPPORTED;
+  }
+  g->pyr_bytes = std::max<int64_t>(pyr, 256);
+  g->cand_total = cand;
+  g->kp_total = kp;
+  (void)ncmax;
+  return ORBX_OK;
+}
+
+}  // namespace orbx

@@ -1,0 +1,193 @@
+/*
+ * orbx.h — C ABI of the MI355X ORB front end (drop-in for ORB-SLAM2's ORBextractor /
+ * ORBmatcher hot path).  Plain pointers and sizes only; no torch, HIP or OpenCV types.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference tree):
+ *   orbx_extractor_create   ORBextractor::ORBextractor        ORB_SLAM2/include/ORBextractor.h:52-53,
+ *                                                             ORB_SLAM2/src/ORBextractor.cc:404-460
+ *   orbx_extractor_tables   GetLevels/GetScaleFactor(s)/...    ORB_SLAM2/include/ORBextractor.h:64-86
+ *   orbx_extract            ORBextractor::operator()          ORB_SLAM2/include/ORBextractor.h:61-62,
+ *                                                             ORB_SLAM2/src/ORBextractor.cc:985-1045
+ *   orbx_extractor_pyramid  ORBextractor::mvImagePyramid      ORB_SLAM2/include/ORBextractor.h:88
+ *   orbx_descriptor_distance ORBmatcher::DescriptorDistance   ORB_SLAM2/src/ORBmatcher.cc:1650-1666
+ *   orbx_search_by_bow_kf_f  ORBmatcher::SearchByBoW(KF*,F&)   ORB_SLAM2/src/ORBmatcher.cc:159-288
+ *   orbx_search_by_bow_kf_kf ORBmatcher::SearchByBoW(KF*,KF*)  ORB_SLAM2/src/ORBmatcher.cc:525-658
+ *   orbx_search_for_triangulation
+ *                           ORBmatcher::SearchForTriangulation ORB_SLAM2/src/ORBmatcher.cc:660-826
+ *   orbx_feature_vector     TemplatedVocabulary::transform(levelsup) node ids
+ *                           ORB_SLAM2/Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1127-1259
+ *
+ * Error convention: every function returns 0 on success or a negative ORBX_E* code; nothing
+ * throws across the ABI.  The reference has no error returns (asserts are compiled out,
+ * ORB_SLAM2/CMakeLists.txt:10-11); callers that must never fail map a negative code to
+ * "no features / no matches".
+ *
+ * Threading: an orbx_extractor is not reentrant (like ORBextractor, which mutates
+ * mvImagePyramid); distinct extractors may run concurrently.  Matcher entry points are
+ * stateless and reentrant (ORBmatcher is called from the Tracking, LocalMapping and
+ * LoopClosing threads at once).
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_ABI_VERSION 1
+
+enum {
+  ORBX_OK = 0,
+  ORBX_EINVAL = -1,     /* bad argument (null pointer, size out of range)          */
+  ORBX_ENOMEM = -2,     /* device or host allocation failed                        */
+  ORBX_EDEVICE = -3,    /* HIP runtime error                                        */
+  ORBX_ECAPACITY = -4,  /* caller buffer too small; *n_out holds the needed count   */
+  ORBX_EUNSUPPORTED = -5 /* configuration outside what the path implements          */
+};
+
+/* == cv::KeyPoint (OpenCV 2.4): {pt.x, pt.y, size, angle, response, octave, class_id}, 28 B.
+ * SURVEY §8a A11. */
+typedef struct {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} orbx_keypoint;
+
+/* ORBextractor constructor arguments (ORB_SLAM2/include/ORBextractor.h:52-53). */
+typedef struct {
+  int32_t nfeatures;
+  float scale_factor;
+  int32_t nlevels;
+  int32_t ini_th_fast;
+  int32_t min_th_fast;
+} orbx_params;
+
+/* A DBoW2::FeatureVector in CSR form (std::map<NodeId, vector<unsigned>>,
+ * FeatureVector.h:21-52): node_ids ascending; node_offsets[n_nodes+1]; node_feats holds the
+ * feature indices of node k at [node_offsets[k], node_offsets[k+1]), ascending. */
+typedef struct {
+  int32_t n_nodes;
+  const uint32_t* node_ids;
+  const int32_t* node_offsets;
+  const int32_t* node_feats;
+} orbx_featvec;
+
+/* One side of SearchByBoW.  `valid[i]` = 1 when feature i has a usable MapPoint
+ * (pMP && !pMP->isBad(), ORBmatcher.cc:191-197, 561-583); may be NULL for the Frame side of
+ * the KF->Frame variant, which does not look at it. */
+typedef struct {
+  int32_t n;
+  const uint8_t* desc;   /* n x 32 B, row per feature */
+  const float* angle;    /* n keypoint angles (degrees) */
+  const uint8_t* valid;  /* n or NULL */
+  orbx_featvec fv;
+} orbx_bow_side;
+
+/* One keyframe of SearchForTriangulation (ORBmatcher.cc:660-826). */
+typedef struct {
+  int32_t n;
+  const uint8_t* desc;          /* n x 32 */
+  const orbx_keypoint* keys_un; /* mvKeysUn */
+  const float* u_right;         /* mvuRight (<0 = mono); NULL = all mono */
+  const uint8_t* has_mp;        /* 1 if GetMapPoint(i) != NULL; NULL = none */
+  orbx_featvec fv;
+  const float* scale_factors;   /* mvScaleFactors [nlevels] */
+  const float* level_sigma2;    /* mvLevelSigma2  [nlevels] */
+  int32_t nlevels;
+} orbx_tri_side;
+
+/* ------------------------------------------------------------------ extractor */
+typedef struct orbx_extractor orbx_extractor;
+
+/* Builds the scale / feature-per-level / umax tables (ORBextractor.cc:404-460) and binds a
+ * HIP stream on `hip_device`. */
+int orbx_extractor_create(const orbx_params* params, int hip_device, orbx_extractor** out);
+int orbx_extractor_destroy(orbx_extractor* ex);
+
+/* Table getters (ORBextractor.h:64-86).  Each array must hold nlevels entries; any may be
+ * NULL.  features_per_level = mnFeaturesPerLevel. */
+int orbx_extractor_tables(const orbx_extractor* ex, int32_t* nlevels, float* scale_factors,
+                          float* inv_scale_factors, float* level_sigma2,
+                          float* inv_level_sigma2, int32_t* features_per_level);
+
+/* ORBextractor::operator(): u8 gray image (w x h, row stride `stride` bytes, host memory)
+ * -> keypoints (level-major, scaled to level-0 coordinates) and n x 32 descriptors.
+ * `cap` is the capacity of kps/desc; on ORBX_ECAPACITY *n_out is the required count.
+ * An empty image (w==0 or h==0) returns ORBX_OK with *n_out = -1 and touches nothing,
+ * mirroring the early return at ORBextractor.cc:987-988. */
+int orbx_extract(orbx_extractor* ex, const uint8_t* img, int32_t w, int32_t h, int64_t stride,
+                 orbx_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out);
+
+/* mvImagePyramid export for the last orbx_extract call: level `level` (ROI only, the 19-px
+ * border is never read by the hot path) into `out` with row stride `stride`.
+ * If out is NULL only *w, *h are written. */
+int orbx_extractor_pyramid(orbx_extractor* ex, int32_t level, uint8_t* out, int64_t stride,
+                           int32_t* w, int32_t* h);
+
+/* ------------------------------------------------------------------ device batch plan
+ * Throughput path: a plan is bound to one extractor configuration, one image size and a
+ * maximum batch.  Inputs and outputs live in device memory (HBM); the plan's HIP stream
+ * runs everything asynchronously.  Used by bench.py and by multi-stream callers. */
+typedef struct orbx_plan orbx_plan;
+
+int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t max_batch,
+                     int hip_device, orbx_plan** out);
+int orbx_plan_destroy(orbx_plan* plan);
+/* Per-image output capacity (keypoints) of the plan. */
+int orbx_plan_capacity(const orbx_plan* plan, int32_t* kp_cap);
+/* d_imgs: device pointer, n_images dense images of w*h bytes (stride = w).  Enqueues the
+ * whole extract on the plan's stream; returns without waiting. */
+int orbx_plan_extract(orbx_plan* plan, const uint8_t* d_imgs, int32_t n_images);
+/* Device pointers of the outputs of the last run: kps [max_batch][kp_cap], desc
+ * [max_batch][kp_cap][32], counts [max_batch]. */
+int orbx_plan_outputs(orbx_plan* plan, orbx_keypoint** d_kps, uint8_t** d_desc,
+                      int32_t** d_counts);
+int orbx_plan_sync(orbx_plan* plan);
+/* Returns the plan's hipStream_t as an opaque pointer. */
+void* orbx_plan_stream(orbx_plan* plan);
+/* Stage timing (HIP events around each kernel, on the plan's stream).  enable=1 arms it
+ * and clears the accumulators; names/ms/launches are copied for up to `cap` stages. */
+int orbx_plan_profile(orbx_plan* plan, int32_t enable);
+int orbx_plan_profile_read(orbx_plan* plan, int32_t cap, char (*names)[32], double* total_ms,
+                           int64_t* launches, int32_t* n_stages);
+
+/* ------------------------------------------------------------------ matcher */
+/* ORBmatcher::DescriptorDistance on n row pairs (host pointers). */
+int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int32_t* out);
+
+/* SearchByBoW(KeyFrame*, Frame&): match[f] = KF feature index matched to frame feature f,
+ * or -1 (vpMapPointMatches[f] = KF MapPoint of that index).  Returns count in *nmatches. */
+int orbx_search_by_bow_kf_f(const orbx_bow_side* kf, const orbx_bow_side* f, float nnratio,
+                            int32_t check_ori, int32_t* match, int32_t* nmatches);
+
+/* SearchByBoW(KeyFrame*, KeyFrame*): match12[i1] = KF2 index or -1. */
+int orbx_search_by_bow_kf_kf(const orbx_bow_side* kf1, const orbx_bow_side* kf2, float nnratio,
+                             int32_t check_ori, int32_t* match12, int32_t* nmatches);
+
+/* SearchForTriangulation: pairs (idx1, idx2) ascending in idx1, up to kf1->n pairs.
+ * F12 row-major 3x3 f32 (cv::Mat F12.at<float>(r,c) = F12[3r+c]); (ex, ey) the epipole of
+ * KF1's centre in KF2 (ORBmatcher.cc:667-673; orbx_epipole computes it). */
+int orbx_search_for_triangulation(const orbx_tri_side* kf1, const orbx_tri_side* kf2,
+                                  const float F12[9], float ex, float ey, int32_t only_stereo,
+                                  float nnratio, int32_t check_ori, int32_t* pairs,
+                                  int32_t* nmatches);
+
+/* Epipole exactly as ORBmatcher.cc:667-673 evaluates it (C2 = R2w*Cw + t2w, f32). */
+int orbx_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx, float fy,
+                 float cx, float cy, float* ex, float* ey);
+
+/* ------------------------------------------------------------------ vocabulary
+ * DBoW2 node ids for the matchers: per feature, the greedy Hamming descent of
+ * TemplatedVocabulary::transform (TemplatedVocabulary.h:1218-1259) stopped at level
+ * L - levelsup.  The tree is given as a complete k-ary layout: level-l nodes stored
+ * contiguously, children of node j of level l at [j*k, j*k+k) of level l+1; node ids follow
+ * DBoW2's file order (root 0, then breadth-first). */
+int orbx_feature_vector(const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
+                        const uint8_t* desc, int32_t n, uint32_t* node_of_feature);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBX_H */

@@ -1,0 +1,291 @@
+"""ctypes binding of the CPU oracle (oracle/orb_oracle.cc).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker.  The product package (ar_orbslam2_amd) never imports it.
+Parity status: see orb_oracle.h — pinned by known-answer tests from the reference's own
+tables; parity against real OpenCV 2.4 primitives is unpinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liborb_oracle.so")
+_lib = None
+
+KEYPOINT_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+     ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class FeatVec(C.Structure):
+    _fields_ = [("n_nodes", C.c_int32), ("node_ids", C.c_void_p), ("node_offsets", C.c_void_p),
+                ("node_feats", C.c_void_p)]
+
+
+class BowSide(C.Structure):
+    _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("angle", C.c_void_p),
+                ("valid", C.c_void_p), ("fv", FeatVec)]
+
+
+class TriSide(C.Structure):
+    _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("keys_un", C.c_void_p),
+                ("u_right", C.c_void_p), ("has_mp", C.c_void_p), ("fv", FeatVec),
+                ("scale_factors", C.c_void_p), ("level_sigma2", C.c_void_p),
+                ("nlevels", C.c_int32)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7):
+    return Params(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast)
+
+
+def extract(img, p=None, tie_mode=0, cap=None, want_pyramid=False):
+    """ORBextractor::operator() restated.  Returns (keypoints structured array, desc [n,32])
+    or, with want_pyramid, also the list of pyramid levels and pre-octree candidate counts."""
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = cap or max(4 * p.nfeatures + 64, 256)
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    lw = np.zeros(p.nlevels, np.int32)
+    lh = np.zeros(p.nlevels, np.int32)
+    ncand = np.zeros(p.nlevels, np.int32)
+    pyr_cap = int(w * h * 4 + 1024) if want_pyramid else 0
+    pyr = np.zeros(pyr_cap, np.uint8) if want_pyramid else None
+    L = lib()
+    L.oracle_extract_ex.restype = C.c_int
+    rc = L.oracle_extract_ex(C.byref(p), _p(img), C.c_int(w), C.c_int(h), C.c_int64(w),
+                             C.c_int(tie_mode), _p(kps), _p(desc), C.c_int(cap), C.byref(n),
+                             _p(pyr), C.c_int64(pyr_cap), _p(lw), _p(lh), _p(ncand))
+    if rc != 0:
+        raise RuntimeError(f"oracle_extract failed rc={rc}")
+    k = n.value
+    out = (kps[:k].copy(), desc[:k].copy())
+    if not want_pyramid:
+        return out
+    levels, off = [], 0
+    for l in range(p.nlevels):
+        sz = int(lw[l]) * int(lh[l])
+        levels.append(pyr[off:off + sz].reshape(int(lh[l]), int(lw[l])).copy())
+        off += sz
+    return out + (levels, ncand.copy())
+
+
+def extract_rc(img, p=None):
+    """Status code only (for edge-case tests)."""
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape if img.ndim == 2 else (0, 0)
+    cap = 4 * p.nfeatures + 64
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(123456)
+    rc = lib().oracle_extract(C.byref(p), _p(img), C.c_int(w), C.c_int(h), C.c_int64(max(w, 1)),
+                              C.c_int(0), _p(kps), _p(desc), C.c_int(cap), C.byref(n))
+    return rc, n.value
+
+
+def tables(p=None, w=640, h=480):
+    p = p or params()
+    n = p.nlevels
+    f = lambda: np.zeros(n, np.float32)
+    scale, inv, s2, is2 = f(), f(), f(), f()
+    fpl = np.zeros(n, np.int32)
+    umax = np.zeros(16, np.int32)
+    lw = np.zeros(n, np.int32)
+    lh = np.zeros(n, np.int32)
+    rc = lib().oracle_tables(C.byref(p), _p(scale), _p(inv), _p(s2), _p(is2), _p(fpl), _p(umax),
+                             _p(lw), _p(lh), C.c_int(w), C.c_int(h))
+    assert rc == 0
+    return dict(scale=scale, inv_scale=inv, sigma2=s2, inv_sigma2=is2, features_per_level=fpl,
+                umax=umax, level_w=lw, level_h=lh)
+
+
+def resize_linear(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear(_p(src), C.c_int(src.shape[1]), C.c_int(src.shape[0]),
+                               C.c_int64(src.shape[1]), _p(dst), C.c_int(dw), C.c_int(dh),
+                               C.c_int64(dw))
+    return dst
+
+
+def gaussian7(src):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    lib().oracle_gaussian7(_p(src), C.c_int(src.shape[1]), C.c_int(src.shape[0]), _p(dst))
+    return dst
+
+
+def fast_atan2(y, x):
+    f = lib().oracle_fast_atan2
+    f.restype = C.c_float
+    f.argtypes = [C.c_float, C.c_float]
+    return f(y, x)
+
+
+def sincosf(x):
+    s, c = C.c_float(), C.c_float()
+    lib().oracle_sincosf(C.c_float(x), C.byref(s), C.byref(c))
+    return s.value, c.value
+
+
+def fast_roi(roi, t):
+    roi = np.ascontiguousarray(roi, np.uint8)
+    rows, cols = roi.shape
+    cap = rows * cols
+    xs = np.zeros(cap, np.int32)
+    ys = np.zeros(cap, np.int32)
+    sc = np.zeros(cap, np.int32)
+    n = lib().oracle_fast_roi(_p(roi), C.c_int(rows), C.c_int(cols), C.c_int64(cols), C.c_int(t),
+                              _p(xs), _p(ys), _p(sc), C.c_int(cap))
+    return xs[:n].copy(), ys[:n].copy(), sc[:n].copy()
+
+
+def fast_score(img, x, y):
+    img = np.ascontiguousarray(img, np.uint8)
+    ptr = img.ctypes.data + int(y) * img.shape[1] + int(x)
+    return lib().oracle_fast_score(C.c_void_p(ptr), C.c_int64(img.shape[1]))
+
+
+def ic_angle(img, x, y):
+    img = np.ascontiguousarray(img, np.uint8)
+    f = lib().oracle_ic_angle
+    f.restype = C.c_float
+    return f(_p(img), C.c_int64(img.shape[1]), C.c_int(x), C.c_int(y))
+
+
+def orb_descriptor(blurred, x, y, angle):
+    blurred = np.ascontiguousarray(blurred, np.uint8)
+    d = np.zeros(32, np.uint8)
+    lib().oracle_orb_descriptor(_p(blurred), C.c_int64(blurred.shape[1]), C.c_int(x), C.c_int(y),
+                                C.c_float(angle), _p(d))
+    return d
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oracle_descriptor_distance(_p(a), _p(b))
+
+
+# ------------------------------------------------------------------ matcher sides
+class _Keep:
+    """Holds numpy buffers alive for the lifetime of a ctypes side struct."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def featvec_struct(fv):
+    node_ids, offsets, feats = fv
+    k = _Keep(node_ids=np.ascontiguousarray(node_ids, np.uint32),
+              offsets=np.ascontiguousarray(offsets, np.int32),
+              feats=np.ascontiguousarray(feats, np.int32))
+    s = FeatVec(len(k.node_ids), _p(k.node_ids), _p(k.offsets), _p(k.feats))
+    return s, k
+
+
+def bow_side(desc, angle, valid, fv):
+    desc = np.ascontiguousarray(desc, np.uint8)
+    angle = np.ascontiguousarray(angle, np.float32)
+    valid = None if valid is None else np.ascontiguousarray(valid, np.uint8)
+    fvs, fk = featvec_struct(fv)
+    s = BowSide(desc.shape[0], _p(desc), _p(angle), _p(valid), fvs)
+    return s, _Keep(desc=desc, angle=angle, valid=valid, fk=fk)
+
+
+def tri_side(desc, keys_un, u_right, has_mp, fv, scale_factors, level_sigma2):
+    desc = np.ascontiguousarray(desc, np.uint8)
+    keys_un = np.ascontiguousarray(keys_un, KEYPOINT_DTYPE)
+    u_right = None if u_right is None else np.ascontiguousarray(u_right, np.float32)
+    has_mp = None if has_mp is None else np.ascontiguousarray(has_mp, np.uint8)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    s2 = np.ascontiguousarray(level_sigma2, np.float32)
+    fvs, fk = featvec_struct(fv)
+    s = TriSide(desc.shape[0], _p(desc), _p(keys_un), _p(u_right), _p(has_mp), fvs, _p(sf),
+                _p(s2), len(sf))
+    return s, _Keep(desc=desc, keys_un=keys_un, u_right=u_right, has_mp=has_mp, sf=sf, s2=s2,
+                    fk=fk)
+
+
+def search_by_bow_kf_f(kf, f, nnratio=0.7, check_ori=True):
+    """kf, f: dicts with desc, angle, valid (kf only), fv=(node_ids, offsets, feats)."""
+    ks, kk = bow_side(kf["desc"], kf["angle"], kf.get("valid"), kf["fv"])
+    fs, fk = bow_side(f["desc"], f["angle"], None, f["fv"])
+    match = np.full(f["desc"].shape[0], -1, np.int32)
+    n = lib().oracle_search_by_bow_kf_f(C.byref(ks), C.byref(fs), C.c_float(nnratio),
+                                        C.c_int(int(check_ori)), _p(match))
+    return n, match
+
+
+def search_by_bow_kf_kf(kf1, kf2, nnratio=0.75, check_ori=True):
+    s1, k1 = bow_side(kf1["desc"], kf1["angle"], kf1.get("valid"), kf1["fv"])
+    s2, k2 = bow_side(kf2["desc"], kf2["angle"], kf2.get("valid"), kf2["fv"])
+    match = np.full(kf1["desc"].shape[0], -1, np.int32)
+    n = lib().oracle_search_by_bow_kf_kf(C.byref(s1), C.byref(s2), C.c_float(nnratio),
+                                         C.c_int(int(check_ori)), _p(match))
+    return n, match
+
+
+def search_for_triangulation(kf1, kf2, F12, ex, ey, only_stereo=False, nnratio=0.6,
+                             check_ori=False):
+    s1, k1 = tri_side(kf1["desc"], kf1["keys"], kf1.get("u_right"), kf1.get("has_mp"), kf1["fv"],
+                      kf1["scale_factors"], kf1["level_sigma2"])
+    s2, k2 = tri_side(kf2["desc"], kf2["keys"], kf2.get("u_right"), kf2.get("has_mp"), kf2["fv"],
+                      kf2["scale_factors"], kf2["level_sigma2"])
+    F = np.ascontiguousarray(F12, np.float32).reshape(9)
+    pairs = np.zeros((max(1, kf1["desc"].shape[0]), 2), np.int32)
+    n = lib().oracle_search_for_triangulation(C.byref(s1), C.byref(s2), _p(F), C.c_float(ex),
+                                              C.c_float(ey), C.c_int(int(only_stereo)),
+                                              C.c_float(nnratio), C.c_int(int(check_ori)),
+                                              _p(pairs))
+    return n, pairs[:n].copy()
+
+
+def epipole(R2w, t2w, Cw, fx, fy, cx, cy):
+    ex, ey = C.c_float(), C.c_float()
+    R = np.ascontiguousarray(R2w, np.float32).reshape(9)
+    t = np.ascontiguousarray(t2w, np.float32).reshape(3)
+    c = np.ascontiguousarray(Cw, np.float32).reshape(3)
+    lib().oracle_epipole(_p(R), _p(t), _p(c), C.c_float(fx), C.c_float(fy), C.c_float(cx),
+                         C.c_float(cy), C.byref(ex), C.byref(ey))
+    return ex.value, ey.value
+
+
+def feature_vector(voc_desc, k, L, levelsup, desc):
+    voc_desc = np.ascontiguousarray(voc_desc, np.uint8)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    out = np.zeros(desc.shape[0], np.uint32)
+    lib().oracle_feature_vector(_p(voc_desc), C.c_int(k), C.c_int(L), C.c_int(levelsup), _p(desc),
+                                C.c_int(desc.shape[0]), _p(out))
+    return out

@@ -1,0 +1,73 @@
+/*
+ * orb_oracle.h — CPU restatement of the reference ORB front end.  TEST INFRASTRUCTURE ONLY:
+ * imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.
+ * Never linked into, called by, or used as a fallback for the product library.
+ *
+ * Parity status: the ORB-SLAM2 logic is restated from ORB_SLAM2/src/ORBextractor.cc and
+ * ORB_SLAM2/src/ORBmatcher.cc (cited per function in orb_oracle.cc); the OpenCV 2.4
+ * primitives it calls (FAST, resize INTER_LINEAR, GaussianBlur, fastAtan2, cvRound) are
+ * restated from their published 2.4 algorithm.  The reference needs
+ * OpenCV 2.4, which is absent, so it cannot be built here: the oracle is pinned
+ * by known-answer tests derived from the reference's own tables (umax, per-level feature
+ * counts, pattern checksum, scale tables) and an exhaustive sincosf check against the host
+ * glibc; bit parity against real OpenCV 2.4 primitives is UNPINNED.
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+#include "../include/orbx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* tie_mode for DistributeOctTree's final sort:
+ *   0 = canonical (size, creation sequence) — the contract shared with the GPU path;
+ *   1 = faithful (size, heap address) — the reference's own, non-deterministic order. */
+int oracle_extract(const orbx_params* p, const uint8_t* img, int w, int h, int64_t stride,
+                   int tie_mode, orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+
+/* Same as oracle_extract but also returns the per-level pyramid (levels packed densely,
+ * level l of size lw[l] x lh[l]) when pyr != NULL, and the pre-octree candidate counts. */
+int oracle_extract_ex(const orbx_params* p, const uint8_t* img, int w, int h, int64_t stride,
+                      int tie_mode, orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out,
+                      uint8_t* pyr, int64_t pyr_cap, int* lw, int* lh, int* n_candidates);
+
+int oracle_tables(const orbx_params* p, float* scale, float* inv_scale, float* sigma2,
+                  float* inv_sigma2, int* feats_per_level, int* umax16, int* level_w,
+                  int* level_h, int w, int h);
+
+/* primitives (known-answer tests) */
+void oracle_resize_linear(const uint8_t* src, int sw, int sh, int64_t sstride, uint8_t* dst,
+                          int dw, int dh, int64_t dstride);
+void oracle_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst);
+float oracle_fast_atan2(float y, float x);
+int oracle_fast_score(const uint8_t* center, int64_t stride); /* max(q0,-q1)-1 */
+/* FAST on one ROI (rows x cols, stride) at threshold t with NMS: xs, ys, scores in raster
+ * order; returns the count (<= cap). */
+int oracle_fast_roi(const uint8_t* roi, int rows, int cols, int64_t stride, int t, int* xs,
+                    int* ys, int* scores, int cap);
+float oracle_ic_angle(const uint8_t* img, int64_t stride, int cx, int cy);
+void oracle_orb_descriptor(const uint8_t* blurred, int64_t stride, int cx, int cy, float angle,
+                           uint8_t* desc32);
+void oracle_sincosf(float x, float* s, float* c);
+
+/* matcher (ORBmatcher.cc) */
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
+int oracle_search_by_bow_kf_f(const orbx_bow_side* kf, const orbx_bow_side* f, float nnratio,
+                              int check_ori, int32_t* match);
+int oracle_search_by_bow_kf_kf(const orbx_bow_side* kf1, const orbx_bow_side* kf2,
+                               float nnratio, int check_ori, int32_t* match12);
+int oracle_search_for_triangulation(const orbx_tri_side* kf1, const orbx_tri_side* kf2,
+                                    const float F12[9], float ex, float ey, int only_stereo,
+                                    float nnratio, int check_ori, int32_t* pairs);
+void oracle_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx,
+                    float fy, float cx, float cy, float* ex, float* ey);
+/* DBoW2 transform restricted to node ids (TemplatedVocabulary.h:1218-1259), complete
+ * k-ary breadth-first layout as in orbx.h. */
+void oracle_feature_vector(const uint8_t* voc_desc, int k, int L, int levelsup,
+                           const uint8_t* desc, int n, uint32_t* node_of_feature);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
