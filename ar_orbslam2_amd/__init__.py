@@ -6,5 +6,8 @@ include/orbx.h, implemented by hand-written gfx950 HIP kernels in csrc/ (liborbx
 """
 from ._ffi import KEYPOINT_DTYPE, LIB_PATH, OrbxError, lib  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
+from .matcher import ORBmatcher, epipole  # noqa: F401
+from .vocabulary import FeatureVector, Vocabulary  # noqa: F401
 
-__all__ = ["ORBextractor", "KEYPOINT_DTYPE", "OrbxError", "lib", "LIB_PATH"]
+__all__ = ["ORBextractor", "ORBmatcher", "FeatureVector", "Vocabulary", "epipole",
+           "KEYPOINT_DTYPE", "OrbxError", "lib", "LIB_PATH"]

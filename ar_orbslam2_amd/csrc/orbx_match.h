@@ -1,0 +1,72 @@
+// orbx_match.h — device-side problem descriptors for the matcher kernels (orbx_match.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbx.h"
+
+namespace orbx {
+
+// One side of SearchByBoW, all pointers in device memory.
+struct DevSide {
+  int n;
+  const uint8_t* desc;
+  const float* angle;
+  const uint8_t* valid;  // nullable: all valid
+  int n_nodes;
+  const uint32_t* node_ids;
+  const int* node_offsets;
+  const int* node_feats;
+};
+
+// mode 0 = SearchByBoW(KF, Frame): s1 = KF, s2 = Frame, match[F idx] = KF idx, accept <= 50.
+// mode 1 = SearchByBoW(KF1, KF2): match[KF1 idx] = KF2 idx, accept < 50, valid on both sides.
+struct BowProblem {
+  DevSide s1, s2;
+  int* match;  // pre-filled with -1
+  int* count;
+  int* error;  // set to 1 when a node has more candidates than a wave tracks
+  int mode;
+  float nnratio;
+  int check_ori;
+};
+
+struct DevFeatVec {
+  int n_nodes;
+  const uint32_t* node_ids;
+  const int* node_offsets;
+  const int* node_feats;
+};
+
+struct DevTriSide {
+  int n;
+  const uint8_t* desc;
+  const orbx_keypoint* keys_un;
+  const float* u_right;   // nullable: mono
+  const uint8_t* has_mp;  // nullable: none
+  DevFeatVec fv;
+  const float* scale_factors;
+  const float* level_sigma2;
+};
+
+struct TriProblem {
+  DevTriSide s1, s2;
+  float F[9];
+  float ex, ey;
+  int only_stereo;
+  int check_ori;
+  int* m12;    // [s1.n], pre-filled with -1
+  int* pairs;  // [s1.n][2]
+  int* count;
+};
+
+int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
+int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
+int launch_featvec(const uint8_t* d_voc, int k, int nid_level, const uint8_t* d_desc,
+                   int64_t desc_stride_img, const int* d_counts, int n_fixed, int max_n,
+                   uint32_t* d_out, int64_t out_stride_img, int nimg, hipStream_t s);
+int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,
+               uint32_t id_lo, int nb, uint32_t* d_ids, int* d_off, int* d_feats,
+               int64_t csr_stride, int* d_nn, int nimg, hipStream_t s);
+
+}  // namespace orbx

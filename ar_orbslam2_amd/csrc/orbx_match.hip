@@ -1,0 +1,766 @@
+// orbx_match.hip — gfx950 kernels for ORBmatcher::SearchByBoW (both overloads),
+// SearchForTriangulation, DescriptorDistance and the DBoW2 node-id transform feeding them.
+//
+//   k_bow_nodes   one wave per keyframe vocabulary node; KF features in node order, the node's
+//                 candidate features across lanes (popcount over 4 x u64), wave min/second-min
+//                 reduction (ORBmatcher.cc:187-250 / 557-622)
+//   k_bow_finish  one workgroup per problem: rotation histogram, ComputeThreeMaxima, filter
+//                 (ORBmatcher.cc:267-285 / 637-655, 1604-1645)
+//   k_tri_nodes   one wave per KF1 node, one lane per KF1 feature (ORBmatcher.cc:694-792)
+//   k_tri_finish  rotation filter + ordered (idx1 ascending) pair compaction (:794-823)
+//   k_featvec     TemplatedVocabulary::transform node ids (TemplatedVocabulary.h:1218-1259)
+//   k_csr         FeatureVector build: stable bucket sort of feature indices by node id
+//                 (FeatureVector.cpp:31-45)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "orbx_internal.h"
+#include "orbx_match.h"
+
+#pragma clang fp contract(off)
+
+namespace orbx {
+
+constexpr int kTH_LOW = 50;
+constexpr int kHISTO = 30;
+
+__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
+  const uint64_t* pa = (const uint64_t*)a;
+  const uint64_t* pb = (const uint64_t*)b;
+  return __popcll(pa[0] ^ pb[0]) + __popcll(pa[1] ^ pb[1]) + __popcll(pa[2] ^ pb[2]) +
+         __popcll(pa[3] ^ pb[3]);
+}
+
+__device__ __forceinline__ int hamming_regs(const uint64_t d[4], const uint8_t* b) {
+  const uint64_t* pb = (const uint64_t*)b;
+  return __popcll(d[0] ^ pb[0]) + __popcll(d[1] ^ pb[1]) + __popcll(d[2] ^ pb[2]) +
+         __popcll(d[3] ^ pb[3]);
+}
+
+__device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int rot_bin(float a1, float a2) {
+  const float factor = 1.0f / kHISTO;
+  float rot = a1 - a2;
+  if (rot < 0.0) rot += 360.0f;
+  int bin = (int)roundf(rot * factor);
+  if (bin == kHISTO) bin = 0;
+  return bin;
+}
+
+// ------------------------------------------------------------------ SearchByBoW
+__global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict__ probs) {
+  const BowProblem& P = probs[blockIdx.y];
+  const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (a >= P.s1.n_nodes) return;
+  const uint32_t id = P.s1.node_ids[a];
+  const int b = lower_bound_u32(P.s2.node_ids, P.s2.n_nodes, id);
+  if (b >= P.s2.n_nodes || P.s2.node_ids[b] != id) return;
+  const int f0 = P.s2.node_offsets[b], m = P.s2.node_offsets[b + 1] - f0;
+  if (m > 64 * 16) {  // more candidates than the per-lane matched bitmap holds
+    if (lane == 0) atomicOr(P.error, 1);
+    return;
+  }
+  const bool kfkf = P.mode == 1;
+  // candidate descriptors of chunk 0 stay in registers
+  uint64_t reg[4] = {0, 0, 0, 0};
+  int i2_0 = -1;
+  bool ok0 = false;
+  if (lane < m) {
+    i2_0 = P.s2.node_feats[f0 + lane];
+    const uint64_t* p = (const uint64_t*)(P.s2.desc + (int64_t)i2_0 * 32);
+    reg[0] = p[0]; reg[1] = p[1]; reg[2] = p[2]; reg[3] = p[3];
+    ok0 = !kfkf || !P.s2.valid || P.s2.valid[i2_0];
+  }
+  uint32_t matched = 0;  // bit c: candidate lane + 64c already matched in this call
+  for (int pa = P.s1.node_offsets[a]; pa < P.s1.node_offsets[a + 1]; pa++) {
+    const int i1 = P.s1.node_feats[pa];
+    if (P.s1.valid && !P.s1.valid[i1]) continue;
+    const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
+    const uint64_t d1[4] = {q[0], q[1], q[2], q[3]};
+    int b1 = 256, bp = 0x7FFFFFFF, b2 = 256;
+    for (int c = 0; c * 64 < m; c++) {
+      const int j = lane + 64 * c;
+      if (j >= m || (matched >> c) & 1) continue;
+      int dist;
+      if (c == 0) {
+        if (!ok0) continue;
+        uint64_t x[4] = {reg[0], reg[1], reg[2], reg[3]};
+        dist = hamming_regs(d1, (const uint8_t*)x);
+      } else {
+        const int i2 = P.s2.node_feats[f0 + j];
+        if (kfkf && P.s2.valid && !P.s2.valid[i2]) continue;
+        dist = hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32);
+      }
+      if (dist < b1) {
+        b2 = b1;
+        b1 = dist;
+        bp = j;
+      } else if (dist < b2) {
+        b2 = dist;
+      }
+    }
+    // wave merge of (best1, position, best2): keeps the first position of the minimum and the
+    // second order statistic, exactly what the sequential loop yields
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int ob1 = __shfl_xor(b1, o), obp = __shfl_xor(bp, o), ob2 = __shfl_xor(b2, o);
+      if (ob1 < b1 || (ob1 == b1 && obp < bp)) {
+        b2 = min(ob2, b1);
+        b1 = ob1;
+        bp = obp;
+      } else {
+        b2 = min(b2, ob1);
+      }
+    }
+    const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
+    if (pass && static_cast<float>(b1) < P.nnratio * static_cast<float>(b2)) {
+      if ((bp & 63) == lane) matched |= 1u << (bp >> 6);
+      if (lane == 0) {
+        const int i2 = P.s2.node_feats[f0 + bp];
+        if (kfkf) P.match[i1] = i2;
+        else P.match[i2] = i1;
+      }
+    }
+  }
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:1604-1645)
+__device__ void three_maxima(const int* h, int& ind1, int& ind2, int& ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  ind1 = ind2 = ind3 = -1;
+  for (int i = 0; i < kHISTO; i++) {
+    const int s = h[i];
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s;
+      ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) {
+    ind2 = -1;
+    ind3 = -1;
+  } else if (max3 < 0.1f * (float)max1) {
+    ind3 = -1;
+  }
+}
+
+// Rotation consistency filter + count.  Entries: mode 0 indexed by F feature (value = KF idx),
+// mode 1 / triangulation indexed by side-1 feature (value = side-2 idx).
+__global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict__ probs) {
+  const BowProblem& P = probs[blockIdx.x];
+  __shared__ int hist[kHISTO];
+  __shared__ int s_ind[3];
+  __shared__ int s_cnt;
+  const int tid = threadIdx.x;
+  if (tid < kHISTO) hist[tid] = 0;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  const bool kfkf = P.mode == 1;
+  const int n = kfkf ? P.s1.n : P.s2.n;
+  if (P.check_ori) {
+    for (int i = tid; i < n; i += 256) {
+      const int m = P.match[i];
+      if (m < 0) continue;
+      const int bin = kfkf ? rot_bin(P.s1.angle[i], P.s2.angle[m]) : rot_bin(P.s1.angle[m], P.s2.angle[i]);
+      atomicAdd(&hist[bin], 1);
+    }
+    __syncthreads();
+    if (tid == 0) three_maxima(hist, s_ind[0], s_ind[1], s_ind[2]);
+    __syncthreads();
+  }
+  int local = 0;
+  for (int i = tid; i < n; i += 256) {
+    const int m = P.match[i];
+    if (m < 0) continue;
+    if (P.check_ori) {
+      const int bin = kfkf ? rot_bin(P.s1.angle[i], P.s2.angle[m]) : rot_bin(P.s1.angle[m], P.s2.angle[i]);
+      if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
+        P.match[i] = -1;
+        continue;
+      }
+    }
+    local++;
+  }
+  atomicAdd(&s_cnt, local);
+  __syncthreads();
+  if (tid == 0) *P.count = s_cnt;
+}
+
+// ------------------------------------------------------------------ SearchForTriangulation
+// CheckDistEpipolarLine (ORBmatcher.cc:140-157) with the reference binary's FMA pattern
+// (SURVEY A.7).
+__device__ __forceinline__ bool epipolar_ok(float x1, float y1, float x2, float y2,
+                                            const float* F, float sigma2) {
+  const float a = __builtin_fmaf(x1, F[0], y1 * F[3]) + F[6];
+  const float b = __builtin_fmaf(x1, F[1], y1 * F[4]) + F[7];
+  const float c = __builtin_fmaf(y1, F[5], x1 * F[2]) + F[8];
+  const float num = __builtin_fmaf(b, y2, x2 * a) + c;
+  const float den = __builtin_fmaf(a, a, b * b);
+  if (den == 0) return false;
+  const float dsqr = num * num / den;
+  return (double)dsqr < 3.84 * (double)sigma2;
+}
+
+__global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict__ probs) {
+  const TriProblem& P = probs[blockIdx.y];
+  const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (a >= P.s1.fv.n_nodes) return;
+  const uint32_t id = P.s1.fv.node_ids[a];
+  const int b = lower_bound_u32(P.s2.fv.node_ids, P.s2.fv.n_nodes, id);
+  if (b >= P.s2.fv.n_nodes || P.s2.fv.node_ids[b] != id) return;
+  const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
+  for (int pa = P.s1.fv.node_offsets[a] + lane; pa < P.s1.fv.node_offsets[a + 1]; pa += 64) {
+    const int i1 = P.s1.fv.node_feats[pa];
+    if (P.s1.has_mp && P.s1.has_mp[i1]) continue;
+    const bool st1 = P.s1.u_right ? P.s1.u_right[i1] >= 0 : false;
+    if (P.only_stereo && !st1) continue;
+    const orbx_keypoint kp1 = P.s1.keys_un[i1];
+    const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
+    const uint64_t d1[4] = {q[0], q[1], q[2], q[3]};
+    int bestDist = kTH_LOW, bestIdx2 = -1;
+    for (int pb = f0; pb < f1; pb++) {
+      const int i2 = P.s2.fv.node_feats[pb];
+      if (P.s2.has_mp && P.s2.has_mp[i2]) continue;  // vbMatched2 is never set (:680, 728)
+      const bool st2 = P.s2.u_right ? P.s2.u_right[i2] >= 0 : false;
+      if (P.only_stereo && !st2) continue;
+      const int dist = hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32);
+      if (dist > kTH_LOW || dist > bestDist) continue;
+      const orbx_keypoint kp2 = P.s2.keys_un[i2];
+      if (!st1 && !st2) {
+        const float dex = P.ex - kp2.x, dey = P.ey - kp2.y;
+        if (__builtin_fmaf(dex, dex, dey * dey) < 100 * P.s2.scale_factors[kp2.octave]) continue;
+      }
+      if (epipolar_ok(kp1.x, kp1.y, kp2.x, kp2.y, P.F, P.s2.level_sigma2[kp2.octave])) {
+        bestIdx2 = i2;
+        bestDist = dist;
+      }
+    }
+    P.m12[i1] = bestIdx2;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict__ probs) {
+  const TriProblem& P = probs[blockIdx.x];
+  __shared__ int hist[kHISTO];
+  __shared__ int s_ind[3];
+  __shared__ int s_scan[257];
+  const int tid = threadIdx.x;
+  const int n = P.s1.n;
+  if (tid < kHISTO) hist[tid] = 0;
+  __syncthreads();
+  if (P.check_ori) {
+    for (int i = tid; i < n; i += 256) {
+      const int m = P.m12[i];
+      if (m >= 0) atomicAdd(&hist[rot_bin(P.s1.keys_un[i].angle, P.s2.keys_un[m].angle)], 1);
+    }
+    __syncthreads();
+    if (tid == 0) three_maxima(hist, s_ind[0], s_ind[1], s_ind[2]);
+    __syncthreads();
+  }
+  // ordered compaction over idx1 (chunked per thread for stability)
+  const int per = (n + 255) / 256;
+  const int beg = min(tid * per, n), end = min(beg + per, n);
+  int mine = 0;
+  for (int i = beg; i < end; i++) {
+    int m = P.m12[i];
+    if (m >= 0 && P.check_ori) {
+      const int bin = rot_bin(P.s1.keys_un[i].angle, P.s2.keys_un[m].angle);
+      if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
+        P.m12[i] = -1;
+        m = -1;
+      }
+    }
+    mine += m >= 0;
+  }
+  s_scan[tid] = mine;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int t = 0; t < 256; t++) {
+      const int x = s_scan[t];
+      s_scan[t] = acc;
+      acc += x;
+    }
+    s_scan[256] = acc;
+  }
+  __syncthreads();
+  int pos = s_scan[tid];
+  for (int i = beg; i < end; i++) {
+    const int m = P.m12[i];
+    if (m >= 0) {
+      P.pairs[2 * pos] = i;
+      P.pairs[2 * pos + 1] = m;
+      pos++;
+    }
+  }
+  if (tid == 0) *P.count = s_scan[256];
+}
+
+// ------------------------------------------------------------------ vocabulary + FeatureVector
+__global__ __launch_bounds__(256) void k_featvec(const uint8_t* __restrict__ voc, int k,
+                                                 int nid_level, const uint8_t* __restrict__ desc,
+                                                 int64_t desc_stride_img,
+                                                 const int* __restrict__ counts, int n_fixed,
+                                                 uint32_t* __restrict__ out,
+                                                 int64_t out_stride_img) {
+  const int img = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n = counts ? counts[img] : n_fixed;
+  if (i >= n) return;
+  const uint64_t* q = (const uint64_t*)(desc + img * desc_stride_img + (int64_t)i * 32);
+  const uint64_t d[4] = {q[0], q[1], q[2], q[3]};
+  uint32_t id = 0;
+  if (nid_level > 0) {
+    int64_t level_off = 1, level_size = 1, j = 0;
+    for (int lvl = 1; lvl <= nid_level; lvl++) {
+      level_size *= k;
+      const int64_t first = level_off + j * k;
+      int64_t best = first;
+      int bestd = hamming_regs(d, voc + first * 32);
+      for (int c = 1; c < k; c++) {
+        const int dd = hamming_regs(d, voc + (first + c) * 32);
+        if (dd < bestd) bestd = dd, best = first + c;
+      }
+      id = (uint32_t)best;
+      j = best - level_off;
+      level_off += level_size;
+    }
+  }
+  out[img * out_stride_img + i] = id;
+}
+
+// Stable bucket sort of feature indices by node id within [id_lo, id_lo + nb) (one workgroup
+// per image): node_ids ascending, offsets, feats ascending within each node.
+__global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_of,
+                                             int64_t node_stride, const int* __restrict__ counts,
+                                             int n_fixed, uint32_t id_lo, int nb,
+                                             uint32_t* __restrict__ node_ids,
+                                             int* __restrict__ offsets, int* __restrict__ feats,
+                                             int64_t csr_stride, int* __restrict__ n_nodes) {
+  extern __shared__ int sm[];
+  int* cnt = sm;       // nb
+  int* cur = sm + nb;  // nb
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const int n = counts ? counts[img] : n_fixed;
+  const uint32_t* nodes = node_of + img * node_stride;
+  uint32_t* oid = node_ids + img * csr_stride;
+  int* ooff = offsets + img * (csr_stride + 1);
+  int* of = feats + img * csr_stride;
+  for (int i = tid; i < nb; i += 256) cnt[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += 256) atomicAdd(&cnt[nodes[i] - id_lo], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0, nn = 0;
+    for (int b = 0; b < nb; b++) {
+      cur[b] = acc;
+      if (cnt[b]) {
+        oid[nn] = id_lo + b;
+        ooff[nn] = acc;
+        nn++;
+      }
+      acc += cnt[b];
+    }
+    ooff[nn] = acc;
+    n_nodes[img] = nn;
+  }
+  __syncthreads();
+  // stable placement by wave 0: chunks of 64 features in index order; a lane's rank inside its
+  // bucket = lanes below it with the same bucket (wave shuffles, no barrier inside the wave)
+  if (tid < 64) {
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int i = c0 + tid;
+      const int bk = i < n ? (int)(nodes[i] - id_lo) : -1;
+      int rank = 0, tot = 0;
+      bool last = true;
+      for (int j = 0; j < 64; j++) {
+        const int o = __shfl(bk, j);
+        if (o == bk) {
+          tot++;
+          if (j < tid) rank++;
+          if (j > tid) last = false;
+        }
+      }
+      const int base = i < n ? cur[bk] : 0;
+      if (i < n) of[base + rank] = i;
+      if (i < n && last) cur[bk] = base + tot;
+    }
+  }
+}
+
+__global__ void k_distance(const uint8_t* a, const uint8_t* b, int n, int* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = hamming32(a + (int64_t)i * 32, b + (int64_t)i * 32);
+}
+
+// ------------------------------------------------------------------ launchers
+int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s) {
+  if (nprob <= 0) return ORBX_OK;
+  if (max_nodes1 > 0)
+    hipLaunchKernelGGL(k_bow_nodes, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
+  hipLaunchKernelGGL(k_bow_finish, dim3(nprob), dim3(256), 0, s, d_probs);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_bow");
+}
+
+int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s) {
+  if (nprob <= 0) return ORBX_OK;
+  if (max_nodes1 > 0)
+    hipLaunchKernelGGL(k_tri_nodes, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
+  hipLaunchKernelGGL(k_tri_finish, dim3(nprob), dim3(256), 0, s, d_probs);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_tri");
+}
+
+int launch_featvec(const uint8_t* d_voc, int k, int nid_level, const uint8_t* d_desc,
+                   int64_t desc_stride_img, const int* d_counts, int n_fixed, int max_n,
+                   uint32_t* d_out, int64_t out_stride_img, int nimg, hipStream_t s) {
+  if (max_n <= 0 || nimg <= 0) return ORBX_OK;
+  hipLaunchKernelGGL(k_featvec, dim3((max_n + 255) / 256, nimg), dim3(256), 0, s, d_voc, k,
+                     nid_level, d_desc, desc_stride_img, d_counts, n_fixed, d_out, out_stride_img);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_featvec");
+}
+
+int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,
+               uint32_t id_lo, int nb, uint32_t* d_ids, int* d_off, int* d_feats,
+               int64_t csr_stride, int* d_nn, int nimg, hipStream_t s) {
+  if (nimg <= 0) return ORBX_OK;
+  const size_t smem = (size_t)(2 * nb) * 4;
+  if (smem > 64 * 1024) return ORBX_EUNSUPPORTED;
+  hipLaunchKernelGGL(k_csr, dim3(nimg), dim3(256), smem, s, d_node_of, node_stride, d_counts,
+                     n_fixed, id_lo, nb, d_ids, d_off, d_feats, csr_stride, d_nn);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_csr");
+}
+
+// ------------------------------------------------------------------ host-pointer ABI
+// Per-thread device workspace (ORBmatcher is called from three threads at once; each thread
+// gets its own stream and buffers).
+struct Workspace {
+  hipStream_t stream = nullptr;
+  char* d = nullptr;
+  size_t cap = 0;
+  int device = -1;
+  ~Workspace() {
+    if (d) hipFree(d);
+    if (stream) hipStreamDestroy(stream);
+  }
+  int reserve(size_t bytes) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (device != dev) {
+      if (d) hipFree(d);
+      if (stream) hipStreamDestroy(stream);
+      d = nullptr;
+      cap = 0;
+      stream = nullptr;
+      device = dev;
+    }
+    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
+      return ORBX_EDEVICE;
+    if (bytes <= cap) return ORBX_OK;
+    if (d) hipFree(d);
+    d = nullptr;
+    cap = std::max(bytes, cap * 2);
+    if (hipMalloc(&d, cap) != hipSuccess) {
+      cap = 0;
+      return ORBX_ENOMEM;
+    }
+    return ORBX_OK;
+  }
+};
+static thread_local Workspace tls_ws;
+
+// Packs host arrays into one staging buffer, uploads them with one copy.
+struct Stager {
+  std::vector<char> host;
+  struct Item {
+    size_t off;
+  };
+  size_t add(const void* p, size_t bytes) {
+    const size_t off = (host.size() + 15) & ~size_t(15);
+    host.resize(off + bytes);
+    if (p && bytes) memcpy(host.data() + off, p, bytes);
+    return off;
+  }
+};
+
+template <class T>
+static T* dptr(char* base, size_t off) {
+  return (T*)(base + off);
+}
+
+}  // namespace orbx
+
+using namespace orbx;
+
+namespace {
+
+struct SideOffs {
+  size_t desc, angle, valid, ids, offs, feats;
+};
+
+bool side_ok(const orbx_bow_side* s) {
+  return s && s->n >= 0 && (s->n == 0 || (s->desc && s->angle)) && s->fv.n_nodes >= 0 &&
+         (s->fv.n_nodes == 0 || (s->fv.node_ids && s->fv.node_offsets && s->fv.node_feats));
+}
+
+// Every feature index must be inside [0, n) so no kernel reads out of bounds.
+bool fv_ok(const orbx_featvec& fv, int n) {
+  if (fv.n_nodes == 0) return true;
+  if (fv.node_offsets[0] != 0) return false;
+  for (int k = 0; k < fv.n_nodes; k++) {
+    if (fv.node_offsets[k + 1] < fv.node_offsets[k]) return false;
+    if (k && fv.node_ids[k] <= fv.node_ids[k - 1]) return false;
+  }
+  for (int i = 0; i < fv.node_offsets[fv.n_nodes]; i++)
+    if (fv.node_feats[i] < 0 || fv.node_feats[i] >= n) return false;
+  return true;
+}
+
+SideOffs stage_side(Stager& st, const orbx_bow_side* s) {
+  SideOffs o;
+  o.desc = st.add(s->desc, (size_t)s->n * 32);
+  o.angle = st.add(s->angle, (size_t)s->n * 4);
+  o.valid = s->valid ? st.add(s->valid, (size_t)s->n) : (size_t)-1;
+  o.ids = st.add(s->fv.node_ids, (size_t)s->fv.n_nodes * 4);
+  o.offs = st.add(s->fv.node_offsets, (size_t)(s->fv.n_nodes + 1) * 4);
+  o.feats = st.add(s->fv.node_feats,
+                   (size_t)(s->fv.n_nodes ? s->fv.node_offsets[s->fv.n_nodes] : 0) * 4);
+  return o;
+}
+
+DevSide dev_side(char* base, const SideOffs& o, const orbx_bow_side* s) {
+  DevSide d;
+  d.n = s->n;
+  d.desc = dptr<const uint8_t>(base, o.desc);
+  d.angle = dptr<const float>(base, o.angle);
+  d.valid = o.valid == (size_t)-1 ? nullptr : dptr<const uint8_t>(base, o.valid);
+  d.n_nodes = s->fv.n_nodes;
+  d.node_ids = dptr<const uint32_t>(base, o.ids);
+  d.node_offsets = dptr<const int>(base, o.offs);
+  d.node_feats = dptr<const int>(base, o.feats);
+  return d;
+}
+
+int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int check_ori,
+            int mode, int32_t* match_out, int32_t* nmatches) {
+  if (!side_ok(s1) || !side_ok(s2) || !match_out || !nmatches) return ORBX_EINVAL;
+  if (!fv_ok(s1->fv, s1->n) || !fv_ok(s2->fv, s2->n)) return ORBX_EINVAL;
+  const int nout = mode == 1 ? s1->n : s2->n;
+  Stager st;
+  SideOffs o1 = stage_side(st, s1), o2 = stage_side(st, s2);
+  const size_t omatch = st.add(nullptr, (size_t)std::max(nout, 1) * 4);
+  const size_t ocount = st.add(nullptr, 16);
+  const size_t oprob = st.add(nullptr, sizeof(BowProblem));
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  BowProblem P;
+  P.s1 = dev_side(base, o1, s1);
+  P.s2 = dev_side(base, o2, s2);
+  P.match = dptr<int>(base, omatch);
+  P.count = dptr<int>(base, ocount);
+  P.error = dptr<int>(base, ocount + 4);
+  P.mode = mode;
+  P.nnratio = nnratio;
+  P.check_ori = check_ori;
+  memcpy(st.host.data() + oprob, &P, sizeof(P));
+  memset(st.host.data() + omatch, 0xFF, (size_t)std::max(nout, 1) * 4);
+  memset(st.host.data() + ocount, 0, 16);
+  hipStream_t s = tls_ws.stream;
+  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), st.host.size(), hipMemcpyHostToDevice, s));
+  rc = launch_bow(dptr<BowProblem>(base, oprob), 1, s1->fv.n_nodes, s);
+  if (rc) return rc;
+  int res[2] = {0, 0};
+  ORBX_HIP(hipMemcpyAsync(res, base + ocount, 8, hipMemcpyDeviceToHost, s));
+  if (nout > 0)
+    ORBX_HIP(hipMemcpyAsync(match_out, base + omatch, (size_t)nout * 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  if (res[1]) return ORBX_EUNSUPPORTED;
+  *nmatches = res[0];
+  return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_search_by_bow_kf_f(const orbx_bow_side* kf, const orbx_bow_side* f, float nnratio,
+                            int32_t check_ori, int32_t* match, int32_t* nmatches) {
+  return run_bow(kf, f, nnratio, check_ori, 0, match, nmatches);
+}
+
+int orbx_search_by_bow_kf_kf(const orbx_bow_side* kf1, const orbx_bow_side* kf2, float nnratio,
+                             int32_t check_ori, int32_t* match12, int32_t* nmatches) {
+  return run_bow(kf1, kf2, nnratio, check_ori, 1, match12, nmatches);
+}
+
+int orbx_search_for_triangulation(const orbx_tri_side* k1, const orbx_tri_side* k2,
+                                  const float F12[9], float ex, float ey, int32_t only_stereo,
+                                  float /*nnratio: not used by the reference here*/,
+                                  int32_t check_ori, int32_t* pairs, int32_t* nmatches) {
+  const orbx_tri_side* ks[2] = {k1, k2};
+  for (const orbx_tri_side* k : ks) {
+    if (!k || k->n < 0 || (k->n && (!k->desc || !k->keys_un)) || !k->scale_factors ||
+        !k->level_sigma2 || k->nlevels < 1 || k->fv.n_nodes < 0 ||
+        (k->fv.n_nodes && (!k->fv.node_ids || !k->fv.node_offsets || !k->fv.node_feats)))
+      return ORBX_EINVAL;
+    if (!fv_ok(k->fv, k->n)) return ORBX_EINVAL;
+    for (int i = 0; i < k->n; i++)
+      if (k->keys_un[i].octave < 0 || k->keys_un[i].octave >= k->nlevels) return ORBX_EINVAL;
+  }
+  if (!F12 || !pairs || !nmatches) return ORBX_EINVAL;
+  Stager st;
+  size_t o[2][9];
+  for (int s = 0; s < 2; s++) {
+    const orbx_tri_side* k = ks[s];
+    o[s][0] = st.add(k->desc, (size_t)k->n * 32);
+    o[s][1] = st.add(k->keys_un, (size_t)k->n * sizeof(orbx_keypoint));
+    o[s][2] = k->u_right ? st.add(k->u_right, (size_t)k->n * 4) : (size_t)-1;
+    o[s][3] = k->has_mp ? st.add(k->has_mp, (size_t)k->n) : (size_t)-1;
+    o[s][4] = st.add(k->fv.node_ids, (size_t)k->fv.n_nodes * 4);
+    o[s][5] = st.add(k->fv.node_offsets, (size_t)(k->fv.n_nodes + 1) * 4);
+    o[s][6] = st.add(k->fv.node_feats,
+                     (size_t)(k->fv.n_nodes ? k->fv.node_offsets[k->fv.n_nodes] : 0) * 4);
+    o[s][7] = st.add(k->scale_factors, (size_t)k->nlevels * 4);
+    o[s][8] = st.add(k->level_sigma2, (size_t)k->nlevels * 4);
+  }
+  const int n1 = std::max(k1->n, 1);
+  const size_t om12 = st.add(nullptr, (size_t)n1 * 4);
+  const size_t opairs = st.add(nullptr, (size_t)n1 * 8);
+  const size_t ocount = st.add(nullptr, 16);
+  const size_t oprob = st.add(nullptr, sizeof(TriProblem));
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  TriProblem P;
+  DevTriSide* ds[2] = {&P.s1, &P.s2};
+  for (int s = 0; s < 2; s++) {
+    const orbx_tri_side* k = ks[s];
+    DevTriSide& d = *ds[s];
+    d.n = k->n;
+    d.desc = dptr<const uint8_t>(base, o[s][0]);
+    d.keys_un = dptr<const orbx_keypoint>(base, o[s][1]);
+    d.u_right = o[s][2] == (size_t)-1 ? nullptr : dptr<const float>(base, o[s][2]);
+    d.has_mp = o[s][3] == (size_t)-1 ? nullptr : dptr<const uint8_t>(base, o[s][3]);
+    d.fv.n_nodes = k->fv.n_nodes;
+    d.fv.node_ids = dptr<const uint32_t>(base, o[s][4]);
+    d.fv.node_offsets = dptr<const int>(base, o[s][5]);
+    d.fv.node_feats = dptr<const int>(base, o[s][6]);
+    d.scale_factors = dptr<const float>(base, o[s][7]);
+    d.level_sigma2 = dptr<const float>(base, o[s][8]);
+  }
+  memcpy(P.F, F12, 36);
+  P.ex = ex;
+  P.ey = ey;
+  P.only_stereo = only_stereo;
+  P.check_ori = check_ori;
+  P.m12 = dptr<int>(base, om12);
+  P.pairs = dptr<int>(base, opairs);
+  P.count = dptr<int>(base, ocount);
+  memcpy(st.host.data() + oprob, &P, sizeof(P));
+  memset(st.host.data() + om12, 0xFF, (size_t)n1 * 4);
+  memset(st.host.data() + ocount, 0, 16);
+  hipStream_t s = tls_ws.stream;
+  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), st.host.size(), hipMemcpyHostToDevice, s));
+  rc = launch_tri(dptr<TriProblem>(base, oprob), 1, k1->fv.n_nodes, s);
+  if (rc) return rc;
+  int cnt = 0;
+  ORBX_HIP(hipMemcpyAsync(&cnt, base + ocount, 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  if (cnt > 0) {
+    ORBX_HIP(hipMemcpyAsync(pairs, base + opairs, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+  }
+  *nmatches = cnt;
+  return ORBX_OK;
+}
+
+int orbx_epipole(const float R[9], const float t[3], const float Cw[3], float fx, float fy,
+                 float cx, float cy, float* ex, float* ey) {
+  // Caller-side helper (LocalMapping computes it before SearchForTriangulation,
+  // ORBmatcher.cc:667-673).  cv::Mat C2 = R2w*Cw + t2w in f32; ex = fmaf(invz, fx*C2x, cx).
+  if (!R || !t || !Cw || !ex || !ey) return ORBX_EINVAL;
+  float C2[3];
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int c = 0; c < 3; c++) s += (double)R[3 * r + c] * (double)Cw[c];
+    C2[r] = (float)s + t[r];
+  }
+  const float invz = 1.0f / C2[2];
+  *ex = fmaf(invz, fx * C2[0], cx);
+  *ey = fmaf(invz, fy * C2[1], cy);
+  return ORBX_OK;
+}
+
+int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int32_t* out) {
+  if (n < 0 || (n > 0 && (!a || !b || !out))) return ORBX_EINVAL;
+  if (n == 0) return ORBX_OK;
+  Stager st;
+  const size_t oa = st.add(a, (size_t)n * 32), ob = st.add(b, (size_t)n * 32);
+  const size_t oo = st.add(nullptr, (size_t)n * 4);
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), oo, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_distance, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)(base + oa), (const uint8_t*)(base + ob), n,
+                     dptr<int>(base, oo));
+  ORBX_HIP(hipGetLastError());
+  ORBX_HIP(hipMemcpyAsync(out, base + oo, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  return ORBX_OK;
+}
+
+int orbx_feature_vector(const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
+                        const uint8_t* desc, int32_t n, uint32_t* node_of_feature) {
+  if (k < 1 || L < 1 || n < 0 || !node_of_feature || (n && !desc) || !voc_desc) return ORBX_EINVAL;
+  if (n == 0) return ORBX_OK;
+  const int nid_level = L - levelsup;
+  int64_t nodes = 1, lsz = 1;
+  for (int l = 1; l <= std::max(nid_level, 0); l++) {
+    lsz *= k;
+    nodes += lsz;
+    if (nodes > (1LL << 31)) return ORBX_EUNSUPPORTED;
+  }
+  Stager st;
+  const size_t ov = st.add(voc_desc, (size_t)nodes * 32);
+  const size_t od = st.add(desc, (size_t)n * 32);
+  const size_t oo = st.add(nullptr, (size_t)n * 4);
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), oo, hipMemcpyHostToDevice, s));
+  rc = launch_featvec(dptr<uint8_t>(base, ov), k, nid_level, dptr<uint8_t>(base, od), 0, nullptr,
+                      n, n, dptr<uint32_t>(base, oo), 0, 1, s);
+  if (rc) return rc;
+  ORBX_HIP(hipMemcpyAsync(node_of_feature, base + oo, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  return ORBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,139 @@
+"""ORBmatcher — host-side mirror of ORB_SLAM2::ORBmatcher's BoW / triangulation searches.
+
+Mirrors ORB_SLAM2/include/ORBmatcher.h:37-80 (constructor, DescriptorDistance, both
+SearchByBoW overloads, SearchForTriangulation, TH_LOW/TH_HIGH/HISTO_LENGTH).  Frames and
+keyframes are passed as plain objects carrying the members the reference reads:
+
+    KF side : mDescriptors (n,32) u8, mvKeysUn / mvKeys (KEYPOINT_DTYPE), mFeatVec
+              (FeatureVector), map-point validity as `valid` (pMP && !pMP->isBad()) or
+              `has_mp` (GetMapPoint(i) != NULL), mvuRight, mvScaleFactors, mvLevelSigma2
+    Frame   : mDescriptors, mvKeys, mFeatVec
+
+Outputs are indices instead of MapPoint pointers: SearchByBoW(KF, F) returns
+(nmatches, match) with match[f] = KF feature index or -1 (the caller maps it to
+vpMapPointsKF[match[f]]); SearchByBoW(KF1, KF2) returns match12[i1] = KF2 index or -1;
+SearchForTriangulation returns (nmatches, pairs[n,2]).  All work runs on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from types import SimpleNamespace
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import KEYPOINT_DTYPE, check, lib, ptr
+
+
+class _Keep(SimpleNamespace):
+    pass
+
+
+def _fv(fv):
+    ids, offs, feats = fv.as_tuple() if hasattr(fv, "as_tuple") else fv
+    k = _Keep(ids=np.ascontiguousarray(ids, np.uint32), offs=np.ascontiguousarray(offs, np.int32),
+              feats=np.ascontiguousarray(feats, np.int32))
+    return _ffi.FeatVec(len(k.ids), ptr(k.ids), ptr(k.offs), ptr(k.feats)), k
+
+
+def _bow_side(desc, keys, valid, fv):
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    angle = np.ascontiguousarray(np.asarray(keys)["angle"], np.float32)
+    valid = None if valid is None else np.ascontiguousarray(valid, np.uint8)
+    fvs, fk = _fv(fv)
+    s = _ffi.BowSide(desc.shape[0], ptr(desc), ptr(angle), ptr(valid), fvs)
+    return s, _Keep(desc=desc, angle=angle, valid=valid, fk=fk)
+
+
+def _tri_side(kf):
+    desc = np.ascontiguousarray(kf.mDescriptors, np.uint8).reshape(-1, 32)
+    keys = np.ascontiguousarray(kf.mvKeysUn, KEYPOINT_DTYPE)
+    ur = getattr(kf, "mvuRight", None)
+    ur = None if ur is None else np.ascontiguousarray(ur, np.float32)
+    hm = getattr(kf, "has_mp", None)
+    hm = None if hm is None else np.ascontiguousarray(hm, np.uint8)
+    sf = np.ascontiguousarray(kf.mvScaleFactors, np.float32)
+    s2 = np.ascontiguousarray(kf.mvLevelSigma2, np.float32)
+    fvs, fk = _fv(kf.mFeatVec)
+    s = _ffi.TriSide(desc.shape[0], ptr(desc), ptr(keys), ptr(ur), ptr(hm), fvs, ptr(sf), ptr(s2),
+                     len(sf))
+    return s, _Keep(desc=desc, keys=keys, ur=ur, hm=hm, sf=sf, s2=s2, fk=fk)
+
+
+class ORBmatcher:
+    TH_HIGH = 100
+    TH_LOW = 50
+    HISTO_LENGTH = 30
+
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self.mfNNratio = float(np.float32(nnratio))
+        self.mbCheckOrientation = bool(checkOri)
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        a = np.ascontiguousarray(a, np.uint8).reshape(-1, 32)
+        b = np.ascontiguousarray(b, np.uint8).reshape(-1, 32)
+        if a.shape != b.shape:
+            raise ValueError("descriptor sets must have the same shape")
+        out = np.zeros(a.shape[0], np.int32)
+        check("orbx_descriptor_distance",
+              lib().orbx_descriptor_distance(ptr(a), ptr(b), C.c_int32(a.shape[0]), ptr(out)))
+        return int(out[0]) if out.shape[0] == 1 else out
+
+    def SearchByBoW(self, kf, other):
+        """SearchByBoW(KeyFrame*, Frame&) when `other` has no map-point masks, otherwise the
+        KeyFrame/KeyFrame overload (`other.is_keyframe` forces the latter)."""
+        if getattr(other, "is_keyframe", False):
+            return self._bow_kf_kf(kf, other)
+        return self._bow_kf_f(kf, other)
+
+    def _bow_kf_f(self, kf, f):
+        ks, kk = _bow_side(kf.mDescriptors, kf.mvKeysUn, getattr(kf, "valid", None), kf.mFeatVec)
+        fs, fk = _bow_side(f.mDescriptors, f.mvKeys, None, f.mFeatVec)
+        match = np.full(fs.n, -1, np.int32)
+        n = C.c_int32()
+        check("orbx_search_by_bow_kf_f",
+              lib().orbx_search_by_bow_kf_f(C.byref(ks), C.byref(fs), C.c_float(self.mfNNratio),
+                                            C.c_int32(int(self.mbCheckOrientation)), ptr(match),
+                                            C.byref(n)))
+        return n.value, match
+
+    def _bow_kf_kf(self, kf1, kf2):
+        s1, k1 = _bow_side(kf1.mDescriptors, kf1.mvKeysUn, getattr(kf1, "valid", None),
+                           kf1.mFeatVec)
+        s2, k2 = _bow_side(kf2.mDescriptors, kf2.mvKeysUn, getattr(kf2, "valid", None),
+                           kf2.mFeatVec)
+        match = np.full(s1.n, -1, np.int32)
+        n = C.c_int32()
+        check("orbx_search_by_bow_kf_kf",
+              lib().orbx_search_by_bow_kf_kf(C.byref(s1), C.byref(s2), C.c_float(self.mfNNratio),
+                                             C.c_int32(int(self.mbCheckOrientation)), ptr(match),
+                                             C.byref(n)))
+        return n.value, match
+
+    def SearchForTriangulation(self, kf1, kf2, F12, bOnlyStereo=False, epipole=None):
+        """`epipole` = (ex, ey) of KF1's centre in KF2 (ORBmatcher.cc:667-673); compute it with
+        `epipole()` from the keyframe poses."""
+        s1, k1 = _tri_side(kf1)
+        s2, k2 = _tri_side(kf2)
+        F = np.ascontiguousarray(F12, np.float32).reshape(9)
+        ex, ey = epipole
+        pairs = np.zeros((max(s1.n, 1), 2), np.int32)
+        n = C.c_int32()
+        check("orbx_search_for_triangulation",
+              lib().orbx_search_for_triangulation(
+                  C.byref(s1), C.byref(s2), ptr(F), C.c_float(ex), C.c_float(ey),
+                  C.c_int32(int(bOnlyStereo)), C.c_float(self.mfNNratio),
+                  C.c_int32(int(self.mbCheckOrientation)), ptr(pairs), C.byref(n)))
+        return n.value, pairs[:n.value].copy()
+
+
+def epipole(R2w, t2w, Cw, fx, fy, cx, cy):
+    ex, ey = C.c_float(), C.c_float()
+    R = np.ascontiguousarray(R2w, np.float32).reshape(9)
+    t = np.ascontiguousarray(t2w, np.float32).reshape(3)
+    c = np.ascontiguousarray(Cw, np.float32).reshape(3)
+    check("orbx_epipole", lib().orbx_epipole(ptr(R), ptr(t), ptr(c), C.c_float(fx), C.c_float(fy),
+                                             C.c_float(cx), C.c_float(cy), C.byref(ex),
+                                             C.byref(ey)))
+    return ex.value, ey.value

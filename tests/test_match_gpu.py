@@ -1,0 +1,116 @@
+"""GPU parity of ORBmatcher (SearchByBoW x2, SearchForTriangulation, DescriptorDistance) and
+the vocabulary node ids against the CPU oracle — identical match arrays and counts."""
+import numpy as np
+import pytest
+
+from ar_orbslam2_amd import FeatureVector, ORBmatcher, Vocabulary, epipole
+from oracle import oracle as O
+
+from matchdata import TUM1_K, fundamental, pair, vocab_desc
+
+pytestmark = pytest.mark.gpu
+
+SHIFT_F = np.array([[0, 0, -1], [0, 0, 1], [1, -1, 0]], np.float32)
+
+
+@pytest.fixture(scope="module")
+def frames():
+    return pair()
+
+
+def _oracle_bow_side(kf, valid=True):
+    return dict(desc=kf.mDescriptors, angle=kf.mvKeysUn["angle"],
+                valid=kf.valid if valid else None, fv=kf.mFeatVec)
+
+
+def test_vocabulary_node_ids(frames):
+    a, b, voc = frames
+    v = Vocabulary(10, 6, voc, 4)
+    for kf in (a, b):
+        got = v.node_ids(kf.mDescriptors)
+        assert np.array_equal(got, kf.nodes)
+        fv = v.transform(kf.mDescriptors)
+        for x, y in zip(fv.as_tuple(), kf.mFeatVec):
+            assert np.array_equal(x, y)
+
+
+def test_descriptor_distance(frames):
+    a, b, _ = frames
+    n = min(len(a.mDescriptors), len(b.mDescriptors))
+    got = ORBmatcher.DescriptorDistance(a.mDescriptors[:n], b.mDescriptors[:n])
+    ref = [O.descriptor_distance(a.mDescriptors[i], b.mDescriptors[i]) for i in range(n)]
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("ratio,ori", [(0.7, True), (0.75, True), (0.9, False), (0.6, True)])
+def test_search_by_bow_kf_frame(frames, ratio, ori):
+    kf, f, _ = frames
+    n_ref, m_ref = O.search_by_bow_kf_f(_oracle_bow_side(kf), _oracle_bow_side(f, False), ratio,
+                                        ori)
+    fr = type("F", (), {})()
+    fr.mDescriptors, fr.mvKeys, fr.mFeatVec = f.mDescriptors, f.mvKeys, f.mFeatVec
+    n, m = ORBmatcher(ratio, ori).SearchByBoW(kf, fr)
+    assert n == n_ref and n > 20
+    assert np.array_equal(m, m_ref)
+
+
+@pytest.mark.parametrize("ratio,ori", [(0.75, True), (0.9, False)])
+def test_search_by_bow_kf_kf(frames, ratio, ori):
+    k1, k2, _ = frames
+    k2.is_keyframe = True
+    n_ref, m_ref = O.search_by_bow_kf_kf(_oracle_bow_side(k1), _oracle_bow_side(k2), ratio, ori)
+    n, m = ORBmatcher(ratio, ori).SearchByBoW(k1, k2)
+    assert n == n_ref and n > 10
+    assert np.array_equal(m, m_ref)
+
+
+def _tri(k1, k2, F, ex, ey, only_stereo, ori):
+    d = lambda k: dict(desc=k.mDescriptors, keys=k.mvKeysUn, u_right=k.mvuRight, has_mp=k.has_mp,
+                       fv=k.mFeatVec, scale_factors=k.mvScaleFactors, level_sigma2=k.mvLevelSigma2)
+    n_ref, p_ref = O.search_for_triangulation(d(k1), d(k2), F, ex, ey, only_stereo, 0.6, ori)
+    n, p = ORBmatcher(0.6, ori).SearchForTriangulation(k1, k2, F, only_stereo, (ex, ey))
+    assert n == n_ref
+    assert np.array_equal(p, p_ref)
+    return n
+
+
+def test_triangulation_realistic_pose(frames):
+    k1, k2, _ = frames
+    fx, fy, cx, cy = TUM1_K
+    ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], fx, fy, cx, cy)
+    assert (ex, ey) == O.epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], fx, fy, cx, cy)
+    _tri(k1, k2, fundamental(), ex, ey, False, False)
+
+
+def test_triangulation_permissive_geometry(frames):
+    # consecutive synthetic frames differ by a (-1,-1) pixel shift: F = [(dx,dy,0)]x makes the
+    # epipolar line of each point pass through its true match, so many candidates survive and
+    # the distance / last-wins rules are exercised; an epipole inside the image exercises the
+    # epipole rejection
+    k1, k2, _ = frames
+    F = SHIFT_F
+    n = _tri(k1, k2, F, 1e6, 1e6, False, False)
+    assert n > 50
+    n2 = _tri(k1, k2, F, 1e6, 1e6, False, True)
+    assert n2 <= n
+    n3 = _tri(k1, k2, F, 320.0, 240.0, False, False)
+    assert n3 <= n
+
+
+def test_triangulation_stereo(frames):
+    k1, k2, _ = frames
+    rng = np.random.default_rng(9)
+    k1.mvuRight = np.where(rng.random(len(k1.mvKeys)) < 0.5, 100.0, -1.0).astype(np.float32)
+    k2.mvuRight = np.where(rng.random(len(k2.mvKeys)) < 0.5, 100.0, -1.0).astype(np.float32)
+    assert _tri(k1, k2, SHIFT_F, 320.0, 240.0, True, False) > 10
+    _tri(k1, k2, SHIFT_F, 320.0, 240.0, False, False)
+
+
+def test_empty_sides():
+    m = ORBmatcher(0.7, True)
+    e = type("E", (), {})()
+    e.mDescriptors = np.zeros((0, 32), np.uint8)
+    e.mvKeys = e.mvKeysUn = np.zeros(0, O.KEYPOINT_DTYPE)
+    e.mFeatVec = FeatureVector.from_nodes(np.zeros(0, np.uint32))
+    n, match = m.SearchByBoW(e, e)
+    assert n == 0 and match.shape == (0,)
