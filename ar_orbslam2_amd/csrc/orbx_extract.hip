@@ -772,12 +772,7 @@ struct orbx_plan {
   hipGraphExec_t graph = nullptr;
   const uint8_t* graph_in = nullptr;
   int graph_n = -1;
-  // profiling
-  bool prof = false;
-  std::vector<std::string> stage_names;
-  std::vector<double> stage_ms;
-  std::vector<long long> stage_launches;
-  std::vector<hipEvent_t> ev;
+  Profiler prof;
 };
 
 namespace {
@@ -789,56 +784,45 @@ int dalloc(T** p, size_t count) {
   return ORBX_OK;
 }
 
-int enqueue(orbx_plan* P, const uint8_t* d_in, int n, bool profile) {
+int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   const Geometry& g = P->g;
   const int L = g.nlevels;
-  std::vector<std::pair<int, hipEvent_t>> marks;
-  auto mark = [&](int stage) {
-    if (!profile) return;
-    hipEvent_t e = P->ev[marks.size()];
-    hipEventRecord(e, P->stream);
-    marks.push_back({stage, e});
-  };
-  mark(-1);
+  Profiler dummy;
+  Profiler& pr = prof ? *prof : dummy;
+  const int st_resize = pr.stage("k_resize"), st_blur = pr.stage("k_blur"),
+            st_fast = pr.stage("k_fast_cells"), st_oct = pr.stage("k_octree"),
+            st_desc = pr.stage("k_describe");
+  pr.mark(P->stream, -1);
   for (int l = 1; l < L; l++) {
     const LevelGeom& D = g.lv[l];
     dim3 grid((D.w * D.h + 255) / 256, n);
     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, P->stream, d_in, P->d_pyr, g.pyr_bytes,
                        P->d_lv, l, P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
-    mark(0);
+    pr.mark(P->stream, st_resize);
   }
   if (P->ntiles > 0) {
     hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, d_in, P->d_pyr,
                        g.pyr_bytes, P->d_blur, P->blur_bytes, P->d_blur_off, P->d_lv, P->d_tiles);
+    pr.mark(P->stream, st_blur);
   }
-  mark(1);
   const int ncells = (int)g.cells.size();
-  if (ncells > 0)
+  if (ncells > 0) {
     hipLaunchKernelGGL(k_fast_cells, dim3(ncells, n), dim3(256), 0, P->stream, d_in, P->d_pyr,
                        g.pyr_bytes, P->d_lv, P->d_cells, ncells, g.ini_th, g.min_th, P->d_cand,
                        g.cand_total, P->d_cell_counts);
-  mark(2);
+    pr.mark(P->stream, st_fast);
+  }
   hipLaunchKernelGGL(k_octree, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream, P->d_lv,
                      P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total, P->d_lin,
                      P->d_label, P->d_okey, P->d_ocount, g.kp_total, L, g.node_cap_max,
                      P->cell_cap);
-  mark(3);
+  pr.mark(P->stream, st_oct);
   hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 3) / 4, n), dim3(256), 0, P->stream, d_in,
                      P->d_pyr, g.pyr_bytes, P->d_blur, P->blur_bytes, P->d_blur_off, P->d_lv, L,
                      P->d_okey, P->d_ocount, g.kp_total, P->d_kps, P->d_desc, P->d_counts);
-  mark(4);
+  pr.mark(P->stream, st_desc);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return report_hip(e, "extract launch");
-  if (profile) {
-    ORBX_HIP(hipEventSynchronize(marks.back().second));
-    for (size_t i = 1; i < marks.size(); i++) {
-      float ms = 0;
-      hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second);
-      const int s = marks[i].first;
-      P->stage_ms[s] += ms;
-      P->stage_launches[s] += 1;
-    }
-  }
   return ORBX_OK;
 }
 
@@ -918,12 +902,6 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)P->oct_smem) != hipSuccess)
     return fail(ORBX_EDEVICE);
-  P->stage_names = {"k_resize", "k_blur", "k_fast_cells", "k_octree", "k_describe"};
-  P->stage_ms.assign(P->stage_names.size(), 0.0);
-  P->stage_launches.assign(P->stage_names.size(), 0);
-  P->ev.resize(g.nlevels + 8);
-  for (auto& e : P->ev)
-    if (hipEventCreate(&e) != hipSuccess) return fail(ORBX_EDEVICE);
   *out = P;
   return ORBX_OK;
 }
@@ -931,8 +909,6 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
 int orbx_plan_destroy(orbx_plan* P) {
   if (!P) return ORBX_OK;
   if (P->graph) hipGraphExecDestroy(P->graph);
-  for (auto& e : P->ev)
-    if (e) hipEventDestroy(e);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xofs,   P->d_yofs,  P->d_xa,
                   P->d_yb,  P->d_blur_off, P->d_tiles, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label,
@@ -955,7 +931,7 @@ int orbx_plan_extract(orbx_plan* P, const uint8_t* d_imgs, int32_t n) {
   ORBX_HIP(hipSetDevice(P->device));
   P->last_in = d_imgs;
   P->last_n = n;
-  if (P->prof) return enqueue(P, d_imgs, n, true);
+  if (P->prof.on) return enqueue(P, d_imgs, n, &P->prof);
   if (!(P->graph && P->graph_in == d_imgs && P->graph_n == n)) {
     if (P->graph) {
       hipGraphExecDestroy(P->graph);
@@ -963,7 +939,7 @@ int orbx_plan_extract(orbx_plan* P, const uint8_t* d_imgs, int32_t n) {
     }
     hipGraph_t gr;
     ORBX_HIP(hipStreamBeginCapture(P->stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue(P, d_imgs, n, false);
+    int rc = enqueue(P, d_imgs, n, nullptr);
     hipError_t e = hipStreamEndCapture(P->stream, &gr);
     if (rc != ORBX_OK) return rc;
     if (e != hipSuccess) return report_hip(e, "hipStreamEndCapture");
@@ -995,24 +971,24 @@ void* orbx_plan_stream(orbx_plan* P) { return P ? (void*)P->stream : nullptr; }
 
 int orbx_plan_profile(orbx_plan* P, int32_t enable) {
   if (!P) return ORBX_EINVAL;
-  P->prof = enable != 0;
-  std::fill(P->stage_ms.begin(), P->stage_ms.end(), 0.0);
-  std::fill(P->stage_launches.begin(), P->stage_launches.end(), 0);
+  P->prof.on = enable != 0;
+  P->prof.reset();
   return ORBX_OK;
 }
 
 int orbx_plan_profile_read(orbx_plan* P, int32_t cap, char (*names)[32], double* total_ms,
                            int64_t* launches, int32_t* n_stages) {
   if (!P) return ORBX_EINVAL;
-  const int n = (int)P->stage_names.size();
+  if (P->prof.collect() != 0) return ORBX_EDEVICE;
+  const int n = (int)P->prof.names.size();
   if (n_stages) *n_stages = n;
   for (int i = 0; i < n && i < cap; i++) {
     if (names) {
-      strncpy(names[i], P->stage_names[i].c_str(), 31);
+      strncpy(names[i], P->prof.names[i].c_str(), 31);
       names[i][31] = 0;
     }
-    if (total_ms) total_ms[i] = P->stage_ms[i];
-    if (launches) launches[i] = P->stage_launches[i];
+    if (total_ms) total_ms[i] = P->prof.ms[i];
+    if (launches) launches[i] = P->prof.launches[i];
   }
   return ORBX_OK;
 }
@@ -1036,6 +1012,24 @@ int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int
   return ORBX_OK;
 }
 
-const void* orbx_plan_geometry(const orbx_plan* P) { return P ? &P->g : nullptr; }
-
 }  // extern "C"
+
+namespace orbx {
+int plan_view(orbx_plan* P, PlanView* v) {
+  if (!P || !v) return ORBX_EINVAL;
+  v->g = &P->g;
+  v->stream = P->stream;
+  v->d_kps = P->d_kps;
+  v->d_desc = P->d_desc;
+  v->d_counts = P->d_counts;
+  v->kp_total = P->g.kp_total;
+  v->max_batch = P->max_batch;
+  return ORBX_OK;
+}
+int plan_enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
+  if (!P || !d_in || n <= 0 || n > P->max_batch) return ORBX_EINVAL;
+  P->last_in = d_in;
+  P->last_n = n;
+  return enqueue(P, d_in, n, prof);
+}
+}  // namespace orbx

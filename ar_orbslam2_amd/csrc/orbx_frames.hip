@@ -1,0 +1,357 @@
+// orbx_frames.hip — device-resident frame pipeline: the whole "ORB extract + match" unit of
+// work of SURVEY §8d for a batch of frames, with no host round trip:
+//   extract (plan)  ->  node ids (k_featvec)  ->  FeatureVector CSR (k_csr)
+//   -> SearchByBoW(prev-as-KF, cur)  ->  SearchForTriangulation(prev-as-KF, cur-as-KF)
+// Frame f of a batch is matched against frame (f-1) mod n of the same batch.  The sequence is
+// captured once into a hipGraph per (input pointer, batch size).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "orbx_internal.h"
+#include "orbx_match.h"
+
+using namespace orbx;
+
+struct orbx_frames {
+  orbx_plan* plan = nullptr;
+  PlanView v{};
+  int device = 0;
+  // vocabulary
+  uint8_t* d_voc = nullptr;
+  int k = 10, L = 6, levelsup = 4, nid_level = 2;
+  uint32_t id_lo = 0;
+  int nb = 1;
+  // per frame
+  uint32_t* d_node_of = nullptr;  // [B][kp]
+  uint32_t* d_ids = nullptr;      // [B][nb]
+  int* d_off = nullptr;           // [B][nb+1]
+  int* d_feats = nullptr;         // [B][kp]
+  int* d_nn = nullptr;            // [B]
+  uint8_t* d_valid = nullptr;     // [B][kp]
+  uint8_t* d_hasmp = nullptr;     // [B][kp]
+  float *d_sf = nullptr, *d_s2 = nullptr;
+  int* d_match = nullptr;      // [B][kp]
+  int* d_bow_count = nullptr;  // [B] + error word
+  int* d_m12 = nullptr;        // [B][kp]
+  int* d_pairs = nullptr;      // [B][kp][2]
+  int* d_tri_count = nullptr;  // [B]
+  BowProblem* d_bprob = nullptr;
+  TriProblem* d_tprob = nullptr;
+  int prob_n = -1;
+  // matching parameters
+  float bow_ratio = 0.7f, tri_ratio = 0.6f;
+  int bow_ori = 1, tri_ori = 0, only_stereo = 0;
+  float F[9] = {0};
+  float ex = 0, ey = 0;
+  // graph cache, one executable graph per (input pointer, batch size)
+  struct GraphEntry {
+    const uint8_t* in;
+    int n;
+    hipGraphExec_t exec;
+  };
+  std::vector<GraphEntry> graphs;
+  Profiler prof;
+  void drop_graphs() {
+    for (auto& g : graphs) hipGraphExecDestroy(g.exec);
+    graphs.clear();
+  }
+};
+
+namespace {
+
+template <class T>
+int dalloc(T** p, size_t count) {
+  if (count == 0) count = 1;
+  if (hipMalloc((void**)p, count * sizeof(T)) != hipSuccess) return ORBX_ENOMEM;
+  return ORBX_OK;
+}
+
+int build_problems(orbx_frames* F, int n) {
+  const int kp = F->v.kp_total;
+  std::vector<BowProblem> bp(n);
+  std::vector<TriProblem> tp(n);
+  for (int f = 0; f < n; f++) {
+    const int kf = (f - 1 + n) % n;
+    auto side = [&](int fr, bool with_valid) {
+      DevSide s{};
+      s.n = 0;
+      s.n_dev = F->v.d_counts + fr;
+      s.desc = F->v.d_desc + (int64_t)fr * kp * 32;
+      s.angle = (const float*)((const char*)(F->v.d_kps + (int64_t)fr * kp) +
+                               offsetof(orbx_keypoint, angle));
+      s.angle_stride = sizeof(orbx_keypoint) / sizeof(float);
+      s.valid = with_valid ? F->d_valid + (int64_t)fr * kp : nullptr;
+      s.n_nodes = 0;
+      s.n_nodes_dev = F->d_nn + fr;
+      s.node_ids = F->d_ids + (int64_t)fr * F->nb;
+      s.node_offsets = F->d_off + (int64_t)fr * (F->nb + 1);
+      s.node_feats = F->d_feats + (int64_t)fr * kp;
+      return s;
+    };
+    BowProblem& B = bp[f];
+    B.s1 = side(kf, true);
+    B.s2 = side(f, false);
+    B.match = F->d_match + (int64_t)f * kp;
+    B.count = F->d_bow_count + f;
+    B.error = F->d_bow_count + F->v.max_batch;
+    B.mode = 0;
+    B.nnratio = F->bow_ratio;
+    B.check_ori = F->bow_ori;
+    auto tside = [&](int fr) {
+      DevTriSide s{};
+      s.n_dev = F->v.d_counts + fr;
+      s.desc = F->v.d_desc + (int64_t)fr * kp * 32;
+      s.keys_un = F->v.d_kps + (int64_t)fr * kp;
+      s.u_right = nullptr;
+      s.has_mp = F->d_hasmp + (int64_t)fr * kp;
+      s.fv.n_nodes_dev = F->d_nn + fr;
+      s.fv.node_ids = F->d_ids + (int64_t)fr * F->nb;
+      s.fv.node_offsets = F->d_off + (int64_t)fr * (F->nb + 1);
+      s.fv.node_feats = F->d_feats + (int64_t)fr * kp;
+      s.scale_factors = F->d_sf;
+      s.level_sigma2 = F->d_s2;
+      return s;
+    };
+    TriProblem& T = tp[f];
+    T.s1 = tside(kf);
+    T.s2 = tside(f);
+    memcpy(T.F, F->F, sizeof(T.F));
+    T.ex = F->ex;
+    T.ey = F->ey;
+    T.only_stereo = F->only_stereo;
+    T.check_ori = F->tri_ori;
+    T.m12 = F->d_m12 + (int64_t)f * kp;
+    T.pairs = F->d_pairs + (int64_t)f * kp * 2;
+    T.count = F->d_tri_count + f;
+  }
+  ORBX_HIP(hipMemcpy(F->d_bprob, bp.data(), sizeof(BowProblem) * n, hipMemcpyHostToDevice));
+  ORBX_HIP(hipMemcpy(F->d_tprob, tp.data(), sizeof(TriProblem) * n, hipMemcpyHostToDevice));
+  F->prob_n = n;
+  return ORBX_OK;
+}
+
+int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
+  Profiler dummy;
+  Profiler& pr = prof ? *prof : dummy;
+  const int st_fv = pr.stage("k_featvec"), st_csr = pr.stage("k_csr"),
+            st_bow = pr.stage("k_bow"), st_tri = pr.stage("k_tri");
+  hipStream_t s = F->v.stream;
+  int rc = plan_enqueue(F->plan, d_in, n, prof);
+  if (rc) return rc;
+  const int kp = F->v.kp_total;
+  rc = launch_featvec(F->d_voc, F->k, F->nid_level, F->v.d_desc, (int64_t)kp * 32, F->v.d_counts,
+                      0, kp, F->d_node_of, kp, n, s);
+  if (rc) return rc;
+  pr.mark(s, st_fv);
+  rc = launch_csr(F->d_node_of, kp, F->v.d_counts, 0, F->id_lo, F->nb, F->d_ids, F->d_off,
+                  F->d_feats, kp, F->d_nn, n, s);
+  if (rc) return rc;
+  pr.mark(s, st_csr);
+  ORBX_HIP(hipMemsetAsync(F->d_match, 0xFF, (size_t)n * kp * 4, s));
+  rc = launch_bow(F->d_bprob, n, F->nb, s);
+  if (rc) return rc;
+  pr.mark(s, st_bow);
+  ORBX_HIP(hipMemsetAsync(F->d_m12, 0xFF, (size_t)n * kp * 4, s));
+  rc = launch_tri(F->d_tprob, n, F->nb, s);
+  if (rc) return rc;
+  pr.mark(s, st_tri);
+  return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_batch,
+                       const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
+                       int hip_device, orbx_frames** out) {
+  if (!p || !out || !voc_desc || k < 2 || L < 1 || levelsup < 0 || max_batch < 1)
+    return ORBX_EINVAL;
+  *out = nullptr;
+  const int nid_level = L - levelsup;
+  if (nid_level < 1) return ORBX_EUNSUPPORTED;  // FeatureVector keyed by the root only
+  int64_t nodes = 1, lsz = 1, id_lo = 0;
+  for (int l = 1; l <= nid_level; l++) {
+    id_lo = nodes;
+    lsz *= k;
+    nodes += lsz;
+  }
+  if (lsz > 8192) return ORBX_EUNSUPPORTED;
+  orbx_frames* F = new (std::nothrow) orbx_frames();
+  if (!F) return ORBX_ENOMEM;
+  auto fail = [&](int rc) {
+    orbx_frames_destroy(F);
+    return rc;
+  };
+  F->device = hip_device;
+  int rc = orbx_plan_create(p, w, h, max_batch, hip_device, &F->plan);
+  if (rc) return fail(rc);
+  plan_view(F->plan, &F->v);
+  F->k = k;
+  F->L = L;
+  F->levelsup = levelsup;
+  F->nid_level = nid_level;
+  F->id_lo = (uint32_t)id_lo;
+  F->nb = (int)lsz;
+  const size_t B = max_batch, kp = F->v.kp_total;
+  if (dalloc(&F->d_voc, nodes * 32) || dalloc(&F->d_node_of, B * kp) ||
+      dalloc(&F->d_ids, B * F->nb) || dalloc(&F->d_off, B * (F->nb + 1)) ||
+      dalloc(&F->d_feats, B * kp) || dalloc(&F->d_nn, B) || dalloc(&F->d_valid, B * kp) ||
+      dalloc(&F->d_hasmp, B * kp) || dalloc(&F->d_sf, p->nlevels) ||
+      dalloc(&F->d_s2, p->nlevels) || dalloc(&F->d_match, B * kp) ||
+      dalloc(&F->d_bow_count, B + 1) || dalloc(&F->d_m12, B * kp) ||
+      dalloc(&F->d_pairs, B * kp * 2) || dalloc(&F->d_tri_count, B) || dalloc(&F->d_bprob, B) ||
+      dalloc(&F->d_tprob, B))
+    return fail(ORBX_ENOMEM);
+  if (hipMemcpy(F->d_voc, voc_desc, nodes * 32, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(F->d_sf, F->v.g->scale, 4 * p->nlevels, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(F->d_s2, F->v.g->sigma2, 4 * p->nlevels, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(F->d_valid, 1, B * kp) != hipSuccess ||
+      hipMemset(F->d_hasmp, 0, B * kp) != hipSuccess ||
+      hipMemset(F->d_bow_count, 0, 4 * (B + 1)) != hipSuccess ||
+      hipMemset(F->d_tri_count, 0, 4 * B) != hipSuccess)
+    return fail(ORBX_EDEVICE);
+  *out = F;
+  return ORBX_OK;
+}
+
+int orbx_frames_destroy(orbx_frames* F) {
+  if (!F) return ORBX_OK;
+  F->drop_graphs();
+  void* ptrs[] = {F->d_voc,   F->d_node_of, F->d_ids,   F->d_off,       F->d_feats,
+                  F->d_nn,    F->d_valid,   F->d_hasmp, F->d_sf,        F->d_s2,
+                  F->d_match, F->d_bow_count, F->d_m12, F->d_pairs,     F->d_tri_count,
+                  F->d_bprob, F->d_tprob};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  if (F->plan) orbx_plan_destroy(F->plan);
+  delete F;
+  return ORBX_OK;
+}
+
+int orbx_frames_capacity(const orbx_frames* F, int32_t* kp_cap) {
+  if (!F || !kp_cap) return ORBX_EINVAL;
+  *kp_cap = F->v.kp_total;
+  return ORBX_OK;
+}
+
+int orbx_frames_set_masks(orbx_frames* F, const uint8_t* valid, const uint8_t* has_mp) {
+  if (!F) return ORBX_EINVAL;
+  const size_t bytes = (size_t)F->v.max_batch * F->v.kp_total;
+  if (valid) ORBX_HIP(hipMemcpy(F->d_valid, valid, bytes, hipMemcpyHostToDevice));
+  if (has_mp) ORBX_HIP(hipMemcpy(F->d_hasmp, has_mp, bytes, hipMemcpyHostToDevice));
+  return ORBX_OK;
+}
+
+int orbx_frames_set_matching(orbx_frames* F, float bow_ratio, int32_t bow_check_ori,
+                             const float F12[9], float ex, float ey, float tri_ratio,
+                             int32_t tri_check_ori, int32_t only_stereo) {
+  if (!F || !F12) return ORBX_EINVAL;
+  F->bow_ratio = bow_ratio;
+  F->bow_ori = bow_check_ori;
+  memcpy(F->F, F12, sizeof(F->F));
+  F->ex = ex;
+  F->ey = ey;
+  F->tri_ratio = tri_ratio;
+  F->tri_ori = tri_check_ori;
+  F->only_stereo = only_stereo;
+  F->prob_n = -1;  // rebuild problem descriptors
+  F->drop_graphs();
+  return ORBX_OK;
+}
+
+int orbx_frames_run(orbx_frames* F, const uint8_t* d_imgs, int32_t n) {
+  if (!F || !d_imgs || n < 1 || n > F->v.max_batch) return ORBX_EINVAL;
+  ORBX_HIP(hipSetDevice(F->device));
+  if (F->prob_n != n) {
+    int rc = build_problems(F, n);
+    if (rc) return rc;
+    F->drop_graphs();
+  }
+  if (F->prof.on) return enqueue(F, d_imgs, n, &F->prof);
+  hipGraphExec_t exec = nullptr;
+  for (auto& g : F->graphs)
+    if (g.in == d_imgs && g.n == n) exec = g.exec;
+  if (!exec) {
+    if (F->graphs.size() >= 16) F->drop_graphs();
+    hipGraph_t gr;
+    ORBX_HIP(hipStreamBeginCapture(F->v.stream, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue(F, d_imgs, n, nullptr);
+    hipError_t e = hipStreamEndCapture(F->v.stream, &gr);
+    if (rc) return rc;
+    if (e != hipSuccess) return report_hip(e, "hipStreamEndCapture");
+    e = hipGraphInstantiate(&exec, gr, nullptr, nullptr, 0);
+    hipGraphDestroy(gr);
+    if (e != hipSuccess) return report_hip(e, "hipGraphInstantiate");
+    F->graphs.push_back({d_imgs, n, exec});
+  }
+  ORBX_HIP(hipGraphLaunch(exec, F->v.stream));
+  return ORBX_OK;
+}
+
+int orbx_frames_sync(orbx_frames* F) {
+  if (!F) return ORBX_EINVAL;
+  ORBX_HIP(hipStreamSynchronize(F->v.stream));
+  return ORBX_OK;
+}
+
+int orbx_frames_results(orbx_frames* F, int32_t n, int32_t* kp_counts, int32_t* bow_matches,
+                        int32_t* tri_matches, int32_t* error) {
+  if (!F || n < 1 || n > F->v.max_batch) return ORBX_EINVAL;
+  hipStream_t s = F->v.stream;
+  if (kp_counts) ORBX_HIP(hipMemcpyAsync(kp_counts, F->v.d_counts, 4 * n, hipMemcpyDeviceToHost, s));
+  if (bow_matches)
+    ORBX_HIP(hipMemcpyAsync(bow_matches, F->d_bow_count, 4 * n, hipMemcpyDeviceToHost, s));
+  if (tri_matches)
+    ORBX_HIP(hipMemcpyAsync(tri_matches, F->d_tri_count, 4 * n, hipMemcpyDeviceToHost, s));
+  if (error)
+    ORBX_HIP(hipMemcpyAsync(error, F->d_bow_count + F->v.max_batch, 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  return ORBX_OK;
+}
+
+int orbx_frames_outputs(orbx_frames* F, orbx_keypoint** d_kps, uint8_t** d_desc,
+                        int32_t** d_counts, uint32_t** d_node_of, int32_t** d_bow_match,
+                        int32_t** d_tri_pairs) {
+  if (!F) return ORBX_EINVAL;
+  if (d_kps) *d_kps = F->v.d_kps;
+  if (d_desc) *d_desc = F->v.d_desc;
+  if (d_counts) *d_counts = F->v.d_counts;
+  if (d_node_of) *d_node_of = F->d_node_of;
+  if (d_bow_match) *d_bow_match = F->d_match;
+  if (d_tri_pairs) *d_tri_pairs = F->d_pairs;
+  return ORBX_OK;
+}
+
+void* orbx_frames_stream(orbx_frames* F) { return F ? (void*)F->v.stream : nullptr; }
+
+int orbx_frames_profile(orbx_frames* F, int32_t enable) {
+  if (!F) return ORBX_EINVAL;
+  F->prof.on = enable != 0;
+  F->prof.reset();
+  return ORBX_OK;
+}
+
+int orbx_frames_profile_read(orbx_frames* F, int32_t cap, char (*names)[32], double* total_ms,
+                             int64_t* launches, int32_t* n_stages) {
+  if (!F) return ORBX_EINVAL;
+  if (F->prof.collect() != 0) return ORBX_EDEVICE;
+  const int n = (int)F->prof.names.size();
+  if (n_stages) *n_stages = n;
+  for (int i = 0; i < n && i < cap; i++) {
+    if (names) {
+      strncpy(names[i], F->prof.names[i].c_str(), 31);
+      names[i][31] = 0;
+    }
+    if (total_ms) total_ms[i] = F->prof.ms[i];
+    if (launches) launches[i] = F->prof.launches[i];
+  }
+  return ORBX_OK;
+}
+
+}  // extern "C"

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/orbx.h"
@@ -68,6 +69,60 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
 // Tables only (no image size): scale factors, sigma2, features per level, umax.
 void build_tables(const orbx_params& p, Geometry* g);
 
+// Stage timing with HIP events recorded on the launching stream between kernels.  Marks are
+// only read back in collect(), so profiling adds no host synchronisation to the timed loop.
+struct Profiler {
+  bool on = false;
+  std::vector<std::string> names;
+  std::vector<double> ms;
+  std::vector<long long> launches;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  std::vector<std::pair<int, hipEvent_t>> marks;  // stage -1 = segment start
+  int stage(const char* name) {
+    for (size_t i = 0; i < names.size(); i++)
+      if (names[i] == name) return (int)i;
+    names.push_back(name);
+    ms.push_back(0);
+    launches.push_back(0);
+    return (int)names.size() - 1;
+  }
+  void mark(hipStream_t s, int st) {
+    if (!on) return;
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      pool.push_back(e);
+    }
+    hipEvent_t e = pool[used++];
+    hipEventRecord(e, s);
+    marks.push_back({st, e});
+  }
+  int collect() {
+    if (marks.empty()) return 0;
+    if (hipEventSynchronize(marks.back().second) != hipSuccess) return -3;
+    for (size_t i = 1; i < marks.size(); i++) {
+      if (marks[i].first < 0) continue;
+      float t = 0;
+      hipEventElapsedTime(&t, marks[i - 1].second, marks[i].second);
+      ms[marks[i].first] += t;
+      launches[marks[i].first] += 1;
+    }
+    marks.clear();
+    used = 0;
+    return 0;
+  }
+  void reset() {
+    marks.clear();
+    used = 0;
+    for (auto& m : ms) m = 0;
+    for (auto& l : launches) l = 0;
+  }
+  ~Profiler() {
+    for (auto e : pool) hipEventDestroy(e);
+  }
+};
+
 #define ORBX_HIP(call)                                       \
   do {                                                       \
     hipError_t e_ = (call);                                  \
@@ -75,5 +130,18 @@ void build_tables(const orbx_params& p, Geometry* g);
   } while (0)
 
 int report_hip(hipError_t e, const char* what);
+
+// Internal plan access for the frame pipeline (orbx_frames.hip).
+struct PlanView {
+  const Geometry* g;
+  hipStream_t stream;
+  orbx_keypoint* d_kps;
+  uint8_t* d_desc;
+  int* d_counts;
+  int kp_total;
+  int max_batch;
+};
+int plan_view(orbx_plan* P, PlanView* v);
+int plan_enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof);
 
 }  // namespace orbx

@@ -10,14 +10,25 @@ namespace orbx {
 // One side of SearchByBoW, all pointers in device memory.
 struct DevSide {
   int n;
+  const int* n_dev;        // nullable: when set, the feature count lives in device memory
   const uint8_t* desc;
-  const float* angle;
-  const uint8_t* valid;  // nullable: all valid
+  const float* angle;      // angle of feature i at angle[i * angle_stride]
+  int angle_stride;
+  const uint8_t* valid;    // nullable: all valid
   int n_nodes;
+  const int* n_nodes_dev;  // nullable: device-side node count
   const uint32_t* node_ids;
   const int* node_offsets;
   const int* node_feats;
 };
+
+__device__ __forceinline__ int side_n(const DevSide& s) { return s.n_dev ? *s.n_dev : s.n; }
+__device__ __forceinline__ int side_nodes(const DevSide& s) {
+  return s.n_nodes_dev ? *s.n_nodes_dev : s.n_nodes;
+}
+__device__ __forceinline__ float side_angle(const DevSide& s, int i) {
+  return s.angle[(int64_t)i * s.angle_stride];
+}
 
 // mode 0 = SearchByBoW(KF, Frame): s1 = KF, s2 = Frame, match[F idx] = KF idx, accept <= 50.
 // mode 1 = SearchByBoW(KF1, KF2): match[KF1 idx] = KF2 idx, accept < 50, valid on both sides.
@@ -33,6 +44,7 @@ struct BowProblem {
 
 struct DevFeatVec {
   int n_nodes;
+  const int* n_nodes_dev;  // nullable
   const uint32_t* node_ids;
   const int* node_offsets;
   const int* node_feats;
@@ -40,6 +52,7 @@ struct DevFeatVec {
 
 struct DevTriSide {
   int n;
+  const int* n_dev;  // nullable
   const uint8_t* desc;
   const orbx_keypoint* keys_un;
   const float* u_right;   // nullable: mono
@@ -48,6 +61,11 @@ struct DevTriSide {
   const float* scale_factors;
   const float* level_sigma2;
 };
+
+__device__ __forceinline__ int tri_n(const DevTriSide& s) { return s.n_dev ? *s.n_dev : s.n; }
+__device__ __forceinline__ int tri_nodes(const DevTriSide& s) {
+  return s.fv.n_nodes_dev ? *s.fv.n_nodes_dev : s.fv.n_nodes;
+}
 
 struct TriProblem {
   DevTriSide s1, s2;
@@ -67,6 +85,7 @@ int launch_featvec(const uint8_t* d_voc, int k, int nid_level, const uint8_t* d_
                    uint32_t* d_out, int64_t out_stride_img, int nimg, hipStream_t s);
 int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,
                uint32_t id_lo, int nb, uint32_t* d_ids, int* d_off, int* d_feats,
-               int64_t csr_stride, int* d_nn, int nimg, hipStream_t s);
+               int64_t feats_stride, int* d_nn, int nimg, hipStream_t s);
+// d_ids is [nimg][nb], d_off is [nimg][nb + 1], d_feats is [nimg][feats_stride].
 
 }  // namespace orbx

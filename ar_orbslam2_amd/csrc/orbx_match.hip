@@ -66,10 +66,11 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
   const BowProblem& P = probs[blockIdx.y];
   const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (a >= P.s1.n_nodes) return;
+  if (a >= side_nodes(P.s1)) return;
   const uint32_t id = P.s1.node_ids[a];
-  const int b = lower_bound_u32(P.s2.node_ids, P.s2.n_nodes, id);
-  if (b >= P.s2.n_nodes || P.s2.node_ids[b] != id) return;
+  const int nn2 = side_nodes(P.s2);
+  const int b = lower_bound_u32(P.s2.node_ids, nn2, id);
+  if (b >= nn2 || P.s2.node_ids[b] != id) return;
   const int f0 = P.s2.node_offsets[b], m = P.s2.node_offsets[b + 1] - f0;
   if (m > 64 * 16) {  // more candidates than the per-lane matched bitmap holds
     if (lane == 0) atomicOr(P.error, 1);
@@ -176,12 +177,13 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
   if (tid == 0) s_cnt = 0;
   __syncthreads();
   const bool kfkf = P.mode == 1;
-  const int n = kfkf ? P.s1.n : P.s2.n;
+  const int n = kfkf ? side_n(P.s1) : side_n(P.s2);
   if (P.check_ori) {
     for (int i = tid; i < n; i += 256) {
       const int m = P.match[i];
       if (m < 0) continue;
-      const int bin = kfkf ? rot_bin(P.s1.angle[i], P.s2.angle[m]) : rot_bin(P.s1.angle[m], P.s2.angle[i]);
+      const int bin = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m))
+                            : rot_bin(side_angle(P.s1, m), side_angle(P.s2, i));
       atomicAdd(&hist[bin], 1);
     }
     __syncthreads();
@@ -193,7 +195,8 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
     const int m = P.match[i];
     if (m < 0) continue;
     if (P.check_ori) {
-      const int bin = kfkf ? rot_bin(P.s1.angle[i], P.s2.angle[m]) : rot_bin(P.s1.angle[m], P.s2.angle[i]);
+      const int bin = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m))
+                            : rot_bin(side_angle(P.s1, m), side_angle(P.s2, i));
       if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
         P.match[i] = -1;
         continue;
@@ -225,10 +228,11 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
   const TriProblem& P = probs[blockIdx.y];
   const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (a >= P.s1.fv.n_nodes) return;
+  if (a >= tri_nodes(P.s1)) return;
   const uint32_t id = P.s1.fv.node_ids[a];
-  const int b = lower_bound_u32(P.s2.fv.node_ids, P.s2.fv.n_nodes, id);
-  if (b >= P.s2.fv.n_nodes || P.s2.fv.node_ids[b] != id) return;
+  const int nn2 = tri_nodes(P.s2);
+  const int b = lower_bound_u32(P.s2.fv.node_ids, nn2, id);
+  if (b >= nn2 || P.s2.fv.node_ids[b] != id) return;
   const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
   for (int pa = P.s1.fv.node_offsets[a] + lane; pa < P.s1.fv.node_offsets[a + 1]; pa += 64) {
     const int i1 = P.s1.fv.node_feats[pa];
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
   __shared__ int s_ind[3];
   __shared__ int s_scan[257];
   const int tid = threadIdx.x;
-  const int n = P.s1.n;
+  const int n = tri_n(P.s1);
   if (tid < kHISTO) hist[tid] = 0;
   __syncthreads();
   if (P.check_ori) {
@@ -357,16 +361,16 @@ __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_o
                                              int n_fixed, uint32_t id_lo, int nb,
                                              uint32_t* __restrict__ node_ids,
                                              int* __restrict__ offsets, int* __restrict__ feats,
-                                             int64_t csr_stride, int* __restrict__ n_nodes) {
+                                             int64_t feats_stride, int* __restrict__ n_nodes) {
   extern __shared__ int sm[];
   int* cnt = sm;       // nb
   int* cur = sm + nb;  // nb
   const int img = blockIdx.x, tid = threadIdx.x;
   const int n = counts ? counts[img] : n_fixed;
   const uint32_t* nodes = node_of + img * node_stride;
-  uint32_t* oid = node_ids + img * csr_stride;
-  int* ooff = offsets + img * (csr_stride + 1);
-  int* of = feats + img * csr_stride;
+  uint32_t* oid = node_ids + (int64_t)img * nb;        // [img][nb]
+  int* ooff = offsets + (int64_t)img * (nb + 1);       // [img][nb + 1]
+  int* of = feats + img * feats_stride;                // [img][feats_stride]
   for (int i = tid; i < nb; i += 256) cnt[i] = 0;
   __syncthreads();
   for (int i = tid; i < n; i += 256) atomicAdd(&cnt[nodes[i] - id_lo], 1);
@@ -445,12 +449,12 @@ int launch_featvec(const uint8_t* d_voc, int k, int nid_level, const uint8_t* d_
 
 int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,
                uint32_t id_lo, int nb, uint32_t* d_ids, int* d_off, int* d_feats,
-               int64_t csr_stride, int* d_nn, int nimg, hipStream_t s) {
+               int64_t feats_stride, int* d_nn, int nimg, hipStream_t s) {
   if (nimg <= 0) return ORBX_OK;
   const size_t smem = (size_t)(2 * nb) * 4;
   if (smem > 64 * 1024) return ORBX_EUNSUPPORTED;
   hipLaunchKernelGGL(k_csr, dim3(nimg), dim3(256), smem, s, d_node_of, node_stride, d_counts,
-                     n_fixed, id_lo, nb, d_ids, d_off, d_feats, csr_stride, d_nn);
+                     n_fixed, id_lo, nb, d_ids, d_off, d_feats, feats_stride, d_nn);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_csr");
 }
@@ -553,10 +557,11 @@ SideOffs stage_side(Stager& st, const orbx_bow_side* s) {
 }
 
 DevSide dev_side(char* base, const SideOffs& o, const orbx_bow_side* s) {
-  DevSide d;
+  DevSide d{};
   d.n = s->n;
   d.desc = dptr<const uint8_t>(base, o.desc);
   d.angle = dptr<const float>(base, o.angle);
+  d.angle_stride = 1;
   d.valid = o.valid == (size_t)-1 ? nullptr : dptr<const uint8_t>(base, o.valid);
   d.n_nodes = s->fv.n_nodes;
   d.node_ids = dptr<const uint32_t>(base, o.ids);
@@ -578,7 +583,7 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
   int rc = tls_ws.reserve(st.host.size());
   if (rc) return rc;
   char* base = tls_ws.d;
-  BowProblem P;
+  BowProblem P{};
   P.s1 = dev_side(base, o1, s1);
   P.s2 = dev_side(base, o2, s2);
   P.match = dptr<int>(base, omatch);
@@ -656,7 +661,7 @@ int orbx_search_for_triangulation(const orbx_tri_side* k1, const orbx_tri_side* 
   int rc = tls_ws.reserve(st.host.size());
   if (rc) return rc;
   char* base = tls_ws.d;
-  TriProblem P;
+  TriProblem P{};
   DevTriSide* ds[2] = {&P.s1, &P.s2};
   for (int s = 0; s < 2; s++) {
     const orbx_tri_side* k = ks[s];

@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/s of ORB extract + match (BASELINE.json metric) on MI355X.
+
+One step = one batch of `--batch` synthetic 640x480 frames (BASELINE.json configs[1], TUM
+fr1/xyz mono geometry, 1000 features) already resident in HBM, pushed through the whole
+device pipeline: ORBextractor (pyramid, FAST cells, octree, orientation, rBRIEF), vocabulary
+node ids + FeatureVector, SearchByBoW(prev-as-KF, cur) and SearchForTriangulation(prev-as-KF,
+cur-as-KF) (SURVEY §8d unit of work).  Multi-GPU: one process per GPU, each rank processes its
+own camera stream (weak scaling, no data-path collective; RCCL only carries the barrier and
+the max-over-ranks time).
+
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events on the
+pipeline stream over the timed region) and the CPU oracle baseline (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec ORB extract+match, 640×480 1000-feat; bit-exact descriptors"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CONFIGS = {
+    "C2": dict(w=640, h=480, nfeatures=1000,
+               workload="TUM fr1/xyz mono 640x480, 1000 features, 1xMI355X HIP extract+match"),
+    "C3": dict(w=752, h=480, nfeatures=1200, workload="EuRoC MH01 geometry 752x480, 1200 features"),
+    "C4": dict(w=1241, h=376, nfeatures=2000, workload="KITTI 00 geometry 1241x376, 2000 features"),
+    "C5": dict(w=1920, h=1080, nfeatures=4000, workload="synthetic 1920x1080, 4000 features"),
+}
+
+
+def level_sizes(w, h, inv_scale):
+    return [(int(np.rint(np.float32(w) * np.float32(s))), int(np.rint(np.float32(h) * np.float32(s))))
+            for s in inv_scale]
+
+
+def algorithmic_bytes(levels, n_kp, n_img):
+    """Per-kernel algorithmic bytes for one launch over n_img images (SURVEY §8d byte model:
+    input read, resize read+write, FAST read, blur read+write, 28+32 B per keypoint)."""
+    P = [w * h for w, h in levels]
+    per_resize = [(P[l - 1] + P[l]) * n_img for l in range(1, len(P))]
+    return {
+        "k_resize": sum(per_resize) / max(len(per_resize), 1),  # average launch
+        "k_blur": 2 * sum(P) * n_img,
+        "k_fast_cells": sum(P) * n_img,
+        "k_describe": 60 * n_kp,
+        "k_featvec": 36 * n_kp,
+        "total_per_frame": P[0] + sum(per_resize) / n_img + 3 * sum(P) + 60 * n_kp / n_img,
+    }
+
+
+def cpu_baseline(cfg, seconds):
+    """The CPU oracle (orb_oracle.cc restating ORBextractor/ORBmatcher) on this host, 1 thread,
+    on consecutive frames of the same synthetic stream: extract + SearchByBoW +
+    SearchForTriangulation per frame."""
+    from oracle import oracle as O
+    from ar_orbslam2_amd import synth
+    from ar_orbslam2_amd.pipeline import TUM1_K, fundamental_from_pose
+    w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
+    p = O.params(nf)
+    t = O.tables(p, w, h)
+    rng = np.random.default_rng(42)
+    voc = rng.integers(0, 256, (111, 32), dtype=np.uint8)
+    F = fundamental_from_pose()
+    ex, ey = O.epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
+    base = synth.canvas(w, h, 0)
+    imgs = [synth.frame(w, h, i, 0, base) for i in range(64)]
+
+    def fv(nodes):
+        order = np.argsort(nodes, kind="stable").astype(np.int32)
+        ids, counts = np.unique(nodes, return_counts=True)
+        offs = np.zeros(len(ids) + 1, np.int32)
+        np.cumsum(counts, out=offs[1:])
+        return ids.astype(np.uint32), offs, order
+
+    prev = None
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        img = imgs[n % len(imgs)]
+        kps, desc = O.extract(img, p)
+        nodes = O.feature_vector(voc, 10, 6, 4, desc)
+        r = np.random.default_rng(n)
+        cur = dict(desc=desc, angle=kps["angle"], keys=kps, fv=fv(nodes),
+                   valid=(r.random(len(kps)) < 0.6).astype(np.uint8),
+                   has_mp=(r.random(len(kps)) < 0.4).astype(np.uint8),
+                   scale_factors=t["scale"], level_sigma2=t["sigma2"])
+        if prev is not None:
+            O.search_by_bow_kf_f(prev, dict(cur, valid=None), 0.7, True)
+            O.search_for_triangulation(prev, cur, F, ex, ey, False, 0.6, False)
+        prev = cur
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 4:
+            break
+    return dict(value=n / el, unit="frames/s", cores=1, kind="port",
+                sample=f"{n} consecutive {w}x{h} synthetic frames, CPU oracle (oracle/orb_oracle.cc, "
+                       f"g++ -O3 -march=x86-64-v3 -ffp-contract=off), 1 thread, extract + "
+                       f"SearchByBoW + SearchForTriangulation per frame, {el:.1f} s on "
+                       f"{platform.processor() or platform.machine()}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="frames per step (per GPU)")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="time with captured hipGraphs and no per-kernel events")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+
+    from ar_orbslam2_amd import ORBextractor, Vocabulary, epipole, synth
+    from ar_orbslam2_amd.pipeline import TUM1_K, FramePipeline, fundamental_from_pose
+
+    cfg = CONFIGS[args.config]
+    w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
+    voc = Vocabulary.synthetic()
+    pipe = FramePipeline(w, h, B, voc, nf, device=local)
+    pipe.seeded_masks(range(B))
+    ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
+    pipe.set_matching(fundamental_from_pose(), (ex, ey), bow_ratio=0.7, bow_check_ori=True,
+                      tri_ratio=0.6, tri_check_ori=False)
+    # synthetic frames of this rank's camera stream, resident in HBM before timing
+    base = synth.canvas(w, h, stream=rank)
+    pool = []
+    for pi in range(args.pool):
+        fr = np.stack([synth.frame(w, h, pi * B + i, rank, base) for i in range(B)])
+        pool.append(torch.from_numpy(fr).cuda())
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        pipe.run(pool[i % len(pool)].data_ptr(), B)
+    pipe.sync()
+    kp_counts, bow, tri, err = pipe.results(B)
+    if err:
+        raise RuntimeError("matcher reported a node larger than its per-wave capacity")
+
+    profile = not args.no_profile
+    if profile:
+        pipe.profile(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        pipe.run(pool[i % len(pool)].data_ptr(), B)
+    pipe.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stages = pipe.profile_read() if profile else {}
+    pipe.profile(False)
+    kp_counts, bow, tri, _ = pipe.results(B)
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames = world * B * args.steps
+    value = frames / elapsed
+    ex_tables = ORBextractor(nf)
+    levels = level_sizes(w, h, ex_tables.GetInverseScaleFactors())
+    n_kp = int(kp_counts.sum())
+    alg = algorithmic_bytes(levels, n_kp, B)
+    roofline = None
+    if stages:
+        dom = max(stages, key=lambda k: stages[k][0])
+        ms, launches = stages[dom]
+        avg_s = ms / 1e3 / max(launches, 1)
+        a_bytes = alg.get(dom)
+        achieved = (a_bytes / avg_s / 1e9) if a_bytes is not None else None
+        roofline = {"bound": "hbm", "kernel": dom,
+                    "achieved": round(achieved, 3) if achieved is not None else None,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
+                    "traffic": None,
+                    "avg_launch_us": round(avg_s * 1e6, 2),
+                    "algorithmic_bytes_per_launch": a_bytes,
+                    "stages_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()}}
+
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B,
+                   "image": f"{w}x{h}", "nfeatures": nf, "nlevels": 8, "scale_factor": 1.2,
+                   "parallelism": f"{world} independent camera streams (one per GPU)",
+                   "keypoints_per_frame": round(n_kp / B, 1),
+                   "bow_matches_per_frame": round(float(bow.mean()), 1),
+                   "triangulation_matches_per_frame": round(float(tri.mean()), 1),
+                   "timing": "HIP events per kernel" if profile else "hipGraph replay"},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -153,6 +153,41 @@ int orbx_plan_profile(orbx_plan* plan, int32_t enable);
 int orbx_plan_profile_read(orbx_plan* plan, int32_t cap, char (*names)[32], double* total_ms,
                            int64_t* launches, int32_t* n_stages);
 
+/* ------------------------------------------------------------------ device frame pipeline
+ * The whole per-frame unit of work of the benchmark on device-resident frames:
+ * extract -> vocabulary node ids -> FeatureVector (CSR) -> SearchByBoW(prev-as-KF, cur) ->
+ * SearchForTriangulation(prev-as-KF, cur-as-KF).  Frame f of a batch is matched against frame
+ * (f-1) mod n.  `voc_desc` holds the breadth-first node descriptors of a complete k-ary tree
+ * down to level L - levelsup (see orbx_feature_vector). */
+typedef struct orbx_frames orbx_frames;
+int orbx_frames_create(const orbx_params* params, int32_t w, int32_t h, int32_t max_batch,
+                       const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
+                       int hip_device, orbx_frames** out);
+int orbx_frames_destroy(orbx_frames* fr);
+int orbx_frames_capacity(const orbx_frames* fr, int32_t* kp_cap);
+/* Host masks [max_batch][kp_cap]: valid = KF-side usable MapPoint for SearchByBoW, has_mp =
+ * GetMapPoint(i) != NULL for SearchForTriangulation.  Either may be NULL (left unchanged). */
+int orbx_frames_set_masks(orbx_frames* fr, const uint8_t* valid, const uint8_t* has_mp);
+int orbx_frames_set_matching(orbx_frames* fr, float bow_ratio, int32_t bow_check_ori,
+                             const float F12[9], float ex, float ey, float tri_ratio,
+                             int32_t tri_check_ori, int32_t only_stereo);
+/* Enqueue one batch (d_imgs: n dense w*h device images); asynchronous. */
+int orbx_frames_run(orbx_frames* fr, const uint8_t* d_imgs, int32_t n);
+int orbx_frames_sync(orbx_frames* fr);
+/* Host copies of the per-frame counts of the last run (synchronises). */
+int orbx_frames_results(orbx_frames* fr, int32_t n, int32_t* kp_counts, int32_t* bow_matches,
+                        int32_t* tri_matches, int32_t* error);
+/* Device pointers: kps/desc [max_batch][kp_cap], counts [max_batch], node ids
+ * [max_batch][kp_cap], bow match [max_batch][kp_cap] (frame-indexed, value = KF index),
+ * triangulation pairs [max_batch][kp_cap][2]. */
+int orbx_frames_outputs(orbx_frames* fr, orbx_keypoint** d_kps, uint8_t** d_desc,
+                        int32_t** d_counts, uint32_t** d_node_of, int32_t** d_bow_match,
+                        int32_t** d_tri_pairs);
+void* orbx_frames_stream(orbx_frames* fr);
+int orbx_frames_profile(orbx_frames* fr, int32_t enable);
+int orbx_frames_profile_read(orbx_frames* fr, int32_t cap, char (*names)[32], double* total_ms,
+                             int64_t* launches, int32_t* n_stages);
+
 /* ------------------------------------------------------------------ matcher */
 /* ORBmatcher::DescriptorDistance on n row pairs (host pointers). */
 int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int32_t* out);

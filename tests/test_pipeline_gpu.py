@@ -1,0 +1,75 @@
+"""GPU parity of the device frame pipeline (bench.py's unit of work) against the CPU oracle:
+per-frame keypoints/descriptors, node ids, SearchByBoW matches and SearchForTriangulation
+pairs for a small batch, frame f matched against frame (f-1) mod n."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from ar_orbslam2_amd import KEYPOINT_DTYPE, Vocabulary, epipole, synth
+from ar_orbslam2_amd.pipeline import TUM1_K, FramePipeline, fundamental_from_pose
+from oracle import oracle as O
+
+from matchdata import featvec
+
+pytestmark = pytest.mark.gpu
+
+_hip = None
+
+
+def d2h(ptr, nbytes):
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+    out = np.zeros(nbytes, np.uint8)
+    rc = _hip.hipMemcpy(C.c_void_p(out.ctypes.data), C.c_void_p(ptr), C.c_size_t(nbytes), 2)
+    assert rc == 0
+    return out
+
+
+@pytest.mark.parametrize("w,h,nf,n", [(640, 480, 1000, 4), (752, 480, 1200, 3)])
+def test_pipeline_matches_oracle(w, h, nf, n):
+    voc = Vocabulary.synthetic()
+    pipe = FramePipeline(w, h, n, voc, nf)
+    valid, has_mp = pipe.seeded_masks(range(n))
+    F = fundamental_from_pose()
+    ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
+    pipe.set_matching(F, (ex, ey), bow_ratio=0.7, bow_check_ori=True, tri_ratio=0.6,
+                      tri_check_ori=False)
+    frames = synth.frames(w, h, n, stream=2)
+    d = torch.from_numpy(frames).cuda()
+    pipe.run(d.data_ptr(), n)
+    pipe.run(d.data_ptr(), n)  # second run replays the captured graph
+    pipe.sync()
+    counts, bow, tri, err = pipe.results(n)
+    assert err == 0
+    cap = pipe.kp_cap
+    out = pipe.device_outputs()
+    kps_all = d2h(out["kps"], n * cap * 28).view(KEYPOINT_DTYPE).reshape(n, cap)
+    desc_all = d2h(out["desc"], n * cap * 32).reshape(n, cap, 32)
+    nodes_all = d2h(out["node_of"], n * cap * 4).view(np.uint32).reshape(n, cap)
+    match_all = d2h(out["bow_match"], n * cap * 4).view(np.int32).reshape(n, cap)
+    pairs_all = d2h(out["tri_pairs"], n * cap * 8).view(np.int32).reshape(n, cap, 2)
+    t = O.tables(O.params(nf), w, h)
+    ref = []
+    for f in range(n):
+        kps, desc = O.extract(frames[f], O.params(nf))
+        k = len(kps)
+        assert counts[f] == k
+        assert np.array_equal(kps_all[f, :k], kps)
+        assert np.array_equal(desc_all[f, :k], desc)
+        nodes = O.feature_vector(voc.node_desc, 10, 6, 4, desc)
+        assert np.array_equal(nodes_all[f, :k], nodes)
+        ref.append(dict(desc=desc, angle=kps["angle"], keys=kps, fv=featvec(nodes),
+                        valid=valid[f, :k], has_mp=has_mp[f, :k], scale_factors=t["scale"],
+                        level_sigma2=t["sigma2"]))
+    for f in range(n):
+        kf, cur = ref[(f - 1) % n], ref[f]
+        nb, mb = O.search_by_bow_kf_f(kf, dict(cur, valid=None), 0.7, True)
+        assert bow[f] == nb
+        assert np.array_equal(match_all[f, :len(cur["desc"])], mb)
+        nt, pt = O.search_for_triangulation(kf, cur, F, ex, ey, False, 0.6, False)
+        assert tri[f] == nt
+        assert np.array_equal(pairs_all[f, :nt], pt)
+    pipe.close()
