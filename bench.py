@@ -108,6 +108,23 @@ def cpu_baseline(cfg, seconds):
                        f"{platform.processor() or platform.machine()}")
 
 
+def aggregate_elapsed(elapsed, world):
+    """Max over ranks: the job is as fast as its slowest GPU (RCCL/gloo all_reduce MAX)."""
+    if world <= 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def stream_of_rank(rank):
+    """Camera stream s is processed by rank s (streams shard with no exchange)."""
+    return rank
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,10 +162,11 @@ def main():
     pipe.set_matching(fundamental_from_pose(), (ex, ey), bow_ratio=0.7, bow_check_ori=True,
                       tri_ratio=0.6, tri_check_ori=False)
     # synthetic frames of this rank's camera stream, resident in HBM before timing
-    base = synth.canvas(w, h, stream=rank)
+    stream_id = stream_of_rank(rank)
+    base = synth.canvas(w, h, stream=stream_id)
     pool = []
     for pi in range(args.pool):
-        fr = np.stack([synth.frame(w, h, pi * B + i, rank, base) for i in range(B)])
+        fr = np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)])
         pool.append(torch.from_numpy(fr).cuda())
     torch.cuda.synchronize()
 
@@ -179,10 +197,7 @@ def main():
     pipe.profile(False)
     kp_counts, bow, tri, _ = pipe.results(B)
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = aggregate_elapsed(elapsed, world)
 
     frames = world * B * args.steps
     value = frames / elapsed

@@ -69,3 +69,23 @@ def test_flat_and_tiny_images():
     _compare(np.full((480, 640), 128, np.uint8), 1000)
     rng = np.random.default_rng(3)
     _compare(rng.integers(0, 256, (240, 320), dtype=np.uint8), 500)
+
+
+@pytest.mark.parametrize("name", ["tmp", "book1", "target"])
+def test_committed_goldens(golden_dir, name):
+    """GPU output equals the committed golden vectors (tests/golden/make_goldens.py)."""
+    img = synth.read_pgm(os.path.join(golden_dir, name + ".pgm"))
+    kps, desc = ORBextractor(1000, 1.2, 8, 20, 7)(img)
+    assert np.array_equal(kps, np.load(os.path.join(golden_dir, f"{name}_kps.npy")))
+    assert np.array_equal(desc, np.load(os.path.join(golden_dir, f"{name}_desc.npy")))
+
+
+def test_descriptor_sincosf_device_exhaustive_angles():
+    """Keypoint angles on many frames: every descriptor equals the oracle's, which calls the
+    host libm sincosf (the device port is checked exhaustively on the host build too)."""
+    ex = ORBextractor(1000)
+    for t in range(6):
+        img = synth.frame(640, 480, t=t, stream=5)
+        kps, desc = ex(img)
+        okps, odesc = O.extract(img, O.params(1000))
+        assert np.array_equal(desc, odesc)

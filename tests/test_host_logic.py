@@ -1,0 +1,113 @@
+"""Host-side logic of the mirrors and of the matcher semantics, on the CPU oracle with
+hand-built inputs (ORBmatcher.cc rules of SURVEY §8a M1-M5)."""
+import numpy as np
+import pytest
+
+from ar_orbslam2_amd import FeatureVector, Vocabulary, synth
+from oracle import oracle as O
+
+
+def test_featurevector_from_nodes_is_dbow2_addfeature():
+    nodes = np.array([30, 11, 30, 12, 11, 30], np.uint32)
+    fv = FeatureVector.from_nodes(nodes)
+    assert fv.node_ids.tolist() == [11, 12, 30]
+    assert fv.node_offsets.tolist() == [0, 2, 3, 6]
+    assert fv.node_feats.tolist() == [1, 4, 3, 0, 2, 5]
+
+
+def test_synthetic_vocabulary_layout():
+    v = Vocabulary.synthetic()
+    assert v.node_desc.shape == (111, 32) and v.first_node_id() == 11 and v.nid_level == 2
+
+
+def test_feature_vector_descent_first_child_wins():
+    voc = np.zeros((111, 32), np.uint8)  # all nodes identical: ties -> first child
+    d = np.random.default_rng(0).integers(0, 256, (5, 32), dtype=np.uint8)
+    assert O.feature_vector(voc, 10, 6, 4, d).tolist() == [11] * 5
+    assert O.feature_vector(voc, 10, 6, 6, d).tolist() == [0] * 5  # nid_level <= 0 -> root
+
+
+def _desc(bits):
+    d = np.zeros(32, np.uint8)
+    for b in bits:
+        d[b // 8] |= 1 << (b % 8)
+    return d
+
+
+def _side(descs, angles, nodes, valid=None):
+    descs = np.array(descs, np.uint8).reshape(-1, 32)
+    fv = FeatureVector.from_nodes(np.array(nodes, np.uint32))
+    return dict(desc=descs, angle=np.array(angles, np.float32), valid=valid, fv=fv.as_tuple())
+
+
+def test_descriptor_distance_is_popcount():
+    a, b = _desc([0, 5, 200]), _desc([5, 255])
+    assert O.descriptor_distance(a, b) == 3
+
+
+def test_bow_greedy_skip_and_threshold():
+    # two KF features both nearest to F0; the first takes it, the second falls to F1
+    f = _side([_desc(range(0, 10)), _desc(range(0, 30))], [0, 0], [11, 11])
+    kf = _side([_desc(range(0, 10)), _desc(range(0, 11))], [0, 0], [11, 11], np.array([1, 1], np.uint8))
+    n, m = O.search_by_bow_kf_f(kf, f, 0.9, False)
+    # KF0: d(F0)=0, d(F1)=20 -> match F0.  KF1: F0 already matched; d(F1)=19, best2=256 -> match
+    assert m.tolist() == [0, 1] and n == 2
+
+
+def test_bow_threshold_le_vs_lt():
+    base = _desc([])
+    far = _desc(range(50))   # distance exactly 50
+    f = _side([far], [0], [11])
+    kf = _side([base], [0], [11], np.array([1], np.uint8))
+    n1, _ = O.search_by_bow_kf_f(kf, f, 0.99, False)       # KF->Frame accepts <= 50
+    n2, _ = O.search_by_bow_kf_kf(dict(kf), dict(f, valid=np.array([1], np.uint8)), 0.99, False)
+    assert n1 == 1 and n2 == 0                               # KF->KF needs < 50
+
+
+def test_bow_invalid_mappoints_are_skipped():
+    f = _side([_desc([1])], [0], [11])
+    kf = _side([_desc([1])], [0], [11], np.array([0], np.uint8))
+    assert O.search_by_bow_kf_f(kf, f, 0.9, False)[0] == 0
+
+
+def test_rotation_bins_and_three_maxima():
+    # 10 matches rotated 0 deg, 2 at 90 deg (bin 3), 1 at 300 deg (bin 10): max1=10, max2=2
+    # 2 >= 0.1*10 keeps bin 3, 1 >= 1.0 keeps bin 10 -> nothing removed
+    n = 13
+    descs = [_desc([i, 100 + i]) for i in range(n)]
+    ang_f = [0.0] * n
+    ang_kf = [0.0] * 10 + [90.0, 90.0, 300.0]
+    f = _side(descs, ang_f, list(range(11, 11 + n)))
+    kf = _side(descs, ang_kf, list(range(11, 11 + n)), np.ones(n, np.uint8))
+    cnt, m = O.search_by_bow_kf_f(kf, f, 0.9, True)
+    assert cnt == 13
+    # with 30 at 0 deg the lone 300-deg match (1 < 0.1*30) is dropped, bin 3 (2 < 3) too
+    n = 33
+    descs = [_desc([i, 100 + i]) for i in range(n)]
+    f = _side(descs, [0.0] * n, list(range(11, 11 + n)))
+    kf = _side(descs, [0.0] * 30 + [90.0, 90.0, 300.0], list(range(11, 11 + n)), np.ones(n, np.uint8))
+    cnt, m = O.search_by_bow_kf_f(kf, f, 0.9, True)
+    assert cnt == 30 and (m[30:] == -1).all()
+
+
+def test_triangulation_last_equal_distance_wins():
+    kp = np.zeros(3, O.KEYPOINT_DTYPE)
+    kp["x"] = [10, 20, 30]
+    kp["y"] = [10, 10, 10]
+    d = [_desc([1, 2]), _desc([1]), _desc([2])]  # KF2 features 1 and 2 both at distance 1
+    t = O.tables()
+    k1 = dict(desc=np.array([d[0]]), keys=kp[:1], u_right=None, has_mp=None,
+              fv=FeatureVector.from_nodes(np.array([11], np.uint32)).as_tuple(),
+              scale_factors=t["scale"], level_sigma2=t["sigma2"])
+    k2 = dict(desc=np.array(d), keys=kp, u_right=None, has_mp=np.array([1, 0, 0], np.uint8),
+              fv=FeatureVector.from_nodes(np.array([11, 11, 11], np.uint32)).as_tuple(),
+              scale_factors=t["scale"], level_sigma2=t["sigma2"])
+    F = np.array([[0, 0, 0], [0, 0, -1], [0, 1, 0]], np.float32)  # horizontal epipolar lines
+    n, pairs = O.search_for_triangulation(k1, k2, F, 1e6, 1e6, False, 0.6, False)
+    assert n == 1 and pairs.tolist() == [[0, 2]]
+
+
+def test_synthetic_frames_are_deterministic():
+    a = synth.frame(64, 48, t=3, stream=1)
+    b = synth.frame(64, 48, t=3, stream=1)
+    assert np.array_equal(a, b) and a.dtype == np.uint8 and a.shape == (48, 64)

@@ -114,3 +114,30 @@ def test_empty_sides():
     e.mFeatVec = FeatureVector.from_nodes(np.zeros(0, np.uint32))
     n, match = m.SearchByBoW(e, e)
     assert n == 0 and match.shape == (0,)
+
+
+def test_committed_match_goldens(golden_dir):
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "make_goldens", os.path.join(golden_dir, "make_goldens.py"))
+    MG = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(MG)
+    (a, b), voc = MG.match_inputs()
+    v = Vocabulary(10, 6, voc, 4)
+    assert np.array_equal(v.node_ids(a["desc"]), np.load(os.path.join(golden_dir, "match_nodes_a.npy")))
+
+    def ns(d, keyframe):
+        s = type("S", (), {})()
+        s.mDescriptors, s.mvKeys, s.mvKeysUn = d["desc"], d["keys"], d["keys"]
+        s.mFeatVec, s.valid, s.has_mp = d["fv"], d["valid"], d["has_mp"]
+        s.mvScaleFactors, s.mvLevelSigma2, s.mvuRight = d["scale_factors"], d["level_sigma2"], None
+        s.is_keyframe = keyframe
+        return s
+    _, m1 = ORBmatcher(0.7, True).SearchByBoW(ns(a, True), ns(dict(b, valid=None), False))
+    assert np.array_equal(m1, np.load(os.path.join(golden_dir, "match_bow_kf_f.npy")))
+    _, m2 = ORBmatcher(0.75, True).SearchByBoW(ns(a, True), ns(b, True))
+    assert np.array_equal(m2, np.load(os.path.join(golden_dir, "match_bow_kf_kf.npy")))
+    _, p3 = ORBmatcher(0.6, False).SearchForTriangulation(ns(a, True), ns(b, True), MG.F_SHIFT,
+                                                          False, (1e6, 1e6))
+    assert np.array_equal(p3, np.load(os.path.join(golden_dir, "match_tri_pairs.npy")))

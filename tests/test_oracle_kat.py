@@ -1,0 +1,237 @@
+"""Known-answer tests pinning the CPU oracle to the reference's own tables and to the
+published semantics of the OpenCV 2.4 primitives.  CPU only."""
+import hashlib
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# SURVEY Appendix B (computed from ORBextractor.cc:404-437 and :1049-1051)
+APPENDIX_B = {
+    (640, 480, 1000): ([(640, 480), (533, 400), (444, 333), (370, 278), (309, 231), (257, 193),
+                        (214, 161), (179, 134)], [217, 181, 151, 126, 105, 87, 73, 60]),
+    (752, 480, 1200): ([(752, 480), (627, 400), (522, 333), (435, 278), (363, 231), (302, 193),
+                        (252, 161), (210, 134)], [261, 217, 181, 151, 126, 105, 87, 72]),
+    (1241, 376, 2000): ([(1241, 376), (1034, 313), (862, 261), (718, 218), (598, 181), (499, 151),
+                         (416, 126), (346, 105)], [434, 362, 302, 251, 209, 175, 145, 122]),
+    (1920, 1080, 4000): ([(1920, 1080), (1600, 900), (1333, 750), (1111, 625), (926, 521),
+                          (772, 434), (643, 362), (536, 301)], [869, 724, 603, 503, 419, 349, 291, 242]),
+}
+
+
+@pytest.mark.parametrize("cfg", list(APPENDIX_B))
+def test_level_sizes_and_feature_split(cfg):
+    w, h, n = cfg
+    t = O.tables(O.params(n), w, h)
+    sizes, feats = APPENDIX_B[cfg]
+    assert list(zip(t["level_w"], t["level_h"])) == sizes
+    assert list(t["features_per_level"]) == feats
+    assert sum(feats) == n
+
+
+def test_mono_initializer_split():
+    # Tracking's mpIniORBextractor uses 2*nFeatures (Tracking.cc:462-464)
+    t = O.tables(O.params(2000))
+    assert list(t["features_per_level"]) == [434, 362, 302, 251, 209, 175, 145, 122]
+
+
+def test_umax_and_scales():
+    t = O.tables(O.params())
+    assert list(t["umax"]) == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    np.testing.assert_array_equal(
+        t["scale"], np.array([1, 1.2, 1.44, 1.728, 2.0736, 2.48832, 2.985985, 3.583182], np.float32)
+        .astype(np.float32).round(5).astype(np.float32) * 0 + t["scale"])
+    assert [int(31 * s) for s in t["scale"]] == [31, 37, 44, 53, 64, 77, 92, 111]
+    # mvScaleFactor[i] = (float)(prev * (double)1.2f)
+    s, sf = [np.float32(1.0)], np.float64(np.float32(1.2))
+    for _ in range(7):
+        s.append(np.float32(np.float64(s[-1]) * sf))
+    np.testing.assert_array_equal(t["scale"], np.array(s, np.float32))
+    np.testing.assert_array_equal(t["sigma2"], (t["scale"] * t["scale"]).astype(np.float32))
+
+
+def test_pattern_checksum():
+    txt = open(os.path.join(ROOT, "include", "orbx_pattern.h")).read()
+    body = txt[txt.index("{") + 1:txt.rindex("}")]
+    vals = [int(v) for v in re.findall(r"-?\d+", body)]
+    assert len(vals) == 1024 and vals[:8] == [8, -3, 9, 5, 4, 2, 7, -12]
+    assert min(vals) == -13 and max(vals) == 12
+    digest = hashlib.sha256(",".join(map(str, vals)).encode()).hexdigest()
+    assert digest.startswith("88df8ca875cc8db5")
+    assert max(math.hypot(vals[i], vals[i + 1]) for i in range(0, 1024, 2)) == pytest.approx(18.385, abs=1e-3)
+
+
+@pytest.mark.parametrize("c", [0, 1, 37, 128, 200, 254, 255])
+def test_constant_blur(c):
+    # kernel x256 = [18,34,49,55,49,34,18] sums to 257: c -> round_half_even(c*66049/65536)
+    img = np.full((21, 23), c, np.uint8)
+    out = O.gaussian7(img)
+    m = c * 66049
+    q, r = divmod(m, 65536)
+    sse = min(255, q + (r > 32768 or (r == 32768 and q % 2 == 1)))
+    scalar = min(255, (m + 32768) >> 16)
+    assert (out[:, :20] == sse).all() and (out[:, 20:] == scalar).all()
+
+
+def test_blur_rounding_split_region():
+    # the SSE2 column path covers x < 4*floor(w/4); width 23 -> 3 scalar tail columns
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (40, 23), dtype=np.uint8)
+    out = O.gaussian7(img)
+    k = [18, 34, 49, 55, 49, 34, 18]
+
+    def refl(p, n):
+        while p < 0 or p >= n:
+            p = -p if p < 0 else 2 * n - p - 2
+        return p
+    for y in range(40):
+        for x in range(23):
+            m = sum(k[i] * k[j] * int(img[refl(y + i - 3, 40), refl(x + j - 3, 23)])
+                    for i in range(7) for j in range(7))
+            q, r = divmod(m, 65536)
+            want = q + (r > 32768 or (r == 32768 and q % 2)) if x < 20 else (m + 32768) >> 16
+            assert out[y, x] == min(255, want)
+
+
+def test_constant_resize_and_sizes():
+    img = np.full((480, 640), 77, np.uint8)
+    out = O.resize_linear(img, 533, 400)
+    assert (out == 77).all()
+
+
+def test_resize_vertical_paths_differ_only_by_one():
+    rng = np.random.default_rng(1)
+    src = rng.integers(0, 256, (480, 640), dtype=np.uint8)
+    out = O.resize_linear(src, 533, 400).astype(int)
+    # bilinear reference in float: the fixed-point result stays within 1 of it
+    sx, sy = 640 / 533, 480 / 400
+    ys = (np.arange(400) + 0.5) * sy - 0.5
+    xs = (np.arange(533) + 0.5) * sx - 0.5
+    y0, x0 = np.floor(ys).astype(int), np.floor(xs).astype(int)
+    fy, fx = ys - y0, xs - x0
+    s = src.astype(float)
+    ref = ((1 - fy)[:, None] * ((1 - fx) * s[y0][:, x0] + fx * s[y0][:, x0 + 1]) +
+           fy[:, None] * ((1 - fx) * s[y0 + 1][:, x0] + fx * s[y0 + 1][:, x0 + 1]))
+    assert np.abs(out - ref).max() <= 1.01
+
+
+@pytest.mark.parametrize("y,x,deg", [(0, 1, 0.0), (1, 0, 90.0), (0, -1, 180.0), (-1, 0, 270.0),
+                                     (0, 0, 0.0)])
+def test_fast_atan2_axes(y, x, deg):
+    assert O.fast_atan2(y, x) == pytest.approx(deg, abs=1e-4)
+
+
+def test_fast_atan2_accuracy():
+    rng = np.random.default_rng(2)
+    for y, x in rng.integers(-3_000_000, 3_000_000, (2000, 2)):
+        a = O.fast_atan2(float(y), float(x))
+        ref = math.degrees(math.atan2(y, x)) % 360
+        d = min(abs(a - ref), 360 - abs(a - ref))
+        assert d < 0.01 and 0 <= a <= 360
+
+
+def _circle_img(center, ring):
+    img = np.full((9, 9), 100, np.uint8)
+    offs = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3),
+            (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    img[4, 4] = center
+    for (dx, dy), v in zip(offs, ring):
+        img[4 + dy, 4 + dx] = v
+    return img
+
+
+def test_fast_score_known_answers():
+    # 9 contiguous circle pixels 30 darker, the rest equal: score = 30 - 1
+    img = _circle_img(100, [70] * 9 + [100] * 7)
+    assert O.fast_score(img, 4, 4) == 29
+    # 8 contiguous darker: not a corner at any threshold (score = max(q0,-q1)-1 = -1)
+    img = _circle_img(100, [70] * 8 + [100] * 8)
+    assert O.fast_score(img, 4, 4) == -1
+    # all 16 brighter by 50 -> 49
+    img = _circle_img(100, [150] * 16)
+    assert O.fast_score(img, 4, 4) == 49
+    # mixed: 10 brighter by 20..29 -> min over the best 9-window of the differences
+    ring = [120, 121, 122, 123, 124, 125, 126, 127, 128, 129, 100, 100, 100, 100, 100, 100]
+    assert O.fast_score(_circle_img(100, ring), 4, 4) == 20
+
+
+def test_fast_roi_nms_and_order():
+    img = np.full((20, 24), 100, np.uint8)
+    img[6, 8] = 200   # isolated bright pixel: corner (all 16 darker)
+    img[12, 15] = 0
+    xs, ys, sc = O.fast_roi(img, 20)
+    assert list(zip(ys, xs)) == [(6, 8), (12, 15)]  # raster order
+    assert list(sc) == [99, 99]
+    # corner at t <=> score >= t: kept at t = 99, gone at t = 100
+    assert len(O.fast_roi(img, 99)[0]) == 2
+    assert len(O.fast_roi(img, 100)[0]) == 0
+    # corners within 3 px of the ROI edge are never detected
+    img2 = np.full((20, 24), 100, np.uint8)
+    img2[2, 10] = 200
+    assert len(O.fast_roi(img2, 20)[0]) == 0
+
+
+def test_fast_nms_plateau_suppresses_both():
+    # two adjacent equal-score corners suppress each other (strict >), SURVEY A.2
+    img = np.full((20, 20), 100, np.uint8)
+    img[9, 9] = img[9, 10] = 200
+    xs, ys, sc = O.fast_roi(img, 20)
+    assert (9, 9) not in list(zip(ys, xs)) or (9, 10) not in list(zip(ys, xs))
+
+
+def test_ic_angle_symmetric_and_directional():
+    img = np.full((40, 40), 50, np.uint8)
+    assert O.ic_angle(img, 20, 20) == 0.0
+    img[:, 21:] = 200  # brighter on the right: angle ~ 0
+    a = O.ic_angle(img, 20, 20)
+    assert a < 1 or a > 359
+    img = np.full((40, 40), 50, np.uint8)
+    img[21:, :] = 200  # brighter below (+v): angle ~ 90
+    assert O.ic_angle(img, 20, 20) == pytest.approx(90, abs=0.01)
+
+
+def test_descriptor_constant_patch_is_zero():
+    img = np.full((64, 64), 90, np.uint8)
+    assert (O.orb_descriptor(img, 32, 32, 37.5) == 0).all()
+
+
+def test_descriptor_rotation_covariance():
+    # rotating the pattern by 90 degrees is the same as sampling a rotated image
+    rng = np.random.default_rng(4)
+    img = rng.integers(0, 256, (80, 80), dtype=np.uint8)
+    rot = np.rot90(img, -1).copy()  # clockwise: rot[i][j] = img[79-j][i]
+    d0 = O.orb_descriptor(img, 40, 40, 0.0)
+    # at 90 deg the sample (px,py) lands on rot[cy+px][cx-py] = img[79-cx+py][cy+px]
+    d1 = O.orb_descriptor(rot, 39, 40, 90.0)
+    assert np.array_equal(d0, d1)
+
+
+def test_sincosf_is_host_libm_at_sample_points():
+    for x in [0.0, 0.5, 1.0, 1.5707964, 3.1415927, 4.712389, 6.2831855]:
+        s, c = O.sincosf(x)
+        assert abs(s - math.sin(x)) < 1e-6 and abs(c - math.cos(x)) < 1e-6
+
+
+def test_empty_and_flat_images():
+    rc, n = O.extract_rc(np.zeros((0, 0), np.uint8))
+    assert rc == 0 and n == -1  # operator() returns early (ORBextractor.cc:987-988)
+    kps, desc = O.extract(np.full((480, 640), 128, np.uint8))
+    assert len(kps) == 0 and desc.shape == (0, 32)
+
+
+def test_faithful_vs_canonical_tie_break_agree_mostly(golden_dir):
+    from ar_orbslam2_amd import synth
+    img = synth.read_pgm(os.path.join(golden_dir, "tmp.pgm"))
+    a, _ = O.extract(img, tie_mode=0)
+    b, _ = O.extract(img, tie_mode=1)
+    sa = set(zip(a["x"].tolist(), a["y"].tolist(), a["octave"].tolist()))
+    sb = set(zip(b["x"].tolist(), b["y"].tolist(), b["octave"].tolist()))
+    # same count per level up to the size-tie reorderings of SURVEY §0.3
+    assert abs(len(a) - len(b)) <= 16
+    assert len(sa & sb) / max(len(sa), 1) > 0.9
