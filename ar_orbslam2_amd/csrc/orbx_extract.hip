@@ -5,7 +5,8 @@
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
 //   k_resize      x (nlevels-1)  pyramid level l from level l-1     (cv::resize INTER_LINEAR)
 //   k_blur        x 1            all levels, 64x16 LDS tiles         (GaussianBlur 7x7 s=2)
-//   k_fast_cells  x 1            one workgroup per FAST cell         (cv::FAST + cell fallback)
+//   k_fast_score  x 1            64x16 tiles, all levels            (FAST score map)
+//   k_fast_nms    x 1            one wave per FAST cell             (cv::FAST NMS + cell fallback)
 //   k_octree      x 1            one workgroup per (image, level)    (DistributeOctTree)
 //   k_describe    x 1            one wave per keypoint               (IC_Angle + rBRIEF)
 // Level 0 is read in place from the caller's input buffer; levels >= 1 live in the pyramid
@@ -32,11 +33,10 @@ __constant__ int8_t c_pattern[1024];
 __constant__ int c_umax[kHalfPatch + 1];
 
 // ------------------------------------------------------------------ helpers
-__device__ __forceinline__ const uint8_t* level_base(const uint8_t* in, const uint8_t* pyr,
-                                                     int64_t pyr_bytes, const LevelGeom& g,
-                                                     int level, int img) {
-  return level == 0 ? in + (int64_t)img * g.w * g.h
-                    : pyr + (int64_t)img * pyr_bytes + g.pyr_off;
+// Every level (level 0 copied in by k_copy0) lives in the image's pitched pyramid block.
+__device__ __forceinline__ const uint8_t* level_base(const uint8_t* pyr, int64_t pyr_bytes,
+                                                     const LevelGeom& g, int img) {
+  return pyr + (int64_t)img * pyr_bytes + g.pyr_off;
 }
 
 __device__ __forceinline__ int reflect101(int p, int len) {
@@ -101,32 +101,33 @@ __device__ int block_scan_excl(int* a, int M, int* s_tmp) {
   return total;
 }
 
+// ------------------------------------------------------------------ k_copy0
+// Level 0 = the input image (ComputePyramid level 0, ORBextractor.cc:1066-1068) copied into the
+// 64-B pitched pyramid block so every later kernel reads aligned dwords.
+__global__ __launch_bounds__(256) void k_copy0(const uint8_t* __restrict__ in,
+                                               uint8_t* __restrict__ pyr, int64_t pyr_bytes,
+                                               const LevelGeom* __restrict__ lv) {
+  const LevelGeom& G = lv[0];
+  const int img = blockIdx.z, y = blockIdx.y;
+  const int x4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (x4 >= G.w) return;
+  const uint8_t* src = in + ((int64_t)img * G.h + y) * G.w + x4;
+  uint32_t v = src[0];
+  if (x4 + 1 < G.w) v |= (uint32_t)src[1] << 8;
+  if (x4 + 2 < G.w) v |= (uint32_t)src[2] << 16;
+  if (x4 + 3 < G.w) v |= (uint32_t)src[3] << 24;
+  *(uint32_t*)(pyr + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch + x4) = v;
+}
+
 // ------------------------------------------------------------------ k_resize
 // cv::resize(level l-1 ROI -> level l ROI, INTER_LINEAR), 8UC1 fixed point:
 // horizontal taps Q11 ints, vertical pass = SSE2 mulhi form for x < vxs, scalar
-// (H0*b0 + H1*b1 + 2^21) >> 22 tail.  One thread per output pixel; rows of level l-1 are L2
-// resident (written by the previous launch).
-__global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ in,
-                                                uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-                                                const LevelGeom* __restrict__ lv, int level,
-                                                const int* __restrict__ xofs,
-                                                const int16_t* __restrict__ xa,
-                                                const int* __restrict__ yofs,
-                                                const int16_t* __restrict__ yb) {
-  const LevelGeom& D = lv[level];
-  const LevelGeom& S = lv[level - 1];
-  const int img = blockIdx.y;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= D.w * D.h) return;
-  const int dy = idx / D.w, dx = idx - dy * D.w;
-  const uint8_t* src = level_base(in, pyr, pyr_bytes, S, level - 1, img);
-  uint8_t* dst = pyr + (int64_t)img * pyr_bytes + D.pyr_off;
-  const int sy0 = yofs[D.coef_y + dy];
-  const int ya = sy0 >= 0 ? (sy0 < S.h ? sy0 : S.h - 1) : 0;
-  const int yb1 = sy0 + 1 >= 0 ? (sy0 + 1 < S.h ? sy0 + 1 : S.h - 1) : 0;
+// (H0*b0 + H1*b1 + 2^21) >> 22 tail.  One thread per 4 output pixels (one aligned dword
+// store); the two source rows of level l-1 are L2 resident (written by the previous launch).
+__device__ __forceinline__ int resize_px(const uint8_t* r0, const uint8_t* r1, int dx,
+                                         const LevelGeom& D, const int* __restrict__ xofs,
+                                         const int16_t* __restrict__ xa, int b0, int b1) {
   const int x0 = xofs[D.coef_x + dx];
-  const uint8_t* r0 = src + (int64_t)ya * S.w;
-  const uint8_t* r1 = src + (int64_t)yb1 * S.w;
   int h0, h1;
   if (dx < D.xmax) {
     const int a0 = xa[2 * (D.coef_x + dx)], a1 = xa[2 * (D.coef_x + dx) + 1];
@@ -136,7 +137,6 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ in,
     h0 = r0[x0] * 2048;
     h1 = r1[x0] * 2048;
   }
-  const int b0 = yb[2 * (D.coef_y + dy)], b1 = yb[2 * (D.coef_y + dy) + 1];
   int v;
   if (dx < D.vxs) {
     const int t0 = max(-32768, min(32767, h0 >> 4));
@@ -148,7 +148,36 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ in,
   } else {
     v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
   }
-  dst[(int64_t)dy * D.w + dx] = (uint8_t)max(0, min(255, v));
+  return max(0, min(255, v));
+}
+
+__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, int64_t pyr_bytes,
+                                                const LevelGeom* __restrict__ lv, int level,
+                                                const int* __restrict__ xofs,
+                                                const int16_t* __restrict__ xa,
+                                                const int* __restrict__ yofs,
+                                                const int16_t* __restrict__ yb) {
+  const LevelGeom& D = lv[level];
+  const LevelGeom& S = lv[level - 1];
+  const int img = blockIdx.z, dy = blockIdx.y;
+  const int dx0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (dx0 >= D.w) return;
+  const uint8_t* src = level_base(pyr, pyr_bytes, S, img);
+  uint8_t* dst = pyr + (int64_t)img * pyr_bytes + D.pyr_off;
+  const int sy0 = yofs[D.coef_y + dy];
+  const int ya = sy0 >= 0 ? (sy0 < S.h ? sy0 : S.h - 1) : 0;
+  const int yb1 = sy0 + 1 >= 0 ? (sy0 + 1 < S.h ? sy0 + 1 : S.h - 1) : 0;
+  const uint8_t* r0 = src + (int64_t)ya * S.pitch;
+  const uint8_t* r1 = src + (int64_t)yb1 * S.pitch;
+  const int b0 = yb[2 * (D.coef_y + dy)], b1 = yb[2 * (D.coef_y + dy) + 1];
+  uint32_t out = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int dx = dx0 + k;
+    if (dx < D.w) out |= (uint32_t)resize_px(r0, r1, dx, D, xofs, xa, b0, b1) << (8 * k);
+  }
+  // pitch is a multiple of 64, so the padding bytes of the last dword are in the row's pad
+  *(uint32_t*)(dst + (int64_t)dy * D.pitch + dx0) = out;
 }
 
 // ------------------------------------------------------------------ k_blur
@@ -156,53 +185,88 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ in,
 // (SURVEY A.4): integer row pass with taps [18,34,49,55,49,34,18], column pass rounded
 // half-even (SSE2 f32 region x < 4*floor(w/4)) or half-up (scalar tail).  Values below 256
 // are exact in f32, so half-even rounding of m/65536 is done on the integer m.
-constexpr int kBlurTW = 64, kBlurTH = 16;
+// Tile 64 x 32 outputs: interior tiles stage the (32+6) x 72 input window with aligned dword
+// loads, border tiles byte-wise through reflect101; every thread then produces 4 adjacent
+// row sums (ds_write_b128) and 4 adjacent outputs (7 x ds_read_b128, one dword store).
+constexpr int kBlurTW = 64, kBlurTH = 32;
 struct BlurTile {
-  int16_t level, tx, ty, pad;
+  int16_t level, tx, ty, interior;
 };
 
-__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ in,
-                                              const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-                                              uint8_t* __restrict__ blur, int64_t blur_bytes,
-                                              const int64_t* __restrict__ blur_off,
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
+                                              uint8_t* __restrict__ blur,
                                               const LevelGeom* __restrict__ lv,
                                               const BlurTile* __restrict__ tiles) {
-  __shared__ uint8_t s_in[kBlurTH + 6][kBlurTW + 8];
-  __shared__ int s_row[kBlurTH + 6][kBlurTW + 1];
+  __shared__ __align__(16) uint32_t s_in[kBlurTH + 6][(kBlurTW + 8) / 4];
+  __shared__ __align__(16) int s_row[kBlurTH + 6][kBlurTW];
   const BlurTile T = tiles[blockIdx.x];
   const int img = blockIdx.y;
   const LevelGeom& G = lv[T.level];
-  const uint8_t* src = level_base(in, pyr, pyr_bytes, G, T.level, img);
-  uint8_t* dst = blur + (int64_t)img * blur_bytes + blur_off[T.level];
+  const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
+  uint8_t* dst = blur + (int64_t)img * pyr_bytes + G.pyr_off;
   const int X0 = T.tx * kBlurTW, Y0 = T.ty * kBlurTH;
   const int tid = threadIdx.x;
-  for (int i = tid; i < (kBlurTH + 6) * (kBlurTW + 6); i += 256) {
-    const int r = i / (kBlurTW + 6), c = i - r * (kBlurTW + 6);
-    const int y = reflect101(Y0 + r - 3, G.h), x = reflect101(X0 + c - 3, G.w);
-    s_in[r][c] = src[(int64_t)y * G.w + x];
+  constexpr int kWords = (kBlurTW + 8) / 4;  // window columns X0-4 .. X0+67
+  if (T.interior) {
+    for (int i = tid; i < (kBlurTH + 6) * kWords; i += 256) {
+      const int r = i / kWords, c = i - r * kWords;
+      s_in[r][c] = *(const uint32_t*)(src + (int64_t)(Y0 + r - 3) * G.pitch + X0 - 4 + 4 * c);
+    }
+  } else {
+    uint8_t* sb = (uint8_t*)s_in;
+    for (int i = tid; i < (kBlurTH + 6) * (kBlurTW + 8); i += 256) {
+      const int r = i / (kBlurTW + 8), c = i - r * (kBlurTW + 8);
+      const int y = reflect101(min(Y0 + r - 3, G.h + 8), G.h);
+      const int x = reflect101(min(X0 + c - 4, G.w + 8), G.w);
+      sb[r * (kBlurTW + 8) + c] = src[(int64_t)y * G.pitch + x];
+    }
   }
   __syncthreads();
   const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;
-  for (int i = tid; i < (kBlurTH + 6) * kBlurTW; i += 256) {
-    const int r = i / kBlurTW, c = i - r * kBlurTW;
-    const uint8_t* p = &s_in[r][c];
-    s_row[r][c] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+  for (int i = tid; i < (kBlurTH + 6) * (kBlurTW / 4); i += 256) {
+    const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
+    // bytes X0+4q-4 .. X0+4q+7 of row r
+    const uint32_t w0 = s_in[r][q], w1 = s_in[r][q + 1], w2 = s_in[r][q + 2];
+    int b[12];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      b[k] = (w0 >> (8 * k)) & 0xFF;
+      b[4 + k] = (w1 >> (8 * k)) & 0xFF;
+      b[8 + k] = (w2 >> (8 * k)) & 0xFF;
+    }
+    int4 o;
+    o.x = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
+    o.y = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
+    o.z = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
+    o.w = k0 * (b[4] + b[10]) + k1 * (b[5] + b[9]) + k2 * (b[6] + b[8]) + k3 * b[7];
+    *(int4*)&s_row[r][4 * q] = o;
   }
   __syncthreads();
-  for (int i = tid; i < kBlurTH * kBlurTW; i += 256) {
-    const int r = i / kBlurTW, c = i - r * kBlurTW;
-    const int x = X0 + c, y = Y0 + r;
+  for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
+    const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
+    const int x = X0 + 4 * q, y = Y0 + r;
     if (x >= G.w || y >= G.h) continue;
-    const int m = k0 * (s_row[r][c] + s_row[r + 6][c]) + k1 * (s_row[r + 1][c] + s_row[r + 5][c]) +
-                  k2 * (s_row[r + 2][c] + s_row[r + 4][c]) + k3 * s_row[r + 3][c];
-    int v;
-    if (x < G.bxs) {
-      const int q = m >> 16, rem = m & 0xFFFF;  // m >= 0
-      v = q + (rem > 0x8000 || (rem == 0x8000 && (q & 1)));
-    } else {
-      v = (m + 32768) >> 16;
+    int4 R[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) R[k] = *(const int4*)&s_row[r + k][4 * q];
+    int m[4];
+    m[0] = k0 * (R[0].x + R[6].x) + k1 * (R[1].x + R[5].x) + k2 * (R[2].x + R[4].x) + k3 * R[3].x;
+    m[1] = k0 * (R[0].y + R[6].y) + k1 * (R[1].y + R[5].y) + k2 * (R[2].y + R[4].y) + k3 * R[3].y;
+    m[2] = k0 * (R[0].z + R[6].z) + k1 * (R[1].z + R[5].z) + k2 * (R[2].z + R[4].z) + k3 * R[3].z;
+    m[3] = k0 * (R[0].w + R[6].w) + k1 * (R[1].w + R[5].w) + k2 * (R[2].w + R[4].w) + k3 * R[3].w;
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int v;
+      if (x + k < G.bxs) {
+        const int qv = m[k] >> 16, rem = m[k] & 0xFFFF;  // m >= 0
+        v = qv + (rem > 0x8000 || (rem == 0x8000 && (qv & 1)));
+      } else {
+        v = (m[k] + 32768) >> 16;
+      }
+      out |= (uint32_t)min(255, v) << (8 * k);
     }
-    dst[(int64_t)y * G.w + x] = (uint8_t)min(255, v);
+    *(uint32_t*)(dst + (int64_t)y * G.pitch + x) = out;  // bytes past w land in the row pad
   }
 }
 
@@ -271,91 +335,176 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* V, int vs, int p, int t)
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_fast_cells(
-    const uint8_t* __restrict__ in, const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-    const LevelGeom* __restrict__ lv, const CellGeom* __restrict__ cells, int ncells,
-    int ini_th, int min_th, uint32_t* __restrict__ cand, int cand_total,
-    int* __restrict__ cell_counts) {
-  __shared__ uint8_t s_roi[kCellMax * kCellMax];
-  __shared__ uint8_t s_v[(kCellMax - 4) * (kCellMax - 4)];
-  __shared__ int s_tmp[8];
-  const int ci = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+// Necessary condition for "corner at t" (9 contiguous darker/brighter): two consecutive
+// quarter points of the circle (0,4,8,12) both darker or both brighter.
+__device__ __forceinline__ bool fast_maybe(const uint8_t* s, int stride, int x, int y, int t) {
+  const uint8_t* c = s + y * stride + x;
+  const int v = c[0];
+  const int p0 = c[3 * stride], p4 = c[3], p8 = c[-3 * stride], p12 = c[-3];
+  const int lo = v - t, hi = v + t;
+  const bool d0 = p0 < lo, d4 = p4 < lo, d8 = p8 < lo, d12 = p12 < lo;
+  const bool b0 = p0 > hi, b4 = p4 > hi, b8 = p8 > hi, b12 = p12 > hi;
+  return ((d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0)) |
+         ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0));
+}
+
+// ---- k_fast_score: FAST score map V = clamp(cornerScore+1, 0, 255) of every pixel of the
+// detection region [19, w-19) x [19, h-19) of every level (0 elsewhere).  A pixel that fails the
+// quarter-point test at min(iniThFAST, minThFAST) cannot be a corner at either threshold, so
+// its V (<= threshold) is equivalent to 0 in every NMS; only candidates get the full score.
+// Tile 64 x 64: aligned-dword staging of the (64+6) x 72 window, then per wave 16 rows, a
+// wave-local queue of candidates (ballot + mbcnt, no block barrier) scored 64 at a time.
+constexpr int kFastTW = 64, kFastTH = 64;
+struct FastTile {
+  int16_t level, tx, ty, pad;
+};
+
+__global__ __launch_bounds__(256) void k_fast_score(const uint8_t* __restrict__ pyr,
+                                                    int64_t pyr_bytes,
+                                                    uint8_t* __restrict__ vmap,
+                                                    const LevelGeom* __restrict__ lv,
+                                                    const FastTile* __restrict__ tiles, int t_lo) {
+  constexpr int kW = (kFastTW + 8) / 4;  // dwords per staged row: X0-4 .. X0+67
+  __shared__ __align__(16) uint32_t s_in[kFastTH + 6][kW];
+  __shared__ __align__(16) uint8_t s_v[kFastTH][kFastTW];
+  __shared__ uint16_t s_q[4][(kFastTH / 4) * 64];
+  const FastTile T = tiles[blockIdx.x];
+  const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const LevelGeom& G = lv[T.level];
+  const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
+  const int X0 = T.tx * kFastTW, Y0 = T.ty * kFastTH;
+  for (int i = tid; i < (kFastTH + 6) * kW; i += 256) {
+    const int r = i / kW, c = i - r * kW;
+    const int y = min(max(Y0 + r - 3, 0), G.h - 1);
+    const int x = X0 - 4 + 4 * c;
+    s_in[r][c] = (x >= 0 && x + 4 <= G.pitch) ? *(const uint32_t*)(src + (int64_t)y * G.pitch + x)
+                                              : 0u;
+  }
+  __syncthreads();
+  const uint8_t* sb = (const uint8_t*)s_in;
+  constexpr int SB = kW * 4;  // staged row stride in bytes
+  const int x = X0 + lane;
+  const bool xin = x >= kEdge && x < G.w - kEdge;
+  uint16_t* q = s_q[wid];
+  int nq = 0;
+#pragma unroll 4
+  for (int rr = 0; rr < kFastTH / 4; rr++) {
+    const int r = wid * (kFastTH / 4) + rr, y = Y0 + r;
+    s_v[r][lane] = 0;
+    const bool f = xin && y >= kEdge && y < G.h - kEdge &&
+                   fast_maybe(sb, SB, lane + 4, r + 3, t_lo);
+    const uint64_t m = __ballot(f);
+    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    if (f) q[nq + rank] = (uint16_t)((r << 6) | lane);
+    nq += __popcll(m);
+  }
+  for (int i0 = 0; i0 < nq; i0 += 64) {
+    const int i = i0 + lane;
+    if (i < nq) {
+      const int e = q[i], r = e >> 6, c = e & 63;
+      const int sc = fast_score(sb, SB, c + 4, r + 3);
+      s_v[r][c] = (uint8_t)min(255, max(0, sc + 1));
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < kFastTH * (kFastTW / 4); i += 256) {
+    const int r = i >> 4, c4 = (i & 15) * 4;  // kFastTH rows x 16 dwords
+    const int y = Y0 + r;
+    if (y < G.h && X0 + c4 < G.pitch)
+      *(uint32_t*)(vmap + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch + X0 + c4) =
+          *(const uint32_t*)&s_v[r][c4];
+  }
+}
+
+// ---- k_fast_nms: cv::FAST's strict 8-neighbour NMS restricted to each cell's detection
+// region (neighbours outside it count as 0), survivors at iniThFAST, else at minThFAST
+// (ORBextractor.cc:776-784), raster-ordered compaction into the cell's candidate slot.
+// One wave per cell; the cell's V window (<= 62 x 62) is staged in LDS with the ring zeroed.
+__global__ __launch_bounds__(256) void k_fast_nms(const uint8_t* __restrict__ vmap,
+                                                  int64_t pyr_bytes,
+                                                  const LevelGeom* __restrict__ lv,
+                                                  const CellGeom* __restrict__ cells, int ncells,
+                                                  int ini_th, int min_th,
+                                                  uint32_t* __restrict__ cand, int cand_total,
+                                                  int* __restrict__ cell_counts) {
+  constexpr int VS = kCellMax - 2;  // 64 >= dc + 2
+  __shared__ uint8_t s_w[4][(kCellMax - 4) * VS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ci = blockIdx.x * 4 + wid, img = blockIdx.y;
+  if (ci >= ncells) return;
   const CellGeom C = cells[ci];
   const LevelGeom& G = lv[C.level];
-  const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;
-  const int dr = rows - 6, dc = cols - 6;
+  const int dr = C.y1 - C.y0 - 6, dc = C.x1 - C.x0 - 6;
   int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
   if (dr <= 0 || dc <= 0) {
-    if (tid == 0) *cnt_out = 0;
+    if (lane == 0) *cnt_out = 0;
     return;
   }
-  const uint8_t* L = level_base(in, pyr, pyr_bytes, G, C.level, img);
-  for (int i = tid; i < rows * cols; i += 256) {
-    const int r = i / cols, c = i - r * cols;
-    s_roi[i] = L[(int64_t)(C.y0 + r) * G.w + C.x0 + c];
-  }
-  const int vs = dc + 2;  // score map with a zero ring (out-of-region neighbours count as 0)
-  for (int i = tid; i < (dr + 2) * vs; i += 256) s_v[i] = 0;
-  __syncthreads();
+  uint8_t* W = s_w[wid];
+  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + G.pyr_off +
+                     (int64_t)(C.y0 + 3) * G.pitch + C.x0 + 3;
+  // W[(r+1)*VS + c+1] = V at detection pixel (r, c); the ring is 0 (cell-local NMS)
+  for (int i = lane; i < (dr + 2) * VS; i += 64) W[i] = 0;
   const int npix = dr * dc;
-  const int per = (npix + 255) / 256;
-  const int beg = min(tid * per, npix), end = min(beg + per, npix);
-  for (int p = beg; p < end; p++) {
-    const int r = p / dc, c = p - r * dc;
-    const int s = fast_score(s_roi, cols, c + 3, r + 3);
-    s_v[(r + 1) * vs + c + 1] = (uint8_t)min(255, max(0, s + 1));
-  }
-  __syncthreads();
-  int mine = 0;
-  for (int p = beg; p < end; p++) {
-    const int r = p / dc, c = p - r * dc;
-    mine += nms_keep(s_v, vs, (r + 1) * vs + c + 1, ini_th);
-  }
-  int total = block_sum<256>(mine, s_tmp);
-  int t = ini_th;
-  if (total == 0 && min_th != ini_th) {
-    t = min_th;
-    mine = 0;
-    for (int p = beg; p < end; p++) {
-      const int r = p / dc, c = p - r * dc;
-      mine += nms_keep(s_v, vs, (r + 1) * vs + c + 1, t);
-    }
-  }
-  // stable block exclusive scan of per-thread counts
-  __shared__ int s_cnt[256];
-  s_cnt[tid] = mine;
-  __syncthreads();
-  if (tid < 64) {
-    int a = s_cnt[tid * 4], b = s_cnt[tid * 4 + 1], c = s_cnt[tid * 4 + 2], d = s_cnt[tid * 4 + 3];
-    const int loc = a + b + c + d;
-    int v = loc;
+  const float rdc = 1.0f / (float)dc;  // (p + 0.5) / dc is never within 1/120 of an integer
+  constexpr int U = 8;
+  for (int b = 0; b < npix; b += 64 * U) {
+    uint8_t v[U];
+    int wi[U];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int n = __shfl_up(v, off);
-      if (tid >= off) v += n;
-    }
-    int base = v - loc;
-    s_cnt[tid * 4] = base;
-    s_cnt[tid * 4 + 1] = base + a;
-    s_cnt[tid * 4 + 2] = base + a + b;
-    s_cnt[tid * 4 + 3] = base + a + b + c;
-    if (tid == 63) s_tmp[0] = v;
-  }
-  __syncthreads();
-  total = s_tmp[0];
-  int pos = s_cnt[tid];
-  uint32_t* out = cand + (int64_t)img * cand_total + C.slot_off;
-  if (mine) {
-    for (int p = beg; p < end; p++) {
-      const int r = p / dc, c = p - r * dc;
-      const int q = (r + 1) * vs + c + 1;
-      if (nms_keep(s_v, vs, q, t)) {
-        const uint32_t x = (uint32_t)(c + 3 + C.offx), y = (uint32_t)(r + 3 + C.offy);
-        out[pos++] = x | (y << 12) | ((uint32_t)(s_v[q] - 1) << 24);
+    for (int k = 0; k < U; k++) {  // issue every load of the batch before any LDS store
+      const int p = b + k * 64 + lane;
+      wi[k] = -1;
+      v[k] = 0;
+      if (p < npix) {
+        const int r = (int)(((float)p + 0.5f) * rdc), c = p - r * dc;
+        wi[k] = (r + 1) * VS + c + 1;
+        v[k] = V[(int64_t)r * G.pitch + c];
       }
     }
+#pragma unroll
+    for (int k = 0; k < U; k++)
+      if (wi[k] >= 0) W[wi[k]] = v[k];
   }
-  if (tid == 0) *cnt_out = total;
+  // survivors at iniThFAST, in raster order = flattened order; keep bits per iteration
+  const int iters = (npix + 63) >> 6;  // <= 57
+  uint64_t kb = 0;
+  int total = 0;
+  for (int it = 0; it < iters; it++) {
+    const int p = it * 64 + lane;
+    bool k = false;
+    if (p < npix) {
+      const int r = (int)(((float)p + 0.5f) * rdc), c = p - r * dc;
+      k = nms_keep(W, VS, (r + 1) * VS + c + 1, ini_th);
+    }
+    kb |= (uint64_t)k << it;
+    total += __popcll(__ballot(k));
+  }
+  const int t = ini_th;
+  uint32_t* out = cand + (int64_t)img * cand_total + C.slot_off;
+  int nout = 0;
+  const bool redo = total == 0 && min_th != ini_th;  // ORBextractor.cc:780-784
+  for (int it = 0; it < iters; it++) {
+    const int p = it * 64 + lane;
+    int r = 0, c = 0;
+    bool k = (kb >> it) & 1;
+    if (p < npix) {
+      r = (int)(((float)p + 0.5f) * rdc);
+      c = p - r * dc;
+      if (redo) k = nms_keep(W, VS, (r + 1) * VS + c + 1, min_th);
+    }
+    const uint64_t m = __ballot(k);
+    if (k) {
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      const uint32_t x = (uint32_t)(c + 3 + C.offx), y = (uint32_t)(r + 3 + C.offy);
+      out[nout + rank] = x | (y << 12) | ((uint32_t)(W[(r + 1) * VS + c + 1] - 1) << 24);
+    }
+    nout += __popcll(m);
+  }
+  (void)t;
+  if (lane == 0) *cnt_out = nout;
 }
 
 // ------------------------------------------------------------------ k_octree
@@ -653,8 +802,7 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
 // fmaf + cvRound sampling (ORBextractor.cc:101-144), then the level-0 scaling of
 // operator() (:1035-1041).  Output is level-major like `_keypoints`/`descriptors`.
 __global__ __launch_bounds__(256) void k_describe(
-    const uint8_t* __restrict__ in, const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-    const uint8_t* __restrict__ blur, int64_t blur_bytes, const int64_t* __restrict__ blur_off,
+    const uint8_t* __restrict__ pyr, int64_t pyr_bytes, const uint8_t* __restrict__ blur,
     const LevelGeom* __restrict__ lv, int nlevels, const uint32_t* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
@@ -679,8 +827,8 @@ __global__ __launch_bounds__(256) void k_describe(
   const int cx = (int)(key & 0xFFF) + (kEdge - 3), cy = (int)((key >> 12) & 0xFFF) + (kEdge - 3);
   const float response = (float)(key >> 24);
   // IC_Angle: lanes 0..30 rows v = 0..7, lanes 32..62 rows v = 8..15; u = (lane & 31) - 15
-  const uint8_t* L = level_base(in, pyr, pyr_bytes, G, level, img);
-  const uint8_t* center = L + (int64_t)cy * G.w + cx;
+  const uint8_t* L = level_base(pyr, pyr_bytes, G, img);
+  const uint8_t* center = L + (int64_t)cy * G.pitch + cx;
   int m10 = 0, m01 = 0;
   const int u = (lane & 31) - 15;
   if ((lane & 31) < 31) {
@@ -691,7 +839,7 @@ __global__ __launch_bounds__(256) void k_describe(
       if (v == 0) {
         m10 += u * center[u];
       } else {
-        const int vp = center[u + v * G.w], vm = center[u - v * G.w];
+        const int vp = center[u + v * G.pitch], vm = center[u - v * G.pitch];
         m10 += u * (vp + vm);
         m01 += v * (vp - vm);
       }
@@ -707,8 +855,8 @@ __global__ __launch_bounds__(256) void k_describe(
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float sn, cs;
   orbx_sincosf(angle * factorPI, &sn, &cs);
-  const uint8_t* B = blur + (int64_t)img * blur_bytes + blur_off[level];
-  const uint8_t* bc = B + (int64_t)cy * G.w + cx;
+  const uint8_t* B = blur + (int64_t)img * pyr_bytes + G.pyr_off;
+  const uint8_t* bc = B + (int64_t)cy * G.pitch + cx;
   int nib = 0;
 #pragma unroll
   for (int m = 0; m < 4; m++) {
@@ -720,7 +868,7 @@ __global__ __launch_bounds__(256) void k_describe(
       const float py = (float)c_pattern[pair * 4 + e * 2 + 1];
       const int row = (int)__builtin_rintf(__builtin_fmaf(px, sn, py * cs));
       const int col = (int)__builtin_rintf(__builtin_fmaf(px, cs, -(py * sn)));
-      t[e] = bc[(int64_t)row * G.w + col];
+      t[e] = bc[(int64_t)row * G.pitch + col];
     }
     nib |= (t[0] < t[1]) << m;
   }
@@ -755,10 +903,11 @@ struct orbx_plan {
   CellGeom* d_cells = nullptr;
   int *d_xofs = nullptr, *d_yofs = nullptr;
   int16_t *d_xa = nullptr, *d_yb = nullptr;
-  int64_t* d_blur_off = nullptr;
   BlurTile* d_tiles = nullptr;
   int ntiles = 0;
-  int64_t blur_bytes = 0;
+  FastTile* d_ftiles = nullptr;
+  int nftiles = 0;
+  uint8_t* d_vmap = nullptr;
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
   uint32_t *d_cand = nullptr, *d_lin = nullptr, *d_okey = nullptr;
   int *d_cell_counts = nullptr, *d_label = nullptr, *d_ocount = nullptr, *d_counts = nullptr;
@@ -789,27 +938,38 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   const int L = g.nlevels;
   Profiler dummy;
   Profiler& pr = prof ? *prof : dummy;
-  const int st_resize = pr.stage("k_resize"), st_blur = pr.stage("k_blur"),
-            st_fast = pr.stage("k_fast_cells"), st_oct = pr.stage("k_octree"),
-            st_desc = pr.stage("k_describe");
+  const int st_copy = pr.stage("k_copy0"), st_resize = pr.stage("k_resize"),
+            st_blur = pr.stage("k_blur"), st_fs = pr.stage("k_fast_score"),
+            st_fast = pr.stage("k_fast_nms"),
+            st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe");
   pr.mark(P->stream, -1);
+  {
+    const LevelGeom& G = g.lv[0];
+    dim3 grid((G.w / 4 + 256) / 256, G.h, n);
+    hipLaunchKernelGGL(k_copy0, grid, dim3(256), 0, P->stream, d_in, P->d_pyr, g.pyr_bytes,
+                       P->d_lv);
+    pr.mark(P->stream, st_copy);
+  }
   for (int l = 1; l < L; l++) {
     const LevelGeom& D = g.lv[l];
-    dim3 grid((D.w * D.h + 255) / 256, n);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, P->stream, d_in, P->d_pyr, g.pyr_bytes,
-                       P->d_lv, l, P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
+    dim3 grid((D.w / 4 + 256) / 256, D.h, n);
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, P->stream, P->d_pyr, g.pyr_bytes, P->d_lv, l,
+                       P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
     pr.mark(P->stream, st_resize);
   }
   if (P->ntiles > 0) {
-    hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, d_in, P->d_pyr,
-                       g.pyr_bytes, P->d_blur, P->blur_bytes, P->d_blur_off, P->d_lv, P->d_tiles);
+    hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
+                       g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles);
     pr.mark(P->stream, st_blur);
   }
   const int ncells = (int)g.cells.size();
   if (ncells > 0) {
-    hipLaunchKernelGGL(k_fast_cells, dim3(ncells, n), dim3(256), 0, P->stream, d_in, P->d_pyr,
-                       g.pyr_bytes, P->d_lv, P->d_cells, ncells, g.ini_th, g.min_th, P->d_cand,
-                       g.cand_total, P->d_cell_counts);
+    hipLaunchKernelGGL(k_fast_score, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
+                       g.pyr_bytes, P->d_vmap, P->d_lv, P->d_ftiles, min(g.ini_th, g.min_th));
+    pr.mark(P->stream, st_fs);
+    hipLaunchKernelGGL(k_fast_nms, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
+                       P->d_vmap, g.pyr_bytes, P->d_lv, P->d_cells, ncells, g.ini_th, g.min_th,
+                       P->d_cand, g.cand_total, P->d_cell_counts);
     pr.mark(P->stream, st_fast);
   }
   hipLaunchKernelGGL(k_octree, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream, P->d_lv,
@@ -817,9 +977,9 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                      P->d_label, P->d_okey, P->d_ocount, g.kp_total, L, g.node_cap_max,
                      P->cell_cap);
   pr.mark(P->stream, st_oct);
-  hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 3) / 4, n), dim3(256), 0, P->stream, d_in,
-                     P->d_pyr, g.pyr_bytes, P->d_blur, P->blur_bytes, P->d_blur_off, P->d_lv, L,
-                     P->d_okey, P->d_ocount, g.kp_total, P->d_kps, P->d_desc, P->d_counts);
+  hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 3) / 4, n), dim3(256), 0, P->stream,
+                     P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, P->d_okey, P->d_ocount,
+                     g.kp_total, P->d_kps, P->d_desc, P->d_counts);
   pr.mark(P->stream, st_desc);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return report_hip(e, "extract launch");
@@ -856,26 +1016,44 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     return fail(ORBX_EDEVICE);
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)));
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), g.umax, sizeof(g.umax)));
-  // blur layout: every level, dense
-  std::vector<int64_t> boff(g.nlevels);
-  int64_t bb = 0;
+  // blur tiles over every level (the blurred pyramid has the pyramid's pitched layout)
   std::vector<BlurTile> tiles;
   for (int l = 0; l < g.nlevels; l++) {
-    boff[l] = bb;
-    bb += ((int64_t)g.lv[l].w * g.lv[l].h + 255) / 256 * 256;
-    for (int ty = 0; ty * kBlurTH < g.lv[l].h; ty++)
-      for (int tx = 0; tx * kBlurTW < g.lv[l].w; tx++)
-        tiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, 0});
+    const LevelGeom& G = g.lv[l];
+    for (int ty = 0; ty * kBlurTH < G.h; ty++)
+      for (int tx = 0; tx * kBlurTW < G.w; tx++) {
+        const int X0 = tx * kBlurTW, Y0 = ty * kBlurTH;
+        const bool interior = X0 >= 4 && X0 + kBlurTW + 4 <= G.w && Y0 >= 3 &&
+                              Y0 + kBlurTH + 3 <= G.h;
+        tiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, (int16_t)interior});
+      }
   }
-  P->blur_bytes = bb;
+  for (const CellGeom& c : g.cells)
+    if (c.x1 - c.x0 > kCellMax || c.y1 - c.y0 > kCellMax) return fail(ORBX_EUNSUPPORTED);
   P->ntiles = (int)tiles.size();
+  // FAST score tiles: those intersecting the detection region [19, w-19) x [19, h-19)
+  std::vector<FastTile> ftiles;
+  for (int l = 0; l < g.nlevels; l++) {
+    const LevelGeom& G = g.lv[l];
+    if (!G.ncells) continue;
+    for (int ty = 0; ty * kFastTH < G.h; ty++)
+      for (int tx = 0; tx * kFastTW < G.w; tx++) {
+        const int X0 = tx * kFastTW, Y0 = ty * kFastTH;
+        if (X0 + kFastTW <= kEdge || X0 >= G.w - kEdge || Y0 + kFastTH <= kEdge ||
+            Y0 >= G.h - kEdge)
+          continue;
+        ftiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, 0});
+      }
+  }
+  P->nftiles = (int)ftiles.size();
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
   const size_t B = (size_t)max_batch;
   if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, g.cells.size()) ||
       dalloc(&P->d_xofs, g.xofs.size()) || dalloc(&P->d_yofs, g.yofs.size()) ||
       dalloc(&P->d_xa, g.xa.size()) || dalloc(&P->d_yb, g.yb.size()) ||
-      dalloc(&P->d_blur_off, g.nlevels) || dalloc(&P->d_tiles, tiles.size()) ||
-      dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * bb) ||
+      dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_ftiles, ftiles.size()) ||
+      dalloc(&P->d_vmap, B * g.pyr_bytes) ||
+      dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
       dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels) ||
@@ -890,8 +1068,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       up(P->d_xofs, g.xofs.data(), 4 * g.xofs.size()) ||
       up(P->d_yofs, g.yofs.data(), 4 * g.yofs.size()) ||
       up(P->d_xa, g.xa.data(), 2 * g.xa.size()) || up(P->d_yb, g.yb.data(), 2 * g.yb.size()) ||
-      up(P->d_blur_off, boff.data(), 8 * boff.size()) ||
-      up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()))
+      up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
+      up(P->d_ftiles, ftiles.data(), sizeof(FastTile) * ftiles.size()))
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   const size_t NC = (size_t)g.node_cap_max;
@@ -910,7 +1088,7 @@ int orbx_plan_destroy(orbx_plan* P) {
   if (!P) return ORBX_OK;
   if (P->graph) hipGraphExecDestroy(P->graph);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xofs,   P->d_yofs,  P->d_xa,
-                  P->d_yb,  P->d_blur_off, P->d_tiles, P->d_pyr,  P->d_blur,
+                  P->d_yb,  P->d_tiles, P->d_ftiles, P->d_vmap, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label,
                   P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
   for (void* p : ptrs)
@@ -1005,9 +1183,9 @@ int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int
   if (!P || !P->last_in || img < 0 || img >= P->last_n || level < 0 || level >= P->g.nlevels)
     return ORBX_EINVAL;
   const LevelGeom& G = P->g.lv[level];
-  const uint8_t* src = level == 0 ? P->last_in + (int64_t)img * G.w * G.h
-                                  : P->d_pyr + (int64_t)img * P->g.pyr_bytes + G.pyr_off;
-  ORBX_HIP(hipMemcpy2DAsync(out, stride, src, G.w, G.w, G.h, hipMemcpyDeviceToHost, P->stream));
+  const uint8_t* src = P->d_pyr + (int64_t)img * P->g.pyr_bytes + G.pyr_off;
+  ORBX_HIP(hipMemcpy2DAsync(out, stride, src, G.pitch, G.w, G.h, hipMemcpyDeviceToHost,
+                            P->stream));
   ORBX_HIP(hipStreamSynchronize(P->stream));
   return ORBX_OK;
 }

@@ -132,9 +132,11 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
         return ORBX_EUNSUPPORTED;
       }
       resize_tables(P.w, P.h, L.w, L.h, g, &L);
-      L.pyr_off = pyr;
-      pyr += ((int64_t)L.w * L.h + 255) / 256 * 256;
     }
+    // every level (level 0 is copied in) lives in the pitched pyramid block
+    L.pitch = (L.w + 63) & ~63;
+    L.pyr_off = pyr;
+    pyr += ((int64_t)L.pitch * L.h + 255) / 256 * 256;
     L.bxs = (L.w / 4) * 4;
     L.scale = g->scale[l];
     L.size = (float)(int)(kPatch * g->scale[l]);

@@ -23,7 +23,8 @@ constexpr int kMaxIni = 64;     // initial octree columns supported (nIni)
 // 735-757, 1047-1072).
 struct LevelGeom {
   int w, h;            // level size (cvRound((float)cols * invScale))
-  int64_t pyr_off;     // offset of the level inside one image's pyramid block
+  int pitch;           // row pitch in the pyramid / blur blocks (w rounded up to 64 B)
+  int64_t pyr_off;     // offset of the level inside one image's pyramid (and blur) block
   int coef_x, coef_y;  // offsets into the resize coefficient tables (levels >= 1)
   int xmax;            // HResizeLinear clamp start (dx >= xmax reads S[x0]*2048)
   int vxs;             // VResizeLinearVec_32s8u SSE2 region: x < vxs
