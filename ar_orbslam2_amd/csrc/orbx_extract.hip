@@ -5,8 +5,8 @@
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
 //   k_resize      x (nlevels-1)  pyramid level l from level l-1     (cv::resize INTER_LINEAR)
 //   k_blur        x 1            all levels, 64x16 LDS tiles         (GaussianBlur 7x7 s=2)
-//   k_fast_score  x 1            64x16 tiles, all levels            (FAST score map)
-//   k_fast_nms    x 1            one wave per FAST cell             (cv::FAST NMS + cell fallback)
+//   k_fast_tile   x 1            64x64 tiles, all levels            (FAST score + cell-local NMS)
+//   k_fast_compact x 1           one wave per FAST cell             (fallback + ordered compaction)
 //   k_octree      x 1            one workgroup per (image, level)    (DistributeOctTree)
 //   k_describe    x 1            one wave per keypoint               (IC_Angle + rBRIEF)
 // Level 0 is read in place from the caller's input buffer; levels >= 1 live in the pyramid
@@ -101,6 +101,45 @@ __device__ int block_scan_excl(int* a, int M, int* s_tmp) {
   return total;
 }
 
+// 64-bit exclusive scan in place (packed counters; one scan instead of several).
+template <int NT>
+__device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
+  const int per = (M + NT - 1) / NT;
+  const int t = threadIdx.x;
+  const int beg = min(t * per, M), end = min(beg + per, M);
+  uint64_t sum = 0;
+  for (int i = beg; i < end; i++) sum += a[i];
+  const int lane = t & 63, wid = t >> 6;
+  uint64_t v = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t n = __shfl_up(v, off);
+    if (lane >= off) v += n;
+  }
+  __syncthreads();
+  if (lane == 63) s_tmp[wid] = v;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t acc = 0;
+    for (int w = 0; w < NT / 64; w++) {
+      const uint64_t x = s_tmp[w];
+      s_tmp[w] = acc;
+      acc += x;
+    }
+    s_tmp[NT / 64] = acc;
+  }
+  __syncthreads();
+  uint64_t run = s_tmp[wid] + v - sum;
+  for (int i = beg; i < end; i++) {
+    const uint64_t x = a[i];
+    a[i] = run;
+    run += x;
+  }
+  const uint64_t total = s_tmp[NT / 64];
+  __syncthreads();
+  return total;
+}
+
 // ------------------------------------------------------------------ k_copy0
 // Level 0 = the input image (ComputePyramid level 0, ORBextractor.cc:1066-1068) copied into the
 // 64-B pitched pyramid block so every later kernel reads aligned dwords.
@@ -159,9 +198,12 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, int64
                                                 const int16_t* __restrict__ yb) {
   const LevelGeom& D = lv[level];
   const LevelGeom& S = lv[level - 1];
-  const int img = blockIdx.z, dy = blockIdx.y;
-  const int dx0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (dx0 >= D.w) return;
+  const int img = blockIdx.y;
+  const int q4 = (D.w + 3) >> 2;  // dword groups per row; one thread per group, rows flattened
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= q4 * D.h) return;
+  const int dy = idx / q4;
+  const int dx0 = (idx - dy * q4) * 4;
   const uint8_t* src = level_base(pyr, pyr_bytes, S, img);
   uint8_t* dst = pyr + (int64_t)img * pyr_bytes + D.pyr_off;
   const int sy0 = yofs[D.coef_y + dy];
@@ -270,7 +312,7 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
   }
 }
 
-// ------------------------------------------------------------------ k_fast_cells
+// ------------------------------------------------------------------ FAST
 // One workgroup per FAST cell of ComputeKeyPointsOctTree (ORBextractor.cc:758-796): cv::FAST
 // with NMS on the cell ROI at iniThFAST, again at minThFAST when no keypoint survives, then an
 // order-preserving (raster) compaction into the cell's candidate slot.  Score = OpenCV 2.4
@@ -335,175 +377,200 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* V, int vs, int p, int t)
   return true;
 }
 
-// Necessary condition for "corner at t" (9 contiguous darker/brighter): two consecutive
-// quarter points of the circle (0,4,8,12) both darker or both brighter.
+// Necessary condition for "corner at t" (9 contiguous darker or brighter circle points): any
+// 9-arc contains 4 cyclically consecutive even positions (0,2,...,14) of the circle, which must
+// then all be darker / all brighter.  Rejects ~4x more pixels than the quarter-point test.
 __device__ __forceinline__ bool fast_maybe(const uint8_t* s, int stride, int x, int y, int t) {
   const uint8_t* c = s + y * stride + x;
   const int v = c[0];
-  const int p0 = c[3 * stride], p4 = c[3], p8 = c[-3 * stride], p12 = c[-3];
+  const int e[8] = {c[3 * stride], c[2 * stride + 2], c[3], c[-2 * stride + 2],
+                    c[-3 * stride], c[-2 * stride - 2], c[-3], c[2 * stride - 2]};
   const int lo = v - t, hi = v + t;
-  const bool d0 = p0 < lo, d4 = p4 < lo, d8 = p8 < lo, d12 = p12 < lo;
-  const bool b0 = p0 > hi, b4 = p4 > hi, b8 = p8 > hi, b12 = p12 > hi;
-  return ((d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0)) |
-         ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0));
+  uint32_t dm = 0, bm = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    dm |= (uint32_t)(e[k] < lo) << k;
+    bm |= (uint32_t)(e[k] > hi) << k;
+  }
+  dm |= dm << 8;
+  bm |= bm << 8;
+  const uint32_t rd = dm & (dm >> 1) & (dm >> 2) & (dm >> 3);
+  const uint32_t rb = bm & (bm >> 1) & (bm >> 2) & (bm >> 3);
+  return ((rd | rb) & 0xFF) != 0;
 }
 
-// ---- k_fast_score: FAST score map V = clamp(cornerScore+1, 0, 255) of every pixel of the
-// detection region [19, w-19) x [19, h-19) of every level (0 elsewhere).  A pixel that fails the
-// quarter-point test at min(iniThFAST, minThFAST) cannot be a corner at either threshold, so
-// its V (<= threshold) is equivalent to 0 in every NMS; only candidates get the full score.
-// Tile 64 x 64: aligned-dword staging of the (64+6) x 72 window, then per wave 16 rows, a
-// wave-local queue of candidates (ballot + mbcnt, no block barrier) scored 64 at a time.
-constexpr int kFastTW = 64, kFastTH = 64;
+// ---- k_fast_tile: FAST for 64 x 64 output pixels of one level per workgroup.
+//  (1) score map V = clamp(cornerScore+1, 0, 255) on the tile plus a 1-px ring, for pixels
+//      of the detection region [19, w-19) x [19, h-19) (0 elsewhere).  A pixel failing the
+//      quarter-point test at min(iniThFAST, minThFAST) cannot be a corner at either threshold,
+//      so its V (<= threshold) is equivalent to 0 in every NMS: only candidates are scored,
+//      from wave-local queues (ballot + mbcnt).
+//  (2) cv::FAST's strict 8-neighbour NMS at both thresholds, with neighbours outside the
+//      pixel's own FAST cell (or outside the detection region) counting as 0 — the cell-local
+//      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  One ballot per
+//      row gives the 64-bit keep word of that row for each threshold.
+constexpr int kFastT = 64;
 struct FastTile {
   int16_t level, tx, ty, pad;
 };
 
-__global__ __launch_bounds__(256) void k_fast_score(const uint8_t* __restrict__ pyr,
-                                                    int64_t pyr_bytes,
-                                                    uint8_t* __restrict__ vmap,
-                                                    const LevelGeom* __restrict__ lv,
-                                                    const FastTile* __restrict__ tiles, int t_lo) {
-  constexpr int kW = (kFastTW + 8) / 4;  // dwords per staged row: X0-4 .. X0+67
-  __shared__ __align__(16) uint32_t s_in[kFastTH + 6][kW];
-  __shared__ __align__(16) uint8_t s_v[kFastTH][kFastTW];
-  __shared__ uint16_t s_q[4][(kFastTH / 4) * 64];
+__global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ pyr,
+                                                   int64_t pyr_bytes, uint8_t* __restrict__ vmap,
+                                                   uint64_t* __restrict__ bitmaps,
+                                                   int64_t bm_words,
+                                                   const LevelGeom* __restrict__ lv,
+                                                   const FastTile* __restrict__ tiles, int ini_th,
+                                                   int min_th) {
+  constexpr int kIn = kFastT + 8;   // staged window: X0-4 .. X0+67, Y0-4 .. Y0+67
+  constexpr int kWin = kFastT + 2;  // V window: X0-1 .. X0+64, Y0-1 .. Y0+64
+  constexpr int kVS = kWin + 2;     // V row stride
+  constexpr int kQ = (kWin * kWin + 255) / 256 * 64;
+  __shared__ __align__(16) uint32_t s_in[kIn][kIn / 4];
+  __shared__ __align__(4) uint8_t s_v[kWin * kVS];
+  __shared__ uint16_t s_q[4][kQ];
   const FastTile T = tiles[blockIdx.x];
   const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const LevelGeom& G = lv[T.level];
   const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
-  const int X0 = T.tx * kFastTW, Y0 = T.ty * kFastTH;
-  for (int i = tid; i < (kFastTH + 6) * kW; i += 256) {
-    const int r = i / kW, c = i - r * kW;
-    const int y = min(max(Y0 + r - 3, 0), G.h - 1);
+  const int X0 = T.tx * kFastT, Y0 = T.ty * kFastT;
+  for (int i = tid; i < kIn * (kIn / 4); i += 256) {
+    const int r = i / (kIn / 4), c = i - r * (kIn / 4);
+    const int y = min(max(Y0 + r - 4, 0), G.h - 1);
     const int x = X0 - 4 + 4 * c;
     s_in[r][c] = (x >= 0 && x + 4 <= G.pitch) ? *(const uint32_t*)(src + (int64_t)y * G.pitch + x)
                                               : 0u;
   }
   __syncthreads();
   const uint8_t* sb = (const uint8_t*)s_in;
-  constexpr int SB = kW * 4;  // staged row stride in bytes
-  const int x = X0 + lane;
-  const bool xin = x >= kEdge && x < G.w - kEdge;
+  const int t_lo = min(ini_th, min_th);
+  const int ylo = kEdge, yhi = G.h - kEdge, xlo = kEdge, xhi = G.w - kEdge;
   uint16_t* q = s_q[wid];
   int nq = 0;
-#pragma unroll 4
-  for (int rr = 0; rr < kFastTH / 4; rr++) {
-    const int r = wid * (kFastTH / 4) + rr, y = Y0 + r;
-    s_v[r][lane] = 0;
-    const bool f = xin && y >= kEdge && y < G.h - kEdge &&
-                   fast_maybe(sb, SB, lane + 4, r + 3, t_lo);
+  for (int i0 = wid * 64; i0 < kWin * kWin; i0 += 256) {
+    const int i = i0 + lane;
+    const int vy = i / kWin, vx = i - vy * kWin;
+    const int y = Y0 - 1 + vy, x = X0 - 1 + vx;
+    bool f = false;
+    if (i < kWin * kWin) {
+      s_v[vy * kVS + vx] = 0;
+      f = y >= ylo && y < yhi && x >= xlo && x < xhi && fast_maybe(sb, kIn, vx + 3, vy + 3, t_lo);
+    }
     const uint64_t m = __ballot(f);
     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    if (f) q[nq + rank] = (uint16_t)((r << 6) | lane);
+    if (f) q[nq + rank] = (uint16_t)i;
     nq += __popcll(m);
   }
-  for (int i0 = 0; i0 < nq; i0 += 64) {
-    const int i = i0 + lane;
-    if (i < nq) {
-      const int e = q[i], r = e >> 6, c = e & 63;
-      const int sc = fast_score(sb, SB, c + 4, r + 3);
-      s_v[r][c] = (uint8_t)min(255, max(0, sc + 1));
+  for (int j0 = 0; j0 < nq; j0 += 64) {
+    const int j = j0 + lane;
+    if (j < nq) {
+      const int i = q[j], vy = i / kWin, vx = i - vy * kWin;
+      const int sc = fast_score(sb, kIn, vx + 3, vy + 3);
+      s_v[vy * kVS + vx] = (uint8_t)min(255, max(0, sc + 1));
     }
   }
   __syncthreads();
-  for (int i = tid; i < kFastTH * (kFastTW / 4); i += 256) {
-    const int r = i >> 4, c4 = (i & 15) * 4;  // kFastTH rows x 16 dwords
-    const int y = Y0 + r;
-    if (y < G.h && X0 + c4 < G.pitch)
-      *(uint32_t*)(vmap + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch + X0 + c4) =
-          *(const uint32_t*)&s_v[r][c4];
+  // NMS, wave w: rows 16w .. 16w+15 of the tile, lane = column.  The cell masks split into a
+  // per-lane column part (computed once) and a row part that is uniform across the wave.
+  const int x = X0 + lane;
+  const float rw = 1.0f / (float)max(G.wcell, 1), rh = 1.0f / (float)max(G.hcell, 1);
+  const int jx = (int)(((float)(x - kEdge) + 0.5f) * rw);
+  const int rx = x - kEdge - jx * G.wcell;
+  const bool xin = x >= xlo && x < xhi;
+  const int mL = rx != 0 ? 0xFF : 0, mR = (rx != G.wcell - 1 && x + 1 < xhi) ? 0xFF : 0;
+  uint64_t* bm_ini = bitmaps + (int64_t)img * bm_words + G.bm_off;
+  uint64_t* bm_min = bm_ini + (int64_t)G.bm_wpr * G.h;
+  uint8_t* vout = vmap + (int64_t)img * pyr_bytes + G.pyr_off;
+#pragma unroll 2
+  for (int rr = 0; rr < kFastT / 4; rr++) {
+    const int r = wid * (kFastT / 4) + rr, y = Y0 + r;
+    if (y >= G.h) break;  // wave-uniform
+    const int iy = (int)(((float)(y - kEdge) + 0.5f) * rh);
+    const int ry = y - kEdge - iy * G.hcell;
+    const bool yin = y >= ylo && y < yhi;
+    const int mU = ry != 0 ? 0xFF : 0, mD = (ry != G.hcell - 1 && y + 1 < yhi) ? 0xFF : 0;
+    const int vc = (r + 1) * kVS + lane + 1;
+    const int v = s_v[vc];
+    const int n0 = s_v[vc - kVS - 1] & mU & mL, n1 = s_v[vc - kVS] & mU,
+              n2 = s_v[vc - kVS + 1] & mU & mR, n3 = s_v[vc - 1] & mL, n4 = s_v[vc + 1] & mR,
+              n5 = s_v[vc + kVS - 1] & mD & mL, n6 = s_v[vc + kVS] & mD,
+              n7 = s_v[vc + kVS + 1] & mD & mR;
+    const int nmax = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+    // a neighbour counts with its score V-1 only if it is a corner at t (V > t), and that count
+    // is monotone in V, so the largest masked neighbour decides: keep iff V > t and
+    // V-1 > (nmax > t ? nmax-1 : 0)
+    const bool cand = xin && yin;
+    const bool ki = cand && v > ini_th && v - 1 > (nmax > ini_th ? nmax - 1 : 0);
+    const bool km = cand && v > min_th && v - 1 > (nmax > min_th ? nmax - 1 : 0);
+    const uint64_t wi = __ballot(ki), wm = __ballot(km);
+    if (lane == 0) {
+      bm_ini[(int64_t)y * G.bm_wpr + T.tx] = wi;
+      bm_min[(int64_t)y * G.bm_wpr + T.tx] = wm;
+    }
+    vout[(int64_t)y * G.pitch + x] = (uint8_t)v;
   }
 }
 
-// ---- k_fast_nms: cv::FAST's strict 8-neighbour NMS restricted to each cell's detection
-// region (neighbours outside it count as 0), survivors at iniThFAST, else at minThFAST
-// (ORBextractor.cc:776-784), raster-ordered compaction into the cell's candidate slot.
-// One wave per cell; the cell's V window (<= 62 x 62) is staged in LDS with the ring zeroed.
-__global__ __launch_bounds__(256) void k_fast_nms(const uint8_t* __restrict__ vmap,
-                                                  int64_t pyr_bytes,
-                                                  const LevelGeom* __restrict__ lv,
-                                                  const CellGeom* __restrict__ cells, int ncells,
-                                                  int ini_th, int min_th,
-                                                  uint32_t* __restrict__ cand, int cand_total,
-                                                  int* __restrict__ cell_counts) {
-  constexpr int VS = kCellMax - 2;  // 64 >= dc + 2
-  __shared__ uint8_t s_w[4][(kCellMax - 4) * VS];
+// ---- k_fast_compact: per FAST cell (one wave, lane = detection row): survivors at
+// iniThFAST, else at minThFAST (ORBextractor.cc:780-784), raster order (row prefix sum, then
+// ascending x) into the cell's candidate slot, keys relative to minBorder = 16.
+__global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict__ vmap,
+                                                      int64_t pyr_bytes,
+                                                      const uint64_t* __restrict__ bitmaps,
+                                                      int64_t bm_words,
+                                                      const LevelGeom* __restrict__ lv,
+                                                      const CellGeom* __restrict__ cells,
+                                                      int ncells, uint32_t* __restrict__ cand,
+                                                      int cand_total,
+                                                      int* __restrict__ cell_counts) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int ci = blockIdx.x * 4 + wid, img = blockIdx.y;
   if (ci >= ncells) return;
   const CellGeom C = cells[ci];
   const LevelGeom& G = lv[C.level];
-  const int dr = C.y1 - C.y0 - 6, dc = C.x1 - C.x0 - 6;
+  const int dr = C.y1 - C.y0 - 6, cx0 = C.x0 + 3, cx1 = C.x1 - 3;
   int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
-  if (dr <= 0 || dc <= 0) {
+  if (dr <= 0 || cx1 <= cx0) {
     if (lane == 0) *cnt_out = 0;
     return;
   }
-  uint8_t* W = s_w[wid];
-  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + G.pyr_off +
-                     (int64_t)(C.y0 + 3) * G.pitch + C.x0 + 3;
-  // W[(r+1)*VS + c+1] = V at detection pixel (r, c); the ring is 0 (cell-local NMS)
-  for (int i = lane; i < (dr + 2) * VS; i += 64) W[i] = 0;
-  const int npix = dr * dc;
-  const float rdc = 1.0f / (float)dc;  // (p + 0.5) / dc is never within 1/120 of an integer
-  constexpr int U = 8;
-  for (int b = 0; b < npix; b += 64 * U) {
-    uint8_t v[U];
-    int wi[U];
+  const uint64_t* bm = bitmaps + (int64_t)img * bm_words + G.bm_off;
+  const int y = C.y0 + 3 + lane;
+  const int wa = cx0 >> 6, sh = cx0 & 63, width = cx1 - cx0;  // width <= 60
+  const uint64_t wmask = width >= 64 ? ~0ull : ((1ull << width) - 1);
+  auto row_bits = [&](const uint64_t* plane) -> uint64_t {
+    if (lane >= dr) return 0;
+    const uint64_t* row = plane + (int64_t)y * G.bm_wpr + wa;
+    uint64_t b = row[0] >> sh;
+    if (sh && sh + width > 64) b |= row[1] << (64 - sh);
+    return b & wmask;
+  };
+  uint64_t bits = row_bits(bm);
+  int cnt = __popcll(bits);
+  int total = cnt;
 #pragma unroll
-    for (int k = 0; k < U; k++) {  // issue every load of the batch before any LDS store
-      const int p = b + k * 64 + lane;
-      wi[k] = -1;
-      v[k] = 0;
-      if (p < npix) {
-        const int r = (int)(((float)p + 0.5f) * rdc), c = p - r * dc;
-        wi[k] = (r + 1) * VS + c + 1;
-        v[k] = V[(int64_t)r * G.pitch + c];
-      }
-    }
+  for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o);
+  if (total == 0) {
+    bits = row_bits(bm + (int64_t)G.bm_wpr * G.h);
+    cnt = __popcll(bits);
+  }
+  int incl = cnt;
 #pragma unroll
-    for (int k = 0; k < U; k++)
-      if (wi[k] >= 0) W[wi[k]] = v[k];
+  for (int o = 1; o < 64; o <<= 1) {
+    const int n = __shfl_up(incl, o);
+    if (lane >= o) incl += n;
   }
-  // survivors at iniThFAST, in raster order = flattened order; keep bits per iteration
-  const int iters = (npix + 63) >> 6;  // <= 57
-  uint64_t kb = 0;
-  int total = 0;
-  for (int it = 0; it < iters; it++) {
-    const int p = it * 64 + lane;
-    bool k = false;
-    if (p < npix) {
-      const int r = (int)(((float)p + 0.5f) * rdc), c = p - r * dc;
-      k = nms_keep(W, VS, (r + 1) * VS + c + 1, ini_th);
-    }
-    kb |= (uint64_t)k << it;
-    total += __popcll(__ballot(k));
-  }
-  const int t = ini_th;
+  int pos = incl - cnt;
+  const int nout = __shfl(incl, 63);
   uint32_t* out = cand + (int64_t)img * cand_total + C.slot_off;
-  int nout = 0;
-  const bool redo = total == 0 && min_th != ini_th;  // ORBextractor.cc:780-784
-  for (int it = 0; it < iters; it++) {
-    const int p = it * 64 + lane;
-    int r = 0, c = 0;
-    bool k = (kb >> it) & 1;
-    if (p < npix) {
-      r = (int)(((float)p + 0.5f) * rdc);
-      c = p - r * dc;
-      if (redo) k = nms_keep(W, VS, (r + 1) * VS + c + 1, min_th);
-    }
-    const uint64_t m = __ballot(k);
-    if (k) {
-      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-      const uint32_t x = (uint32_t)(c + 3 + C.offx), y = (uint32_t)(r + 3 + C.offy);
-      out[nout + rank] = x | (y << 12) | ((uint32_t)(W[(r + 1) * VS + c + 1] - 1) << 24);
-    }
-    nout += __popcll(m);
+  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch;
+  while (bits) {
+    const int k = __builtin_ctzll(bits);
+    bits &= bits - 1;
+    const int xx = cx0 + k;
+    out[pos++] = (uint32_t)(xx - (kEdge - 3)) | ((uint32_t)(y - (kEdge - 3)) << 12) |
+                 ((uint32_t)(V[xx] - 1) << 24);
   }
-  (void)t;
   if (lane == 0) *cnt_out = nout;
 }
 
@@ -529,65 +596,24 @@ __device__ __forceinline__ int quad_of(uint32_t key, int x0, int x1, int y0, int
   return x < xm ? (y < ym ? 0 : 2) : (y < ym ? 1 : 3);
 }
 
-__global__ __launch_bounds__(kOctNT) void k_octree(
-    const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
-    const CellGeom* __restrict__ cells, const uint32_t* __restrict__ cand, int cand_total,
-    uint32_t* __restrict__ lin, int* __restrict__ label, uint32_t* __restrict__ okey,
-    int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ int s_tmp[kOctNT / 64 + 1];
-  __shared__ int s_misc[8];
-  const int level = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
-  const LevelGeom& G = lv[level];
-  int* oc = ocount + img * nlevels + level;
-  if (G.ncells == 0) {
-    if (tid == 0) *oc = 0;
-    return;
-  }
-  const int NC = node_cap;
-  // LDS carve
-  unsigned char* p = smem;
-  auto take = [&](size_t bytes) {
-    unsigned char* r = p;
-    p += (bytes + 15) & ~size_t(15);
-    return r;
-  };
+struct OctCtx {
   OctNodes A, B;
-  A.x0 = (int16_t*)take(2 * NC); A.x1 = (int16_t*)take(2 * NC);
-  A.y0 = (int16_t*)take(2 * NC); A.y1 = (int16_t*)take(2 * NC);
-  A.cnt = (int*)take(4 * NC); A.seq = (int*)take(4 * NC);
-  B.x0 = (int16_t*)take(2 * NC); B.x1 = (int16_t*)take(2 * NC);
-  B.y0 = (int16_t*)take(2 * NC); B.y1 = (int16_t*)take(2 * NC);
-  B.cnt = (int*)take(4 * NC); B.seq = (int*)take(4 * NC);
-  int* cc = (int*)take(16 * NC);
-  int* t1 = (int*)take(4 * NC);
-  int* t2 = (int*)take(4 * NC);
-  int* t3 = (int*)take(4 * NC);
-  int* t4 = (int*)take(4 * NC);
-  int* cpre = (int*)take(4 * (cell_cap + 1));
+  int *cc, *t1, *t2, *t3, *t4, *s_tmp, *s_misc;
+  uint64_t *pk, *s_tmp64;
+  uint32_t* outk;
+  int* oc;
+};
 
-  // 1. gather candidates of this level in cell order (vToDistributeKeys)
-  const int* cntv = cell_counts + (int64_t)img * ncells + G.cell_begin;
-  for (int i = tid; i < G.ncells; i += kOctNT) cpre[i] = cntv[i];
-  __syncthreads();
-  const int n = block_scan_excl<kOctNT>(cpre, G.ncells, s_tmp);
-  const uint32_t* cb = cand + (int64_t)img * cand_total;
-  uint32_t* keys = lin + (int64_t)img * cand_total + G.cand_off;
-  int* lab = label + (int64_t)img * cand_total + G.cand_off;
-  {
-    const int wid = tid >> 6, lane = tid & 63;
-    for (int c = wid; c < G.ncells; c += kOctNT / 64) {
-      const CellGeom C = cells[G.cell_begin + c];
-      const int k = cntv[c], o = cpre[c];
-      for (int i = lane; i < k; i += 64) keys[o + i] = cb[C.slot_off + i];
-    }
-  }
-  __syncthreads();
-  uint32_t* outk = okey + (int64_t)img * kp_total + G.kp_off;
-  if (n == 0) {
-    if (tid == 0) *oc = 0;
-    return;
-  }
+// Octree passes on keys/labels that live either in LDS (fits) or in global scratch; inlined
+// per call site so each copy uses the address space it was given (ds_* vs global_*).
+__device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, uint32_t* keys,
+                                            int* lab, const int n) {
+  const int tid = threadIdx.x;
+  OctNodes A = X.A, B = X.B;
+  int *cc = X.cc, *t1 = X.t1, *t2 = X.t2, *t3 = X.t3, *t4 = X.t4, *s_tmp = X.s_tmp,
+      *s_misc = X.s_misc;
+  uint32_t* outk = X.outk;
+  int* oc = X.oc;
   // 2. initial nodes (ORBextractor.cc:530-567)
   const int nini = G.nini;
   for (int i = tid; i < nini; i += kOctNT) {
@@ -627,43 +653,74 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
     const int prevSize = size;
     for (int i = tid; i < 4 * size; i += kOctNT) cc[i] = 0;
     __syncthreads();
-    for (int k = tid; k < n; k += kOctNT) {
-      const int nd = lab[k];
-      if (cur.cnt[nd] > 1) {
-        const int q = quad_of(keys[k], cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
+    // quadrant counts; keys are in cell order, so a wave's keys usually share one node and the
+    // four counts are added with one atomic each instead of one per key
+    const int lane = tid & 63;
+    for (int k0 = 0; k0 < n; k0 += kOctNT) {
+      const int k = k0 + tid;
+      int nd = -1, q = -1;
+      if (k < n) {
+        nd = lab[k];
+        if (cur.cnt[nd] > 1) q = quad_of(keys[k], cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
+      }
+      const uint64_t act = __ballot(q >= 0);
+      if (!act) continue;
+      const int first = __builtin_ctzll(act);
+      const int ndf = __shfl(nd, first);
+      if (__ballot(q >= 0 && nd != ndf) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int c = __popcll(__ballot(q == j));
+          if (lane == first && c) atomicAdd(&cc[4 * ndf + j], c);
+        }
+      } else if (q >= 0) {
         atomicAdd(&cc[4 * nd + q], 1);
       }
     }
     __syncthreads();
-    // per-node stats: t1 = nonEmpty children (0 if not expandable), t2 = children with >1
-    int nexp_local = 0;
-    for (int i = tid; i < size; i += kOctNT) {
-      const bool e = cur.cnt[i] > 1;
-      int ne = 0, nx = 0;
-      if (e) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          ne += cc[4 * i + q] > 0;
-          nx += cc[4 * i + q] > 1;
-        }
-      }
-      t1[i] = ne;
-      t2[i] = e;  // divided flag (outer pass divides every expandable node)
-      nexp_local += nx;
-    }
-    const int nToExpand = block_sum<kOctNT>(nexp_local, s_tmp);
-    int T, newSize;
+    int T, newSize, nToExpand;
     if (!final_mode) {
-      // outer pass: process order = list order; t1 -> childPre
-      T = block_scan_excl<kOctNT>(t1, size, s_tmp);
-      for (int i = tid; i < size; i += kOctNT) t3[i] = !t2[i];
+      // outer pass (list order): one packed scan gives childPre (bits 0-19), the rank among
+      // undivided nodes (20-39) and the total of children with > 1 key (40-)
+      uint64_t* pk = X.pk;
+      for (int i = tid; i < size; i += kOctNT) {
+        const bool e = cur.cnt[i] > 1;
+        uint64_t ne = 0, nx = 0;
+        if (e) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            ne += cc[4 * i + q] > 0;
+            nx += cc[4 * i + q] > 1;
+          }
+        }
+        t2[i] = e;  // divided flag (the outer pass divides every expandable node)
+        pk[i] = ne | ((uint64_t)!e << 20) | (nx << 40);
+      }
       __syncthreads();
-      const int nd_total = block_scan_excl<kOctNT>(t3, size, s_tmp);
-      newSize = T + nd_total;
+      const uint64_t tot = block_scan_excl64<kOctNT>(pk, size, X.s_tmp64);
+      T = (int)(tot & 0xFFFFF);
+      newSize = T + (int)((tot >> 20) & 0xFFFFF);
+      nToExpand = (int)(tot >> 40);
       // base: divided -> T-1-childPre (child j at base-j); else newpos
-      for (int i = tid; i < size; i += kOctNT) t4[i] = t2[i] ? T - 1 - t1[i] : T + t3[i];
+      for (int i = tid; i < size; i += kOctNT) {
+        const uint64_t e = pk[i];
+        const int pre = (int)(e & 0xFFFFF), ndr = (int)((e >> 20) & 0xFFFFF);
+        t1[i] = pre;
+        t4[i] = t2[i] ? T - 1 - pre : T + ndr;
+      }
       __syncthreads();
     } else {
+      int nexp_local = 0;
+      for (int i = tid; i < size; i += kOctNT) {
+        const bool e = cur.cnt[i] > 1;
+        int ne = 0;
+        if (e) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) ne += cc[4 * i + q] > 0;
+        }
+        t1[i] = ne;
+      }
+      nToExpand = block_sum<kOctNT>(nexp_local, s_tmp);
       // final refinement: visit expandable nodes by (size desc, seq desc)
       int E_local = 0;
       for (int i = tid; i < size; i += kOctNT) {
@@ -796,6 +853,81 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
   if (tid == 0) *oc = size;
 }
 
+
+__global__ __launch_bounds__(kOctNT) void k_octree(
+    const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
+    const CellGeom* __restrict__ cells, const uint32_t* __restrict__ cand, int cand_total,
+    uint32_t* __restrict__ lin, int* __restrict__ label, uint32_t* __restrict__ okey,
+    int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
+    int key_cap) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ int s_tmp[kOctNT / 64 + 1];
+  __shared__ int s_misc[8];
+  const int level = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const LevelGeom& G = lv[level];
+  int* oc = ocount + img * nlevels + level;
+  if (G.ncells == 0) {
+    if (tid == 0) *oc = 0;
+    return;
+  }
+  const int NC = node_cap;
+  // LDS carve
+  unsigned char* p = smem;
+  auto take = [&](size_t bytes) {
+    unsigned char* r = p;
+    p += (bytes + 15) & ~size_t(15);
+    return r;
+  };
+  OctNodes A, B;
+  A.x0 = (int16_t*)take(2 * NC); A.x1 = (int16_t*)take(2 * NC);
+  A.y0 = (int16_t*)take(2 * NC); A.y1 = (int16_t*)take(2 * NC);
+  A.cnt = (int*)take(4 * NC); A.seq = (int*)take(4 * NC);
+  B.x0 = (int16_t*)take(2 * NC); B.x1 = (int16_t*)take(2 * NC);
+  B.y0 = (int16_t*)take(2 * NC); B.y1 = (int16_t*)take(2 * NC);
+  B.cnt = (int*)take(4 * NC); B.seq = (int*)take(4 * NC);
+  int* cc = (int*)take(16 * NC);
+  int* t1 = (int*)take(4 * NC);
+  int* t2 = (int*)take(4 * NC);
+  int* t3 = (int*)take(4 * NC);
+  int* t4 = (int*)take(4 * NC);
+  int* cpre = (int*)take(4 * (cell_cap + 1));
+  uint64_t* pk = (uint64_t*)take(8 * NC);
+  __shared__ uint64_t s_tmp64[kOctNT / 64 + 1];
+
+  // 1. gather candidates of this level in cell order (vToDistributeKeys)
+  const int* cntv = cell_counts + (int64_t)img * ncells + G.cell_begin;
+  for (int i = tid; i < G.ncells; i += kOctNT) cpre[i] = cntv[i];
+  __syncthreads();
+  const int n = block_scan_excl<kOctNT>(cpre, G.ncells, s_tmp);
+  const uint32_t* cb = cand + (int64_t)img * cand_total;
+  uint32_t* keys = lin + (int64_t)img * cand_total + G.cand_off;
+  int* lab = label + (int64_t)img * cand_total + G.cand_off;
+  {
+    const int wid = tid >> 6, lane = tid & 63;
+    for (int c = wid; c < G.ncells; c += kOctNT / 64) {
+      const CellGeom C = cells[G.cell_begin + c];
+      const int k = cntv[c], o = cpre[c];
+      for (int i = lane; i < k; i += 64) keys[o + i] = cb[C.slot_off + i];
+    }
+  }
+  __syncthreads();
+  uint32_t* outk = okey + (int64_t)img * kp_total + G.kp_off;
+  if (n == 0) {
+    if (tid == 0) *oc = 0;
+    return;
+  }
+  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, pk, s_tmp64, outk, oc};
+  if (n <= key_cap) {  // keys + labels fit in LDS: every octree pass stays on-chip
+    uint32_t* kl = (uint32_t*)take(4 * (size_t)key_cap);
+    int* ll = (int*)take(4 * (size_t)key_cap);
+    for (int k = tid; k < n; k += kOctNT) kl[k] = keys[k];
+    __syncthreads();
+    octree_core(G, X, kl, ll, n);
+  } else {
+    octree_core(G, X, keys, lab, n);
+  }
+}
+
 // ------------------------------------------------------------------ k_describe
 // One wave per retained keypoint: IC_Angle on the unblurred level (ORBextractor.cc:73-98),
 // cv::fastAtan2, glibc sincosf, rBRIEF on the blurred level with the reference binary's
@@ -826,20 +958,52 @@ __global__ __launch_bounds__(256) void k_describe(
   const uint32_t key = okey[(int64_t)img * kp_total + slot];
   const int cx = (int)(key & 0xFFF) + (kEdge - 3), cy = (int)((key >> 12) & 0xFFF) + (kEdge - 3);
   const float response = (float)(key >> 24);
-  // IC_Angle: lanes 0..30 rows v = 0..7, lanes 32..62 rows v = 8..15; u = (lane & 31) - 15
+  // Stage both patches with aligned dword loads issued together: the raw 31 x 31 patch
+  // (IC_Angle, radius 15) and the blurred 37 x 37 patch (rBRIEF samples, radius <= 18).  The
+  // sample positions depend on the angle, so fetching the whole blurred patch up front hides
+  // that gather behind the first one.
+  constexpr int RW = 10, BW = 11;  // dwords per staged row (31+3 / 37+3 bytes, rounded up)
+  __shared__ uint32_t s_raw[4][31 * RW];
+  __shared__ uint32_t s_blr[4][37 * BW];
+  const int wv = threadIdx.x >> 6;
   const uint8_t* L = level_base(pyr, pyr_bytes, G, img);
-  const uint8_t* center = L + (int64_t)cy * G.pitch + cx;
+  const uint8_t* B = blur + (int64_t)img * pyr_bytes + G.pyr_off;
+  const int fr = (cx - 15) >> 2, lr = (cx + 15) >> 2;  // raw dword columns
+  const int fb = (cx - 18) >> 2, lb = (cx + 18) >> 2;  // blurred dword columns
+  uint32_t vr[5], vb[7];
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const int i = lane + 64 * k, r = i / RW, c = i - r * RW;
+    vr[k] = (i < 31 * RW && fr + c <= lr)
+                ? *(const uint32_t*)(L + (int64_t)(cy - 15 + r) * G.pitch + 4 * (fr + c)) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    const int i = lane + 64 * k, r = i / BW, c = i - r * BW;
+    vb[k] = (i < 37 * BW && fb + c <= lb)
+                ? *(const uint32_t*)(B + (int64_t)(cy - 18 + r) * G.pitch + 4 * (fb + c)) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 5; k++)
+    if (lane + 64 * k < 31 * RW) s_raw[wv][lane + 64 * k] = vr[k];
+#pragma unroll
+  for (int k = 0; k < 7; k++)
+    if (lane + 64 * k < 37 * BW) s_blr[wv][lane + 64 * k] = vb[k];
+  const uint8_t* raw = (const uint8_t*)s_raw[wv] + 15 * (4 * RW) + (cx - 4 * fr);  // center
+  const uint8_t* bc = (const uint8_t*)s_blr[wv] + 18 * (4 * BW) + (cx - 4 * fb);
+  constexpr int RS = 4 * RW, BS = 4 * BW;
+  // IC_Angle (ORBextractor.cc:73-98): lanes 0..30 rows v = 0..7, lanes 32..62 rows v = 8..15
   int m10 = 0, m01 = 0;
   const int u = (lane & 31) - 15;
   if ((lane & 31) < 31) {
-    const int vb = lane < 32 ? 0 : 8, ve = lane < 32 ? 8 : 16;
-    for (int v = vb; v < ve; v++) {
+    const int vb0 = lane < 32 ? 0 : 8, ve = lane < 32 ? 8 : 16;
+    for (int v = vb0; v < ve; v++) {
       const int d = c_umax[v];
       if (u < -d || u > d) continue;
       if (v == 0) {
-        m10 += u * center[u];
+        m10 += u * raw[u];
       } else {
-        const int vp = center[u + v * G.pitch], vm = center[u - v * G.pitch];
+        const int vp = raw[u + v * RS], vm = raw[u - v * RS];
         m10 += u * (vp + vm);
         m01 += v * (vp - vm);
       }
@@ -855,8 +1019,6 @@ __global__ __launch_bounds__(256) void k_describe(
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float sn, cs;
   orbx_sincosf(angle * factorPI, &sn, &cs);
-  const uint8_t* B = blur + (int64_t)img * pyr_bytes + G.pyr_off;
-  const uint8_t* bc = B + (int64_t)cy * G.pitch + cx;
   int nib = 0;
 #pragma unroll
   for (int m = 0; m < 4; m++) {
@@ -868,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_describe(
       const float py = (float)c_pattern[pair * 4 + e * 2 + 1];
       const int row = (int)__builtin_rintf(__builtin_fmaf(px, sn, py * cs));
       const int col = (int)__builtin_rintf(__builtin_fmaf(px, cs, -(py * sn)));
-      t[e] = bc[(int64_t)row * G.pitch + col];
+      t[e] = bc[row * BS + col];
     }
     nib |= (t[0] < t[1]) << m;
   }
@@ -908,12 +1070,14 @@ struct orbx_plan {
   FastTile* d_ftiles = nullptr;
   int nftiles = 0;
   uint8_t* d_vmap = nullptr;
+  uint64_t* d_bitmaps = nullptr;
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
   uint32_t *d_cand = nullptr, *d_lin = nullptr, *d_okey = nullptr;
   int *d_cell_counts = nullptr, *d_label = nullptr, *d_ocount = nullptr, *d_counts = nullptr;
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   size_t oct_smem = 0;
+  int key_cap = 0;
   int cell_cap = 0;
   const uint8_t* last_in = nullptr;
   int last_n = 0;
@@ -939,8 +1103,8 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   Profiler dummy;
   Profiler& pr = prof ? *prof : dummy;
   const int st_copy = pr.stage("k_copy0"), st_resize = pr.stage("k_resize"),
-            st_blur = pr.stage("k_blur"), st_fs = pr.stage("k_fast_score"),
-            st_fast = pr.stage("k_fast_nms"),
+            st_blur = pr.stage("k_blur"), st_fs = pr.stage("k_fast_tile"),
+            st_fast = pr.stage("k_fast_compact"),
             st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe");
   pr.mark(P->stream, -1);
   {
@@ -952,7 +1116,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   }
   for (int l = 1; l < L; l++) {
     const LevelGeom& D = g.lv[l];
-    dim3 grid((D.w / 4 + 256) / 256, D.h, n);
+    dim3 grid((((D.w + 3) / 4) * D.h + 255) / 256, n);
     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, P->stream, P->d_pyr, g.pyr_bytes, P->d_lv, l,
                        P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
     pr.mark(P->stream, st_resize);
@@ -964,18 +1128,19 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   }
   const int ncells = (int)g.cells.size();
   if (ncells > 0) {
-    hipLaunchKernelGGL(k_fast_score, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
-                       g.pyr_bytes, P->d_vmap, P->d_lv, P->d_ftiles, min(g.ini_th, g.min_th));
+    hipLaunchKernelGGL(k_fast_tile, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
+                       g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
+                       g.ini_th, g.min_th);
     pr.mark(P->stream, st_fs);
-    hipLaunchKernelGGL(k_fast_nms, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
-                       P->d_vmap, g.pyr_bytes, P->d_lv, P->d_cells, ncells, g.ini_th, g.min_th,
-                       P->d_cand, g.cand_total, P->d_cell_counts);
+    hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
+                       P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_lv, P->d_cells,
+                       ncells, P->d_cand, g.cand_total, P->d_cell_counts);
     pr.mark(P->stream, st_fast);
   }
   hipLaunchKernelGGL(k_octree, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream, P->d_lv,
                      P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total, P->d_lin,
                      P->d_label, P->d_okey, P->d_ocount, g.kp_total, L, g.node_cap_max,
-                     P->cell_cap);
+                     P->cell_cap, P->key_cap);
   pr.mark(P->stream, st_oct);
   hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 3) / 4, n), dim3(256), 0, P->stream,
                      P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, P->d_okey, P->d_ocount,
@@ -1036,10 +1201,10 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   for (int l = 0; l < g.nlevels; l++) {
     const LevelGeom& G = g.lv[l];
     if (!G.ncells) continue;
-    for (int ty = 0; ty * kFastTH < G.h; ty++)
-      for (int tx = 0; tx * kFastTW < G.w; tx++) {
-        const int X0 = tx * kFastTW, Y0 = ty * kFastTH;
-        if (X0 + kFastTW <= kEdge || X0 >= G.w - kEdge || Y0 + kFastTH <= kEdge ||
+    for (int ty = 0; ty * kFastT < G.h; ty++)
+      for (int tx = 0; tx * kFastT < G.w; tx++) {
+        const int X0 = tx * kFastT, Y0 = ty * kFastT;
+        if (X0 + kFastT <= kEdge || X0 >= G.w - kEdge || Y0 + kFastT <= kEdge ||
             Y0 >= G.h - kEdge)
           continue;
         ftiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, 0});
@@ -1052,7 +1217,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc(&P->d_xofs, g.xofs.size()) || dalloc(&P->d_yofs, g.yofs.size()) ||
       dalloc(&P->d_xa, g.xa.size()) || dalloc(&P->d_yb, g.yb.size()) ||
       dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_ftiles, ftiles.size()) ||
-      dalloc(&P->d_vmap, B * g.pyr_bytes) ||
+      dalloc(&P->d_vmap, B * g.pyr_bytes) || dalloc(&P->d_bitmaps, B * g.bm_words) ||
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
@@ -1075,8 +1240,16 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   const size_t NC = (size_t)g.node_cap_max;
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   P->oct_smem = 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
-                r16(4 * (P->cell_cap + 1));
-  if (P->oct_smem > 160 * 1024) return fail(ORBX_EUNSUPPORTED);
+                r16(4 * (P->cell_cap + 1)) + r16(8 * NC);
+  if (P->oct_smem > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
+  {  // LDS-resident keys: up to 4096 per level (typical levels hold < 2500 candidates), which
+     // keeps the workgroup at ~50 KB of LDS so 3 fit per CU; larger levels use global scratch
+    int cap = 0;
+    for (int l = 0; l < g.nlevels; l++) cap = std::max(cap, g.lv[l].cand_cap);
+    const size_t budget = 150 * 1024 - P->oct_smem;
+    P->key_cap = (int)std::min<size_t>({(size_t)cap, (size_t)4096, budget / 8 / 16 * 16});
+    P->oct_smem += 2 * r16(4 * (size_t)P->key_cap);
+  }
   if (hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)P->oct_smem) != hipSuccess)
     return fail(ORBX_EDEVICE);
@@ -1088,7 +1261,7 @@ int orbx_plan_destroy(orbx_plan* P) {
   if (!P) return ORBX_OK;
   if (P->graph) hipGraphExecDestroy(P->graph);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xofs,   P->d_yofs,  P->d_xa,
-                  P->d_yb,  P->d_tiles, P->d_ftiles, P->d_vmap, P->d_pyr,  P->d_blur,
+                  P->d_yb,  P->d_tiles, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label,
                   P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
   for (void* p : ptrs)

@@ -106,6 +106,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
   g->ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
   g->min_th = std::min(std::max(p.min_th_fast, 0), 255);
   g->cells.clear();
+  g->bm_words = 0;
   g->xofs.clear();
   g->yofs.clear();
   g->xa.clear();
@@ -148,8 +149,13 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
     L.cell_begin = (int)g->cells.size();
     L.cand_off = cand;
+    L.bm_wpr = L.pitch / 64;
+    L.bm_off = g->bm_words;
+    g->bm_words += 2 * (int64_t)L.bm_wpr * L.h;
     if (nCols > 0 && nRows > 0) {
       const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+      L.wcell = wCell;
+      L.hcell = hCell;
       for (int i = 0; i < nRows; i++) {
         const float iniY = (float)(minB + i * hCell);
         float maxY = iniY + hCell + 6;

@@ -30,6 +30,9 @@ struct LevelGeom {
   int vxs;             // VResizeLinearVec_32s8u SSE2 region: x < vxs
   int bxs;             // SymmColumnVec_32s8u region: x < 4*floor(w/4)
   int cell_begin, ncells;  // range in the cell table
+  int wcell, hcell;        // FAST cell size (ORBextractor.cc:755-756)
+  int64_t bm_off;          // FAST keep bitmaps (u64 words) inside one image's bitmap block
+  int bm_wpr;              // bitmap words per row (pitch / 64)
   int cand_off, cand_cap;  // candidate region (keys) inside one image's candidate block
   int nfeat;               // mnFeaturesPerLevel
   int nini;                // DistributeOctTree initial columns
@@ -57,6 +60,7 @@ struct Geometry {
   std::vector<int> xofs, yofs;        // resize source offsets
   std::vector<int16_t> xa, yb;        // resize fixed-point coefficients (pairs)
   int64_t pyr_bytes = 0;              // per image
+  int64_t bm_words = 0;               // per image: two keep planes (ini, min) per level
   int cand_total = 0;                 // per image candidate keys
   int kp_total = 0;                   // per image final keypoint slots
   int node_cap_max = 0;

@@ -88,53 +88,72 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
     ok0 = !kfkf || !P.s2.valid || P.s2.valid[i2_0];
   }
   uint32_t matched = 0;  // bit c: candidate lane + 64c already matched in this call
-  for (int pa = P.s1.node_offsets[a]; pa < P.s1.node_offsets[a + 1]; pa++) {
-    const int i1 = P.s1.node_feats[pa];
-    if (P.s1.valid && !P.s1.valid[i1]) continue;
-    const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
-    const uint64_t d1[4] = {q[0], q[1], q[2], q[3]};
-    int b1 = 256, bp = 0x7FFFFFFF, b2 = 256;
-    for (int c = 0; c * 64 < m; c++) {
-      const int j = lane + 64 * c;
-      if (j >= m || (matched >> c) & 1) continue;
-      int dist;
-      if (c == 0) {
-        if (!ok0) continue;
-        uint64_t x[4] = {reg[0], reg[1], reg[2], reg[3]};
-        dist = hamming_regs(d1, (const uint8_t*)x);
-      } else {
-        const int i2 = P.s2.node_feats[f0 + j];
-        if (kfkf && P.s2.valid && !P.s2.valid[i2]) continue;
-        dist = hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32);
-      }
-      if (dist < b1) {
-        b2 = b1;
-        b1 = dist;
-        bp = j;
-      } else if (dist < b2) {
-        b2 = dist;
+  const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
+  for (int c0 = a0; c0 < a1; c0 += 64) {
+    // prefetch up to 64 KF features of the node (index, validity, descriptor) so the serial
+    // per-feature loop below only shuffles registers
+    const int my = c0 + lane;
+    int i1_l = -1;
+    bool ok_l = false;
+    uint64_t dl0 = 0, dl1 = 0, dl2 = 0, dl3 = 0;
+    if (my < a1) {
+      i1_l = P.s1.node_feats[my];
+      ok_l = !P.s1.valid || P.s1.valid[i1_l];
+      if (ok_l) {
+        const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1_l * 32);
+        dl0 = q[0]; dl1 = q[1]; dl2 = q[2]; dl3 = q[3];
       }
     }
-    // wave merge of (best1, position, best2): keeps the first position of the minimum and the
-    // second order statistic, exactly what the sequential loop yields
+    uint64_t okm = __ballot(ok_l);
+    while (okm) {
+      const int j = __builtin_ctzll(okm);
+      okm &= okm - 1;
+      const int i1 = __shfl(i1_l, j);
+      const uint64_t d1[4] = {(uint64_t)__shfl((long long)dl0, j), (uint64_t)__shfl((long long)dl1, j),
+                              (uint64_t)__shfl((long long)dl2, j), (uint64_t)__shfl((long long)dl3, j)};
+      int b1 = 256, bp = 0x7FFFFFFF, b2 = 256;
+      for (int c = 0; c * 64 < m; c++) {
+        const int jj = lane + 64 * c;
+        if (jj >= m || (matched >> c) & 1) continue;
+        int dist;
+        if (c == 0) {
+          if (!ok0) continue;
+          uint64_t x[4] = {reg[0], reg[1], reg[2], reg[3]};
+          dist = hamming_regs(d1, (const uint8_t*)x);
+        } else {
+          const int i2 = P.s2.node_feats[f0 + jj];
+          if (kfkf && P.s2.valid && !P.s2.valid[i2]) continue;
+          dist = hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32);
+        }
+        if (dist < b1) {
+          b2 = b1;
+          b1 = dist;
+          bp = jj;
+        } else if (dist < b2) {
+          b2 = dist;
+        }
+      }
+      // wave merge of (best1, position, best2): keeps the first position of the minimum and the
+      // second order statistic, exactly what the sequential loop yields
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int ob1 = __shfl_xor(b1, o), obp = __shfl_xor(bp, o), ob2 = __shfl_xor(b2, o);
-      if (ob1 < b1 || (ob1 == b1 && obp < bp)) {
-        b2 = min(ob2, b1);
-        b1 = ob1;
-        bp = obp;
-      } else {
-        b2 = min(b2, ob1);
+      for (int o = 1; o < 64; o <<= 1) {
+        const int ob1 = __shfl_xor(b1, o), obp = __shfl_xor(bp, o), ob2 = __shfl_xor(b2, o);
+        if (ob1 < b1 || (ob1 == b1 && obp < bp)) {
+          b2 = min(ob2, b1);
+          b1 = ob1;
+          bp = obp;
+        } else {
+          b2 = min(b2, ob1);
+        }
       }
-    }
-    const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
-    if (pass && static_cast<float>(b1) < P.nnratio * static_cast<float>(b2)) {
-      if ((bp & 63) == lane) matched |= 1u << (bp >> 6);
-      if (lane == 0) {
-        const int i2 = P.s2.node_feats[f0 + bp];
-        if (kfkf) P.match[i1] = i2;
-        else P.match[i2] = i1;
+      const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
+      if (pass && static_cast<float>(b1) < P.nnratio * static_cast<float>(b2)) {
+        if ((bp & 63) == lane) matched |= 1u << (bp >> 6);
+        if (lane == 0) {
+          const int i2 = P.s2.node_feats[f0 + bp];
+          if (kfkf) P.match[i1] = i2;
+          else P.match[i2] = i1;
+        }
       }
     }
   }
@@ -234,33 +253,79 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
   const int b = lower_bound_u32(P.s2.fv.node_ids, nn2, id);
   if (b >= nn2 || P.s2.fv.node_ids[b] != id) return;
   const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
-  for (int pa = P.s1.fv.node_offsets[a] + lane; pa < P.s1.fv.node_offsets[a + 1]; pa += 64) {
-    const int i1 = P.s1.fv.node_feats[pa];
-    if (P.s1.has_mp && P.s1.has_mp[i1]) continue;
-    const bool st1 = P.s1.u_right ? P.s1.u_right[i1] >= 0 : false;
-    if (P.only_stereo && !st1) continue;
-    const orbx_keypoint kp1 = P.s1.keys_un[i1];
-    const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
-    const uint64_t d1[4] = {q[0], q[1], q[2], q[3]};
+  // KF2 node features are staged 64 at a time in this wave's LDS (descriptor, keypoint,
+  // stereo/map-point flags); every lane then scans them in node order for its KF1 feature
+  __shared__ uint64_t s_d[4][64][4];
+  __shared__ float s_x[4][64], s_y[4][64];
+  __shared__ int s_i2[4][64], s_oct[4][64];
+  const int wv = threadIdx.x >> 6;
+  for (int pa0 = P.s1.fv.node_offsets[a]; pa0 < P.s1.fv.node_offsets[a + 1]; pa0 += 64) {
+    const int pa = pa0 + lane;
+    bool live = pa < P.s1.fv.node_offsets[a + 1];
+    int i1 = 0;
+    bool st1 = false;
+    orbx_keypoint kp1{};
+    uint64_t d1[4] = {0, 0, 0, 0};
+    if (live) {
+      i1 = P.s1.fv.node_feats[pa];
+      if (P.s1.has_mp && P.s1.has_mp[i1]) live = false;
+      st1 = P.s1.u_right ? P.s1.u_right[i1] >= 0 : false;
+      if (P.only_stereo && !st1) live = false;
+    }
+    if (live) {
+      kp1 = P.s1.keys_un[i1];
+      const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
+      d1[0] = q[0]; d1[1] = q[1]; d1[2] = q[2]; d1[3] = q[3];
+    }
     int bestDist = kTH_LOW, bestIdx2 = -1;
-    for (int pb = f0; pb < f1; pb++) {
-      const int i2 = P.s2.fv.node_feats[pb];
-      if (P.s2.has_mp && P.s2.has_mp[i2]) continue;  // vbMatched2 is never set (:680, 728)
-      const bool st2 = P.s2.u_right ? P.s2.u_right[i2] >= 0 : false;
-      if (P.only_stereo && !st2) continue;
-      const int dist = hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32);
-      if (dist > kTH_LOW || dist > bestDist) continue;
-      const orbx_keypoint kp2 = P.s2.keys_un[i2];
-      if (!st1 && !st2) {
-        const float dex = P.ex - kp2.x, dey = P.ey - kp2.y;
-        if (__builtin_fmaf(dex, dex, dey * dey) < 100 * P.s2.scale_factors[kp2.octave]) continue;
+    for (int pb0 = f0; pb0 < f1; pb0 += 64) {
+      const int nb = min(64, f1 - pb0);
+      {  // stage chunk: entry skipped (i2 = -1) when it has a map point or fails only_stereo
+        int i2 = -1;
+        if (lane < nb) {
+          i2 = P.s2.fv.node_feats[pb0 + lane];
+          const bool st2 = P.s2.u_right ? P.s2.u_right[i2] >= 0 : false;
+          // `vbMatched2[idx2] || pMP2` (:728): vbMatched2 is never set in this function
+          if ((P.s2.has_mp && P.s2.has_mp[i2]) || (P.only_stereo && !st2)) {
+            i2 = -1;
+          } else {
+            const uint64_t* q = (const uint64_t*)(P.s2.desc + (int64_t)i2 * 32);
+            s_d[wv][lane][0] = q[0];
+            s_d[wv][lane][1] = q[1];
+            s_d[wv][lane][2] = q[2];
+            s_d[wv][lane][3] = q[3];
+            const orbx_keypoint kp2 = P.s2.keys_un[i2];
+            s_x[wv][lane] = kp2.x;
+            s_y[wv][lane] = kp2.y;
+            s_oct[wv][lane] = kp2.octave | (st2 ? 0x10000 : 0);
+          }
+        }
+        if (lane < 64) s_i2[wv][lane] = i2;
       }
-      if (epipolar_ok(kp1.x, kp1.y, kp2.x, kp2.y, P.F, P.s2.level_sigma2[kp2.octave])) {
-        bestIdx2 = i2;
-        bestDist = dist;
+      if (live) {
+        for (int j = 0; j < nb; j++) {
+          const int i2 = s_i2[wv][j];
+          if (i2 < 0) continue;
+          const uint64_t* dd = s_d[wv][j];
+          const int dist = __popcll(d1[0] ^ dd[0]) + __popcll(d1[1] ^ dd[1]) +
+                           __popcll(d1[2] ^ dd[2]) + __popcll(d1[3] ^ dd[3]);
+          if (dist > kTH_LOW || dist > bestDist) continue;
+          const int oc2 = s_oct[wv][j];
+          const bool st2 = oc2 >> 16;
+          const int oct2 = oc2 & 0xFFFF;
+          const float x2 = s_x[wv][j], y2 = s_y[wv][j];
+          if (!st1 && !st2) {
+            const float dex = P.ex - x2, dey = P.ey - y2;
+            if (__builtin_fmaf(dex, dex, dey * dey) < 100 * P.s2.scale_factors[oct2]) continue;
+          }
+          if (epipolar_ok(kp1.x, kp1.y, x2, y2, P.F, P.s2.level_sigma2[oct2])) {
+            bestIdx2 = i2;
+            bestDist = dist;
+          }
+        }
       }
     }
-    P.m12[i1] = bestIdx2;
+    if (pa < P.s1.fv.node_offsets[a + 1] && live) P.m12[i1] = bestIdx2;
   }
 }
 
@@ -375,40 +440,57 @@ __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_o
   __syncthreads();
   for (int i = tid; i < n; i += 256) atomicAdd(&cnt[nodes[i] - id_lo], 1);
   __syncthreads();
-  if (tid == 0) {
-    int acc = 0, nn = 0;
-    for (int b = 0; b < nb; b++) {
-      cur[b] = acc;
-      if (cnt[b]) {
-        oid[nn] = id_lo + b;
-        ooff[nn] = acc;
-        nn++;
+  // bucket starts: wave-0 exclusive scan over the nb buckets, 64 at a time
+  if (tid < 64) {
+    int run = 0, nn = 0;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+      const int b = b0 + tid;
+      const int c = b < nb ? cnt[b] : 0;
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(incl, o);
+        if (tid >= o) incl += x;
       }
-      acc += cnt[b];
+      const uint64_t ne = __ballot(c > 0);
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0));
+      if (b < nb) {
+        cur[b] = run + incl - c;
+        if (c > 0) {
+          oid[nn + rank] = id_lo + b;
+          ooff[nn + rank] = run + incl - c;
+        }
+      }
+      run += __shfl(incl, 63);
+      nn += __popcll(ne);
     }
-    ooff[nn] = acc;
-    n_nodes[img] = nn;
+    if (tid == 0) {
+      ooff[nn] = run;
+      n_nodes[img] = nn;
+    }
   }
   __syncthreads();
   // stable placement by wave 0: chunks of 64 features in index order; a lane's rank inside its
-  // bucket = lanes below it with the same bucket (wave shuffles, no barrier inside the wave)
+  // bucket = lanes below it with the same bucket, from one ballot per bucket-id bit
   if (tid < 64) {
+    int nbits = 1;
+    while ((1 << nbits) < nb) nbits++;
+    const uint64_t lt = (1ull << tid) - 1, gt = ~((2ull << tid) - 1);
     for (int c0 = 0; c0 < n; c0 += 64) {
       const int i = c0 + tid;
-      const int bk = i < n ? (int)(nodes[i] - id_lo) : -1;
-      int rank = 0, tot = 0;
-      bool last = true;
-      for (int j = 0; j < 64; j++) {
-        const int o = __shfl(bk, j);
-        if (o == bk) {
-          tot++;
-          if (j < tid) rank++;
-          if (j > tid) last = false;
-        }
+      const bool valid = i < n;
+      const int bk = valid ? (int)(nodes[i] - id_lo) : 0;
+      uint64_t eq = __ballot(valid);
+      for (int bit = 0; bit < nbits; bit++) {
+        const uint64_t m = __ballot(valid && ((bk >> bit) & 1));
+        eq &= ((bk >> bit) & 1) ? m : ~m;
       }
-      const int base = i < n ? cur[bk] : 0;
-      if (i < n) of[base + rank] = i;
-      if (i < n && last) cur[bk] = base + tot;
+      if (valid) {
+        const int base = cur[bk];
+        of[base + __popcll(eq & lt)] = i;
+        if ((eq & gt) == 0) cur[bk] = base + __popcll(eq);  // last lane of the bucket
+      }
     }
   }
 }

@@ -48,13 +48,35 @@ def algorithmic_bytes(levels, n_kp, n_img):
     P = [w * h for w, h in levels]
     per_resize = [(P[l - 1] + P[l]) * n_img for l in range(1, len(P))]
     return {
+        "k_copy0": 2 * P[0] * n_img,                            # level 0 into the pitched block
         "k_resize": sum(per_resize) / max(len(per_resize), 1),  # average launch
         "k_blur": 2 * sum(P) * n_img,
-        "k_fast_cells": sum(P) * n_img,
+        "k_fast_tile": sum(P) * n_img,                          # every level pixel read once
+        "k_fast_compact": sum(P) * n_img / 4,                   # 2 NMS bits per pixel
         "k_describe": 60 * n_kp,
         "k_featvec": 36 * n_kp,
         "total_per_frame": P[0] + sum(per_resize) / n_img + 3 * sum(P) + 60 * n_kp / n_img,
     }
+
+
+def pmc_traffic(pmc_dir, kernel):
+    """HBM-side bytes per launch of `kernel` from separate rocprofv3 --pmc passes
+    (FETCH_SIZE, WRITE_SIZE, both in KB).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2→fabric
+    requests (Infinity-Cache hits included) and reads 1/2 of the bytes of 16-B-per-lane streaming
+    loads; these kernels use 1-4 B accesses, which the guide leaves uncalibrated, so the value is
+    reported uncorrected (FETCH_SIZE + WRITE_SIZE) x 1024."""
+    import csv
+    tot = {}
+    for name, counter in (("fetch_size.csv", "FETCH_SIZE"), ("write_size.csv", "WRITE_SIZE")):
+        path = os.path.join(pmc_dir, name)
+        if not os.path.exists(path):
+            return None
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+                if r["Kernel_Name"].split("(")[0].endswith("::" + kernel) and r["Counter_Name"] == counter]
+        if not vals:
+            return None
+        tot[counter] = sum(vals) / len(vals)
+    return round((tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024)
 
 
 def cpu_baseline(cfg, seconds):
@@ -133,6 +155,12 @@ def main():
     ap.add_argument("--batch", type=int, default=64, help="frames per step (per GPU)")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="independent camera-stream pipelines per GPU, one HIP stream each "
+                         "(kernels are latency-bound; two streams fill the CUs the other leaves idle)")
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01_pmc"),
+                    help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE CSVs of this bench command, used "
+                         "for roofline.traffic (per launch of the dominant kernel)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
@@ -156,18 +184,24 @@ def main():
     cfg = CONFIGS[args.config]
     w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
     voc = Vocabulary.synthetic()
-    pipe = FramePipeline(w, h, B, voc, nf, device=local)
-    pipe.seeded_masks(range(B))
+    S = max(1, args.streams)
     ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
-    pipe.set_matching(fundamental_from_pose(), (ex, ey), bow_ratio=0.7, bow_check_ori=True,
-                      tri_ratio=0.6, tri_check_ori=False)
-    # synthetic frames of this rank's camera stream, resident in HBM before timing
-    stream_id = stream_of_rank(rank)
-    base = synth.canvas(w, h, stream=stream_id)
-    pool = []
-    for pi in range(args.pool):
-        fr = np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)])
-        pool.append(torch.from_numpy(fr).cuda())
+    pipes, pools = [], []
+    for si in range(S):
+        pipe = FramePipeline(w, h, B, voc, nf, device=local)
+        pipe.seeded_masks(range(B))
+        pipe.set_matching(fundamental_from_pose(), (ex, ey), bow_ratio=0.7, bow_check_ori=True,
+                          tri_ratio=0.6, tri_check_ori=False)
+        # synthetic frames of this camera stream, resident in HBM before timing
+        stream_id = stream_of_rank(rank) * S + si
+        base = synth.canvas(w, h, stream=stream_id)
+        pool = []
+        for pi in range(args.pool):
+            fr = np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)])
+            pool.append(torch.from_numpy(fr).cuda())
+        pipes.append(pipe)
+        pools.append(pool)
+    pipe = pipes[0]
     torch.cuda.synchronize()
 
     def barrier():
@@ -175,31 +209,38 @@ def main():
             dist.barrier()
 
     for i in range(args.warmup):
-        pipe.run(pool[i % len(pool)].data_ptr(), B)
-    pipe.sync()
-    kp_counts, bow, tri, err = pipe.results(B)
-    if err:
-        raise RuntimeError("matcher reported a node larger than its per-wave capacity")
+        for p, pool in zip(pipes, pools):
+            p.run(pool[i % len(pool)].data_ptr(), B)
+    for p in pipes:
+        p.sync()
+        if p.results(B)[3]:
+            raise RuntimeError("matcher reported a node larger than its per-wave capacity")
 
     profile = not args.no_profile
     if profile:
-        pipe.profile(True)
+        for p in pipes:
+            p.profile(True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        pipe.run(pool[i % len(pool)].data_ptr(), B)
-    pipe.sync()
+        for p, pool in zip(pipes, pools):
+            p.run(pool[i % len(pool)].data_ptr(), B)
+    for p in pipes:
+        p.sync()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     stages = pipe.profile_read() if profile else {}
-    pipe.profile(False)
+    for p in pipes:
+        if profile:
+            p.profile_read()
+        p.profile(False)
     kp_counts, bow, tri, _ = pipe.results(B)
 
     elapsed = aggregate_elapsed(elapsed, world)
 
-    frames = world * B * args.steps
+    frames = world * S * B * args.steps
     value = frames / elapsed
     ex_tables = ORBextractor(nf)
     levels = level_sizes(w, h, ex_tables.GetInverseScaleFactors())
@@ -216,19 +257,23 @@ def main():
                     "achieved": round(achieved, 3) if achieved is not None else None,
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
-                    "traffic": None,
+                    "traffic": pmc_traffic(args.pmc_dir, dom),
+                    "traffic_note": "uncorrected (FETCH_SIZE+WRITE_SIZE)*1024 per launch from "
+                                    "rocprofv3 --pmc passes of this command (profiles/r01_pmc)",
                     "avg_launch_us": round(avg_s * 1e6, 2),
                     "algorithmic_bytes_per_launch": a_bytes,
-                    "stages_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()}}
+                    "stages_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()},
+                    "stages_of": "camera stream 0 (kernels of other streams overlap them)" if S > 1 else "the only stream"}
 
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B,
+        "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B * S,
+                   "camera_streams_per_gpu": S, "frames_per_batch": B,
                    "image": f"{w}x{h}", "nfeatures": nf, "nlevels": 8, "scale_factor": 1.2,
-                   "parallelism": f"{world} independent camera streams (one per GPU)",
+                   "parallelism": f"{world} GPU(s) x {S} independent camera streams, no collective",
                    "keypoints_per_frame": round(n_kp / B, 1),
                    "bow_matches_per_frame": round(float(bow.mean()), 1),
                    "triangulation_matches_per_frame": round(float(tri.mean()), 1),
