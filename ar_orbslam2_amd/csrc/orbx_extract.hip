@@ -39,6 +39,19 @@ __device__ __forceinline__ const uint8_t* level_base(const uint8_t* pyr, int64_t
   return pyr + (int64_t)img * pyr_bytes + g.pyr_off;
 }
 
+// XCD-aware block order (MI355X_MICROARCH.md: workgroups go round-robin to the 8 XCDs by
+// linear block id, each XCD with its own L2).  Remaps the linear id so each XCD runs one
+// contiguous range of (image, tile) blocks: neighbouring tiles share their halo rows and
+// columns in the same L2 instead of fetching them on different XCDs.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+  const int gx = gridDim.x, total = gx * gridDim.y;
+  int lin = blockIdx.y * gx + blockIdx.x;
+  const int q = total >> 3;
+  if (lin < (q << 3)) lin = (lin & 7) * q + (lin >> 3);
+  by = lin / gx;
+  bx = lin - by * gx;
+}
+
 __device__ __forceinline__ int reflect101(int p, int len) {
   if (len == 1) return 0;
   while (p < 0 || p >= len) {
@@ -159,67 +172,94 @@ __global__ __launch_bounds__(256) void k_copy0(const uint8_t* __restrict__ in,
 }
 
 // ------------------------------------------------------------------ k_resize
-// cv::resize(level l-1 ROI -> level l ROI, INTER_LINEAR), 8UC1 fixed point:
-// horizontal taps Q11 ints, vertical pass = SSE2 mulhi form for x < vxs, scalar
-// (H0*b0 + H1*b1 + 2^21) >> 22 tail.  One thread per 4 output pixels (one aligned dword
-// store); the two source rows of level l-1 are L2 resident (written by the previous launch).
-__device__ __forceinline__ int resize_px(const uint8_t* r0, const uint8_t* r1, int dx,
-                                         const LevelGeom& D, const int* __restrict__ xofs,
-                                         const int16_t* __restrict__ xa, int b0, int b1) {
-  const int x0 = xofs[D.coef_x + dx];
-  int h0, h1;
-  if (dx < D.xmax) {
-    const int a0 = xa[2 * (D.coef_x + dx)], a1 = xa[2 * (D.coef_x + dx) + 1];
-    h0 = r0[x0] * a0 + r0[x0 + 1] * a1;
-    h1 = r1[x0] * a0 + r1[x0 + 1] * a1;
-  } else {
-    h0 = r0[x0] * 2048;
-    h1 = r1[x0] * 2048;
-  }
-  int v;
-  if (dx < D.vxs) {
-    const int t0 = max(-32768, min(32767, h0 >> 4));
-    const int t1 = max(-32768, min(32767, h1 >> 4));
-    int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);
-    m = max(-32768, min(32767, m));
-    m = max(-32768, min(32767, m + 2));
-    v = m >> 2;
-  } else {
-    v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-  }
-  return max(0, min(255, v));
-}
+// cv::resize(level l-1 ROI -> level l ROI, INTER_LINEAR), 8UC1 fixed point, the
+// way OpenCV's resizeGeneric_ runs it: horizontal pass once per source row into int buffers
+// (HResizeLinear, taps Q11), then the vertical pass per output row (VResizeLinear: SSE2
+// mulhi form for x < vxs, scalar (H0*b0 + H1*b1 + 2^21) >> 22 tail).
+// One workgroup = kRzRows output rows x kRzCols output columns of one image: the source
+// window is staged in LDS with aligned dword loads, the horizontal sums of each source row
+// it needs are computed once into LDS, then every thread writes 4 output pixels per row as
+// one dword.
 
 __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                                 const LevelGeom* __restrict__ lv, int level,
+                                                int ncolblk,
                                                 const int* __restrict__ xofs,
                                                 const int16_t* __restrict__ xa,
                                                 const int* __restrict__ yofs,
                                                 const int16_t* __restrict__ yb) {
+  __shared__ __align__(16) uint32_t s_src[kRzSrcRows][kRzSrcWords];
+  __shared__ __align__(16) int s_h[kRzSrcRows][kRzCols];
   const LevelGeom& D = lv[level];
   const LevelGeom& S = lv[level - 1];
-  const int img = blockIdx.y;
-  const int q4 = (D.w + 3) >> 2;  // dword groups per row; one thread per group, rows flattened
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= q4 * D.h) return;
-  const int dy = idx / q4;
-  const int dx0 = (idx - dy * q4) * 4;
+  int bx, img;
+  xcd_block(bx, img);
+  const int band = bx / ncolblk, cb = bx - band * ncolblk;
+  const int R0 = band * kRzRows, C0 = cb * kRzCols;
+  const int R1 = min(R0 + kRzRows, D.h), C1 = min(C0 + kRzCols, D.w);
+  const int tid = threadIdx.x;
   const uint8_t* src = level_base(pyr, pyr_bytes, S, img);
   uint8_t* dst = pyr + (int64_t)img * pyr_bytes + D.pyr_off;
-  const int sy0 = yofs[D.coef_y + dy];
-  const int ya = sy0 >= 0 ? (sy0 < S.h ? sy0 : S.h - 1) : 0;
-  const int yb1 = sy0 + 1 >= 0 ? (sy0 + 1 < S.h ? sy0 + 1 : S.h - 1) : 0;
-  const uint8_t* r0 = src + (int64_t)ya * S.pitch;
-  const uint8_t* r1 = src + (int64_t)yb1 * S.pitch;
-  const int b0 = yb[2 * (D.coef_y + dy)], b1 = yb[2 * (D.coef_y + dy) + 1];
-  uint32_t out = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int dx = dx0 + k;
-    if (dx < D.w) out |= (uint32_t)resize_px(r0, r1, dx, D, xofs, xa, b0, b1) << (8 * k);
+  // source window: rows clamp(yofs(R0)) .. clamp(yofs(R1-1)+1), bytes xofs(C0) .. xofs(C1-1)+1
+  const int ys_lo = min(max(yofs[D.coef_y + R0], 0), S.h - 1);
+  const int ys_hi = min(max(yofs[D.coef_y + R1 - 1] + 1, 0), S.h - 1);
+  const int nrows = ys_hi - ys_lo + 1;
+  const int xw_lo = xofs[D.coef_x + C0] & ~3;
+  const int xw_hi = xofs[D.coef_x + C1 - 1] + 1;
+  const int nwords = (xw_hi - xw_lo) / 4 + 1;
+  if (nrows > kRzSrcRows || nwords > kRzSrcWords) return;  // excluded by build_geometry
+  for (int i = tid; i < nrows * nwords; i += 256) {
+    const int r = i / nwords, c = i - r * nwords;
+    s_src[r][c] = *(const uint32_t*)(src + (int64_t)(ys_lo + r) * S.pitch + xw_lo + 4 * c);
   }
-  // pitch is a multiple of 64, so the padding bytes of the last dword are in the row's pad
-  *(uint32_t*)(dst + (int64_t)dy * D.pitch + dx0) = out;
+  __syncthreads();
+  // horizontal pass: thread = output column
+  {
+    const int dx = C0 + tid;
+    if (dx < C1) {
+      const int x0 = xofs[D.coef_x + dx] - xw_lo;
+      const int a0 = xa[2 * (D.coef_x + dx)], a1 = xa[2 * (D.coef_x + dx) + 1];
+      const uint8_t* sb = (const uint8_t*)s_src;
+      if (dx < D.xmax) {
+        for (int r = 0; r < nrows; r++)
+          s_h[r][tid] = sb[r * kRzSrcWords * 4 + x0] * a0 + sb[r * kRzSrcWords * 4 + x0 + 1] * a1;
+      } else {
+        for (int r = 0; r < nrows; r++) s_h[r][tid] = sb[r * kRzSrcWords * 4 + x0] * 2048;
+      }
+    }
+  }
+  __syncthreads();
+  // vertical pass: 64 threads per output row, 4 adjacent columns each
+  const int q = tid & 63;
+  const int c4 = C0 + 4 * q;
+  if (c4 >= C1) return;
+  for (int dy = R0 + (tid >> 6); dy < R1; dy += 4) {
+    const int sy0 = yofs[D.coef_y + dy];
+    const int ra = min(max(sy0, 0), S.h - 1) - ys_lo;
+    const int rb = min(max(sy0 + 1, 0), S.h - 1) - ys_lo;
+    const int b0 = yb[2 * (D.coef_y + dy)], b1 = yb[2 * (D.coef_y + dy) + 1];
+    const int4 H0 = *(const int4*)&s_h[ra][4 * q];
+    const int4 H1 = *(const int4*)&s_h[rb][4 * q];
+    const int h0[4] = {H0.x, H0.y, H0.z, H0.w}, h1[4] = {H1.x, H1.y, H1.z, H1.w};
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int v;
+      if (c4 + k < D.vxs) {
+        const int t0 = max(-32768, min(32767, h0[k] >> 4));
+        const int t1 = max(-32768, min(32767, h1[k] >> 4));
+        int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);
+        m = max(-32768, min(32767, m));
+        m = max(-32768, min(32767, m + 2));
+        v = m >> 2;
+      } else {
+        v = (h0[k] * b0 + h1[k] * b1 + (1 << 21)) >> 22;
+      }
+      out |= (uint32_t)max(0, min(255, v)) << (8 * k);
+    }
+    // pitch is a multiple of 64, so bytes past w of the last dword land in the row's pad
+    *(uint32_t*)(dst + (int64_t)dy * D.pitch + c4) = out;
+  }
 }
 
 // ------------------------------------------------------------------ k_blur
@@ -241,8 +281,9 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
                                               const BlurTile* __restrict__ tiles) {
   __shared__ __align__(16) uint32_t s_in[kBlurTH + 6][(kBlurTW + 8) / 4];
   __shared__ __align__(16) int s_row[kBlurTH + 6][kBlurTW];
-  const BlurTile T = tiles[blockIdx.x];
-  const int img = blockIdx.y;
+  int bx, img;
+  xcd_block(bx, img);
+  const BlurTile T = tiles[bx];
   const LevelGeom& G = lv[T.level];
   const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
   uint8_t* dst = blur + (int64_t)img * pyr_bytes + G.pyr_off;
@@ -402,17 +443,47 @@ __device__ __forceinline__ bool fast_maybe(const uint8_t* s, int stride, int x, 
 // ---- k_fast_tile: FAST for 64 x 64 output pixels of one level per workgroup.
 //  (1) score map V = clamp(cornerScore+1, 0, 255) on the tile plus a 1-px ring, for pixels
 //      of the detection region [19, w-19) x [19, h-19) (0 elsewhere).  A pixel failing the
-//      quarter-point test at min(iniThFAST, minThFAST) cannot be a corner at either threshold,
-//      so its V (<= threshold) is equivalent to 0 in every NMS: only candidates are scored,
-//      from wave-local queues (ballot + mbcnt).
+//      even-point test at min(iniThFAST, minThFAST) cannot be a corner at either threshold, so
+//      its V (<= threshold) is equivalent to 0 in every NMS: only candidates are scored, from
+//      wave-local queues (ballot + mbcnt).  The test runs on 4 adjacent pixels per lane: the
+//      circle bytes of the 4 pixels are one (alignbyte-shifted) LDS dword, compared as two
+//      packed-i16 pairs whose sign bits are folded into one flag word per circle point.
 //  (2) cv::FAST's strict 8-neighbour NMS at both thresholds, with neighbours outside the
 //      pixel's own FAST cell (or outside the detection region) counting as 0 — the cell-local
-//      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  One ballot per
-//      row gives the 64-bit keep word of that row for each threshold.
+//      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  Lane = column,
+//      each wave walks 16 rows keeping the masked 3-wide row maxima of the rows above/below in
+//      registers; one ballot per row and threshold gives the 64-bit keep word of that row.
 constexpr int kFastT = 64;
 struct FastTile {
   int16_t level, tx, ty, pad;
 };
+
+// bytes x+dx .. x+dx+3 of an LDS row given its dwords d-1, d, d+1 (x = 4d)
+template <int DX>
+__device__ __forceinline__ uint32_t bytes_at(uint32_t wm, uint32_t w0, uint32_t wp) {
+  if constexpr (DX == 0) return w0;
+  else if constexpr (DX > 0) return __builtin_amdgcn_alignbyte(wp, w0, DX);
+  else return __builtin_amdgcn_alignbyte(w0, wm, 4 + DX);
+}
+
+// pk_i16 sign bits of (a - b) for the even / odd byte pairs of two u8x4 words
+__device__ __forceinline__ uint32_t pk_sub_i16(uint32_t a, uint32_t b) {
+  typedef short v2s __attribute__((ext_vector_type(2)));
+  v2s x = __builtin_bit_cast(v2s, a), y = __builtin_bit_cast(v2s, b);
+  return __builtin_bit_cast(uint32_t, (v2s)(x - y));
+}
+
+// darker / brighter flags of one circle point for 4 pixels: sign bit (bit 8j+7) of byte j =
+// pixel x+j.  Bytes 0,2 and 1,3 are compared as packed-i16 pairs; one v_perm gathers the
+// four sign-carrying high bytes back into pixel order.
+__device__ __forceinline__ void circle_flags(uint32_t e, uint32_t loE, uint32_t loO,
+                                             uint32_t hiE, uint32_t hiO, uint32_t& dark,
+                                             uint32_t& bright) {
+  const uint32_t eE = __builtin_amdgcn_perm(0u, e, 0x0c020c00u);
+  const uint32_t eO = __builtin_amdgcn_perm(0u, e, 0x0c030c01u);
+  dark = __builtin_amdgcn_perm(pk_sub_i16(eO, loO), pk_sub_i16(eE, loE), 0x07030501u);
+  bright = __builtin_amdgcn_perm(pk_sub_i16(hiO, eO), pk_sub_i16(hiE, eE), 0x07030501u);
+}
 
 __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ pyr,
                                                    int64_t pyr_bytes, uint8_t* __restrict__ vmap,
@@ -421,93 +492,157 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
                                                    const LevelGeom* __restrict__ lv,
                                                    const FastTile* __restrict__ tiles, int ini_th,
                                                    int min_th) {
-  constexpr int kIn = kFastT + 8;   // staged window: X0-4 .. X0+67, Y0-4 .. Y0+67
-  constexpr int kWin = kFastT + 2;  // V window: X0-1 .. X0+64, Y0-1 .. Y0+64
-  constexpr int kVS = kWin + 2;     // V row stride
-  constexpr int kQ = (kWin * kWin + 255) / 256 * 64;
-  __shared__ __align__(16) uint32_t s_in[kIn][kIn / 4];
-  __shared__ __align__(4) uint8_t s_v[kWin * kVS];
+  constexpr int kInR = kFastT + 8;        // staged rows Y0-4 .. Y0+67
+  constexpr int kInD = (kFastT + 16) / 4; // staged dwords: columns X0-8 .. X0+71
+  constexpr int kWinR = kFastT + 2;       // V rows Y0-1 .. Y0+64
+  constexpr int kWinG = (kFastT + 8) / 4; // V column groups: X0-4 .. X0+67
+  constexpr int kVS = kWinG * 4;          // V row stride (bytes)
+  constexpr int kGroups = kWinR * kWinG;
+  constexpr int kQ = (kGroups + 255) / 256 * 256;  // per-wave queue bound (4 px per group)
+  __shared__ __align__(16) uint32_t s_in[kInR][kInD];
+  __shared__ __align__(16) uint32_t s_v32[kWinR * kWinG];
   __shared__ uint16_t s_q[4][kQ];
-  const FastTile T = tiles[blockIdx.x];
-  const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int bx, img;
+  xcd_block(bx, img);
+  const FastTile T = tiles[bx];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar row math
   const LevelGeom& G = lv[T.level];
   const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
   const int X0 = T.tx * kFastT, Y0 = T.ty * kFastT;
-  for (int i = tid; i < kIn * (kIn / 4); i += 256) {
-    const int r = i / (kIn / 4), c = i - r * (kIn / 4);
+  for (int i = tid; i < kInR * kInD; i += 256) {
+    const int r = i / kInD, c = i - r * kInD;
     const int y = min(max(Y0 + r - 4, 0), G.h - 1);
-    const int x = X0 - 4 + 4 * c;
+    const int x = X0 - 8 + 4 * c;
     s_in[r][c] = (x >= 0 && x + 4 <= G.pitch) ? *(const uint32_t*)(src + (int64_t)y * G.pitch + x)
                                               : 0u;
   }
   __syncthreads();
-  const uint8_t* sb = (const uint8_t*)s_in;
   const int t_lo = min(ini_th, min_th);
   const int ylo = kEdge, yhi = G.h - kEdge, xlo = kEdge, xhi = G.w - kEdge;
+  const uint32_t tt = (uint32_t)t_lo * 0x00010001u;
   uint16_t* q = s_q[wid];
   int nq = 0;
-  for (int i0 = wid * 64; i0 < kWin * kWin; i0 += 256) {
-    const int i = i0 + lane;
-    const int vy = i / kWin, vx = i - vy * kWin;
-    const int y = Y0 - 1 + vy, x = X0 - 1 + vx;
-    bool f = false;
-    if (i < kWin * kWin) {
-      s_v[vy * kVS + vx] = 0;
-      f = y >= ylo && y < yhi && x >= xlo && x < xhi && fast_maybe(sb, kIn, vx + 3, vy + 3, t_lo);
+  for (int g0 = wid * 64; g0 < kGroups; g0 += 256) {
+    const int g = g0 + lane;
+    const int vy = g / kWinG, c = g - vy * kWinG;
+    const int y = Y0 - 1 + vy, x = X0 - 4 + 4 * c;
+    uint32_t pass = 0;  // bit j: pixel x+j passes
+    if (g < kGroups) {
+      s_v32[g] = 0;
+      if (y >= ylo && y < yhi && x + 3 >= xlo && x < xhi) {
+        const int r = vy + 3, d = c + 1;
+        const uint32_t* R0 = s_in[r];
+        const uint32_t C = R0[d];
+        const uint32_t cE = __builtin_amdgcn_perm(0u, C, 0x0c020c00u);
+        const uint32_t cO = __builtin_amdgcn_perm(0u, C, 0x0c030c01u);
+        const uint32_t loE = pk_sub_i16(cE, tt), loO = pk_sub_i16(cO, tt);
+        const uint32_t hiE = cE + tt, hiO = cO + tt;  // <= 510 per half, no carry
+        const uint32_t *Rm3 = s_in[r - 3], *Rm2 = s_in[r - 2], *Rp2 = s_in[r + 2],
+                       *Rp3 = s_in[r + 3];
+        const uint32_t m2a = Rm2[d - 1], m2b = Rm2[d], m2c = Rm2[d + 1];
+        const uint32_t p2a = Rp2[d - 1], p2b = Rp2[d], p2c = Rp2[d + 1];
+        const uint32_t r0a = R0[d - 1], r0c = R0[d + 1];
+        // even circle points in circle order: (0,3) (2,2) (3,0) (2,-2) (0,-3) (-2,-2) (-3,0) (-2,2)
+        uint32_t fd[8], fb[8];
+        circle_flags(Rp3[d], loE, loO, hiE, hiO, fd[0], fb[0]);
+        circle_flags(bytes_at<2>(p2a, p2b, p2c), loE, loO, hiE, hiO, fd[1], fb[1]);
+        circle_flags(bytes_at<3>(r0a, C, r0c), loE, loO, hiE, hiO, fd[2], fb[2]);
+        circle_flags(bytes_at<2>(m2a, m2b, m2c), loE, loO, hiE, hiO, fd[3], fb[3]);
+        circle_flags(Rm3[d], loE, loO, hiE, hiO, fd[4], fb[4]);
+        circle_flags(bytes_at<-2>(m2a, m2b, m2c), loE, loO, hiE, hiO, fd[5], fb[5]);
+        circle_flags(bytes_at<-3>(r0a, C, r0c), loE, loO, hiE, hiO, fd[6], fb[6]);
+        circle_flags(bytes_at<-2>(p2a, p2b, p2c), loE, loO, hiE, hiO, fd[7], fb[7]);
+        // any 9-arc contains 4 cyclically consecutive even points, all darker or all brighter
+        uint32_t pd[8], pb[8], any = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          pd[k] = fd[k] & fd[(k + 1) & 7];
+          pb[k] = fb[k] & fb[(k + 1) & 7];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) any |= (pd[k] & pd[(k + 2) & 7]) | (pb[k] & pb[(k + 2) & 7]);
+        pass = ((any >> 7) & 1u) | ((any >> 14) & 2u) | ((any >> 21) & 4u) | ((any >> 28) & 8u);
+        // detection region, per pixel
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (x + j < xlo || x + j >= xhi) pass &= ~(1u << j);
+      }
     }
-    const uint64_t m = __ballot(f);
-    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    if (f) q[nq + rank] = (uint16_t)i;
-    nq += __popcll(m);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const bool fj = (pass >> j) & 1u;
+      const uint64_t m = __ballot(fj);
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      if (fj) q[nq + rank] = (uint16_t)(g * 4 + j);
+      nq += __popcll(m);
+    }
   }
+  // s_v32 zeroing above happens-before the score writes below only within a wave's own
+  // groups; candidates are queued by the same wave that zeroed their group.
+  uint8_t* s_v = (uint8_t*)s_v32;
   for (int j0 = 0; j0 < nq; j0 += 64) {
     const int j = j0 + lane;
     if (j < nq) {
-      const int i = q[j], vy = i / kWin, vx = i - vy * kWin;
-      const int sc = fast_score(sb, kIn, vx + 3, vy + 3);
-      s_v[vy * kVS + vx] = (uint8_t)min(255, max(0, sc + 1));
+      const int i = q[j];  // = vy * kVS + vx
+      const int vy = i / kVS, vx = i - vy * kVS;
+      const int sc = fast_score((const uint8_t*)s_in, kInD * 4, vx + 4, vy + 3);
+      s_v[i] = (uint8_t)min(255, max(0, sc + 1));
     }
   }
   __syncthreads();
-  // NMS, wave w: rows 16w .. 16w+15 of the tile, lane = column.  The cell masks split into a
-  // per-lane column part (computed once) and a row part that is uniform across the wave.
+  // NMS, wave w: rows 16w .. 16w+15 of the tile, lane = column.  V window column of x is
+  // x - X0 + 4, row of y is y - Y0 + 1.
   const int x = X0 + lane;
-  const float rw = 1.0f / (float)max(G.wcell, 1), rh = 1.0f / (float)max(G.hcell, 1);
-  const int jx = (int)(((float)(x - kEdge) + 0.5f) * rw);
-  const int rx = x - kEdge - jx * G.wcell;
+  // position of x / y inside its FAST cell (detection rows/columns 19 + i*hCell ..): the
+  // cell edges are where a neighbour belongs to another cell ROI and counts as 0
+  const int wc = max(G.wcell, 1), hc = max(G.hcell, 1);
+  const int rx = ((x - kEdge) % wc + wc) % wc;
   const bool xin = x >= xlo && x < xhi;
-  const int mL = rx != 0 ? 0xFF : 0, mR = (rx != G.wcell - 1 && x + 1 < xhi) ? 0xFF : 0;
+  const int mL = rx != 0 ? 0xFF : 0, mR = (rx != wc - 1 && x + 1 < xhi) ? 0xFF : 0;
   uint64_t* bm_ini = bitmaps + (int64_t)img * bm_words + G.bm_off;
   uint64_t* bm_min = bm_ini + (int64_t)G.bm_wpr * G.h;
   uint8_t* vout = vmap + (int64_t)img * pyr_bytes + G.pyr_off;
-#pragma unroll 2
+  const int r0 = wid * (kFastT / 4);
+  int ry = ((Y0 + r0 - kEdge) % hc + hc) % hc;  // scalar, advanced per row
+  // keep at t  <=>  V > t and V-1 > (nmax > t ? nmax-1 : 0)  <=>  V > (nmax > t ? nmax : max(t,1))
+  // (a neighbour counts with its score V-1 only if it is a corner at t, V > t; the count is
+  // monotone in V, so the largest masked neighbour decides)
+  const int ini1 = max(ini_th, 1), min1 = max(min_th, 1);
+  // masked left/right neighbours and centre of V-window row vr
+  auto row_lr = [&](int vr, int& vc, int& lr) {
+    const uint8_t* p = s_v + vr * kVS + lane + 4;
+    vc = p[0];
+    lr = max(p[-1] & mL, p[1] & mR);
+  };
+  int vc_prev, lr_prev, vc_cur, lr_cur;
+  row_lr(r0, vc_prev, lr_prev);      // image row Y0 + r0 - 1
+  row_lr(r0 + 1, vc_cur, lr_cur);    // image row Y0 + r0
+  int hm_prev = max(lr_prev, vc_prev);
   for (int rr = 0; rr < kFastT / 4; rr++) {
-    const int r = wid * (kFastT / 4) + rr, y = Y0 + r;
+    const int r = r0 + rr, y = Y0 + r;
     if (y >= G.h) break;  // wave-uniform
-    const int iy = (int)(((float)(y - kEdge) + 0.5f) * rh);
-    const int ry = y - kEdge - iy * G.hcell;
+    int vc_next, lr_next;
+    row_lr(r + 2, vc_next, lr_next);
     const bool yin = y >= ylo && y < yhi;
-    const int mU = ry != 0 ? 0xFF : 0, mD = (ry != G.hcell - 1 && y + 1 < yhi) ? 0xFF : 0;
-    const int vc = (r + 1) * kVS + lane + 1;
-    const int v = s_v[vc];
-    const int n0 = s_v[vc - kVS - 1] & mU & mL, n1 = s_v[vc - kVS] & mU,
-              n2 = s_v[vc - kVS + 1] & mU & mR, n3 = s_v[vc - 1] & mL, n4 = s_v[vc + 1] & mR,
-              n5 = s_v[vc + kVS - 1] & mD & mL, n6 = s_v[vc + kVS] & mD,
-              n7 = s_v[vc + kVS + 1] & mD & mR;
-    const int nmax = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
-    // a neighbour counts with its score V-1 only if it is a corner at t (V > t), and that count
-    // is monotone in V, so the largest masked neighbour decides: keep iff V > t and
-    // V-1 > (nmax > t ? nmax-1 : 0)
+    const bool up = ry != 0, dn = ry != hc - 1 && y + 1 < yhi;  // wave-uniform
+    ry = ry + 1 == hc ? 0 : ry + 1;
+    const int nmax = max(max(up ? hm_prev : 0, dn ? max(lr_next, vc_next) : 0), lr_cur);
+    const int v = vc_cur;
     const bool cand = xin && yin;
-    const bool ki = cand && v > ini_th && v - 1 > (nmax > ini_th ? nmax - 1 : 0);
-    const bool km = cand && v > min_th && v - 1 > (nmax > min_th ? nmax - 1 : 0);
+    const bool ki = cand && v > (nmax > ini_th ? nmax : ini1);
+    const bool km = cand && v > (nmax > min_th ? nmax : min1);
     const uint64_t wi = __ballot(ki), wm = __ballot(km);
     if (lane == 0) {
       bm_ini[(int64_t)y * G.bm_wpr + T.tx] = wi;
       bm_min[(int64_t)y * G.bm_wpr + T.tx] = wm;
     }
-    vout[(int64_t)y * G.pitch + x] = (uint8_t)v;
+    // k_fast_compact reads V only at survivors of either threshold
+    if (ki || km) vout[(int64_t)y * G.pitch + x] = (uint8_t)v;
+    hm_prev = max(lr_cur, vc_cur);
+    vc_cur = vc_next;
+    lr_cur = lr_next;
   }
 }
 
@@ -524,7 +659,9 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
                                                       int cand_total,
                                                       int* __restrict__ cell_counts) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int ci = blockIdx.x * 4 + wid, img = blockIdx.y;
+  int bx, img;
+  xcd_block(bx, img);
+  const int ci = bx * 4 + wid;
   if (ci >= ncells) return;
   const CellGeom C = cells[ci];
   const LevelGeom& G = lv[C.level];
@@ -938,11 +1075,12 @@ __global__ __launch_bounds__(256) void k_describe(
     const LevelGeom* __restrict__ lv, int nlevels, const uint32_t* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
-  const int img = blockIdx.y;
+  int bx, img;
+  xcd_block(bx, img);
   const int lane = threadIdx.x & 63;
-  const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int slot = bx * 4 + (threadIdx.x >> 6);
   const int* oc = ocount + img * nlevels;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bx == 0 && threadIdx.x == 0) {
     int t = 0;
     for (int l = 0; l < nlevels; l++) t += oc[l];
     counts[img] = t;
@@ -1116,9 +1254,10 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   }
   for (int l = 1; l < L; l++) {
     const LevelGeom& D = g.lv[l];
-    dim3 grid((((D.w + 3) / 4) * D.h + 255) / 256, n);
+    const int ncolblk = (D.w + kRzCols - 1) / kRzCols;
+    dim3 grid(ncolblk * ((D.h + kRzRows - 1) / kRzRows), n);
     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, P->stream, P->d_pyr, g.pyr_bytes, P->d_lv, l,
-                       P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
+                       ncolblk, P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
     pr.mark(P->stream, st_resize);
   }
   if (P->ntiles > 0) {

@@ -135,7 +135,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
       resize_tables(P.w, P.h, L.w, L.h, g, &L);
     }
     // every level (level 0 is copied in) lives in the pitched pyramid block
-    L.pitch = (L.w + 63) & ~63;
+    L.pitch = (L.w + 4 + 63) & ~63;  // >= w + 4: a row's last dword never straddles the row end
     L.pyr_off = pyr;
     pyr += ((int64_t)L.pitch * L.h + 255) / 256 * 256;
     L.bxs = (L.w / 4) * 4;
@@ -205,6 +205,28 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     L.kp_cap = L.node_cap;
     kp += L.kp_cap;
     g->node_cap_max = std::max(g->node_cap_max, L.node_cap);
+  }
+  // k_resize source windows (kRzRows x kRzCols output tiles) must fit its LDS staging
+  for (int l = 1; l < p.nlevels; l++) {
+    const LevelGeom& D = g->lv[l];
+    const LevelGeom& S = g->lv[l - 1];
+    for (int r0 = 0; r0 < D.h; r0 += kRzRows) {
+      const int r1 = std::min(r0 + kRzRows, D.h);
+      const int lo = std::min(std::max(g->yofs[D.coef_y + r0], 0), S.h - 1);
+      const int hi = std::min(std::max(g->yofs[D.coef_y + r1 - 1] + 1, 0), S.h - 1);
+      if (hi - lo + 1 > kRzSrcRows) {
+        if (why) *why = "scale factor too large for the resize tile";
+        return ORBX_EUNSUPPORTED;
+      }
+    }
+    for (int c0 = 0; c0 < D.w; c0 += kRzCols) {
+      const int c1 = std::min(c0 + kRzCols, D.w);
+      const int lo = g->xofs[D.coef_x + c0] & ~3, hi = g->xofs[D.coef_x + c1 - 1] + 1;
+      if ((hi - lo) / 4 + 1 > kRzSrcWords || (hi | 3) >= S.pitch) {
+        if (why) *why = "scale factor too large for the resize tile";
+        return ORBX_EUNSUPPORTED;
+      }
+    }
   }
   if (cand >= (1 << 24)) {
     if (why) *why = "candidate capacity exceeds 2^24";

@@ -21,6 +21,12 @@ constexpr int kMaxIni = 64;     // initial octree columns supported (nIni)
 
 // Per pyramid level, computed on the host once per plan (ORBextractor.cc:404-460,
 // 735-757, 1047-1072).
+// k_resize workgroup tile: output rows x columns, and the LDS source window it may need
+// (build_geometry rejects scale factors whose windows exceed it)
+constexpr int kRzRows = 16, kRzCols = 256;
+constexpr int kRzSrcRows = 24;
+constexpr int kRzSrcWords = 88;
+
 struct LevelGeom {
   int w, h;            // level size (cvRound((float)cols * invScale))
   int pitch;           // row pitch in the pyramid / blur blocks (w rounded up to 64 B)

@@ -155,9 +155,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64, help="frames per step (per GPU)")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="independent camera-stream pipelines per GPU, one HIP stream each "
-                         "(kernels are latency-bound; two streams fill the CUs the other leaves idle)")
+                         "(kernels are latency-bound; concurrent streams fill the CUs the others leave idle)")
     ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01_pmc"),
                     help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE CSVs of this bench command, used "
                          "for roofline.traffic (per launch of the dominant kernel)")
