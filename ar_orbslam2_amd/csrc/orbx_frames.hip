@@ -1,6 +1,7 @@
 // orbx_frames.hip — device-resident frame pipeline: the whole "ORB extract + match" unit of
 // work of SURVEY §8d for a batch of frames, with no host round trip:
-//   extract (plan)  ->  node ids (k_featvec)  ->  FeatureVector CSR (k_csr)
+//   extract (plan)  ->  Frame::ComputeBoW: vocabulary descent (k_voc_transform), BowVector
+//   (k_bowvec), FeatureVector CSR (k_csr)
 //   -> SearchByBoW(prev-as-KF, cur)  ->  SearchForTriangulation(prev-as-KF, cur-as-KF)
 // Frame f of a batch is matched against frame (f-1) mod n of the same batch.  The sequence is
 // captured once into a hipGraph per (input pointer, batch size).
@@ -14,6 +15,7 @@
 
 #include "orbx_internal.h"
 #include "orbx_match.h"
+#include "orbx_vocab.h"
 
 using namespace orbx;
 
@@ -22,12 +24,19 @@ struct orbx_frames {
   PlanView v{};
   int device = 0;
   // vocabulary
-  uint8_t* d_voc = nullptr;
-  int k = 10, L = 6, levelsup = 4, nid_level = 2;
-  uint32_t id_lo = 0;
+  const orbx_vocabulary* voc = nullptr;
+  VocView vv{};
+  const VocRanks* ranks = nullptr;
+  int scoring = 0, weighting = 0, levelsup = 4, nid_level = 2;
   int nb = 1;
   // per frame
-  uint32_t* d_node_of = nullptr;  // [B][kp]
+  uint32_t* d_node_of = nullptr;  // [B][kp] FeatureVector node id
+  uint32_t* d_rank_of = nullptr;  // [B][kp] FeatureVector rank (k_csr bucket)
+  uint32_t* d_word_of = nullptr;  // [B][kp]
+  double* d_wt_of = nullptr;      // [B][kp]
+  uint32_t* d_bow_words = nullptr;  // [B][kp]
+  double* d_bow_vals = nullptr;     // [B][kp]
+  int* d_bow_n = nullptr;           // [B]
   uint32_t* d_ids = nullptr;      // [B][nb]
   int* d_off = nullptr;           // [B][nb+1]
   int* d_feats = nullptr;         // [B][kp]
@@ -138,18 +147,24 @@ int build_problems(orbx_frames* F, int n) {
 int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
   Profiler dummy;
   Profiler& pr = prof ? *prof : dummy;
-  const int st_fv = pr.stage("k_featvec"), st_csr = pr.stage("k_csr"),
+  const int st_fv = pr.stage("k_voc_transform"), st_bv = pr.stage("k_bowvec"),
+            st_csr = pr.stage("k_csr"),
             st_bow = pr.stage("k_bow"), st_tri = pr.stage("k_tri");
   hipStream_t s = F->v.stream;
   int rc = plan_enqueue(F->plan, d_in, n, prof);
   if (rc) return rc;
   const int kp = F->v.kp_total;
-  rc = launch_featvec(F->d_voc, F->k, F->nid_level, F->v.d_desc, (int64_t)kp * 32, F->v.d_counts,
-                      0, kp, F->d_node_of, kp, n, s);
+  rc = launch_voc_transform(F->vv, F->nid_level, F->ranks->d_rank_of_node, F->v.d_desc,
+                            (int64_t)kp * 32, F->v.d_counts, 0, kp, F->d_word_of, F->d_rank_of,
+                            F->d_node_of, F->d_wt_of, kp, n, s);
   if (rc) return rc;
   pr.mark(s, st_fv);
-  rc = launch_csr(F->d_node_of, kp, F->v.d_counts, 0, F->id_lo, F->nb, F->d_ids, F->d_off,
-                  F->d_feats, kp, F->d_nn, n, s);
+  rc = launch_bowvec(F->scoring, F->weighting, F->d_word_of, F->d_wt_of, kp, F->v.d_counts, 0, kp,
+                     F->d_bow_words, F->d_bow_vals, kp, F->d_bow_n, n, s);
+  if (rc) return rc;
+  pr.mark(s, st_bv);
+  rc = launch_csr(F->d_rank_of, kp, F->v.d_counts, 0, 0, F->nb, F->ranks->d_rank_ids, F->d_ids,
+                  F->d_off, F->d_feats, kp, F->d_nn, n, s);
   if (rc) return rc;
   pr.mark(s, st_csr);
   ORBX_HIP(hipMemsetAsync(F->d_match, 0xFF, (size_t)n * kp * 4, s));
@@ -168,20 +183,19 @@ int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
 extern "C" {
 
 int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_batch,
-                       const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
-                       int hip_device, orbx_frames** out) {
-  if (!p || !out || !voc_desc || k < 2 || L < 1 || levelsup < 0 || max_batch < 1)
-    return ORBX_EINVAL;
+                       const orbx_vocabulary* voc, int32_t levelsup, int hip_device,
+                       orbx_frames** out) {
+  if (!p || !out || !voc || levelsup < 0 || max_batch < 1) return ORBX_EINVAL;
   *out = nullptr;
-  const int nid_level = L - levelsup;
-  if (nid_level < 1) return ORBX_EUNSUPPORTED;  // FeatureVector keyed by the root only
-  int64_t nodes = 1, lsz = 1, id_lo = 0;
-  for (int l = 1; l <= nid_level; l++) {
-    id_lo = nodes;
-    lsz *= k;
-    nodes += lsz;
-  }
-  if (lsz > 8192) return ORBX_EUNSUPPORTED;
+  int voc_dev = 0;
+  VocView vv;
+  int rc = vocab_view(voc, &vv, &voc_dev);
+  if (rc) return rc;
+  if (voc_dev != hip_device) return ORBX_EINVAL;
+  const VocRanks* R = nullptr;
+  rc = vocab_ranks(voc, levelsup, &R);
+  if (rc) return rc;
+  if (R->nb > 8192) return ORBX_EUNSUPPORTED;  // FeatureVector buckets live in LDS
   orbx_frames* F = new (std::nothrow) orbx_frames();
   if (!F) return ORBX_ENOMEM;
   auto fail = [&](int rc) {
@@ -189,17 +203,23 @@ int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_b
     return rc;
   };
   F->device = hip_device;
-  int rc = orbx_plan_create(p, w, h, max_batch, hip_device, &F->plan);
+  rc = orbx_plan_create(p, w, h, max_batch, hip_device, &F->plan);
   if (rc) return fail(rc);
   plan_view(F->plan, &F->v);
-  F->k = k;
-  F->L = L;
+  if (F->v.kp_total > 8192) return fail(ORBX_EUNSUPPORTED);  // k_bowvec sorts in LDS
+  int32_t L = 0;
+  orbx_vocabulary_info(voc, nullptr, &L, &F->scoring, &F->weighting, nullptr, nullptr);
+  F->voc = voc;
+  F->vv = vv;
+  F->ranks = R;
   F->levelsup = levelsup;
-  F->nid_level = nid_level;
-  F->id_lo = (uint32_t)id_lo;
-  F->nb = (int)lsz;
+  F->nid_level = L - levelsup;
+  F->nb = std::max(R->nb, 1);
   const size_t B = max_batch, kp = F->v.kp_total;
-  if (dalloc(&F->d_voc, nodes * 32) || dalloc(&F->d_node_of, B * kp) ||
+  if (dalloc(&F->d_node_of, B * kp) || dalloc(&F->d_rank_of, B * kp) ||
+      dalloc(&F->d_word_of, B * kp) ||
+      dalloc(&F->d_wt_of, B * kp) || dalloc(&F->d_bow_words, B * kp) ||
+      dalloc(&F->d_bow_vals, B * kp) || dalloc(&F->d_bow_n, B) ||
       dalloc(&F->d_ids, B * F->nb) || dalloc(&F->d_off, B * (F->nb + 1)) ||
       dalloc(&F->d_feats, B * kp) || dalloc(&F->d_nn, B) || dalloc(&F->d_valid, B * kp) ||
       dalloc(&F->d_hasmp, B * kp) || dalloc(&F->d_sf, p->nlevels) ||
@@ -208,8 +228,7 @@ int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_b
       dalloc(&F->d_pairs, B * kp * 2) || dalloc(&F->d_tri_count, B) || dalloc(&F->d_bprob, B) ||
       dalloc(&F->d_tprob, B))
     return fail(ORBX_ENOMEM);
-  if (hipMemcpy(F->d_voc, voc_desc, nodes * 32, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(F->d_sf, F->v.g->scale, 4 * p->nlevels, hipMemcpyHostToDevice) != hipSuccess ||
+  if (hipMemcpy(F->d_sf, F->v.g->scale, 4 * p->nlevels, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(F->d_s2, F->v.g->sigma2, 4 * p->nlevels, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(F->d_valid, 1, B * kp) != hipSuccess ||
       hipMemset(F->d_hasmp, 0, B * kp) != hipSuccess ||
@@ -223,7 +242,8 @@ int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_b
 int orbx_frames_destroy(orbx_frames* F) {
   if (!F) return ORBX_OK;
   F->drop_graphs();
-  void* ptrs[] = {F->d_voc,   F->d_node_of, F->d_ids,   F->d_off,       F->d_feats,
+  void* ptrs[] = {F->d_rank_of, F->d_word_of, F->d_wt_of, F->d_bow_words, F->d_bow_vals, F->d_bow_n,
+                  F->d_node_of, F->d_ids,   F->d_off,       F->d_feats,
                   F->d_nn,    F->d_valid,   F->d_hasmp, F->d_sf,        F->d_s2,
                   F->d_match, F->d_bow_count, F->d_m12, F->d_pairs,     F->d_tri_count,
                   F->d_bprob, F->d_tprob};
@@ -325,6 +345,16 @@ int orbx_frames_outputs(orbx_frames* F, orbx_keypoint** d_kps, uint8_t** d_desc,
   if (d_node_of) *d_node_of = F->d_node_of;
   if (d_bow_match) *d_bow_match = F->d_match;
   if (d_tri_pairs) *d_tri_pairs = F->d_pairs;
+  return ORBX_OK;
+}
+
+int orbx_frames_bow(orbx_frames* F, uint32_t** d_bow_words, double** d_bow_values,
+                    int32_t** d_bow_n, uint32_t** d_word_of) {
+  if (!F) return ORBX_EINVAL;
+  if (d_bow_words) *d_bow_words = F->d_bow_words;
+  if (d_bow_values) *d_bow_values = F->d_bow_vals;
+  if (d_bow_n) *d_bow_n = F->d_bow_n;
+  if (d_word_of) *d_word_of = F->d_word_of;
   return ORBX_OK;
 }
 

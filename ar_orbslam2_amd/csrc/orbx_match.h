@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
 #include "../../include/orbx.h"
 
 namespace orbx {
@@ -80,12 +84,62 @@ struct TriProblem {
 
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
 int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
-int launch_featvec(const uint8_t* d_voc, int k, int nid_level, const uint8_t* d_desc,
-                   int64_t desc_stride_img, const int* d_counts, int n_fixed, int max_n,
-                   uint32_t* d_out, int64_t out_stride_img, int nimg, hipStream_t s);
 int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,
-               uint32_t id_lo, int nb, uint32_t* d_ids, int* d_off, int* d_feats,
-               int64_t feats_stride, int* d_nn, int nimg, hipStream_t s);
+               uint32_t id_lo, int nb, const uint32_t* d_rank_ids, uint32_t* d_ids, int* d_off,
+               int* d_feats, int64_t feats_stride, int* d_nn, int nimg, hipStream_t s);
 // d_ids is [nimg][nb], d_off is [nimg][nb + 1], d_feats is [nimg][feats_stride].
 
+// ------------------------------------------------------------------ host-pointer ABI helpers
+// Per-thread device workspace (ORBmatcher / the vocabulary are called from the Tracking,
+// LocalMapping and LoopClosing threads at once; each thread gets its own stream and buffers).
+struct Workspace {
+  hipStream_t stream = nullptr;
+  char* d = nullptr;
+  size_t cap = 0;
+  int device = -1;
+  ~Workspace() {
+    if (d) (void)hipFree(d);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  int reserve(size_t bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (device != dev) {
+      if (d) (void)hipFree(d);
+      if (stream) (void)hipStreamDestroy(stream);
+      d = nullptr;
+      cap = 0;
+      stream = nullptr;
+      device = dev;
+    }
+    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
+      return ORBX_EDEVICE;
+    if (bytes <= cap) return ORBX_OK;
+    if (d) (void)hipFree(d);
+    d = nullptr;
+    cap = std::max(bytes, cap * 2);
+    if (hipMalloc(&d, cap) != hipSuccess) {
+      cap = 0;
+      return ORBX_ENOMEM;
+    }
+    return ORBX_OK;
+  }
+};
+extern thread_local Workspace tls_ws;
+
+// Packs host arrays into one staging buffer, uploaded with one copy.
+struct Stager {
+  std::vector<char> host;
+  size_t add(const void* p, size_t bytes) {
+    const size_t off = (host.size() + 15) & ~size_t(15);
+    host.resize(off + bytes);
+    if (p && bytes) memcpy(host.data() + off, p, bytes);
+    return off;
+  }
+};
+
+template <class T>
+static inline T* dptr(char* base, size_t off) {
+  return (T*)(base + off);
+}
 }  // namespace orbx

@@ -8,7 +8,6 @@
 //                 (ORBmatcher.cc:267-285 / 637-655, 1604-1645)
 //   k_tri_nodes   one wave per KF1 node, one lane per KF1 feature (ORBmatcher.cc:694-792)
 //   k_tri_finish  rotation filter + ordered (idx1 ascending) pair compaction (:794-823)
-//   k_featvec     TemplatedVocabulary::transform node ids (TemplatedVocabulary.h:1218-1259)
 //   k_csr         FeatureVector build: stable bucket sort of feature indices by node id
 //                 (FeatureVector.cpp:31-45)
 #include <hip/hip_runtime.h>
@@ -387,43 +386,15 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
 }
 
 // ------------------------------------------------------------------ vocabulary + FeatureVector
-__global__ __launch_bounds__(256) void k_featvec(const uint8_t* __restrict__ voc, int k,
-                                                 int nid_level, const uint8_t* __restrict__ desc,
-                                                 int64_t desc_stride_img,
-                                                 const int* __restrict__ counts, int n_fixed,
-                                                 uint32_t* __restrict__ out,
-                                                 int64_t out_stride_img) {
-  const int img = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int n = counts ? counts[img] : n_fixed;
-  if (i >= n) return;
-  const uint64_t* q = (const uint64_t*)(desc + img * desc_stride_img + (int64_t)i * 32);
-  const uint64_t d[4] = {q[0], q[1], q[2], q[3]};
-  uint32_t id = 0;
-  if (nid_level > 0) {
-    int64_t level_off = 1, level_size = 1, j = 0;
-    for (int lvl = 1; lvl <= nid_level; lvl++) {
-      level_size *= k;
-      const int64_t first = level_off + j * k;
-      int64_t best = first;
-      int bestd = hamming_regs(d, voc + first * 32);
-      for (int c = 1; c < k; c++) {
-        const int dd = hamming_regs(d, voc + (first + c) * 32);
-        if (dd < bestd) bestd = dd, best = first + c;
-      }
-      id = (uint32_t)best;
-      j = best - level_off;
-      level_off += level_size;
-    }
-  }
-  out[img * out_stride_img + i] = id;
-}
-
-// Stable bucket sort of feature indices by node id within [id_lo, id_lo + nb) (one workgroup
-// per image): node_ids ascending, offsets, feats ascending within each node.
+// Stable bucket sort of feature indices by node bucket (one workgroup per image): bucket of
+// feature i = node_of[i] - id_lo in [0, nb), or 0xFFFFFFFF for a feature the FeatureVector
+// skips (stopped word).  Bucket b is node id rank_ids[b] (or id_lo + b when rank_ids is null);
+// buckets ascend with node id.  Output: node_ids ascending, offsets, feats ascending within
+// each node (FeatureVector::addFeature in index order, FeatureVector.cpp:31-45).
 __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_of,
                                              int64_t node_stride, const int* __restrict__ counts,
                                              int n_fixed, uint32_t id_lo, int nb,
+                                             const uint32_t* __restrict__ rank_ids,
                                              uint32_t* __restrict__ node_ids,
                                              int* __restrict__ offsets, int* __restrict__ feats,
                                              int64_t feats_stride, int* __restrict__ n_nodes) {
@@ -438,7 +409,8 @@ __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_o
   int* of = feats + img * feats_stride;                // [img][feats_stride]
   for (int i = tid; i < nb; i += 256) cnt[i] = 0;
   __syncthreads();
-  for (int i = tid; i < n; i += 256) atomicAdd(&cnt[nodes[i] - id_lo], 1);
+  for (int i = tid; i < n; i += 256)
+    if (nodes[i] != 0xFFFFFFFFu) atomicAdd(&cnt[nodes[i] - id_lo], 1);
   __syncthreads();
   // bucket starts: wave-0 exclusive scan over the nb buckets, 64 at a time
   if (tid < 64) {
@@ -458,7 +430,7 @@ __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_o
       if (b < nb) {
         cur[b] = run + incl - c;
         if (c > 0) {
-          oid[nn + rank] = id_lo + b;
+          oid[nn + rank] = rank_ids ? rank_ids[b] : id_lo + b;
           ooff[nn + rank] = run + incl - c;
         }
       }
@@ -479,8 +451,9 @@ __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_o
     const uint64_t lt = (1ull << tid) - 1, gt = ~((2ull << tid) - 1);
     for (int c0 = 0; c0 < n; c0 += 64) {
       const int i = c0 + tid;
-      const bool valid = i < n;
-      const int bk = valid ? (int)(nodes[i] - id_lo) : 0;
+      const uint32_t nd = i < n ? nodes[i] : 0xFFFFFFFFu;
+      const bool valid = nd != 0xFFFFFFFFu;
+      const int bk = valid ? (int)(nd - id_lo) : 0;
       uint64_t eq = __ballot(valid);
       for (int bit = 0; bit < nbits; bit++) {
         const uint64_t m = __ballot(valid && ((bk >> bit) & 1));
@@ -519,84 +492,20 @@ int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_tri");
 }
 
-int launch_featvec(const uint8_t* d_voc, int k, int nid_level, const uint8_t* d_desc,
-                   int64_t desc_stride_img, const int* d_counts, int n_fixed, int max_n,
-                   uint32_t* d_out, int64_t out_stride_img, int nimg, hipStream_t s) {
-  if (max_n <= 0 || nimg <= 0) return ORBX_OK;
-  hipLaunchKernelGGL(k_featvec, dim3((max_n + 255) / 256, nimg), dim3(256), 0, s, d_voc, k,
-                     nid_level, d_desc, desc_stride_img, d_counts, n_fixed, d_out, out_stride_img);
-  hipError_t e = hipGetLastError();
-  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_featvec");
-}
-
 int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,
-               uint32_t id_lo, int nb, uint32_t* d_ids, int* d_off, int* d_feats,
-               int64_t feats_stride, int* d_nn, int nimg, hipStream_t s) {
+               uint32_t id_lo, int nb, const uint32_t* d_rank_ids, uint32_t* d_ids, int* d_off,
+               int* d_feats, int64_t feats_stride, int* d_nn, int nimg, hipStream_t s) {
   if (nimg <= 0) return ORBX_OK;
   const size_t smem = (size_t)(2 * nb) * 4;
   if (smem > 64 * 1024) return ORBX_EUNSUPPORTED;
   hipLaunchKernelGGL(k_csr, dim3(nimg), dim3(256), smem, s, d_node_of, node_stride, d_counts,
-                     n_fixed, id_lo, nb, d_ids, d_off, d_feats, feats_stride, d_nn);
+                     n_fixed, id_lo, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride, d_nn);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_csr");
 }
 
 // ------------------------------------------------------------------ host-pointer ABI
-// Per-thread device workspace (ORBmatcher is called from three threads at once; each thread
-// gets its own stream and buffers).
-struct Workspace {
-  hipStream_t stream = nullptr;
-  char* d = nullptr;
-  size_t cap = 0;
-  int device = -1;
-  ~Workspace() {
-    if (d) hipFree(d);
-    if (stream) hipStreamDestroy(stream);
-  }
-  int reserve(size_t bytes) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (device != dev) {
-      if (d) hipFree(d);
-      if (stream) hipStreamDestroy(stream);
-      d = nullptr;
-      cap = 0;
-      stream = nullptr;
-      device = dev;
-    }
-    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
-      return ORBX_EDEVICE;
-    if (bytes <= cap) return ORBX_OK;
-    if (d) hipFree(d);
-    d = nullptr;
-    cap = std::max(bytes, cap * 2);
-    if (hipMalloc(&d, cap) != hipSuccess) {
-      cap = 0;
-      return ORBX_ENOMEM;
-    }
-    return ORBX_OK;
-  }
-};
-static thread_local Workspace tls_ws;
-
-// Packs host arrays into one staging buffer, uploads them with one copy.
-struct Stager {
-  std::vector<char> host;
-  struct Item {
-    size_t off;
-  };
-  size_t add(const void* p, size_t bytes) {
-    const size_t off = (host.size() + 15) & ~size_t(15);
-    host.resize(off + bytes);
-    if (p && bytes) memcpy(host.data() + off, p, bytes);
-    return off;
-  }
-};
-
-template <class T>
-static T* dptr(char* base, size_t off) {
-  return (T*)(base + off);
-}
+thread_local Workspace tls_ws;
 
 }  // namespace orbx
 
@@ -818,34 +727,6 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int3
                      dptr<int>(base, oo));
   ORBX_HIP(hipGetLastError());
   ORBX_HIP(hipMemcpyAsync(out, base + oo, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
-  return ORBX_OK;
-}
-
-int orbx_feature_vector(const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
-                        const uint8_t* desc, int32_t n, uint32_t* node_of_feature) {
-  if (k < 1 || L < 1 || n < 0 || !node_of_feature || (n && !desc) || !voc_desc) return ORBX_EINVAL;
-  if (n == 0) return ORBX_OK;
-  const int nid_level = L - levelsup;
-  int64_t nodes = 1, lsz = 1;
-  for (int l = 1; l <= std::max(nid_level, 0); l++) {
-    lsz *= k;
-    nodes += lsz;
-    if (nodes > (1LL << 31)) return ORBX_EUNSUPPORTED;
-  }
-  Stager st;
-  const size_t ov = st.add(voc_desc, (size_t)nodes * 32);
-  const size_t od = st.add(desc, (size_t)n * 32);
-  const size_t oo = st.add(nullptr, (size_t)n * 4);
-  int rc = tls_ws.reserve(st.host.size());
-  if (rc) return rc;
-  char* base = tls_ws.d;
-  hipStream_t s = tls_ws.stream;
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), oo, hipMemcpyHostToDevice, s));
-  rc = launch_featvec(dptr<uint8_t>(base, ov), k, nid_level, dptr<uint8_t>(base, od), 0, nullptr,
-                      n, n, dptr<uint32_t>(base, oo), 0, 1, s);
-  if (rc) return rc;
-  ORBX_HIP(hipMemcpyAsync(node_of_feature, base + oo, (size_t)n * 4, hipMemcpyDeviceToHost, s));
   ORBX_HIP(hipStreamSynchronize(s));
   return ORBX_OK;
 }

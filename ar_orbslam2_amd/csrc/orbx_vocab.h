@@ -1,0 +1,47 @@
+// orbx_vocab.h — device view of a DBoW2 vocabulary (orbx_vocab.hip) for the frame pipeline.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbx.h"
+
+namespace orbx {
+
+// Children of a node are contiguous records [child_begin, child_begin + nchild): descriptor
+// (32 B) and meta {node id, that node's child_begin, its nchild, its word id}.
+struct VocView {
+  const uint8_t* cdesc;  // [n_nodes - 1][32]
+  const int4* cmeta;     // [n_nodes - 1]
+  const double* weight;  // [n_nodes] node weight (Node::weight)
+  const double* word_weight;  // [n_words] weight of word w's node (m_words[w]->weight)
+  int root_cb, root_nc;
+  int n_words;
+  int k;
+};
+
+// FeatureVector node table of one levelsup: possible FeatureVector nodes, ascending id
+struct VocRanks {
+  int levelsup = -1;
+  int nb = 0;
+  uint32_t* d_rank_of_node = nullptr;  // [n_nodes] rank, 0xFFFFFFFF if never a FeatureVector key
+  uint32_t* d_rank_ids = nullptr;      // [nb] node id of rank b
+};
+
+int vocab_view(const orbx_vocabulary* voc, VocView* v, int* device);
+int vocab_ranks(const orbx_vocabulary* voc, int levelsup, const VocRanks** out);
+
+// Per feature of every image: word id, FeatureVector rank and node id (0xFFFFFFFF when
+// stopped; d_node_of nullable), and the weight of the node the descent ended on.
+int launch_voc_transform(const VocView& V, int nid_level, const uint32_t* d_rank_of_node,
+                         const uint8_t* d_desc, int64_t desc_stride_img, const int* d_counts,
+                         int n_fixed, int max_n, uint32_t* d_word_of, uint32_t* d_rank_of,
+                         uint32_t* d_node_of, double* d_weight_of, int64_t out_stride_img,
+                         int nimg, hipStream_t s);
+// BowVector of every image from the word ids and weights (TemplatedVocabulary.h:1144-1197).
+// max_n <= 8192.
+int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
+                  const double* d_weight_of, int64_t in_stride, const int* d_counts, int n_fixed,
+                  int max_n, uint32_t* d_words, double* d_values, int64_t out_stride,
+                  int* d_nwords, int nimg, hipStream_t s);
+
+}  // namespace orbx

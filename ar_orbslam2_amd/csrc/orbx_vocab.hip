@@ -1,0 +1,687 @@
+// orbx_vocab.hip — DBoW2 TemplatedVocabulary<FORB::TDescriptor, FORB> on the device:
+// text loader, greedy Hamming descent, BowVector and FeatureVector
+// (ORB_SLAM2/Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h, BowVector.cpp, FeatureVector.cpp).
+//
+//   k_voc_transform  one 16- (k <= 16) or 32-lane group per feature: lane c scores child c of
+//                    the current node, the group's (distance, child) minimum picks the next
+//                    node; child records are contiguous per parent so a level is one
+//                    coalesced round trip (transform, TemplatedVocabulary.h:1218-1259)
+//   k_bowvec         one workgroup per image: stable LSD radix sort of the features by word
+//                    in LDS, per-word weight sums in feature order (BowVector::addWeight /
+//                    addIfNotExist, BowVector.cpp:38-62), then the scoring's L1/L2
+//                    normalisation as one ordered pass (BowVector::normalize, :66-98)
+// The FeatureVector CSR reuses k_csr (orbx_match.hip) over the node ranks built here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "orbx_internal.h"
+#include "orbx_match.h"
+#include "orbx_vocab.h"
+
+#pragma clang fp contract(off)
+
+struct orbx_vocabulary {
+  int device = 0;
+  int k = 0, L = 0, scoring = 0, weighting = 0;
+  int n_nodes = 1, n_words = 0;  // n_nodes counts the root
+  // host tree (node ids in file order)
+  std::vector<int> parent, depth, child_begin, nchild;
+  std::vector<uint32_t> child_ids;  // per-parent contiguous child records
+  std::vector<int> word_of_node;    // 0 unless flagged leaf (Node(): word_id(0))
+  // device
+  uint8_t* d_cdesc = nullptr;
+  int4* d_cmeta = nullptr;
+  double* d_weight = nullptr;
+  double* d_word_weight = nullptr;
+  std::mutex m;
+  std::vector<orbx::VocRanks*> ranks;
+  ~orbx_vocabulary() {
+    for (void* p : {(void*)d_cdesc, (void*)d_cmeta, (void*)d_weight, (void*)d_word_weight})
+      if (p) (void)hipFree(p);
+    for (auto* r : ranks) {
+      if (r->d_rank_of_node) (void)hipFree(r->d_rank_of_node);
+      if (r->d_rank_ids) (void)hipFree(r->d_rank_ids);
+      delete r;
+    }
+  }
+};
+
+namespace orbx {
+
+// ------------------------------------------------------------------ k_voc_transform
+template <int G>
+__global__ __launch_bounds__(256) void k_voc_transform(VocView V, int nid_level,
+                                                       const uint32_t* __restrict__ rank_of_node,
+                                                       const uint8_t* __restrict__ desc,
+                                                       int64_t desc_stride,
+                                                       const int* __restrict__ counts,
+                                                       int n_fixed, uint32_t* __restrict__ word_out,
+                                                       uint32_t* __restrict__ rank_out,
+                                                       uint32_t* __restrict__ node_out,
+                                                       double* __restrict__ weight_out,
+                                                       int64_t out_stride) {
+  const int img = blockIdx.y, tid = threadIdx.x;
+  const int c = tid & (G - 1);
+  const int f = blockIdx.x * (256 / G) + tid / G;
+  const int n = counts ? counts[img] : n_fixed;
+  const bool active = f < n;  // uniform within a group
+  uint64_t d[4] = {0, 0, 0, 0};
+  if (active) {
+    const uint4* q = (const uint4*)(desc + img * desc_stride + (int64_t)f * 32);
+    const uint4 a = q[0], b = q[1];
+    d[0] = a.x | ((uint64_t)a.y << 32);
+    d[1] = a.z | ((uint64_t)a.w << 32);
+    d[2] = b.x | ((uint64_t)b.y << 32);
+    d[3] = b.z | ((uint64_t)b.w << 32);
+  }
+  int cb = V.root_cb, nc = (active && V.n_words > 0) ? V.root_nc : 0;
+  int node = 0, level = 0, word = 0;
+  uint32_t nid = nid_level <= 0 ? 0u : 0xFFFFFFFFu;
+  const int lane = tid & 63, gbase = lane & ~(G - 1);
+  while (__any(nc > 0)) {
+    const bool go = nc > 0;
+    int key = 0x7FFFFFFF;
+    int4 meta = make_int4(0, 0, 0, 0);
+    if (go && c < nc) {
+      const uint4* cd = (const uint4*)(V.cdesc + (int64_t)(cb + c) * 32);
+      const uint4 a = cd[0], b = cd[1];
+      const int dist = __popcll(d[0] ^ (a.x | ((uint64_t)a.y << 32))) +
+                       __popcll(d[1] ^ (a.z | ((uint64_t)a.w << 32))) +
+                       __popcll(d[2] ^ (b.x | ((uint64_t)b.y << 32))) +
+                       __popcll(d[3] ^ (b.z | ((uint64_t)b.w << 32)));
+      meta = V.cmeta[cb + c];
+      key = dist * 64 + c;  // strict `d < best_d` over children in order: lowest c on ties
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) key = min(key, __shfl_xor(key, o));
+    const int src = gbase + (key & 63);
+    const int mx = __shfl(meta.x, src), my = __shfl(meta.y, src), mz = __shfl(meta.z, src),
+              mw = __shfl(meta.w, src);
+    if (go) {
+      ++level;
+      node = mx;
+      cb = my;
+      nc = mz;
+      word = mw;
+      if (level == nid_level) nid = (uint32_t)node;
+    }
+  }
+  if (!active || c != 0) return;
+  const int64_t o = img * out_stride + f;
+  if (V.n_words == 0) {  // transform: if(empty()) return;
+    word_out[o] = 0xFFFFFFFFu;
+    rank_out[o] = 0xFFFFFFFFu;
+    if (node_out) node_out[o] = 0xFFFFFFFFu;
+    weight_out[o] = 0;
+    return;
+  }
+  if (nid == 0xFFFFFFFFu) nid = (uint32_t)node;  // leaf above L - levelsup (header)
+  const double w = V.weight[node];
+  weight_out[o] = w;
+  const bool keep = w > 0;  // `if(w > 0) // not stopped`
+  word_out[o] = keep ? (uint32_t)word : 0xFFFFFFFFu;
+  rank_out[o] = keep ? rank_of_node[nid] : 0xFFFFFFFFu;
+  if (node_out) node_out[o] = keep ? nid : 0xFFFFFFFFu;
+}
+
+// ------------------------------------------------------------------ k_bowvec
+__device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x = __shfl_up(incl, o);
+    if (lane >= o) incl += x;
+  }
+  if (lane == 63) s_tmp[wid] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int w = 0; w < 4; w++) {
+    if (w < wid) base += s_tmp[w];
+    tot += s_tmp[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+// Stable LSD radix sort of the non-stopped features by word id (10-bit digits, as many passes
+// as the largest word id needs), so each word's features stay in index order: the order
+// BowVector::addWeight accumulates them in.  Keys are (word << 32 | feature) pairs; every
+// wave scatters its own contiguous quarter of the current order, behind per-(digit, wave)
+// offsets (digit-major, wave-minor: stable).
+constexpr int kRadixBits = 10, kRadixB = 1 << kRadixBits;
+
+__global__ __launch_bounds__(256) void k_bowvec(int must, int l1, int tf,
+                                                const uint32_t* __restrict__ word_of,
+                                                const double* __restrict__ weight_of,
+                                                int64_t in_stride, const int* __restrict__ counts,
+                                                int n_fixed, int cap,
+                                                uint32_t* __restrict__ out_words,
+                                                double* __restrict__ out_vals, int64_t out_stride,
+                                                int* __restrict__ out_n) {
+  extern __shared__ __align__(16) int sm[];
+  uint64_t* s_a = (uint64_t*)sm;            // [cap] keys (ping)
+  uint64_t* s_b = s_a + cap;                // [cap] keys (pong)
+  int* s_cnt = (int*)(s_b + cap);           // [kRadixB][4] per (digit, wave)
+  __shared__ int s_tmp[4];
+  __shared__ unsigned s_max;
+  __shared__ double s_norm;
+  const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n = counts ? counts[img] : n_fixed;
+  const uint32_t* wo = word_of + img * in_stride;
+  const double* wt = weight_of + img * in_stride;
+  if (tid == 0) s_max = 0;
+  const int per = cap / 256;  // thread t owns indices [t*per, (t+1)*per)
+  uint32_t* s_w = (uint32_t*)s_b;  // words staged in the pong buffer
+  for (int i = tid; i < cap; i += 256) s_w[i] = i < n ? wo[i] : 0xFFFFFFFFu;  // coalesced
+  __syncthreads();
+  int cnt = 0;
+  unsigned mx = 0;
+  for (int i = tid * per; i < (tid + 1) * per; i++) {
+    const uint32_t w = s_w[i];
+    if (w != 0xFFFFFFFFu) {
+      cnt++;
+      mx = max(mx, w);
+    }
+  }
+  atomicMax(&s_max, mx);
+  int m;
+  int pos = block_excl_scan(cnt, s_tmp, &m);  // stable compaction of the kept features
+  for (int i = tid * per; i < (tid + 1) * per; i++) {
+    const uint32_t w = s_w[i];
+    if (w != 0xFFFFFFFFu) s_a[pos++] = ((uint64_t)w << 32) | (uint32_t)i;
+  }
+  __syncthreads();
+  const unsigned wmax = s_max;
+  const int q0 = (int)(((int64_t)m * wid) / 4), q1 = (int)(((int64_t)m * (wid + 1)) / 4);
+  for (int shift = 0; m > 0 && shift < 32 && (shift == 0 || (wmax >> shift) != 0);
+       shift += kRadixBits) {
+    for (int b = tid; b < 4 * kRadixB; b += 256) s_cnt[b] = 0;
+    __syncthreads();
+    for (int j = q0 + lane; j < q1; j += 64)
+      atomicAdd(&s_cnt[4 * ((int)(s_a[j] >> (32 + shift)) & (kRadixB - 1)) + wid], 1);
+    __syncthreads();
+    {  // exclusive scan over (digit, wave): 32 entries per thread
+      constexpr int E = 4 * kRadixB / 256;
+      int c[E], sum = 0;
+#pragma unroll
+      for (int q = 0; q < E; q++) {
+        c[q] = s_cnt[tid * E + q];
+        sum += c[q];
+      }
+      int tot;
+      int base = block_excl_scan(sum, s_tmp, &tot);
+#pragma unroll
+      for (int q = 0; q < E; q++) {
+        s_cnt[tid * E + q] = base;
+        base += c[q];
+      }
+    }
+    __syncthreads();
+    {  // stable scatter of this wave's quarter, 64 keys at a time
+      const uint64_t lt = (1ull << lane) - 1, gt = ~((2ull << lane) - 1);
+      for (int c0 = q0; c0 < q1; c0 += 64) {
+        const int j = c0 + lane;
+        const bool valid = j < q1;
+        const uint64_t key = valid ? s_a[j] : 0;
+        const int dg = (int)(key >> (32 + shift)) & (kRadixB - 1);
+        uint64_t eq = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < kRadixBits; bit++) {
+          const uint64_t mb = __ballot(valid && ((dg >> bit) & 1));
+          eq &= ((dg >> bit) & 1) ? mb : ~mb;
+        }
+        if (valid) {
+          int* slot = &s_cnt[4 * dg + wid];
+          const int base = *slot;
+          s_b[base + __popcll(eq & lt)] = key;
+          if ((eq & gt) == 0) *slot = base + __popcll(eq);  // last lane of the digit
+        }
+      }
+    }
+    __syncthreads();
+    uint64_t* t = s_a;
+    s_a = s_b;
+    s_b = t;
+  }
+  // run starts of equal words (contiguous chunks per thread, stable block scan), kept in
+  // the free pong buffer
+  int* s_pos = (int*)s_b;
+  cnt = 0;
+  for (int j = tid * per; j < (tid + 1) * per; j++)
+    cnt += j < m && (j == 0 || (s_a[j] >> 32) != (s_a[j - 1] >> 32));
+  int nu;
+  pos = block_excl_scan(cnt, s_tmp, &nu);
+  for (int j = tid * per; j < (tid + 1) * per; j++)
+    if (j < m && (j == 0 || (s_a[j] >> 32) != (s_a[j - 1] >> 32))) s_pos[pos++] = j;
+  if (tid == 0) s_pos[nu] = m;
+  __syncthreads();
+  uint32_t* ow = out_words + img * out_stride;
+  double* ov = out_vals + img * out_stride;
+  for (int o = tid; o < nu; o += 256) {
+    const int a = s_pos[o], b = s_pos[o + 1];
+    double v = wt[(uint32_t)s_a[a]];  // insert(value_type(id, w)) of the first occurrence
+    if (tf)
+      for (int j = a + 1; j < b; j++) v += wt[(uint32_t)s_a[j]];  // addWeight, feature order
+    if (tf && !must) v /= (double)nu;  // TemplatedVocabulary.h:1165-1172
+    ow[o] = (uint32_t)(s_a[a] >> 32);
+    ov[o] = v;
+  }
+  if (tid == 0) out_n[img] = nu;
+  if (!must) return;
+  __syncthreads();
+  // the values back into LDS (over the pong keys) for the ordered normalisation pass
+  double* s_val = (double*)s_b;
+  for (int o = tid; o < nu; o += 256) s_val[o] = ov[o];
+  __syncthreads();
+  if (tid == 0) {  // BowVector::normalize: one ordered pass over the words
+    // (the adds stay in word order; LDS reads are batched 8 at a time)
+    double norm = 0.0;
+    int o = 0;
+    if (l1) {
+      for (; o + 8 <= nu; o += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) norm += fabs(v[j]);
+      }
+      for (; o < nu; o++) norm += fabs(s_val[o]);
+    } else {
+      // built -O3 -march=native (Thirdparty/DBoW2/CMakeLists.txt): `norm += v * v` contracts
+      for (; o + 8 <= nu; o += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) norm = fma(v[j], v[j], norm);
+      }
+      for (; o < nu; o++) norm = fma(s_val[o], s_val[o], norm);
+      norm = sqrt(norm);
+    }
+    s_norm = norm;
+  }
+  __syncthreads();
+  const double norm = s_norm;
+  if (norm > 0.0)
+    for (int o = tid; o < nu; o += 256) ov[o] = s_val[o] / norm;
+}
+
+int launch_voc_transform(const VocView& V, int nid_level, const uint32_t* d_rank_of_node,
+                         const uint8_t* d_desc, int64_t desc_stride_img, const int* d_counts,
+                         int n_fixed, int max_n, uint32_t* d_word_of, uint32_t* d_rank_of,
+                         uint32_t* d_node_of, double* d_weight_of, int64_t out_stride_img,
+                         int nimg, hipStream_t s) {
+  if (max_n <= 0 || nimg <= 0) return ORBX_OK;
+  if (V.k <= 16) {
+    hipLaunchKernelGGL(k_voc_transform<16>, dim3((max_n + 15) / 16, nimg), dim3(256), 0, s, V,
+                       nid_level, d_rank_of_node, d_desc, desc_stride_img, d_counts, n_fixed,
+                       d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img);
+  } else if (V.k <= 32) {
+    hipLaunchKernelGGL(k_voc_transform<32>, dim3((max_n + 7) / 8, nimg), dim3(256), 0, s, V,
+                       nid_level, d_rank_of_node, d_desc, desc_stride_img, d_counts, n_fixed,
+                       d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img);
+  } else {
+    return ORBX_EUNSUPPORTED;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_voc_transform");
+}
+
+int bowvec_cap(int max_n) {
+  int cap = 256;
+  while (cap < max_n) cap <<= 1;
+  return cap;
+}
+
+int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
+                  const double* d_weight_of, int64_t in_stride, const int* d_counts, int n_fixed,
+                  int max_n, uint32_t* d_words, double* d_values, int64_t out_stride,
+                  int* d_nwords, int nimg, hipStream_t s) {
+  if (nimg <= 0) return ORBX_OK;
+  const int cap = bowvec_cap(std::max(max_n, 1));
+  const size_t smem = 16 * (size_t)cap + 16 * kRadixB;
+  if (cap > 8192) return ORBX_EUNSUPPORTED;
+  const int must = scoring != ORBX_SCORE_DOT_PRODUCT;
+  const int l1 = scoring != ORBX_SCORE_L2;
+  const int tf = weighting == ORBX_WEIGHT_TF_IDF || weighting == ORBX_WEIGHT_TF;
+  if (smem > 64 * 1024) {  // more than the default dynamic LDS limit (8192 features: 104 KB)
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+      attr = hipFuncSetAttribute((const void*)k_bowvec, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 16 * 8192 + 16 * kRadixB);
+    });
+    if (attr != hipSuccess) return report_hip(attr, "hipFuncSetAttribute(k_bowvec)");
+  }
+  hipLaunchKernelGGL(k_bowvec, dim3(nimg), dim3(256), smem, s, must, l1, tf, d_word_of,
+                     d_weight_of, in_stride, d_counts, n_fixed, cap, d_words, d_values,
+                     out_stride, d_nwords);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_bowvec");
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+
+template <class T>
+int dalloc(T** p, size_t count) {
+  if (count == 0) count = 1;
+  if (hipMalloc((void**)p, count * sizeof(T)) != hipSuccess) return ORBX_ENOMEM;
+  return ORBX_OK;
+}
+
+// Build the tree and upload it (node i of the arrays is node id i + 1).
+int build_vocabulary(orbx_vocabulary* V, int n, const int32_t* parent, const uint8_t* is_leaf,
+                     const uint8_t* desc, const double* weight) {
+  const int N = n + 1;
+  V->n_nodes = N;
+  V->parent.assign(N, 0);
+  V->depth.assign(N, 0);
+  V->word_of_node.assign(N, 0);
+  std::vector<std::vector<uint32_t>> children(N);
+  std::vector<double> w(N, 0.0);  // root: Node(): weight(0)
+  std::vector<int> words;
+  for (int i = 0; i < n; i++) {
+    const int nid = i + 1, pid = parent[i];
+    if (pid < 0 || pid >= nid) return ORBX_EINVAL;  // m_nodes[pid] must already exist
+    V->parent[nid] = pid;
+    V->depth[nid] = V->depth[pid] + 1;
+    children[pid].push_back((uint32_t)nid);
+    w[nid] = weight[i];
+    if (is_leaf[i]) {
+      V->word_of_node[nid] = (int)words.size();
+      words.push_back(nid);
+    }
+  }
+  V->n_words = (int)words.size();
+  // per-parent contiguous child records
+  V->child_begin.assign(N, 0);
+  V->nchild.assign(N, 0);
+  V->child_ids.clear();
+  V->child_ids.reserve(n);
+  for (int p = 0; p < N; p++) {
+    V->child_begin[p] = (int)V->child_ids.size();
+    V->nchild[p] = (int)children[p].size();
+    if (V->nchild[p] > 32) return ORBX_EUNSUPPORTED;  // more children than a lane group
+    V->child_ids.insert(V->child_ids.end(), children[p].begin(), children[p].end());
+  }
+  std::vector<uint8_t> cdesc((size_t)std::max(n, 1) * 32);
+  std::vector<int4> cmeta(std::max(n, 1));
+  for (size_t j = 0; j < V->child_ids.size(); j++) {
+    const uint32_t c = V->child_ids[j];
+    memcpy(&cdesc[j * 32], desc + (size_t)(c - 1) * 32, 32);
+    cmeta[j] = make_int4((int)c, V->child_begin[c], V->nchild[c], V->word_of_node[c]);
+  }
+  std::vector<double> ww(std::max(V->n_words, 1), 0.0);
+  for (int k = 0; k < V->n_words; k++) ww[k] = w[words[k]];
+  if (hipSetDevice(V->device) != hipSuccess) return ORBX_EDEVICE;
+  if (dalloc(&V->d_cdesc, cdesc.size()) || dalloc(&V->d_cmeta, cmeta.size()) ||
+      dalloc(&V->d_weight, (size_t)N) || dalloc(&V->d_word_weight, ww.size()))
+    return ORBX_ENOMEM;
+  if (hipMemcpy(V->d_cdesc, cdesc.data(), cdesc.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(V->d_cmeta, cmeta.data(), cmeta.size() * sizeof(int4), hipMemcpyHostToDevice) !=
+          hipSuccess ||
+      hipMemcpy(V->d_weight, w.data(), (size_t)N * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(V->d_word_weight, ww.data(), ww.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return ORBX_EDEVICE;
+  return ORBX_OK;
+}
+
+// strtol-based "int int 32*int double" line parser (std::stringstream >> semantics for
+// well-formed lines; FORB::fromString keeps a byte whose token fails to parse as 0 here,
+// the cv::Mat byte it leaves untouched is indeterminate in the reference)
+bool parse_node_line(const char* s, int* pid, int* leaf, uint8_t* d, double* w) {
+  char* e;
+  errno = 0;
+  long v = strtol(s, &e, 10);
+  if (e == s) return false;
+  *pid = (int)v;
+  s = e;
+  v = strtol(s, &e, 10);
+  *leaf = e == s ? 0 : (int)v;
+  s = e;
+  for (int i = 0; i < 32; i++) {
+    v = strtol(s, &e, 10);
+    d[i] = e == s ? 0 : (uint8_t)v;
+    s = e;
+  }
+  const double x = strtod(s, &e);
+  *w = e == s ? 0.0 : x;
+  return true;
+}
+
+}  // namespace
+
+int vocab_view(const orbx_vocabulary* V, VocView* v, int* device) {
+  if (!V || !v) return ORBX_EINVAL;
+  v->cdesc = V->d_cdesc;
+  v->cmeta = V->d_cmeta;
+  v->weight = V->d_weight;
+  v->word_weight = V->d_word_weight;
+  v->root_cb = V->child_begin.empty() ? 0 : V->child_begin[0];
+  v->root_nc = V->nchild.empty() ? 0 : V->nchild[0];
+  v->n_words = V->n_words;
+  v->k = 0;
+  for (int c : V->nchild) v->k = std::max(v->k, c);
+  if (device) *device = V->device;
+  return ORBX_OK;
+}
+
+// FeatureVector keys for a levelsup: the nodes at depth L - levelsup, plus the leaves above
+// it (where the descent stops early), ranked by ascending id.
+int vocab_ranks(const orbx_vocabulary* Vc, int levelsup, const VocRanks** out) {
+  orbx_vocabulary* V = const_cast<orbx_vocabulary*>(Vc);
+  std::lock_guard<std::mutex> lk(V->m);
+  for (auto* r : V->ranks)
+    if (r->levelsup == levelsup) {
+      *out = r;
+      return ORBX_OK;
+    }
+  const int nid_level = V->L - levelsup;
+  std::vector<uint32_t> ids;
+  std::vector<uint32_t> rank(V->n_nodes, 0xFFFFFFFFu);
+  if (nid_level <= 0) {
+    ids.push_back(0);
+  } else {
+    for (int i = 1; i < V->n_nodes; i++)
+      if (V->depth[i] == nid_level || (V->depth[i] < nid_level && V->nchild[i] == 0))
+        ids.push_back((uint32_t)i);
+  }
+  for (size_t b = 0; b < ids.size(); b++) rank[ids[b]] = (uint32_t)b;
+  VocRanks* r = new (std::nothrow) VocRanks();
+  if (!r) return ORBX_ENOMEM;
+  r->levelsup = levelsup;
+  r->nb = (int)ids.size();
+  if (hipSetDevice(V->device) != hipSuccess) {
+    delete r;
+    return ORBX_EDEVICE;
+  }
+  if (dalloc(&r->d_rank_of_node, rank.size()) || dalloc(&r->d_rank_ids, ids.size()) ||
+      hipMemcpy(r->d_rank_of_node, rank.data(), rank.size() * 4, hipMemcpyHostToDevice) !=
+          hipSuccess ||
+      (ids.size() &&
+       hipMemcpy(r->d_rank_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice) !=
+           hipSuccess)) {
+    if (r->d_rank_of_node) (void)hipFree(r->d_rank_of_node);
+    if (r->d_rank_ids) (void)hipFree(r->d_rank_ids);
+    delete r;
+    return ORBX_ENOMEM;
+  }
+  V->ranks.push_back(r);
+  *out = r;
+  return ORBX_OK;
+}
+
+}  // namespace orbx
+
+using namespace orbx;
+
+extern "C" {
+
+int orbx_vocabulary_create(int32_t k, int32_t L, int32_t scoring, int32_t weighting,
+                           int32_t n_nodes, const int32_t* parent, const uint8_t* is_leaf,
+                           const uint8_t* desc, const double* weight, int32_t hip_device,
+                           orbx_vocabulary** out) {
+  if (!out) return ORBX_EINVAL;
+  *out = nullptr;
+  // the loader's header check (TemplatedVocabulary.h:1360-1364)
+  if (k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 ||
+      weighting > 3 || n_nodes < 0)
+    return ORBX_EINVAL;
+  if (n_nodes > 0 && (!parent || !is_leaf || !desc || !weight)) return ORBX_EINVAL;
+  orbx_vocabulary* V = new (std::nothrow) orbx_vocabulary();
+  if (!V) return ORBX_ENOMEM;
+  V->device = hip_device;
+  V->k = k;
+  V->L = L;
+  V->scoring = scoring;
+  V->weighting = weighting;
+  const int rc = build_vocabulary(V, n_nodes, parent, is_leaf, desc, weight);
+  if (rc) {
+    delete V;
+    return rc;
+  }
+  *out = V;
+  return ORBX_OK;
+}
+
+int orbx_vocabulary_load_text(const char* path, int32_t hip_device, orbx_vocabulary** out) {
+  if (!path || !out) return ORBX_EINVAL;
+  *out = nullptr;
+  FILE* f = fopen(path, "r");
+  if (!f) return ORBX_EINVAL;
+  std::string line;
+  char buf[4096];
+  auto getline = [&](std::string& s) -> bool {
+    s.clear();
+    while (fgets(buf, sizeof(buf), f)) {
+      s += buf;
+      if (!s.empty() && s.back() == '\n') return true;
+    }
+    return !s.empty();
+  };
+  int k = -1, L = -1, n1 = -1, n2 = -1;
+  if (!getline(line) || sscanf(line.c_str(), "%d %d %d %d", &k, &L, &n1, &n2) != 4) {
+    fclose(f);
+    return ORBX_EINVAL;
+  }
+  if (k < 0 || k > 20 || L < 1 || L > 10 || n1 < 0 || n1 > 5 || n2 < 0 || n2 > 3) {
+    fclose(f);
+    return ORBX_EINVAL;
+  }
+  std::vector<int32_t> parent;
+  std::vector<uint8_t> leaf, desc;
+  std::vector<double> weight;
+  while (getline(line)) {
+    if (line.find_first_not_of(" \t\r\n") == std::string::npos) continue;
+    int pid, lf;
+    uint8_t d[32];
+    double w;
+    if (!parse_node_line(line.c_str(), &pid, &lf, d, &w)) {
+      fclose(f);
+      return ORBX_EINVAL;
+    }
+    parent.push_back(pid);
+    leaf.push_back(lf > 0);
+    desc.insert(desc.end(), d, d + 32);
+    weight.push_back(w);
+  }
+  fclose(f);
+  return orbx_vocabulary_create(k, L, n1, n2, (int32_t)parent.size(), parent.data(),
+                                leaf.data(), desc.data(), weight.data(), hip_device, out);
+}
+
+int orbx_vocabulary_destroy(orbx_vocabulary* voc) {
+  delete voc;
+  return ORBX_OK;
+}
+
+int orbx_vocabulary_info(const orbx_vocabulary* V, int32_t* k, int32_t* L, int32_t* scoring,
+                         int32_t* weighting, int32_t* n_nodes, int32_t* n_words) {
+  if (!V) return ORBX_EINVAL;
+  if (k) *k = V->k;
+  if (L) *L = V->L;
+  if (scoring) *scoring = V->scoring;
+  if (weighting) *weighting = V->weighting;
+  if (n_nodes) *n_nodes = V->n_nodes;
+  if (n_words) *n_words = V->n_words;
+  return ORBX_OK;
+}
+
+int orbx_vocabulary_transform(const orbx_vocabulary* V, const uint8_t* desc, int32_t n,
+                              int32_t levelsup, uint32_t* word_of, uint32_t* node_of,
+                              uint32_t* bow_words, double* bow_values, int32_t* bow_n,
+                              uint32_t* fv_node_ids, int32_t* fv_offsets, int32_t* fv_feats,
+                              int32_t* fv_n) {
+  if (!V || n < 0 || (n && !desc) || !bow_words || !bow_values || !bow_n || !fv_node_ids ||
+      !fv_offsets || !fv_feats || !fv_n)
+    return ORBX_EINVAL;
+  if (n > 8192) return ORBX_EUNSUPPORTED;
+  const VocRanks* R = nullptr;
+  int rc = vocab_ranks(V, levelsup, &R);
+  if (rc) return rc;
+  if (R->nb > 8192) return ORBX_EUNSUPPORTED;  // k_csr buckets live in LDS
+  VocView view;
+  vocab_view(V, &view, nullptr);
+  const int nn = std::max(n, 1);
+  Stager st;
+  const size_t od = st.add(desc, (size_t)n * 32);
+  const size_t upload = st.host.size();
+  const size_t ow = st.add(nullptr, (size_t)nn * 4), orank = st.add(nullptr, (size_t)nn * 4),
+               onode = st.add(nullptr, (size_t)nn * 4),
+               owt = st.add(nullptr, (size_t)nn * 8), obw = st.add(nullptr, (size_t)nn * 4),
+               obv = st.add(nullptr, (size_t)nn * 8), obn = st.add(nullptr, 4),
+               ofi = st.add(nullptr, (size_t)R->nb * 4),
+               ofo = st.add(nullptr, ((size_t)R->nb + 1) * 4), off = st.add(nullptr, (size_t)nn * 4),
+               ofn = st.add(nullptr, 4);
+  rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  if (upload) ORBX_HIP(hipMemcpyAsync(base, st.host.data(), upload, hipMemcpyHostToDevice, s));
+  if (n > 0) {
+    rc = launch_voc_transform(view, V->L - levelsup, R->d_rank_of_node, dptr<uint8_t>(base, od),
+                              0, nullptr, n, n, dptr<uint32_t>(base, ow),
+                              dptr<uint32_t>(base, orank), dptr<uint32_t>(base, onode),
+                              dptr<double>(base, owt), 0, 1, s);
+    if (rc) return rc;
+  }
+  rc = launch_bowvec(V->scoring, V->weighting, dptr<uint32_t>(base, ow), dptr<double>(base, owt),
+                     0, nullptr, n, n, dptr<uint32_t>(base, obw), dptr<double>(base, obv), 0,
+                     dptr<int>(base, obn), 1, s);
+  if (rc) return rc;
+  rc = launch_csr(dptr<uint32_t>(base, orank), 0, nullptr, n, 0, std::max(R->nb, 1),
+                  R->d_rank_ids, dptr<uint32_t>(base, ofi), dptr<int>(base, ofo),
+                  dptr<int>(base, off), 0, dptr<int>(base, ofn), 1, s);
+  if (rc) return rc;
+  std::vector<char> back(st.host.size() - ow);
+  ORBX_HIP(hipMemcpyAsync(back.data(), base + ow, back.size(), hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  auto at = [&](size_t o) { return back.data() + (o - ow); };
+  const int nb = *(const int*)at(obn), nf = *(const int*)at(ofn);
+  memcpy(bow_words, at(obw), (size_t)nb * 4);
+  memcpy(bow_values, at(obv), (size_t)nb * 8);
+  *bow_n = nb;
+  memcpy(fv_node_ids, at(ofi), (size_t)nf * 4);
+  memcpy(fv_offsets, at(ofo), ((size_t)nf + 1) * 4);
+  const int nfeat = ((const int*)at(ofo))[nf];
+  memcpy(fv_feats, at(off), (size_t)nfeat * 4);
+  *fv_n = nf;
+  if (word_of && n) memcpy(word_of, at(ow), (size_t)n * 4);
+  if (node_of && n) memcpy(node_of, at(onode), (size_t)n * 4);
+  return ORBX_OK;
+}
+
+}  // extern "C"

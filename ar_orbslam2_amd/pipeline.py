@@ -1,7 +1,7 @@
 """FramePipeline — the batched, device-resident "ORB extract + match" unit of work.
 
 Wraps orbx_frames (include/orbx.h): per batch of n frames already in HBM it runs the
-extractor, the vocabulary node ids, the FeatureVector build, SearchByBoW(prev-as-KF, cur) and
+extractor, Frame::ComputeBoW (vocabulary descent, BowVector, FeatureVector), SearchByBoW(prev-as-KF, cur) and
 SearchForTriangulation(prev-as-KF, cur-as-KF) (SURVEY §8d unit of work), entirely on the GPU
 stream of the pipeline.  Frame f is matched against frame (f-1) mod n of the same batch.
 """
@@ -28,7 +28,7 @@ def fundamental_from_pose(K=TUM1_K, t=(0.10, 0.02, 0.05)):
 
 class FramePipeline:
     def __init__(self, w, h, max_batch, vocabulary, nfeatures=1000, scale_factor=1.2, nlevels=8,
-                 ini_th_fast=20, min_th_fast=7, device=0):
+                 ini_th_fast=20, min_th_fast=7, device=0, levelsup=4):
         self.w, self.h, self.max_batch = int(w), int(h), int(max_batch)
         self.params = _ffi.Params(int(nfeatures), float(scale_factor), int(nlevels),
                                   int(ini_th_fast), int(min_th_fast))
@@ -36,10 +36,8 @@ class FramePipeline:
         self._h = C.c_void_p()
         check("orbx_frames_create",
               lib().orbx_frames_create(C.byref(self.params), C.c_int32(self.w), C.c_int32(self.h),
-                                       C.c_int32(self.max_batch), ptr(vocabulary.node_desc),
-                                       C.c_int32(vocabulary.k), C.c_int32(vocabulary.L),
-                                       C.c_int32(vocabulary.levelsup), C.c_int(device),
-                                       C.byref(self._h)))
+                                       C.c_int32(self.max_batch), vocabulary.handle,
+                                       C.c_int32(levelsup), C.c_int(device), C.byref(self._h)))
         cap = C.c_int32()
         check("orbx_frames_capacity", lib().orbx_frames_capacity(self._h, C.byref(cap)))
         self.kp_cap = cap.value
@@ -105,6 +103,12 @@ class FramePipeline:
         names = ["kps", "desc", "counts", "node_of", "bow_match", "tri_pairs"]
         ptrs = [C.c_void_p() for _ in names]
         check("orbx_frames_outputs", lib().orbx_frames_outputs(self._h, *[C.byref(p) for p in ptrs]))
+        return {k: p.value for k, p in zip(names, ptrs)}
+
+    def bow_outputs(self):
+        names = ["bow_words", "bow_values", "bow_n", "word_of"]
+        ptrs = [C.c_void_p() for _ in names]
+        check("orbx_frames_bow", lib().orbx_frames_bow(self._h, *[C.byref(p) for p in ptrs]))
         return {k: p.value for k, p in zip(names, ptrs)}
 
     def stream(self):

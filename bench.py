@@ -3,9 +3,10 @@
 
 One step = one batch of `--batch` synthetic 640x480 frames (BASELINE.json configs[1], TUM
 fr1/xyz mono geometry, 1000 features) already resident in HBM, pushed through the whole
-device pipeline: ORBextractor (pyramid, FAST cells, octree, orientation, rBRIEF), vocabulary
-node ids + FeatureVector, SearchByBoW(prev-as-KF, cur) and SearchForTriangulation(prev-as-KF,
-cur-as-KF) (SURVEY §8d unit of work).  Multi-GPU: one process per GPU, each rank processes its
+device pipeline: ORBextractor (pyramid, FAST cells, octree, orientation, rBRIEF),
+Frame::ComputeBoW (full DBoW2 descent of the seeded k=10, L=6 vocabulary: word ids, BowVector,
+FeatureVector), SearchByBoW(prev-as-KF, cur) and SearchForTriangulation(prev-as-KF, cur-as-KF)
+(SURVEY §8d unit of work).  Multi-GPU: one process per GPU, each rank processes its
 own camera stream (weak scaling, no data-path collective; RCCL only carries the barrier and
 the max-over-ranks time).
 
@@ -54,7 +55,8 @@ def algorithmic_bytes(levels, n_kp, n_img):
         "k_fast_tile": sum(P) * n_img,                          # every level pixel read once
         "k_fast_compact": sum(P) * n_img / 4,                   # 2 NMS bits per pixel
         "k_describe": 60 * n_kp,
-        "k_featvec": 36 * n_kp,
+        "k_voc_transform": 52 * n_kp,                          # desc in; word, rank, node, weight out
+        "k_bowvec": 24 * n_kp,
         "total_per_frame": P[0] + sum(per_resize) / n_img + 3 * sum(P) + 60 * n_kp / n_img,
     }
 
@@ -89,19 +91,14 @@ def cpu_baseline(cfg, seconds):
     w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
     p = O.params(nf)
     t = O.tables(p, w, h)
-    rng = np.random.default_rng(42)
-    voc = rng.integers(0, 256, (111, 32), dtype=np.uint8)
+    from ar_orbslam2_amd.vocabulary import complete_tree
+    ndesc = sum(10 ** l for l in range(7))
+    voc = O.Vocabulary.from_nodes(10, 6, 0, 0, *complete_tree(
+        10, 6, np.random.default_rng(42).integers(0, 256, (ndesc, 32), dtype=np.uint8)))
     F = fundamental_from_pose()
     ex, ey = O.epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
     base = synth.canvas(w, h, 0)
     imgs = [synth.frame(w, h, i, 0, base) for i in range(64)]
-
-    def fv(nodes):
-        order = np.argsort(nodes, kind="stable").astype(np.int32)
-        ids, counts = np.unique(nodes, return_counts=True)
-        offs = np.zeros(len(ids) + 1, np.int32)
-        np.cumsum(counts, out=offs[1:])
-        return ids.astype(np.uint32), offs, order
 
     prev = None
     n = 0
@@ -109,9 +106,10 @@ def cpu_baseline(cfg, seconds):
     while True:
         img = imgs[n % len(imgs)]
         kps, desc = O.extract(img, p)
-        nodes = O.feature_vector(voc, 10, 6, 4, desc)
+        b = voc.transform(desc, 4)  # Frame::ComputeBoW: BowVector + FeatureVector
         r = np.random.default_rng(n)
-        cur = dict(desc=desc, angle=kps["angle"], keys=kps, fv=fv(nodes),
+        cur = dict(desc=desc, angle=kps["angle"], keys=kps,
+                   fv=(b["fv_ids"], b["fv_off"], b["fv_feats"]),
                    valid=(r.random(len(kps)) < 0.6).astype(np.uint8),
                    has_mp=(r.random(len(kps)) < 0.4).astype(np.uint8),
                    scale_factors=t["scale"], level_sigma2=t["sigma2"])
@@ -126,7 +124,7 @@ def cpu_baseline(cfg, seconds):
     return dict(value=n / el, unit="frames/s", cores=1, kind="port",
                 sample=f"{n} consecutive {w}x{h} synthetic frames, CPU oracle (oracle/orb_oracle.cc, "
                        f"g++ -O3 -march=x86-64-v3 -ffp-contract=off), 1 thread, extract + "
-                       f"SearchByBoW + SearchForTriangulation per frame, {el:.1f} s on "
+                       f"ComputeBoW + SearchByBoW + SearchForTriangulation per frame, {el:.1f} s on "
                        f"{platform.processor() or platform.machine()}")
 
 

@@ -14,8 +14,10 @@
  *   orbx_search_by_bow_kf_kf ORBmatcher::SearchByBoW(KF*,KF*)  ORB_SLAM2/src/ORBmatcher.cc:525-658
  *   orbx_search_for_triangulation
  *                           ORBmatcher::SearchForTriangulation ORB_SLAM2/src/ORBmatcher.cc:660-826
- *   orbx_feature_vector     TemplatedVocabulary::transform(levelsup) node ids
- *                           ORB_SLAM2/Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1127-1259
+ *   orbx_vocabulary_*       DBoW2 TemplatedVocabulary<FORB>: loadFromTextFile and
+ *                           transform(features, BowVector&, FeatureVector&, levelsup)
+ *                           ORB_SLAM2/Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1127-1259,
+ *                           1338-1424 (called by Frame::ComputeBoW, ORB_SLAM2/src/Frame.cc:400-407)
  *
  * Error convention: every function returns 0 on success or a negative ORBX_E* code; nothing
  * throws across the ABI.  The reference has no error returns (asserts are compiled out,
@@ -153,16 +155,58 @@ int orbx_plan_profile(orbx_plan* plan, int32_t enable);
 int orbx_plan_profile_read(orbx_plan* plan, int32_t cap, char (*names)[32], double* total_ms,
                            int64_t* launches, int32_t* n_stages);
 
+/* ------------------------------------------------------------------ vocabulary
+ * DBoW2 TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary, ORB_SLAM2/include/
+ * ORBVocabulary.h), device resident.  Node ids follow DBoW2's file order (root 0, the n
+ * nodes given are ids 1..n); word ids number the nodes flagged leaf in that order
+ * (TemplatedVocabulary.h:1402-1416). */
+typedef struct orbx_vocabulary orbx_vocabulary;
+enum { ORBX_WEIGHT_TF_IDF = 0, ORBX_WEIGHT_TF = 1, ORBX_WEIGHT_IDF = 2, ORBX_WEIGHT_BINARY = 3 };
+enum {
+  ORBX_SCORE_L1 = 0, ORBX_SCORE_L2 = 1, ORBX_SCORE_CHI_SQUARE = 2, ORBX_SCORE_KL = 3,
+  ORBX_SCORE_BHATTACHARYYA = 4, ORBX_SCORE_DOT_PRODUCT = 5
+};
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424): header
+ * "k L scoring weighting", then one "parent isLeaf d0 .. d31 weight" line per node.  Blank
+ * lines are skipped (the reference's trailing-newline phantom node is not created: its
+ * descriptor is indeterminate).  ORBX_EINVAL on a header the reference rejects or a parent id
+ * that is not an earlier node. */
+int orbx_vocabulary_load_text(const char* path, int32_t hip_device, orbx_vocabulary** out);
+/* The same tree from arrays (node i of the arrays is node id i+1). */
+int orbx_vocabulary_create(int32_t k, int32_t L, int32_t scoring, int32_t weighting,
+                           int32_t n_nodes, const int32_t* parent, const uint8_t* is_leaf,
+                           const uint8_t* desc, const double* weight, int32_t hip_device,
+                           orbx_vocabulary** out);
+int orbx_vocabulary_destroy(orbx_vocabulary* voc);
+/* n_nodes counts the root. */
+int orbx_vocabulary_info(const orbx_vocabulary* voc, int32_t* k, int32_t* L, int32_t* scoring,
+                         int32_t* weighting, int32_t* n_nodes, int32_t* n_words);
+/* TemplatedVocabulary::transform(features, BowVector& v, FeatureVector& fv, levelsup)
+ * (TemplatedVocabulary.h:1127-1198) on n host descriptors.  Outputs (host, capacity n each):
+ *   word_of[i], node_of[i]  word id / FeatureVector node id of feature i, 0xFFFFFFFF when the
+ *                           word's weight is <= 0 (stopped; nullable outputs)
+ *   bow_words/bow_values    BowVector in word-id order (values f64, weighted and normalised as
+ *                           the vocabulary's scoring/weighting prescribe), *bow_n entries
+ *   fv_node_ids/fv_offsets/fv_feats  FeatureVector in node-id order (CSR; offsets n+1),
+ *                           *fv_n nodes.
+ * When the descent reaches a leaf above level L - levelsup the FeatureVector node is that
+ * leaf (the reference leaves it uninitialised). */
+int orbx_vocabulary_transform(const orbx_vocabulary* voc, const uint8_t* desc, int32_t n,
+                              int32_t levelsup, uint32_t* word_of, uint32_t* node_of,
+                              uint32_t* bow_words, double* bow_values, int32_t* bow_n,
+                              uint32_t* fv_node_ids, int32_t* fv_offsets, int32_t* fv_feats,
+                              int32_t* fv_n);
+
 /* ------------------------------------------------------------------ device frame pipeline
  * The whole per-frame unit of work of the benchmark on device-resident frames:
- * extract -> vocabulary node ids -> FeatureVector (CSR) -> SearchByBoW(prev-as-KF, cur) ->
- * SearchForTriangulation(prev-as-KF, cur-as-KF).  Frame f of a batch is matched against frame
- * (f-1) mod n.  `voc_desc` holds the breadth-first node descriptors of a complete k-ary tree
- * down to level L - levelsup (see orbx_feature_vector). */
+ * extract -> Frame::ComputeBoW (vocabulary transform: word ids, BowVector, FeatureVector) ->
+ * SearchByBoW(prev-as-KF, cur) -> SearchForTriangulation(prev-as-KF, cur-as-KF).  Frame f of
+ * a batch is matched against frame (f-1) mod n.  `voc` must outlive the pipeline and live on
+ * the same device. */
 typedef struct orbx_frames orbx_frames;
 int orbx_frames_create(const orbx_params* params, int32_t w, int32_t h, int32_t max_batch,
-                       const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
-                       int hip_device, orbx_frames** out);
+                       const orbx_vocabulary* voc, int32_t levelsup, int hip_device,
+                       orbx_frames** out);
 int orbx_frames_destroy(orbx_frames* fr);
 int orbx_frames_capacity(const orbx_frames* fr, int32_t* kp_cap);
 /* Host masks [max_batch][kp_cap]: valid = KF-side usable MapPoint for SearchByBoW, has_mp =
@@ -177,12 +221,16 @@ int orbx_frames_sync(orbx_frames* fr);
 /* Host copies of the per-frame counts of the last run (synchronises). */
 int orbx_frames_results(orbx_frames* fr, int32_t n, int32_t* kp_counts, int32_t* bow_matches,
                         int32_t* tri_matches, int32_t* error);
-/* Device pointers: kps/desc [max_batch][kp_cap], counts [max_batch], node ids
- * [max_batch][kp_cap], bow match [max_batch][kp_cap] (frame-indexed, value = KF index),
- * triangulation pairs [max_batch][kp_cap][2]. */
+/* Device pointers: kps/desc [max_batch][kp_cap], counts [max_batch], FeatureVector node id
+ * per feature [max_batch][kp_cap] (0xFFFFFFFF = stopped word), bow match [max_batch][kp_cap]
+ * (frame-indexed, value = KF index), triangulation pairs [max_batch][kp_cap][2]. */
 int orbx_frames_outputs(orbx_frames* fr, orbx_keypoint** d_kps, uint8_t** d_desc,
                         int32_t** d_counts, uint32_t** d_node_of, int32_t** d_bow_match,
                         int32_t** d_tri_pairs);
+/* Device pointers of the BowVectors: word ids / values [max_batch][kp_cap], entries per frame
+ * [max_batch]; word id per feature [max_batch][kp_cap] (0xFFFFFFFF = stopped). */
+int orbx_frames_bow(orbx_frames* fr, uint32_t** d_bow_words, double** d_bow_values,
+                    int32_t** d_bow_n, uint32_t** d_word_of);
 void* orbx_frames_stream(orbx_frames* fr);
 int orbx_frames_profile(orbx_frames* fr, int32_t enable);
 int orbx_frames_profile_read(orbx_frames* fr, int32_t cap, char (*names)[32], double* total_ms,
@@ -212,15 +260,6 @@ int orbx_search_for_triangulation(const orbx_tri_side* kf1, const orbx_tri_side*
 /* Epipole exactly as ORBmatcher.cc:667-673 evaluates it (C2 = R2w*Cw + t2w, f32). */
 int orbx_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx, float fy,
                  float cx, float cy, float* ex, float* ey);
-
-/* ------------------------------------------------------------------ vocabulary
- * DBoW2 node ids for the matchers: per feature, the greedy Hamming descent of
- * TemplatedVocabulary::transform (TemplatedVocabulary.h:1218-1259) stopped at level
- * L - levelsup.  The tree is given as a complete k-ary layout: level-l nodes stored
- * contiguously, children of node j of level l at [j*k, j*k+k) of level l+1; node ids follow
- * DBoW2's file order (root 0, then breadth-first). */
-int orbx_feature_vector(const uint8_t* voc_desc, int32_t k, int32_t L, int32_t levelsup,
-                        const uint8_t* desc, int32_t n, uint32_t* node_of_feature);
 
 #ifdef __cplusplus
 }

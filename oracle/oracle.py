@@ -289,3 +289,61 @@ def feature_vector(voc_desc, k, L, levelsup, desc):
     lib().oracle_feature_vector(_p(voc_desc), C.c_int(k), C.c_int(L), C.c_int(levelsup), _p(desc),
                                 C.c_int(desc.shape[0]), _p(out))
     return out
+
+
+# ---------------------------------------------------------------- DBoW2 (dbow2_oracle.cc)
+class Vocabulary:
+    """TemplatedVocabulary<FORB> restatement: nodes 1..n in file order (root 0 implicit)."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise ValueError("oracle vocabulary rejected")
+        self._h = C.c_void_p(handle)
+
+    @staticmethod
+    def from_nodes(k, L, scoring, weighting, parent, is_leaf, desc, weight):
+        parent = np.ascontiguousarray(parent, np.int32)
+        is_leaf = np.ascontiguousarray(is_leaf, np.uint8)
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        weight = np.ascontiguousarray(weight, np.float64)
+        L_ = lib()
+        L_.oracle_voc_create.restype = C.c_void_p
+        h = L_.oracle_voc_create(C.c_int(k), C.c_int(L), C.c_int(scoring), C.c_int(weighting),
+                                 C.c_int(len(parent)), _p(parent), _p(is_leaf), _p(desc),
+                                 _p(weight))
+        return Vocabulary(h)
+
+    @staticmethod
+    def load_text(path):
+        L_ = lib()
+        L_.oracle_voc_load_text.restype = C.c_void_p
+        return Vocabulary(L_.oracle_voc_load_text(str(path).encode()))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oracle_voc_destroy(self._h)
+            self._h = None
+
+    def info(self):
+        v = [C.c_int() for _ in range(6)]
+        lib().oracle_voc_info(self._h, *[C.byref(x) for x in v])
+        return dict(zip(("k", "L", "scoring", "weighting", "n_nodes", "n_words"),
+                        (x.value for x in v)))
+
+    def transform(self, desc, levelsup=4):
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = desc.shape[0]
+        word_of = np.zeros(n, np.uint32)
+        node_of = np.zeros(n, np.uint32)
+        bw = np.zeros(max(n, 1), np.uint32)
+        bv = np.zeros(max(n, 1), np.float64)
+        fi = np.zeros(max(n, 1), np.uint32)
+        fo = np.zeros(n + 1, np.int32)
+        ff = np.zeros(max(n, 1), np.int32)
+        bn, fn = C.c_int(), C.c_int()
+        lib().oracle_voc_transform(self._h, _p(desc), C.c_int(n), C.c_int(levelsup), _p(word_of),
+                                   _p(node_of), _p(bw), _p(bv), C.byref(bn), _p(fi), _p(fo),
+                                   _p(ff), C.byref(fn))
+        return dict(word_of=word_of, node_of=node_of, bow_words=bw[:bn.value],
+                    bow_values=bv[:bn.value], fv_ids=fi[:fn.value], fv_off=fo[:fn.value + 1],
+                    fv_feats=ff[:fo[fn.value]])

@@ -67,6 +67,19 @@ void oracle_epipole(const float R2w[9], const float t2w[3], const float Cw[3], f
 void oracle_feature_vector(const uint8_t* voc_desc, int k, int L, int levelsup,
                            const uint8_t* desc, int n, uint32_t* node_of_feature);
 
+/* DBoW2 vocabulary (dbow2_oracle.cc): opaque handle, nodes 1..n_nodes in file order */
+void* oracle_voc_create(int k, int L, int scoring, int weighting, int n_nodes,
+                        const int32_t* parent, const uint8_t* is_leaf, const uint8_t* desc,
+                        const double* weight);
+void* oracle_voc_load_text(const char* path);
+void oracle_voc_destroy(void* h);
+void oracle_voc_info(const void* h, int* k, int* L, int* scoring, int* weighting, int* n_nodes,
+                     int* n_words);
+void oracle_voc_transform(const void* h, const uint8_t* desc, int n, int levelsup,
+                          uint32_t* word_of, uint32_t* node_of, uint32_t* bow_words,
+                          double* bow_values, int* bow_n, uint32_t* fv_ids, int32_t* fv_off,
+                          int32_t* fv_feats, int* fv_n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,7 +3,8 @@ hand-built inputs (ORBmatcher.cc rules of SURVEY §8a M1-M5)."""
 import numpy as np
 import pytest
 
-from ar_orbslam2_amd import FeatureVector, Vocabulary, synth
+from ar_orbslam2_amd import FeatureVector, synth
+from ar_orbslam2_amd.vocabulary import complete_tree
 from oracle import oracle as O
 
 
@@ -13,11 +14,20 @@ def test_featurevector_from_nodes_is_dbow2_addfeature():
     assert fv.node_ids.tolist() == [11, 12, 30]
     assert fv.node_offsets.tolist() == [0, 2, 3, 6]
     assert fv.node_feats.tolist() == [1, 4, 3, 0, 2, 5]
+    # stopped words (weight <= 0) are not added
+    fv = FeatureVector.from_nodes(np.array([30, 0xFFFFFFFF, 11], np.uint32))
+    assert fv.node_ids.tolist() == [11, 30] and fv.node_feats.tolist() == [2, 0]
 
 
-def test_synthetic_vocabulary_layout():
-    v = Vocabulary.synthetic()
-    assert v.node_desc.shape == (111, 32) and v.first_node_id() == 11 and v.nid_level == 2
+def test_complete_tree_breadth_first_layout():
+    desc = np.arange(1111 * 32, dtype=np.uint32).astype(np.uint8).reshape(1111, 32)
+    parent, is_leaf, d, w = complete_tree(10, 3, desc)
+    assert len(parent) == 1110
+    assert parent[:10].tolist() == [0] * 10                     # level 1: ids 1..10
+    assert parent[10:20].tolist() == [1] * 10 and parent[109] == 10  # level 2: ids 11..110
+    assert parent[110] == 11 and parent[1109] == 110            # level 3: ids 111..1110
+    assert is_leaf.sum() == 1000 and is_leaf[110:].all() and not is_leaf[:110].any()
+    assert np.array_equal(d, desc[1:]) and (w[110:] == 1.0).all() and (w[:110] == 0).all()
 
 
 def test_feature_vector_descent_first_child_wins():

@@ -25,11 +25,11 @@ def _oracle_bow_side(kf, valid=True):
 
 def test_vocabulary_node_ids(frames):
     a, b, voc = frames
-    v = Vocabulary(10, 6, voc, 4)
+    v = Vocabulary.complete(10, 6, voc)  # the 111-node tree: levels 0..2
     for kf in (a, b):
         got = v.node_ids(kf.mDescriptors)
         assert np.array_equal(got, kf.nodes)
-        fv = v.transform(kf.mDescriptors)
+        _, fv = v.transform(kf.mDescriptors)
         for x, y in zip(fv.as_tuple(), kf.mFeatVec):
             assert np.array_equal(x, y)
 
@@ -124,7 +124,7 @@ def test_committed_match_goldens(golden_dir):
     MG = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(MG)
     (a, b), voc = MG.match_inputs()
-    v = Vocabulary(10, 6, voc, 4)
+    v = Vocabulary.complete(10, 6, voc)
     assert np.array_equal(v.node_ids(a["desc"]), np.load(os.path.join(golden_dir, "match_nodes_a.npy")))
 
     def ns(d, keyframe):

@@ -8,6 +8,7 @@ import pytest
 import torch
 
 from ar_orbslam2_amd import KEYPOINT_DTYPE, Vocabulary, epipole, synth
+from ar_orbslam2_amd.vocabulary import complete_tree
 from ar_orbslam2_amd.pipeline import TUM1_K, FramePipeline, fundamental_from_pose
 from oracle import oracle as O
 
@@ -28,9 +29,23 @@ def d2h(ptr, nbytes):
     return out
 
 
+_VOCS = []
+
+
+def _vocabs():
+    """The bench vocabulary (complete k=10, L=6, seed 42) on the GPU and in the oracle."""
+    if not _VOCS:
+        n = sum(10 ** l for l in range(7))
+        desc = np.random.default_rng(42).integers(0, 256, (n, 32), dtype=np.uint8)
+        arrays = complete_tree(10, 6, desc)
+        _VOCS.append((Vocabulary.from_nodes(10, 6, 0, 0, *arrays),
+                      O.Vocabulary.from_nodes(10, 6, 0, 0, *arrays)))
+    return _VOCS[0]
+
+
 @pytest.mark.parametrize("w,h,nf,n", [(640, 480, 1000, 4), (752, 480, 1200, 3)])
 def test_pipeline_matches_oracle(w, h, nf, n):
-    voc = Vocabulary.synthetic()
+    voc, oracle_voc = _vocabs()
     pipe = FramePipeline(w, h, n, voc, nf)
     valid, has_mp = pipe.seeded_masks(range(n))
     F = fundamental_from_pose()
@@ -49,6 +64,11 @@ def test_pipeline_matches_oracle(w, h, nf, n):
     kps_all = d2h(out["kps"], n * cap * 28).view(KEYPOINT_DTYPE).reshape(n, cap)
     desc_all = d2h(out["desc"], n * cap * 32).reshape(n, cap, 32)
     nodes_all = d2h(out["node_of"], n * cap * 4).view(np.uint32).reshape(n, cap)
+    bo = pipe.bow_outputs()
+    words_all = d2h(bo["bow_words"], n * cap * 4).view(np.uint32).reshape(n, cap)
+    vals_all = d2h(bo["bow_values"], n * cap * 8).view(np.float64).reshape(n, cap)
+    nw_all = d2h(bo["bow_n"], n * 4).view(np.int32)
+    word_of_all = d2h(bo["word_of"], n * cap * 4).view(np.uint32).reshape(n, cap)
     match_all = d2h(out["bow_match"], n * cap * 4).view(np.int32).reshape(n, cap)
     pairs_all = d2h(out["tri_pairs"], n * cap * 8).view(np.int32).reshape(n, cap, 2)
     t = O.tables(O.params(nf), w, h)
@@ -59,8 +79,13 @@ def test_pipeline_matches_oracle(w, h, nf, n):
         assert counts[f] == k
         assert np.array_equal(kps_all[f, :k], kps)
         assert np.array_equal(desc_all[f, :k], desc)
-        nodes = O.feature_vector(voc.node_desc, 10, 6, 4, desc)
+        r = oracle_voc.transform(desc, 4)  # Frame::ComputeBoW
+        nodes = r["node_of"]
         assert np.array_equal(nodes_all[f, :k], nodes)
+        assert np.array_equal(word_of_all[f, :k], r["word_of"])
+        assert nw_all[f] == len(r["bow_words"])
+        assert np.array_equal(words_all[f, :nw_all[f]], r["bow_words"])
+        assert np.array_equal(vals_all[f, :nw_all[f]], r["bow_values"])  # bit-exact f64
         ref.append(dict(desc=desc, angle=kps["angle"], keys=kps, fv=featvec(nodes),
                         valid=valid[f, :k], has_mp=has_mp[f, :k], scale_factors=t["scale"],
                         level_sigma2=t["sigma2"]))

@@ -1,0 +1,93 @@
+"""GPU parity of the DBoW2 vocabulary (orbx_vocabulary_*: loader, k_voc_transform, k_bowvec,
+k_csr) against the CPU restatement (oracle/dbow2_oracle.cc): word ids, FeatureVector node ids,
+BowVector word ids and f64 values bit for bit, FeatureVector CSR."""
+import numpy as np
+import pytest
+
+from ar_orbslam2_amd import Vocabulary
+from ar_orbslam2_amd._ffi import OrbxError
+from ar_orbslam2_amd.vocabulary import complete_tree
+from oracle import oracle as O
+
+from vocabdata import kat_features, kat_tree, random_tree, write_text
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(gpu, ref):
+    assert np.array_equal(gpu["word_of"], ref["word_of"])
+    assert np.array_equal(gpu["node_of"], ref["node_of"])
+    assert np.array_equal(gpu["bow"].word_ids, ref["bow_words"])
+    assert gpu["bow"].values.tobytes() == ref["bow_values"].tobytes()  # bit-exact f64
+    fv = gpu["fv"]
+    assert np.array_equal(fv.node_ids, ref["fv_ids"])
+    assert np.array_equal(fv.node_offsets, ref["fv_off"])
+    assert np.array_equal(fv.node_feats, ref["fv_feats"])
+
+
+@pytest.mark.parametrize("scoring,weighting", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 0), (5, 0),
+                                               (5, 1), (1, 0)])
+@pytest.mark.parametrize("levelsup", [0, 1, 2])
+def test_kat_tree_all_scorings(scoring, weighting, levelsup):
+    arrays = kat_tree()
+    g = Vocabulary.from_nodes(2, 2, scoring, weighting, *arrays)
+    o = O.Vocabulary.from_nodes(2, 2, scoring, weighting, *arrays)
+    f = kat_features()
+    _same(g.transform_full(f, levelsup), o.transform(f, levelsup))
+
+
+@pytest.mark.parametrize("seed,k,depth", [(1, 6, 4), (2, 3, 6), (3, 10, 3), (4, 20, 2),
+                                          (5, 16, 3), (6, 17, 3)])
+@pytest.mark.parametrize("n", [0, 1, 17, 1000, 4100])
+def test_random_irregular_trees(seed, k, depth, n):
+    arrays = random_tree(seed, k=k, depth=depth)
+    L = depth + 1  # declared deeper than the tree: some FeatureVector nodes are early leaves
+    g = Vocabulary.from_nodes(k, L, 0, 0, *arrays)
+    o = O.Vocabulary.from_nodes(k, L, 0, 0, *arrays)
+    rng = np.random.default_rng(seed * 100 + n)
+    f = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    # near-duplicates of node descriptors make distance ties and repeated words likely
+    if n > 10:
+        f[: n // 2] = arrays[2][rng.integers(0, len(arrays[2]), n // 2)]
+        f[: n // 4, 0] ^= 1
+    for levelsup in (1, 2, depth):
+        _same(g.transform_full(f, levelsup), o.transform(f, levelsup))
+
+
+def test_text_loader_on_gpu(tmp_path):
+    arrays = random_tree(11, k=8, depth=4)
+    p = tmp_path / "voc.txt"
+    write_text(p, 8, 4, 1, 0, *arrays)
+    g = Vocabulary.load_text(p)
+    o = O.Vocabulary.load_text(p)
+    assert (g.k, g.L, g.scoring, g.weighting, g.n_nodes, g.n_words) == tuple(o.info().values())
+    f = np.random.default_rng(5).integers(0, 256, (2000, 32), dtype=np.uint8)
+    _same(g.transform_full(f, 2), o.transform(f, 2))
+
+
+def test_bench_vocabulary_k10_L6():
+    n = sum(10 ** l for l in range(7))
+    desc = np.random.default_rng(42).integers(0, 256, (n, 32), dtype=np.uint8)
+    arrays = complete_tree(10, 6, desc)
+    g = Vocabulary.synthetic()
+    assert (g.n_nodes, g.n_words) == (n, 10 ** 6)
+    o = O.Vocabulary.from_nodes(10, 6, 0, 0, *arrays)
+    f = np.random.default_rng(9).integers(0, 256, (1500, 32), dtype=np.uint8)
+    _same(g.transform_full(f, 4), o.transform(f, 4))
+
+
+def test_errors(tmp_path):
+    p = tmp_path / "bad.txt"
+    p.write_text("21 6 0 0\n0 1 " + "0 " * 32 + " 1\n")
+    with pytest.raises(OrbxError):
+        Vocabulary.load_text(p)
+    with pytest.raises(OrbxError):  # parent id must name an earlier node
+        Vocabulary.from_nodes(2, 2, 0, 0, np.array([0, 3], np.int32), np.ones(2, np.uint8),
+                              np.zeros((2, 32), np.uint8), np.ones(2))
+    g = Vocabulary.from_nodes(2, 2, 0, 0, *kat_tree())
+    with pytest.raises(OrbxError):  # more features than k_bowvec sorts in LDS
+        g.transform_full(np.zeros((8193, 32), np.uint8))
+    e = Vocabulary.from_nodes(10, 6, 0, 0, np.zeros(0, np.int32), np.zeros(0, np.uint8),
+                              np.zeros((0, 32), np.uint8), np.zeros(0))
+    r = e.transform_full(kat_features())
+    assert len(r["bow"]) == 0 and len(r["fv"]) == 0 and (r["word_of"] == 0xFFFFFFFF).all()
