@@ -27,7 +27,7 @@ EXPORTS = [
     "orbx_plan_extract", "orbx_plan_outputs", "orbx_plan_sync", "orbx_plan_stream",
     "orbx_plan_profile", "orbx_plan_profile_read", "orbx_descriptor_distance",
     "orbx_search_by_bow_kf_f", "orbx_search_by_bow_kf_kf", "orbx_search_for_triangulation",
-    "orbx_epipole", "orbx_vocabulary_load_text", "orbx_vocabulary_create",
+    "orbx_epipole", "orbx_stereo_matches", "orbx_vocabulary_load_text", "orbx_vocabulary_create",
     "orbx_vocabulary_destroy", "orbx_vocabulary_info", "orbx_vocabulary_transform",
     "orbx_frames_create", "orbx_frames_destroy",
     "orbx_frames_capacity", "orbx_frames_set_masks", "orbx_frames_set_matching",

@@ -8,6 +8,8 @@
 #include <string>
 
 #include "orbx_internal.h"
+#include "orbx_match.h"
+#include "orbx_stereo.h"
 
 using namespace orbx;
 
@@ -117,6 +119,66 @@ int orbx_extractor_pyramid(orbx_extractor* ex, int32_t level, uint8_t* out, int6
   if (!out) return ORBX_OK;
   if (stride < lw) return ORBX_EINVAL;
   return orbx_plan_level_download(ex->plan, 0, level, out, stride);
+}
+
+// Frame::ComputeStereoMatches (ORB_SLAM2/src/Frame.cc:471-643) on the last extraction of a
+// left and a right extractor (their keypoints, descriptors and mvImagePyramid are still
+// resident on the device).  uright / depth: host arrays of the left keypoint count.
+int orbx_stereo_matches(orbx_extractor* left, orbx_extractor* right, float mb, float mbf,
+                        float* uright, float* depth, int32_t* n_out) {
+  if (!left || !right || !uright || !depth || !left->has_run || !right->has_run)
+    return ORBX_EINVAL;
+  if (left->pw != right->pw || left->ph != right->ph || left->device != right->device ||
+      left->params.nlevels != right->params.nlevels ||
+      left->params.scale_factor != right->params.scale_factor)
+    return ORBX_EINVAL;
+  ORBX_HIP(hipSetDevice(left->device));
+  PlanView vl, vr;
+  plan_view(left->plan, &vl);
+  plan_view(right->plan, &vr);
+  int nrows;
+  int64_t row_cap;
+  stereo_scratch(*vl.g, vr.kp_total, &nrows, &row_cap);
+  const int kp = vl.kp_total;
+  Stager st;
+  const size_t oprob = st.add(nullptr, sizeof(StereoProblem));
+  const size_t ouse = st.add(nullptr, (size_t)kp * 4), odep = st.add(nullptr, (size_t)kp * 4),
+               osad = st.add(nullptr, (size_t)kp * 4), ocnt = st.add(nullptr, 4),
+               ooff = st.add(nullptr, ((size_t)nrows + 1) * 4),
+               oidx = st.add(nullptr, (size_t)row_cap * 4);
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  StereoProblem P{};
+  P.kl = vl.d_kps;
+  P.dl = vl.d_desc;
+  P.nl = vl.d_counts;
+  P.kr = vr.d_kps;
+  P.dr = vr.d_desc;
+  P.nr = vr.d_counts;
+  P.pyrL = vl.d_pyr;
+  P.pyrR = vr.d_pyr;
+  P.uright = dptr<float>(base, ouse);
+  P.depth = dptr<float>(base, odep);
+  P.sad = dptr<int>(base, osad);
+  P.row_off = dptr<int>(base, ooff);
+  P.row_idx = dptr<int>(base, oidx);
+  ORBX_HIP(hipMemcpyAsync(base + oprob, &P, sizeof(P), hipMemcpyHostToDevice, s));
+  rc = launch_stereo(dptr<StereoProblem>(base, oprob), 1, vl.d_lv, vl.g->nlevels, nrows, row_cap,
+                     kp, mb, mbf, s);
+  if (rc) return rc;
+  int32_t n = 0;
+  ORBX_HIP(hipMemcpyAsync(&n, vl.d_counts, 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  (void)ocnt;
+  if (n > 0) {
+    ORBX_HIP(hipMemcpyAsync(uright, base + ouse, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(depth, base + odep, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+  }
+  if (n_out) *n_out = n;
+  return ORBX_OK;
 }
 
 }  // extern "C"

@@ -1514,6 +1514,9 @@ int plan_view(orbx_plan* P, PlanView* v) {
   v->d_counts = P->d_counts;
   v->kp_total = P->g.kp_total;
   v->max_batch = P->max_batch;
+  v->d_pyr = P->d_pyr;
+  v->pyr_bytes = P->g.pyr_bytes;
+  v->d_lv = P->d_lv;
   return ORBX_OK;
 }
 int plan_enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {

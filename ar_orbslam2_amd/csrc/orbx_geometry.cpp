@@ -140,6 +140,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     pyr += ((int64_t)L.pitch * L.h + 255) / 256 * 256;
     L.bxs = (L.w / 4) * 4;
     L.scale = g->scale[l];
+    L.inv_scale = g->inv_scale[l];
     L.size = (float)(int)(kPatch * g->scale[l]);
     L.nfeat = g->feats[l];
     // ComputeKeyPointsOctTree cell grid (ORBextractor.cc:742-796)

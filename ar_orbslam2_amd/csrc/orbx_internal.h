@@ -49,6 +49,7 @@ struct LevelGeom {
   int kp_off, kp_cap;      // per-image final keypoint slots for this level
   float scale;             // mvScaleFactor
   float size;              // (float)(int)(PATCH_SIZE * scale)
+  float inv_scale;         // mvInvScaleFactor
 };
 
 struct CellGeom {
@@ -151,6 +152,9 @@ struct PlanView {
   int* d_counts;
   int kp_total;
   int max_batch;
+  const uint8_t* d_pyr;   // [max_batch][pyr_bytes] pitched raw pyramid (mvImagePyramid)
+  int64_t pyr_bytes;
+  const LevelGeom* d_lv;  // [nlevels] device copy of g->lv
 };
 int plan_view(orbx_plan* P, PlanView* v);
 int plan_enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof);

@@ -55,3 +55,28 @@ def read_pgm(path):
     parts = data.split(b"\n", 3)
     w, h = map(int, parts[1].split())
     return np.frombuffer(parts[3], np.uint8, count=w * h).reshape(h, w).copy()
+
+
+STEREO_PAD = 48  # extra canvas columns for the disparities
+
+
+def stereo_pair(w, h, t=0, stream=0, disparity=(12, 20), base=None):
+    """Rectified synthetic stereo frame t of stream s: the left image is a crop of the seeded
+    canvas, the right one the same scene seen with disparity d (a left pixel (u, v) appears
+    at (u - d, v) on the right): d = disparity[0] on the background and disparity[1] inside a
+    central rectangle (a nearer plane).  Independent per-image noise, seeded (s, t, side)."""
+    Wc = w + STEREO_PAD
+    base = canvas(Wc, h, stream + 1000) if base is None else base
+    ox, oy = t % PAD_X, t % PAD_Y
+    d0, d1 = disparity
+    left = base[oy:oy + h, ox:ox + w]
+    right = base[oy:oy + h, ox + d0:ox + d0 + w].copy()
+    # nearer plane: right columns [x0-d1, x1-d1) show left columns [x0, x1)
+    x0, x1, y0, y1 = w // 3, 2 * w // 3, h // 3, 2 * h // 3
+    right[y0:y1, x0 - d1:x1 - d1] = left[y0:y1, x0:x1]
+    out = []
+    for side, img in enumerate((left, right)):
+        rng = np.random.default_rng([stream, t, 7, side])
+        noisy = img + rng.normal(0.0, 4.0, img.shape)
+        out.append(np.clip(np.rint(noisy), 0, 255).astype(np.uint8))
+    return out[0], out[1]

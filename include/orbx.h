@@ -155,6 +155,16 @@ int orbx_plan_profile(orbx_plan* plan, int32_t enable);
 int orbx_plan_profile_read(orbx_plan* plan, int32_t cap, char (*names)[32], double* total_ms,
                            int64_t* launches, int32_t* n_stages);
 
+/* ------------------------------------------------------------------ stereo
+ * Frame::ComputeStereoMatches (ORB_SLAM2/src/Frame.cc:471-643) on the last extraction of a
+ * left and a right extractor of the same image size and pyramid: for every left keypoint,
+ * mvuRight / mvDepth (-1 when unmatched), host arrays of at least the left keypoint count,
+ * which is returned in *n_out.  mb = baseline, mbf = baseline * fx (Frame::mb, Frame::mbf).
+ * Where the reference's cv::Mat ranges would leave the pyramid level (it asserts), the
+ * keypoint stays unmatched. */
+int orbx_stereo_matches(orbx_extractor* left, orbx_extractor* right, float mb, float mbf,
+                        float* uright, float* depth, int32_t* n_out);
+
 /* ------------------------------------------------------------------ vocabulary
  * DBoW2 TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary, ORB_SLAM2/include/
  * ORBVocabulary.h), device resident.  Node ids follow DBoW2's file order (root 0, the n

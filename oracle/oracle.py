@@ -347,3 +347,33 @@ class Vocabulary:
         return dict(word_of=word_of, node_of=node_of, bow_words=bw[:bn.value],
                     bow_values=bv[:bn.value], fv_ids=fi[:fn.value], fv_off=fo[:fn.value + 1],
                     fv_feats=ff[:fo[fn.value]])
+
+
+# ---------------------------------------------------------------- stereo (stereo_oracle.cc)
+def stereo_matches(kl, dl, kr, dr, pyr_left, pyr_right, scale, inv_scale, mb, mbf):
+    """Frame::ComputeStereoMatches restated: (mvuRight, mvDepth, SAD or -1) per left keypoint.
+    pyr_left / pyr_right: lists of 2-D uint8 level images (mvImagePyramid)."""
+    kl = np.ascontiguousarray(kl, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kr, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(dl, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(dr, np.uint8).reshape(-1, 32)
+    L = len(pyr_left)
+    pl = [np.ascontiguousarray(x, np.uint8) for x in pyr_left]
+    pr = [np.ascontiguousarray(x, np.uint8) for x in pyr_right]
+    for a, b in zip(pl, pr):
+        assert a.shape == b.shape
+    PL = (C.c_void_p * L)(*[x.ctypes.data for x in pl])
+    PR = (C.c_void_p * L)(*[x.ctypes.data for x in pr])
+    lw = np.array([x.shape[1] for x in pl], np.int32)
+    lh = np.array([x.shape[0] for x in pl], np.int32)
+    ls = np.array([x.strides[0] for x in pl], np.int64)
+    sc = np.ascontiguousarray(scale, np.float32)
+    isc = np.ascontiguousarray(inv_scale, np.float32)
+    n = len(kl)
+    ur = np.zeros(max(n, 1), np.float32)
+    dp = np.zeros(max(n, 1), np.float32)
+    sd = np.zeros(max(n, 1), np.int32)
+    lib().oracle_stereo_matches(_p(kl), C.c_int(n), _p(dl), _p(kr), C.c_int(len(kr)), _p(dr),
+                                PL, PR, _p(lw), _p(lh), _p(ls), _p(sc), _p(isc),
+                                C.c_float(mb), C.c_float(mbf), _p(ur), _p(dp), _p(sd))
+    return ur[:n], dp[:n], sd[:n]

@@ -80,6 +80,14 @@ void oracle_voc_transform(const void* h, const uint8_t* desc, int n, int levelsu
                           double* bow_values, int* bow_n, uint32_t* fv_ids, int32_t* fv_off,
                           int32_t* fv_feats, int* fv_n);
 
+/* Frame::ComputeStereoMatches (stereo_oracle.cc): per-level pyramid pointers + strides */
+void oracle_stereo_matches(const orbx_keypoint* kl, int nl, const uint8_t* dl,
+                           const orbx_keypoint* kr, int nr, const uint8_t* dr,
+                           const uint8_t* const* pyrL, const uint8_t* const* pyrR,
+                           const int* lw, const int* lh, const int64_t* lstride,
+                           const float* scale, const float* inv_scale, float mb, float mbf,
+                           float* uright, float* depth, int* sad);
+
 #ifdef __cplusplus
 }
 #endif
