@@ -29,10 +29,10 @@ EXPORTS = [
     "orbx_search_by_bow_kf_f", "orbx_search_by_bow_kf_kf", "orbx_search_for_triangulation",
     "orbx_epipole", "orbx_stereo_matches", "orbx_vocabulary_load_text", "orbx_vocabulary_create",
     "orbx_vocabulary_destroy", "orbx_vocabulary_info", "orbx_vocabulary_transform",
-    "orbx_frames_create", "orbx_frames_destroy",
+    "orbx_frames_create", "orbx_frames_create_stereo", "orbx_frames_destroy",
     "orbx_frames_capacity", "orbx_frames_set_masks", "orbx_frames_set_matching",
     "orbx_frames_run", "orbx_frames_sync", "orbx_frames_results", "orbx_frames_outputs",
-    "orbx_frames_bow", "orbx_frames_stream", "orbx_frames_profile", "orbx_frames_profile_read",
+    "orbx_frames_bow", "orbx_frames_stereo", "orbx_frames_stream", "orbx_frames_profile", "orbx_frames_profile_read",
 ]
 
 

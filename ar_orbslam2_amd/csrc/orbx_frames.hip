@@ -3,6 +3,9 @@
 //   extract (plan)  ->  Frame::ComputeBoW: vocabulary descent (k_voc_transform), BowVector
 //   (k_bowvec), FeatureVector CSR (k_csr)
 //   -> SearchByBoW(prev-as-KF, cur)  ->  SearchForTriangulation(prev-as-KF, cur-as-KF)
+// Stereo pipelines take frames as interleaved (left, right) image pairs, run
+// Frame::ComputeStereoMatches (orbx_stereo.hip) after the extraction, and feed ComputeBoW and
+// the matchers with the left images and their mvuRight (Frame.cc:78-96).
 // Frame f of a batch is matched against frame (f-1) mod n of the same batch.  The sequence is
 // captured once into a hipGraph per (input pointer, batch size).
 #include <hip/hip_runtime.h>
@@ -16,6 +19,7 @@
 #include "orbx_internal.h"
 #include "orbx_match.h"
 #include "orbx_vocab.h"
+#include "orbx_stereo.h"
 
 using namespace orbx;
 
@@ -29,6 +33,20 @@ struct orbx_frames {
   const VocRanks* ranks = nullptr;
   int scoring = 0, weighting = 0, levelsup = 4, nid_level = 2;
   int nb = 1;
+  int max_frames = 0;
+  int bow_err_slot() const { return max_frames; }
+  // stereo
+  int stereo = 0;
+  float mb = 0, mbf = 0;
+  int st_nrows = 0;
+  int64_t st_row_cap = 0;
+  int* d_lcounts = nullptr;  // [B] left keypoint counts (stereo)
+  float* d_uright = nullptr;  // [B][kp] mvuRight
+  float* d_depth = nullptr;   // [B][kp] mvDepth
+  int* d_sad = nullptr;       // [B][kp]
+  int* d_row_off = nullptr;   // [B][nrows + 1]
+  int* d_row_idx = nullptr;   // [B][row_cap]
+  StereoProblem* d_sprob = nullptr;
   // per frame
   uint32_t* d_node_of = nullptr;  // [B][kp] FeatureVector node id
   uint32_t* d_rank_of = nullptr;  // [B][kp] FeatureVector rank (k_csr bucket)
@@ -80,6 +98,10 @@ int dalloc(T** p, size_t count) {
   return ORBX_OK;
 }
 
+// image index of frame f's (left) image, and the per-frame count array
+inline int limg(const orbx_frames* F, int f) { return F->stereo ? 2 * f : f; }
+inline int* fcounts(const orbx_frames* F) { return F->stereo ? F->d_lcounts : F->v.d_counts; }
+
 int build_problems(orbx_frames* F, int n) {
   const int kp = F->v.kp_total;
   std::vector<BowProblem> bp(n);
@@ -89,9 +111,9 @@ int build_problems(orbx_frames* F, int n) {
     auto side = [&](int fr, bool with_valid) {
       DevSide s{};
       s.n = 0;
-      s.n_dev = F->v.d_counts + fr;
-      s.desc = F->v.d_desc + (int64_t)fr * kp * 32;
-      s.angle = (const float*)((const char*)(F->v.d_kps + (int64_t)fr * kp) +
+      s.n_dev = fcounts(F) + fr;
+      s.desc = F->v.d_desc + (int64_t)limg(F, fr) * kp * 32;
+      s.angle = (const float*)((const char*)(F->v.d_kps + (int64_t)limg(F, fr) * kp) +
                                offsetof(orbx_keypoint, angle));
       s.angle_stride = sizeof(orbx_keypoint) / sizeof(float);
       s.valid = with_valid ? F->d_valid + (int64_t)fr * kp : nullptr;
@@ -107,16 +129,16 @@ int build_problems(orbx_frames* F, int n) {
     B.s2 = side(f, false);
     B.match = F->d_match + (int64_t)f * kp;
     B.count = F->d_bow_count + f;
-    B.error = F->d_bow_count + F->v.max_batch;
+    B.error = F->d_bow_count + F->bow_err_slot();
     B.mode = 0;
     B.nnratio = F->bow_ratio;
     B.check_ori = F->bow_ori;
     auto tside = [&](int fr) {
       DevTriSide s{};
-      s.n_dev = F->v.d_counts + fr;
-      s.desc = F->v.d_desc + (int64_t)fr * kp * 32;
-      s.keys_un = F->v.d_kps + (int64_t)fr * kp;
-      s.u_right = nullptr;
+      s.n_dev = fcounts(F) + fr;
+      s.desc = F->v.d_desc + (int64_t)limg(F, fr) * kp * 32;
+      s.keys_un = F->v.d_kps + (int64_t)limg(F, fr) * kp;
+      s.u_right = F->stereo ? F->d_uright + (int64_t)fr * kp : nullptr;
       s.has_mp = F->d_hasmp + (int64_t)fr * kp;
       s.fv.n_nodes_dev = F->d_nn + fr;
       s.fv.node_ids = F->d_ids + (int64_t)fr * F->nb;
@@ -138,6 +160,26 @@ int build_problems(orbx_frames* F, int n) {
     T.pairs = F->d_pairs + (int64_t)f * kp * 2;
     T.count = F->d_tri_count + f;
   }
+  if (F->stereo) {
+    std::vector<StereoProblem> sp(n);
+    for (int f = 0; f < n; f++) {
+      StereoProblem& S = sp[f];
+      S.kl = F->v.d_kps + (int64_t)(2 * f) * kp;
+      S.dl = F->v.d_desc + (int64_t)(2 * f) * kp * 32;
+      S.nl = F->v.d_counts + 2 * f;
+      S.kr = F->v.d_kps + (int64_t)(2 * f + 1) * kp;
+      S.dr = F->v.d_desc + (int64_t)(2 * f + 1) * kp * 32;
+      S.nr = F->v.d_counts + 2 * f + 1;
+      S.pyrL = F->v.d_pyr + (int64_t)(2 * f) * F->v.pyr_bytes;
+      S.pyrR = F->v.d_pyr + (int64_t)(2 * f + 1) * F->v.pyr_bytes;
+      S.uright = F->d_uright + (int64_t)f * kp;
+      S.depth = F->d_depth + (int64_t)f * kp;
+      S.sad = F->d_sad + (int64_t)f * kp;
+      S.row_off = F->d_row_off + (int64_t)f * (F->st_nrows + 1);
+      S.row_idx = F->d_row_idx + (int64_t)f * F->st_row_cap;
+    }
+    ORBX_HIP(hipMemcpy(F->d_sprob, sp.data(), sizeof(StereoProblem) * n, hipMemcpyHostToDevice));
+  }
   ORBX_HIP(hipMemcpy(F->d_bprob, bp.data(), sizeof(BowProblem) * n, hipMemcpyHostToDevice));
   ORBX_HIP(hipMemcpy(F->d_tprob, tp.data(), sizeof(TriProblem) * n, hipMemcpyHostToDevice));
   F->prob_n = n;
@@ -151,19 +193,29 @@ int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
             st_csr = pr.stage("k_csr"),
             st_bow = pr.stage("k_bow"), st_tri = pr.stage("k_tri");
   hipStream_t s = F->v.stream;
-  int rc = plan_enqueue(F->plan, d_in, n, prof);
+  int rc = plan_enqueue(F->plan, d_in, F->stereo ? 2 * n : n, prof);
   if (rc) return rc;
   const int kp = F->v.kp_total;
+  const int ist = F->stereo ? 2 : 1;  // image step of the frames' (left) images
+  if (F->stereo) {
+    const int st_st = pr.stage("k_stereo");
+    // left counts of the interleaved (left, right) images, contiguous per frame
+    ORBX_HIP(hipMemcpy2DAsync(F->d_lcounts, 4, F->v.d_counts, 8, 4, n, hipMemcpyDeviceToDevice, s));
+    rc = launch_stereo(F->d_sprob, n, F->v.d_lv, F->v.g->nlevels, F->st_nrows, F->st_row_cap, kp,
+                       F->mb, F->mbf, s);
+    if (rc) return rc;
+    pr.mark(s, st_st);
+  }
   rc = launch_voc_transform(F->vv, F->nid_level, F->ranks->d_rank_of_node, F->v.d_desc,
-                            (int64_t)kp * 32, F->v.d_counts, 0, kp, F->d_word_of, F->d_rank_of,
+                            (int64_t)kp * 32 * ist, fcounts(F), 0, kp, F->d_word_of, F->d_rank_of,
                             F->d_node_of, F->d_wt_of, kp, n, s);
   if (rc) return rc;
   pr.mark(s, st_fv);
-  rc = launch_bowvec(F->scoring, F->weighting, F->d_word_of, F->d_wt_of, kp, F->v.d_counts, 0, kp,
+  rc = launch_bowvec(F->scoring, F->weighting, F->d_word_of, F->d_wt_of, kp, fcounts(F), 0, kp,
                      F->d_bow_words, F->d_bow_vals, kp, F->d_bow_n, n, s);
   if (rc) return rc;
   pr.mark(s, st_bv);
-  rc = launch_csr(F->d_rank_of, kp, F->v.d_counts, 0, 0, F->nb, F->ranks->d_rank_ids, F->d_ids,
+  rc = launch_csr(F->d_rank_of, kp, fcounts(F), 0, 0, F->nb, F->ranks->d_rank_ids, F->d_ids,
                   F->d_off, F->d_feats, kp, F->d_nn, n, s);
   if (rc) return rc;
   pr.mark(s, st_csr);
@@ -182,9 +234,9 @@ int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
 
 extern "C" {
 
-int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_batch,
-                       const orbx_vocabulary* voc, int32_t levelsup, int hip_device,
-                       orbx_frames** out) {
+static int frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_batch,
+                         const orbx_vocabulary* voc, int32_t levelsup, int stereo, float mb,
+                         float mbf, int hip_device, orbx_frames** out) {
   if (!p || !out || !voc || levelsup < 0 || max_batch < 1) return ORBX_EINVAL;
   *out = nullptr;
   int voc_dev = 0;
@@ -203,7 +255,11 @@ int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_b
     return rc;
   };
   F->device = hip_device;
-  rc = orbx_plan_create(p, w, h, max_batch, hip_device, &F->plan);
+  F->stereo = stereo;
+  F->max_frames = max_batch;
+  F->mb = mb;
+  F->mbf = mbf;
+  rc = orbx_plan_create(p, w, h, stereo ? 2 * max_batch : max_batch, hip_device, &F->plan);
   if (rc) return fail(rc);
   plan_view(F->plan, &F->v);
   if (F->v.kp_total > 8192) return fail(ORBX_EUNSUPPORTED);  // k_bowvec sorts in LDS
@@ -228,6 +284,14 @@ int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_b
       dalloc(&F->d_pairs, B * kp * 2) || dalloc(&F->d_tri_count, B) || dalloc(&F->d_bprob, B) ||
       dalloc(&F->d_tprob, B))
     return fail(ORBX_ENOMEM);
+  if (stereo) {
+    stereo_scratch(*F->v.g, (int)kp, &F->st_nrows, &F->st_row_cap);
+    if (dalloc(&F->d_lcounts, B) || dalloc(&F->d_uright, B * kp) ||
+        dalloc(&F->d_depth, B * kp) || dalloc(&F->d_sad, B * kp) ||
+        dalloc(&F->d_row_off, B * (F->st_nrows + 1)) ||
+        dalloc(&F->d_row_idx, B * (size_t)F->st_row_cap) || dalloc(&F->d_sprob, B))
+      return fail(ORBX_ENOMEM);
+  }
   if (hipMemcpy(F->d_sf, F->v.g->scale, 4 * p->nlevels, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(F->d_s2, F->v.g->sigma2, 4 * p->nlevels, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(F->d_valid, 1, B * kp) != hipSuccess ||
@@ -239,10 +303,23 @@ int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_b
   return ORBX_OK;
 }
 
+int orbx_frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_batch,
+                       const orbx_vocabulary* voc, int32_t levelsup, int hip_device,
+                       orbx_frames** out) {
+  return frames_create(p, w, h, max_batch, voc, levelsup, 0, 0.f, 0.f, hip_device, out);
+}
+
+int orbx_frames_create_stereo(const orbx_params* p, int32_t w, int32_t h, int32_t max_batch,
+                              const orbx_vocabulary* voc, int32_t levelsup, float mb, float mbf,
+                              int hip_device, orbx_frames** out) {
+  return frames_create(p, w, h, max_batch, voc, levelsup, 1, mb, mbf, hip_device, out);
+}
+
 int orbx_frames_destroy(orbx_frames* F) {
   if (!F) return ORBX_OK;
   F->drop_graphs();
-  void* ptrs[] = {F->d_rank_of, F->d_word_of, F->d_wt_of, F->d_bow_words, F->d_bow_vals, F->d_bow_n,
+  void* ptrs[] = {F->d_lcounts, F->d_uright, F->d_depth, F->d_sad, F->d_row_off, F->d_row_idx,
+                  F->d_sprob, F->d_rank_of, F->d_word_of, F->d_wt_of, F->d_bow_words, F->d_bow_vals, F->d_bow_n,
                   F->d_node_of, F->d_ids,   F->d_off,       F->d_feats,
                   F->d_nn,    F->d_valid,   F->d_hasmp, F->d_sf,        F->d_s2,
                   F->d_match, F->d_bow_count, F->d_m12, F->d_pairs,     F->d_tri_count,
@@ -262,7 +339,7 @@ int orbx_frames_capacity(const orbx_frames* F, int32_t* kp_cap) {
 
 int orbx_frames_set_masks(orbx_frames* F, const uint8_t* valid, const uint8_t* has_mp) {
   if (!F) return ORBX_EINVAL;
-  const size_t bytes = (size_t)F->v.max_batch * F->v.kp_total;
+  const size_t bytes = (size_t)F->max_frames * F->v.kp_total;
   if (valid) ORBX_HIP(hipMemcpy(F->d_valid, valid, bytes, hipMemcpyHostToDevice));
   if (has_mp) ORBX_HIP(hipMemcpy(F->d_hasmp, has_mp, bytes, hipMemcpyHostToDevice));
   return ORBX_OK;
@@ -286,7 +363,7 @@ int orbx_frames_set_matching(orbx_frames* F, float bow_ratio, int32_t bow_check_
 }
 
 int orbx_frames_run(orbx_frames* F, const uint8_t* d_imgs, int32_t n) {
-  if (!F || !d_imgs || n < 1 || n > F->v.max_batch) return ORBX_EINVAL;
+  if (!F || !d_imgs || n < 1 || n > F->max_frames) return ORBX_EINVAL;
   ORBX_HIP(hipSetDevice(F->device));
   if (F->prob_n != n) {
     int rc = build_problems(F, n);
@@ -322,15 +399,15 @@ int orbx_frames_sync(orbx_frames* F) {
 
 int orbx_frames_results(orbx_frames* F, int32_t n, int32_t* kp_counts, int32_t* bow_matches,
                         int32_t* tri_matches, int32_t* error) {
-  if (!F || n < 1 || n > F->v.max_batch) return ORBX_EINVAL;
+  if (!F || n < 1 || n > F->max_frames) return ORBX_EINVAL;
   hipStream_t s = F->v.stream;
-  if (kp_counts) ORBX_HIP(hipMemcpyAsync(kp_counts, F->v.d_counts, 4 * n, hipMemcpyDeviceToHost, s));
+  if (kp_counts) ORBX_HIP(hipMemcpyAsync(kp_counts, fcounts(F), 4 * n, hipMemcpyDeviceToHost, s));
   if (bow_matches)
     ORBX_HIP(hipMemcpyAsync(bow_matches, F->d_bow_count, 4 * n, hipMemcpyDeviceToHost, s));
   if (tri_matches)
     ORBX_HIP(hipMemcpyAsync(tri_matches, F->d_tri_count, 4 * n, hipMemcpyDeviceToHost, s));
   if (error)
-    ORBX_HIP(hipMemcpyAsync(error, F->d_bow_count + F->v.max_batch, 4, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(error, F->d_bow_count + F->bow_err_slot(), 4, hipMemcpyDeviceToHost, s));
   ORBX_HIP(hipStreamSynchronize(s));
   return ORBX_OK;
 }
@@ -345,6 +422,13 @@ int orbx_frames_outputs(orbx_frames* F, orbx_keypoint** d_kps, uint8_t** d_desc,
   if (d_node_of) *d_node_of = F->d_node_of;
   if (d_bow_match) *d_bow_match = F->d_match;
   if (d_tri_pairs) *d_tri_pairs = F->d_pairs;
+  return ORBX_OK;
+}
+
+int orbx_frames_stereo(orbx_frames* F, float** d_uright, float** d_depth) {
+  if (!F || !F->stereo) return ORBX_EINVAL;
+  if (d_uright) *d_uright = F->d_uright;
+  if (d_depth) *d_depth = F->d_depth;
   return ORBX_OK;
 }
 

@@ -28,16 +28,28 @@ def fundamental_from_pose(K=TUM1_K, t=(0.10, 0.02, 0.05)):
 
 class FramePipeline:
     def __init__(self, w, h, max_batch, vocabulary, nfeatures=1000, scale_factor=1.2, nlevels=8,
-                 ini_th_fast=20, min_th_fast=7, device=0, levelsup=4):
+                 ini_th_fast=20, min_th_fast=7, device=0, levelsup=4, stereo=None):
+        """stereo=(mb, mbf) makes a stereo pipeline: a frame is an interleaved (left, right)
+        image pair, so `run` takes 2n images for n frames."""
         self.w, self.h, self.max_batch = int(w), int(h), int(max_batch)
         self.params = _ffi.Params(int(nfeatures), float(scale_factor), int(nlevels),
                                   int(ini_th_fast), int(min_th_fast))
         self.voc = vocabulary
+        self.stereo = stereo is not None
         self._h = C.c_void_p()
-        check("orbx_frames_create",
-              lib().orbx_frames_create(C.byref(self.params), C.c_int32(self.w), C.c_int32(self.h),
-                                       C.c_int32(self.max_batch), vocabulary.handle,
-                                       C.c_int32(levelsup), C.c_int(device), C.byref(self._h)))
+        if self.stereo:
+            check("orbx_frames_create_stereo",
+                  lib().orbx_frames_create_stereo(C.byref(self.params), C.c_int32(self.w),
+                                                  C.c_int32(self.h), C.c_int32(self.max_batch),
+                                                  vocabulary.handle, C.c_int32(levelsup),
+                                                  C.c_float(stereo[0]), C.c_float(stereo[1]),
+                                                  C.c_int(device), C.byref(self._h)))
+        else:
+            check("orbx_frames_create",
+                  lib().orbx_frames_create(C.byref(self.params), C.c_int32(self.w),
+                                           C.c_int32(self.h), C.c_int32(self.max_batch),
+                                           vocabulary.handle, C.c_int32(levelsup),
+                                           C.c_int(device), C.byref(self._h)))
         cap = C.c_int32()
         check("orbx_frames_capacity", lib().orbx_frames_capacity(self._h, C.byref(cap)))
         self.kp_cap = cap.value
@@ -82,7 +94,8 @@ class FramePipeline:
                                              C.c_int32(int(only_stereo))))
 
     def run(self, d_imgs_ptr, n):
-        """Enqueue one batch; `d_imgs_ptr` is a device pointer to n dense h*w uint8 frames."""
+        """Enqueue one batch of n frames; `d_imgs_ptr` is a device pointer to n dense h*w uint8
+        images (2n, interleaved left/right, for a stereo pipeline)."""
         check("orbx_frames_run", lib().orbx_frames_run(self._h, C.c_void_p(d_imgs_ptr),
                                                        C.c_int32(n)))
 
@@ -110,6 +123,11 @@ class FramePipeline:
         ptrs = [C.c_void_p() for _ in names]
         check("orbx_frames_bow", lib().orbx_frames_bow(self._h, *[C.byref(p) for p in ptrs]))
         return {k: p.value for k, p in zip(names, ptrs)}
+
+    def stereo_outputs(self):
+        ur, dp = C.c_void_p(), C.c_void_p()
+        check("orbx_frames_stereo", lib().orbx_frames_stereo(self._h, C.byref(ur), C.byref(dp)))
+        return {"uright": ur.value, "depth": dp.value}
 
     def stream(self):
         return lib().orbx_frames_stream(self._h)

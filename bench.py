@@ -32,8 +32,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CONFIGS = {
     "C2": dict(w=640, h=480, nfeatures=1000,
                workload="TUM fr1/xyz mono 640x480, 1000 features, 1xMI355X HIP extract+match"),
-    "C3": dict(w=752, h=480, nfeatures=1200, workload="EuRoC MH01 geometry 752x480, 1200 features"),
-    "C4": dict(w=1241, h=376, nfeatures=2000, workload="KITTI 00 geometry 1241x376, 2000 features"),
+    "C3": dict(w=752, h=480, nfeatures=1200, stereo=(47.90639384423901, 435.2046959714599),
+               workload="EuRoC MH01 stereo geometry 2x752x480, 1200 features, stereo matching"),
+    "C4": dict(w=1241, h=376, nfeatures=2000, stereo=(386.1448, 718.856),
+               workload="KITTI 00 stereo geometry 2x1241x376, 2000 features, stereo matching"),
     "C5": dict(w=1920, h=1080, nfeatures=4000, workload="synthetic 1920x1080, 4000 features"),
 }
 
@@ -97,21 +99,34 @@ def cpu_baseline(cfg, seconds):
         10, 6, np.random.default_rng(42).integers(0, 256, (ndesc, 32), dtype=np.uint8)))
     F = fundamental_from_pose()
     ex, ey = O.epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
-    base = synth.canvas(w, h, 0)
-    imgs = [synth.frame(w, h, i, 0, base) for i in range(64)]
+    stereo = cfg.get("stereo")
+    if stereo:
+        from ar_orbslam2_amd.stereo import stereo_params
+        mb, mbf = stereo_params(*stereo)
+        imgs = [synth.stereo_pair(w, h, i, 0) for i in range(16)]
+    else:
+        base = synth.canvas(w, h, 0)
+        imgs = [synth.frame(w, h, i, 0, base) for i in range(64)]
 
     prev = None
     n = 0
     t0 = time.perf_counter()
     while True:
         img = imgs[n % len(imgs)]
-        kps, desc = O.extract(img, p)
+        u_right = None
+        if stereo:
+            kps, desc, pl, _ = O.extract(img[0], p, want_pyramid=True)
+            kr, dr, pr, _ = O.extract(img[1], p, want_pyramid=True)
+            u_right = O.stereo_matches(kps, desc, kr, dr, pl, pr, t["scale"], t["inv_scale"],
+                                       mb, mbf)[0]
+        else:
+            kps, desc = O.extract(img, p)
         b = voc.transform(desc, 4)  # Frame::ComputeBoW: BowVector + FeatureVector
         r = np.random.default_rng(n)
         cur = dict(desc=desc, angle=kps["angle"], keys=kps,
                    fv=(b["fv_ids"], b["fv_off"], b["fv_feats"]),
                    valid=(r.random(len(kps)) < 0.6).astype(np.uint8),
-                   has_mp=(r.random(len(kps)) < 0.4).astype(np.uint8),
+                   has_mp=(r.random(len(kps)) < 0.4).astype(np.uint8), u_right=u_right,
                    scale_factors=t["scale"], level_sigma2=t["sigma2"])
         if prev is not None:
             O.search_by_bow_kf_f(prev, dict(cur, valid=None), 0.7, True)
@@ -122,8 +137,9 @@ def cpu_baseline(cfg, seconds):
         if el >= seconds and n >= 4:
             break
     return dict(value=n / el, unit="frames/s", cores=1, kind="port",
-                sample=f"{n} consecutive {w}x{h} synthetic frames, CPU oracle (oracle/orb_oracle.cc, "
-                       f"g++ -O3 -march=x86-64-v3 -ffp-contract=off), 1 thread, extract + "
+                sample=f"{n} consecutive {w}x{h} synthetic {'stereo ' if stereo else ''}frames, CPU "
+                       f"oracle (oracle/*.cc, g++ -O3 -march=x86-64-v3 -ffp-contract=off), 1 thread, "
+                       f"extract{' x2 + ComputeStereoMatches' if stereo else ''} + "
                        f"ComputeBoW + SearchByBoW + SearchForTriangulation per frame, {el:.1f} s on "
                        f"{platform.processor() or platform.machine()}")
 
@@ -185,18 +201,28 @@ def main():
     S = max(1, args.streams)
     ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
     pipes, pools = [], []
+    stereo = None
+    if cfg.get("stereo"):
+        from ar_orbslam2_amd.stereo import stereo_params
+        stereo = stereo_params(*cfg["stereo"])
     for si in range(S):
-        pipe = FramePipeline(w, h, B, voc, nf, device=local)
+        pipe = FramePipeline(w, h, B, voc, nf, device=local, stereo=stereo)
         pipe.seeded_masks(range(B))
         pipe.set_matching(fundamental_from_pose(), (ex, ey), bow_ratio=0.7, bow_check_ori=True,
                           tri_ratio=0.6, tri_check_ori=False)
         # synthetic frames of this camera stream, resident in HBM before timing
         stream_id = stream_of_rank(rank) * S + si
-        base = synth.canvas(w, h, stream=stream_id)
         pool = []
-        for pi in range(args.pool):
-            fr = np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)])
-            pool.append(torch.from_numpy(fr).cuda())
+        if stereo:
+            pairs = [synth.stereo_pair(w, h, t, stream_id) for t in range(min(B, 32))]
+            for pi in range(args.pool):  # interleaved (left, right) images
+                fr = np.stack([im for i in range(B) for im in pairs[(pi * 7 + i) % len(pairs)]])
+                pool.append(torch.from_numpy(fr).cuda())
+        else:
+            base = synth.canvas(w, h, stream=stream_id)
+            for pi in range(args.pool):
+                fr = np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)])
+                pool.append(torch.from_numpy(fr).cuda())
         pipes.append(pipe)
         pools.append(pool)
     pipe = pipes[0]
@@ -243,7 +269,8 @@ def main():
     ex_tables = ORBextractor(nf)
     levels = level_sizes(w, h, ex_tables.GetInverseScaleFactors())
     n_kp = int(kp_counts.sum())
-    alg = algorithmic_bytes(levels, n_kp, B)
+    # stereo: both images of a frame are extracted (right keypoint count ~ left)
+    alg = algorithmic_bytes(levels, 2 * n_kp if stereo else n_kp, 2 * B if stereo else B)
     roofline = None
     if stages:
         dom = max(stages, key=lambda k: stages[k][0])
@@ -270,7 +297,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B * S,
                    "camera_streams_per_gpu": S, "frames_per_batch": B,
-                   "image": f"{w}x{h}", "nfeatures": nf, "nlevels": 8, "scale_factor": 1.2,
+                   "image": f"{w}x{h}", "images_per_frame": 2 if stereo else 1,
+                   "nfeatures": nf, "nlevels": 8, "scale_factor": 1.2,
                    "parallelism": f"{world} GPU(s) x {S} independent camera streams, no collective",
                    "keypoints_per_frame": round(n_kp / B, 1),
                    "bow_matches_per_frame": round(float(bow.mean()), 1),

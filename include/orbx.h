@@ -217,6 +217,13 @@ typedef struct orbx_frames orbx_frames;
 int orbx_frames_create(const orbx_params* params, int32_t w, int32_t h, int32_t max_batch,
                        const orbx_vocabulary* voc, int32_t levelsup, int hip_device,
                        orbx_frames** out);
+/* Stereo pipeline (Frame's stereo constructor, ORB_SLAM2/src/Frame.cc:66-123): a frame is an
+ * interleaved (left, right) image pair, d_imgs of orbx_frames_run holds 2n images; after the
+ * extraction Frame::ComputeStereoMatches fills mvuRight / mvDepth, and ComputeBoW and the
+ * matchers run on the left images (SearchForTriangulation with mvuRight). */
+int orbx_frames_create_stereo(const orbx_params* params, int32_t w, int32_t h,
+                              int32_t max_batch, const orbx_vocabulary* voc, int32_t levelsup,
+                              float mb, float mbf, int hip_device, orbx_frames** out);
 int orbx_frames_destroy(orbx_frames* fr);
 int orbx_frames_capacity(const orbx_frames* fr, int32_t* kp_cap);
 /* Host masks [max_batch][kp_cap]: valid = KF-side usable MapPoint for SearchByBoW, has_mp =
@@ -231,7 +238,8 @@ int orbx_frames_sync(orbx_frames* fr);
 /* Host copies of the per-frame counts of the last run (synchronises). */
 int orbx_frames_results(orbx_frames* fr, int32_t n, int32_t* kp_counts, int32_t* bow_matches,
                         int32_t* tri_matches, int32_t* error);
-/* Device pointers: kps/desc [max_batch][kp_cap], counts [max_batch], FeatureVector node id
+/* Device pointers: kps/desc [images][kp_cap], counts [images] (images = 2 x frames for
+ * stereo, left image of frame f at 2f), FeatureVector node id
  * per feature [max_batch][kp_cap] (0xFFFFFFFF = stopped word), bow match [max_batch][kp_cap]
  * (frame-indexed, value = KF index), triangulation pairs [max_batch][kp_cap][2]. */
 int orbx_frames_outputs(orbx_frames* fr, orbx_keypoint** d_kps, uint8_t** d_desc,
@@ -239,6 +247,8 @@ int orbx_frames_outputs(orbx_frames* fr, orbx_keypoint** d_kps, uint8_t** d_desc
                         int32_t** d_tri_pairs);
 /* Device pointers of the BowVectors: word ids / values [max_batch][kp_cap], entries per frame
  * [max_batch]; word id per feature [max_batch][kp_cap] (0xFFFFFFFF = stopped). */
+/* Stereo pipelines: mvuRight / mvDepth per left keypoint, [max_batch][kp_cap] device. */
+int orbx_frames_stereo(orbx_frames* fr, float** d_uright, float** d_depth);
 int orbx_frames_bow(orbx_frames* fr, uint32_t** d_bow_words, double** d_bow_values,
                     int32_t** d_bow_n, uint32_t** d_word_of);
 void* orbx_frames_stream(orbx_frames* fr);

@@ -98,3 +98,62 @@ def test_pipeline_matches_oracle(w, h, nf, n):
         assert tri[f] == nt
         assert np.array_equal(pairs_all[f, :nt], pt)
     pipe.close()
+
+
+@pytest.mark.parametrize("w,h,nf,cam,n", [(752, 480, 1200, (47.90639384423901, 435.2046959714599), 3),
+                                          (1241, 376, 2000, (386.1448, 718.856), 2)])
+def test_stereo_pipeline_matches_oracle(w, h, nf, cam, n):
+    """EuRoC / KITTI stereo geometry (SURVEY configs C3 / C4): extraction of both images,
+    ComputeStereoMatches, ComputeBoW of the left image, SearchByBoW and SearchForTriangulation
+    with mvuRight, frame f against frame (f-1) mod n."""
+    from ar_orbslam2_amd.stereo import stereo_params
+    mb, mbf = stereo_params(*cam)
+    voc, oracle_voc = _vocabs()
+    pipe = FramePipeline(w, h, n, voc, nf, stereo=(mb, mbf))
+    valid, has_mp = pipe.seeded_masks(range(n))
+    F = fundamental_from_pose()
+    ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
+    pipe.set_matching(F, (ex, ey), bow_ratio=0.7, bow_check_ori=True, tri_ratio=0.6,
+                      tri_check_ori=False)
+    pairs = [synth.stereo_pair(w, h, t, 5, (10 + 2 * t, 25)) for t in range(n)]
+    imgs = np.stack([im for pr in pairs for im in pr])
+    d = torch.from_numpy(imgs).cuda()
+    pipe.run(d.data_ptr(), n)
+    pipe.sync()
+    counts, bow, tri, err = pipe.results(n)
+    assert err == 0
+    cap = pipe.kp_cap
+    out = pipe.device_outputs()
+    so = pipe.stereo_outputs()
+    kps_all = d2h(out["kps"], 2 * n * cap * 28).view(KEYPOINT_DTYPE).reshape(2 * n, cap)
+    match_all = d2h(out["bow_match"], n * cap * 4).view(np.int32).reshape(n, cap)
+    pairs_all = d2h(out["tri_pairs"], n * cap * 8).view(np.int32).reshape(n, cap, 2)
+    ur_all = d2h(so["uright"], n * cap * 4).view(np.float32).reshape(n, cap)
+    dp_all = d2h(so["depth"], n * cap * 4).view(np.float32).reshape(n, cap)
+    p = O.params(nf)
+    t = O.tables(p, w, h)
+    ref = []
+    for f in range(n):
+        kl, dl, pl, _ = O.extract(pairs[f][0], p, want_pyramid=True)
+        kr, dr, prr, _ = O.extract(pairs[f][1], p, want_pyramid=True)
+        k = len(kl)
+        assert counts[f] == k
+        assert np.array_equal(kps_all[2 * f, :k], kl)
+        assert np.array_equal(kps_all[2 * f + 1, :len(kr)], kr)
+        ur, dp, _ = O.stereo_matches(kl, dl, kr, dr, pl, prr, t["scale"], t["inv_scale"], mb, mbf)
+        assert ur_all[f, :k].tobytes() == ur.tobytes()
+        assert dp_all[f, :k].tobytes() == dp.tobytes()
+        assert (ur >= 0).sum() > 100
+        r = oracle_voc.transform(dl, 4)
+        ref.append(dict(desc=dl, angle=kl["angle"], keys=kl, fv=featvec(r["node_of"]),
+                        valid=valid[f, :k], has_mp=has_mp[f, :k], u_right=ur,
+                        scale_factors=t["scale"], level_sigma2=t["sigma2"]))
+    for f in range(n):
+        kf, cur = ref[(f - 1) % n], ref[f]
+        nb, mbm = O.search_by_bow_kf_f(kf, dict(cur, valid=None), 0.7, True)
+        assert bow[f] == nb
+        assert np.array_equal(match_all[f, :len(cur["desc"])], mbm)
+        nt, pt = O.search_for_triangulation(kf, cur, F, ex, ey, False, 0.6, False)
+        assert tri[f] == nt
+        assert np.array_equal(pairs_all[f, :nt], pt)
+    pipe.close()
