@@ -221,8 +221,9 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, int64
       const int a0 = xa[2 * (D.coef_x + dx)], a1 = xa[2 * (D.coef_x + dx) + 1];
       const uint8_t* sb = (const uint8_t*)s_src;
       if (dx < D.xmax) {
-        for (int r = 0; r < nrows; r++)
-          s_h[r][tid] = sb[r * kRzSrcWords * 4 + x0] * a0 + sb[r * kRzSrcWords * 4 + x0 + 1] * a1;
+        for (int r = 0; r < nrows; r++)  // 24-bit multiplies: u8 x Q11 tap
+          s_h[r][tid] = __mul24(sb[r * kRzSrcWords * 4 + x0], a0) +
+                        __mul24(sb[r * kRzSrcWords * 4 + x0 + 1], a1);
       } else {
         for (int r = 0; r < nrows; r++) s_h[r][tid] = sb[r * kRzSrcWords * 4 + x0] * 2048;
       }
@@ -248,12 +249,12 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, int64
       if (c4 + k < D.vxs) {
         const int t0 = max(-32768, min(32767, h0[k] >> 4));
         const int t1 = max(-32768, min(32767, h1[k] >> 4));
-        int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);
+        int m = (__mul24(t0, b0) >> 16) + (__mul24(t1, b1) >> 16);  // |t|, |b| < 2^15
         m = max(-32768, min(32767, m));
         m = max(-32768, min(32767, m + 2));
         v = m >> 2;
       } else {
-        v = (h0[k] * b0 + h1[k] * b1 + (1 << 21)) >> 22;
+        v = (__mul24(h0[k], b0) + __mul24(h1[k], b1) + (1 << 21)) >> 22;  // h < 2^20, b <= 2^11
       }
       out |= (uint32_t)max(0, min(255, v)) << (8 * k);
     }
@@ -296,12 +297,22 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
       s_in[r][c] = *(const uint32_t*)(src + (int64_t)(Y0 + r - 3) * G.pitch + X0 - 4 + 4 * c);
     }
   } else {
-    uint8_t* sb = (uint8_t*)s_in;
-    for (int i = tid; i < (kBlurTH + 6) * (kBlurTW + 8); i += 256) {
-      const int r = i / (kBlurTW + 8), c = i - r * (kBlurTW + 8);
+    // border tile: each window row reflected once (reflect-101), whole dwords where the 4
+    // bytes are inside the level, byte-wise reflect only for dwords crossing the left/right
+    // edge; dwords wholly past the last column any output reads (w + 2) stay unset
+    for (int i = tid; i < (kBlurTH + 6) * kWords; i += 256) {
+      const int r = i / kWords, c = i - r * kWords;
       const int y = reflect101(min(Y0 + r - 3, G.h + 8), G.h);
-      const int x = reflect101(min(X0 + c - 4, G.w + 8), G.w);
-      sb[r * (kBlurTW + 8) + c] = src[(int64_t)y * G.pitch + x];
+      const uint8_t* row = src + (int64_t)y * G.pitch;
+      const int x = X0 - 4 + 4 * c;
+      uint32_t v = 0;
+      if (x >= 0 && x + 4 <= G.w) {
+        v = *(const uint32_t*)(row + x);
+      } else if (x < G.w + 3) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) v |= (uint32_t)row[reflect101(min(x + k, G.w + 8), G.w)] << (8 * k);
+      }
+      s_in[r][c] = v;
     }
   }
   __syncthreads();
@@ -318,10 +329,15 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
       b[8 + k] = (w2 >> (8 * k)) & 0xFF;
     }
     int4 o;
-    o.x = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
-    o.y = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
-    o.z = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
-    o.w = k0 * (b[4] + b[10]) + k1 * (b[5] + b[9]) + k2 * (b[6] + b[8]) + k3 * b[7];
+    // 24-bit multiplies (full rate): every operand < 2^24
+    auto tap7 = [&](int c) {
+      return (int)(__umul24(b[c - 3] + b[c + 3], k0) + __umul24(b[c - 2] + b[c + 2], k1) +
+                   __umul24(b[c - 1] + b[c + 1], k2) + __umul24(b[c], k3));
+    };
+    o.x = tap7(4);
+    o.y = tap7(5);
+    o.z = tap7(6);
+    o.w = tap7(7);
     *(int4*)&s_row[r][4 * q] = o;
   }
   __syncthreads();
@@ -333,23 +349,25 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
 #pragma unroll
     for (int k = 0; k < 7; k++) R[k] = *(const int4*)&s_row[r + k][4 * q];
     int m[4];
-    m[0] = k0 * (R[0].x + R[6].x) + k1 * (R[1].x + R[5].x) + k2 * (R[2].x + R[4].x) + k3 * R[3].x;
-    m[1] = k0 * (R[0].y + R[6].y) + k1 * (R[1].y + R[5].y) + k2 * (R[2].y + R[4].y) + k3 * R[3].y;
-    m[2] = k0 * (R[0].z + R[6].z) + k1 * (R[1].z + R[5].z) + k2 * (R[2].z + R[4].z) + k3 * R[3].z;
-    m[3] = k0 * (R[0].w + R[6].w) + k1 * (R[1].w + R[5].w) + k2 * (R[2].w + R[4].w) + k3 * R[3].w;
+    // row sums <= 255 * 257 = 65535: pair sums < 2^24, 24-bit multiplies are exact
+    auto col7 = [&](int a0, int a1, int a2, int a3, int a4, int a5, int a6) {
+      return (int)(__umul24(a0 + a6, k0) + __umul24(a1 + a5, k1) + __umul24(a2 + a4, k2) +
+                   __umul24(a3, k3));
+    };
+    m[0] = col7(R[0].x, R[1].x, R[2].x, R[3].x, R[4].x, R[5].x, R[6].x);
+    m[1] = col7(R[0].y, R[1].y, R[2].y, R[3].y, R[4].y, R[5].y, R[6].y);
+    m[2] = col7(R[0].z, R[1].z, R[2].z, R[3].z, R[4].z, R[5].z, R[6].z);
+    m[3] = col7(R[0].w, R[1].w, R[2].w, R[3].w, R[4].w, R[5].w, R[6].w);
     uint32_t out = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      int v;
-      if (x + k < G.bxs) {
-        const int qv = m[k] >> 16, rem = m[k] & 0xFFFF;  // m >= 0
-        v = qv + (rem > 0x8000 || (rem == 0x8000 && (qv & 1)));
-      } else {
-        v = (m[k] + 32768) >> 16;
-      }
-      out |= (uint32_t)min(255, v) << (8 * k);
+      // m / 65536 rounded half-even in the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up
+      // in the scalar tail; m >= 0
+      const uint32_t mk = (uint32_t)m[k];
+      const uint32_t add = x + k < G.bxs ? 0x7FFFu + ((mk >> 16) & 1u) : 0x8000u;
+      out |= min(255u, (mk + add) >> 16) << (8 * k);
     }
-    *(uint32_t*)(dst + (int64_t)y * G.pitch + x) = out;  // bytes past w land in the row pad
+    *(uint32_t*)(dst + (uint32_t)(y * G.pitch + x)) = out;  // bytes past w land in the row pad
   }
 }
 
@@ -1070,9 +1088,13 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
 // cv::fastAtan2, glibc sincosf, rBRIEF on the blurred level with the reference binary's
 // fmaf + cvRound sampling (ORBextractor.cc:101-144), then the level-0 scaling of
 // operator() (:1035-1041).  Output is level-major like `_keypoints`/`descriptors`.
+struct KpOffsets {  // per-level first keypoint slot (LevelGeom::kp_off), by value
+  int off[kMaxLevels + 1];
+};
+
 __global__ __launch_bounds__(256) void k_describe(
     const uint8_t* __restrict__ pyr, int64_t pyr_bytes, const uint8_t* __restrict__ blur,
-    const LevelGeom* __restrict__ lv, int nlevels, const uint32_t* __restrict__ okey,
+    const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const uint32_t* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
   int bx, img;
@@ -1087,7 +1109,8 @@ __global__ __launch_bounds__(256) void k_describe(
   }
   if (slot >= kp_total) return;
   int level = 0;
-  while (level + 1 < nlevels && slot >= lv[level + 1].kp_off) level++;
+#pragma unroll
+  for (int l = 1; l < kMaxLevels; l++) level += (l < nlevels && slot >= ko.off[l]);
   const LevelGeom& G = lv[level];
   const int idx = slot - G.kp_off;
   if (idx >= oc[level]) return;
@@ -1113,13 +1136,13 @@ __global__ __launch_bounds__(256) void k_describe(
   for (int k = 0; k < 5; k++) {
     const int i = lane + 64 * k, r = i / RW, c = i - r * RW;
     vr[k] = (i < 31 * RW && fr + c <= lr)
-                ? *(const uint32_t*)(L + (int64_t)(cy - 15 + r) * G.pitch + 4 * (fr + c)) : 0u;
+                ? *(const uint32_t*)(L + (uint32_t)((cy - 15 + r) * G.pitch + 4 * (fr + c))) : 0u;
   }
 #pragma unroll
   for (int k = 0; k < 7; k++) {
     const int i = lane + 64 * k, r = i / BW, c = i - r * BW;
     vb[k] = (i < 37 * BW && fb + c <= lb)
-                ? *(const uint32_t*)(B + (int64_t)(cy - 18 + r) * G.pitch + 4 * (fb + c)) : 0u;
+                ? *(const uint32_t*)(B + (uint32_t)((cy - 18 + r) * G.pitch + 4 * (fb + c))) : 0u;
   }
 #pragma unroll
   for (int k = 0; k < 5; k++)
@@ -1139,11 +1162,11 @@ __global__ __launch_bounds__(256) void k_describe(
       const int d = c_umax[v];
       if (u < -d || u > d) continue;
       if (v == 0) {
-        m10 += u * raw[u];
+        m10 += __mul24(u, (int)raw[u]);
       } else {
-        const int vp = raw[u + v * RS], vm = raw[u - v * RS];
-        m10 += u * (vp + vm);
-        m01 += v * (vp - vm);
+        const int vp = raw[u + __mul24(v, RS)], vm = raw[u - __mul24(v, RS)];
+        m10 += __mul24(u, vp + vm);
+        m01 += __mul24(v, vp - vm);
       }
     }
   }
@@ -1168,7 +1191,7 @@ __global__ __launch_bounds__(256) void k_describe(
       const float py = (float)c_pattern[pair * 4 + e * 2 + 1];
       const int row = (int)__builtin_rintf(__builtin_fmaf(px, sn, py * cs));
       const int col = (int)__builtin_rintf(__builtin_fmaf(px, cs, -(py * sn)));
-      t[e] = bc[row * BS + col];
+      t[e] = bc[__mul24(row, BS) + col];
     }
     nib |= (t[0] < t[1]) << m;
   }
@@ -1281,8 +1304,10 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                      P->d_label, P->d_okey, P->d_ocount, g.kp_total, L, g.node_cap_max,
                      P->cell_cap, P->key_cap);
   pr.mark(P->stream, st_oct);
+  KpOffsets ko{};
+  for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
   hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 3) / 4, n), dim3(256), 0, P->stream,
-                     P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, P->d_okey, P->d_ocount,
+                     P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, ko, P->d_okey, P->d_ocount,
                      g.kp_total, P->d_kps, P->d_desc, P->d_counts);
   pr.mark(P->stream, st_desc);
   hipError_t e = hipGetLastError();
