@@ -27,7 +27,8 @@ EXPORTS = [
     "orbx_plan_extract", "orbx_plan_outputs", "orbx_plan_sync", "orbx_plan_stream",
     "orbx_plan_profile", "orbx_plan_profile_read", "orbx_descriptor_distance",
     "orbx_search_by_bow_kf_f", "orbx_search_by_bow_kf_kf", "orbx_search_for_triangulation",
-    "orbx_epipole", "orbx_stereo_matches", "orbx_vocabulary_load_text", "orbx_vocabulary_create",
+    "orbx_epipole", "orbx_search_by_projection", "orbx_search_by_projection_last",
+    "orbx_stereo_matches", "orbx_vocabulary_load_text", "orbx_vocabulary_create",
     "orbx_vocabulary_destroy", "orbx_vocabulary_info", "orbx_vocabulary_transform",
     "orbx_frames_create", "orbx_frames_create_stereo", "orbx_frames_destroy",
     "orbx_frames_capacity", "orbx_frames_set_masks", "orbx_frames_set_matching",
@@ -62,6 +63,26 @@ class TriSide(C.Structure):
                 ("u_right", C.c_void_p), ("has_mp", C.c_void_p), ("fv", FeatVec),
                 ("scale_factors", C.c_void_p), ("level_sigma2", C.c_void_p),
                 ("nlevels", C.c_int32)]
+
+
+class ProjFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("desc", C.c_void_p),
+                ("u_right", C.c_void_p), ("has_mp_obs", C.c_void_p), ("min_x", C.c_float),
+                ("min_y", C.c_float), ("max_x", C.c_float), ("max_y", C.c_float),
+                ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float),
+                ("scale_factors", C.c_void_p), ("nlevels", C.c_int32)]
+
+
+class ProjPoints(C.Structure):
+    _fields_ = [("n", C.c_int32), ("track", C.c_void_p), ("proj_x", C.c_void_p),
+                ("proj_y", C.c_void_p), ("proj_xr", C.c_void_p), ("pred_level", C.c_void_p),
+                ("view_cos", C.c_void_p), ("desc", C.c_void_p)]
+
+
+class ProjLast(C.Structure):
+    _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
+                ("ur", C.c_void_p), ("octave", C.c_void_p), ("angle", C.c_void_p),
+                ("desc", C.c_void_p)]
 
 
 _lib = None

@@ -128,6 +128,48 @@ class ORBmatcher:
         return n.value, pairs[:n.value].copy()
 
 
+    # -------------------------------------------------------------- tracking searches
+    def SearchByProjection(self, F, points, th=3.0, bMono=None, forward=False, backward=False):
+        """Both tracking overloads (ORBmatcher.cc:45-137 and 1331-1474), on the GPU.
+
+        F: current frame — mvKeysUn, mDescriptors, mvuRight (None = mono), `has_mp_obs`
+           (mvpMapPoints[i] && Observations() > 0), grid frame mnMinX, mnMinY, mnMaxX, mnMaxY,
+           mfGridElementWidthInv, mfGridElementHeightInv, mvScaleFactors.
+        points with `proj_x` — local-map points (SearchByProjection(F, vpMapPoints, th)):
+           track, proj_x, proj_y, proj_xr, pred_level, view_cos, desc.
+        points with `u` — the last frame (SearchByProjection(CurrentFrame, LastFrame, th,
+           bMono)): valid, u, v, ur, octave, angle, desc; forward / backward are bForward /
+           bBackward (both False when bMono).
+        Returns (nmatches, match) with match[f] = point / last-frame index or -1."""
+        fr, keep = _proj_frame(F)
+        n = fr.n
+        match = np.zeros(max(n, 1), np.int32)
+        nm = C.c_int32()
+        if hasattr(points, "proj_x") or (isinstance(points, dict) and "proj_x" in points):
+            p, pk = _proj_struct(points, _ffi.ProjPoints, [
+                ("track", np.uint8), ("proj_x", np.float32), ("proj_y", np.float32),
+                ("proj_xr", np.float32), ("pred_level", np.int32), ("view_cos", np.float32),
+                ("desc", np.uint8)])
+            check("orbx_search_by_projection",
+                  lib().orbx_search_by_projection(C.byref(fr), C.byref(p), C.c_float(th),
+                                                  C.c_float(self.mfNNratio), ptr(match),
+                                                  C.byref(nm)))
+        else:
+            if bMono:
+                forward = backward = False
+            p, pk = _proj_struct(points, _ffi.ProjLast, [
+                ("valid", np.uint8), ("u", np.float32), ("v", np.float32), ("ur", np.float32),
+                ("octave", np.int32), ("angle", np.float32), ("desc", np.uint8)])
+            check("orbx_search_by_projection_last",
+                  lib().orbx_search_by_projection_last(C.byref(fr), C.byref(p), C.c_float(th),
+                                                       C.c_int32(int(forward)),
+                                                       C.c_int32(int(backward)),
+                                                       C.c_int32(int(self.mbCheckOrientation)),
+                                                       ptr(match), C.byref(nm)))
+        return nm.value, match[:n].copy()
+
+
+
 def epipole(R2w, t2w, Cw, fx, fy, cx, cy):
     ex, ey = C.c_float(), C.c_float()
     R = np.ascontiguousarray(R2w, np.float32).reshape(9)
@@ -137,3 +179,35 @@ def epipole(R2w, t2w, Cw, fx, fy, cx, cy):
                                              C.c_float(cx), C.c_float(cy), C.byref(ex),
                                              C.byref(ey)))
     return ex.value, ey.value
+
+
+def _get(obj, name, alt=None):
+    if isinstance(obj, dict):
+        return obj.get(name, obj.get(alt) if alt else None)
+    v = getattr(obj, name, None)
+    return getattr(obj, alt, None) if v is None and alt else v
+
+
+def _proj_frame(F):
+    keys = np.ascontiguousarray(_get(F, "mvKeysUn", "keys_un"), KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(_get(F, "mDescriptors", "desc"), np.uint8).reshape(-1, 32)
+    ur = _get(F, "mvuRight", "u_right")
+    ur = None if ur is None else np.ascontiguousarray(ur, np.float32)
+    hm = _get(F, "has_mp_obs")
+    hm = None if hm is None else np.ascontiguousarray(hm, np.uint8)
+    sf = np.ascontiguousarray(_get(F, "mvScaleFactors", "scale_factors"), np.float32)
+    vals = [float(_get(F, a, b)) for a, b in (("mnMinX", "min_x"), ("mnMinY", "min_y"),
+                                              ("mnMaxX", "max_x"), ("mnMaxY", "max_y"),
+                                              ("mfGridElementWidthInv", "grid_w_inv"),
+                                              ("mfGridElementHeightInv", "grid_h_inv"))]
+    s = _ffi.ProjFrame(len(keys), ptr(keys), ptr(desc), ptr(ur), ptr(hm), *vals, ptr(sf), len(sf))
+    return s, _Keep(keys=keys, desc=desc, ur=ur, hm=hm, sf=sf)
+
+
+def _proj_struct(points, cls, spec):
+    arrs = []
+    for name, t in spec:
+        v = _get(points, name)
+        arrs.append(None if v is None else np.ascontiguousarray(v, t))
+    n = len(arrs[0])
+    return cls(n, *[ptr(a) for a in arrs]), arrs

@@ -155,6 +155,59 @@ int orbx_plan_profile(orbx_plan* plan, int32_t enable);
 int orbx_plan_profile_read(orbx_plan* plan, int32_t cap, char (*names)[32], double* total_ms,
                            int64_t* launches, int32_t* n_stages);
 
+/* ------------------------------------------------------------------ projection searches
+ * The current Frame as the tracking searches see it: mvKeysUn, mDescriptors, mvuRight, the
+ * feature grid frame (mnMinX.., mfGridElementWidthInv/HeightInv; FRAME_GRID 64 x 48,
+ * Frame.h:39-40), mvScaleFactors, and has_mp_obs[i] = mvpMapPoints[i] &&
+ * mvpMapPoints[i]->Observations() > 0 (those features are skipped). */
+typedef struct {
+  int32_t n;
+  const orbx_keypoint* keys_un;
+  const uint8_t* desc;         /* [n][32] */
+  const float* u_right;        /* [n], NULL for monocular */
+  const uint8_t* has_mp_obs;   /* [n], NULL = none */
+  float min_x, min_y, max_x, max_y;
+  float grid_w_inv, grid_h_inv;
+  const float* scale_factors;  /* [nlevels] */
+  int32_t nlevels;
+} orbx_proj_frame;
+/* Local-map points for SearchByProjection(Frame&, vector<MapPoint*>, th): per point
+ * track = mbTrackInView && !isBad(), and the isInFrustum results mTrackProjX / Y / XR,
+ * mnTrackScaleLevel, mTrackViewCos (Frame::isInFrustum, Frame.cc:260-330), descriptor
+ * GetDescriptor().  Every point passed has Observations() > 0. */
+typedef struct {
+  int32_t n;
+  const uint8_t* track;
+  const float *proj_x, *proj_y, *proj_xr;
+  const int32_t* pred_level;
+  const float* view_cos;
+  const uint8_t* desc;         /* [n][32] */
+} orbx_proj_points;
+/* Last-frame points for SearchByProjection(CurrentFrame, LastFrame, th, bMono): valid[i] =
+ * LastFrame.mvpMapPoints[i] && !mvbOutlier[i] && invzc >= 0; u, v the projection into the
+ * current frame and ur = u - mbf*invzc (ORBmatcher.cc:1364-1383, evaluated by the caller with
+ * the reference's cv::Mat pose products); octave = LastFrame.mvKeys[i].octave, angle =
+ * LastFrame.mvKeysUn[i].angle, desc = pMP->GetDescriptor(). */
+typedef struct {
+  int32_t n;
+  const uint8_t* valid;
+  const float *u, *v, *ur;
+  const int32_t* octave;
+  const float* angle;
+  const uint8_t* desc;         /* [n][32] */
+} orbx_proj_last;
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+ * (ORB_SLAM2/src/ORBmatcher.cc:45-137): match[f] = index of the point assigned to frame
+ * feature f in this call (F.mvpMapPoints[f] = vpMapPoints[match[f]]), else -1. */
+int orbx_search_by_projection(const orbx_proj_frame* frame, const orbx_proj_points* points,
+                              float th, float nnratio, int32_t* match, int32_t* nmatches);
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ * (ORBmatcher.cc:1331-1474): match[f] = last-frame index whose MapPoint is assigned to current
+ * feature f, else -1.  forward / backward = bForward / bBackward (:1348-1349). */
+int orbx_search_by_projection_last(const orbx_proj_frame* frame, const orbx_proj_last* last,
+                                   float th, int32_t forward, int32_t backward,
+                                   int32_t check_ori, int32_t* match, int32_t* nmatches);
+
 /* ------------------------------------------------------------------ stereo
  * Frame::ComputeStereoMatches (ORB_SLAM2/src/Frame.cc:471-643) on the last extraction of a
  * left and a right extractor of the same image size and pyramid: for every left keypoint,

@@ -377,3 +377,74 @@ def stereo_matches(kl, dl, kr, dr, pyr_left, pyr_right, scale, inv_scale, mb, mb
                                 PL, PR, _p(lw), _p(lh), _p(ls), _p(sc), _p(isc),
                                 C.c_float(mb), C.c_float(mbf), _p(ur), _p(dp), _p(sd))
     return ur[:n], dp[:n], sd[:n]
+
+
+# ---------------------------------------------------------------- projection searches
+class ProjFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("desc", C.c_void_p),
+                ("u_right", C.c_void_p), ("has_mp_obs", C.c_void_p), ("min_x", C.c_float),
+                ("min_y", C.c_float), ("max_x", C.c_float), ("max_y", C.c_float),
+                ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float),
+                ("scale_factors", C.c_void_p), ("nlevels", C.c_int32)]
+
+
+class ProjPoints(C.Structure):
+    _fields_ = [("n", C.c_int32), ("track", C.c_void_p), ("proj_x", C.c_void_p),
+                ("proj_y", C.c_void_p), ("proj_xr", C.c_void_p), ("pred_level", C.c_void_p),
+                ("view_cos", C.c_void_p), ("desc", C.c_void_p)]
+
+
+class ProjLast(C.Structure):
+    _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
+                ("ur", C.c_void_p), ("octave", C.c_void_p), ("angle", C.c_void_p),
+                ("desc", C.c_void_p)]
+
+
+def _arrs(d, spec):
+    return {k: (None if d.get(k) is None else np.ascontiguousarray(d[k], t)) for k, t in spec}
+
+
+def proj_frame(f):
+    """f: dict(keys_un, desc, u_right|None, has_mp_obs|None, min_x, min_y, max_x, max_y,
+    grid_w_inv, grid_h_inv, scale_factors)."""
+    a = _arrs(f, [("keys_un", KEYPOINT_DTYPE), ("desc", np.uint8), ("u_right", np.float32),
+                  ("has_mp_obs", np.uint8), ("scale_factors", np.float32)])
+    s = ProjFrame(len(a["keys_un"]), _p(a["keys_un"]), _p(a["desc"]), _p(a["u_right"]),
+                  _p(a["has_mp_obs"]), f["min_x"], f["min_y"], f["max_x"], f["max_y"],
+                  f["grid_w_inv"], f["grid_h_inv"], _p(a["scale_factors"]),
+                  len(a["scale_factors"]))
+    return s, a
+
+
+def features_in_area(f, x, y, r, min_level, max_level, cap=100000):
+    s, keep = proj_frame(f)
+    out = np.zeros(cap, np.int32)
+    n = lib().oracle_features_in_area(C.byref(s), C.c_float(x), C.c_float(y), C.c_float(r),
+                                      C.c_int(min_level), C.c_int(max_level), _p(out), C.c_int(cap))
+    return out[:n].copy()
+
+
+def search_by_projection(f, pts, th, nnratio):
+    s, keep = proj_frame(f)
+    a = _arrs(pts, [("track", np.uint8), ("proj_x", np.float32), ("proj_y", np.float32),
+                    ("proj_xr", np.float32), ("pred_level", np.int32), ("view_cos", np.float32),
+                    ("desc", np.uint8)])
+    p = ProjPoints(len(a["track"]), *[_p(a[k]) for k in ("track", "proj_x", "proj_y", "proj_xr",
+                                                          "pred_level", "view_cos", "desc")])
+    match = np.zeros(max(s.n, 1), np.int32)
+    n = lib().oracle_search_by_projection(C.byref(s), C.byref(p), C.c_float(th),
+                                          C.c_float(nnratio), _p(match))
+    return n, match[:s.n].copy()
+
+
+def search_by_projection_last(f, last, th, forward, backward, check_ori):
+    s, keep = proj_frame(f)
+    a = _arrs(last, [("valid", np.uint8), ("u", np.float32), ("v", np.float32), ("ur", np.float32),
+                     ("octave", np.int32), ("angle", np.float32), ("desc", np.uint8)])
+    p = ProjLast(len(a["valid"]), *[_p(a[k]) for k in ("valid", "u", "v", "ur", "octave", "angle",
+                                                        "desc")])
+    match = np.zeros(max(s.n, 1), np.int32)
+    n = lib().oracle_search_by_projection_last(C.byref(s), C.byref(p), C.c_float(th),
+                                               C.c_int(int(forward)), C.c_int(int(backward)),
+                                               C.c_int(int(check_ori)), _p(match))
+    return n, match[:s.n].copy()

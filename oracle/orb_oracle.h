@@ -88,6 +88,14 @@ void oracle_stereo_matches(const orbx_keypoint* kl, int nl, const uint8_t* dl,
                            const float* scale, const float* inv_scale, float mb, float mbf,
                            float* uright, float* depth, int* sad);
 
+/* tracking searches (projection_oracle.cc) */
+int oracle_features_in_area(const orbx_proj_frame* F, float x, float y, float r, int minLevel,
+                            int maxLevel, int32_t* out, int cap);
+int oracle_search_by_projection(const orbx_proj_frame* F, const orbx_proj_points* M, float th,
+                                float nnratio, int32_t* match);
+int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_last* P, float th,
+                                     int forward, int backward, int check_ori, int32_t* match);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,236 @@
+// projection_oracle.cc — CPU restatement of the tracking searches
+//   Frame::AssignFeaturesToGrid / PosInGrid / GetFeaturesInArea (ORB_SLAM2/src/Frame.cc:235-250,
+//     332-398)
+//   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)   (ORBmatcher.cc:45-137)
+//   ORBmatcher::SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
+//                                                                          (ORBmatcher.cc:1331-1474)
+// TEST INFRASTRUCTURE ONLY (see orb_oracle.h).  MapPoint state enters as plain arrays: the
+// caller evaluates mbTrackInView / isBad / the projections (Frame::isInFrustum, the pose
+// products) exactly as the reference does and passes the results; every MapPoint passed has
+// Observations() > 0, so a frame feature matched earlier in the same call is skipped by the
+// later ones, as in the reference.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "orb_oracle.h"
+
+namespace {
+
+constexpr int kCols = 64, kRows = 48;  // FRAME_GRID_COLS / FRAME_GRID_ROWS (Frame.h:39-40)
+
+int hamming(const uint8_t* a, const uint8_t* b) {
+  int d = 0;
+  for (int i = 0; i < 32; i++) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+  return d;
+}
+
+struct Grid {
+  std::vector<int> cell[kCols][kRows];
+};
+
+void assign_grid(const orbx_proj_frame* F, Grid* G) {
+  for (int i = 0; i < F->n; i++) {  // AssignFeaturesToGrid + PosInGrid
+    const orbx_keypoint& kp = F->keys_un[i];
+    const int posX = (int)std::round((kp.x - F->min_x) * F->grid_w_inv);
+    const int posY = (int)std::round((kp.y - F->min_y) * F->grid_h_inv);
+    if (posX < 0 || posX >= kCols || posY < 0 || posY >= kRows) continue;
+    G->cell[posX][posY].push_back(i);
+  }
+}
+
+std::vector<int> features_in_area(const orbx_proj_frame* F, const Grid& G, float x, float y,
+                                  float r, int minLevel, int maxLevel) {
+  std::vector<int> out;
+  const int nMinCellX = std::max(0, (int)std::floor((x - F->min_x - r) * F->grid_w_inv));
+  if (nMinCellX >= kCols) return out;
+  const int nMaxCellX = std::min(kCols - 1, (int)std::ceil((x - F->min_x + r) * F->grid_w_inv));
+  if (nMaxCellX < 0) return out;
+  const int nMinCellY = std::max(0, (int)std::floor((y - F->min_y - r) * F->grid_h_inv));
+  if (nMinCellY >= kRows) return out;
+  const int nMaxCellY = std::min(kRows - 1, (int)std::ceil((y - F->min_y + r) * F->grid_h_inv));
+  if (nMaxCellY < 0) return out;
+  const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+  for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+    for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+      for (int idx : G.cell[ix][iy]) {
+        const orbx_keypoint& kpUn = F->keys_un[idx];
+        if (bCheckLevels) {
+          if (kpUn.octave < minLevel) continue;
+          if (maxLevel >= 0 && kpUn.octave > maxLevel) continue;
+        }
+        const float distx = kpUn.x - x, disty = kpUn.y - y;
+        if (std::fabs(distx) < r && std::fabs(disty) < r) out.push_back(idx);
+      }
+  return out;
+}
+
+void three_maxima(const int* histo, int L, int* i1, int* i2, int* i3) {  // :1604-1645
+  int max1 = 0, max2 = 0, max3 = 0;
+  *i1 = *i2 = *i3 = -1;
+  for (int i = 0; i < L; i++) {
+    const int s = histo[i];
+    if (s > max1) {
+      max3 = max2;
+      max2 = max1;
+      max1 = s;
+      *i3 = *i2;
+      *i2 = *i1;
+      *i1 = i;
+    } else if (s > max2) {
+      max3 = max2;
+      max2 = s;
+      *i3 = *i2;
+      *i2 = i;
+    } else if (s > max3) {
+      max3 = s;
+      *i3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) {
+    *i2 = -1;
+    *i3 = -1;
+  } else if (max3 < 0.1f * (float)max1) {
+    *i3 = -1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// GetFeaturesInArea on the frame's grid: indices in the reference's order, count returned.
+int oracle_features_in_area(const orbx_proj_frame* F, float x, float y, float r, int minLevel,
+                            int maxLevel, int32_t* out, int cap) {
+  Grid G;
+  assign_grid(F, &G);
+  std::vector<int> v = features_in_area(F, G, x, y, r, minLevel, maxLevel);
+  for (size_t i = 0; i < v.size() && (int)i < cap; i++) out[i] = v[i];
+  return (int)v.size();
+}
+
+// SearchByProjection(Frame&, vector<MapPoint*>, th): match[f] = map point index assigned to
+// frame feature f in this call, else -1.  Returns nmatches.
+int oracle_search_by_projection(const orbx_proj_frame* F, const orbx_proj_points* M, float th,
+                                float nnratio, int32_t* match) {
+  Grid G;
+  assign_grid(F, &G);
+  std::vector<uint8_t> claimed(F->n, 0);
+  for (int i = 0; i < F->n; i++) {
+    match[i] = -1;
+    if (F->has_mp_obs && F->has_mp_obs[i]) claimed[i] = 1;
+  }
+  const bool bFactor = th != 1.0;
+  int nmatches = 0;
+  for (int iMP = 0; iMP < M->n; iMP++) {
+    if (!M->track[iMP]) continue;  // !mbTrackInView || isBad()
+    const int nPredictedLevel = M->pred_level[iMP];
+    float r = M->view_cos[iMP] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:130-136)
+    if (bFactor) r *= th;
+    const float rs = r * F->scale_factors[nPredictedLevel];
+    const std::vector<int> vIndices = features_in_area(F, G, M->proj_x[iMP], M->proj_y[iMP], rs,
+                                                       nPredictedLevel - 1, nPredictedLevel);
+    if (vIndices.empty()) continue;
+    const uint8_t* MPdescriptor = M->desc + (size_t)iMP * 32;
+    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+    for (int idx : vIndices) {
+      if (claimed[idx]) continue;
+      if (F->u_right && F->u_right[idx] > 0) {
+        const float er = std::fabs(M->proj_xr[iMP] - F->u_right[idx]);
+        if (er > r * F->scale_factors[nPredictedLevel]) continue;
+      }
+      const int dist = hamming(MPdescriptor, F->desc + (size_t)idx * 32);
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestLevel2 = bestLevel;
+        bestLevel = F->keys_un[idx].octave;
+        bestIdx = idx;
+      } else if (dist < bestDist2) {
+        bestLevel2 = F->keys_un[idx].octave;
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= 100) {  // TH_HIGH
+      if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+      match[bestIdx] = iMP;
+      claimed[bestIdx] = 1;
+      nmatches++;
+    }
+  }
+  return nmatches;
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono): match[f] = last-frame index whose
+// MapPoint was assigned to current feature f, else -1.  forward/backward are the reference's
+// bForward/bBackward (tlc.z vs mb, already false when mono).
+int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_last* P, float th,
+                                     int forward, int backward, int check_ori, int32_t* match) {
+  Grid G;
+  assign_grid(F, &G);
+  std::vector<uint8_t> claimed(F->n, 0);
+  for (int i = 0; i < F->n; i++) {
+    match[i] = -1;
+    if (F->has_mp_obs && F->has_mp_obs[i]) claimed[i] = 1;
+  }
+  const int HISTO = 30;
+  const float factor = 1.0f / HISTO;
+  std::vector<int> rotHist[30];
+  int nmatches = 0;
+  for (int i = 0; i < P->n; i++) {
+    if (!P->valid[i]) continue;  // pMP && !mvbOutlier[i] && invzc >= 0
+    const float u = P->u[i], v = P->v[i];
+    if (u < F->min_x || u > F->max_x) continue;
+    if (v < F->min_y || v > F->max_y) continue;
+    const int nLastOctave = P->octave[i];
+    const float radius = th * F->scale_factors[nLastOctave];
+    std::vector<int> vIndices2;
+    if (forward) vIndices2 = features_in_area(F, G, u, v, radius, nLastOctave, -1);
+    else if (backward) vIndices2 = features_in_area(F, G, u, v, radius, 0, nLastOctave);
+    else vIndices2 = features_in_area(F, G, u, v, radius, nLastOctave - 1, nLastOctave + 1);
+    if (vIndices2.empty()) continue;
+    const uint8_t* dMP = P->desc + (size_t)i * 32;
+    int bestDist = 256, bestIdx2 = -1;
+    for (int i2 : vIndices2) {
+      if (claimed[i2]) continue;
+      if (F->u_right && F->u_right[i2] > 0) {
+        const float er = std::fabs(P->ur[i] - F->u_right[i2]);
+        if (er > radius) continue;
+      }
+      const int dist = hamming(dMP, F->desc + (size_t)i2 * 32);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = i2;
+      }
+    }
+    if (bestDist <= 100) {
+      match[bestIdx2] = i;
+      claimed[bestIdx2] = 1;
+      nmatches++;
+      if (check_ori) {
+        float rot = P->angle[i] - F->keys_un[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == HISTO) bin = 0;
+        rotHist[bin].push_back(bestIdx2);
+      }
+    }
+  }
+  if (check_ori) {
+    int hs[30];
+    for (int b = 0; b < HISTO; b++) hs[b] = (int)rotHist[b].size();
+    int ind1, ind2, ind3;
+    three_maxima(hs, HISTO, &ind1, &ind2, &ind3);
+    for (int b = 0; b < HISTO; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (int idx : rotHist[b]) {
+        match[idx] = -1;
+        nmatches--;
+      }
+    }
+  }
+  return nmatches;
+}
+
+}  // extern "C"

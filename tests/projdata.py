@@ -1,0 +1,51 @@
+"""Inputs for the tracking-search tests: a current frame extracted by the oracle and map
+points derived from the previous synthetic frame's features (descriptors with a few bits
+flipped, projections jittered around where the feature moved), seeded."""
+import numpy as np
+
+from ar_orbslam2_amd import synth
+from oracle import oracle as O
+
+
+def frame_dict(kps, desc, w, h, scale, u_right=None, has_mp_obs=None):
+    return dict(keys_un=kps, desc=desc, u_right=u_right, has_mp_obs=has_mp_obs,
+                min_x=0.0, min_y=0.0, max_x=float(w), max_y=float(h),
+                grid_w_inv=float(np.float32(64) / np.float32(w)),
+                grid_h_inv=float(np.float32(48) / np.float32(h)), scale_factors=scale)
+
+
+def scene(w=640, h=480, nf=1000, t=5, seed=0, stereo=False, mp_frac=0.1):
+    p = O.params(nf)
+    tb = O.tables(p, w, h)
+    base = synth.canvas(w, h, 2)
+    prev = synth.frame(w, h, t - 1, 2, base)
+    cur = synth.frame(w, h, t, 2, base)
+    kp0, d0 = O.extract(prev, p)
+    kp1, d1 = O.extract(cur, p)
+    rng = np.random.default_rng(seed)
+    n1 = len(kp1)
+    u_right = None
+    if stereo:
+        u_right = np.where(rng.random(n1) < 0.6, kp1["x"] - rng.uniform(2, 30, n1),
+                           -1.0).astype(np.float32)
+    has = (rng.random(n1) < mp_frac).astype(np.uint8)
+    F = frame_dict(kp1, d1, w, h, tb["scale"], u_right, has)
+    # frame t is the canvas crop at (t mod 17, t mod 11): features move by (-1, -1)
+    n0 = len(kp0)
+    dx = np.float32(-1.0) + rng.normal(0, 1.0, n0).astype(np.float32)
+    dy = np.float32(-1.0) + rng.normal(0, 1.0, n0).astype(np.float32)
+    desc = d0.copy()
+    flips = rng.integers(0, 256, (n0, 6))
+    for k in range(6):
+        desc[np.arange(n0), flips[:, k] // 8] ^= (1 << (flips[:, k] % 8)).astype(np.uint8)
+    x = (kp0["x"] + dx).astype(np.float32)
+    y = (kp0["y"] + dy).astype(np.float32)
+    disp = rng.uniform(2, 30, n0).astype(np.float32)
+    pts = dict(track=(rng.random(n0) < 0.9).astype(np.uint8), proj_x=x, proj_y=y,
+               proj_xr=(x - disp).astype(np.float32),
+               pred_level=np.clip(kp0["octave"] + rng.integers(-1, 2, n0), 0, 7).astype(np.int32),
+               view_cos=rng.uniform(0.99, 1.0, n0).astype(np.float32), desc=desc)
+    last = dict(valid=(rng.random(n0) < 0.85).astype(np.uint8), u=x, v=y,
+                ur=(x - disp).astype(np.float32), octave=kp0["octave"].astype(np.int32),
+                angle=kp0["angle"].astype(np.float32), desc=desc)
+    return F, pts, last

@@ -1,0 +1,198 @@
+"""The tracking-search restatement (oracle/projection_oracle.cc) against a second restatement
+written here in Python/float32, line by line from ORB_SLAM2/src/Frame.cc:235-398 and
+ORB_SLAM2/src/ORBmatcher.cc:45-137, 1331-1474, 1604-1645.  CPU only."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+from projdata import scene
+
+F32 = np.float32
+
+
+def grid(F):
+    g = {}
+    for i, k in enumerate(F["keys_un"]):
+        px = int(np.round(F32(F32(k["x"]) - F32(F["min_x"])) * F32(F["grid_w_inv"])))
+        py = int(np.round(F32(F32(k["y"]) - F32(F["min_y"])) * F32(F["grid_h_inv"])))
+        # std::round is half away from zero; np.round is half-even: fix the .5 cases
+        for axis, (v, c) in enumerate(((k["x"], F["min_x"]), (k["y"], F["min_y"]))):
+            t = F32(F32(v) - F32(c)) * F32(F["grid_w_inv"] if axis == 0 else F["grid_h_inv"])
+            r = math.floor(abs(float(t)) + 0.5) * (1 if t >= 0 else -1)
+            if axis == 0:
+                px = r
+            else:
+                py = r
+        if 0 <= px < 64 and 0 <= py < 48:
+            g.setdefault((px, py), []).append(i)
+    return g
+
+
+def in_area(F, g, x, y, r, minLevel=-1, maxLevel=-1):
+    x, y, r = F32(x), F32(y), F32(r)
+    gw, gh = F32(F["grid_w_inv"]), F32(F["grid_h_inv"])
+    mx, my = F32(F["min_x"]), F32(F["min_y"])
+    x0 = max(0, int(math.floor(F32(F32(x - mx) - r) * gw)))
+    if x0 >= 64:
+        return []
+    x1 = min(63, int(math.ceil(F32(F32(x - mx) + r) * gw)))
+    if x1 < 0:
+        return []
+    y0 = max(0, int(math.floor(F32(F32(y - my) - r) * gh)))
+    if y0 >= 48:
+        return []
+    y1 = min(47, int(math.ceil(F32(F32(y - my) + r) * gh)))
+    if y1 < 0:
+        return []
+    check = minLevel > 0 or maxLevel >= 0
+    out = []
+    for ix in range(x0, x1 + 1):
+        for iy in range(y0, y1 + 1):
+            for i in g.get((ix, iy), []):
+                k = F["keys_un"][i]
+                if check and (k["octave"] < minLevel or (maxLevel >= 0 and k["octave"] > maxLevel)):
+                    continue
+                if abs(F32(k["x"]) - x) < r and abs(F32(k["y"]) - y) < r:
+                    out.append(i)
+    return out
+
+
+def ham(a, b):
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def py_local(F, P, th, nnratio):
+    g = grid(F)
+    n = len(F["keys_un"])
+    claimed = [bool(F["has_mp_obs"][i]) for i in range(n)]
+    match = [-1] * n
+    nm = 0
+    sc = F["scale_factors"]
+    for i in range(len(P["track"])):
+        if not P["track"][i]:
+            continue
+        lev = int(P["pred_level"][i])
+        r = F32(2.5) if float(P["view_cos"][i]) > 0.998 else F32(4.0)
+        if th != 1.0:
+            r = F32(r * F32(th))
+        rs = F32(r * F32(sc[lev]))
+        idxs = in_area(F, g, P["proj_x"][i], P["proj_y"][i], rs, lev - 1, lev)
+        bd, bl, bd2, bl2, bi = 256, -1, 256, -1, -1
+        for idx in idxs:
+            if claimed[idx]:
+                continue
+            if F["u_right"] is not None and F["u_right"][idx] > 0:
+                if abs(F32(P["proj_xr"][i]) - F32(F["u_right"][idx])) > rs:
+                    continue
+            d = ham(P["desc"][i], F["desc"][idx])
+            if d < bd:
+                bd2, bd, bl2, bl, bi = bd, d, bl, int(F["keys_un"][idx]["octave"]), idx
+            elif d < bd2:
+                bl2, bd2 = int(F["keys_un"][idx]["octave"]), d
+        if bd <= 100:
+            if bl == bl2 and F32(bd) > F32(nnratio) * F32(bd2):
+                continue
+            match[bi] = i
+            claimed[bi] = True
+            nm += 1
+    return nm, np.array(match, np.int32)
+
+
+def py_last(F, L, th, fwd, bwd, ori):
+    g = grid(F)
+    n = len(F["keys_un"])
+    claimed = [bool(F["has_mp_obs"][i]) for i in range(n)]
+    match = [-1] * n
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for i in range(len(L["valid"])):
+        if not L["valid"][i]:
+            continue
+        u, v = F32(L["u"][i]), F32(L["v"][i])
+        if u < F["min_x"] or u > F["max_x"] or v < F["min_y"] or v > F["max_y"]:
+            continue
+        o = int(L["octave"][i])
+        rad = F32(F32(th) * F32(F["scale_factors"][o]))
+        if fwd:
+            idxs = in_area(F, g, u, v, rad, o, -1)
+        elif bwd:
+            idxs = in_area(F, g, u, v, rad, 0, o)
+        else:
+            idxs = in_area(F, g, u, v, rad, o - 1, o + 1)
+        bd, bi = 256, -1
+        for idx in idxs:
+            if claimed[idx]:
+                continue
+            if F["u_right"] is not None and F["u_right"][idx] > 0:
+                if abs(F32(L["ur"][i]) - F32(F["u_right"][idx])) > rad:
+                    continue
+            d = ham(L["desc"][i], F["desc"][idx])
+            if d < bd:
+                bd, bi = d, idx
+        if bd <= 100:
+            match[bi] = i
+            claimed[bi] = True
+            nm += 1
+            if ori:
+                rot = F32(F32(L["angle"][i]) - F32(F["keys_un"][bi]["angle"]))
+                if rot < 0:
+                    rot = F32(rot + F32(360))
+                t = F32(rot * F32(F32(1) / F32(30)))
+                b = int(math.floor(abs(float(t)) + 0.5))
+                hist[0 if b == 30 else b].append(bi)
+    if ori:
+        m1 = m2 = m3 = 0
+        i1 = i2 = i3 = -1
+        for b in range(30):
+            s = len(hist[b])
+            if s > m1:
+                m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, b
+            elif s > m2:
+                m3, m2, i3, i2 = m2, s, i2, b
+            elif s > m3:
+                m3, i3 = s, b
+        if m2 < F32(0.1) * F32(m1):
+            i2 = i3 = -1
+        elif m3 < F32(0.1) * F32(m1):
+            i3 = -1
+        for b in range(30):
+            if b not in (i1, i2, i3):
+                for idx in hist[b]:
+                    match[idx] = -1
+                    nm -= 1
+    return nm, np.array(match, np.int32)
+
+
+@pytest.mark.parametrize("stereo", [False, True])
+def test_features_in_area_order(stereo):
+    F, P, _ = scene(stereo=stereo)
+    g = grid(F)
+    rng = np.random.default_rng(1)
+    for _ in range(40):
+        x, y = rng.uniform(-20, 660), rng.uniform(-20, 500)
+        r = rng.uniform(1, 60)
+        lo, hi = int(rng.integers(-1, 4)), int(rng.integers(-1, 8))
+        assert O.features_in_area(F, x, y, r, lo, hi).tolist() == in_area(F, g, x, y, r, lo, hi)
+
+
+@pytest.mark.parametrize("stereo,th", [(False, 1.0), (True, 1.0), (False, 3.0), (True, 5.0)])
+def test_search_by_projection_local_map(stereo, th):
+    F, P, _ = scene(stereo=stereo, seed=int(th))
+    n, m = O.search_by_projection(F, P, th, 0.8)
+    pn, pm = py_local(F, P, th, 0.8)
+    assert n == pn and np.array_equal(m, pm)
+    assert n > 200
+
+
+@pytest.mark.parametrize("stereo,th,fwd,bwd,ori", [(False, 7.0, 0, 0, True), (True, 15.0, 0, 0, True),
+                                                  (True, 7.0, 1, 0, True), (True, 7.0, 0, 1, False),
+                                                  (False, 14.0, 0, 0, False)])
+def test_search_by_projection_last_frame(stereo, th, fwd, bwd, ori):
+    F, _, L = scene(stereo=stereo, seed=int(th) + fwd)
+    n, m = O.search_by_projection_last(F, L, th, fwd, bwd, ori)
+    pn, pm = py_last(F, L, th, fwd, bwd, ori)
+    assert n == pn and np.array_equal(m, pm)
+    assert n > 200
