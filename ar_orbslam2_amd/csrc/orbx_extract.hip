@@ -3,7 +3,7 @@
 //
 // One plan = one image size + one parameter set + a maximum batch.  A batch of images runs
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
-//   k_resize      x (nlevels-1)  pyramid level l from level l-1     (cv::resize INTER_LINEAR)
+//   k_pyramid     level 0 copy + every level (cv::resize INTER_LINEAR), one launch, row bands
 //   k_blur        x 1            all levels, 64x16 LDS tiles         (GaussianBlur 7x7 s=2)
 //   k_fast_tile   x 1            64x64 tiles, all levels            (FAST score + cell-local NMS)
 //   k_fast_compact x 1           one wave per FAST cell             (fallback + ordered compaction)
@@ -33,7 +33,7 @@ __constant__ int8_t c_pattern[1024];
 __constant__ int c_umax[kHalfPatch + 1];
 
 // ------------------------------------------------------------------ helpers
-// Every level (level 0 copied in by k_copy0) lives in the image's pitched pyramid block.
+// Every level (level 0 copied in by k_pyramid) lives in the image's pitched pyramid block.
 __device__ __forceinline__ const uint8_t* level_base(const uint8_t* pyr, int64_t pyr_bytes,
                                                      const LevelGeom& g, int img) {
   return pyr + (int64_t)img * pyr_bytes + g.pyr_off;
@@ -153,113 +153,111 @@ __device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
   return total;
 }
 
-// ------------------------------------------------------------------ k_copy0
-// Level 0 = the input image (ComputePyramid level 0, ORBextractor.cc:1066-1068) copied into the
-// 64-B pitched pyramid block so every later kernel reads aligned dwords.
-__global__ __launch_bounds__(256) void k_copy0(const uint8_t* __restrict__ in,
-                                               uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-                                               const LevelGeom* __restrict__ lv) {
-  const LevelGeom& G = lv[0];
-  const int img = blockIdx.z, y = blockIdx.y;
-  const int x4 = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (x4 >= G.w) return;
-  const uint8_t* src = in + ((int64_t)img * G.h + y) * G.w + x4;
-  uint32_t v = src[0];
-  if (x4 + 1 < G.w) v |= (uint32_t)src[1] << 8;
-  if (x4 + 2 < G.w) v |= (uint32_t)src[2] << 16;
-  if (x4 + 3 < G.w) v |= (uint32_t)src[3] << 24;
-  *(uint32_t*)(pyr + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch + x4) = v;
-}
-
-// ------------------------------------------------------------------ k_resize
-// cv::resize(level l-1 ROI -> level l ROI, INTER_LINEAR), 8UC1 fixed point, the
-// way OpenCV's resizeGeneric_ runs it: horizontal pass once per source row into int buffers
-// (HResizeLinear, taps Q11), then the vertical pass per output row (VResizeLinear: SSE2
-// mulhi form for x < vxs, scalar (H0*b0 + H1*b1 + 2^21) >> 22 tail).
-// One workgroup = kRzRows output rows x kRzCols output columns of one image: the source
-// window is staged in LDS with aligned dword loads, the horizontal sums of each source row
-// it needs are computed once into LDS, then every thread writes 4 output pixels per row as
-// one dword.
-
-__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-                                                const LevelGeom* __restrict__ lv, int level,
-                                                int ncolblk,
-                                                const int* __restrict__ xofs,
-                                                const int16_t* __restrict__ xa,
-                                                const int* __restrict__ yofs,
-                                                const int16_t* __restrict__ yb) {
-  __shared__ __align__(16) uint32_t s_src[kRzSrcRows][kRzSrcWords];
-  __shared__ __align__(16) int s_h[kRzSrcRows][kRzCols];
-  const LevelGeom& D = lv[level];
-  const LevelGeom& S = lv[level - 1];
-  int bx, img;
-  xcd_block(bx, img);
-  const int band = bx / ncolblk, cb = bx - band * ncolblk;
-  const int R0 = band * kRzRows, C0 = cb * kRzCols;
-  const int R1 = min(R0 + kRzRows, D.h), C1 = min(C0 + kRzCols, D.w);
+// ------------------------------------------------------------------ k_pyramid
+// ComputePyramid (ORBextractor.cc:1047-1072) in one launch: one workgroup per (image, row
+// band) copies its level-0 rows into the 64-B pitched pyramid block (every later kernel reads
+// aligned dwords) and then builds every level of its band from the previous one with
+// cv::resize INTER_LINEAR 8UC1: horizontal Q11 taps, vertical SSE2 mulhi form for
+// x < vxs, scalar (H0*b0 + H1*b1 + 2^21) >> 22 tail.  Bands overlap by the rows the next level
+// needs (Geometry::bands), so no band waits for another: a row two bands share is computed by
+// both, to the same bytes.  A level step runs in chunks of kPyRows x kPyCols outputs whose
+// source window is staged in LDS with aligned dword loads; a thread owns one 4-pixel column
+// group of the chunk (its taps loaded once) and walks the rows.
+__global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ in,
+                                                 uint8_t* __restrict__ pyr, int64_t pyr_bytes,
+                                                 const LevelGeom* __restrict__ lv, int nlevels,
+                                                 const PyrBand* __restrict__ bands,
+                                                 const int* __restrict__ xofs,
+                                                 const int16_t* __restrict__ xa,
+                                                 const int* __restrict__ yofs,
+                                                 const int16_t* __restrict__ yb) {
+  __shared__ __align__(16) uint32_t s_src[kPySrcRows * kPySrcWords];
+  int band, img;
+  xcd_block(band, img);
+  const PyrBand& B = bands[band];
   const int tid = threadIdx.x;
-  const uint8_t* src = level_base(pyr, pyr_bytes, S, img);
-  uint8_t* dst = pyr + (int64_t)img * pyr_bytes + D.pyr_off;
-  // source window: rows clamp(yofs(R0)) .. clamp(yofs(R1-1)+1), bytes xofs(C0) .. xofs(C1-1)+1
-  const int ys_lo = min(max(yofs[D.coef_y + R0], 0), S.h - 1);
-  const int ys_hi = min(max(yofs[D.coef_y + R1 - 1] + 1, 0), S.h - 1);
-  const int nrows = ys_hi - ys_lo + 1;
-  const int xw_lo = xofs[D.coef_x + C0] & ~3;
-  const int xw_hi = xofs[D.coef_x + C1 - 1] + 1;
-  const int nwords = (xw_hi - xw_lo) / 4 + 1;
-  if (nrows > kRzSrcRows || nwords > kRzSrcWords) return;  // excluded by build_geometry
-  for (int i = tid; i < nrows * nwords; i += 256) {
-    const int r = i / nwords, c = i - r * nwords;
-    s_src[r][c] = *(const uint32_t*)(src + (int64_t)(ys_lo + r) * S.pitch + xw_lo + 4 * c);
-  }
-  __syncthreads();
-  // horizontal pass: thread = output column
-  {
-    const int dx = C0 + tid;
-    if (dx < C1) {
-      const int x0 = xofs[D.coef_x + dx] - xw_lo;
-      const int a0 = xa[2 * (D.coef_x + dx)], a1 = xa[2 * (D.coef_x + dx) + 1];
-      const uint8_t* sb = (const uint8_t*)s_src;
-      if (dx < D.xmax) {
-        for (int r = 0; r < nrows; r++)  // 24-bit multiplies: u8 x Q11 tap
-          s_h[r][tid] = __mul24(sb[r * kRzSrcWords * 4 + x0], a0) +
-                        __mul24(sb[r * kRzSrcWords * 4 + x0 + 1], a1);
-      } else {
-        for (int r = 0; r < nrows; r++) s_h[r][tid] = sb[r * kRzSrcWords * 4 + x0] * 2048;
-      }
+  uint8_t* base = pyr + (int64_t)img * pyr_bytes;
+  {  // level 0: the input rows of the band (ORBextractor.cc:1066-1068)
+    const LevelGeom& G = lv[0];
+    const uint8_t* src = in + (int64_t)img * G.h * G.w;
+    const int q4 = (G.w + 3) >> 2, lo = B.lo[0], nr = B.hi[0] - lo;
+    for (int i = tid; i < nr * q4; i += 256) {
+      const int r = i / q4, x4 = (i - r * q4) * 4, y = lo + r;
+      const uint8_t* s = src + (int64_t)y * G.w + x4;
+      uint32_t v = s[0];
+      if (x4 + 1 < G.w) v |= (uint32_t)s[1] << 8;
+      if (x4 + 2 < G.w) v |= (uint32_t)s[2] << 16;
+      if (x4 + 3 < G.w) v |= (uint32_t)s[3] << 24;
+      *(uint32_t*)(base + G.pyr_off + (uint32_t)(y * G.pitch + x4)) = v;
     }
   }
-  __syncthreads();
-  // vertical pass: 64 threads per output row, 4 adjacent columns each
-  const int q = tid & 63;
-  const int c4 = C0 + 4 * q;
-  if (c4 >= C1) return;
-  for (int dy = R0 + (tid >> 6); dy < R1; dy += 4) {
-    const int sy0 = yofs[D.coef_y + dy];
-    const int ra = min(max(sy0, 0), S.h - 1) - ys_lo;
-    const int rb = min(max(sy0 + 1, 0), S.h - 1) - ys_lo;
-    const int b0 = yb[2 * (D.coef_y + dy)], b1 = yb[2 * (D.coef_y + dy) + 1];
-    const int4 H0 = *(const int4*)&s_h[ra][4 * q];
-    const int4 H1 = *(const int4*)&s_h[rb][4 * q];
-    const int h0[4] = {H0.x, H0.y, H0.z, H0.w}, h1[4] = {H1.x, H1.y, H1.z, H1.w};
-    uint32_t out = 0;
+  const uint8_t* sb = (const uint8_t*)s_src;
+  constexpr int RS = kPySrcWords * 4;  // staged row stride (bytes)
+  for (int l = 1; l < nlevels; l++) {
+    __syncthreads();  // level l-1 of this band written (and the LDS window free)
+    const LevelGeom& D = lv[l];
+    const LevelGeom& S = lv[l - 1];
+    const uint8_t* sp = base + S.pyr_off;
+    uint8_t* dp = base + D.pyr_off;
+    for (int r0 = B.lo[l]; r0 < B.hi[l]; r0 += kPyRows) {
+      const int r1 = min(r0 + kPyRows, B.hi[l]);
+      const int ys_lo = min(max(yofs[D.coef_y + r0], 0), S.h - 1);
+      const int ys_hi = min(max(yofs[D.coef_y + r1 - 1] + 1, 0), S.h - 1);
+      const int nrows = ys_hi - ys_lo + 1;
+      for (int c0 = 0; c0 < D.w; c0 += kPyCols) {
+        const int c1 = min(c0 + kPyCols, D.w);
+        const int xw_lo = xofs[D.coef_x + c0] & ~3;
+        const int nwords = (xofs[D.coef_x + c1 - 1] + 1 - xw_lo) / 4 + 1;
+        if (nrows > kPySrcRows || nwords > kPySrcWords) return;  // excluded by build_geometry
+        __syncthreads();
+        for (int i = tid; i < nrows * nwords; i += 256) {
+          const int r = i / nwords, c = i - r * nwords;
+          s_src[r * kPySrcWords + c] =
+              *(const uint32_t*)(sp + (uint32_t)((ys_lo + r) * S.pitch + xw_lo + 4 * c));
+        }
+        __syncthreads();
+        const int ngroups = (c1 - c0 + 3) >> 2;
+        for (int g = tid; g < ngroups * 2; g += 256) {  // 2 rows of groups per 256 threads
+          const int q = g >> 1, rpar = g & 1;
+          const int dx0 = c0 + 4 * q;
+          int x0[4], a0[4], a1[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      int v;
-      if (c4 + k < D.vxs) {
-        const int t0 = max(-32768, min(32767, h0[k] >> 4));
-        const int t1 = max(-32768, min(32767, h1[k] >> 4));
-        int m = (__mul24(t0, b0) >> 16) + (__mul24(t1, b1) >> 16);  // |t|, |b| < 2^15
-        m = max(-32768, min(32767, m));
-        m = max(-32768, min(32767, m + 2));
-        v = m >> 2;
-      } else {
-        v = (__mul24(h0[k], b0) + __mul24(h1[k], b1) + (1 << 21)) >> 22;  // h < 2^20, b <= 2^11
+          for (int k = 0; k < 4; k++) {
+            const int dx = min(dx0 + k, D.w - 1);
+            x0[k] = xofs[D.coef_x + dx] - xw_lo;
+            a0[k] = dx < D.xmax ? xa[2 * (D.coef_x + dx)] : 2048;
+            a1[k] = dx < D.xmax ? xa[2 * (D.coef_x + dx) + 1] : 0;
+          }
+          for (int dy = r0 + rpar; dy < r1; dy += 2) {
+            const int sy0 = yofs[D.coef_y + dy];
+            const int ra = (min(max(sy0, 0), S.h - 1) - ys_lo) * RS;
+            const int rb = (min(max(sy0 + 1, 0), S.h - 1) - ys_lo) * RS;
+            const int b0 = yb[2 * (D.coef_y + dy)], b1 = yb[2 * (D.coef_y + dy) + 1];
+            uint32_t out = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              // HResizeLinear (a1 = 0 past xmax: S[x0] * 2048)
+              const int h0 = __mul24((int)sb[ra + x0[k]], a0[k]) + __mul24((int)sb[ra + x0[k] + 1], a1[k]);
+              const int h1 = __mul24((int)sb[rb + x0[k]], a0[k]) + __mul24((int)sb[rb + x0[k] + 1], a1[k]);
+              int v;
+              if (dx0 + k < D.vxs) {  // VResizeLinearVec_32s8u
+                const int t0 = max(-32768, min(32767, h0 >> 4));
+                const int t1 = max(-32768, min(32767, h1 >> 4));
+                int m = (__mul24(t0, b0) >> 16) + (__mul24(t1, b1) >> 16);  // |t|, |b| < 2^15
+                m = max(-32768, min(32767, m));
+                m = max(-32768, min(32767, m + 2));
+                v = m >> 2;
+              } else {
+                v = (__mul24(h0, b0) + __mul24(h1, b1) + (1 << 21)) >> 22;  // h < 2^20, b <= 2^11
+              }
+              out |= (uint32_t)max(0, min(255, v)) << (8 * k);
+            }
+            // pitch >= w + 4: bytes past w of the last group land in the row's pad
+            *(uint32_t*)(dp + (uint32_t)(dy * D.pitch + dx0)) = out;
+          }
+        }
       }
-      out |= (uint32_t)max(0, min(255, v)) << (8 * k);
     }
-    // pitch is a multiple of 64, so bytes past w of the last dword land in the row's pad
-    *(uint32_t*)(dst + (int64_t)dy * D.pitch + c4) = out;
   }
 }
 
@@ -1084,10 +1082,12 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
 }
 
 // ------------------------------------------------------------------ k_describe
-// One wave per retained keypoint: IC_Angle on the unblurred level (ORBextractor.cc:73-98),
-// cv::fastAtan2, glibc sincosf, rBRIEF on the blurred level with the reference binary's
-// fmaf + cvRound sampling (ORBextractor.cc:101-144), then the level-0 scaling of
-// operator() (:1035-1041).  Output is level-major like `_keypoints`/`descriptors`.
+// One half-wave (32 lanes) per retained keypoint, 8 keypoints per workgroup: IC_Angle on the
+// unblurred level (ORBextractor.cc:73-98), cv::fastAtan2, glibc sincosf, rBRIEF on the blurred
+// level with the reference binary's fmaf + cvRound sampling (ORBextractor.cc:101-144, SURVEY
+// A.6) — lane j produces descriptor byte j from pairs 8j..8j+7 — then the level-0 scaling of
+// operator() (:1035-1041).  Output is level-major like `_keypoints`/`descriptors`.  Two
+// keypoints per wave share the per-keypoint scalar work (angle, sincos, addressing).
 struct KpOffsets {  // per-level first keypoint slot (LevelGeom::kp_off), by value
   int off[kMaxLevels + 1];
 };
@@ -1097,93 +1097,94 @@ __global__ __launch_bounds__(256) void k_describe(
     const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const uint32_t* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
+  constexpr int RW = 10, BW = 11;  // dwords per staged row (31+3 / 37+3 bytes, rounded up)
+  constexpr int RN = 31 * RW, BN = 37 * BW;
+  __shared__ uint32_t s_raw[8][RN];
+  __shared__ uint32_t s_blr[8][BN];
   int bx, img;
   xcd_block(bx, img);
-  const int lane = threadIdx.x & 63;
-  const int slot = bx * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int hw = threadIdx.x >> 5;  // half-wave of the workgroup, 0..7
+  const int slot = bx * 8 + hw;
   const int* oc = ocount + img * nlevels;
   if (bx == 0 && threadIdx.x == 0) {
     int t = 0;
     for (int l = 0; l < nlevels; l++) t += oc[l];
     counts[img] = t;
   }
-  if (slot >= kp_total) return;
   int level = 0;
 #pragma unroll
   for (int l = 1; l < kMaxLevels; l++) level += (l < nlevels && slot >= ko.off[l]);
   const LevelGeom& G = lv[level];
-  const int idx = slot - G.kp_off;
-  if (idx >= oc[level]) return;
-  int outpos = idx;
-  for (int l = 0; l < level; l++) outpos += oc[l];
-  const uint32_t key = okey[(int64_t)img * kp_total + slot];
-  const int cx = (int)(key & 0xFFF) + (kEdge - 3), cy = (int)((key >> 12) & 0xFFF) + (kEdge - 3);
-  const float response = (float)(key >> 24);
-  // Stage both patches with aligned dword loads issued together: the raw 31 x 31 patch
-  // (IC_Angle, radius 15) and the blurred 37 x 37 patch (rBRIEF samples, radius <= 18).  The
-  // sample positions depend on the angle, so fetching the whole blurred patch up front hides
-  // that gather behind the first one.
-  constexpr int RW = 10, BW = 11;  // dwords per staged row (31+3 / 37+3 bytes, rounded up)
-  __shared__ uint32_t s_raw[4][31 * RW];
-  __shared__ uint32_t s_blr[4][37 * BW];
-  const int wv = threadIdx.x >> 6;
+  const int idx = slot - ko.off[level];
+  const bool active = slot < kp_total && idx < oc[level];  // uniform within the half-wave
+  int cx = 0, cy = 0;
+  uint32_t key = 0;
+  if (active) {
+    key = okey[(int64_t)img * kp_total + slot];
+    cx = (int)(key & 0xFFF) + (kEdge - 3);
+    cy = (int)((key >> 12) & 0xFFF) + (kEdge - 3);
+  }
+  // stage both patches with aligned dword loads issued together: the raw 31 x 31 patch
+  // (IC_Angle, radius 15) and the blurred 37 x 37 patch (rBRIEF samples, radius <= 18)
   const uint8_t* L = level_base(pyr, pyr_bytes, G, img);
-  const uint8_t* B = blur + (int64_t)img * pyr_bytes + G.pyr_off;
+  const uint8_t* Bp = blur + (int64_t)img * pyr_bytes + G.pyr_off;
   const int fr = (cx - 15) >> 2, lr = (cx + 15) >> 2;  // raw dword columns
   const int fb = (cx - 18) >> 2, lb = (cx + 18) >> 2;  // blurred dword columns
-  uint32_t vr[5], vb[7];
+  if (active) {
+    uint32_t vr[(RN + 31) / 32], vb[(BN + 31) / 32];
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const int i = lane + 64 * k, r = i / RW, c = i - r * RW;
-    vr[k] = (i < 31 * RW && fr + c <= lr)
-                ? *(const uint32_t*)(L + (uint32_t)((cy - 15 + r) * G.pitch + 4 * (fr + c))) : 0u;
+    for (int k = 0; k < (RN + 31) / 32; k++) {
+      const int i = hl + 32 * k, r = i / RW, c = i - r * RW;
+      vr[k] = (i < RN && fr + c <= lr)
+                  ? *(const uint32_t*)(L + (uint32_t)((cy - 15 + r) * G.pitch + 4 * (fr + c)))
+                  : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < (BN + 31) / 32; k++) {
+      const int i = hl + 32 * k, r = i / BW, c = i - r * BW;
+      vb[k] = (i < BN && fb + c <= lb)
+                  ? *(const uint32_t*)(Bp + (uint32_t)((cy - 18 + r) * G.pitch + 4 * (fb + c)))
+                  : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < (RN + 31) / 32; k++)
+      if (hl + 32 * k < RN) s_raw[hw][hl + 32 * k] = vr[k];
+#pragma unroll
+    for (int k = 0; k < (BN + 31) / 32; k++)
+      if (hl + 32 * k < BN) s_blr[hw][hl + 32 * k] = vb[k];
   }
-#pragma unroll
-  for (int k = 0; k < 7; k++) {
-    const int i = lane + 64 * k, r = i / BW, c = i - r * BW;
-    vb[k] = (i < 37 * BW && fb + c <= lb)
-                ? *(const uint32_t*)(B + (uint32_t)((cy - 18 + r) * G.pitch + 4 * (fb + c))) : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < 5; k++)
-    if (lane + 64 * k < 31 * RW) s_raw[wv][lane + 64 * k] = vr[k];
-#pragma unroll
-  for (int k = 0; k < 7; k++)
-    if (lane + 64 * k < 37 * BW) s_blr[wv][lane + 64 * k] = vb[k];
-  const uint8_t* raw = (const uint8_t*)s_raw[wv] + 15 * (4 * RW) + (cx - 4 * fr);  // center
-  const uint8_t* bc = (const uint8_t*)s_blr[wv] + 18 * (4 * BW) + (cx - 4 * fb);
   constexpr int RS = 4 * RW, BS = 4 * BW;
-  // IC_Angle (ORBextractor.cc:73-98): lanes 0..30 rows v = 0..7, lanes 32..62 rows v = 8..15
+  const uint8_t* raw = (const uint8_t*)s_raw[hw] + 15 * RS + (cx - 4 * fr);  // centre
+  const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - 4 * fb);
+  // IC_Angle (ORBextractor.cc:73-98): lane hl < 31 is column u = hl - 15, rows v = 0..15
   int m10 = 0, m01 = 0;
-  const int u = (lane & 31) - 15;
-  if ((lane & 31) < 31) {
-    const int vb0 = lane < 32 ? 0 : 8, ve = lane < 32 ? 8 : 16;
-    for (int v = vb0; v < ve; v++) {
+  if (active && hl < 31) {
+    const int u = hl - 15;
+    m10 = __mul24(u, (int)raw[u]);
+    for (int v = 1; v <= kHalfPatch; v++) {
       const int d = c_umax[v];
       if (u < -d || u > d) continue;
-      if (v == 0) {
-        m10 += __mul24(u, (int)raw[u]);
-      } else {
-        const int vp = raw[u + __mul24(v, RS)], vm = raw[u - __mul24(v, RS)];
-        m10 += __mul24(u, vp + vm);
-        m01 += __mul24(v, vp - vm);
-      }
+      const int vp = raw[u + __mul24(v, RS)], vm = raw[u - __mul24(v, RS)];
+      m10 += __mul24(u, vp + vm);
+      m01 += __mul24(v, vp - vm);
     }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
+  for (int o = 16; o > 0; o >>= 1) {  // within the half-wave
     m10 += __shfl_xor(m10, o);
     m01 += __shfl_xor(m01, o);
   }
+  if (!active) return;
   const float angle = orbx_fast_atan2((float)m01, (float)m10);
-  // descriptor on the blurred level
+  // descriptor on the blurred level: byte hl from pairs 8 hl .. 8 hl + 7, LSB first
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float sn, cs;
   orbx_sincosf(angle * factorPI, &sn, &cs);
-  int nib = 0;
+  uint32_t byte = 0;
 #pragma unroll
-  for (int m = 0; m < 4; m++) {
-    const int pair = lane * 4 + m;
+  for (int m = 0; m < 8; m++) {
+    const int pair = hl * 8 + m;
     int t[2];
 #pragma unroll
     for (int e = 0; e < 2; e++) {
@@ -1193,18 +1194,19 @@ __global__ __launch_bounds__(256) void k_describe(
       const int col = (int)__builtin_rintf(__builtin_fmaf(px, cs, -(py * sn)));
       t[e] = bc[__mul24(row, BS) + col];
     }
-    nib |= (t[0] < t[1]) << m;
+    byte |= (uint32_t)(t[0] < t[1]) << m;
   }
-  const int other = __shfl_xor(nib, 1);
+  int outpos = idx;
+  for (int l = 0; l < level; l++) outpos += oc[l];
   const int64_t o = (int64_t)img * kp_total + outpos;
-  if ((lane & 1) == 0) desc[o * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
-  if (lane == 0) {
+  desc[o * 32 + hl] = (uint8_t)byte;
+  if (hl == 0) {
     orbx_keypoint k;
     k.x = level ? (float)(cx) * G.scale : (float)cx;
     k.y = level ? (float)(cy) * G.scale : (float)cy;
     k.size = G.size;
     k.angle = angle;
-    k.response = response;
+    k.response = (float)(key >> 24);
     k.octave = level;
     k.class_id = -1;
     kps[o] = k;
@@ -1228,6 +1230,7 @@ struct orbx_plan {
   int16_t *d_xa = nullptr, *d_yb = nullptr;
   BlurTile* d_tiles = nullptr;
   int ntiles = 0;
+  PyrBand* d_bands = nullptr;
   FastTile* d_ftiles = nullptr;
   int nftiles = 0;
   uint8_t* d_vmap = nullptr;
@@ -1263,26 +1266,14 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   const int L = g.nlevels;
   Profiler dummy;
   Profiler& pr = prof ? *prof : dummy;
-  const int st_copy = pr.stage("k_copy0"), st_resize = pr.stage("k_resize"),
+  const int st_pyr = pr.stage("k_pyramid"),
             st_blur = pr.stage("k_blur"), st_fs = pr.stage("k_fast_tile"),
             st_fast = pr.stage("k_fast_compact"),
             st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe");
   pr.mark(P->stream, -1);
-  {
-    const LevelGeom& G = g.lv[0];
-    dim3 grid((G.w / 4 + 256) / 256, G.h, n);
-    hipLaunchKernelGGL(k_copy0, grid, dim3(256), 0, P->stream, d_in, P->d_pyr, g.pyr_bytes,
-                       P->d_lv);
-    pr.mark(P->stream, st_copy);
-  }
-  for (int l = 1; l < L; l++) {
-    const LevelGeom& D = g.lv[l];
-    const int ncolblk = (D.w + kRzCols - 1) / kRzCols;
-    dim3 grid(ncolblk * ((D.h + kRzRows - 1) / kRzRows), n);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, P->stream, P->d_pyr, g.pyr_bytes, P->d_lv, l,
-                       ncolblk, P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
-    pr.mark(P->stream, st_resize);
-  }
+  hipLaunchKernelGGL(k_pyramid, dim3(g.nbands, n), dim3(256), 0, P->stream, d_in, P->d_pyr,
+                     g.pyr_bytes, P->d_lv, L, P->d_bands, P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
+  pr.mark(P->stream, st_pyr);
   if (P->ntiles > 0) {
     hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles);
@@ -1306,7 +1297,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
-  hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 3) / 4, n), dim3(256), 0, P->stream,
+  hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 7) / 8, n), dim3(256), 0, P->stream,
                      P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, ko, P->d_okey, P->d_ocount,
                      g.kp_total, P->d_kps, P->d_desc, P->d_counts);
   pr.mark(P->stream, st_desc);
@@ -1380,7 +1371,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, g.cells.size()) ||
       dalloc(&P->d_xofs, g.xofs.size()) || dalloc(&P->d_yofs, g.yofs.size()) ||
       dalloc(&P->d_xa, g.xa.size()) || dalloc(&P->d_yb, g.yb.size()) ||
-      dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_ftiles, ftiles.size()) ||
+      dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_bands, (size_t)g.nbands) || dalloc(&P->d_ftiles, ftiles.size()) ||
       dalloc(&P->d_vmap, B * g.pyr_bytes) || dalloc(&P->d_bitmaps, B * g.bm_words) ||
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
@@ -1398,6 +1389,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       up(P->d_yofs, g.yofs.data(), 4 * g.yofs.size()) ||
       up(P->d_xa, g.xa.data(), 2 * g.xa.size()) || up(P->d_yb, g.yb.data(), 2 * g.yb.size()) ||
       up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
+      up(P->d_bands, g.bands, sizeof(PyrBand) * g.nbands) ||
       up(P->d_ftiles, ftiles.data(), sizeof(FastTile) * ftiles.size()))
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
@@ -1425,7 +1417,7 @@ int orbx_plan_destroy(orbx_plan* P) {
   if (!P) return ORBX_OK;
   if (P->graph) hipGraphExecDestroy(P->graph);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xofs,   P->d_yofs,  P->d_xa,
-                  P->d_yb,  P->d_tiles, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
+                  P->d_yb,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label,
                   P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
   for (void* p : ptrs)

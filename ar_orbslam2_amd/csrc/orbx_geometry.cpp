@@ -207,24 +207,44 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     kp += L.kp_cap;
     g->node_cap_max = std::max(g->node_cap_max, L.node_cap);
   }
-  // k_resize source windows (kRzRows x kRzCols output tiles) must fit its LDS staging
+  // k_pyramid row bands: band b owns rows [b*h_l/nb, (b+1)*h_l/nb) of every level and
+  // computes, going down from the top level, the rows the next level's rows need as well
+  // (rows shared by two bands are computed by both, identically)
+  g->nbands = std::min(kMaxBands, std::max(1, h / kPyBandH));
+  for (int b = 0; b < g->nbands; b++) {
+    PyrBand& B = g->bands[b];
+    for (int l = 0; l < p.nlevels; l++) {
+      B.lo[l] = (int)((int64_t)b * g->lv[l].h / g->nbands);
+      B.hi[l] = (int)((int64_t)(b + 1) * g->lv[l].h / g->nbands);
+    }
+    for (int l = p.nlevels - 1; l >= 1; l--) {
+      const LevelGeom& D = g->lv[l];
+      const LevelGeom& S = g->lv[l - 1];
+      if (B.hi[l] <= B.lo[l]) continue;
+      const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
+      const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
+      B.lo[l - 1] = std::min(B.lo[l - 1], slo);
+      B.hi[l - 1] = std::max(B.hi[l - 1], shi);
+    }
+  }
+  // k_pyramid chunks (kPyRows x kPyCols output pixels) must find their source window in LDS
   for (int l = 1; l < p.nlevels; l++) {
     const LevelGeom& D = g->lv[l];
     const LevelGeom& S = g->lv[l - 1];
-    for (int r0 = 0; r0 < D.h; r0 += kRzRows) {
-      const int r1 = std::min(r0 + kRzRows, D.h);
+    for (int r0 = 0; r0 < D.h; r0++) {
+      const int r1 = std::min(r0 + kPyRows, D.h);
       const int lo = std::min(std::max(g->yofs[D.coef_y + r0], 0), S.h - 1);
       const int hi = std::min(std::max(g->yofs[D.coef_y + r1 - 1] + 1, 0), S.h - 1);
-      if (hi - lo + 1 > kRzSrcRows) {
-        if (why) *why = "scale factor too large for the resize tile";
+      if (hi - lo + 1 > kPySrcRows) {
+        if (why) *why = "scale factor too large for the pyramid chunk";
         return ORBX_EUNSUPPORTED;
       }
     }
-    for (int c0 = 0; c0 < D.w; c0 += kRzCols) {
-      const int c1 = std::min(c0 + kRzCols, D.w);
+    for (int c0 = 0; c0 < D.w; c0++) {
+      const int c1 = std::min(c0 + kPyCols, D.w);
       const int lo = g->xofs[D.coef_x + c0] & ~3, hi = g->xofs[D.coef_x + c1 - 1] + 1;
-      if ((hi - lo) / 4 + 1 > kRzSrcWords || (hi | 3) >= S.pitch) {
-        if (why) *why = "scale factor too large for the resize tile";
+      if ((hi - lo) / 4 + 1 > kPySrcWords || (hi | 3) >= S.pitch) {
+        if (why) *why = "scale factor too large for the pyramid chunk";
         return ORBX_EUNSUPPORTED;
       }
     }

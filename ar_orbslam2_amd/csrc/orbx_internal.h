@@ -21,11 +21,26 @@ constexpr int kMaxIni = 64;     // initial octree columns supported (nIni)
 
 // Per pyramid level, computed on the host once per plan (ORBextractor.cc:404-460,
 // 735-757, 1047-1072).
-// k_resize workgroup tile: output rows x columns, and the LDS source window it may need
-// (build_geometry rejects scale factors whose windows exceed it)
-constexpr int kRzRows = 16, kRzCols = 256;
-constexpr int kRzSrcRows = 24;
-constexpr int kRzSrcWords = 88;
+// k_pyramid: every image split into row bands, one workgroup per (image, band) builds all
+// levels of its band; a level step runs in chunks of kPyRows x kPyCols output pixels whose
+// source window is staged in LDS (build_geometry rejects scale factors whose windows exceed it)
+#ifndef ORBX_PY_ROWS
+#define ORBX_PY_ROWS 16
+#endif
+#ifndef ORBX_PY_COLS
+#define ORBX_PY_COLS 512
+#endif
+#ifndef ORBX_PY_BANDH
+#define ORBX_PY_BANDH 20
+#endif
+constexpr int kPyRows = ORBX_PY_ROWS, kPyCols = ORBX_PY_COLS;
+constexpr int kPySrcRows = (kPyRows * 13 + 9) / 10 + 3;
+constexpr int kPySrcWords = (kPyCols * 13 / 10 + 8) / 4 + 2;
+constexpr int kPyBandH = ORBX_PY_BANDH;  // level-0 rows per band (at most kMaxBands bands)
+constexpr int kMaxBands = 32;
+struct PyrBand {
+  int lo[kMaxLevels], hi[kMaxLevels];  // rows of each level this band computes (with halo)
+};
 
 struct LevelGeom {
   int w, h;            // level size (cvRound((float)cols * invScale))
@@ -67,6 +82,8 @@ struct Geometry {
   std::vector<int> xofs, yofs;        // resize source offsets
   std::vector<int16_t> xa, yb;        // resize fixed-point coefficients (pairs)
   int64_t pyr_bytes = 0;              // per image
+  int nbands = 1;                     // k_pyramid row bands per image
+  PyrBand bands[kMaxBands];
   int64_t bm_words = 0;               // per image: two keep planes (ini, min) per level
   int cand_total = 0;                 // per image candidate keys
   int kp_total = 0;                   // per image final keypoint slots
