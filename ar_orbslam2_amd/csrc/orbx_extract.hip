@@ -216,41 +216,41 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ in,
               *(const uint32_t*)(sp + (uint32_t)((ys_lo + r) * S.pitch + xw_lo + 4 * c));
         }
         __syncthreads();
-        const int ngroups = (c1 - c0 + 3) >> 2;
-        for (int g = tid; g < ngroups * 2; g += 256) {  // 2 rows of groups per 256 threads
-          const int q = g >> 1, rpar = g & 1;
+        const int ngroups = (c1 - c0 + 3) >> 2;  // <= 128: one group per thread and row parity
+        const int q = tid & 127;
+        const int rpar = __builtin_amdgcn_readfirstlane(tid >> 7);  // wave-uniform row parity
+        if (q < ngroups) {
           const int dx0 = c0 + 4 * q;
           int x0[4], a0[4], a1[4];
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             const int dx = min(dx0 + k, D.w - 1);
             x0[k] = xofs[D.coef_x + dx] - xw_lo;
-            a0[k] = dx < D.xmax ? xa[2 * (D.coef_x + dx)] : 2048;
-            a1[k] = dx < D.xmax ? xa[2 * (D.coef_x + dx) + 1] : 0;
+            const int aa = *(const int*)&xa[2 * (D.coef_x + dx)];  // (a0, a1) int16 pair
+            const bool past = dx >= D.xmax;  // HResizeLinear: S[x0] * 2048 past xmax
+            a0[k] = past ? 2048 : (int)(int16_t)(aa & 0xFFFF);
+            a1[k] = past ? 0 : (aa >> 16);
           }
           for (int dy = r0 + rpar; dy < r1; dy += 2) {
-            const int sy0 = yofs[D.coef_y + dy];
+            const int sy0 = yofs[D.coef_y + dy];  // wave-uniform: scalar loads
+            const int bb = *(const int*)&yb[2 * (D.coef_y + dy)];
+            const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = bb >> 16;
             const int ra = (min(max(sy0, 0), S.h - 1) - ys_lo) * RS;
             const int rb = (min(max(sy0 + 1, 0), S.h - 1) - ys_lo) * RS;
-            const int b0 = yb[2 * (D.coef_y + dy)], b1 = yb[2 * (D.coef_y + dy) + 1];
             uint32_t out = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-              // HResizeLinear (a1 = 0 past xmax: S[x0] * 2048)
               const int h0 = __mul24((int)sb[ra + x0[k]], a0[k]) + __mul24((int)sb[ra + x0[k] + 1], a1[k]);
               const int h1 = __mul24((int)sb[rb + x0[k]], a0[k]) + __mul24((int)sb[rb + x0[k] + 1], a1[k]);
-              int v;
-              if (dx0 + k < D.vxs) {  // VResizeLinearVec_32s8u
-                const int t0 = max(-32768, min(32767, h0 >> 4));
-                const int t1 = max(-32768, min(32767, h1 >> 4));
-                int m = (__mul24(t0, b0) >> 16) + (__mul24(t1, b1) >> 16);  // |t|, |b| < 2^15
-                m = max(-32768, min(32767, m));
-                m = max(-32768, min(32767, m + 2));
-                v = m >> 2;
-              } else {
-                v = (__mul24(h0, b0) + __mul24(h1, b1) + (1 << 21)) >> 22;  // h < 2^20, b <= 2^11
-              }
-              out |= (uint32_t)max(0, min(255, v)) << (8 * k);
+              // VResizeLinearVec_32s8u (x < vxs) and the scalar tail, selected without a
+              // branch.  Coefficients are in [0, 2048] with pair sums <= 2049 (checked in
+              // resize_tables), so h < 2^19 and every OpenCV saturation here is a no-op:
+              // h >> 4 < 32767, the mulhi sum <= 1020, both results in [0, 255].
+              const uint32_t m = (__umul24((uint32_t)h0 >> 4, b0) >> 16) +
+                                 (__umul24((uint32_t)h1 >> 4, b1) >> 16);
+              const uint32_t vsse = (m + 2) >> 2;
+              const uint32_t vsc = (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
+              out |= (uint32_t)(dx0 + k < D.vxs ? vsse : vsc) << (8 * k);
             }
             // pitch >= w + 4: bytes past w of the last group land in the row's pad
             *(uint32_t*)(dp + (uint32_t)(dy * D.pitch + dx0)) = out;
@@ -736,6 +736,7 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
 // key is its max response with the lowest candidate index.  The final-refinement sort uses the
 // canonical (size, creation sequence) tie-break.
 constexpr int kOctNT = 256;
+constexpr int kOctRegKeys = 16;  // keys per thread kept in registers (levels of <= 4096 candidates)
 
 struct OctNodes {
   int16_t *x0, *x1, *y0, *y1;
@@ -757,11 +758,63 @@ struct OctCtx {
   int* oc;
 };
 
-// Octree passes on keys/labels that live either in LDS (fits) or in global scratch; inlined
-// per call site so each copy uses the address space it was given (ds_* vs global_*).
-__device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, uint32_t* keys,
-                                            int* lab, const int n) {
+// Where the octree keeps its keys (packed x:12 y:12 score:8) and their node labels.  Thread t
+// owns keys t, t + kOctNT, t + 2 kOctNT, ...
+//   RegKeys<R>: in registers (n <= R * kOctNT): no LDS for keys, more workgroups per CU, and
+//               the quadrant of each key is kept from the count pass to the relabel pass;
+//   MemKeys:    in global scratch (larger levels).
+template <int R>
+struct RegKeys {
+  static constexpr bool kRegs = true;
+  uint32_t key[R];
+  int lab[R];
+  uint32_t q2 = 0;  // 2 bits per key: quadrant inside its node (valid when the node splits)
+  int n;
+  __device__ int nj() const { return R; }
+  __device__ uint32_t get_key(int j) const { return key[j]; }
+  __device__ int get_lab(int j) const { return lab[j]; }
+  __device__ void set_lab(int j, int v) { lab[j] = v; }
+  __device__ void set_q(int j, int q) { q2 = (q2 & ~(3u << (2 * j))) | ((uint32_t)q << (2 * j)); }
+  __device__ int get_q(int j, const OctNodes&, int) const { return (q2 >> (2 * j)) & 3; }
+};
+
+struct MemKeys {
+  static constexpr bool kRegs = false;
+  uint32_t* keys;
+  int* labs;
+  int n;
+  __device__ int nj() const { return (n + kOctNT - 1) / kOctNT; }
+  __device__ uint32_t get_key(int j) const { return keys[threadIdx.x + kOctNT * j]; }
+  __device__ int get_lab(int j) const { return labs[threadIdx.x + kOctNT * j]; }
+  __device__ void set_lab(int j, int v) { labs[threadIdx.x + kOctNT * j] = v; }
+  __device__ void set_q(int, int) {}
+  __device__ int get_q(int j, const OctNodes& cur, int nd) const {
+    return quad_of(get_key(j), cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
+  }
+};
+
+// loop over this thread's keys: f(j, k) for k = tid + kOctNT j < n (unrolled for registers)
+template <class KS, class F>
+__device__ __forceinline__ void each_key(KS& ks, F f) {
+  if constexpr (KS::kRegs) {
+#pragma unroll
+    for (int j = 0; j < ks.nj(); j++) {
+      const int k = threadIdx.x + kOctNT * j;
+      if (k < ks.n) f(j, k);
+    }
+  } else {
+    for (int j = 0; j < ks.nj(); j++) {
+      const int k = threadIdx.x + kOctNT * j;
+      if (k < ks.n) f(j, k);
+    }
+  }
+}
+
+template <class KS>
+__device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, KS& ks,
+                                            const uint32_t* keys_mem) {
   const int tid = threadIdx.x;
+  const int n = ks.n;
   OctNodes A = X.A, B = X.B;
   int *cc = X.cc, *t1 = X.t1, *t2 = X.t2, *t3 = X.t3, *t4 = X.t4, *s_tmp = X.s_tmp,
       *s_misc = X.s_misc;
@@ -778,12 +831,12 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
     A.seq[i] = i;
   }
   __syncthreads();
-  for (int k = tid; k < n; k += kOctNT) {
-    const float x = (float)(keys[k] & 0xFFF);
+  each_key(ks, [&](int j, int) {
+    const float x = (float)(ks.get_key(j) & 0xFFF);
     const int ni = min((int)(x / G.hx), nini - 1);
-    lab[k] = ni;
+    ks.set_lab(j, ni);
     atomicAdd(&A.cnt[ni], 1);
-  }
+  });
   __syncthreads();
   // drop empty initial nodes, keep order
   for (int i = tid; i < nini; i += kOctNT) t1[i] = A.cnt[i] > 0;
@@ -796,7 +849,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       B.cnt[j] = A.cnt[i]; B.seq[j] = A.seq[i];
     }
   __syncthreads();
-  for (int k = tid; k < n; k += kOctNT) lab[k] = t1[lab[k]];
+  each_key(ks, [&](int j, int) { ks.set_lab(j, t1[ks.get_lab(j)]); });
   __syncthreads();
   OctNodes cur = B, nxt = A;
   int seqc = nini;
@@ -809,26 +862,36 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
     // quadrant counts; keys are in cell order, so a wave's keys usually share one node and the
     // four counts are added with one atomic each instead of one per key
     const int lane = tid & 63;
-    for (int k0 = 0; k0 < n; k0 += kOctNT) {
-      const int k = k0 + tid;
+    auto count_one = [&](int j) {
+      const int k = tid + kOctNT * j;
       int nd = -1, q = -1;
       if (k < n) {
-        nd = lab[k];
-        if (cur.cnt[nd] > 1) q = quad_of(keys[k], cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
+        nd = ks.get_lab(j);
+        if (cur.cnt[nd] > 1) {
+          q = quad_of(ks.get_key(j), cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
+          ks.set_q(j, q);
+        }
       }
       const uint64_t act = __ballot(q >= 0);
-      if (!act) continue;
+      if (!act) return;
       const int first = __builtin_ctzll(act);
       const int ndf = __shfl(nd, first);
       if (__ballot(q >= 0 && nd != ndf) == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int c = __popcll(__ballot(q == j));
-          if (lane == first && c) atomicAdd(&cc[4 * ndf + j], c);
+        for (int jj = 0; jj < 4; jj++) {
+          const int c = __popcll(__ballot(q == jj));
+          if (lane == first && c) atomicAdd(&cc[4 * ndf + jj], c);
         }
       } else if (q >= 0) {
         atomicAdd(&cc[4 * nd + q], 1);
       }
+    };
+    // every lane runs every j (the ballots need the whole wave)
+    if constexpr (KS::kRegs) {
+#pragma unroll
+      for (int j = 0; j < ks.nj(); j++) count_one(j);
+    } else {
+      for (int j = 0; j < ks.nj(); j++) count_one(j);
     }
     __syncthreads();
     int T, newSize, nToExpand;
@@ -964,17 +1027,17 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       }
     }
     // relabel keys
-    for (int k = tid; k < n; k += kOctNT) {
-      const int nd = lab[k];
+    each_key(ks, [&](int j, int) {
+      const int nd = ks.get_lab(j);
       if (t2[nd]) {
-        const int q = quad_of(keys[k], cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
-        int j = 0;
-        for (int qq = 0; qq < q; qq++) j += cc[4 * nd + qq] > 0;
-        lab[k] = t4[nd] - j;
+        const int q = ks.get_q(j, cur, nd);
+        int c = 0;
+        for (int qq = 0; qq < q; qq++) c += cc[4 * nd + qq] > 0;
+        ks.set_lab(j, t4[nd] - c);
       } else {
-        lab[k] = t4[nd];
+        ks.set_lab(j, t4[nd]);
       }
-    }
+    });
     __syncthreads();
     {
       OctNodes tmp = cur;
@@ -994,14 +1057,14 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   unsigned* best = (unsigned*)t1;
   for (int i = tid; i < size; i += kOctNT) best[i] = 0;
   __syncthreads();
-  for (int k = tid; k < n; k += kOctNT) {
-    const uint32_t key = keys[k];
-    atomicMax(&best[lab[k]], ((key >> 24) << 24) | (0xFFFFFFu - (unsigned)k));
-  }
+  each_key(ks, [&](int j, int k) {
+    const uint32_t key = ks.get_key(j);
+    atomicMax(&best[ks.get_lab(j)], ((key >> 24) << 24) | (0xFFFFFFu - (unsigned)k));
+  });
   __syncthreads();
   for (int i = tid; i < size; i += kOctNT) {
     const int k = (int)(0xFFFFFFu - (best[i] & 0xFFFFFFu));
-    outk[i] = keys[k];
+    outk[i] = keys_mem[k];
   }
   if (tid == 0) *oc = size;
 }
@@ -1013,6 +1076,7 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
     uint32_t* __restrict__ lin, int* __restrict__ label, uint32_t* __restrict__ okey,
     int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
     int key_cap) {
+  (void)key_cap;
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_tmp[kOctNT / 64 + 1];
   __shared__ int s_misc[8];
@@ -1070,14 +1134,19 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
     return;
   }
   OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, pk, s_tmp64, outk, oc};
-  if (n <= key_cap) {  // keys + labels fit in LDS: every octree pass stays on-chip
-    uint32_t* kl = (uint32_t*)take(4 * (size_t)key_cap);
-    int* ll = (int*)take(4 * (size_t)key_cap);
-    for (int k = tid; k < n; k += kOctNT) kl[k] = keys[k];
-    __syncthreads();
-    octree_core(G, X, kl, ll, n);
+  if (n <= kOctRegKeys * kOctNT) {  // keys + labels in registers: every pass stays on-chip
+    RegKeys<kOctRegKeys> ks;
+    ks.n = n;
+#pragma unroll
+    for (int j = 0; j < kOctRegKeys; j++) {
+      const int k = tid + kOctNT * j;
+      ks.key[j] = k < n ? keys[k] : 0u;
+      ks.lab[j] = 0;
+    }
+    octree_core(G, X, ks, keys);
   } else {
-    octree_core(G, X, keys, lab, n);
+    MemKeys ks{keys, lab, n};
+    octree_core(G, X, ks, keys);
   }
 }
 
@@ -1398,14 +1467,9 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->oct_smem = 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
                 r16(4 * (P->cell_cap + 1)) + r16(8 * NC);
   if (P->oct_smem > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
-  {  // LDS-resident keys: up to 4096 per level (typical levels hold < 2500 candidates), which
-     // keeps the workgroup at ~50 KB of LDS so 3 fit per CU; larger levels use global scratch
-    int cap = 0;
-    for (int l = 0; l < g.nlevels; l++) cap = std::max(cap, g.lv[l].cand_cap);
-    const size_t budget = 150 * 1024 - P->oct_smem;
-    P->key_cap = (int)std::min<size_t>({(size_t)cap, (size_t)4096, budget / 8 / 16 * 16});
-    P->oct_smem += 2 * r16(4 * (size_t)P->key_cap);
-  }
+  // keys and labels live in registers (up to kOctRegKeys * kOctNT per level) or in global
+  // scratch, never in LDS: the octree workgroup needs only its node arrays on chip
+  P->key_cap = kOctRegKeys * kOctNT;
   if (hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)P->oct_smem) != hipSuccess)
     return fail(ORBX_EDEVICE);

@@ -59,7 +59,7 @@ void build_tables(const orbx_params& p, Geometry* g) {
 }
 
 // cv::resize INTER_LINEAR coefficient tables (OpenCV 2.4 imgwarp.cpp).
-static void resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom* L) {
+static bool resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom* L) {
   const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
   const double sx = 1. / inv_sx, sy = 1. / inv_sy;
   L->coef_x = (int)g->xofs.size();
@@ -89,10 +89,18 @@ static void resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom
     g->yb.push_back((int16_t)std::min(32767, std::max(-32768, cv_round(c1 * 2048))));
   }
   L->xmax = xmax;
+  bool ok = true;
+  // k_pyramid drops OpenCV's saturations: they are no-ops while every coefficient is in
+  // [0, 2048] and each pair sums to at most 2049 (rounding may give 2049).
+  for (size_t i = 2 * L->coef_x; i < g->xa.size(); i += 2)
+    if (g->xa[i] < 0 || g->xa[i + 1] < 0 || g->xa[i] + g->xa[i + 1] > 2049) ok = false;
+  for (size_t i = 2 * L->coef_y; i < g->yb.size(); i += 2)
+    if (g->yb[i] < 0 || g->yb[i + 1] < 0 || g->yb[i] + g->yb[i + 1] > 2049) ok = false;
   int xs = 0;  // VResizeLinearVec_32s8u: 16-wide while x <= W-16, 4-wide while x < W-4
   while (xs <= dw - 16) xs += 16;
   while (xs < dw - 4) xs += 4;
   L->vxs = xs;
+  return ok;
 }
 
 int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string* why) {
@@ -132,7 +140,10 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
         if (why) *why = "exact 2x decimation (INTER_AREA path)";
         return ORBX_EUNSUPPORTED;
       }
-      resize_tables(P.w, P.h, L.w, L.h, g, &L);
+      if (!resize_tables(P.w, P.h, L.w, L.h, g, &L)) {
+        if (why) *why = "resize coefficients outside [0, 2048]";
+        return ORBX_EUNSUPPORTED;
+      }
     }
     // every level (level 0 is copied in) lives in the pitched pyramid block
     L.pitch = (L.w + 4 + 63) & ~63;  // >= w + 4: a row's last dword never straddles the row end
