@@ -3,7 +3,7 @@
 //
 // One plan = one image size + one parameter set + a maximum batch.  A batch of images runs
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
-//   k_pyramid     level 0 copy + every level (cv::resize INTER_LINEAR), one launch, row bands
+//   k_pyramid     level 0 copy + every level (cv::resize INTER_LINEAR), 2 launches, row bands
 //   k_blur        x 1            all levels, 64x16 LDS tiles         (GaussianBlur 7x7 s=2)
 //   k_fast_tile   x 1            64x64 tiles, all levels            (FAST score + cell-local NMS)
 //   k_fast_compact x 1           one wave per FAST cell             (fallback + ordered compaction)
@@ -154,108 +154,175 @@ __device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
 }
 
 // ------------------------------------------------------------------ k_pyramid
-// ComputePyramid (ORBextractor.cc:1047-1072) in one launch: one workgroup per (image, row
-// band) copies its level-0 rows into the 64-B pitched pyramid block (every later kernel reads
-// aligned dwords) and then builds every level of its band from the previous one with
-// cv::resize INTER_LINEAR 8UC1: horizontal Q11 taps, vertical SSE2 mulhi form for
-// x < vxs, scalar (H0*b0 + H1*b1 + 2^21) >> 22 tail.  Bands overlap by the rows the next level
-// needs (Geometry::bands), so no band waits for another: a row two bands share is computed by
-// both, to the same bytes.  A level step runs in chunks of kPyRows x kPyCols outputs whose
-// source window is staged in LDS with aligned dword loads; a thread owns one 4-pixel column
-// group of the chunk (its taps loaded once) and walks the rows.
-__global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ in,
-                                                 uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-                                                 const LevelGeom* __restrict__ lv, int nlevels,
-                                                 const PyrBand* __restrict__ bands,
-                                                 const int* __restrict__ xofs,
-                                                 const int16_t* __restrict__ xa,
-                                                 const int* __restrict__ yofs,
-                                                 const int16_t* __restrict__ yb) {
-  __shared__ __align__(16) uint32_t s_src[kPySrcRows * kPySrcWords];
+// ComputePyramid (ORBextractor.cc:1047-1072) in a few launches (Geometry::pyr_stages): the first
+// copies level 0 into the 64-B pitched pyramid block (every later kernel reads aligned dwords)
+// and builds levels 1..3, the next ones build four levels each from the last level stored.
+// One workgroup per (image, row band) builds its band of the stage's levels, each from the
+// previous one, with cv::resize INTER_LINEAR 8UC1: horizontal Q11 taps, vertical
+// SSE2 mulhi form for x < vxs, scalar (H0*b0 + H1*b1 + 2^21) >> 22 tail.  Bands overlap by
+// the rows the next level needs (Geometry::bands), so no band waits for another; a band keeps
+// its rows of the level just built in LDS (even levels in buffer A, odd ones at buf_b) and
+// reads the next level's sources there, so each level costs one barrier and the pyramid block
+// is only written, by the band that owns the row.  Work items are (row, 4-pixel column group)
+// pairs dealt round-robin over the kPyNT threads.
+// i = r * n + c for 0 <= i < 2^20, 1 <= n: (i + 0.5) / n is >= 0.5 / n from an integer, so
+// the float quotient truncates to r; the two fix-ups are insurance.
+__device__ __forceinline__ void py_divmod(int i, int n, float inv_n, int& r, int& c) {
+  r = (int)(((float)i + 0.5f) * inv_n);
+  c = i - __mul24(r, n);
+  if (c < 0) r--, c += n;
+  if (c >= n) r++, c -= n;
+}
+
+// One resize work item: output row r (band-relative) and 4-pixel group at dx0, with its taps.
+struct PyItem {
+  int r, dx0;
+  int2 yt;
+  int4 t01, t23;
+};
+
+__device__ __forceinline__ PyItem py_load(int i, int ng, float inv_ng, const int2* __restrict__ xt,
+                                          const int2* __restrict__ yt, int dlo) {
+  PyItem it;
+  int g;
+  py_divmod(i, ng, inv_ng, it.r, g);
+  it.dx0 = 4 * g;
+  it.yt = yt[dlo + it.r];
+  it.t01 = *(const int4*)(xt + it.dx0);  // coef_x % 4 == 0 and runs padded: aligned, in range
+  it.t23 = *(const int4*)(xt + it.dx0 + 2);
+  return it;
+}
+
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {  // a, b < 2^24
+  return (uint32_t)(((uint64_t)(a & 0xFFFFFF) * (uint64_t)(b & 0xFFFFFF)) >> 32);
+}
+
+// Four output pixels of cv::resize INTER_LINEAR 8UC1.  Coefficients are in
+// [0, 2049] (checked in resize_tables), so every OpenCV saturation on the way is a no-op:
+// H = S0*a0 + S1*a1 < 2^19, H >> 4 < 32767, the mulhi sum <= 1020, results in [0, 255].
+// The taps carry a << 4, so g = H << 4 and (H >> 4) << 8 = g & ~0xFF: the SSE2 16-bit
+// _mm_mulhi_epi16(H >> 4, b) = ((H >> 4) * b) >> 16 = mulhi_u24((H >> 4) << 8, b << 8).
+__device__ __forceinline__ uint32_t py_resize4(const PyItem& it, const uint8_t* sb, int slo,
+                                               int spitch, int sh1, int vxs) {
+  const uint32_t b0 = it.yt.y & 0xFFFF, b1 = (uint32_t)it.yt.y >> 16;
+  const int ra = __mul24(min(max(it.yt.x, 0), sh1) - slo, spitch);
+  const int rb = __mul24(min(max(it.yt.x + 1, 0), sh1) - slo, spitch);
+  const int xs[4] = {it.t01.x, it.t01.z, it.t23.x, it.t23.z};
+  const uint32_t as[4] = {(uint32_t)it.t01.y, (uint32_t)it.t01.w, (uint32_t)it.t23.y,
+                          (uint32_t)it.t23.w};
+  uint32_t g0[4], g1[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t a0 = as[k] & 0xFFFF, a1 = as[k] >> 16;
+    g0[k] = __umul24(sb[ra + xs[k]], a0) + __umul24(sb[ra + xs[k] + 1], a1);
+    g1[k] = __umul24(sb[rb + xs[k]], a0) + __umul24(sb[rb + xs[k] + 1], a1);
+  }
+  uint32_t out = 0;
+  if (it.dx0 + 3 < vxs) {  // VResizeLinearVec_32s8u: the whole group in the SSE2 region
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t m = mulhi_u24(g0[k] & 0x7FFF00, b0 << 8) + mulhi_u24(g1[k] & 0x7FFF00, b1 << 8);
+      out |= ((m + 2) >> 2) << (8 * k);
+    }
+  } else {  // the row end: SSE2 up to vxs, then the scalar (H0*b0 + H1*b1 + 2^21) >> 22
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t m = mulhi_u24(g0[k] & 0x7FFF00, b0 << 8) + mulhi_u24(g1[k] & 0x7FFF00, b1 << 8);
+      const uint32_t vsc = (__umul24(g0[k] >> 4, b0) + __umul24(g1[k] >> 4, b1) + (1u << 21)) >> 22;
+      out |= (it.dx0 + k < vxs ? (m + 2) >> 2 : vsc) << (8 * k);
+    }
+  }
+  return out;
+}
+
+__global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ in,
+                                                  uint8_t* __restrict__ pyr, int64_t pyr_bytes,
+                                                  const LevelGeom* __restrict__ lv, int l0, int l1,
+                                                  const PyrBand* __restrict__ bands,
+                                                  const int2* __restrict__ xtap,
+                                                  const int2* __restrict__ ytap, int buf_b) {
+  extern __shared__ __align__(16) uint8_t s_pyr[];
   int band, img;
   xcd_block(band, img);
   const PyrBand& B = bands[band];
   const int tid = threadIdx.x;
   uint8_t* base = pyr + (int64_t)img * pyr_bytes;
-  {  // level 0: the input rows of the band (ORBextractor.cc:1066-1068)
-    const LevelGeom& G = lv[0];
-    const uint8_t* src = in + (int64_t)img * G.h * G.w;
-    const int q4 = (G.w + 3) >> 2, lo = B.lo[0], nr = B.hi[0] - lo;
-    for (int i = tid; i < nr * q4; i += 256) {
-      const int r = i / q4, x4 = (i - r * q4) * 4, y = lo + r;
-      const uint8_t* s = src + (int64_t)y * G.w + x4;
-      uint32_t v = s[0];
-      if (x4 + 1 < G.w) v |= (uint32_t)s[1] << 8;
-      if (x4 + 2 < G.w) v |= (uint32_t)s[2] << 16;
-      if (x4 + 3 < G.w) v |= (uint32_t)s[3] << 24;
-      *(uint32_t*)(base + G.pyr_off + (uint32_t)(y * G.pitch + x4)) = v;
+  {  // the source level's band rows into LDS (buffer of parity l0 - 1)
+    const LevelGeom& G = lv[l0 - 1];
+    const int lo = B.lo[l0 - 1], nr = B.hi[l0 - 1] - lo, pitch = G.pitch;
+    uint8_t* sdst = s_pyr + ((l0 - 1) & 1 ? buf_b : 0);
+    const bool input = l0 == 1;  // level 0 comes from the input (ORBextractor.cc:1066-1068)
+    const int w = input ? G.w : pitch;  // a pyramid row is copied pad and all
+    const uint8_t* src = input ? in + (int64_t)img * G.h * G.w : base + G.pyr_off;
+    const int own_lo = input ? B.own_lo[0] : 0, own_hi = input ? B.own_hi[0] : 0;
+    uint8_t* dst = base + G.pyr_off;
+    if ((w & 15) == 0) {  // 16-byte chunks, four per thread in flight
+      const int nch = w >> 4, items = nr * nch;
+      const float inv = 1.0f / (float)nch;
+      for (int i0 = tid; i0 < items; i0 += 4 * kPyNT) {
+        // past the end a thread repeats the last chunk: identical bytes to identical places
+        uint4 v[4];
+        int rr[4], cc[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          py_divmod(min(i0 + kPyNT * u, items - 1), nch, inv, rr[u], cc[u]);
+          v[u] = *(const uint4*)(src + (int64_t)(lo + rr[u]) * w + 16 * cc[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)  // pin the loads here: all four in flight together
+          asm volatile("" : "+v"(v[u].x), "+v"(v[u].y), "+v"(v[u].z), "+v"(v[u].w));
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int y = lo + rr[u];
+          *(uint4*)(sdst + __mul24(rr[u], pitch) + 16 * cc[u]) = v[u];
+          if (y >= own_lo && y < own_hi) *(uint4*)(dst + (uint32_t)__mul24(y, pitch) + 16 * cc[u]) = v[u];
+        }
+      }
+    } else {  // any input width: dwords assembled from bytes
+      const int q4 = (w + 3) >> 2, items = nr * q4;
+      const float inv = 1.0f / (float)q4;
+      for (int i = tid; i < items; i += kPyNT) {
+        int r, c;
+        py_divmod(i, q4, inv, r, c);
+        const int x4 = 4 * c, y = lo + r;
+        const uint8_t* s = src + (int64_t)y * w + x4;
+        uint32_t v = s[0];
+        if (x4 + 1 < w) v |= (uint32_t)s[1] << 8;
+        if (x4 + 2 < w) v |= (uint32_t)s[2] << 16;
+        if (x4 + 3 < w) v |= (uint32_t)s[3] << 24;
+        *(uint32_t*)(sdst + __mul24(r, pitch) + x4) = v;
+        if (y >= own_lo && y < own_hi) *(uint32_t*)(dst + (uint32_t)__mul24(y, pitch) + x4) = v;
+      }
     }
   }
-  const uint8_t* sb = (const uint8_t*)s_src;
-  constexpr int RS = kPySrcWords * 4;  // staged row stride (bytes)
-  for (int l = 1; l < nlevels; l++) {
-    __syncthreads();  // level l-1 of this band written (and the LDS window free)
+  for (int l = l0; l <= l1; l++) {
+    __syncthreads();  // level l-1 of this band is in LDS
     const LevelGeom& D = lv[l];
     const LevelGeom& S = lv[l - 1];
-    const uint8_t* sp = base + S.pyr_off;
+    const uint8_t* sb = s_pyr + ((l - 1) & 1 ? buf_b : 0);
+    uint8_t* db = s_pyr + (l & 1 ? buf_b : 0);
     uint8_t* dp = base + D.pyr_off;
-    for (int r0 = B.lo[l]; r0 < B.hi[l]; r0 += kPyRows) {
-      const int r1 = min(r0 + kPyRows, B.hi[l]);
-      const int ys_lo = min(max(yofs[D.coef_y + r0], 0), S.h - 1);
-      const int ys_hi = min(max(yofs[D.coef_y + r1 - 1] + 1, 0), S.h - 1);
-      const int nrows = ys_hi - ys_lo + 1;
-      for (int c0 = 0; c0 < D.w; c0 += kPyCols) {
-        const int c1 = min(c0 + kPyCols, D.w);
-        const int xw_lo = xofs[D.coef_x + c0] & ~3;
-        const int nwords = (xofs[D.coef_x + c1 - 1] + 1 - xw_lo) / 4 + 1;
-        if (nrows > kPySrcRows || nwords > kPySrcWords) return;  // excluded by build_geometry
-        __syncthreads();
-        for (int i = tid; i < nrows * nwords; i += 256) {
-          const int r = i / nwords, c = i - r * nwords;
-          s_src[r * kPySrcWords + c] =
-              *(const uint32_t*)(sp + (uint32_t)((ys_lo + r) * S.pitch + xw_lo + 4 * c));
-        }
-        __syncthreads();
-        const int ngroups = (c1 - c0 + 3) >> 2;  // <= 128: one group per thread and row parity
-        const int q = tid & 127;
-        const int rpar = __builtin_amdgcn_readfirstlane(tid >> 7);  // wave-uniform row parity
-        if (q < ngroups) {
-          const int dx0 = c0 + 4 * q;
-          int x0[4], a0[4], a1[4];
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const int dx = min(dx0 + k, D.w - 1);
-            x0[k] = xofs[D.coef_x + dx] - xw_lo;
-            const int aa = *(const int*)&xa[2 * (D.coef_x + dx)];  // (a0, a1) int16 pair
-            const bool past = dx >= D.xmax;  // HResizeLinear: S[x0] * 2048 past xmax
-            a0[k] = past ? 2048 : (int)(int16_t)(aa & 0xFFFF);
-            a1[k] = past ? 0 : (aa >> 16);
-          }
-          for (int dy = r0 + rpar; dy < r1; dy += 2) {
-            const int sy0 = yofs[D.coef_y + dy];  // wave-uniform: scalar loads
-            const int bb = *(const int*)&yb[2 * (D.coef_y + dy)];
-            const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = bb >> 16;
-            const int ra = (min(max(sy0, 0), S.h - 1) - ys_lo) * RS;
-            const int rb = (min(max(sy0 + 1, 0), S.h - 1) - ys_lo) * RS;
-            uint32_t out = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-              const int h0 = __mul24((int)sb[ra + x0[k]], a0[k]) + __mul24((int)sb[ra + x0[k] + 1], a1[k]);
-              const int h1 = __mul24((int)sb[rb + x0[k]], a0[k]) + __mul24((int)sb[rb + x0[k] + 1], a1[k]);
-              // VResizeLinearVec_32s8u (x < vxs) and the scalar tail, selected without a
-              // branch.  Coefficients are in [0, 2048] with pair sums <= 2049 (checked in
-              // resize_tables), so h < 2^19 and every OpenCV saturation here is a no-op:
-              // h >> 4 < 32767, the mulhi sum <= 1020, both results in [0, 255].
-              const uint32_t m = (__umul24((uint32_t)h0 >> 4, b0) >> 16) +
-                                 (__umul24((uint32_t)h1 >> 4, b1) >> 16);
-              const uint32_t vsse = (m + 2) >> 2;
-              const uint32_t vsc = (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
-              out |= (uint32_t)(dx0 + k < D.vxs ? vsse : vsc) << (8 * k);
-            }
-            // pitch >= w + 4: bytes past w of the last group land in the row's pad
-            *(uint32_t*)(dp + (uint32_t)(dy * D.pitch + dx0)) = out;
-          }
-        }
+    const int slo = B.lo[l - 1], dlo = B.lo[l], ng = (D.w + 3) >> 2;
+    const int items = max(0, B.hi[l] - dlo) * ng;
+    const float inv_ng = 1.0f / (float)ng;
+    const bool keep = l < l1;  // the stage's last level is not read back
+    const int dpitch = D.pitch, spitch = S.pitch, sh1 = S.h - 1, vxs = D.vxs;
+    const int own_lo = B.own_lo[l], own_hi = B.own_hi[l];
+    const int2* xt = xtap + D.coef_x;
+    const int2* yt = ytap + D.coef_y;
+    for (int i = tid; i < items; i += 2 * kPyNT) {  // two items per thread in flight
+      const PyItem A = py_load(i, ng, inv_ng, xt, yt, dlo);
+      const PyItem C = py_load(min(i + kPyNT, items - 1), ng, inv_ng, xt, yt, dlo);
+      const uint32_t oa = py_resize4(A, sb, slo, spitch, sh1, vxs);
+      const uint32_t oc = py_resize4(C, sb, slo, spitch, sh1, vxs);
+      // pitch >= w + 4: bytes past w of the last group land in the row's pad
+      if (keep) *(uint32_t*)(db + __mul24(A.r, dpitch) + A.dx0) = oa;
+      if (dlo + A.r >= own_lo && dlo + A.r < own_hi)
+        *(uint32_t*)(dp + (uint32_t)__mul24(dlo + A.r, dpitch) + A.dx0) = oa;
+      if (i + kPyNT < items) {
+        if (keep) *(uint32_t*)(db + __mul24(C.r, dpitch) + C.dx0) = oc;
+        if (dlo + C.r >= own_lo && dlo + C.r < own_hi)
+          *(uint32_t*)(dp + (uint32_t)__mul24(dlo + C.r, dpitch) + C.dx0) = oc;
       }
     }
   }
@@ -1295,8 +1362,7 @@ struct orbx_plan {
   hipStream_t stream = nullptr;
   LevelGeom* d_lv = nullptr;
   CellGeom* d_cells = nullptr;
-  int *d_xofs = nullptr, *d_yofs = nullptr;
-  int16_t *d_xa = nullptr, *d_yb = nullptr;
+  int2 *d_xtap = nullptr, *d_ytap = nullptr;
   BlurTile* d_tiles = nullptr;
   int ntiles = 0;
   PyrBand* d_bands = nullptr;
@@ -1340,8 +1406,10 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
             st_fast = pr.stage("k_fast_compact"),
             st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe");
   pr.mark(P->stream, -1);
-  hipLaunchKernelGGL(k_pyramid, dim3(g.nbands, n), dim3(256), 0, P->stream, d_in, P->d_pyr,
-                     g.pyr_bytes, P->d_lv, L, P->d_bands, P->d_xofs, P->d_xa, P->d_yofs, P->d_yb);
+  for (const PyrStage& st : g.pyr_stages)
+    hipLaunchKernelGGL(k_pyramid, dim3(st.nbands, n), dim3(kPyNT), st.smem, P->stream, d_in,
+                       P->d_pyr, g.pyr_bytes, P->d_lv, st.l0, st.l1, P->d_bands + st.band0,
+                       P->d_xtap, P->d_ytap, st.buf_b);
   pr.mark(P->stream, st_pyr);
   if (P->ntiles > 0) {
     hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
@@ -1438,9 +1506,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
   const size_t B = (size_t)max_batch;
   if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, g.cells.size()) ||
-      dalloc(&P->d_xofs, g.xofs.size()) || dalloc(&P->d_yofs, g.yofs.size()) ||
-      dalloc(&P->d_xa, g.xa.size()) || dalloc(&P->d_yb, g.yb.size()) ||
-      dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_bands, (size_t)g.nbands) || dalloc(&P->d_ftiles, ftiles.size()) ||
+      dalloc(&P->d_xtap, g.xtap.size() / 2) || dalloc(&P->d_ytap, g.ytap.size() / 2) ||
+      dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_bands, g.bands.size()) || dalloc(&P->d_ftiles, ftiles.size()) ||
       dalloc(&P->d_vmap, B * g.pyr_bytes) || dalloc(&P->d_bitmaps, B * g.bm_words) ||
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
@@ -1454,11 +1521,10 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   };
   if (up(P->d_lv, g.lv, sizeof(LevelGeom) * g.nlevels) ||
       up(P->d_cells, g.cells.data(), sizeof(CellGeom) * g.cells.size()) ||
-      up(P->d_xofs, g.xofs.data(), 4 * g.xofs.size()) ||
-      up(P->d_yofs, g.yofs.data(), 4 * g.yofs.size()) ||
-      up(P->d_xa, g.xa.data(), 2 * g.xa.size()) || up(P->d_yb, g.yb.data(), 2 * g.yb.size()) ||
+      up(P->d_xtap, g.xtap.data(), 4 * g.xtap.size()) ||
+      up(P->d_ytap, g.ytap.data(), 4 * g.ytap.size()) ||
       up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
-      up(P->d_bands, g.bands, sizeof(PyrBand) * g.nbands) ||
+      up(P->d_bands, g.bands.data(), sizeof(PyrBand) * g.bands.size()) ||
       up(P->d_ftiles, ftiles.data(), sizeof(FastTile) * ftiles.size()))
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
@@ -1480,8 +1546,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
 int orbx_plan_destroy(orbx_plan* P) {
   if (!P) return ORBX_OK;
   if (P->graph) hipGraphExecDestroy(P->graph);
-  void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xofs,   P->d_yofs,  P->d_xa,
-                  P->d_yb,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
+  void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xtap,   P->d_ytap,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label,
                   P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
   for (void* p : ptrs)

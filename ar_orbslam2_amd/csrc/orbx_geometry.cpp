@@ -62,8 +62,8 @@ void build_tables(const orbx_params& p, Geometry* g) {
 static bool resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom* L) {
   const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
   const double sx = 1. / inv_sx, sy = 1. / inv_sy;
-  L->coef_x = (int)g->xofs.size();
-  L->coef_y = (int)g->yofs.size();
+  L->coef_x = (int)g->xtap.size() / 2;  // multiple of 4 (every run padded)
+  L->coef_y = (int)g->ytap.size() / 2;
   int xmax = dw;
   for (int dx = 0; dx < dw; dx++) {
     float fx = (float)((dx + 0.5) * sx - 0.5);
@@ -89,12 +89,24 @@ static bool resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom
     g->yb.push_back((int16_t)std::min(32767, std::max(-32768, cv_round(c1 * 2048))));
   }
   L->xmax = xmax;
+  for (int dx = 0; dx < (dw + 3) / 4 * 4; dx++) {
+    const int i = 2 * (g->xofs.size() - dw + std::min(dx, dw - 1));
+    const int a0 = std::min(dx, dw - 1) >= xmax ? 2048 : g->xa[i];
+    const int a1 = std::min(dx, dw - 1) >= xmax ? 0 : g->xa[i + 1];
+    g->xtap.push_back(g->xofs[i / 2]);
+    g->xtap.push_back((int32_t)((uint32_t)(a0 << 4) | ((uint32_t)(a1 << 4) << 16)));  // Q15
+  }
+  for (int dy = 0; dy < dh; dy++) {
+    const int i = (int)g->yofs.size() - dh + dy;
+    g->ytap.push_back(g->yofs[i]);
+    g->ytap.push_back((g->yb[2 * i] & 0xFFFF) | (g->yb[2 * i + 1] << 16));
+  }
   bool ok = true;
   // k_pyramid drops OpenCV's saturations: they are no-ops while every coefficient is in
   // [0, 2048] and each pair sums to at most 2049 (rounding may give 2049).
-  for (size_t i = 2 * L->coef_x; i < g->xa.size(); i += 2)
+  for (size_t i = 2 * (g->xofs.size() - dw); i < g->xa.size(); i += 2)
     if (g->xa[i] < 0 || g->xa[i + 1] < 0 || g->xa[i] + g->xa[i + 1] > 2049) ok = false;
-  for (size_t i = 2 * L->coef_y; i < g->yb.size(); i += 2)
+  for (size_t i = 2 * (g->yofs.size() - dh); i < g->yb.size(); i += 2)
     if (g->yb[i] < 0 || g->yb[i + 1] < 0 || g->yb[i] + g->yb[i + 1] > 2049) ok = false;
   int xs = 0;  // VResizeLinearVec_32s8u: 16-wide while x <= W-16, 4-wide while x < W-4
   while (xs <= dw - 16) xs += 16;
@@ -218,47 +230,67 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     kp += L.kp_cap;
     g->node_cap_max = std::max(g->node_cap_max, L.node_cap);
   }
-  // k_pyramid row bands: band b owns rows [b*h_l/nb, (b+1)*h_l/nb) of every level and
-  // computes, going down from the top level, the rows the next level's rows need as well
-  // (rows shared by two bands are computed by both, identically)
-  g->nbands = std::min(kMaxBands, std::max(1, h / kPyBandH));
-  for (int b = 0; b < g->nbands; b++) {
-    PyrBand& B = g->bands[b];
-    for (int l = 0; l < p.nlevels; l++) {
-      B.lo[l] = (int)((int64_t)b * g->lv[l].h / g->nbands);
-      B.hi[l] = (int)((int64_t)(b + 1) * g->lv[l].h / g->nbands);
+  // k_pyramid stages: levels 1..kPyStage0, then kPyStageN at a time.  In a stage, band b
+  // owns rows [b*h_l/nb, (b+1)*h_l/nb) of every level and computes, going down from the
+  // stage's last level, the rows the next level's rows need as well (rows shared by two bands
+  // are computed by both, identically; only the owner stores them).  Its level l rows stay in
+  // LDS for level l+1: even levels in buffer A, odd ones in B.  The recomputed cone grows by
+  // ~2 rows per level below the top, so stages stay short.
+  g->pyr_stages.clear();
+  g->bands.clear();
+  for (int l0 = 1; l0 < p.nlevels;) {
+    PyrStage st;
+    st.l0 = l0;
+    st.l1 = std::min(p.nlevels - 1, l0 + (l0 == 1 ? kPyStage0 : kPyStageN) - 1);
+    const int hs = g->lv[l0 - 1].h;
+    std::vector<PyrBand> bands;
+    for (int nb = std::max(1, hs / kPyBandH);; nb++) {
+      bands.assign(nb, PyrBand{});
+      int need[2] = {0, 0};
+      for (int b = 0; b < nb; b++) {
+        PyrBand& B = bands[b];
+        for (int l = st.l0 - 1; l <= st.l1; l++) {
+          B.own_lo[l] = B.lo[l] = (int)((int64_t)b * g->lv[l].h / nb);
+          B.own_hi[l] = B.hi[l] = (int)((int64_t)(b + 1) * g->lv[l].h / nb);
+        }
+        for (int l = st.l1; l >= st.l0; l--) {
+          const LevelGeom& D = g->lv[l];
+          const LevelGeom& S = g->lv[l - 1];
+          if (B.hi[l] <= B.lo[l]) continue;
+          const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
+          const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
+          B.lo[l - 1] = std::min(B.lo[l - 1], slo);
+          B.hi[l - 1] = std::max(B.hi[l - 1], shi);
+        }
+        for (int l = st.l0 - 1; l <= st.l1; l++)
+          need[l & 1] = std::max(need[l & 1], std::max(0, B.hi[l] - B.lo[l]) * g->lv[l].pitch);
+      }
+      st.buf_b = (need[0] + 15) & ~15;
+      st.smem = st.buf_b + need[1];
+      if (st.smem <= kPyMaxSmem) break;
+      if (nb >= hs) {
+        if (why) *why = "image too wide for the pyramid bands";
+        return ORBX_EUNSUPPORTED;
+      }
     }
-    for (int l = p.nlevels - 1; l >= 1; l--) {
-      const LevelGeom& D = g->lv[l];
-      const LevelGeom& S = g->lv[l - 1];
-      if (B.hi[l] <= B.lo[l]) continue;
-      const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
-      const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
-      B.lo[l - 1] = std::min(B.lo[l - 1], slo);
-      B.hi[l - 1] = std::max(B.hi[l - 1], shi);
-    }
+    st.band0 = (int)g->bands.size();
+    st.nbands = (int)bands.size();
+    g->bands.insert(g->bands.end(), bands.begin(), bands.end());
+    g->pyr_stages.push_back(st);
+    l0 = st.l1 + 1;
   }
-  // k_pyramid chunks (kPyRows x kPyCols output pixels) must find their source window in LDS
-  for (int l = 1; l < p.nlevels; l++) {
-    const LevelGeom& D = g->lv[l];
-    const LevelGeom& S = g->lv[l - 1];
-    for (int r0 = 0; r0 < D.h; r0++) {
-      const int r1 = std::min(r0 + kPyRows, D.h);
-      const int lo = std::min(std::max(g->yofs[D.coef_y + r0], 0), S.h - 1);
-      const int hi = std::min(std::max(g->yofs[D.coef_y + r1 - 1] + 1, 0), S.h - 1);
-      if (hi - lo + 1 > kPySrcRows) {
-        if (why) *why = "scale factor too large for the pyramid chunk";
-        return ORBX_EUNSUPPORTED;
-      }
+  if (p.nlevels == 1) {  // level 0 alone: one copy stage
+    PyrStage st{1, 0, 0, 0, 0, 0};
+    const int nb = std::max(1, g->lv[0].h / kPyBandH);
+    for (int b = 0; b < nb; b++) {
+      PyrBand B{};
+      B.own_lo[0] = B.lo[0] = (int)((int64_t)b * g->lv[0].h / nb);
+      B.own_hi[0] = B.hi[0] = (int)((int64_t)(b + 1) * g->lv[0].h / nb);
+      g->bands.push_back(B);
     }
-    for (int c0 = 0; c0 < D.w; c0++) {
-      const int c1 = std::min(c0 + kPyCols, D.w);
-      const int lo = g->xofs[D.coef_x + c0] & ~3, hi = g->xofs[D.coef_x + c1 - 1] + 1;
-      if ((hi - lo) / 4 + 1 > kPySrcWords || (hi | 3) >= S.pitch) {
-        if (why) *why = "scale factor too large for the pyramid chunk";
-        return ORBX_EUNSUPPORTED;
-      }
-    }
+    st.nbands = nb;
+    st.smem = std::max(16, (g->lv[0].h / nb + 1) * g->lv[0].pitch);
+    g->pyr_stages.push_back(st);
   }
   if (cand >= (1 << 24)) {
     if (why) *why = "candidate capacity exceeds 2^24";

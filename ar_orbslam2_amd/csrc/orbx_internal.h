@@ -21,32 +21,41 @@ constexpr int kMaxIni = 64;     // initial octree columns supported (nIni)
 
 // Per pyramid level, computed on the host once per plan (ORBextractor.cc:404-460,
 // 735-757, 1047-1072).
-// k_pyramid: every image split into row bands, one workgroup per (image, band) builds all
-// levels of its band; a level step runs in chunks of kPyRows x kPyCols output pixels whose
-// source window is staged in LDS (build_geometry rejects scale factors whose windows exceed it)
-#ifndef ORBX_PY_ROWS
-#define ORBX_PY_ROWS 16
-#endif
-#ifndef ORBX_PY_COLS
-#define ORBX_PY_COLS 512
-#endif
+// k_pyramid: the levels are built in a few stages (one launch each); a stage splits every
+// image into row bands, one workgroup per (image, band) builds the stage's levels of its band
+// with the band's previous level held in LDS (two ping-pong buffers)
 #ifndef ORBX_PY_BANDH
-#define ORBX_PY_BANDH 20
+#define ORBX_PY_BANDH 32
 #endif
-constexpr int kPyRows = ORBX_PY_ROWS, kPyCols = ORBX_PY_COLS;
-constexpr int kPySrcRows = (kPyRows * 13 + 9) / 10 + 3;
-constexpr int kPySrcWords = (kPyCols * 13 / 10 + 8) / 4 + 2;
-constexpr int kPyBandH = ORBX_PY_BANDH;  // level-0 rows per band (at most kMaxBands bands)
-constexpr int kMaxBands = 32;
+#ifndef ORBX_PY_NT
+#define ORBX_PY_NT 512
+#endif
+#ifndef ORBX_PY_STAGE0
+#define ORBX_PY_STAGE0 3
+#endif
+#ifndef ORBX_PY_STAGEN
+#define ORBX_PY_STAGEN 4
+#endif
+constexpr int kPyBandH = ORBX_PY_BANDH;  // source-level rows per band (more if LDS is short)
+constexpr int kPyNT = ORBX_PY_NT;        // k_pyramid threads per workgroup
+constexpr int kPyStage0 = ORBX_PY_STAGE0;  // levels built by the first stage (from the input)
+constexpr int kPyStageN = ORBX_PY_STAGEN;  // levels per later stage (from the pyramid)
+constexpr int kPyMaxSmem = 64 * 1024;    // k_pyramid dynamic LDS bound (both buffers)
 struct PyrBand {
-  int lo[kMaxLevels], hi[kMaxLevels];  // rows of each level this band computes (with halo)
+  int lo[kMaxLevels], hi[kMaxLevels];      // rows of each level this band computes (with halo)
+  int own_lo[kMaxLevels], own_hi[kMaxLevels];  // rows it writes to the pyramid (a partition)
+};
+struct PyrStage {
+  int l0, l1;          // builds levels l0..l1 from level l0 - 1 (the input when l0 == 1)
+  int band0, nbands;   // its bands in Geometry::bands
+  int smem, buf_b;     // LDS bytes, offset of the odd-level buffer
 };
 
 struct LevelGeom {
   int w, h;            // level size (cvRound((float)cols * invScale))
   int pitch;           // row pitch in the pyramid / blur blocks (w rounded up to 64 B)
   int64_t pyr_off;     // offset of the level inside one image's pyramid (and blur) block
-  int coef_x, coef_y;  // offsets into the resize coefficient tables (levels >= 1)
+  int coef_x, coef_y;  // offsets into the k_pyramid tap tables (xtap, ytap entries; levels >= 1)
   int xmax;            // HResizeLinear clamp start (dx >= xmax reads S[x0]*2048)
   int vxs;             // VResizeLinearVec_32s8u SSE2 region: x < vxs
   int bxs;             // SymmColumnVec_32s8u region: x < 4*floor(w/4)
@@ -81,9 +90,13 @@ struct Geometry {
   std::vector<CellGeom> cells;
   std::vector<int> xofs, yofs;        // resize source offsets
   std::vector<int16_t> xa, yb;        // resize fixed-point coefficients (pairs)
+  // k_pyramid taps, one int32 pair per output column / row: {x0, a0 << 4 | a1 << 20} (past
+  // xmax already a0 = 2048, a1 = 0; coefficients in [0, 2049]), every level's column run
+  // padded to a multiple of 4 entries; {y0, b0 | b1 << 16}
+  std::vector<int32_t> xtap, ytap;
   int64_t pyr_bytes = 0;              // per image
-  int nbands = 1;                     // k_pyramid row bands per image
-  PyrBand bands[kMaxBands];
+  std::vector<PyrStage> pyr_stages;   // k_pyramid launches, in order
+  std::vector<PyrBand> bands;         // every stage's row bands
   int64_t bm_words = 0;               // per image: two keep planes (ini, min) per level
   int cand_total = 0;                 // per image candidate keys
   int kp_total = 0;                   // per image final keypoint slots

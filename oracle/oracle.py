@@ -79,7 +79,7 @@ def extract(img, p=None, tie_mode=0, cap=None, want_pyramid=False):
     lw = np.zeros(p.nlevels, np.int32)
     lh = np.zeros(p.nlevels, np.int32)
     ncand = np.zeros(p.nlevels, np.int32)
-    pyr_cap = int(w * h * 4 + 1024) if want_pyramid else 0
+    pyr_cap = int(w * h * p.nlevels + 1024) if want_pyramid else 0
     pyr = np.zeros(pyr_cap, np.uint8) if want_pyramid else None
     L = lib()
     L.oracle_extract_ex.restype = C.c_int

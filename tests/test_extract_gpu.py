@@ -89,3 +89,12 @@ def test_descriptor_sincosf_device_exhaustive_angles():
         kps, desc = ex(img)
         okps, odesc = O.extract(img, O.params(1000))
         assert np.array_equal(desc, odesc)
+
+
+@pytest.mark.parametrize("nlevels,scale", [(1, 1.2), (2, 1.2), (4, 1.2), (5, 1.3), (8, 1.1),
+                                           (6, 1.5)])
+@pytest.mark.parametrize("w,h", [(640, 480), (321, 203)])
+def test_level_counts_and_scales(nlevels, scale, w, h):
+    """Pyramid stages and row bands for other level counts, scale factors and widths that are
+    not multiples of 16 (byte-assembled level-0 rows)."""
+    _compare(synth.frame(w, h, t=2, stream=4), 800, scale=scale, nlevels=nlevels)
