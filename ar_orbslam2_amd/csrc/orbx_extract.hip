@@ -533,9 +533,9 @@ __device__ __forceinline__ bool fast_maybe(const uint8_t* s, int stride, int x, 
 //      packed-i16 pairs whose sign bits are folded into one flag word per circle point.
 //  (2) cv::FAST's strict 8-neighbour NMS at both thresholds, with neighbours outside the
 //      pixel's own FAST cell (or outside the detection region) counting as 0 — the cell-local
-//      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  Lane = column,
-//      each wave walks 16 rows keeping the masked 3-wide row maxima of the rows above/below in
-//      registers; one ballot per row and threshold gives the 64-bit keep word of that row.
+//      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  Evaluated at the
+//      queued candidates only (one lane each); survivors set their bit in the row's 64-bit
+//      keep word in LDS (ds_or), which one thread per row and threshold then stores.
 constexpr int kFastT = 64;
 struct FastTile {
   int16_t level, tx, ty, pad;
@@ -674,58 +674,61 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
       s_v[i] = (uint8_t)min(255, max(0, sc + 1));
     }
   }
+  // keep words of the tile's 64 rows at both thresholds; cell-edge masks of its columns / rows
+  __shared__ uint64_t s_keep[2][kFastT];
+  __shared__ uint8_t s_cm[kFastT], s_rm[kFastT];
+  if (tid < kFastT) {
+    s_keep[0][tid] = 0;
+    s_keep[1][tid] = 0;
+    // position inside its FAST cell (detection rows/columns 19 + i*cell ..): at the cell edges
+    // a neighbour belongs to another cell ROI and counts as 0; bit 0 = left / up allowed,
+    // bit 1 = right / down allowed
+    const int wc = max(G.wcell, 1), x = X0 + tid;
+    const int rx = ((x - kEdge) % wc + wc) % wc;
+    s_cm[tid] = (rx != 0 ? 1 : 0) | (rx != wc - 1 && x + 1 < xhi ? 2 : 0);
+  } else if (tid < 2 * kFastT) {
+    const int hc = max(G.hcell, 1), y = Y0 + tid - kFastT;
+    const int ry = ((y - kEdge) % hc + hc) % hc;
+    s_rm[tid - kFastT] = (ry != 0 ? 1 : 0) | (ry != hc - 1 && y + 1 < yhi ? 2 : 0);
+  }
   __syncthreads();
-  // NMS, wave w: rows 16w .. 16w+15 of the tile, lane = column.  V window column of x is
-  // x - X0 + 4, row of y is y - Y0 + 1.
-  const int x = X0 + lane;
-  // position of x / y inside its FAST cell (detection rows/columns 19 + i*hCell ..): the
-  // cell edges are where a neighbour belongs to another cell ROI and counts as 0
-  const int wc = max(G.wcell, 1), hc = max(G.hcell, 1);
-  const int rx = ((x - kEdge) % wc + wc) % wc;
-  const bool xin = x >= xlo && x < xhi;
-  const int mL = rx != 0 ? 0xFF : 0, mR = (rx != wc - 1 && x + 1 < xhi) ? 0xFF : 0;
-  uint64_t* bm_ini = bitmaps + (int64_t)img * bm_words + G.bm_off;
-  uint64_t* bm_min = bm_ini + (int64_t)G.bm_wpr * G.h;
-  uint8_t* vout = vmap + (int64_t)img * pyr_bytes + G.pyr_off;
-  const int r0 = wid * (kFastT / 4);
-  int ry = ((Y0 + r0 - kEdge) % hc + hc) % hc;  // scalar, advanced per row
+  // cv::FAST's strict 8-neighbour NMS at both thresholds, evaluated at the queued candidates
+  // of the tile proper (every other pixel has V = 0 and is never kept).
   // keep at t  <=>  V > t and V-1 > (nmax > t ? nmax-1 : 0)  <=>  V > (nmax > t ? nmax : max(t,1))
   // (a neighbour counts with its score V-1 only if it is a corner at t, V > t; the count is
   // monotone in V, so the largest masked neighbour decides)
   const int ini1 = max(ini_th, 1), min1 = max(min_th, 1);
-  // masked left/right neighbours and centre of V-window row vr
-  auto row_lr = [&](int vr, int& vc, int& lr) {
-    const uint8_t* p = s_v + vr * kVS + lane + 4;
-    vc = p[0];
-    lr = max(p[-1] & mL, p[1] & mR);
-  };
-  int vc_prev, lr_prev, vc_cur, lr_cur;
-  row_lr(r0, vc_prev, lr_prev);      // image row Y0 + r0 - 1
-  row_lr(r0 + 1, vc_cur, lr_cur);    // image row Y0 + r0
-  int hm_prev = max(lr_prev, vc_prev);
-  for (int rr = 0; rr < kFastT / 4; rr++) {
-    const int r = r0 + rr, y = Y0 + r;
-    if (y >= G.h) break;  // wave-uniform
-    int vc_next, lr_next;
-    row_lr(r + 2, vc_next, lr_next);
-    const bool yin = y >= ylo && y < yhi;
-    const bool up = ry != 0, dn = ry != hc - 1 && y + 1 < yhi;  // wave-uniform
-    ry = ry + 1 == hc ? 0 : ry + 1;
-    const int nmax = max(max(up ? hm_prev : 0, dn ? max(lr_next, vc_next) : 0), lr_cur);
-    const int v = vc_cur;
-    const bool cand = xin && yin;
-    const bool ki = cand && v > (nmax > ini_th ? nmax : ini1);
-    const bool km = cand && v > (nmax > min_th ? nmax : min1);
-    const uint64_t wi = __ballot(ki), wm = __ballot(km);
-    if (lane == 0) {
-      bm_ini[(int64_t)y * G.bm_wpr + T.tx] = wi;
-      bm_min[(int64_t)y * G.bm_wpr + T.tx] = wm;
-    }
+  uint8_t* vout = vmap + (int64_t)img * pyr_bytes + G.pyr_off;
+  for (int j0 = 0; j0 < nq; j0 += 64) {
+    const int j = j0 + lane;
+    if (j >= nq) break;
+    const int i = q[j];
+    const int vy = i / kVS, vx = i - vy * kVS;
+    const int tx = vx - 4, ty = vy - 1;  // tile coordinates
+    if (tx < 0 || tx >= kFastT || ty < 0 || ty >= kFastT) continue;
+    const int v = s_v[i];
+    const int cm = s_cm[tx], rm = s_rm[ty];
+    const int mL = cm & 1 ? 0xFF : 0, mR = cm & 2 ? 0xFF : 0;
+    const int mU = rm & 1 ? 0xFF : 0, mD = rm & 2 ? 0xFF : 0;
+    const uint8_t* pu = s_v + i - kVS;
+    const uint8_t* pd = s_v + i + kVS;
+    const int hu = max((int)pu[0], max(pu[-1] & mL, pu[1] & mR)) & mU;
+    const int hd = max((int)pd[0], max(pd[-1] & mL, pd[1] & mR)) & mD;
+    const int nmax = max(max(hu, hd), max(s_v[i - 1] & mL, s_v[i + 1] & mR));
+    const bool ki = v > (nmax > ini_th ? nmax : ini1);
+    const bool km = v > (nmax > min_th ? nmax : min1);
+    if (ki) atomicOr((unsigned long long*)&s_keep[0][ty], 1ull << tx);
+    if (km) atomicOr((unsigned long long*)&s_keep[1][ty], 1ull << tx);
     // k_fast_compact reads V only at survivors of either threshold
-    if (ki || km) vout[(int64_t)y * G.pitch + x] = (uint8_t)v;
-    hm_prev = max(lr_cur, vc_cur);
-    vc_cur = vc_next;
-    lr_cur = lr_next;
+    if (ki || km) vout[(int64_t)(Y0 + ty) * G.pitch + X0 + tx] = (uint8_t)v;
+  }
+  __syncthreads();
+  if (tid < 2 * kFastT) {
+    const int pl = tid >> 6, ty = tid & 63, y = Y0 + ty;
+    if (y < G.h) {
+      uint64_t* bm = bitmaps + (int64_t)img * bm_words + G.bm_off + (int64_t)pl * G.bm_wpr * G.h;
+      bm[(int64_t)y * G.bm_wpr + T.tx] = s_keep[pl][ty];
+    }
   }
 }
 
