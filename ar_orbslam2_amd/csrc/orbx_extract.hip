@@ -528,9 +528,9 @@ __device__ __forceinline__ bool fast_maybe(const uint8_t* s, int stride, int x, 
 //      of the detection region [19, w-19) x [19, h-19) (0 elsewhere).  A pixel failing the
 //      even-point test at min(iniThFAST, minThFAST) cannot be a corner at either threshold, so
 //      its V (<= threshold) is equivalent to 0 in every NMS: only candidates are scored, from
-//      wave-local queues (ballot + mbcnt).  The test runs on 4 adjacent pixels per lane: the
-//      circle bytes of the 4 pixels are one (alignbyte-shifted) LDS dword, compared as two
-//      packed-i16 pairs whose sign bits are folded into one flag word per circle point.
+//      wave-local queues (mbcnt ranks).  The test runs one pixel per lane: each circle point's
+//      darker / brighter compare is a v_cmp into a 64-bit lane mask, and the arc logic runs on
+//      those masks in the scalar unit.
 //  (2) cv::FAST's strict 8-neighbour NMS at both thresholds, with neighbours outside the
 //      pixel's own FAST cell (or outside the detection region) counting as 0 — the cell-local
 //      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  Evaluated at the
@@ -581,10 +581,11 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   constexpr int kWinG = (kFastT + 8) / 4; // V column groups: X0-4 .. X0+67
   constexpr int kVS = kWinG * 4;          // V row stride (bytes)
   constexpr int kGroups = kWinR * kWinG;
-  constexpr int kQ = (kGroups + 255) / 256 * 256;  // per-wave queue bound (4 px per group)
+  constexpr int kRowB = kInD * 4;         // staged row stride (bytes)
+  constexpr int kQ = (kWinR + 3) / 4 * 64 + 64;  // per-wave queue bound (rows + ring pass)
   __shared__ __align__(16) uint32_t s_in[kInR][kInD];
   __shared__ __align__(16) uint32_t s_v32[kWinR * kWinG];
-  __shared__ uint16_t s_q[4][kQ];
+  __shared__ uint16_t s_q[4][kQ + 64];
   int bx, img;
   xcd_block(bx, img);
   const FastTile T = tiles[bx];
@@ -593,77 +594,73 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   const LevelGeom& G = lv[T.level];
   const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
   const int X0 = T.tx * kFastT, Y0 = T.ty * kFastT;
-  for (int i = tid; i < kInR * kInD; i += 256) {
-    const int r = i / kInD, c = i - r * kInD;
+  // staged window: rows Y0-4 .. Y0+67 clamped, 8-byte pieces of columns X0-8 .. X0+71 (zero
+  // left of the image; the 64-B pitch covers the right side)
+  for (int i = tid; i < kInR * (kInD / 2); i += 256) {
+    const int r = i / (kInD / 2), c = i - r * (kInD / 2);
     const int y = min(max(Y0 + r - 4, 0), G.h - 1);
-    const int x = X0 - 8 + 4 * c;
-    s_in[r][c] = (x >= 0 && x + 4 <= G.pitch) ? *(const uint32_t*)(src + (int64_t)y * G.pitch + x)
-                                              : 0u;
+    const int x = X0 - 8 + 8 * c;
+    *(uint2*)&s_in[r][2 * c] = (x >= 0 && x < G.pitch)
+                                   ? *(const uint2*)(src + (int64_t)y * G.pitch + x)
+                                   : make_uint2(0u, 0u);
   }
+  for (int i = tid; i < kGroups; i += 256) s_v32[i] = 0;
   __syncthreads();
   const int t_lo = min(ini_th, min_th);
   const int ylo = kEdge, yhi = G.h - kEdge, xlo = kEdge, xhi = G.w - kEdge;
-  const uint32_t tt = (uint32_t)t_lo * 0x00010001u;
   uint16_t* q = s_q[wid];
   int nq = 0;
-  for (int g0 = wid * 64; g0 < kGroups; g0 += 256) {
-    const int g = g0 + lane;
-    const int vy = g / kWinG, c = g - vy * kWinG;
-    const int y = Y0 - 1 + vy, x = X0 - 4 + 4 * c;
-    uint32_t pass = 0;  // bit j: pixel x+j passes
-    if (g < kGroups) {
-      s_v32[g] = 0;
-      if (y >= ylo && y < yhi && x + 3 >= xlo && x < xhi) {
-        const int r = vy + 3, d = c + 1;
-        const uint32_t* R0 = s_in[r];
-        const uint32_t C = R0[d];
-        const uint32_t cE = __builtin_amdgcn_perm(0u, C, 0x0c020c00u);
-        const uint32_t cO = __builtin_amdgcn_perm(0u, C, 0x0c030c01u);
-        const uint32_t loE = pk_sub_i16(cE, tt), loO = pk_sub_i16(cO, tt);
-        const uint32_t hiE = cE + tt, hiO = cO + tt;  // <= 510 per half, no carry
-        const uint32_t *Rm3 = s_in[r - 3], *Rm2 = s_in[r - 2], *Rp2 = s_in[r + 2],
-                       *Rp3 = s_in[r + 3];
-        const uint32_t m2a = Rm2[d - 1], m2b = Rm2[d], m2c = Rm2[d + 1];
-        const uint32_t p2a = Rp2[d - 1], p2b = Rp2[d], p2c = Rp2[d + 1];
-        const uint32_t r0a = R0[d - 1], r0c = R0[d + 1];
-        // even circle points in circle order: (0,3) (2,2) (3,0) (2,-2) (0,-3) (-2,-2) (-3,0) (-2,2)
-        uint32_t fd[8], fb[8];
-        circle_flags(Rp3[d], loE, loO, hiE, hiO, fd[0], fb[0]);
-        circle_flags(bytes_at<2>(p2a, p2b, p2c), loE, loO, hiE, hiO, fd[1], fb[1]);
-        circle_flags(bytes_at<3>(r0a, C, r0c), loE, loO, hiE, hiO, fd[2], fb[2]);
-        circle_flags(bytes_at<2>(m2a, m2b, m2c), loE, loO, hiE, hiO, fd[3], fb[3]);
-        circle_flags(Rm3[d], loE, loO, hiE, hiO, fd[4], fb[4]);
-        circle_flags(bytes_at<-2>(m2a, m2b, m2c), loE, loO, hiE, hiO, fd[5], fb[5]);
-        circle_flags(bytes_at<-3>(r0a, C, r0c), loE, loO, hiE, hiO, fd[6], fb[6]);
-        circle_flags(bytes_at<-2>(p2a, p2b, p2c), loE, loO, hiE, hiO, fd[7], fb[7]);
-        // any 9-arc contains 4 cyclically consecutive even points, all darker or all brighter
-        uint32_t pd[8], pb[8], any = 0;
+  const uint8_t* sin8 = (const uint8_t*)s_in;
+  // one candidate test: lane masks of the even-point test for the lanes' pixels, centre byte
+  // of each at c + 3 * kRowB + 3 (c = top-left of its 7x7 neighbourhood)
+  auto test = [&](const uint8_t* c, uint64_t ok) -> uint64_t {
+    const int v = c[3 * kRowB + 3];
+    const int lo = v - t_lo, hi = v + t_lo;
+    // even circle points in circle order: (0,3) (2,2) (3,0) (2,-2) (0,-3) (-2,-2) (-3,0) (-2,2)
+    const int e[8] = {c[6 * kRowB + 3], c[5 * kRowB + 5], c[3 * kRowB + 6], c[kRowB + 5],
+                      c[3],             c[kRowB + 1],     c[3 * kRowB],     c[5 * kRowB + 1]};
+    uint64_t dk[8], bk[8];  // lane masks: point k darker / brighter than the threshold band
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-          pd[k] = fd[k] & fd[(k + 1) & 7];
-          pb[k] = fb[k] & fb[(k + 1) & 7];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) any |= (pd[k] & pd[(k + 2) & 7]) | (pb[k] & pb[(k + 2) & 7]);
-        pass = ((any >> 7) & 1u) | ((any >> 14) & 2u) | ((any >> 21) & 4u) | ((any >> 28) & 8u);
-        // detection region, per pixel
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (x + j < xlo || x + j >= xhi) pass &= ~(1u << j);
-      }
+    for (int k = 0; k < 8; k++) {
+      dk[k] = __ballot(e[k] < lo);
+      bk[k] = __ballot(e[k] > hi);
     }
+    // any 9-arc contains 4 cyclically consecutive even points, all darker or all brighter:
+    // with A_k = D_k & D_k+1, OR_k A_k & A_k+2 = (A0|A4)&(A2|A6) | (A1|A5)&(A3|A7)
+    uint64_t pd[8], pb[8];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const bool fj = (pass >> j) & 1u;
-      const uint64_t m = __ballot(fj);
-      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-      if (fj) q[nq + rank] = (uint16_t)(g * 4 + j);
-      nq += __popcll(m);
+    for (int k = 0; k < 8; k++) {
+      pd[k] = dk[k] & dk[(k + 1) & 7];
+      pb[k] = bk[k] & bk[(k + 1) & 7];
     }
+    const uint64_t any = ((pd[0] | pd[4]) & (pd[2] | pd[6])) | ((pd[1] | pd[5]) & (pd[3] | pd[7])) |
+                         ((pb[0] | pb[4]) & (pb[2] | pb[6])) | ((pb[1] | pb[5]) & (pb[3] | pb[7]));
+    return any & ok;
+  };
+  // every lane stores: failing lanes into the wave's 64 spare slots past kQ (no exec juggling)
+  auto enqueue = [&](uint64_t pass, int idx) {
+    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pass >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)pass, 0));
+    q[(pass >> lane) & 1 ? nq + rank : kQ + lane] = (uint16_t)idx;
+    nq += __popcll(pass);
+  };
+  // V window coordinates: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, byte vx + 4
+  // holds the pixel.  Tile columns: lane = column, one wave-uniform row per pass.
+  const uint64_t col_ok = __ballot(X0 + lane >= xlo && X0 + lane < xhi);
+  if (col_ok != 0) {
+    const int vy_lo = max(0, ylo - (Y0 - 1)), vy_hi = min(kWinR, yhi - (Y0 - 1));
+#pragma unroll 2
+    for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)  // rows = wid mod 4
+      enqueue(test(sin8 + vy * kRowB + lane + 5, col_ok), vy * kVS + 4 + lane);
   }
-  // s_v32 zeroing above happens-before the score writes below only within a wave's own
-  // groups; candidates are queued by the same wave that zeroed their group.
+  // ring columns X0-1 (vx 3) and X0+64 (vx 68): 2 * kWinR pixels, lane k = (row, side)
+  for (int k0 = wid * 64; k0 < 2 * kWinR; k0 += 256) {
+    const int k = k0 + lane;
+    const int vy = min(k >> 1, kWinR - 1), vx = k & 1 ? 4 + kFastT : 3;
+    const int x = X0 - 4 + vx, y = Y0 - 1 + vy;
+    const uint64_t ok = __ballot(k < 2 * kWinR && x >= xlo && x < xhi && y >= ylo && y < yhi);
+    if (ok != 0) enqueue(test(sin8 + vy * kRowB + vx + 1, ok), vy * kVS + vx);
+  }
   uint8_t* s_v = (uint8_t*)s_v32;
   for (int j0 = 0; j0 < nq; j0 += 64) {
     const int j = j0 + lane;
