@@ -487,51 +487,48 @@ __device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, i
   return max(q0, -q1) - 1;
 }
 
-__device__ __forceinline__ bool nms_keep(const uint8_t* V, int vs, int p, int t) {
-  const int v = V[p];
-  if (v <= t) return false;
-  const int s = v - 1;
-  const int nb[8] = {p - vs - 1, p - vs, p - vs + 1, p - 1, p + 1, p + vs - 1, p + vs, p + vs + 1};
+// Even-point pretest for one pixel per lane (row stride RS of the staged bytes; c = top-left
+// byte of the pixel's 7x7 neighbourhood): lane mask of the pixels in ok that may be corners at
+// t.  Any 9-arc contains 4 cyclically consecutive even circle points, all darker or all
+// brighter; each point's compare is a v_cmp into a lane mask and, with A_k = D_k & D_k+1,
+// OR_k A_k & A_k+2 = (A0|A4)&(A2|A6) | (A1|A5)&(A3|A7) runs in the scalar unit.
+template <int RS>
+__device__ __forceinline__ uint64_t fast_pretest(const uint8_t* c, int t, uint64_t ok) {
+  const int v = c[3 * RS + 3];
+  const int lo = v - t, hi = v + t;
+  // even circle points in circle order: (0,3) (2,2) (3,0) (2,-2) (0,-3) (-2,-2) (-3,0) (-2,2)
+  const int e[8] = {c[6 * RS + 3], c[5 * RS + 5], c[3 * RS + 6], c[RS + 5],
+                    c[3],          c[RS + 1],     c[3 * RS],     c[5 * RS + 1]};
+  uint64_t pd[8], pb[8], dk[8], bk[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const int q = V[nb[k]];
-    const int nq = q > t ? q - 1 : 0;
-    if (!(s > nq)) return false;
+    dk[k] = __ballot(e[k] < lo);
+    bk[k] = __ballot(e[k] > hi);
   }
-  return true;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    pd[k] = dk[k] & dk[(k + 1) & 7];
+    pb[k] = bk[k] & bk[(k + 1) & 7];
+  }
+  const uint64_t any = ((pd[0] | pd[4]) & (pd[2] | pd[6])) | ((pd[1] | pd[5]) & (pd[3] | pd[7])) |
+                       ((pb[0] | pb[4]) & (pb[2] | pb[6])) | ((pb[1] | pb[5]) & (pb[3] | pb[7]));
+  return any & ok;
 }
 
-// Necessary condition for "corner at t" (9 contiguous darker or brighter circle points): any
-// 9-arc contains 4 cyclically consecutive even positions (0,2,...,14) of the circle, which must
-// then all be darker / all brighter.  Rejects ~4x more pixels than the quarter-point test.
-__device__ __forceinline__ bool fast_maybe(const uint8_t* s, int stride, int x, int y, int t) {
-  const uint8_t* c = s + y * stride + x;
-  const int v = c[0];
-  const int e[8] = {c[3 * stride], c[2 * stride + 2], c[3], c[-2 * stride + 2],
-                    c[-3 * stride], c[-2 * stride - 2], c[-3], c[2 * stride - 2]};
-  const int lo = v - t, hi = v + t;
-  uint32_t dm = 0, bm = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    dm |= (uint32_t)(e[k] < lo) << k;
-    bm |= (uint32_t)(e[k] > hi) << k;
-  }
-  dm |= dm << 8;
-  bm |= bm << 8;
-  const uint32_t rd = dm & (dm >> 1) & (dm >> 2) & (dm >> 3);
-  const uint32_t rb = bm & (bm >> 1) & (bm >> 2) & (bm >> 3);
-  return ((rd | rb) & 0xFF) != 0;
+// rank of this lane among the set lanes of m
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
 // ---- k_fast_tile: FAST for 64 x 64 output pixels of one level per workgroup.
 //  (1) score map V = clamp(cornerScore+1, 0, 255) on the tile plus a 1-px ring, for pixels
 //      of the detection region [19, w-19) x [19, h-19) (0 elsewhere).  A pixel failing the
-//      even-point test at min(iniThFAST, minThFAST) cannot be a corner at either threshold, so
-//      its V (<= threshold) is equivalent to 0 in every NMS: only candidates are scored, from
+//      even-point test at iniThFAST cannot be a corner at it, so its V (<= threshold) is
+//      equivalent to 0 in the NMS: only candidates are scored, from
 //      wave-local queues (mbcnt ranks).  The test runs one pixel per lane: each circle point's
 //      darker / brighter compare is a v_cmp into a 64-bit lane mask, and the arc logic runs on
 //      those masks in the scalar unit.
-//  (2) cv::FAST's strict 8-neighbour NMS at both thresholds, with neighbours outside the
+//  (2) cv::FAST's strict 8-neighbour NMS at iniThFAST, with neighbours outside the
 //      pixel's own FAST cell (or outside the detection region) counting as 0 — the cell-local
 //      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  Evaluated at the
 //      queued candidates only (one lane each); survivors set their bit in the row's 64-bit
@@ -541,40 +538,13 @@ struct FastTile {
   int16_t level, tx, ty, pad;
 };
 
-// bytes x+dx .. x+dx+3 of an LDS row given its dwords d-1, d, d+1 (x = 4d)
-template <int DX>
-__device__ __forceinline__ uint32_t bytes_at(uint32_t wm, uint32_t w0, uint32_t wp) {
-  if constexpr (DX == 0) return w0;
-  else if constexpr (DX > 0) return __builtin_amdgcn_alignbyte(wp, w0, DX);
-  else return __builtin_amdgcn_alignbyte(w0, wm, 4 + DX);
-}
-
-// pk_i16 sign bits of (a - b) for the even / odd byte pairs of two u8x4 words
-__device__ __forceinline__ uint32_t pk_sub_i16(uint32_t a, uint32_t b) {
-  typedef short v2s __attribute__((ext_vector_type(2)));
-  v2s x = __builtin_bit_cast(v2s, a), y = __builtin_bit_cast(v2s, b);
-  return __builtin_bit_cast(uint32_t, (v2s)(x - y));
-}
-
-// darker / brighter flags of one circle point for 4 pixels: sign bit (bit 8j+7) of byte j =
-// pixel x+j.  Bytes 0,2 and 1,3 are compared as packed-i16 pairs; one v_perm gathers the
-// four sign-carrying high bytes back into pixel order.
-__device__ __forceinline__ void circle_flags(uint32_t e, uint32_t loE, uint32_t loO,
-                                             uint32_t hiE, uint32_t hiO, uint32_t& dark,
-                                             uint32_t& bright) {
-  const uint32_t eE = __builtin_amdgcn_perm(0u, e, 0x0c020c00u);
-  const uint32_t eO = __builtin_amdgcn_perm(0u, e, 0x0c030c01u);
-  dark = __builtin_amdgcn_perm(pk_sub_i16(eO, loO), pk_sub_i16(eE, loE), 0x07030501u);
-  bright = __builtin_amdgcn_perm(pk_sub_i16(hiO, eO), pk_sub_i16(hiE, eE), 0x07030501u);
-}
-
 __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ pyr,
                                                    int64_t pyr_bytes, uint8_t* __restrict__ vmap,
                                                    uint64_t* __restrict__ bitmaps,
                                                    int64_t bm_words,
                                                    const LevelGeom* __restrict__ lv,
-                                                   const FastTile* __restrict__ tiles, int ini_th,
-                                                   int min_th) {
+                                                   const FastTile* __restrict__ tiles,
+                                                   int ini_th) {
   constexpr int kInR = kFastT + 8;        // staged rows Y0-4 .. Y0+67
   constexpr int kInD = (kFastT + 16) / 4; // staged dwords: columns X0-8 .. X0+71
   constexpr int kWinR = kFastT + 2;       // V rows Y0-1 .. Y0+64
@@ -606,42 +576,13 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   }
   for (int i = tid; i < kGroups; i += 256) s_v32[i] = 0;
   __syncthreads();
-  const int t_lo = min(ini_th, min_th);
   const int ylo = kEdge, yhi = G.h - kEdge, xlo = kEdge, xhi = G.w - kEdge;
   uint16_t* q = s_q[wid];
   int nq = 0;
   const uint8_t* sin8 = (const uint8_t*)s_in;
-  // one candidate test: lane masks of the even-point test for the lanes' pixels, centre byte
-  // of each at c + 3 * kRowB + 3 (c = top-left of its 7x7 neighbourhood)
-  auto test = [&](const uint8_t* c, uint64_t ok) -> uint64_t {
-    const int v = c[3 * kRowB + 3];
-    const int lo = v - t_lo, hi = v + t_lo;
-    // even circle points in circle order: (0,3) (2,2) (3,0) (2,-2) (0,-3) (-2,-2) (-3,0) (-2,2)
-    const int e[8] = {c[6 * kRowB + 3], c[5 * kRowB + 5], c[3 * kRowB + 6], c[kRowB + 5],
-                      c[3],             c[kRowB + 1],     c[3 * kRowB],     c[5 * kRowB + 1]};
-    uint64_t dk[8], bk[8];  // lane masks: point k darker / brighter than the threshold band
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      dk[k] = __ballot(e[k] < lo);
-      bk[k] = __ballot(e[k] > hi);
-    }
-    // any 9-arc contains 4 cyclically consecutive even points, all darker or all brighter:
-    // with A_k = D_k & D_k+1, OR_k A_k & A_k+2 = (A0|A4)&(A2|A6) | (A1|A5)&(A3|A7)
-    uint64_t pd[8], pb[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      pd[k] = dk[k] & dk[(k + 1) & 7];
-      pb[k] = bk[k] & bk[(k + 1) & 7];
-    }
-    const uint64_t any = ((pd[0] | pd[4]) & (pd[2] | pd[6])) | ((pd[1] | pd[5]) & (pd[3] | pd[7])) |
-                         ((pb[0] | pb[4]) & (pb[2] | pb[6])) | ((pb[1] | pb[5]) & (pb[3] | pb[7]));
-    return any & ok;
-  };
   // every lane stores: failing lanes into the wave's 64 spare slots past kQ (no exec juggling)
   auto enqueue = [&](uint64_t pass, int idx) {
-    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pass >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)pass, 0));
-    q[(pass >> lane) & 1 ? nq + rank : kQ + lane] = (uint16_t)idx;
+    q[(pass >> lane) & 1 ? nq + lane_rank(pass) : kQ + lane] = (uint16_t)idx;
     nq += __popcll(pass);
   };
   // V window coordinates: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, byte vx + 4
@@ -649,9 +590,9 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   const uint64_t col_ok = __ballot(X0 + lane >= xlo && X0 + lane < xhi);
   if (col_ok != 0) {
     const int vy_lo = max(0, ylo - (Y0 - 1)), vy_hi = min(kWinR, yhi - (Y0 - 1));
-#pragma unroll 2
     for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)  // rows = wid mod 4
-      enqueue(test(sin8 + vy * kRowB + lane + 5, col_ok), vy * kVS + 4 + lane);
+      enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th, col_ok),
+              vy * kVS + 4 + lane);
   }
   // ring columns X0-1 (vx 3) and X0+64 (vx 68): 2 * kWinR pixels, lane k = (row, side)
   for (int k0 = wid * 64; k0 < 2 * kWinR; k0 += 256) {
@@ -659,7 +600,7 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     const int vy = min(k >> 1, kWinR - 1), vx = k & 1 ? 4 + kFastT : 3;
     const int x = X0 - 4 + vx, y = Y0 - 1 + vy;
     const uint64_t ok = __ballot(k < 2 * kWinR && x >= xlo && x < xhi && y >= ylo && y < yhi);
-    if (ok != 0) enqueue(test(sin8 + vy * kRowB + vx + 1, ok), vy * kVS + vx);
+    if (ok != 0) enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + vx + 1, ini_th, ok), vy * kVS + vx);
   }
   uint8_t* s_v = (uint8_t*)s_v32;
   for (int j0 = 0; j0 < nq; j0 += 64) {
@@ -671,12 +612,11 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
       s_v[i] = (uint8_t)min(255, max(0, sc + 1));
     }
   }
-  // keep words of the tile's 64 rows at both thresholds; cell-edge masks of its columns / rows
-  __shared__ uint64_t s_keep[2][kFastT];
+  // keep words of the tile's 64 rows; cell-edge masks of its columns / rows
+  __shared__ uint64_t s_keep[kFastT];
   __shared__ uint8_t s_cm[kFastT], s_rm[kFastT];
   if (tid < kFastT) {
-    s_keep[0][tid] = 0;
-    s_keep[1][tid] = 0;
+    s_keep[tid] = 0;
     // position inside its FAST cell (detection rows/columns 19 + i*cell ..): at the cell edges
     // a neighbour belongs to another cell ROI and counts as 0; bit 0 = left / up allowed,
     // bit 1 = right / down allowed
@@ -689,12 +629,12 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     s_rm[tid - kFastT] = (ry != 0 ? 1 : 0) | (ry != hc - 1 && y + 1 < yhi ? 2 : 0);
   }
   __syncthreads();
-  // cv::FAST's strict 8-neighbour NMS at both thresholds, evaluated at the queued candidates
-  // of the tile proper (every other pixel has V = 0 and is never kept).
+  // cv::FAST's strict 8-neighbour NMS at iniThFAST, evaluated at the queued candidates of the
+  // tile proper (every other pixel has V = 0 and is never kept).
   // keep at t  <=>  V > t and V-1 > (nmax > t ? nmax-1 : 0)  <=>  V > (nmax > t ? nmax : max(t,1))
   // (a neighbour counts with its score V-1 only if it is a corner at t, V > t; the count is
   // monotone in V, so the largest masked neighbour decides)
-  const int ini1 = max(ini_th, 1), min1 = max(min_th, 1);
+  const int ini1 = max(ini_th, 1);
   uint8_t* vout = vmap + (int64_t)img * pyr_bytes + G.pyr_off;
   for (int j0 = 0; j0 < nq; j0 += 64) {
     const int j = j0 + lane;
@@ -712,26 +652,47 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     const int hu = max((int)pu[0], max(pu[-1] & mL, pu[1] & mR)) & mU;
     const int hd = max((int)pd[0], max(pd[-1] & mL, pd[1] & mR)) & mD;
     const int nmax = max(max(hu, hd), max(s_v[i - 1] & mL, s_v[i + 1] & mR));
-    const bool ki = v > (nmax > ini_th ? nmax : ini1);
-    const bool km = v > (nmax > min_th ? nmax : min1);
-    if (ki) atomicOr((unsigned long long*)&s_keep[0][ty], 1ull << tx);
-    if (km) atomicOr((unsigned long long*)&s_keep[1][ty], 1ull << tx);
-    // k_fast_compact reads V only at survivors of either threshold
-    if (ki || km) vout[(int64_t)(Y0 + ty) * G.pitch + X0 + tx] = (uint8_t)v;
+    if (v > (nmax > ini_th ? nmax : ini1)) {
+      atomicOr((unsigned long long*)&s_keep[ty], 1ull << tx);
+      vout[(int64_t)(Y0 + ty) * G.pitch + X0 + tx] = (uint8_t)v;  // read at survivors only
+    }
   }
   __syncthreads();
-  if (tid < 2 * kFastT) {
-    const int pl = tid >> 6, ty = tid & 63, y = Y0 + ty;
-    if (y < G.h) {
-      uint64_t* bm = bitmaps + (int64_t)img * bm_words + G.bm_off + (int64_t)pl * G.bm_wpr * G.h;
-      bm[(int64_t)y * G.bm_wpr + T.tx] = s_keep[pl][ty];
-    }
+  if (tid < kFastT) {
+    const int y = Y0 + tid;
+    if (y < G.h) bitmaps[(int64_t)img * bm_words + G.bm_off + (int64_t)y * G.bm_wpr + T.tx] = s_keep[tid];
   }
 }
 
 // ---- k_fast_compact: per FAST cell (one wave, lane = detection row): survivors at
-// iniThFAST, else at minThFAST (ORBextractor.cc:780-784), raster order (row prefix sum, then
-// ascending x) into the cell's candidate slot, keys relative to minBorder = 16.
+// iniThFAST (ORBextractor.cc:780) in raster order (row prefix sum, then ascending x) into the
+// cell's candidate slot, keys relative to minBorder = 16.  A cell without any is queued for
+// k_fast_fallback (the minThFAST retry, ORBextractor.cc:782-784).
+__device__ __forceinline__ uint32_t cand_key(int x, int y, int v) {
+  return (uint32_t)(x - (kEdge - 3)) | ((uint32_t)(y - (kEdge - 3)) << 12) | ((uint32_t)(v - 1) << 24);
+}
+
+// raster-order compaction of a cell's keep rows (lane = detection row): out slot, count
+template <class VAt>
+__device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int cx0,
+                                             uint32_t* out, int* cnt_out, VAt v_at) {
+  const int cnt = __popcll(bits);
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int n = __shfl_up(incl, o);
+    if (lane >= o) incl += n;
+  }
+  int pos = incl - cnt;
+  const int nout = __shfl(incl, 63);
+  while (bits) {
+    const int k = __builtin_ctzll(bits);
+    bits &= bits - 1;
+    out[pos++] = cand_key(cx0 + k, y, v_at(k));
+  }
+  if (lane == 0) *cnt_out = nout;
+}
+
 __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict__ vmap,
                                                       int64_t pyr_bytes,
                                                       const uint64_t* __restrict__ bitmaps,
@@ -740,7 +701,9 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
                                                       const CellGeom* __restrict__ cells,
                                                       int ncells, uint32_t* __restrict__ cand,
                                                       int cand_total,
-                                                      int* __restrict__ cell_counts) {
+                                                      int* __restrict__ cell_counts,
+                                                      int* __restrict__ fb_count,
+                                                      int* __restrict__ fb_list) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int bx, img;
   xcd_block(bx, img);
@@ -758,40 +721,128 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
   const int y = C.y0 + 3 + lane;
   const int wa = cx0 >> 6, sh = cx0 & 63, width = cx1 - cx0;  // width <= 60
   const uint64_t wmask = width >= 64 ? ~0ull : ((1ull << width) - 1);
-  auto row_bits = [&](const uint64_t* plane) -> uint64_t {
-    if (lane >= dr) return 0;
-    const uint64_t* row = plane + (int64_t)y * G.bm_wpr + wa;
-    uint64_t b = row[0] >> sh;
-    if (sh && sh + width > 64) b |= row[1] << (64 - sh);
-    return b & wmask;
-  };
-  uint64_t bits = row_bits(bm);
-  int cnt = __popcll(bits);
-  int total = cnt;
+  uint64_t bits = 0;
+  if (lane < dr) {
+    const uint64_t* row = bm + (int64_t)y * G.bm_wpr + wa;
+    bits = row[0] >> sh;
+    if (sh && sh + width > 64) bits |= row[1] << (64 - sh);
+    bits &= wmask;
+  }
+  if (__ballot(bits != 0) == 0) {  // no keypoint at iniThFAST: k_fast_fallback takes the cell
+    if (lane == 0) {  // queue fb_big of the image: counts [2 img + fb_big], lists of ncells
+      const int qi = 2 * img + C.fb_big;
+      fb_list[(int64_t)qi * ncells + atomicAdd(fb_count + qi, 1)] = ci;
+    }
+    return;
+  }
+  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch + cx0;
+  compact_rows(bits, lane, y, cx0, cand + (int64_t)img * cand_total + C.slot_off, cnt_out,
+               [&](int k) { return (int)V[k]; });
+}
+
+// ---- k_fast_fallback: the cells queued by k_fast_compact, one wave each (kFbWG workgroups
+// per image walk the queue): cv::FAST with NMS at minThFAST on the cell image
+// (ORBextractor.cc:782-784).  The ROI is staged in LDS; each detection row runs the even-point
+// pretest, candidates are scored in batches of 64 from a wave queue into a zero-ringed V map
+// (pixels outside the cell's detection region count as 0: the NMS is cell-local by
+// construction), then the NMS per row gives the keep rows that are compacted as above.
+// Cells at most 32 wide run two detection rows per wave step (half-wave each).
+// Instantiated for RS x MAXR staged windows: <44, 44> (cells up to 38 wide/high, the usual
+// 30-px grid) and <72, 66> (any cell, wCell / hCell < 60).
+constexpr int kFbWG = 16;  // workgroups per image
+template <int RS, int MAXR>
+__global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict__ pyr,
+                                                       int64_t pyr_bytes,
+                                                       const LevelGeom* __restrict__ lv,
+                                                       const CellGeom* __restrict__ cells,
+                                                       int ncells, const int* __restrict__ fb_count,
+                                                       const int* __restrict__ fb_list, int min_th,
+                                                       uint32_t* __restrict__ cand, int cand_total,
+                                                       int* __restrict__ cell_counts) {
+  __shared__ __align__(16) uint8_t s_src[4][MAXR * RS + 16];
+  __shared__ __align__(16) uint8_t s_vv[4][(MAXR - 4) * RS];
+  __shared__ uint16_t s_q[4][128 + 64];
+  __shared__ uint64_t s_rows[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int img = blockIdx.y;
+  const int qi = 2 * img + (RS > 44);  // this instance's queue (k_fast_compact)
+  const int nfb = fb_count[qi];
+  uint8_t* S = s_src[wid];
+  uint8_t* V = s_vv[wid];
+  uint16_t* q = s_q[wid];
+  const int t1 = max(min_th, 1);
+  for (int k = blockIdx.x * 4 + wid; k < nfb; k += gridDim.x * 4) {  // wave-uniform
+    const int ci = fb_list[(int64_t)qi * ncells + k];
+    const CellGeom C = cells[ci];
+    const LevelGeom& G = lv[C.level];
+    const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
+    const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3 (fb_big)
+    const int dr = rows - 6, cw = cols - 6;            // > 0 (k_fast_compact)
+    // stage the ROI as aligned dwords (its first pixel lands at byte sh of each staged row;
+    // the 64-B pitch covers the last dword), four loads in flight per lane; zero the V map
+    // (rows dr + 2, columns cw + 2 with the ring)
+    const int a0 = C.x0 & ~3, sh = C.x0 & 3, words = (sh + cols + 3) >> 2;  // <= RS / 4
+    const uint8_t* srow = src + (int64_t)C.y0 * G.pitch + a0;
+    const int items = rows * words;
+    const float inv = 1.0f / (float)words;
+    for (int i0 = lane; i0 < items; i0 += 256) {
+      uint32_t v[4];
+      int rr[4], cc[4];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o);
-  if (total == 0) {
-    bits = row_bits(bm + (int64_t)G.bm_wpr * G.h);
-    cnt = __popcll(bits);
-  }
-  int incl = cnt;
+      for (int u = 0; u < 4; u++) {
+        py_divmod(min(i0 + 64 * u, items - 1), words, inv, rr[u], cc[u]);
+        v[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr[u], G.pitch) + 4 * cc[u]);
+      }
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int n = __shfl_up(incl, o);
-    if (lane >= o) incl += n;
+      for (int u = 0; u < 4; u++) asm volatile("" : "+v"(v[u]));
+#pragma unroll
+      for (int u = 0; u < 4; u++) *(uint32_t*)(S + rr[u] * RS + 4 * cc[u]) = v[u];
+    }
+    for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
+    const uint8_t* Sx = S + sh;  // pixel (r, c) of the ROI at Sx[r * RS + c]
+    const bool half = cw <= 32;  // wave-uniform
+    const int col = half ? lane & 31 : lane, sub = half ? lane >> 5 : 0, step = half ? 2 : 1;
+    int nq = 0;
+    auto score_batch = [&](int m) {  // the first m (<= 64) queued candidates, then shift
+      if (lane < m) {
+        const int e = q[lane], r = e >> 6, c = e & 63;
+        const int sc = fast_score(Sx, RS, c + 3, r + 3);
+        V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
+      }
+      const int rest = nq - m;
+      const uint16_t moved = lane < rest ? q[m + lane] : 0;
+      if (lane < rest) q[lane] = moved;
+      nq = rest;
+    };
+    for (int r0 = 0; r0 < dr; r0 += step) {
+      const int r = r0 + sub;
+      const uint64_t ok = __ballot(col < cw && r < dr);
+      const uint64_t pass = fast_pretest<RS>(Sx + min(r, dr - 1) * RS + col, min_th, ok);
+      q[(pass >> lane) & 1 ? nq + lane_rank(pass) : 128 + lane] = (uint16_t)(r * 64 + col);
+      nq += __popcll(pass);
+      if (nq >= 64) score_batch(64);
+    }
+    if (nq > 0) score_batch(nq);
+    // NMS at minThFAST; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
+    for (int r0 = 0; r0 < dr; r0 += step) {
+      const int r = r0 + sub;
+      const uint8_t* p = V + (min(r, dr - 1) + 1) * RS + col + 1;
+      const int v = p[0];
+      const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
+                           max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
+      const uint64_t keep = __ballot(col < cw && r < dr && v > (nmax > min_th ? nmax : t1));
+      if (lane == 0) {
+        s_rows[wid][r0] = half ? keep & 0xFFFFFFFFull : keep;
+        if (half && r0 + 1 < dr) s_rows[wid][r0 + 1] = keep >> 32;
+      }
+    }
+    const uint64_t bits = lane < dr ? s_rows[wid][lane] : 0;
+    const uint8_t* Vr = V + (lane + 1) * RS + 1;
+    compact_rows(bits, lane, C.y0 + 3 + lane, C.x0 + 3,
+                 cand + (int64_t)img * cand_total + C.slot_off,
+                 cell_counts + (int64_t)img * ncells + ci, [&](int kk) { return (int)Vr[kk]; });
   }
-  int pos = incl - cnt;
-  const int nout = __shfl(incl, 63);
-  uint32_t* out = cand + (int64_t)img * cand_total + C.slot_off;
-  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch;
-  while (bits) {
-    const int k = __builtin_ctzll(bits);
-    bits &= bits - 1;
-    const int xx = cx0 + k;
-    out[pos++] = (uint32_t)(xx - (kEdge - 3)) | ((uint32_t)(y - (kEdge - 3)) << 12) |
-                 ((uint32_t)(V[xx] - 1) << 24);
-  }
-  if (lane == 0) *cnt_out = nout;
 }
 
 // ------------------------------------------------------------------ k_octree
@@ -1373,6 +1424,7 @@ struct orbx_plan {
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
   uint32_t *d_cand = nullptr, *d_lin = nullptr, *d_okey = nullptr;
   int *d_cell_counts = nullptr, *d_label = nullptr, *d_ocount = nullptr, *d_counts = nullptr;
+  int *d_fb_count = nullptr, *d_fb_list = nullptr;  // k_fast_fallback queue per image
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   size_t oct_smem = 0;
@@ -1420,11 +1472,20 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   if (ncells > 0) {
     hipLaunchKernelGGL(k_fast_tile, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
-                       g.ini_th, g.min_th);
+                       g.ini_th);
     pr.mark(P->stream, st_fs);
+    hipMemsetAsync(P->d_fb_count, 0, sizeof(int) * 2 * n, P->stream);
     hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
                        P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_lv, P->d_cells,
-                       ncells, P->d_cand, g.cand_total, P->d_cell_counts);
+                       ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
+                       P->d_fb_list);
+    hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
+                       P->d_pyr, g.pyr_bytes, P->d_lv, P->d_cells, ncells, P->d_fb_count,
+                       P->d_fb_list, g.min_th, P->d_cand, g.cand_total, P->d_cell_counts);
+    hipLaunchKernelGGL((k_fast_fallback<72, kCellMax>), dim3(kFbWG / 4, n), dim3(256), 0,
+                       P->stream, P->d_pyr, g.pyr_bytes, P->d_lv, P->d_cells, ncells,
+                       P->d_fb_count, P->d_fb_list, g.min_th, P->d_cand, g.cand_total,
+                       P->d_cell_counts);
     pr.mark(P->stream, st_fast);
   }
   hipLaunchKernelGGL(k_octree, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream, P->d_lv,
@@ -1512,6 +1573,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
+      dalloc(&P->d_fb_count, 2 * B) || dalloc(&P->d_fb_list, 2 * B * g.cells.size()) ||
       dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels) ||
       dalloc(&P->d_counts, B) || dalloc(&P->d_kps, B * g.kp_total) ||
       dalloc(&P->d_desc, B * g.kp_total * 32))
@@ -1547,7 +1609,7 @@ int orbx_plan_destroy(orbx_plan* P) {
   if (!P) return ORBX_OK;
   if (P->graph) hipGraphExecDestroy(P->graph);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xtap,   P->d_ytap,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
-                  P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label,
+                  P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label, P->d_fb_count, P->d_fb_list,
                   P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
   for (void* p : ptrs)
     if (p) hipFree(p);

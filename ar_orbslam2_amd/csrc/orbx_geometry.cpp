@@ -175,7 +175,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     L.cand_off = cand;
     L.bm_wpr = L.pitch / 64;
     L.bm_off = g->bm_words;
-    g->bm_words += 2 * (int64_t)L.bm_wpr * L.h;
+    g->bm_words += (int64_t)L.bm_wpr * L.h;
     if (nCols > 0 && nRows > 0) {
       const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
       L.wcell = wCell;
@@ -198,6 +198,8 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
           c.offx = (int16_t)(j * wCell);
           c.offy = (int16_t)(i * hCell);
           c.level = (int16_t)l;
+          // k_fast_fallback instance: 0 = <44, 44>, 1 = <72, kCellMax>
+          c.fb_big = (int16_t)(c.x1 - c.x0 + 3 > 44 || c.y1 - c.y0 > 44);
           const int dc = c.x1 - c.x0 - 6, dr = c.y1 - c.y0 - 6;
           // strict 8-neighbour NMS survivors form an independent set of the king graph
           c.slot_cap = (dc > 0 && dr > 0) ? ((dc + 1) / 2) * ((dr + 1) / 2) : 0;

@@ -79,7 +79,7 @@ struct LevelGeom {
 struct CellGeom {
   int16_t x0, y0, x1, y1;  // cell image ROI in level coordinates [x0,x1) x [y0,y1)
   int16_t offx, offy;      // j*wCell, i*hCell (ORBextractor.cc:789-790)
-  int16_t level, pad;
+  int16_t level, fb_big;  // fb_big: ROI too large for k_fast_fallback<44, 44>
   int slot_off, slot_cap;  // candidate slot inside the image's candidate block
 };
 
@@ -97,7 +97,7 @@ struct Geometry {
   int64_t pyr_bytes = 0;              // per image
   std::vector<PyrStage> pyr_stages;   // k_pyramid launches, in order
   std::vector<PyrBand> bands;         // every stage's row bands
-  int64_t bm_words = 0;               // per image: two keep planes (ini, min) per level
+  int64_t bm_words = 0;               // per image: the iniThFAST keep plane of every level
   int cand_total = 0;                 // per image candidate keys
   int kp_total = 0;                   // per image final keypoint slots
   int node_cap_max = 0;

@@ -98,3 +98,13 @@ def test_level_counts_and_scales(nlevels, scale, w, h):
     """Pyramid stages and row bands for other level counts, scale factors and widths that are
     not multiples of 16 (byte-assembled level-0 rows)."""
     _compare(synth.frame(w, h, t=2, stream=4), 800, scale=scale, nlevels=nlevels)
+
+
+@pytest.mark.parametrize("contrast", [3, 5, 8])
+def test_min_threshold_fallback_cells(contrast):
+    """Low-contrast texture (left half) next to full contrast: many cells find nothing at
+    iniThFAST and retry at minThFAST (k_fast_fallback), the others do not."""
+    img = synth.frame(640, 480, t=1, stream=2).astype(np.int32)
+    img[:, :320] = 128 + (img[:, :320] - 128) // contrast
+    kps = _compare(img.astype(np.uint8), 1000)
+    assert len(kps) > 300
