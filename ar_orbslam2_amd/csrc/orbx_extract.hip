@@ -693,11 +693,11 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
   if (lane == 0) *cnt_out = nout;
 }
 
+constexpr int kCompactCap = 30 * 30;  // survivors of a cell <= slot_cap (cells < 60 x 60)
 __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict__ vmap,
                                                       int64_t pyr_bytes,
                                                       const uint64_t* __restrict__ bitmaps,
                                                       int64_t bm_words,
-                                                      const LevelGeom* __restrict__ lv,
                                                       const CellGeom* __restrict__ cells,
                                                       int ncells, uint32_t* __restrict__ cand,
                                                       int cand_total,
@@ -709,21 +709,18 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
   xcd_block(bx, img);
   const int ci = bx * 4 + wid;
   if (ci >= ncells) return;
-  const CellGeom C = cells[ci];
-  const LevelGeom& G = lv[C.level];
-  const int dr = C.y1 - C.y0 - 6, cx0 = C.x0 + 3, cx1 = C.x1 - 3;
+  const CellGeom C = cells[ci];  // one dependent load: everything below addresses from it
+  const int dr = C.y1 - C.y0 - 6, cx0 = C.x0 + 3, width = C.x1 - 3 - cx0;  // width <= 60
   int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
-  if (dr <= 0 || cx1 <= cx0) {
+  if (dr <= 0 || width <= 0) {
     if (lane == 0) *cnt_out = 0;
     return;
   }
-  const uint64_t* bm = bitmaps + (int64_t)img * bm_words + G.bm_off;
-  const int y = C.y0 + 3 + lane;
-  const int wa = cx0 >> 6, sh = cx0 & 63, width = cx1 - cx0;  // width <= 60
+  const int sh = cx0 & 63;
   const uint64_t wmask = width >= 64 ? ~0ull : ((1ull << width) - 1);
   uint64_t bits = 0;
   if (lane < dr) {
-    const uint64_t* row = bm + (int64_t)y * G.bm_wpr + wa;
+    const uint64_t* row = bitmaps + (int64_t)img * bm_words + C.bm_row0 + lane * C.bm_wpr;
     bits = row[0] >> sh;
     if (sh && sh + width > 64) bits |= row[1] << (64 - sh);
     bits &= wmask;
@@ -735,17 +732,39 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
     }
     return;
   }
-  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + G.pyr_off + (int64_t)y * G.pitch + cx0;
-  compact_rows(bits, lane, y, cx0, cand + (int64_t)img * cand_total + C.slot_off, cnt_out,
-               [&](int k) { return (int)V[k]; });
+  // raster order: row prefix sum, then ascending x.  Each row lists its survivors (row, column)
+  // at its prefix slots in LDS; then lane s takes survivor s: one round of parallel V loads and
+  // coalesced key stores per 64 survivors.
+  __shared__ uint16_t s_rc[4][kCompactCap];
+  uint16_t* rc = s_rc[wid];
+  const int cnt = __popcll(bits);
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int n = __shfl_up(incl, o);
+    if (lane >= o) incl += n;
+  }
+  const int nout = __shfl(incl, 63);  // <= slot_cap <= kCompactCap
+  for (int pos = incl - cnt; bits; bits &= bits - 1)
+    rc[pos++] = (uint16_t)((lane << 8) | __builtin_ctzll(bits));
+  uint32_t* out = cand + (int64_t)img * cand_total + C.slot_off;
+  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + C.v_row0;
+  for (int s0 = 0; s0 < nout; s0 += 64) {
+    const int si = s0 + lane;
+    if (si < nout) {
+      const int e = rc[si], r = e >> 8, k = e & 0xFF;
+      out[si] = cand_key(cx0 + k, C.y0 + 3 + r, (int)V[r * C.pitch + k]);
+    }
+  }
+  if (lane == 0) *cnt_out = nout;
 }
 
 // ---- k_fast_fallback: the cells queued by k_fast_compact, one wave each (kFbWG workgroups
 // per image walk the queue): cv::FAST with NMS at minThFAST on the cell image
 // (ORBextractor.cc:782-784).  The ROI is staged in LDS; each detection row runs the even-point
-// pretest, candidates are scored in batches of 64 from a wave queue into a zero-ringed V map
-// (pixels outside the cell's detection region count as 0: the NMS is cell-local by
-// construction), then the NMS per row gives the keep rows that are compacted as above.
+// pretest into a wave queue, the queued candidates are scored into a zero-ringed V map (pixels
+// outside the cell's detection region count as 0: the NMS is cell-local by construction) and
+// NMS'd, setting their bits in the keep rows that are compacted as above.
 // Cells at most 32 wide run two detection rows per wave step (half-wave each).
 // Instantiated for RS x MAXR staged windows: <44, 44> (cells up to 38 wide/high, the usual
 // 30-px grid) and <72, 66> (any cell, wCell / hCell < 60).
@@ -761,7 +780,8 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
                                                        int* __restrict__ cell_counts) {
   __shared__ __align__(16) uint8_t s_src[4][MAXR * RS + 16];
   __shared__ __align__(16) uint8_t s_vv[4][(MAXR - 4) * RS];
-  __shared__ uint16_t s_q[4][128 + 64];
+  constexpr int QCAP = (MAXR - 6) * (RS - 9);  // detection pixels of the largest cell
+  __shared__ uint16_t s_q[4][QCAP + 64];
   __shared__ uint64_t s_rows[4][64];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -803,39 +823,31 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
     const uint8_t* Sx = S + sh;  // pixel (r, c) of the ROI at Sx[r * RS + c]
     const bool half = cw <= 32;  // wave-uniform
     const int col = half ? lane & 31 : lane, sub = half ? lane >> 5 : 0, step = half ? 2 : 1;
+    // every candidate of the cell stays queued (row << 6 | column): scored in batches of 64,
+    // then the NMS runs at the queued pixels only (all others have V = 0)
     int nq = 0;
-    auto score_batch = [&](int m) {  // the first m (<= 64) queued candidates, then shift
-      if (lane < m) {
-        const int e = q[lane], r = e >> 6, c = e & 63;
-        const int sc = fast_score(Sx, RS, c + 3, r + 3);
-        V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
-      }
-      const int rest = nq - m;
-      const uint16_t moved = lane < rest ? q[m + lane] : 0;
-      if (lane < rest) q[lane] = moved;
-      nq = rest;
-    };
     for (int r0 = 0; r0 < dr; r0 += step) {
       const int r = r0 + sub;
       const uint64_t ok = __ballot(col < cw && r < dr);
       const uint64_t pass = fast_pretest<RS>(Sx + min(r, dr - 1) * RS + col, min_th, ok);
-      q[(pass >> lane) & 1 ? nq + lane_rank(pass) : 128 + lane] = (uint16_t)(r * 64 + col);
+      q[(pass >> lane) & 1 ? nq + lane_rank(pass) : QCAP + lane] = (uint16_t)(r * 64 + col);
       nq += __popcll(pass);
-      if (nq >= 64) score_batch(64);
     }
-    if (nq > 0) score_batch(nq);
+    for (int j = lane; j < nq; j += 64) {
+      const int e = q[j], r = e >> 6, c = e & 63;
+      const int sc = fast_score(Sx, RS, c + 3, r + 3);
+      V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
+    }
+    if (lane < dr) s_rows[wid][lane] = 0;
     // NMS at minThFAST; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
-    for (int r0 = 0; r0 < dr; r0 += step) {
-      const int r = r0 + sub;
-      const uint8_t* p = V + (min(r, dr - 1) + 1) * RS + col + 1;
+    for (int j = lane; j < nq; j += 64) {
+      const int e = q[j], r = e >> 6, c = e & 63;
+      const uint8_t* p = V + (r + 1) * RS + c + 1;
       const int v = p[0];
       const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
                            max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
-      const uint64_t keep = __ballot(col < cw && r < dr && v > (nmax > min_th ? nmax : t1));
-      if (lane == 0) {
-        s_rows[wid][r0] = half ? keep & 0xFFFFFFFFull : keep;
-        if (half && r0 + 1 < dr) s_rows[wid][r0 + 1] = keep >> 32;
-      }
+      if (v > (nmax > min_th ? nmax : t1))
+        atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
     }
     const uint64_t bits = lane < dr ? s_rows[wid][lane] : 0;
     const uint8_t* Vr = V + (lane + 1) * RS + 1;
@@ -1476,8 +1488,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
     pr.mark(P->stream, st_fs);
     hipMemsetAsync(P->d_fb_count, 0, sizeof(int) * 2 * n, P->stream);
     hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
-                       P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_lv, P->d_cells,
-                       ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
+                       P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
                        P->d_fb_list);
     hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
                        P->d_pyr, g.pyr_bytes, P->d_lv, P->d_cells, ncells, P->d_fb_count,

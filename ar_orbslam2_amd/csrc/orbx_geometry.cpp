@@ -205,6 +205,10 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
           c.slot_cap = (dc > 0 && dr > 0) ? ((dc + 1) / 2) * ((dr + 1) / 2) : 0;
           c.slot_off = cand;
           cand += c.slot_cap;
+          c.bm_row0 = (int)(L.bm_off + (int64_t)(c.y0 + 3) * L.bm_wpr + ((c.x0 + 3) >> 6));
+          c.v_row0 = (int)(L.pyr_off + (int64_t)(c.y0 + 3) * L.pitch + c.x0 + 3);
+          c.bm_wpr = (int16_t)L.bm_wpr;
+          c.pitch = (int16_t)L.pitch;
           g->cells.push_back(c);
         }
       }

@@ -79,8 +79,13 @@ struct LevelGeom {
 struct CellGeom {
   int16_t x0, y0, x1, y1;  // cell image ROI in level coordinates [x0,x1) x [y0,y1)
   int16_t offx, offy;      // j*wCell, i*hCell (ORBextractor.cc:789-790)
-  int16_t level, fb_big;  // fb_big: ROI too large for k_fast_fallback<44, 44>
+  int16_t level, fb_big;   // fb_big: ROI too large for k_fast_fallback<44, 44>
   int slot_off, slot_cap;  // candidate slot inside the image's candidate block
+  // k_fast_compact addressing of the first detection row (per image): its keep-bitmap word
+  // holding column x0 + 3, and its V byte at column x0 + 3; with the level's row strides
+  int bm_row0, v_row0;
+  int16_t bm_wpr, pitch;
+  int pad;
 };
 
 struct Geometry {
