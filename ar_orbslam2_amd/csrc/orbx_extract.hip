@@ -1316,18 +1316,21 @@ __global__ __launch_bounds__(256) void k_describe(
   for (int l = 1; l < kMaxLevels; l++) level += (l < nlevels && slot >= ko.off[l]);
   const LevelGeom& G = lv[level];
   const int idx = slot - ko.off[level];
-  const bool active = slot < kp_total && idx < oc[level];  // uniform within the half-wave
-  int cx = 0, cy = 0;
-  uint32_t key = 0;
-  if (active) {
-    key = okey[(int64_t)img * kp_total + slot];
-    cx = (int)(key & 0xFFF) + (kEdge - 3);
-    cy = (int)((key >> 12) & 0xFFF) + (kEdge - 3);
-  }
+  // the count, the key and the level's fields in one round of loads, pinned in registers (a
+  // rematerialised load of G per patch row would serialise the patch loads behind it)
+  int noc = oc[level];
+  uint32_t key = okey[(int64_t)img * kp_total + min(slot, kp_total - 1)];
+  int pitch = G.pitch, pyr_off = (int)G.pyr_off;
+  float lscale = G.scale, lsize = G.size;
+  asm volatile("" : "+v"(noc), "+v"(key), "+v"(pitch), "+v"(pyr_off), "+v"(lscale), "+v"(lsize));
+  const bool active = slot < kp_total && idx < noc;  // uniform within the half-wave
+  if (!active) key = 0;
+  const int cx = active ? (int)(key & 0xFFF) + (kEdge - 3) : 0;
+  const int cy = active ? (int)((key >> 12) & 0xFFF) + (kEdge - 3) : 0;
   // stage both patches with aligned dword loads issued together: the raw 31 x 31 patch
   // (IC_Angle, radius 15) and the blurred 37 x 37 patch (rBRIEF samples, radius <= 18)
-  const uint8_t* L = level_base(pyr, pyr_bytes, G, img);
-  const uint8_t* Bp = blur + (int64_t)img * pyr_bytes + G.pyr_off;
+  const uint8_t* L = pyr + (int64_t)img * pyr_bytes + pyr_off;
+  const uint8_t* Bp = blur + (int64_t)img * pyr_bytes + pyr_off;
   const int fr = (cx - 15) >> 2, lr = (cx + 15) >> 2;  // raw dword columns
   const int fb = (cx - 18) >> 2, lb = (cx + 18) >> 2;  // blurred dword columns
   if (active) {
@@ -1336,14 +1339,14 @@ __global__ __launch_bounds__(256) void k_describe(
     for (int k = 0; k < (RN + 31) / 32; k++) {
       const int i = hl + 32 * k, r = i / RW, c = i - r * RW;
       vr[k] = (i < RN && fr + c <= lr)
-                  ? *(const uint32_t*)(L + (uint32_t)((cy - 15 + r) * G.pitch + 4 * (fr + c)))
+                  ? *(const uint32_t*)(L + (uint32_t)((cy - 15 + r) * pitch + 4 * (fr + c)))
                   : 0u;
     }
 #pragma unroll
     for (int k = 0; k < (BN + 31) / 32; k++) {
       const int i = hl + 32 * k, r = i / BW, c = i - r * BW;
       vb[k] = (i < BN && fb + c <= lb)
-                  ? *(const uint32_t*)(Bp + (uint32_t)((cy - 18 + r) * G.pitch + 4 * (fb + c)))
+                  ? *(const uint32_t*)(Bp + (uint32_t)((cy - 18 + r) * pitch + 4 * (fb + c)))
                   : 0u;
     }
 #pragma unroll
@@ -1401,9 +1404,9 @@ __global__ __launch_bounds__(256) void k_describe(
   desc[o * 32 + hl] = (uint8_t)byte;
   if (hl == 0) {
     orbx_keypoint k;
-    k.x = level ? (float)(cx) * G.scale : (float)cx;
-    k.y = level ? (float)(cy) * G.scale : (float)cy;
-    k.size = G.size;
+    k.x = level ? (float)(cx) * lscale : (float)cx;
+    k.y = level ? (float)(cy) * lscale : (float)cy;
+    k.size = lsize;
     k.angle = angle;
     k.response = (float)(key >> 24);
     k.octave = level;
