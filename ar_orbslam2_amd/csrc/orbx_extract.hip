@@ -1206,7 +1206,6 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
     uint32_t* __restrict__ lin, int* __restrict__ label, uint32_t* __restrict__ okey,
     int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
     int key_cap) {
-  (void)key_cap;
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_tmp[kOctNT / 64 + 1];
   __shared__ int s_misc[8];
@@ -1239,22 +1238,33 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
   int* t4 = (int*)take(4 * NC);
   int* cpre = (int*)take(4 * (cell_cap + 1));
   uint64_t* pk = (uint64_t*)take(8 * NC);
+  int* s_slot = (int*)take(4 * cell_cap);
+  uint16_t* own = (uint16_t*)take(2 * key_cap);
   __shared__ uint64_t s_tmp64[kOctNT / 64 + 1];
 
-  // 1. gather candidates of this level in cell order (vToDistributeKeys)
+  // 1. gather candidates of this level in cell order (vToDistributeKeys): counts and slots of
+  // every cell in one round of loads, each key's cell from an owner table, then every key
+  // load in flight at once
   const int* cntv = cell_counts + (int64_t)img * ncells + G.cell_begin;
-  for (int i = tid; i < G.ncells; i += kOctNT) cpre[i] = cntv[i];
+  for (int i = tid; i < G.ncells; i += kOctNT) {
+    cpre[i] = cntv[i];
+    s_slot[i] = cells[G.cell_begin + i].slot_off;
+  }
   __syncthreads();
   const int n = block_scan_excl<kOctNT>(cpre, G.ncells, s_tmp);
   const uint32_t* cb = cand + (int64_t)img * cand_total;
   uint32_t* keys = lin + (int64_t)img * cand_total + G.cand_off;
   int* lab = label + (int64_t)img * cand_total + G.cand_off;
-  {
+  if (n <= key_cap) {
+    for (int c = tid; c < G.ncells; c += kOctNT) {
+      const int e = c + 1 < G.ncells ? cpre[c + 1] : n;
+      for (int k = cpre[c]; k < e; k++) own[k] = (uint16_t)c;
+    }
+  } else {
     const int wid = tid >> 6, lane = tid & 63;
     for (int c = wid; c < G.ncells; c += kOctNT / 64) {
-      const CellGeom C = cells[G.cell_begin + c];
-      const int k = cntv[c], o = cpre[c];
-      for (int i = lane; i < k; i += 64) keys[o + i] = cb[C.slot_off + i];
+      const int e = c + 1 < G.ncells ? cpre[c + 1] : n, o = cpre[c];
+      for (int i = lane; i < e - o; i += 64) keys[o + i] = cb[s_slot[c] + i];
     }
   }
   __syncthreads();
@@ -1264,14 +1274,24 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
     return;
   }
   OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, pk, s_tmp64, outk, oc};
-  if (n <= kOctRegKeys * kOctNT) {  // keys + labels in registers: every pass stays on-chip
+  if (n <= key_cap) {  // keys + labels in registers: every pass stays on-chip
     RegKeys<kOctRegKeys> ks;
     ks.n = n;
 #pragma unroll
     for (int j = 0; j < kOctRegKeys; j++) {
       const int k = tid + kOctNT * j;
-      ks.key[j] = k < n ? keys[k] : 0u;
+      uint32_t v = 0u;
+      if (k < n) {
+        const int c = own[k];
+        v = cb[s_slot[c] + k - cpre[c]];
+      }
+      ks.key[j] = v;
       ks.lab[j] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kOctRegKeys; j++) {  // the final lookup of retained keys reads lin
+      const int k = tid + kOctNT * j;
+      if (k < n) keys[k] = ks.key[j];
     }
     octree_core(G, X, ks, keys);
   } else {
@@ -1606,12 +1626,13 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   const size_t NC = (size_t)g.node_cap_max;
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  P->oct_smem = 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
-                r16(4 * (P->cell_cap + 1)) + r16(8 * NC);
-  if (P->oct_smem > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
-  // keys and labels live in registers (up to kOctRegKeys * kOctNT per level) or in global
-  // scratch, never in LDS: the octree workgroup needs only its node arrays on chip
   P->key_cap = kOctRegKeys * kOctNT;
+  P->oct_smem = 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
+                r16(4 * (P->cell_cap + 1)) + r16(8 * NC) + r16(4 * P->cell_cap) +
+                r16(2 * P->key_cap);
+  if (P->oct_smem > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
+  // keys and labels live in registers (up to kOctRegKeys * kOctNT per level, with a 16-bit
+  // owner cell per key in LDS for the gather) or in global scratch
   if (hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)P->oct_smem) != hipSuccess)
     return fail(ORBX_EDEVICE);
