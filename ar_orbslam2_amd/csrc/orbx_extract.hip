@@ -333,106 +333,105 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
 // (SURVEY A.4): integer row pass with taps [18,34,49,55,49,34,18], column pass rounded
 // half-even (SSE2 f32 region x < 4*floor(w/4)) or half-up (scalar tail).  Values below 256
 // are exact in f32, so half-even rounding of m/65536 is done on the integer m.
-// Tile 64 x 32 outputs: interior tiles stage the (32+6) x 72 input window with aligned dword
-// loads, border tiles byte-wise through reflect101; every thread then produces 4 adjacent
-// row sums (ds_write_b128) and 4 adjacent outputs (7 x ds_read_b128, one dword store).
-constexpr int kBlurTW = 64, kBlurTH = 32;
+// Tile 64 x 64 outputs: interior tiles stage the (64+6) x 72 input window with aligned dword
+// loads, border tiles byte-wise through reflect101.  Row pass in packed u16 (a row sum is at
+// most 255 * 257 = 65535): a thread makes 4 adjacent sums from the byte pairs of three dwords
+// (v_perm) with v_pk_add_u16 / v_pk_mad_u16, stored as 4 u16; column pass in 32 bits, 4
+// adjacent outputs per thread (7 x ds_read_b64, one dword store).
+constexpr int kBlurTW = 64, kBlurTH = 64;
 struct BlurTile {
   int16_t level, tx, ty, interior;
 };
+
+typedef unsigned short blur_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ blur_u16x2 byte_pair(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_bit_cast(blur_u16x2, __builtin_amdgcn_perm(hi, lo, sel));
+}
 
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                               uint8_t* __restrict__ blur,
                                               const LevelGeom* __restrict__ lv,
                                               const BlurTile* __restrict__ tiles) {
-  __shared__ __align__(16) uint32_t s_in[kBlurTH + 6][(kBlurTW + 8) / 4];
-  __shared__ __align__(16) int s_row[kBlurTH + 6][kBlurTW];
+  constexpr int kWords = (kBlurTW + 8) / 4;  // window columns X0-4 .. X0+67
+  constexpr int kRows = kBlurTH + 6;         // window rows Y0-3 .. Y0+66
+  __shared__ __align__(16) uint32_t s_in[kRows][kWords];
+  __shared__ __align__(16) uint16_t s_row[kRows][kBlurTW];
   int bx, img;
   xcd_block(bx, img);
   const BlurTile T = tiles[bx];
   const LevelGeom& G = lv[T.level];
-  const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
-  uint8_t* dst = blur + (int64_t)img * pyr_bytes + G.pyr_off;
+  int pitch = G.pitch, w = G.w, h = G.h, bxs = G.bxs, pyr_off = (int)G.pyr_off;
+  asm volatile("" : "+s"(pitch), "+s"(w), "+s"(h), "+s"(bxs), "+s"(pyr_off));
+  const uint8_t* src = pyr + (int64_t)img * pyr_bytes + pyr_off;
+  uint8_t* dst = blur + (int64_t)img * pyr_bytes + pyr_off;
   const int X0 = T.tx * kBlurTW, Y0 = T.ty * kBlurTH;
   const int tid = threadIdx.x;
-  constexpr int kWords = (kBlurTW + 8) / 4;  // window columns X0-4 .. X0+67
   if (T.interior) {
-    for (int i = tid; i < (kBlurTH + 6) * kWords; i += 256) {
+    for (int i = tid; i < kRows * kWords; i += 256) {
       const int r = i / kWords, c = i - r * kWords;
-      s_in[r][c] = *(const uint32_t*)(src + (int64_t)(Y0 + r - 3) * G.pitch + X0 - 4 + 4 * c);
+      s_in[r][c] = *(const uint32_t*)(src + (int64_t)(Y0 + r - 3) * pitch + X0 - 4 + 4 * c);
     }
   } else {
     // border tile: each window row reflected once (reflect-101), whole dwords where the 4
     // bytes are inside the level, byte-wise reflect only for dwords crossing the left/right
     // edge; dwords wholly past the last column any output reads (w + 2) stay unset
-    for (int i = tid; i < (kBlurTH + 6) * kWords; i += 256) {
+    for (int i = tid; i < kRows * kWords; i += 256) {
       const int r = i / kWords, c = i - r * kWords;
-      const int y = reflect101(min(Y0 + r - 3, G.h + 8), G.h);
-      const uint8_t* row = src + (int64_t)y * G.pitch;
+      const int y = reflect101(min(Y0 + r - 3, h + 8), h);
+      const uint8_t* row = src + (int64_t)y * pitch;
       const int x = X0 - 4 + 4 * c;
       uint32_t v = 0;
-      if (x >= 0 && x + 4 <= G.w) {
+      if (x >= 0 && x + 4 <= w) {
         v = *(const uint32_t*)(row + x);
-      } else if (x < G.w + 3) {
+      } else if (x < w + 3) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) v |= (uint32_t)row[reflect101(min(x + k, G.w + 8), G.w)] << (8 * k);
+        for (int k = 0; k < 4; k++) v |= (uint32_t)row[reflect101(min(x + k, w + 8), w)] << (8 * k);
       }
       s_in[r][c] = v;
     }
   }
   __syncthreads();
-  const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;
-  for (int i = tid; i < (kBlurTH + 6) * (kBlurTW / 4); i += 256) {
-    const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
-    // bytes X0+4q-4 .. X0+4q+7 of row r
+  constexpr uint32_t k0 = 18, k1 = 34, k2 = 49, k3 = 55;
+  const blur_u16x2 K0 = {k0, k0}, K1 = {k1, k1}, K2 = {k2, k2}, K3 = {k3, k3};
+  for (int i = tid; i < kRows * (kBlurTW / 4); i += 256) {
+    const int r = i >> 4, q = i & 15;
+    // window bytes b_0 .. b_11 = X0+4q-4 .. X0+4q+7 of row r; U(i) = (b_i, b_i+1) as u16 pair
     const uint32_t w0 = s_in[r][q], w1 = s_in[r][q + 1], w2 = s_in[r][q + 2];
-    int b[12];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      b[k] = (w0 >> (8 * k)) & 0xFF;
-      b[4 + k] = (w1 >> (8 * k)) & 0xFF;
-      b[8 + k] = (w2 >> (8 * k)) & 0xFF;
-    }
-    int4 o;
-    // 24-bit multiplies (full rate): every operand < 2^24
-    auto tap7 = [&](int c) {
-      return (int)(__umul24(b[c - 3] + b[c + 3], k0) + __umul24(b[c - 2] + b[c + 2], k1) +
-                   __umul24(b[c - 1] + b[c + 1], k2) + __umul24(b[c], k3));
-    };
-    o.x = tap7(4);
-    o.y = tap7(5);
-    o.z = tap7(6);
-    o.w = tap7(7);
-    *(int4*)&s_row[r][4 * q] = o;
+    const blur_u16x2 U1 = byte_pair(w1, w0, 0x0c020c01u), U2 = byte_pair(w1, w0, 0x0c030c02u),
+                     U3 = byte_pair(w1, w0, 0x0c040c03u), U4 = byte_pair(w1, w0, 0x0c050c04u),
+                     U5 = byte_pair(w2, w1, 0x0c020c01u), U6 = byte_pair(w2, w1, 0x0c030c02u),
+                     U7 = byte_pair(w2, w1, 0x0c040c03u), U8 = byte_pair(w2, w1, 0x0c050c04u),
+                     U9 = byte_pair(w2, w1, 0x0c060c05u);
+    // outputs at window bytes 4,5 and 6,7 (taps [18,34,49,55,49,34,18])
+    const blur_u16x2 s01 = (U1 + U7) * K0 + (U2 + U6) * K1 + (U3 + U5) * K2 + U4 * K3;
+    const blur_u16x2 s23 = (U3 + U9) * K0 + (U4 + U8) * K1 + (U5 + U7) * K2 + U6 * K3;
+    *(uint2*)&s_row[r][4 * q] =
+        make_uint2(__builtin_bit_cast(uint32_t, s01), __builtin_bit_cast(uint32_t, s23));
   }
   __syncthreads();
   for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
-    const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
+    const int r = i >> 4, q = i & 15;
     const int x = X0 + 4 * q, y = Y0 + r;
-    if (x >= G.w || y >= G.h) continue;
-    int4 R[7];
+    if (x >= w || y >= h) continue;
+    uint2 R[7];
 #pragma unroll
-    for (int k = 0; k < 7; k++) R[k] = *(const int4*)&s_row[r + k][4 * q];
-    int m[4];
-    // row sums <= 255 * 257 = 65535: pair sums < 2^24, 24-bit multiplies are exact
-    auto col7 = [&](int a0, int a1, int a2, int a3, int a4, int a5, int a6) {
-      return (int)(__umul24(a0 + a6, k0) + __umul24(a1 + a5, k1) + __umul24(a2 + a4, k2) +
-                   __umul24(a3, k3));
+    for (int k = 0; k < 7; k++) R[k] = *(const uint2*)&s_row[r + k][4 * q];
+    // row sums <= 65535: pair sums < 2^24, 24-bit multiplies are exact
+    auto col7 = [&](int sh, bool hi) {
+      auto g = [&](int k) { return hi ? (R[k].y >> sh) & 0xFFFFu : (R[k].x >> sh) & 0xFFFFu; };
+      return (uint32_t)(__umul24(g(0) + g(6), k0) + __umul24(g(1) + g(5), k1) +
+                        __umul24(g(2) + g(4), k2) + __umul24(g(3), k3));
     };
-    m[0] = col7(R[0].x, R[1].x, R[2].x, R[3].x, R[4].x, R[5].x, R[6].x);
-    m[1] = col7(R[0].y, R[1].y, R[2].y, R[3].y, R[4].y, R[5].y, R[6].y);
-    m[2] = col7(R[0].z, R[1].z, R[2].z, R[3].z, R[4].z, R[5].z, R[6].z);
-    m[3] = col7(R[0].w, R[1].w, R[2].w, R[3].w, R[4].w, R[5].w, R[6].w);
+    const uint32_t m[4] = {col7(0, false), col7(16, false), col7(0, true), col7(16, true)};
+    // m / 65536 rounded half-even in the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up in
+    // the scalar tail (m + 0x8000); x is a multiple of 4, as is bxs: one test per group
+    const uint32_t even = x < bxs ? 1u : 0u;
     uint32_t out = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      // m / 65536 rounded half-even in the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up
-      // in the scalar tail; m >= 0
-      const uint32_t mk = (uint32_t)m[k];
-      const uint32_t add = x + k < G.bxs ? 0x7FFFu + ((mk >> 16) & 1u) : 0x8000u;
-      out |= min(255u, (mk + add) >> 16) << (8 * k);
-    }
-    *(uint32_t*)(dst + (uint32_t)(y * G.pitch + x)) = out;  // bytes past w land in the row pad
+    for (int k = 0; k < 4; k++)
+      out |= min(255u, (m[k] + 0x8000u - (~(m[k] >> 16) & even)) >> 16) << (8 * k);
+    *(uint32_t*)(dst + (uint32_t)(y * pitch + x)) = out;  // bytes past w land in the row pad
   }
 }
 

@@ -41,14 +41,22 @@ __device__ __forceinline__ int hamming_regs(const uint64_t d[4], const uint8_t* 
          __popcll(d[3] ^ pb[3]);
 }
 
-__device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t v) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1;
-    else hi = mid;
+// std::lower_bound over a sorted array by the whole wave (wave-uniform arguments): each round
+// probes up to 64 evenly spaced positions at once, so a node lookup costs 2-3 dependent loads
+// instead of log2(n)
+__device__ __forceinline__ int wave_lower_bound(const uint32_t* a, int n, uint32_t v, int lane) {
+  int lo = 0, len = n;
+  while (len > 64) {
+    const int step = (len + 63) >> 6;
+    const int K = (len + step - 1) / step;  // probes lo, lo + step, ... (K <= 64)
+    const int c = __popcll(__ballot(lane < K && a[lo + lane * step] < v));
+    if (c == 0) return lo;
+    const int pc1 = lo + (c - 1) * step;  // a[pc1] < v
+    const int hi = c < K ? lo + c * step : lo + len;  // a[hi] >= v, or the end
+    lo = pc1 + 1;
+    len = hi - lo;
   }
-  return lo;
+  return lo + __popcll(__ballot(lane < len && a[lo + lane] < v));
 }
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {
@@ -68,7 +76,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
   if (a >= side_nodes(P.s1)) return;
   const uint32_t id = P.s1.node_ids[a];
   const int nn2 = side_nodes(P.s2);
-  const int b = lower_bound_u32(P.s2.node_ids, nn2, id);
+  const int b = wave_lower_bound(P.s2.node_ids, nn2, id, lane);
   if (b >= nn2 || P.s2.node_ids[b] != id) return;
   const int f0 = P.s2.node_offsets[b], m = P.s2.node_offsets[b + 1] - f0;
   if (m > 64 * 16) {  // more candidates than the per-lane matched bitmap holds
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
   if (a >= tri_nodes(P.s1)) return;
   const uint32_t id = P.s1.fv.node_ids[a];
   const int nn2 = tri_nodes(P.s2);
-  const int b = lower_bound_u32(P.s2.fv.node_ids, nn2, id);
+  const int b = wave_lower_bound(P.s2.fv.node_ids, nn2, id, lane);
   if (b >= nn2 || P.s2.fv.node_ids[b] != id) return;
   const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
   // KF2 node features are staged 64 at a time in this wave's LDS (descriptor, keypoint,
