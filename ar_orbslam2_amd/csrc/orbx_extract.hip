@@ -1489,7 +1489,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   Profiler& pr = prof ? *prof : dummy;
   const int st_pyr = pr.stage("k_pyramid"),
             st_blur = pr.stage("k_blur"), st_fs = pr.stage("k_fast_tile"),
-            st_fast = pr.stage("k_fast_compact"),
+            st_fast = pr.stage("k_fast_compact"), st_fb = pr.stage("k_fast_fallback"),
             st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe");
   pr.mark(P->stream, -1);
   for (const PyrStage& st : g.pyr_stages)
@@ -1512,6 +1512,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
     hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
                        P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
                        P->d_fb_list);
+    pr.mark(P->stream, st_fast);
     hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
                        P->d_pyr, g.pyr_bytes, P->d_lv, P->d_cells, ncells, P->d_fb_count,
                        P->d_fb_list, g.min_th, P->d_cand, g.cand_total, P->d_cell_counts);
@@ -1519,7 +1520,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                        P->stream, P->d_pyr, g.pyr_bytes, P->d_lv, P->d_cells, ncells,
                        P->d_fb_count, P->d_fb_list, g.min_th, P->d_cand, g.cand_total,
                        P->d_cell_counts);
-    pr.mark(P->stream, st_fast);
+    pr.mark(P->stream, st_fb);
   }
   hipLaunchKernelGGL(k_octree, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream, P->d_lv,
                      P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total, P->d_lin,

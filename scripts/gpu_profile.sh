@@ -12,7 +12,7 @@ timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/gpu_tests.txt 2>&1
 tail -2 $O/gpu_tests.txt
 timeout -k 10 300 python bench.py > $O/bench.jsonl 2> $O/bench.err
 cat $O/bench.jsonl
-BENCH="bench.py --steps 10 --warmup 2 --no-cpu-baseline ${2:-}"
+BENCH="bench.py ${2:-}"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/$BENCH > $O/bench_under_rocprof.jsonl 2> $O/rocprof_trace.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/$BENCH > /dev/null 2> $O/pmc_fetch.err

@@ -1,0 +1,28 @@
+"""Cross-check bench.py's roofline kernel duration (HIP events, single-stream roofline pass)
+against the rocprofv3 kernel trace of the same command.
+
+The timed region runs several camera streams concurrently, so the trace's overall average for
+a kernel includes launches that share the GPU with other streams' kernels; bench.py times the
+roofline kernel in a separate pass on stream 0 alone (its last `--roofline-steps` launches).
+This prints both the overall trace average and the average over those last launches.
+
+Usage: python3 scripts/roofline_check.py <trace dir> <bench json line file> [roofline_steps]"""
+import csv
+import json
+import sys
+
+trace_dir, bench_file = sys.argv[1], sys.argv[2]
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+b = json.loads(open(bench_file).read().strip().splitlines()[-1])
+kern = b["roofline"]["kernel"]
+rows = [r for r in csv.DictReader(open(f"{trace_dir}/run_kernel_trace.csv"))
+        if r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + kern)]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+solo = dur[-steps:]
+print(f"kernel {kern}: {len(dur)} dispatches")
+print(f"  trace average, all dispatches (timed region with concurrent streams + roofline pass): "
+      f"{sum(dur) / len(dur):.2f} us")
+print(f"  trace average, last {steps} dispatches (roofline pass, stream 0 alone): "
+      f"{sum(solo) / len(solo):.2f} us")
+print(f"  bench.py roofline avg_launch_us (HIP events, same pass): {b['roofline']['avg_launch_us']} us")
