@@ -1482,6 +1482,22 @@ int dalloc(T** p, size_t count) {
   return ORBX_OK;
 }
 
+__global__ void k_fill_u32(uint32_t* __restrict__ p, size_t n, uint32_t v) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    p[i] = v;
+}
+
+}  // namespace
+
+int orbx::launch_fill_u32(uint32_t* p, size_t n, uint32_t v, hipStream_t s) {
+  if (n == 0) return ORBX_OK;
+  const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks), dim3(256), 0, s, p, n, v);
+  return ORBX_OK;
+}
+
+namespace {
+
 int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   const Geometry& g = P->g;
   const int L = g.nlevels;
@@ -1508,7 +1524,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                        g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
                        g.ini_th);
     pr.mark(P->stream, st_fs);
-    hipMemsetAsync(P->d_fb_count, 0, sizeof(int) * 2 * n, P->stream);
+    launch_fill_u32((uint32_t*)P->d_fb_count, 2 * (size_t)n, 0u, P->stream);
     hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
                        P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
                        P->d_fb_list);

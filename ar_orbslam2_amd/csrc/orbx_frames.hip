@@ -219,11 +219,11 @@ int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
                   F->d_off, F->d_feats, kp, F->d_nn, n, s);
   if (rc) return rc;
   pr.mark(s, st_csr);
-  ORBX_HIP(hipMemsetAsync(F->d_match, 0xFF, (size_t)n * kp * 4, s));
+  launch_fill_u32((uint32_t*)F->d_match, (size_t)n * kp, 0xFFFFFFFFu, s);
   rc = launch_bow(F->d_bprob, n, F->nb, s);
   if (rc) return rc;
   pr.mark(s, st_bow);
-  ORBX_HIP(hipMemsetAsync(F->d_m12, 0xFF, (size_t)n * kp * 4, s));
+  launch_fill_u32((uint32_t*)F->d_m12, (size_t)n * kp, 0xFFFFFFFFu, s);
   rc = launch_tri(F->d_tprob, n, F->nb, s);
   if (rc) return rc;
   pr.mark(s, st_tri);
@@ -255,6 +255,7 @@ static int frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max
     return rc;
   };
   F->device = hip_device;
+  F->prof.on = getenv("ORBX_SYNC_STAGES") != nullptr;  // debugging: eager, stage-synchronous
   F->stereo = stereo;
   F->max_frames = max_batch;
   F->mb = mb;

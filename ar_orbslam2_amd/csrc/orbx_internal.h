@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <string>
 #include <utility>
@@ -111,6 +113,12 @@ struct Geometry {
   int umax[kHalfPatch + 1];
 };
 
+// Fills n 32-bit words with v on stream s.  Used instead of hipMemsetAsync inside captured
+// hipGraphs: a captured memset node of more than 512 KiB left part of its range unwritten on
+// the MI355X box (C5 batches of 32 frames: d_match kept stale indices, SearchByBoW's finish
+// kernel then read angles out of bounds).
+int launch_fill_u32(uint32_t* p, size_t n, uint32_t v, hipStream_t s);
+
 // Builds every table of a plan; returns ORBX_OK / ORBX_EUNSUPPORTED / ORBX_EINVAL.
 int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string* why);
 // Tables only (no image size): scale factors, sigma2, features per level, umax.
@@ -144,6 +152,13 @@ struct Profiler {
     hipEvent_t e = pool[used++];
     hipEventRecord(e, s);
     marks.push_back({st, e});
+    static const bool sync_stages = getenv("ORBX_SYNC_STAGES") != nullptr;
+    if (sync_stages) {  // debugging aid: locate the stage of an asynchronous device fault
+      const hipError_t err = hipStreamSynchronize(s);
+      if (err != hipSuccess)
+        fprintf(stderr, "[orbx] stage %s: %s\n", st >= 0 ? names[st].c_str() : "(start)",
+                hipGetErrorString(err));
+    }
   }
   int collect() {
     if (marks.empty()) return 0;

@@ -18,6 +18,7 @@ CONFIGS = {
     "C1": (640, 480, 1000),
     "C3": (752, 480, 1200),
     "C4": (1241, 376, 2000),
+    "C5": (1920, 1080, 4000),
 }
 
 

@@ -43,7 +43,8 @@ def _vocabs():
     return _VOCS[0]
 
 
-@pytest.mark.parametrize("w,h,nf,n", [(640, 480, 1000, 4), (752, 480, 1200, 3)])
+@pytest.mark.parametrize("w,h,nf,n", [(640, 480, 1000, 4), (752, 480, 1200, 3),
+                                      (1920, 1080, 4000, 2)])
 def test_pipeline_matches_oracle(w, h, nf, n):
     voc, oracle_voc = _vocabs()
     pipe = FramePipeline(w, h, n, voc, nf)
@@ -153,6 +154,53 @@ def test_stereo_pipeline_matches_oracle(w, h, nf, cam, n):
         nb, mbm = O.search_by_bow_kf_f(kf, dict(cur, valid=None), 0.7, True)
         assert bow[f] == nb
         assert np.array_equal(match_all[f, :len(cur["desc"])], mbm)
+        nt, pt = O.search_for_triangulation(kf, cur, F, ex, ey, False, 0.6, False)
+        assert tri[f] == nt
+        assert np.array_equal(pairs_all[f, :nt], pt)
+    pipe.close()
+
+
+def test_large_batch_graph_replay_c5():
+    """C5 geometry (1920x1080, 4000 features) at a batch whose per-batch match arrays exceed
+    512 KiB, replayed from the captured hipGraph: the match arrays are pre-filled with -1 inside
+    the graph (a captured memset node of that size once left stale indices behind and the
+    rotation filter then read out of bounds).  Frames 0, 1 and n-1 are checked against the
+    oracle (frame 0 is matched against frame n-1)."""
+    w, h, nf, n = 1920, 1080, 4000, 36
+    voc, oracle_voc = _vocabs()
+    pipe = FramePipeline(w, h, n, voc, nf)
+    valid, has_mp = pipe.seeded_masks(range(n))
+    F = fundamental_from_pose()
+    ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
+    pipe.set_matching(F, (ex, ey), bow_ratio=0.7, bow_check_ori=True, tri_ratio=0.6,
+                      tri_check_ori=False)
+    base = synth.canvas(w, h, stream=0)
+    frames = np.stack([synth.frame(w, h, t, 0, base) for t in range(n)])
+    d = torch.from_numpy(frames).cuda()
+    for _ in range(3):  # capture, then replays
+        pipe.run(d.data_ptr(), n)
+    pipe.sync()
+    counts, bow, tri, err = pipe.results(n)
+    assert err == 0
+    cap = pipe.kp_cap
+    assert n * cap * 4 > 512 * 1024
+    out = pipe.device_outputs()
+    match_all = d2h(out["bow_match"], n * cap * 4).view(np.int32).reshape(n, cap)
+    pairs_all = d2h(out["tri_pairs"], n * cap * 8).view(np.int32).reshape(n, cap, 2)
+    t = O.tables(O.params(nf), w, h)
+    ref = {}
+    for f in (n - 1, 0, 1):
+        kps, desc = O.extract(frames[f], O.params(nf))
+        assert counts[f] == len(kps)
+        r = oracle_voc.transform(desc, 4)
+        ref[f] = dict(desc=desc, angle=kps["angle"], keys=kps, fv=featvec(r["node_of"]),
+                      valid=valid[f, :len(kps)], has_mp=has_mp[f, :len(kps)],
+                      scale_factors=t["scale"], level_sigma2=t["sigma2"])
+    for f in (0, 1):
+        kf, cur = ref[(f - 1) % n], ref[f]
+        nb, mb = O.search_by_bow_kf_f(kf, dict(cur, valid=None), 0.7, True)
+        assert bow[f] == nb
+        assert np.array_equal(match_all[f, :len(cur["desc"])], mb)
         nt, pt = O.search_for_triangulation(kf, cur, F, ex, ey, False, 0.6, False)
         assert tri[f] == nt
         assert np.array_equal(pairs_all[f, :nt], pt)
