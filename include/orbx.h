@@ -19,6 +19,16 @@
  *                           ORB_SLAM2/Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1127-1259,
  *                           1338-1424 (called by Frame::ComputeBoW, ORB_SLAM2/src/Frame.cc:400-407)
  *
+ *   orbx_cvorb_*            cv::ORB (OpenCV 2.4, scoreType HARRIS_SCORE/FAST_SCORE) ::operator()
+ *                           as called by the AR marker path: Marker::setTargetImage / Marker::Match
+ *                           ORB_SLAM2/src/Marker.cc:76-84, 98-108; AR-1.3/src/ORBMatcher.cpp:121-122
+ *   orbx_bf_match           BruteForceMatcher<HammingLUT>::match   ORB_SLAM2/src/Marker.cc:110-113
+ *   orbx_good_matches       Marker::Match good-match filter        ORB_SLAM2/src/Marker.cc:115-133
+ *   orbx_nn_match           naive_nn_search / naive_nn_search2     AR-1.3/src/ORBMatcher.cpp:44-102,
+ *                           Marker::searchMatches                  ORB_SLAM2/src/Marker.cc:314-349
+ *   orbx_marker_*           Marker::Match's extract + match + filter for a batch of frames against
+ *                           one target (the homography/RANSAC part stays with the caller)
+ *
  * Error convention: every function returns 0 on success or a negative ORBX_E* code; nothing
  * throws across the ABI.  The reference has no error returns (asserts are compiled out,
  * ORB_SLAM2/CMakeLists.txt:10-11); callers that must never fail map a negative code to
@@ -333,6 +343,91 @@ int orbx_search_for_triangulation(const orbx_tri_side* kf1, const orbx_tri_side*
 /* Epipole exactly as ORBmatcher.cc:667-673 evaluates it (C2 = R2w*Cw + t2w, f32). */
 int orbx_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx, float fy,
                  float cx, float cy, float* ex, float* ey);
+
+/* ------------------------------------------------------------------ AR marker path (cv::ORB) */
+/* cv::ORB constructor arguments (OpenCV 2.4 features2d.hpp): ORB(int nfeatures = 500,
+ * float scaleFactor = 1.2f, int nlevels = 8, int edgeThreshold = 31, int firstLevel = 0,
+ * int WTA_K = 2, int scoreType = ORB::HARRIS_SCORE, int patchSize = 31).  Marker uses the
+ * defaults (Marker.cc:83, 107); AR-1.3's ORBMatcher uses (300, 1.2f, 8, 31, 0, 2, HARRIS, 31)
+ * (AR-1.3/src/ORBMatcher.cpp:121-122).  Implemented: firstLevel 0, WTA_K 2, patchSize 31,
+ * edgeThreshold >= 16; anything else returns ORBX_EUNSUPPORTED. */
+#define ORBX_HARRIS_SCORE 0
+#define ORBX_FAST_SCORE 1
+typedef struct {
+  int32_t nfeatures;
+  float scale_factor;
+  int32_t nlevels;
+  int32_t edge_threshold;
+  int32_t first_level;
+  int32_t wta_k;
+  int32_t score_type;
+  int32_t patch_size;
+} orbx_cvorb_params;
+
+/* == cv::DMatch (OpenCV 2.4): {queryIdx, trainIdx, imgIdx, distance}, 16 B. */
+typedef struct {
+  int32_t query_idx, train_idx, img_idx;
+  float distance;
+} orbx_dmatch;
+
+/* One cv::ORB instance with a batch plan for one image size.  orbx_cvorb_detect is the
+ * drop-in for `orb(image, Mat(), keypoints, descriptors)` on a host image (the plan is rebuilt
+ * when the size changes); keypoints are level-major in the reference's order (the order
+ * KeyPointsFilter::retainBest leaves them in, libstdc++ nth_element/partition), descriptors
+ * n x 32.  An empty image returns *n_out = -1 with the outputs untouched (orb.cpp returns
+ * early); n == 0 means no keypoints (descriptors released). */
+typedef struct orbx_cvorb orbx_cvorb;
+int orbx_cvorb_create(const orbx_cvorb_params* params, int32_t w, int32_t h, int32_t max_batch,
+                      int hip_device, orbx_cvorb** out);
+int orbx_cvorb_destroy(orbx_cvorb* orb);
+int orbx_cvorb_capacity(const orbx_cvorb* orb, int32_t* kp_cap);
+int orbx_cvorb_detect(orbx_cvorb* orb, const uint8_t* img, int32_t w, int32_t h, int64_t stride,
+                      orbx_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out);
+/* Throughput path: n dense h*w u8 images already in device memory, asynchronous on the
+ * instance's stream.  Outputs [max_batch][kp_cap] keypoints / descriptors, counts [max_batch]
+ * (a negative count = that image overflowed the per-level keypoint capacity). */
+int orbx_cvorb_run(orbx_cvorb* orb, const uint8_t* d_imgs, int32_t n);
+int orbx_cvorb_outputs(orbx_cvorb* orb, orbx_keypoint** d_kps, uint8_t** d_desc,
+                       int32_t** d_counts);
+int orbx_cvorb_sync(orbx_cvorb* orb);
+void* orbx_cvorb_stream(orbx_cvorb* orb);
+
+/* BruteForceMatcher<HammingLUT>::match(query, train, matches): for every query row the first
+ * train row of minimum Hamming distance (BFMatcher NORM_HAMMING, k = 1).  out[nq]; *n_out = nq,
+ * or 0 when either side is empty (DescriptorMatcher::knnMatch returns early). */
+int orbx_bf_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_t nt,
+                  orbx_dmatch* out, int32_t* n_out);
+/* Marker::Match's filter: max_dist over the matches (initial 0), keep distance < 0.5*max_dist
+ * (double), in order.  Host-side, no device work (n <= a few thousand). */
+int orbx_good_matches(const orbx_dmatch* matches, int32_t n, orbx_dmatch* good, int32_t* n_good,
+                      double* min_dist, double* max_dist);
+/* naive_nn_search2 / Marker::searchMatches: for every query row (keys2) the nearest and second
+ * nearest train row (keys1), strict `<` updates; accept when min <= (unsigned)(second * ratio)
+ * and min <= max_dist.  ratio <= 0 selects naive_nn_search (no ratio test).  *min_d / *max_d
+ * return the extremes over all evaluated pairs (the reference's global minD/maxD; the caller
+ * merges them into its running values). */
+int orbx_nn_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_t nt,
+                  double ratio, int32_t max_dist, orbx_dmatch* out, int32_t* n_out,
+                  int32_t* min_d, int32_t* max_d);
+
+/* Marker::Match for a batch of frames against one target: cv::ORB extraction of every frame,
+ * BruteForceMatcher match (query = target descriptors, train = frame descriptors) and the
+ * good-match filter, all on the device stream.  Per frame: matches [max_batch][n_target]
+ * (train_idx = -1 if the frame has no keypoints), good flags [max_batch][n_target], counts. */
+typedef struct orbx_marker orbx_marker;
+int orbx_marker_create(const orbx_cvorb_params* params, int32_t w, int32_t h, int32_t max_batch,
+                       int hip_device, orbx_marker** out);
+int orbx_marker_destroy(orbx_marker* mk);
+int orbx_marker_set_target(orbx_marker* mk, const uint8_t* desc, int32_t n);
+int orbx_marker_run(orbx_marker* mk, const uint8_t* d_imgs, int32_t n);
+int orbx_marker_sync(orbx_marker* mk);
+int orbx_marker_results(orbx_marker* mk, int32_t n, int32_t* kp_counts, int32_t* good_counts);
+int orbx_marker_outputs(orbx_marker* mk, orbx_dmatch** d_matches, uint8_t** d_good,
+                        orbx_keypoint** d_kps, uint8_t** d_desc);
+void* orbx_marker_stream(orbx_marker* mk);
+int orbx_marker_profile(orbx_marker* mk, int32_t enable);
+int orbx_marker_profile_read(orbx_marker* mk, int32_t cap, char (*names)[32], double* total_ms,
+                             int64_t* launches, int32_t* n_stages);
 
 #ifdef __cplusplus
 }

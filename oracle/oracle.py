@@ -448,3 +448,118 @@ def search_by_projection_last(f, last, th, forward, backward, check_ori):
                                                C.c_int(int(forward)), C.c_int(int(backward)),
                                                C.c_int(int(check_ori)), _p(match))
     return n, match[:s.n].copy()
+
+
+# ---------------------------------------------------------------- AR marker path (cvorb_oracle.cc)
+DMATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
+                         ("distance", "<f4")])
+HARRIS_SCORE, FAST_SCORE = 0, 1
+
+
+class CvOrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("edge_threshold", C.c_int32), ("first_level", C.c_int32), ("wta_k", C.c_int32),
+                ("score_type", C.c_int32), ("patch_size", C.c_int32)]
+
+
+def cvorb_params(nfeatures=500, scale_factor=1.2, nlevels=8, edge_threshold=31, first_level=0,
+                 wta_k=2, score_type=HARRIS_SCORE, patch_size=31):
+    """cv::ORB 2.4 constructor defaults (the ones Marker.cc:83, 107 uses)."""
+    return CvOrbParams(nfeatures, scale_factor, nlevels, edge_threshold, first_level, wta_k,
+                       score_type, patch_size)
+
+
+def cvorb_levels(p, w, h):
+    n = p.nlevels
+    lw, lh, fe = (np.zeros(n, np.int32) for _ in range(3))
+    sc = np.zeros(n, np.float32)
+    rc = lib().oracle_cvorb_levels(C.byref(p), C.c_int(w), C.c_int(h), _p(lw), _p(lh), _p(sc),
+                                   _p(fe))
+    assert rc == 0, rc
+    return dict(w=lw, h=lh, scale=sc, feats=fe)
+
+
+def cvorb_detect(img, p=None, want_pyramid=False):
+    """cv::ORB::operator()(img, noArray(), kps, desc) restated (OpenCV 2.4 orb.cpp)."""
+    p = p or cvorb_params()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = max(1, w * h // 4)
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int()
+    lv = cvorb_levels(p, w, h)
+    tot = int((lv["w"].astype(np.int64) * lv["h"]).sum())
+    pyr = np.zeros(tot, np.uint8) if want_pyramid else None
+    rc = lib().oracle_cvorb_detect(C.byref(p), _p(img), C.c_int(w), C.c_int(h), C.c_int64(w),
+                                   _p(kps), _p(desc), C.c_int(cap), C.byref(n), _p(pyr),
+                                   C.c_int64(tot))
+    assert rc == 0, rc
+    kps, desc = kps[:n.value].copy(), desc[:n.value].copy()
+    if not want_pyramid:
+        return kps, desc
+    levels, off = [], 0
+    for lw_, lh_ in zip(lv["w"], lv["h"]):
+        levels.append(pyr[off:off + lw_ * lh_].reshape(lh_, lw_))
+        off += lw_ * lh_
+    return kps, desc, levels
+
+
+def retain_best(resp, n_points):
+    """KeyPointsFilter::retainBest with GCC 4.8 nth_element/partition; returns the retained
+    (responses, original indices) in their final order."""
+    resp = np.ascontiguousarray(resp, np.float32).copy()
+    ids = np.arange(len(resp), dtype=np.int32)
+    n = C.c_int()
+    lib().oracle_retain_best(_p(resp), _p(ids), C.c_int(len(resp)), C.c_int(n_points), C.byref(n))
+    return resp[:n.value].copy(), ids[:n.value].copy()
+
+
+def harris(img, x, y):
+    img = np.ascontiguousarray(img, np.uint8)
+    f = lib().oracle_harris
+    f.restype = C.c_float
+    return f(_p(img), C.c_int64(img.shape[1]), C.c_int(x), C.c_int(y))
+
+
+def cvorb_descriptor(blurred, x, y, angle):
+    blurred = np.ascontiguousarray(blurred, np.uint8)
+    d = np.zeros(32, np.uint8)
+    lib().oracle_cvorb_descriptor(_p(blurred), C.c_int64(blurred.shape[1]), C.c_int(x),
+                                  C.c_int(y), C.c_float(angle), _p(d))
+    return d
+
+
+def cos_sin_f64(deg):
+    c, s = C.c_float(), C.c_float()
+    lib().oracle_cos_sin_f64(C.c_float(deg), C.byref(c), C.byref(s))
+    return c.value, s.value
+
+
+def bf_match(query, train):
+    q = np.ascontiguousarray(query, np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
+    out = np.zeros(max(1, len(q)), DMATCH_DTYPE)
+    n = C.c_int()
+    lib().oracle_bf_match(_p(q), C.c_int(len(q)), _p(t), C.c_int(len(t)), _p(out), C.byref(n))
+    return out[:n.value].copy()
+
+
+def good_matches(matches):
+    m = np.ascontiguousarray(matches, DMATCH_DTYPE)
+    good = np.zeros(max(1, len(m)), DMATCH_DTYPE)
+    n = C.c_int()
+    mn, mx = C.c_double(), C.c_double()
+    lib().oracle_good_matches(_p(m), C.c_int(len(m)), _p(good), C.byref(n), C.byref(mn),
+                              C.byref(mx))
+    return good[:n.value].copy(), mn.value, mx.value
+
+
+def nn_match(query, train, ratio=0.8, max_dist=50):
+    q = np.ascontiguousarray(query, np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
+    out = np.zeros(max(1, len(q)), DMATCH_DTYPE)
+    n, mn, mx = C.c_int(), C.c_int(), C.c_int()
+    lib().oracle_nn_match(_p(q), C.c_int(len(q)), _p(t), C.c_int(len(t)), C.c_double(ratio),
+                          C.c_int(max_dist), _p(out), C.byref(n), C.byref(mn), C.byref(mx))
+    return out[:n.value].copy(), mn.value, mx.value

@@ -96,6 +96,25 @@ int oracle_search_by_projection(const orbx_proj_frame* F, const orbx_proj_points
 int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_last* P, float th,
                                      int forward, int backward, int check_ori, int32_t* match);
 
+/* AR marker path (cvorb_oracle.cc): cv::ORB 2.4 + BruteForceMatcher<HammingLUT> + the
+ * Marker / AR-1.3 nearest-neighbour matchers */
+int oracle_cvorb_levels(const orbx_cvorb_params* p, int w, int h, int* lw, int* lh, float* scale,
+                        int* feats);
+void oracle_retain_best(float* resp, int32_t* ids, int n, int n_points, int* n_out);
+float oracle_harris(const uint8_t* img, int64_t stride, int x, int y);
+void oracle_cvorb_descriptor(const uint8_t* blurred, int64_t stride, int cx, int cy, float angle,
+                             uint8_t* desc32);
+void oracle_cos_sin_f64(float deg, float* c, float* s);
+int oracle_cvorb_detect(const orbx_cvorb_params* p, const uint8_t* img, int w, int h,
+                        int64_t stride, orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out,
+                        uint8_t* pyr, int64_t pyr_cap);
+int oracle_bf_match(const uint8_t* query, int nq, const uint8_t* train, int nt, orbx_dmatch* out,
+                    int* n_out);
+int oracle_good_matches(const orbx_dmatch* m, int n, orbx_dmatch* good, int* n_good,
+                        double* min_dist, double* max_dist);
+int oracle_nn_match(const uint8_t* query, int nq, const uint8_t* train, int nt, double ratio,
+                    int max_dist, orbx_dmatch* out, int* n_out, int* min_d, int* max_d);
+
 #ifdef __cplusplus
 }
 #endif
