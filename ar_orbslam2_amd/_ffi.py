@@ -34,7 +34,17 @@ EXPORTS = [
     "orbx_frames_capacity", "orbx_frames_set_masks", "orbx_frames_set_matching",
     "orbx_frames_run", "orbx_frames_sync", "orbx_frames_results", "orbx_frames_outputs",
     "orbx_frames_bow", "orbx_frames_stereo", "orbx_frames_stream", "orbx_frames_profile", "orbx_frames_profile_read",
+    "orbx_cvorb_create", "orbx_cvorb_destroy", "orbx_cvorb_capacity", "orbx_cvorb_detect",
+    "orbx_cvorb_run", "orbx_cvorb_outputs", "orbx_cvorb_sync", "orbx_cvorb_stream",
+    "orbx_bf_match", "orbx_good_matches", "orbx_nn_match", "orbx_marker_create",
+    "orbx_marker_destroy", "orbx_marker_set_target", "orbx_marker_run", "orbx_marker_sync",
+    "orbx_marker_results", "orbx_marker_outputs", "orbx_marker_stream", "orbx_marker_profile",
+    "orbx_marker_profile_read", "orbx_debug_cvorb_cossin", "orbx_debug_retain_best",
 ]
+
+# == cv::DMatch (OpenCV 2.4): queryIdx, trainIdx, imgIdx, distance
+DMATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
+                         ("distance", "<f4")])
 
 
 class OrbxError(RuntimeError):
@@ -46,6 +56,13 @@ class OrbxError(RuntimeError):
 class Params(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class CvorbParams(C.Structure):
+    """cv::ORB constructor arguments (OpenCV 2.4 features2d.hpp), include/orbx.h."""
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("edge_threshold", C.c_int32), ("first_level", C.c_int32), ("wta_k", C.c_int32),
+                ("score_type", C.c_int32), ("patch_size", C.c_int32)]
 
 
 class FeatVec(C.Structure):
@@ -99,6 +116,8 @@ def lib():
         _lib = C.CDLL(LIB_PATH)
         _lib.orbx_plan_stream.restype = C.c_void_p
         _lib.orbx_frames_stream.restype = C.c_void_p
+        _lib.orbx_cvorb_stream.restype = C.c_void_p
+        _lib.orbx_marker_stream.restype = C.c_void_p
     return _lib
 
 

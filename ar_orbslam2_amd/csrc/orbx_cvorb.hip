@@ -1,0 +1,1432 @@
+// orbx_cvorb.hip — the AR marker path on gfx950: cv::ORB::operator() of OpenCV 2.4 (orb.cpp)
+// with HARRIS_SCORE or FAST_SCORE, as ORB_SLAM2/src/Marker.cc:76-84, 98-108 and
+// AR-1.3/src/ORBMatcher.cpp:121-122 call it, plus the brute-force Hamming matchers of the same
+// path (Marker.cc:110-133, AR-1.3/src/ORBMatcher.cpp:44-102).
+//
+// One plan = one image size + one cv::ORB parameter set + a maximum batch.  A batch runs as a
+// fixed launch sequence on the plan's stream (captured once into a hipGraph):
+//   k_pyramid      levels (cv::resize INTER_LINEAR from the previous level; shared with the
+//                  ORBextractor plan, orbx_extract.hip)
+//   k_cvfast       64x16 tiles of every level's border region [edge, w-edge) x [edge, h-edge):
+//                  FAST-9/16 cornerScore at threshold 20 + whole-image 8-neighbour NMS
+//                  (cv::FAST(..., nonmax=true) followed by runByImageBorder) -> keep bitmaps
+//   k_cvselect     one wave per (image, level): raster-order compaction of the keep bitmaps,
+//                  KeyPointsFilter::retainBest(2N), HarrisResponses(7, 0.04), retainBest(N)
+//                  with the exact element order GCC 4.8's nth_element / partition leave
+//   k_blur         GaussianBlur 7x7 sigma 2 of every level (shared with the ORBextractor plan)
+//   k_cvdescribe   one half-wave per keypoint: IC_Angle, fastAtan2, rBRIEF (WTA_K 2) on the
+//                  blurred level with double cos/sin, level-0 scaling, level-major output
+// and for the marker: k_bfmatch (BruteForceMatcher<HammingLUT>::match, query = target) and
+// k_good (Marker::Match's distance < 0.5 * max_dist filter).
+//
+// retainBest on the GPU.  KeyPointsFilter::retainBest is std::nth_element(begin, begin + N,
+// end, response-greater) + std::partition(begin + N, end, response >= ambiguous), so which of
+// the keypoints tied at the boundary survive, and the order of the survivors (the order of
+// the output keypoints and descriptors), are those algorithms' outputs.  Both run here as the
+// same sequence of partitioning steps, each done in parallel: a Hoare-style partition (two
+// scans that stop at "left stoppers" and "right stoppers" and swap) swaps the k-th left stopper
+// with the k-th right stopper from the right exactly while the first is left of the second, so
+// with both stoppers' ranks from ballots and prefix counts every swap pair is known at once.
+// The cut the sequential loop returns is min(first unswapped left stopper, last swapped
+// right stopper).  The median-of-three pivot, the depth-limited heap_select fallback and the
+// final insertion sort of <= 3 elements run on lane 0.  DESIGN.md §10 gives the derivation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/orbx_pattern.h"
+#include "orbx_internal.h"
+#include "orbx_match.h"
+#include "orbx_math.h"
+
+#pragma clang fp contract(off)
+
+namespace orbx {
+namespace cvorb {
+
+__constant__ int8_t c_cv_pattern[1024];
+__constant__ int c_cv_umax[kHalfPatch + 1];
+
+constexpr float kHarrisK = 0.04f;  // HARRIS_K (orb.cpp)
+constexpr int kFastTh = 20;        // computeKeyPoints: FastFeatureDetector fd(20, true)
+constexpr int kTW = 64, kTH = 16;  // k_cvfast tile
+constexpr int kSelCap = 4096;      // k_cvselect: keypoints kept in LDS (more: global scratch)
+
+struct CvLevel {
+  int w, h, pitch, pyr_off;
+  int rx0, rx1, ry0, ry1;  // border region [edge, w-edge) x [edge, h-edge) (empty: rx1 <= rx0)
+  int bm_off, bm_wpr;      // keep bitmap words of this level inside one image's block
+  int feats;               // nfeaturesPerLevel
+  int cand_off, cand_cap;  // global candidate scratch (max strict-NMS survivors of the region)
+  int kp_off, kp_cap;      // per-image keypoint slots of this level
+  float scale, size;       // getScale(level, 0, scaleFactor), patchSize * scale
+};
+
+struct CvTile {
+  int16_t level, tx, ty, pad;
+};
+
+struct __align__(8) CvKey {
+  float r;     // response (FAST score, then Harris)
+  uint32_t k;  // y << 16 | x in level coordinates
+};
+
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+  const int gx = gridDim.x, total = gx * gridDim.y;
+  int lin = blockIdx.y * gx + blockIdx.x;
+  const int q = total >> 3;
+  if (lin < (q << 3)) lin = (lin & 7) * q + (lin >> 3);
+  by = lin / gx;
+  bx = lin - by * gx;
+}
+
+// ------------------------------------------------------------------ k_cvfast
+// cv::FAST(level, keypoints, 20, true) keeps p when score(p) >= 20 and score(p) > V(q) for the
+// 8 neighbours, V(q) = score(q) if q is a corner at 20, else 0 (fast.cpp); then
+// runByImageBorder drops every keypoint outside [edge, w-edge) x [edge, h-edge) (edge >= 18,
+// so every neighbour of a kept pixel is a detection pixel).  A tile stages rows Y0-4..Y0+19
+// and columns X0-4..X0+67 (dword loads), scores the tile plus a 1-px ring into LDS (0 unless a
+// corner; compass-point pretest first: a 9-arc holds two consecutive compass points), then
+// one wave per row ballots the NMS survivors into the row's 64-bit keep word and stores the
+// survivors' scores.
+__global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
+                                                const CvLevel* __restrict__ lv,
+                                                const CvTile* __restrict__ tiles,
+                                                uint64_t* __restrict__ bitmaps, int64_t bm_words,
+                                                uint8_t* __restrict__ smap) {
+  constexpr int SW = kTW + 8, SR = kTH + 8;  // staged bytes per row, rows
+  constexpr int QW = kTW + 2, QR = kTH + 2;  // score ring
+  __shared__ __align__(16) uint32_t s_in[SR * SW / 4];
+  __shared__ uint8_t s_sc[QR * QW];
+  int bx, img;
+  xcd_block(bx, img);
+  const CvTile T = tiles[bx];
+  const CvLevel L = lv[T.level];
+  const int X0 = T.tx * kTW, Y0 = L.ry0 + T.ty * kTH;
+  const uint8_t* src = pyr + (int64_t)img * pyr_bytes + L.pyr_off;
+  const int tid = threadIdx.x;
+  const int pw = L.pitch >> 2;
+  for (int i = tid; i < SR * (SW / 4); i += 256) {
+    const int r = i / (SW / 4), c = i - r * (SW / 4);
+    const int y = min(max(Y0 - 4 + r, 0), L.h - 1);
+    const int cw = min(max((X0 >> 2) - 1 + c, 0), pw - 1);
+    s_in[i] = *(const uint32_t*)(src + (int64_t)y * L.pitch + 4 * cw);
+  }
+  __syncthreads();
+  const uint8_t* S = (const uint8_t*)s_in;
+  const int t = kFastTh;
+  for (int i = tid; i < QR * QW; i += 256) {
+    const int j = i / QW, c = i - j * QW;
+    const int x = X0 - 1 + c, y = Y0 - 1 + j;
+    int sc = 0;
+    if (x >= L.rx0 - 1 && x <= L.rx1 && y >= L.ry0 - 1 && y <= L.ry1) {
+      const uint8_t* p = S + (j + 3) * SW + (c + 3);
+      const int v = p[0];
+      const int d0 = v - p[3 * SW], d4 = v - p[3], d8 = v - p[-3 * SW], d12 = v - p[-3];
+      const bool dk0 = d0 > t, dk4 = d4 > t, dk8 = d8 > t, dk12 = d12 > t;
+      const bool br0 = d0 < -t, br4 = d4 < -t, br8 = d8 < -t, br12 = d12 < -t;
+      const bool pass = (dk0 && dk4) || (dk4 && dk8) || (dk8 && dk12) || (dk12 && dk0) ||
+                        (br0 && br4) || (br4 && br8) || (br8 && br12) || (br12 && br0);
+      if (pass) {
+        const int s = fast_score(S, SW, c + 3, j + 3);
+        sc = s >= t ? s : 0;
+      }
+    }
+    s_sc[i] = (uint8_t)sc;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  const int x = X0 + lane;
+  uint64_t* bm = bitmaps + (int64_t)img * bm_words + L.bm_off;
+  uint8_t* sm = smap + (int64_t)img * pyr_bytes + L.pyr_off;
+  for (int j = wave; j < kTH; j += 4) {
+    const int y = Y0 + j;
+    if (y >= L.ry1) break;  // wave-uniform
+    const uint8_t* q = s_sc + (j + 1) * QW + (lane + 1);
+    const int s = q[0];
+    bool keep = s > 0 && x >= L.rx0 && x < L.rx1;
+    if (keep) {
+      keep = s > q[-QW - 1] && s > q[-QW] && s > q[-QW + 1] && s > q[-1] && s > q[1] &&
+             s > q[QW - 1] && s > q[QW] && s > q[QW + 1];
+    }
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) bm[(int64_t)y * L.bm_wpr + T.tx] = m;
+    if (keep) sm[(int64_t)y * L.pitch + x] = (uint8_t)s;
+  }
+}
+
+// ------------------------------------------------------------------ retainBest (one wave)
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void kswap(CvKey* a, int i, int j) {
+  const CvKey t = a[i];
+  a[i] = a[j];
+  a[j] = t;
+}
+
+struct Stoppers {
+  int K;     // swap pairs
+  int cutL;  // first left stopper that is not swapped (INT_MAX: none)
+  int cutR;  // smallest swapped right-stopper position (hi: none)
+  int rtot;  // right stoppers in [lo, hi)
+};
+
+// The swap sequence of a two-scan partition of [lo, hi): the left scan stops at elements with
+// ls(e), the right scan at rs(e); pair k = (k-th left stopper from lo, k-th right stopper from
+// hi - 1) swaps while the first is left of the second.  Lpos / Rpos hold up to (hi-lo)/2 ints.
+template <class LS, class RS>
+__device__ Stoppers wave_partition(CvKey* a, int lo, int hi, uint32_t* Lpos, uint32_t* Rpos,
+                                   LS ls, RS rs) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1, le = lt | (1ull << lane);
+  int rtot = 0;
+  for (int p0 = lo; p0 < hi; p0 += 64) {
+    const int p = p0 + lane;
+    bool f = false;
+    if (p < hi) f = rs(a[p]);
+    rtot += __popcll(__ballot(f));
+  }
+  int lcnt = 0, rcnt = 0, K = 0, cutL = INT_MAX, cutR = hi;
+  for (int p0 = lo; p0 < hi; p0 += 64) {
+    const int p = p0 + lane;
+    bool lf = false, rf = false;
+    if (p < hi) {
+      const CvKey e = a[p];
+      lf = ls(e);
+      rf = rs(e);
+    }
+    const uint64_t lb = __ballot(lf), rb = __ballot(rf);
+    const int lrank = lcnt + __popcll(lb & lt);
+    const int rrank = rtot - (rcnt + __popcll(rb & le));
+    const bool lsw = lf && rrank > lrank;
+    const bool rsw = rf && lrank > rrank;
+    if (lsw) Lpos[lrank] = p;
+    if (rsw) Rpos[rrank] = p;
+    K += __popcll(__ballot(lsw));
+    const uint64_t un = __ballot(lf && !lsw);
+    if (cutL == INT_MAX && un) cutL = p0 + __ffsll((unsigned long long)un) - 1;
+    const uint64_t rm = __ballot(rsw);
+    if (rm) cutR = min(cutR, p0 + __ffsll((unsigned long long)rm) - 1);
+    lcnt += __popcll(lb);
+    rcnt += __popcll(rb);
+  }
+  __syncthreads();
+  for (int k = lane; k < K; k += 64) kswap(a, Lpos[k], Rpos[k]);
+  __syncthreads();
+  return {K, cutL, cutR, rtot};
+}
+
+__device__ __forceinline__ bool kgreater(const CvKey& x, const CvKey& y) { return x.r > y.r; }
+
+// libstdc++ (GCC 4.8) __move_median_first, __adjust_heap / __heap_select, __insertion_sort with
+// comp = KeypointResponseGreater: sequential, lane 0 only (3 elements; the depth-exhausted
+// fallback; <= 3 elements).
+__device__ void move_median_first(CvKey* a, int x, int y, int z) {
+  if (kgreater(a[x], a[y])) {
+    if (kgreater(a[y], a[z]))
+      kswap(a, x, y);
+    else if (kgreater(a[x], a[z]))
+      kswap(a, x, z);
+  } else if (kgreater(a[x], a[z])) {
+    return;
+  } else if (kgreater(a[y], a[z])) {
+    kswap(a, x, z);
+  } else {
+    kswap(a, x, y);
+  }
+}
+
+__device__ void adjust_heap(CvKey* first, long hole, long len, CvKey value) {
+  const long top = hole;
+  long second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (kgreater(first[second], first[second - 1])) second--;
+    first[hole] = first[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    first[hole] = first[second - 1];
+    hole = second - 1;
+  }
+  long parent = (hole - 1) / 2;
+  while (hole > top && kgreater(first[parent], value)) {
+    first[hole] = first[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  first[hole] = value;
+}
+
+__device__ void heap_select(CvKey* first, long middle, long last) {
+  const long len = middle;
+  if (len >= 2) {
+    for (long parent = (len - 2) / 2;; parent--) {
+      adjust_heap(first, parent, len, first[parent]);
+      if (parent == 0) break;
+    }
+  }
+  for (long i = middle; i < last; ++i)
+    if (kgreater(first[i], first[0])) {
+      const CvKey value = first[i];
+      first[i] = first[0];
+      adjust_heap(first, 0, len, value);
+    }
+}
+
+__device__ void insertion_sort(CvKey* a, int first, int last) {
+  if (first == last) return;
+  for (int i = first + 1; i != last; ++i) {
+    const CvKey val = a[i];
+    if (kgreater(val, a[first])) {
+      for (int k = i; k > first; k--) a[k] = a[k - 1];
+      a[first] = val;
+    } else {
+      int l = i, next = i - 1;
+      while (kgreater(val, a[next])) {
+        a[l] = a[next];
+        l = next;
+        --next;
+      }
+      a[l] = val;
+    }
+  }
+}
+
+// std::nth_element(a + first, a + nth, a + last, greater) as GCC 4.8 implements it
+// (__introselect with __unguarded_partition_pivot).
+__device__ void wave_nth_element(CvKey* a, int first, int nth, int last, uint32_t* Lpos,
+                                 uint32_t* Rpos) {
+  const int lane = threadIdx.x & 63;
+  if (first == last || nth == last) return;
+  int depth = 2 * (31 - __clz(last - first));
+  while (last - first > 3) {
+    if (depth == 0) {
+      if (lane == 0) {
+        heap_select(a + first, nth + 1 - first, last - first);
+        kswap(a, first, nth);
+      }
+      __syncthreads();
+      return;
+    }
+    --depth;
+    if (lane == 0) move_median_first(a, first, first + (last - first) / 2, last - 1);
+    __syncthreads();
+    const float piv = a[first].r;
+    const Stoppers s = wave_partition(
+        a, first + 1, last, Lpos, Rpos, [piv](const CvKey& e) { return !(e.r > piv); },
+        [piv](const CvKey& e) { return !(piv > e.r); });
+    const int cut = min(s.cutL, s.cutR);
+    if (cut <= nth)
+      first = cut;
+    else
+      last = cut;
+  }
+  if (lane == 0) insertion_sort(a, first, last);
+  __syncthreads();
+}
+
+// KeyPointsFilter::retainBest (OpenCV 2.4 keypoint.cpp); returns the new size.
+__device__ int wave_retain_best(CvKey* a, int n, int n_points, uint32_t* Lpos, uint32_t* Rpos) {
+  if (n_points <= 0 || n <= n_points) return n;
+  wave_nth_element(a, 0, n_points, n, Lpos, Rpos);
+  const float amb = a[n_points - 1].r;
+  const Stoppers s = wave_partition(
+      a, n_points, n, Lpos, Rpos, [amb](const CvKey& e) { return !(e.r >= amb); },
+      [amb](const CvKey& e) { return e.r >= amb; });
+  return n_points + s.rtot;
+}
+
+// HarrisResponses(img, pts, 7, 0.04) for an integral keypoint (orb.cpp).
+__device__ float harris_response(const uint8_t* img, int step, int x, int y) {
+  const int r = 3;
+  float scale = (float)((1 << 2) * 7) * 255.0f;
+  scale = 1.0f / scale;
+  const float scale_sq_sq = scale * scale * scale * scale;
+  const uint8_t* ptr0 = img + (y - r) * step + (x - r);
+  int a = 0, b = 0, c = 0;
+  for (int i = 0; i < 7; i++)
+    for (int j = 0; j < 7; j++) {
+      const uint8_t* p = ptr0 + i * step + j;
+      const int Ix = (p[1] - p[-1]) * 2 + (p[-step + 1] - p[-step - 1]) + (p[step + 1] - p[step - 1]);
+      const int Iy = (p[step] - p[-step]) * 2 + (p[step - 1] - p[-step - 1]) + (p[step + 1] - p[-step + 1]);
+      a += Ix * Ix;
+      b += Iy * Iy;
+      c += Ix * Iy;
+    }
+  const float fa = (float)a, fb = (float)b, fc = (float)c;
+  const float t0 = fa * fb;
+  const float t1 = fc * fc;
+  const float s = fa + fb;
+  const float t2 = kHarrisK * s * s;
+  return (t0 - t1 - t2) * scale_sq_sq;
+}
+
+// ------------------------------------------------------------------ k_cvselect
+// One wave per (image, level): computeKeyPoints after FAST (orb.cpp): the raster-order
+// keypoint list, retainBest(2N) + HarrisResponses for HARRIS_SCORE, retainBest(N); the
+// survivors (in their retained order) go to the level's keypoint slots, the count to ocount
+// (a count above kp_cap is reported and the describe stage flags the image).
+__global__ __launch_bounds__(64) void k_cvselect(
+    const uint8_t* __restrict__ pyr, int64_t pyr_bytes, const CvLevel* __restrict__ lv,
+    int nlevels, const uint64_t* __restrict__ bitmaps, int64_t bm_words,
+    const uint8_t* __restrict__ smap, CvKey* __restrict__ gcand, uint32_t* __restrict__ gpos,
+    int cand_total, int harris, CvKey* __restrict__ okey, int kp_total, int* __restrict__ ocount) {
+  extern __shared__ __align__(16) char s_sel[];
+  const int level = blockIdx.x, img = blockIdx.y;
+  const int lane = threadIdx.x;
+  const CvLevel L = lv[level];
+  int* oc = ocount + img * nlevels + level;
+  if (L.rx1 <= L.rx0 || L.ry1 <= L.ry0) {
+    if (lane == 0) *oc = 0;
+    return;
+  }
+  const uint64_t* bm = bitmaps + (int64_t)img * bm_words + L.bm_off;
+  const int w0 = L.rx0 >> 6, nw = ((L.rx1 - 1) >> 6) - w0 + 1, nr = L.ry1 - L.ry0;
+  const int total = nw * nr;
+  int n = 0;
+  for (int q0 = 0; q0 < total; q0 += 64) {
+    const int q = q0 + lane;
+    int c = 0;
+    if (q < total) {
+      const int r = q / nw, k = q - r * nw;
+      c = __popcll(bm[(int64_t)(L.ry0 + r) * L.bm_wpr + w0 + k]);
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    n += c;
+  }
+  CvKey* a;
+  uint32_t *Lpos, *Rpos;
+  if (n <= kSelCap) {
+    a = (CvKey*)s_sel;
+    Lpos = (uint32_t*)(s_sel + 8 * kSelCap);
+    Rpos = Lpos + kSelCap / 2;
+  } else {
+    a = gcand + (int64_t)img * cand_total + L.cand_off;
+    Lpos = gpos + (int64_t)img * cand_total + L.cand_off;
+    Rpos = Lpos + (L.cand_cap + 1) / 2;
+  }
+  // raster order: word q = row-major over (row, word), bits ascending
+  const uint8_t* sm = smap + (int64_t)img * pyr_bytes + L.pyr_off;
+  int base = 0;
+  for (int q0 = 0; q0 < total; q0 += 64) {
+    const int q = q0 + lane;
+    uint64_t word = 0;
+    int r = 0, k = 0;
+    if (q < total) {
+      r = q / nw;
+      k = q - r * nw;
+      word = bm[(int64_t)(L.ry0 + r) * L.bm_wpr + w0 + k];
+    }
+    const int c = __popcll(word);
+    const int incl = wave_incl_scan(c);
+    int pos = base + incl - c;
+    const int y = L.ry0 + r, xb = 64 * (w0 + k);
+    while (word) {
+      const int b = __ffsll((unsigned long long)word) - 1;
+      word &= word - 1;
+      const int x = xb + b;
+      CvKey e;
+      e.r = (float)sm[(int64_t)y * L.pitch + x];
+      e.k = ((uint32_t)y << 16) | (uint32_t)x;
+      a[pos++] = e;
+    }
+    base += __shfl(incl, 63);
+  }
+  __syncthreads();
+  const int feats = L.feats;
+  if (harris) {
+    n = wave_retain_best(a, n, 2 * feats, Lpos, Rpos);
+    const uint8_t* img0 = pyr + (int64_t)img * pyr_bytes + L.pyr_off;
+    for (int i = lane; i < n; i += 64) {
+      const uint32_t key = a[i].k;
+      a[i].r = harris_response(img0, L.pitch, (int)(key & 0xFFFF), (int)(key >> 16));
+    }
+    __syncthreads();
+  }
+  n = wave_retain_best(a, n, feats, Lpos, Rpos);
+  CvKey* out = okey + (int64_t)img * kp_total + L.kp_off;
+  const int m = min(n, L.kp_cap);
+  for (int i = lane; i < m; i += 64) out[i] = a[i];
+  if (lane == 0) *oc = n;
+}
+
+// computeOrbDescriptor's rotation: angle *= (float)(CV_PI/180.f); a = (float)cos(angle),
+// b = (float)sin(angle) through the double ::cos / ::sin (OCML f64 here, glibc in the
+// reference; tests/test_cvorb_gpu.py compares every float angle in [0, 360] with the host libm).
+__device__ __forceinline__ void cv_cos_sin(float angle_deg, float* a, float* b) {
+  float ang = angle_deg;
+  ang *= (float)(3.14159265358979323846 / 180.f);
+  *a = (float)cos((double)ang);
+  *b = (float)sin((double)ang);
+}
+
+// ------------------------------------------------------------------ k_cvdescribe
+// One half-wave per keypoint slot, 8 per workgroup: computeOrientation (IC_Angle on the
+// unblurred level, cvRound(pt) centre = the integral keypoint), then computeOrbDescriptor on
+// the blurred level: a = (float)cos(angle), b = (float)sin(angle) in double, sample
+// (cvRound(x*b + y*a), cvRound(x*a - y*b)) without contraction, bit = I0 < I1; lane j makes
+// byte j.  Then operator()'s `keypoint->pt *= scale` for levels != firstLevel.  Output is
+// level-major (descriptors.rowRange(offset, offset + nkeypoints) per level).
+struct KpOff {
+  int off[kMaxLevels + 1];
+};
+
+__global__ __launch_bounds__(256) void k_cvdescribe(
+    const uint8_t* __restrict__ pyr, int64_t pyr_bytes, const uint8_t* __restrict__ blur,
+    const CvLevel* __restrict__ lv, int nlevels, KpOff ko, const CvKey* __restrict__ okey,
+    const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
+    uint8_t* __restrict__ desc, int* __restrict__ counts) {
+  constexpr int RW = 10, BW = 11;  // dwords per staged row (31+3 / 37+3 bytes, rounded up)
+  constexpr int RN = 31 * RW, BN = 37 * BW;
+  __shared__ uint32_t s_raw[8][RN];
+  __shared__ uint32_t s_blr[8][BN];
+  int bx, img;
+  xcd_block(bx, img);
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int hw = threadIdx.x >> 5;
+  const int slot = bx * 8 + hw;
+  const int* oc = ocount + img * nlevels;
+  if (bx == 0 && threadIdx.x == 0) {
+    int t = 0;
+    bool over = false;
+    for (int l = 0; l < nlevels; l++) {
+      t += oc[l];
+      over |= oc[l] > lv[l].kp_cap;
+    }
+    counts[img] = over ? -t : t;
+  }
+  int level = 0;
+#pragma unroll
+  for (int l = 1; l < kMaxLevels; l++) level += (l < nlevels && slot >= ko.off[l]);
+  const CvLevel& G = lv[level];
+  const int idx = slot - ko.off[level];
+  int noc = min(oc[level], G.kp_cap);
+  const CvKey kk = okey[(int64_t)img * kp_total + min(slot, kp_total - 1)];
+  uint32_t key = kk.k;
+  float resp = kk.r;
+  int pitch = G.pitch, pyr_off = G.pyr_off;
+  float lscale = G.scale, lsize = G.size;
+  asm volatile("" : "+v"(noc), "+v"(key), "+v"(pitch), "+v"(pyr_off), "+v"(lscale), "+v"(lsize));
+  const bool active = slot < kp_total && idx < noc;  // uniform within the half-wave
+  if (!active) key = 0;
+  const int cx = active ? (int)(key & 0xFFFF) : 0;
+  const int cy = active ? (int)(key >> 16) : 0;
+  const uint8_t* Lb = pyr + (int64_t)img * pyr_bytes + pyr_off;
+  const uint8_t* Bp = blur + (int64_t)img * pyr_bytes + pyr_off;
+  const int fr = (cx - 15) >> 2, lr = (cx + 15) >> 2;
+  const int fb = (cx - 18) >> 2, lb = (cx + 18) >> 2;
+  if (active) {
+    uint32_t vr[(RN + 31) / 32], vb[(BN + 31) / 32];
+#pragma unroll
+    for (int k = 0; k < (RN + 31) / 32; k++) {
+      const int i = hl + 32 * k, r = i / RW, c = i - r * RW;
+      vr[k] = (i < RN && fr + c <= lr)
+                  ? *(const uint32_t*)(Lb + (uint32_t)((cy - 15 + r) * pitch + 4 * (fr + c)))
+                  : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < (BN + 31) / 32; k++) {
+      const int i = hl + 32 * k, r = i / BW, c = i - r * BW;
+      vb[k] = (i < BN && fb + c <= lb)
+                  ? *(const uint32_t*)(Bp + (uint32_t)((cy - 18 + r) * pitch + 4 * (fb + c)))
+                  : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < (RN + 31) / 32; k++)
+      if (hl + 32 * k < RN) s_raw[hw][hl + 32 * k] = vr[k];
+#pragma unroll
+    for (int k = 0; k < (BN + 31) / 32; k++)
+      if (hl + 32 * k < BN) s_blr[hw][hl + 32 * k] = vb[k];
+  }
+  constexpr int RS = 4 * RW, BS = 4 * BW;
+  const uint8_t* raw = (const uint8_t*)s_raw[hw] + 15 * RS + (cx - 4 * fr);
+  const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - 4 * fb);
+  int m10 = 0, m01 = 0;
+  if (active && hl < 31) {
+    const int u = hl - 15;
+    m10 = u * (int)raw[u];
+    for (int v = 1; v <= kHalfPatch; v++) {
+      const int d = c_cv_umax[v];
+      if (u < -d || u > d) continue;
+      const int vp = raw[u + v * RS], vm = raw[u - v * RS];
+      m10 += u * (vp + vm);
+      m01 += v * (vp - vm);
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    m10 += __shfl_xor(m10, o);
+    m01 += __shfl_xor(m01, o);
+  }
+  if (!active) return;
+  const float angle = orbx_fast_atan2((float)m01, (float)m10);
+  float ca, sb;
+  cv_cos_sin(angle, &ca, &sb);
+  uint32_t byte = 0;
+#pragma unroll
+  for (int m = 0; m < 8; m++) {
+    const int pair = hl * 8 + m;
+    int t[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const float px = (float)c_cv_pattern[pair * 4 + e * 2];
+      const float py = (float)c_cv_pattern[pair * 4 + e * 2 + 1];
+      const float xr = __fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sb));
+      const float yr = __fadd_rn(__fmul_rn(px, sb), __fmul_rn(py, ca));
+      const int col = (int)__builtin_rintf(xr), row = (int)__builtin_rintf(yr);
+      t[e] = bc[row * BS + col];
+    }
+    byte |= (uint32_t)(t[0] < t[1]) << m;
+  }
+  int outpos = idx;
+  for (int l = 0; l < level; l++) outpos += oc[l];
+  if (outpos >= kp_total) return;  // an overflowed image (count reported negative)
+  const int64_t o = (int64_t)img * kp_total + outpos;
+  desc[o * 32 + hl] = (uint8_t)byte;
+  if (hl == 0) {
+    orbx_keypoint k;
+    k.x = level ? (float)cx * lscale : (float)cx;
+    k.y = level ? (float)cy * lscale : (float)cy;
+    k.size = lsize;
+    k.angle = angle;
+    k.response = resp;
+    k.octave = level;
+    k.class_id = -1;
+    kps[o] = k;
+  }
+}
+
+// ------------------------------------------------------------------ matchers
+__device__ __forceinline__ int hamming8(const uint32_t* q, uint4 t0, uint4 t1) {
+  int d = __popc(q[0] ^ t0.x);
+  d += __popc(q[1] ^ t0.y);
+  d += __popc(q[2] ^ t0.z);
+  d += __popc(q[3] ^ t0.w);
+  d += __popc(q[4] ^ t1.x);
+  d += __popc(q[5] ^ t1.y);
+  d += __popc(q[6] ^ t1.z);
+  d += __popc(q[7] ^ t1.w);
+  return d;
+}
+
+constexpr int kBfQ = 128;     // queries per workgroup (one per thread)
+constexpr int kBfChunk = 256;  // train rows staged in LDS per step
+
+// For every query row the nearest train row (strict `<`: the first minimum) and, for mode 1,
+// the second-nearest distance with naive_nn_search2's update rule, plus the extremes over all
+// pairs.  Train set t of problem p = train + p * train_stride rows, count from tcount[p] (a
+// negative count is treated as empty).  Out: best index (-1 if empty), best and second
+// distance per query.
+__global__ __launch_bounds__(kBfQ) void k_bfmatch(const uint8_t* __restrict__ query, int nq,
+                                                  const uint8_t* __restrict__ train,
+                                                  int64_t train_stride, const int* __restrict__ tcount,
+                                                  int2* __restrict__ best, int* __restrict__ second,
+                                                  int* __restrict__ extremes) {
+  __shared__ uint4 s_t[kBfChunk][2];
+  const int p = blockIdx.y;
+  const int qi = blockIdx.x * kBfQ + threadIdx.x;
+  const int nt = max(tcount[p], 0);
+  const uint8_t* T = train + (int64_t)p * train_stride * 32;
+  uint32_t q[8];
+  if (qi < nq) {
+    const uint4* qp = (const uint4*)(query + (int64_t)qi * 32);
+    const uint4 a = qp[0], b = qp[1];
+    q[0] = a.x, q[1] = a.y, q[2] = a.z, q[3] = a.w, q[4] = b.x, q[5] = b.y, q[6] = b.z, q[7] = b.w;
+  } else {
+    for (int i = 0; i < 8; i++) q[i] = 0;
+  }
+  int bd = INT_MAX, sd = INT_MAX, bi = -1, mn = INT_MAX, mx = 0;
+  for (int j0 = 0; j0 < nt; j0 += kBfChunk) {
+    const int nc = min(kBfChunk, nt - j0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * nc; i += kBfQ)
+      s_t[i >> 1][i & 1] = ((const uint4*)(T + (int64_t)j0 * 32))[i];
+    __syncthreads();
+    if (qi < nq) {
+      for (int j = 0; j < nc; j++) {
+        const int d = hamming8(q, s_t[j][0], s_t[j][1]);
+        if (d < bd) {
+          sd = bd;
+          bd = d;
+          bi = j0 + j;
+        } else if (d < sd) {
+          sd = d;
+        }
+        mn = min(mn, d);
+        mx = max(mx, d);
+      }
+    }
+  }
+  if (qi < nq) {
+    best[(int64_t)p * nq + qi] = make_int2(bi, bd);
+    if (second) second[(int64_t)p * nq + qi] = sd;
+  }
+  if (extremes) {
+    for (int o = 32; o > 0; o >>= 1) {
+      mn = min(mn, __shfl_xor(mn, o));
+      mx = max(mx, __shfl_xor(mx, o));
+    }
+    if ((threadIdx.x & 63) == 0 && nt > 0) {
+      atomicMin(extremes + 2 * p, mn);
+      atomicMax(extremes + 2 * p + 1, mx);
+    }
+  }
+}
+
+// Marker::Match after matcher.match(target, frame): DMatch list (queryIdx = target row), then
+// max_dist over the matches and the good flags `distance < 0.5 * max_dist` (Marker.cc:115-133).
+// One wave per frame.  A frame without keypoints gets train -1 and no good match (Marker::Match
+// returns false before matching).
+__global__ __launch_bounds__(64) void k_good(const int2* __restrict__ best, int nq,
+                                             const int* __restrict__ tcount,
+                                             orbx_dmatch* __restrict__ matches,
+                                             uint8_t* __restrict__ good, int* __restrict__ good_count) {
+  const int p = blockIdx.x, lane = threadIdx.x;
+  const bool empty = tcount[p] <= 0 || nq <= 0;
+  int mx = 0;
+  for (int i = lane; i < nq; i += 64) mx = max(mx, best[(int64_t)p * nq + i].y);
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  int cnt = 0;
+  for (int i = lane; i < nq; i += 64) {
+    const int2 b = best[(int64_t)p * nq + i];
+    orbx_dmatch m;
+    m.query_idx = i;
+    m.train_idx = empty ? -1 : b.x;
+    m.img_idx = 0;
+    m.distance = empty ? 0.f : (float)b.y;
+    matches[(int64_t)p * nq + i] = m;
+    // (double)d < 0.5 * (double)max_dist with integral distances
+    const bool g = !empty && 2 * b.y < mx;
+    good[(int64_t)p * nq + i] = g;
+    cnt += g;
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (lane == 0) good_count[p] = cnt;
+}
+
+// ------------------------------------------------------------------ test hooks
+__global__ void k_debug_cossin(const float* __restrict__ deg, int64_t n, float* __restrict__ c,
+                               float* __restrict__ sn) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    cv_cos_sin(deg[i], c + i, sn + i);
+}
+
+// KeyPointsFilter::retainBest on one array, through LDS (n <= kSelCap) or global memory.
+__global__ __launch_bounds__(64) void k_debug_retain(CvKey* __restrict__ a, int n, int n_points,
+                                                     uint32_t* __restrict__ gpos, int use_lds,
+                                                     int* __restrict__ n_out) {
+  extern __shared__ __align__(16) char s_sel[];
+  CvKey* w = a;
+  uint32_t *Lpos = gpos, *Rpos = gpos + (n + 1) / 2;
+  if (use_lds) {
+    w = (CvKey*)s_sel;
+    Lpos = (uint32_t*)(s_sel + 8 * kSelCap);
+    Rpos = Lpos + kSelCap / 2;
+    for (int i = threadIdx.x; i < n; i += 64) w[i] = a[i];
+    __syncthreads();
+  }
+  const int m = wave_retain_best(w, n, n_points, Lpos, Rpos);
+  if (use_lds)
+    for (int i = threadIdx.x; i < m; i += 64) a[i] = w[i];
+  if (threadIdx.x == 0) *n_out = m;
+}
+
+// ------------------------------------------------------------------ plan
+static inline int cv_round(double v) { return (int)nearbyint(v); }
+
+bool params_supported(const orbx_cvorb_params& p) {
+  return p.nlevels >= 1 && p.nlevels <= kMaxLevels && p.first_level == 0 && p.wta_k == 2 &&
+         p.patch_size == 31 && p.edge_threshold >= 18 && p.scale_factor > 0 &&
+         p.nfeatures >= 0 && (p.score_type == ORBX_HARRIS_SCORE || p.score_type == ORBX_FAST_SCORE);
+}
+
+struct Plan {
+  orbx_cvorb_params p{};
+  int w = 0, h = 0, max_batch = 0, device = 0;
+  bool exact = false;  // keypoint capacity = every possible survivor (drop-in)
+  hipStream_t stream = nullptr;
+  Geometry g;
+  PyrDev pd;
+  CvLevel lv[kMaxLevels];
+  CvLevel* d_lv = nullptr;
+  CvTile* d_tiles = nullptr;
+  int ntiles = 0;
+  int64_t bm_words = 0;
+  int cand_total = 0, kp_total = 0;
+  uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_smap = nullptr;
+  uint64_t* d_bm = nullptr;
+  CvKey *d_cand = nullptr, *d_okey = nullptr;
+  uint32_t* d_pos = nullptr;
+  int *d_ocount = nullptr, *d_counts = nullptr;
+  orbx_keypoint* d_kps = nullptr;
+  uint8_t* d_desc = nullptr;
+  hipGraphExec_t graph = nullptr;
+  const uint8_t* graph_in = nullptr;
+  int graph_n = -1;
+  Profiler* prof = nullptr;  // owned by the caller
+};
+
+template <class T>
+int dalloc(T** p, size_t count) {
+  if (count == 0) count = 1;
+  if (hipMalloc((void**)p, count * sizeof(T)) != hipSuccess) return ORBX_ENOMEM;
+  return ORBX_OK;
+}
+
+void plan_destroy(Plan* P) {
+  if (!P) return;
+  if (P->graph) (void)hipGraphExecDestroy(P->graph);
+  pyr_dev_destroy(&P->pd);
+  void* bufs[] = {P->d_lv, P->d_tiles, P->d_pyr, P->d_blur, P->d_smap, P->d_bm, P->d_cand,
+                  P->d_okey, P->d_pos, P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (P->stream) (void)hipStreamDestroy(P->stream);
+  delete P;
+}
+
+// Level sizes, per-level feature counts and scales of cv::ORB::operator() (orb.cpp):
+// getScale = (float)pow(scaleFactor, level) with the member `double scaleFactor`,
+// sz = (cvRound(cols * (1/scale)), ...), nfeaturesPerLevel by the float geometric series.
+void levels(const orbx_cvorb_params& p, int cols, int rows, int* lw, int* lh, float* sc,
+            int* feats) {
+  const double sf = (double)p.scale_factor;
+  for (int l = 0; l < p.nlevels; l++) {
+    const float s = (float)pow(sf, (double)(l - p.first_level));
+    const float inv = 1 / s;
+    sc[l] = s;
+    lw[l] = cv_round(cols * inv);
+    lh[l] = cv_round(rows * inv);
+  }
+  const float factor = (float)(1.0 / sf);
+  float nd = p.nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)p.nlevels));
+  int sum = 0;
+  for (int l = 0; l < p.nlevels - 1; l++) {
+    feats[l] = cv_round(nd);
+    sum += feats[l];
+    nd *= factor;
+  }
+  feats[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+}
+
+int plan_create(const orbx_cvorb_params& p, int w, int h, int max_batch, int device, bool exact,
+                Plan** out) {
+  *out = nullptr;
+  if (w <= 0 || h <= 0 || max_batch <= 0) return ORBX_EINVAL;
+  if (!params_supported(p)) return ORBX_EUNSUPPORTED;
+  Plan* P = new (std::nothrow) Plan();
+  if (!P) return ORBX_ENOMEM;
+  P->p = p;
+  P->w = w;
+  P->h = h;
+  P->max_batch = max_batch;
+  P->device = device;
+  P->exact = exact;
+  auto fail = [&](int code) {
+    plan_destroy(P);
+    return code;
+  };
+  int lw[kMaxLevels], lh[kMaxLevels], feats[kMaxLevels];
+  float sc[kMaxLevels];
+  levels(p, w, h, lw, lh, sc, feats);
+  Geometry& g = P->g;
+  g.nlevels = p.nlevels;
+  g.w = w;
+  g.h = h;
+  for (int l = 0; l < p.nlevels; l++) {
+    g.lv[l] = LevelGeom{};
+    g.lv[l].w = lw[l];
+    g.lv[l].h = lh[l];
+    if (lw[l] >= 4096 * 16 || lh[l] >= 65536) return fail(ORBX_EUNSUPPORTED);
+  }
+  std::string why;
+  int rc = build_pyramid(&g, &why);
+  if (rc != ORBX_OK) {
+    fprintf(stderr, "[orbx] cv::ORB plan %dx%d unsupported: %s\n", w, h, why.c_str());
+    return fail(rc);
+  }
+  const int b = p.edge_threshold;
+  std::vector<CvTile> tiles;
+  int64_t bm = 0;
+  int cand = 0, kp = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    CvLevel& L = P->lv[l];
+    const LevelGeom& G = g.lv[l];
+    L = CvLevel{};
+    L.w = G.w;
+    L.h = G.h;
+    L.pitch = G.pitch;
+    L.pyr_off = (int)G.pyr_off;
+    // runByImageBorder: an image no larger than 2 * edge keeps nothing
+    const bool has = G.h > 2 * b && G.w > 2 * b;
+    L.rx0 = b;
+    L.ry0 = b;
+    L.rx1 = has ? G.w - b : b;
+    L.ry1 = has ? G.h - b : b;
+    L.bm_wpr = L.pitch / 64;
+    L.bm_off = (int)bm;
+    bm += (int64_t)L.bm_wpr * L.h;
+    L.feats = feats[l];
+    const int rw = L.rx1 - L.rx0, rh = L.ry1 - L.ry0;
+    const int maxsurv = has ? ((rw + 1) / 2) * ((rh + 1) / 2) : 0;
+    L.cand_off = cand;
+    L.cand_cap = maxsurv;
+    cand += maxsurv;
+    L.kp_off = kp;
+    L.kp_cap = exact ? maxsurv : std::min(maxsurv, std::max(2 * feats[l], feats[l] + 64));
+    kp += L.kp_cap;
+    L.scale = sc[l];
+    L.size = p.patch_size * sc[l];
+    if (has)
+      for (int ty = 0; ty * kTH < rh; ty++)
+        for (int tx = L.rx0 / kTW; tx <= (L.rx1 - 1) / kTW; tx++)
+          tiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, 0});
+  }
+  if (bm >= INT_MAX || g.pyr_bytes >= INT_MAX) return fail(ORBX_EUNSUPPORTED);
+  P->bm_words = std::max<int64_t>(bm, 1);
+  P->cand_total = std::max(cand, 1);
+  P->kp_total = std::max(kp, 1);
+  P->ntiles = (int)tiles.size();
+  if (hipSetDevice(device) != hipSuccess) return fail(ORBX_EDEVICE);
+  if (hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(ORBX_EDEVICE);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(c_cv_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)) != hipSuccess)
+    return fail(ORBX_EDEVICE);
+  {
+    orbx_params op{p.nfeatures, p.scale_factor, p.nlevels, 20, 7};
+    Geometry t;
+    build_tables(op, &t);  // umax for halfPatchSize 15 (orb.cpp computes it the same way)
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_cv_umax), t.umax, sizeof(t.umax)) != hipSuccess)
+      return fail(ORBX_EDEVICE);
+  }
+  rc = pyr_dev_create(g, &P->pd);
+  if (rc != ORBX_OK) return fail(rc);
+  const size_t B = (size_t)max_batch;
+  if (dalloc(&P->d_lv, p.nlevels) || dalloc(&P->d_tiles, tiles.size()) ||
+      dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
+      dalloc(&P->d_smap, B * g.pyr_bytes) || dalloc(&P->d_bm, B * P->bm_words) ||
+      dalloc(&P->d_cand, B * P->cand_total) || dalloc(&P->d_pos, B * P->cand_total + 2) ||
+      dalloc(&P->d_okey, B * P->kp_total) || dalloc(&P->d_ocount, B * p.nlevels) ||
+      dalloc(&P->d_counts, B) || dalloc(&P->d_kps, B * P->kp_total) ||
+      dalloc(&P->d_desc, B * P->kp_total * 32))
+    return fail(ORBX_ENOMEM);
+  if (hipMemcpy(P->d_lv, P->lv, sizeof(CvLevel) * p.nlevels, hipMemcpyHostToDevice) ||
+      (tiles.size() && hipMemcpy(P->d_tiles, tiles.data(), sizeof(CvTile) * tiles.size(),
+                                 hipMemcpyHostToDevice)) ||
+      hipMemset(P->d_counts, 0, 4 * B))
+    return fail(ORBX_EDEVICE);
+  const int smem = 8 * kSelCap + 4 * kSelCap;
+  if (hipFuncSetAttribute((const void*)k_cvselect, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          smem) != hipSuccess)
+    return fail(ORBX_EDEVICE);
+  *out = P;
+  return ORBX_OK;
+}
+
+int enqueue(Plan* P, const uint8_t* d_in, int n) {
+  const Geometry& g = P->g;
+  const int L = P->p.nlevels;
+  Profiler dummy;
+  Profiler& pr = P->prof ? *P->prof : dummy;
+  const int st_pyr = pr.stage("k_pyramid"), st_fast = pr.stage("k_cvfast"),
+            st_sel = pr.stage("k_cvselect"), st_blur = pr.stage("k_blur"),
+            st_desc = pr.stage("k_cvdescribe");
+  hipStream_t s = P->stream;
+  pr.mark(s, -1);
+  int rc = launch_pyramid(g, P->pd, d_in, P->d_pyr, n, s);
+  if (rc) return rc;
+  pr.mark(s, st_pyr);
+  if (P->ntiles > 0)
+    hipLaunchKernelGGL(k_cvfast, dim3(P->ntiles, n), dim3(256), 0, s, P->d_pyr, g.pyr_bytes,
+                       P->d_lv, P->d_tiles, P->d_bm, P->bm_words, P->d_smap);
+  pr.mark(s, st_fast);
+  hipLaunchKernelGGL(k_cvselect, dim3(L, n), dim3(64), 12 * kSelCap, s, P->d_pyr, g.pyr_bytes,
+                     P->d_lv, L, P->d_bm, P->bm_words, P->d_smap, P->d_cand, P->d_pos,
+                     P->cand_total, (int)(P->p.score_type == ORBX_HARRIS_SCORE), P->d_okey,
+                     P->kp_total, P->d_ocount);
+  pr.mark(s, st_sel);
+  rc = launch_blur(g, P->pd, P->d_pyr, P->d_blur, n, s);
+  if (rc) return rc;
+  pr.mark(s, st_blur);
+  KpOff ko{};
+  for (int l = 0; l < L; l++) ko.off[l] = P->lv[l].kp_off;
+  ko.off[L] = P->kp_total;
+  hipLaunchKernelGGL(k_cvdescribe, dim3((P->kp_total + 7) / 8, n), dim3(256), 0, s, P->d_pyr,
+                     g.pyr_bytes, P->d_blur, P->d_lv, L, ko, P->d_okey, P->d_ocount, P->kp_total,
+                     P->d_kps, P->d_desc, P->d_counts);
+  pr.mark(s, st_desc);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "cvorb launch");
+}
+
+// Runs a batch: captured into a hipGraph per (input pointer, batch) unless profiling.
+int plan_run(Plan* P, const uint8_t* d_in, int n) {
+  if (!P || !d_in || n <= 0 || n > P->max_batch) return ORBX_EINVAL;
+  ORBX_HIP(hipSetDevice(P->device));
+  if (P->prof && P->prof->on) return enqueue(P, d_in, n);
+  if (!(P->graph && P->graph_in == d_in && P->graph_n == n)) {
+    if (P->graph) {
+      hipGraphExecDestroy(P->graph);
+      P->graph = nullptr;
+    }
+    hipGraph_t gr;
+    ORBX_HIP(hipStreamBeginCapture(P->stream, hipStreamCaptureModeThreadLocal));
+    Profiler* keep = P->prof;
+    P->prof = nullptr;
+    int rc = enqueue(P, d_in, n);
+    P->prof = keep;
+    hipError_t e = hipStreamEndCapture(P->stream, &gr);
+    if (rc != ORBX_OK) return rc;
+    if (e != hipSuccess) return report_hip(e, "hipStreamEndCapture");
+    e = hipGraphInstantiate(&P->graph, gr, nullptr, nullptr, 0);
+    hipGraphDestroy(gr);
+    if (e != hipSuccess) return report_hip(e, "hipGraphInstantiate");
+    P->graph_in = d_in;
+    P->graph_n = n;
+  }
+  ORBX_HIP(hipGraphLaunch(P->graph, P->stream));
+  return ORBX_OK;
+}
+
+int launch_bf(const uint8_t* d_query, int nq, const uint8_t* d_train, int64_t train_stride,
+              const int* d_tcount, int nprob, int2* d_best, int* d_second, int* d_extremes,
+              hipStream_t s) {
+  if (nq <= 0 || nprob <= 0) return ORBX_OK;
+  hipLaunchKernelGGL(k_bfmatch, dim3((nq + kBfQ - 1) / kBfQ, nprob), dim3(kBfQ), 0, s, d_query,
+                     nq, d_train, train_stride, d_tcount, d_best, d_second, d_extremes);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "k_bfmatch");
+}
+
+int profile_read(Profiler& pr, int32_t cap, char (*names)[32], double* total_ms,
+                 int64_t* launches, int32_t* n_stages) {
+  if (pr.collect() != 0) return ORBX_EDEVICE;
+  const int n = (int)pr.names.size();
+  if (n_stages) *n_stages = n;
+  for (int i = 0; i < n && i < cap; i++) {
+    if (names) {
+      strncpy(names[i], pr.names[i].c_str(), 31);
+      names[i][31] = 0;
+    }
+    if (total_ms) total_ms[i] = pr.ms[i];
+    if (launches) launches[i] = pr.launches[i];
+  }
+  return ORBX_OK;
+}
+
+}  // namespace cvorb
+}  // namespace orbx
+
+using namespace orbx;
+using namespace orbx::cvorb;
+
+struct orbx_cvorb {
+  orbx_cvorb_params params{};
+  int device = 0;
+  Plan* tp = nullptr;  // throughput plan (w, h, max_batch)
+  Plan* dp = nullptr;  // drop-in plan: batch 1, exact capacity, rebuilt on a size change
+  uint8_t* d_img = nullptr;
+  Profiler prof;
+};
+
+struct orbx_marker {
+  Plan* plan = nullptr;
+  int device = 0;
+  uint8_t* d_target = nullptr;
+  int n_target = 0;
+  int2* d_best = nullptr;
+  orbx_dmatch* d_matches = nullptr;
+  uint8_t* d_good = nullptr;
+  int* d_good_count = nullptr;
+  int match_cap = 0;  // n_target capacity of the match buffers
+  Profiler prof;
+};
+
+namespace {
+
+int marker_enqueue(orbx_marker* M, int n) {
+  Plan* P = M->plan;
+  Profiler dummy;
+  Profiler& pr = P->prof ? *P->prof : dummy;
+  const int st_bf = pr.stage("k_bfmatch"), st_good = pr.stage("k_good");
+  hipStream_t s = P->stream;
+  int rc = launch_bf(M->d_target, M->n_target, (const uint8_t*)P->d_desc, P->kp_total,
+                     P->d_counts, n, M->d_best, nullptr, nullptr, s);
+  if (rc) return rc;
+  pr.mark(s, st_bf);
+  hipLaunchKernelGGL(k_good, dim3(n), dim3(64), 0, s, M->d_best, M->n_target, P->d_counts,
+                     M->d_matches, M->d_good, M->d_good_count);
+  pr.mark(s, st_good);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "k_good");
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_cvorb_create(const orbx_cvorb_params* params, int32_t w, int32_t h, int32_t max_batch,
+                      int hip_device, orbx_cvorb** out) {
+  if (!params || !out || w <= 0 || h <= 0 || max_batch <= 0) return ORBX_EINVAL;
+  *out = nullptr;
+  if (!params_supported(*params)) return ORBX_EUNSUPPORTED;
+  orbx_cvorb* o = new (std::nothrow) orbx_cvorb();
+  if (!o) return ORBX_ENOMEM;
+  o->params = *params;
+  o->device = hip_device;
+  int rc = plan_create(*params, w, h, max_batch, hip_device, false, &o->tp);
+  if (rc != ORBX_OK) {
+    delete o;
+    return rc;
+  }
+  o->tp->prof = &o->prof;
+  *out = o;
+  return ORBX_OK;
+}
+
+int orbx_cvorb_destroy(orbx_cvorb* o) {
+  if (!o) return ORBX_OK;
+  plan_destroy(o->tp);
+  plan_destroy(o->dp);
+  if (o->d_img) (void)hipFree(o->d_img);
+  delete o;
+  return ORBX_OK;
+}
+
+int orbx_cvorb_capacity(const orbx_cvorb* o, int32_t* kp_cap) {
+  if (!o || !kp_cap) return ORBX_EINVAL;
+  *kp_cap = o->tp->kp_total;
+  return ORBX_OK;
+}
+
+int orbx_cvorb_detect(orbx_cvorb* o, const uint8_t* img, int32_t w, int32_t h, int64_t stride,
+                      orbx_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out) {
+  if (!o || !n_out) return ORBX_EINVAL;
+  if (w <= 0 || h <= 0) {  // orb.cpp: `if (_image.empty()) return;`
+    *n_out = -1;
+    return ORBX_OK;
+  }
+  if (!img || stride < w || cap < 0 || (cap > 0 && (!kps || !desc))) return ORBX_EINVAL;
+  ORBX_HIP(hipSetDevice(o->device));
+  if (!o->dp || o->dp->w != w || o->dp->h != h) {
+    plan_destroy(o->dp);
+    o->dp = nullptr;
+    if (o->d_img) (void)hipFree(o->d_img);
+    o->d_img = nullptr;
+    int rc = plan_create(o->params, w, h, 1, o->device, true, &o->dp);
+    if (rc != ORBX_OK) return rc;
+    ORBX_HIP(hipMalloc(&o->d_img, (size_t)w * h));
+  }
+  Plan* P = o->dp;
+  hipStream_t s = P->stream;
+  ORBX_HIP(hipMemcpy2DAsync(o->d_img, w, img, stride, w, h, hipMemcpyHostToDevice, s));
+  int rc = plan_run(P, o->d_img, 1);
+  if (rc != ORBX_OK) return rc;
+  int32_t n = 0;
+  ORBX_HIP(hipMemcpyAsync(&n, P->d_counts, 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  if (n < 0) return ORBX_ECAPACITY;  // cannot happen with exact capacity
+  *n_out = n;
+  if (n > cap) return ORBX_ECAPACITY;
+  if (n > 0) {
+    ORBX_HIP(hipMemcpyAsync(kps, P->d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(desc, P->d_desc, (size_t)32 * n, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+  }
+  return ORBX_OK;
+}
+
+int orbx_cvorb_run(orbx_cvorb* o, const uint8_t* d_imgs, int32_t n) {
+  if (!o) return ORBX_EINVAL;
+  return plan_run(o->tp, d_imgs, n);
+}
+
+int orbx_cvorb_outputs(orbx_cvorb* o, orbx_keypoint** d_kps, uint8_t** d_desc,
+                       int32_t** d_counts) {
+  if (!o) return ORBX_EINVAL;
+  if (d_kps) *d_kps = o->tp->d_kps;
+  if (d_desc) *d_desc = o->tp->d_desc;
+  if (d_counts) *d_counts = o->tp->d_counts;
+  return ORBX_OK;
+}
+
+int orbx_cvorb_sync(orbx_cvorb* o) {
+  if (!o) return ORBX_EINVAL;
+  ORBX_HIP(hipStreamSynchronize(o->tp->stream));
+  return ORBX_OK;
+}
+
+void* orbx_cvorb_stream(orbx_cvorb* o) { return o ? (void*)o->tp->stream : nullptr; }
+
+int orbx_bf_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_t nt,
+                  orbx_dmatch* out, int32_t* n_out) {
+  if (!n_out || nq < 0 || nt < 0) return ORBX_EINVAL;
+  *n_out = 0;
+  if (nq == 0 || nt == 0) return ORBX_OK;  // knnMatch returns early on an empty side
+  if (!query || !train || !out) return ORBX_EINVAL;
+  Stager st;
+  const size_t oq = st.add(query, (size_t)nq * 32), ot = st.add(train, (size_t)nt * 32);
+  const size_t oc = st.add(&nt, 4), ob = st.add(nullptr, (size_t)nq * 8);
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), ob, hipMemcpyHostToDevice, s));
+  rc = launch_bf(dptr<uint8_t>(base, oq), nq, dptr<uint8_t>(base, ot), 0, dptr<int>(base, oc), 1,
+                 dptr<int2>(base, ob), nullptr, nullptr, s);
+  if (rc) return rc;
+  std::vector<int2> best(nq);
+  ORBX_HIP(hipMemcpyAsync(best.data(), base + ob, (size_t)nq * 8, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  for (int i = 0; i < nq; i++) out[i] = {i, best[i].x, 0, (float)best[i].y};
+  *n_out = nq;
+  return ORBX_OK;
+}
+
+int orbx_good_matches(const orbx_dmatch* m, int32_t n, orbx_dmatch* good, int32_t* n_good,
+                      double* min_dist, double* max_dist) {
+  if (n < 0 || !n_good || (n > 0 && (!m || !good))) return ORBX_EINVAL;
+  double mx = 0, mn = 100;  // Marker.cc:115-120
+  for (int i = 0; i < n; i++) {
+    const double d = m[i].distance;
+    if (d < mn) mn = d;
+    if (d > mx) mx = d;
+  }
+  int k = 0;
+  for (int i = 0; i < n; i++)
+    if (m[i].distance < 0.5 * mx) good[k++] = m[i];
+  *n_good = k;
+  if (min_dist) *min_dist = mn;
+  if (max_dist) *max_dist = mx;
+  return ORBX_OK;
+}
+
+int orbx_nn_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_t nt,
+                  double ratio, int32_t max_dist, orbx_dmatch* out, int32_t* n_out,
+                  int32_t* min_d, int32_t* max_d) {
+  if (!n_out || nq < 0 || nt < 0) return ORBX_EINVAL;
+  *n_out = 0;
+  if (min_d) *min_d = 100;  // the reference's globals start at minD = 100, maxD = 0
+  if (max_d) *max_d = 0;
+  if (nq == 0) return ORBX_OK;
+  if (!query || !out || (nt > 0 && !train)) return ORBX_EINVAL;
+  std::vector<int2> best(nq);
+  std::vector<int> second(nq);
+  int ext[2] = {INT_MAX, 0};
+  if (nt > 0) {
+    Stager st;
+    const size_t oq = st.add(query, (size_t)nq * 32), ot = st.add(train, (size_t)nt * 32);
+    const size_t oc = st.add(&nt, 4), oe = st.add(ext, 8);
+    const size_t ob = st.add(nullptr, (size_t)nq * 8), os = st.add(nullptr, (size_t)nq * 4);
+    int rc = tls_ws.reserve(st.host.size());
+    if (rc) return rc;
+    char* base = tls_ws.d;
+    hipStream_t s = tls_ws.stream;
+    ORBX_HIP(hipMemcpyAsync(base, st.host.data(), ob, hipMemcpyHostToDevice, s));
+    rc = launch_bf(dptr<uint8_t>(base, oq), nq, dptr<uint8_t>(base, ot), 0, dptr<int>(base, oc),
+                   1, dptr<int2>(base, ob), dptr<int>(base, os), dptr<int>(base, oe), s);
+    if (rc) return rc;
+    ORBX_HIP(hipMemcpyAsync(best.data(), base + ob, (size_t)nq * 8, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(second.data(), base + os, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(ext, base + oe, 8, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+  } else {
+    for (int i = 0; i < nq; i++) best[i] = make_int2(-1, INT_MAX), second[i] = INT_MAX;
+  }
+  // AR-1.3/src/ORBMatcher.cpp:96-101 (unsigned arithmetic as the reference)
+  int k = 0;
+  for (int i = 0; i < nq; i++) {
+    const unsigned int mind = (unsigned)best[i].y, secd = (unsigned)second[i];
+    const bool ratio_ok = ratio <= 0 || mind <= (unsigned int)(secd * ratio);
+    if (ratio_ok && mind <= (unsigned)max_dist) out[k++] = {i, best[i].x, 0, (float)mind};
+  }
+  *n_out = k;
+  if (nt > 0) {
+    if (min_d) *min_d = std::min(100, ext[0]);
+    if (max_d) *max_d = ext[1];
+  }
+  return ORBX_OK;
+}
+
+int orbx_debug_cvorb_cossin(const float* deg, int64_t n, float* c, float* s) {
+  if (n < 0 || (n > 0 && (!deg || !c || !s))) return ORBX_EINVAL;
+  if (n == 0) return ORBX_OK;
+  float *d_in = nullptr, *d_c = nullptr, *d_s = nullptr;
+  ORBX_HIP(hipMalloc(&d_in, 4 * (size_t)n));
+  hipError_t e = hipMalloc(&d_c, 4 * (size_t)n);
+  if (e == hipSuccess) e = hipMalloc(&d_s, 4 * (size_t)n);
+  if (e == hipSuccess) e = hipMemcpy(d_in, deg, 4 * (size_t)n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_debug_cossin, dim3(2048), dim3(256), 0, 0, d_in, n, d_c, d_s);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(c, d_c, 4 * (size_t)n, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(s, d_s, 4 * (size_t)n, hipMemcpyDeviceToHost);
+  (void)hipFree(d_in);
+  if (d_c) (void)hipFree(d_c);
+  if (d_s) (void)hipFree(d_s);
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "orbx_debug_cvorb_cossin");
+}
+
+int orbx_debug_retain_best(float* resp, uint32_t* ids, int32_t n, int32_t n_points,
+                           int32_t force_global, int32_t* n_out) {
+  if (n < 0 || !n_out || (n > 0 && (!resp || !ids))) return ORBX_EINVAL;
+  std::vector<CvKey> v(std::max(n, 1));
+  for (int i = 0; i < n; i++) v[i] = {resp[i], ids[i]};
+  CvKey* d_a = nullptr;
+  uint32_t* d_pos = nullptr;
+  int* d_n = nullptr;
+  ORBX_HIP(hipMalloc(&d_a, sizeof(CvKey) * v.size()));
+  hipError_t e = hipMalloc(&d_pos, 4 * (v.size() + 2));
+  if (e == hipSuccess) e = hipMalloc(&d_n, 4);
+  if (e == hipSuccess) e = hipMemcpy(d_a, v.data(), sizeof(CvKey) * v.size(), hipMemcpyHostToDevice);
+  const int use_lds = !force_global && n <= kSelCap;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_debug_retain,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 12 * kSelCap);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_debug_retain, dim3(1), dim3(64), 12 * kSelCap, 0, d_a, n, n_points,
+                       d_pos, use_lds, d_n);
+    e = hipGetLastError();
+  }
+  int m = 0;
+  if (e == hipSuccess) e = hipMemcpy(&m, d_n, 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(v.data(), d_a, sizeof(CvKey) * v.size(), hipMemcpyDeviceToHost);
+  (void)hipFree(d_a);
+  if (d_pos) (void)hipFree(d_pos);
+  if (d_n) (void)hipFree(d_n);
+  if (e != hipSuccess) return report_hip(e, "orbx_debug_retain_best");
+  for (int i = 0; i < m; i++) resp[i] = v[i].r, ids[i] = v[i].k;
+  *n_out = m;
+  return ORBX_OK;
+}
+
+int orbx_marker_create(const orbx_cvorb_params* params, int32_t w, int32_t h, int32_t max_batch,
+                       int hip_device, orbx_marker** out) {
+  if (!params || !out || w <= 0 || h <= 0 || max_batch <= 0) return ORBX_EINVAL;
+  *out = nullptr;
+  orbx_marker* M = new (std::nothrow) orbx_marker();
+  if (!M) return ORBX_ENOMEM;
+  M->device = hip_device;
+  int rc = plan_create(*params, w, h, max_batch, hip_device, false, &M->plan);
+  if (rc != ORBX_OK) {
+    delete M;
+    return rc;
+  }
+  M->plan->prof = &M->prof;
+  if (hipMalloc(&M->d_good_count, 4 * (size_t)max_batch) != hipSuccess) {
+    orbx_marker_destroy(M);
+    return ORBX_ENOMEM;
+  }
+  *out = M;
+  return ORBX_OK;
+}
+
+int orbx_marker_destroy(orbx_marker* M) {
+  if (!M) return ORBX_OK;
+  plan_destroy(M->plan);
+  void* bufs[] = {M->d_target, M->d_best, M->d_matches, M->d_good, M->d_good_count};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  delete M;
+  return ORBX_OK;
+}
+
+// Marker::setTargetImage's descriptors (mDescriptors1), n x 32 host bytes.
+int orbx_marker_set_target(orbx_marker* M, const uint8_t* desc, int32_t n) {
+  if (!M || n < 0 || (n > 0 && !desc)) return ORBX_EINVAL;
+  ORBX_HIP(hipSetDevice(M->device));
+  ORBX_HIP(hipStreamSynchronize(M->plan->stream));
+  if (n > M->match_cap) {
+    void* bufs[] = {M->d_target, M->d_best, M->d_matches, M->d_good};
+    for (void* b : bufs)
+      if (b) (void)hipFree(b);
+    M->d_target = nullptr;
+    M->d_best = nullptr;
+    M->d_matches = nullptr;
+    M->d_good = nullptr;
+    M->match_cap = 0;
+    const size_t B = (size_t)M->plan->max_batch;
+    if (hipMalloc(&M->d_target, (size_t)n * 32) != hipSuccess ||
+        hipMalloc(&M->d_best, B * n * sizeof(int2)) != hipSuccess ||
+        hipMalloc(&M->d_matches, B * n * sizeof(orbx_dmatch)) != hipSuccess ||
+        hipMalloc(&M->d_good, B * n) != hipSuccess)
+      return ORBX_ENOMEM;
+    M->match_cap = n;
+  }
+  if (n > 0) ORBX_HIP(hipMemcpy(M->d_target, desc, (size_t)n * 32, hipMemcpyHostToDevice));
+  M->n_target = n;
+  return ORBX_OK;
+}
+
+int orbx_marker_run(orbx_marker* M, const uint8_t* d_imgs, int32_t n) {
+  if (!M) return ORBX_EINVAL;
+  Plan* P = M->plan;
+  if (!d_imgs || n <= 0 || n > P->max_batch) return ORBX_EINVAL;
+  ORBX_HIP(hipSetDevice(M->device));
+  // the extraction graph (one per input pointer and batch), then the two matcher launches
+  int rc = plan_run(P, d_imgs, n);
+  if (rc) return rc;
+  return marker_enqueue(M, n);
+}
+
+int orbx_marker_sync(orbx_marker* M) {
+  if (!M) return ORBX_EINVAL;
+  ORBX_HIP(hipStreamSynchronize(M->plan->stream));
+  return ORBX_OK;
+}
+
+int orbx_marker_results(orbx_marker* M, int32_t n, int32_t* kp_counts, int32_t* good_counts) {
+  if (!M || n < 0 || n > M->plan->max_batch) return ORBX_EINVAL;
+  hipStream_t s = M->plan->stream;
+  if (kp_counts)
+    ORBX_HIP(hipMemcpyAsync(kp_counts, M->plan->d_counts, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  if (good_counts)
+    ORBX_HIP(hipMemcpyAsync(good_counts, M->d_good_count, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  return ORBX_OK;
+}
+
+int orbx_marker_outputs(orbx_marker* M, orbx_dmatch** d_matches, uint8_t** d_good,
+                        orbx_keypoint** d_kps, uint8_t** d_desc) {
+  if (!M) return ORBX_EINVAL;
+  if (d_matches) *d_matches = M->d_matches;
+  if (d_good) *d_good = M->d_good;
+  if (d_kps) *d_kps = M->plan->d_kps;
+  if (d_desc) *d_desc = M->plan->d_desc;
+  return ORBX_OK;
+}
+
+void* orbx_marker_stream(orbx_marker* M) { return M ? (void*)M->plan->stream : nullptr; }
+
+int orbx_marker_profile(orbx_marker* M, int32_t enable) {
+  if (!M) return ORBX_EINVAL;
+  M->prof.on = enable != 0;
+  M->prof.reset();
+  return ORBX_OK;
+}
+
+int orbx_marker_profile_read(orbx_marker* M, int32_t cap, char (*names)[32], double* total_ms,
+                             int64_t* launches, int32_t* n_stages) {
+  if (!M) return ORBX_EINVAL;
+  return profile_read(M->prof, cap, names, total_ms, launches, n_stages);
+}
+
+}  // extern "C"

@@ -442,49 +442,7 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
 // cornerScore<16>; V = score+1 clamped to [0,255] so "corner at t" is V > t.
 constexpr int kCellMax = 66;  // wCell, hCell < 60 (+6)
 
-__device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, int y) {
-  const uint8_t* c = s + y * stride + x;
-  const int v = c[0];
-  int d[16];
-  d[0] = v - c[3 * stride];
-  d[1] = v - c[3 * stride + 1];
-  d[2] = v - c[2 * stride + 2];
-  d[3] = v - c[stride + 3];
-  d[4] = v - c[3];
-  d[5] = v - c[-stride + 3];
-  d[6] = v - c[-2 * stride + 2];
-  d[7] = v - c[-3 * stride + 1];
-  d[8] = v - c[-3 * stride];
-  d[9] = v - c[-3 * stride - 1];
-  d[10] = v - c[-2 * stride - 2];
-  d[11] = v - c[-stride - 3];
-  d[12] = v - c[-3];
-  d[13] = v - c[stride - 3];
-  d[14] = v - c[2 * stride - 2];
-  d[15] = v - c[3 * stride - 1];
-  // sliding min/max over 9 consecutive circle points (wrap-around)
-  int mn2[16], mx2[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn2[k] = min(d[k], d[(k + 1) & 15]);
-    mx2[k] = max(d[k], d[(k + 1) & 15]);
-  }
-  int mn4[16], mx4[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-  }
-  int q0 = -1000, q1 = 1000;
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int a = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-    const int b = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-    q0 = max(q0, a);
-    q1 = min(q1, b);
-  }
-  return max(q0, -q1) - 1;
-}
+// fast_score: orbx_internal.h
 
 // Even-point pretest for one pixel per lane (row stride RS of the staged bytes; c = top-left
 // byte of the pixel's 7x7 neighbourhood): lane mask of the pixels in ok that may be corners at
@@ -1496,6 +1454,77 @@ int orbx::launch_fill_u32(uint32_t* p, size_t n, uint32_t v, hipStream_t s) {
   return ORBX_OK;
 }
 
+// Blur tiles over every level (the blurred pyramid has the pyramid's pitched layout).
+static std::vector<BlurTile> blur_tiles(const Geometry& g) {
+  std::vector<BlurTile> tiles;
+  for (int l = 0; l < g.nlevels; l++) {
+    const LevelGeom& G = g.lv[l];
+    for (int ty = 0; ty * kBlurTH < G.h; ty++)
+      for (int tx = 0; tx * kBlurTW < G.w; tx++) {
+        const int X0 = tx * kBlurTW, Y0 = ty * kBlurTH;
+        const bool interior = X0 >= 4 && X0 + kBlurTW + 4 <= G.w && Y0 >= 3 &&
+                              Y0 + kBlurTH + 3 <= G.h;
+        tiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, (int16_t)interior});
+      }
+  }
+  return tiles;
+}
+
+int orbx::pyr_dev_create(const Geometry& g, PyrDev* d) {
+  *d = PyrDev{};
+  const std::vector<BlurTile> tiles = blur_tiles(g);
+  d->ntiles = (int)tiles.size();
+  BlurTile* dt = nullptr;
+  if (dalloc(&d->d_lv, g.nlevels) || dalloc(&d->d_xtap, g.xtap.size() / 2 + 1) ||
+      dalloc(&d->d_ytap, g.ytap.size() / 2 + 1) || dalloc(&d->d_bands, g.bands.size()) ||
+      dalloc(&dt, tiles.size())) {
+    d->d_tiles = dt;
+    pyr_dev_destroy(d);
+    return ORBX_ENOMEM;
+  }
+  d->d_tiles = dt;
+  auto up = [&](void* p, const void* h, size_t bytes) {
+    return bytes ? hipMemcpy(p, h, bytes, hipMemcpyHostToDevice) : hipSuccess;
+  };
+  if (up(d->d_lv, g.lv, sizeof(LevelGeom) * g.nlevels) ||
+      up(d->d_xtap, g.xtap.data(), 4 * g.xtap.size()) ||
+      up(d->d_ytap, g.ytap.data(), 4 * g.ytap.size()) ||
+      up(d->d_bands, g.bands.data(), sizeof(PyrBand) * g.bands.size()) ||
+      up(dt, tiles.data(), sizeof(BlurTile) * tiles.size())) {
+    pyr_dev_destroy(d);
+    return ORBX_EDEVICE;
+  }
+  return ORBX_OK;
+}
+
+void orbx::pyr_dev_destroy(PyrDev* d) {
+  if (d->d_lv) (void)hipFree(d->d_lv);
+  if (d->d_xtap) (void)hipFree(d->d_xtap);
+  if (d->d_ytap) (void)hipFree(d->d_ytap);
+  if (d->d_bands) (void)hipFree(d->d_bands);
+  if (d->d_tiles) (void)hipFree(d->d_tiles);
+  *d = PyrDev{};
+}
+
+int orbx::launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint8_t* d_pyr,
+                         int n, hipStream_t s) {
+  for (const PyrStage& st : g.pyr_stages)
+    hipLaunchKernelGGL(k_pyramid, dim3(st.nbands, n), dim3(kPyNT), st.smem, s, d_in, d_pyr,
+                       g.pyr_bytes, d.d_lv, st.l0, st.l1, d.d_bands + st.band0, d.d_xtap,
+                       d.d_ytap, st.buf_b);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_pyramid");
+}
+
+int orbx::launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur,
+                      int n, hipStream_t s) {
+  if (d.ntiles > 0)
+    hipLaunchKernelGGL(k_blur, dim3(d.ntiles, n), dim3(256), 0, s, d_pyr, g.pyr_bytes, d_blur,
+                       d.d_lv, (const BlurTile*)d.d_tiles);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_blur");
+}
+
 namespace {
 
 int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
@@ -1584,18 +1613,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     return fail(ORBX_EDEVICE);
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)));
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), g.umax, sizeof(g.umax)));
-  // blur tiles over every level (the blurred pyramid has the pyramid's pitched layout)
-  std::vector<BlurTile> tiles;
-  for (int l = 0; l < g.nlevels; l++) {
-    const LevelGeom& G = g.lv[l];
-    for (int ty = 0; ty * kBlurTH < G.h; ty++)
-      for (int tx = 0; tx * kBlurTW < G.w; tx++) {
-        const int X0 = tx * kBlurTW, Y0 = ty * kBlurTH;
-        const bool interior = X0 >= 4 && X0 + kBlurTW + 4 <= G.w && Y0 >= 3 &&
-                              Y0 + kBlurTH + 3 <= G.h;
-        tiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, (int16_t)interior});
-      }
-  }
+  const std::vector<BlurTile> tiles = blur_tiles(g);
   for (const CellGeom& c : g.cells)
     if (c.x1 - c.x0 > kCellMax || c.y1 - c.y0 > kCellMax) return fail(ORBX_EUNSUPPORTED);
   P->ntiles = (int)tiles.size();

@@ -115,30 +115,19 @@ static bool resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom
   return ok;
 }
 
-int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string* why) {
-  if (p.nlevels < 1 || p.nlevels > kMaxLevels || p.nfeatures < 0 || !(p.scale_factor > 0)) {
-    if (why) *why = "bad params";
-    return ORBX_EINVAL;
-  }
-  build_tables(p, g);
-  g->w = w;
-  g->h = h;
-  g->ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
-  g->min_th = std::min(std::max(p.min_th_fast, 0), 255);
-  g->cells.clear();
-  g->bm_words = 0;
+// The pyramid part of a plan for the level sizes already in g->lv[0 .. g->nlevels): cv::resize
+// tables of every level >= 1, pitches and offsets in the pyramid block, k_pyramid stages.
+int build_pyramid(Geometry* g, std::string* why) {
   g->xofs.clear();
   g->yofs.clear();
   g->xa.clear();
   g->yb.clear();
+  g->xtap.clear();
+  g->ytap.clear();
+  const int nl = g->nlevels;
   int64_t pyr = 0;
-  int cand = 0, kp = 0, ncmax = 0;
-  for (int l = 0; l < p.nlevels; l++) {
+  for (int l = 0; l < nl; l++) {
     LevelGeom& L = g->lv[l];
-    L = LevelGeom{};
-    // ComputePyramid (ORBextractor.cc:1049-1051)
-    L.w = cv_round((float)w * g->inv_scale[l]);
-    L.h = cv_round((float)h * g->inv_scale[l]);
     if (L.w < 1 || L.h < 1) {
       if (why) *why = "empty pyramid level";
       return ORBX_EUNSUPPORTED;
@@ -162,6 +151,97 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     L.pyr_off = pyr;
     pyr += ((int64_t)L.pitch * L.h + 255) / 256 * 256;
     L.bxs = (L.w / 4) * 4;
+  }
+  g->pyr_bytes = std::max<int64_t>(pyr, 256);
+  // k_pyramid stages: levels 1..kPyStage0, then kPyStageN at a time.  In a stage, band b
+  // owns rows [b*h_l/nb, (b+1)*h_l/nb) of every level and computes, going down from the
+  // stage's last level, the rows the next level's rows need as well (rows shared by two bands
+  // are computed by both, identically; only the owner stores them).  Its level l rows stay in
+  // LDS for level l+1: even levels in buffer A, odd ones in B.  The recomputed cone grows by
+  // ~2 rows per level below the top, so stages stay short.
+  g->pyr_stages.clear();
+  g->bands.clear();
+  for (int l0 = 1; l0 < nl;) {
+    PyrStage st;
+    st.l0 = l0;
+    st.l1 = std::min(nl - 1, l0 + (l0 == 1 ? kPyStage0 : kPyStageN) - 1);
+    const int hs = g->lv[l0 - 1].h;
+    std::vector<PyrBand> bands;
+    for (int nb = std::max(1, hs / kPyBandH);; nb++) {
+      bands.assign(nb, PyrBand{});
+      int need[2] = {0, 0};
+      for (int b = 0; b < nb; b++) {
+        PyrBand& B = bands[b];
+        for (int l = st.l0 - 1; l <= st.l1; l++) {
+          B.own_lo[l] = B.lo[l] = (int)((int64_t)b * g->lv[l].h / nb);
+          B.own_hi[l] = B.hi[l] = (int)((int64_t)(b + 1) * g->lv[l].h / nb);
+        }
+        for (int l = st.l1; l >= st.l0; l--) {
+          const LevelGeom& D = g->lv[l];
+          const LevelGeom& S = g->lv[l - 1];
+          if (B.hi[l] <= B.lo[l]) continue;
+          const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
+          const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
+          B.lo[l - 1] = std::min(B.lo[l - 1], slo);
+          B.hi[l - 1] = std::max(B.hi[l - 1], shi);
+        }
+        for (int l = st.l0 - 1; l <= st.l1; l++)
+          need[l & 1] = std::max(need[l & 1], std::max(0, B.hi[l] - B.lo[l]) * g->lv[l].pitch);
+      }
+      st.buf_b = (need[0] + 15) & ~15;
+      st.smem = st.buf_b + need[1];
+      if (st.smem <= kPyMaxSmem) break;
+      if (nb >= hs) {
+        if (why) *why = "image too wide for the pyramid bands";
+        return ORBX_EUNSUPPORTED;
+      }
+    }
+    st.band0 = (int)g->bands.size();
+    st.nbands = (int)bands.size();
+    g->bands.insert(g->bands.end(), bands.begin(), bands.end());
+    g->pyr_stages.push_back(st);
+    l0 = st.l1 + 1;
+  }
+  if (nl == 1) {  // level 0 alone: one copy stage
+    PyrStage st{1, 0, 0, 0, 0, 0};
+    const int nb = std::max(1, g->lv[0].h / kPyBandH);
+    for (int b = 0; b < nb; b++) {
+      PyrBand B{};
+      B.own_lo[0] = B.lo[0] = (int)((int64_t)b * g->lv[0].h / nb);
+      B.own_hi[0] = B.hi[0] = (int)((int64_t)(b + 1) * g->lv[0].h / nb);
+      g->bands.push_back(B);
+    }
+    st.nbands = nb;
+    st.smem = std::max(16, (g->lv[0].h / nb + 1) * g->lv[0].pitch);
+    g->pyr_stages.push_back(st);
+  }
+  return ORBX_OK;
+}
+
+int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string* why) {
+  if (p.nlevels < 1 || p.nlevels > kMaxLevels || p.nfeatures < 0 || !(p.scale_factor > 0)) {
+    if (why) *why = "bad params";
+    return ORBX_EINVAL;
+  }
+  build_tables(p, g);
+  g->w = w;
+  g->h = h;
+  g->ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
+  g->min_th = std::min(std::max(p.min_th_fast, 0), 255);
+  g->cells.clear();
+  g->bm_words = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelGeom& L = g->lv[l];
+    L = LevelGeom{};
+    // ComputePyramid (ORBextractor.cc:1049-1051)
+    L.w = cv_round((float)w * g->inv_scale[l]);
+    L.h = cv_round((float)h * g->inv_scale[l]);
+  }
+  int rc = build_pyramid(g, why);
+  if (rc != ORBX_OK) return rc;
+  int cand = 0, kp = 0, ncmax = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelGeom& L = g->lv[l];
     L.scale = g->scale[l];
     L.inv_scale = g->inv_scale[l];
     L.size = (float)(int)(kPatch * g->scale[l]);
@@ -236,73 +316,10 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     kp += L.kp_cap;
     g->node_cap_max = std::max(g->node_cap_max, L.node_cap);
   }
-  // k_pyramid stages: levels 1..kPyStage0, then kPyStageN at a time.  In a stage, band b
-  // owns rows [b*h_l/nb, (b+1)*h_l/nb) of every level and computes, going down from the
-  // stage's last level, the rows the next level's rows need as well (rows shared by two bands
-  // are computed by both, identically; only the owner stores them).  Its level l rows stay in
-  // LDS for level l+1: even levels in buffer A, odd ones in B.  The recomputed cone grows by
-  // ~2 rows per level below the top, so stages stay short.
-  g->pyr_stages.clear();
-  g->bands.clear();
-  for (int l0 = 1; l0 < p.nlevels;) {
-    PyrStage st;
-    st.l0 = l0;
-    st.l1 = std::min(p.nlevels - 1, l0 + (l0 == 1 ? kPyStage0 : kPyStageN) - 1);
-    const int hs = g->lv[l0 - 1].h;
-    std::vector<PyrBand> bands;
-    for (int nb = std::max(1, hs / kPyBandH);; nb++) {
-      bands.assign(nb, PyrBand{});
-      int need[2] = {0, 0};
-      for (int b = 0; b < nb; b++) {
-        PyrBand& B = bands[b];
-        for (int l = st.l0 - 1; l <= st.l1; l++) {
-          B.own_lo[l] = B.lo[l] = (int)((int64_t)b * g->lv[l].h / nb);
-          B.own_hi[l] = B.hi[l] = (int)((int64_t)(b + 1) * g->lv[l].h / nb);
-        }
-        for (int l = st.l1; l >= st.l0; l--) {
-          const LevelGeom& D = g->lv[l];
-          const LevelGeom& S = g->lv[l - 1];
-          if (B.hi[l] <= B.lo[l]) continue;
-          const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
-          const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
-          B.lo[l - 1] = std::min(B.lo[l - 1], slo);
-          B.hi[l - 1] = std::max(B.hi[l - 1], shi);
-        }
-        for (int l = st.l0 - 1; l <= st.l1; l++)
-          need[l & 1] = std::max(need[l & 1], std::max(0, B.hi[l] - B.lo[l]) * g->lv[l].pitch);
-      }
-      st.buf_b = (need[0] + 15) & ~15;
-      st.smem = st.buf_b + need[1];
-      if (st.smem <= kPyMaxSmem) break;
-      if (nb >= hs) {
-        if (why) *why = "image too wide for the pyramid bands";
-        return ORBX_EUNSUPPORTED;
-      }
-    }
-    st.band0 = (int)g->bands.size();
-    st.nbands = (int)bands.size();
-    g->bands.insert(g->bands.end(), bands.begin(), bands.end());
-    g->pyr_stages.push_back(st);
-    l0 = st.l1 + 1;
-  }
-  if (p.nlevels == 1) {  // level 0 alone: one copy stage
-    PyrStage st{1, 0, 0, 0, 0, 0};
-    const int nb = std::max(1, g->lv[0].h / kPyBandH);
-    for (int b = 0; b < nb; b++) {
-      PyrBand B{};
-      B.own_lo[0] = B.lo[0] = (int)((int64_t)b * g->lv[0].h / nb);
-      B.own_hi[0] = B.hi[0] = (int)((int64_t)(b + 1) * g->lv[0].h / nb);
-      g->bands.push_back(B);
-    }
-    st.nbands = nb;
-    st.smem = std::max(16, (g->lv[0].h / nb + 1) * g->lv[0].pitch);
-    g->pyr_stages.push_back(st);
-  }
   if (cand >= (1 << 24)) {
     if (why) *why = "candidate capacity exceeds 2^24";
     return ORBX_EUNSUPPORTED;
   }
-  g->pyr_bytes = std::max<int64_t>(pyr, 256);
   g->cand_total = cand;
   g->kp_total = kp;
   (void)ncmax;

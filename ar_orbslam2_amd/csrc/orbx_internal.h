@@ -123,6 +123,71 @@ int launch_fill_u32(uint32_t* p, size_t n, uint32_t v, hipStream_t s);
 int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string* why);
 // Tables only (no image size): scale factors, sigma2, features per level, umax.
 void build_tables(const orbx_params& p, Geometry* g);
+// The pyramid part of a Geometry for the level sizes already in lv[0 .. nlevels).w / h:
+// cv::resize tables, pitches, offsets and k_pyramid stages (shared with the cv::ORB plan).
+int build_pyramid(Geometry* g, std::string* why);
+
+// Device tables of k_pyramid / k_blur for one Geometry (orbx_extract.hip), and their launches:
+// the pitched pyramid of n dense h x w input images, and its GaussianBlur 7x7 sigma 2 copy.
+struct PyrDev {
+  LevelGeom* d_lv = nullptr;
+  int2 *d_xtap = nullptr, *d_ytap = nullptr;
+  PyrBand* d_bands = nullptr;
+  void* d_tiles = nullptr;  // BlurTile[ntiles]
+  int ntiles = 0;
+};
+int pyr_dev_create(const Geometry& g, PyrDev* d);
+void pyr_dev_destroy(PyrDev* d);
+int launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint8_t* d_pyr, int n,
+                   hipStream_t s);
+int launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur, int n,
+                hipStream_t s);
+
+// OpenCV 2.4 cornerScore<16> at (x, y) of a u8 image with row stride `stride`:
+// the pixel is a FAST-9/16 corner at threshold t iff the score is >= t.
+__device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, int y) {
+  const uint8_t* c = s + y * stride + x;
+  const int v = c[0];
+  int d[16];
+  d[0] = v - c[3 * stride];
+  d[1] = v - c[3 * stride + 1];
+  d[2] = v - c[2 * stride + 2];
+  d[3] = v - c[stride + 3];
+  d[4] = v - c[3];
+  d[5] = v - c[-stride + 3];
+  d[6] = v - c[-2 * stride + 2];
+  d[7] = v - c[-3 * stride + 1];
+  d[8] = v - c[-3 * stride];
+  d[9] = v - c[-3 * stride - 1];
+  d[10] = v - c[-2 * stride - 2];
+  d[11] = v - c[-stride - 3];
+  d[12] = v - c[-3];
+  d[13] = v - c[stride - 3];
+  d[14] = v - c[2 * stride - 2];
+  d[15] = v - c[3 * stride - 1];
+  // sliding min/max over 9 consecutive circle points (wrap-around)
+  int mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn2[k] = min(d[k], d[(k + 1) & 15]);
+    mx2[k] = max(d[k], d[(k + 1) & 15]);
+  }
+  int mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+  }
+  int q0 = -1000, q1 = 1000;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int a = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+    const int b = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+    q0 = max(q0, a);
+    q1 = min(q1, b);
+  }
+  return max(q0, -q1) - 1;
+}
 
 // Stage timing with HIP events recorded on the launching stream between kernels.  Marks are
 // only read back in collect(), so profiling adds no host synchronisation to the timed loop.

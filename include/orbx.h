@@ -350,7 +350,8 @@ int orbx_epipole(const float R2w[9], const float t2w[3], const float Cw[3], floa
  * int WTA_K = 2, int scoreType = ORB::HARRIS_SCORE, int patchSize = 31).  Marker uses the
  * defaults (Marker.cc:83, 107); AR-1.3's ORBMatcher uses (300, 1.2f, 8, 31, 0, 2, HARRIS, 31)
  * (AR-1.3/src/ORBMatcher.cpp:121-122).  Implemented: firstLevel 0, WTA_K 2, patchSize 31,
- * edgeThreshold >= 16; anything else returns ORBX_EUNSUPPORTED. */
+ * edgeThreshold >= 18 (the 37 x 37 descriptor window stays inside the level); anything else
+ * returns ORBX_EUNSUPPORTED. */
 #define ORBX_HARRIS_SCORE 0
 #define ORBX_FAST_SCORE 1
 typedef struct {
@@ -428,6 +429,15 @@ void* orbx_marker_stream(orbx_marker* mk);
 int orbx_marker_profile(orbx_marker* mk, int32_t enable);
 int orbx_marker_profile_read(orbx_marker* mk, int32_t cap, char (*names)[32], double* total_ms,
                              int64_t* launches, int32_t* n_stages);
+
+/* ------------------------------------------------------------------ test hooks (not product API) */
+/* The device computeOrbDescriptor rotation (float)cos/sin((double)(deg * (float)(CV_PI/180.f)))
+ * for n host angles; and KeyPointsFilter::retainBest (orb.cpp's nth_element + partition) run by
+ * the k_cvselect wave routine on one host array (in LDS when n <= 4096 unless force_global),
+ * resp/ids rewritten in the retained order.  Used by tests/test_cvorb_gpu.py. */
+int orbx_debug_cvorb_cossin(const float* deg, int64_t n, float* c, float* s);
+int orbx_debug_retain_best(float* resp, uint32_t* ids, int32_t n, int32_t n_points,
+                           int32_t force_global, int32_t* n_out);
 
 #ifdef __cplusplus
 }

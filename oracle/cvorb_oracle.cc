@@ -31,6 +31,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../include/orbx_pattern.h"
@@ -296,7 +297,7 @@ Levels cvorb_levels(const orbx_cvorb_params& p, int cols, int rows) {
 
 bool supported(const orbx_cvorb_params& p) {
   return p.nlevels >= 1 && p.nlevels <= 16 && p.first_level == 0 && p.wta_k == 2 &&
-         p.patch_size == 31 && p.edge_threshold >= 16 && p.scale_factor > 0 &&
+         p.patch_size == 31 && p.edge_threshold >= 18 && p.scale_factor > 0 &&
          p.nfeatures >= 0 && (p.score_type == ORBX_HARRIS_SCORE || p.score_type == ORBX_FAST_SCORE);
 }
 
@@ -343,6 +344,22 @@ void oracle_cos_sin_f64(float deg, float* c, float* s) {
   float angle = deg * (float)(M_PI / 180.f);
   *c = (float)cos((double)angle);
   *s = (float)sin((double)angle);
+}
+
+// The same for the n consecutive float bit patterns from bits0 (host libm), on `threads` threads.
+void oracle_cos_sin_f64_range(uint32_t bits0, int64_t n, float* c, float* s, int threads) {
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; t++)
+    pool.emplace_back([=]() {
+      for (int64_t i = t; i < n; i += threads) {
+        const uint32_t b = bits0 + (uint32_t)i;
+        float deg;
+        memcpy(&deg, &b, 4);
+        oracle_cos_sin_f64(deg, c + i, s + i);
+      }
+    });
+  for (auto& th : pool) th.join();
 }
 
 // cv::ORB::operator()(image, noArray(), keypoints, descriptors) (orb.cpp, OpenCV 2.4)

@@ -536,6 +536,15 @@ def cos_sin_f64(deg):
     return c.value, s.value
 
 
+def cos_sin_f64_range(bits0, n, threads=8):
+    """(float)cos/sin((double)(deg * (float)(pi/180))) for the n float bit patterns from bits0."""
+    c = np.zeros(n, np.float32)
+    s = np.zeros(n, np.float32)
+    lib().oracle_cos_sin_f64_range(C.c_uint32(bits0), C.c_int64(n), _p(c), _p(s),
+                                   C.c_int(threads))
+    return c, s
+
+
 def bf_match(query, train):
     q = np.ascontiguousarray(query, np.uint8).reshape(-1, 32)
     t = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)

@@ -101,6 +101,7 @@ int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_l
 int oracle_cvorb_levels(const orbx_cvorb_params* p, int w, int h, int* lw, int* lh, float* scale,
                         int* feats);
 void oracle_retain_best(float* resp, int32_t* ids, int n, int n_points, int* n_out);
+void oracle_cos_sin_f64_range(uint32_t bits0, int64_t n, float* c, float* s, int threads);
 float oracle_harris(const uint8_t* img, int64_t stride, int x, int y);
 void oracle_cvorb_descriptor(const uint8_t* blurred, int64_t stride, int cx, int cy, float angle,
                              uint8_t* desc32);
