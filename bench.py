@@ -37,7 +37,13 @@ CONFIGS = {
     "C4": dict(w=1241, h=376, nfeatures=2000, stereo=(386.1448, 718.856),
                workload="KITTI 00 stereo geometry 2x1241x376, 2000 features, stereo matching"),
     "C5": dict(w=1920, h=1080, nfeatures=4000, workload="synthetic 1920x1080, 4000 features"),
+    # the AR marker path (Marker::Match: cv::ORB 2.4 HARRIS 500 features on
+    # the frame, BruteForceMatcher<HammingLUT> against the target's descriptors, good filter)
+    "AR": dict(w=640, h=480, nfeatures=500, marker=True,
+               workload="AR marker path 640x480: cv::ORB (500, HARRIS_SCORE) + BruteForceMatcher "
+                        "vs a 500-feature target + Marker::Match filter"),
 }
+MARKER_METRIC = "frames/sec AR Marker::Match (cv::ORB HARRIS 500 + BF Hamming match), 640x480"
 
 
 def level_sizes(w, h, inv_scale):
@@ -144,6 +150,144 @@ def cpu_baseline(cfg, seconds):
                        f"{platform.processor() or platform.machine()}")
 
 
+def cpu_baseline_marker(cfg, seconds, target_desc):
+    """The CPU oracle of the marker path (cvorb_oracle.cc), 1 thread: cv::ORB of the frame,
+    BruteForceMatcher match against the target, Marker::Match's good filter, per frame."""
+    from oracle import oracle as O
+    from ar_orbslam2_amd import synth
+    w, h = cfg["w"], cfg["h"]
+    base = synth.canvas(w, h, 0)
+    imgs = [synth.frame(w, h, i, 0, base) for i in range(32)]
+    p = O.cvorb_params(cfg["nfeatures"])
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        kps, desc = O.cvorb_detect(imgs[n % len(imgs)], p)
+        O.good_matches(O.bf_match(target_desc, desc))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 4:
+            break
+    return dict(value=n / el, unit="frames/s", cores=1, kind="port",
+                sample=f"{n} consecutive {w}x{h} synthetic frames, CPU oracle (oracle/cvorb_oracle.cc, "
+                       f"g++ -O3 -march=x86-64-v3 -ffp-contract=off), 1 thread, cv::ORB + "
+                       f"BruteForceMatcher vs {len(target_desc)} target descriptors + good filter "
+                       f"per frame, {el:.1f} s on {platform.processor() or platform.machine()}")
+
+
+def marker_bytes(levels, n_kp, n_img, n_target):
+    """Algorithmic bytes per launch of the marker-path kernels (same byte model as §8d; the
+    matcher reads both descriptor sets once per frame)."""
+    P = [w * h for w, h in levels]
+    per_resize = [(P[l - 1] + P[l]) * n_img for l in range(1, len(P))]
+    return {"k_pyramid": (2 * P[0] * n_img + sum(per_resize)) / 2,
+            "k_cvfast": sum(P) * n_img, "k_blur": 2 * sum(P) * n_img,
+            "k_cvselect": sum(P) * n_img / 8 + 8 * n_kp, "k_cvdescribe": 60 * n_kp,
+            "k_bfmatch": 32 * (n_kp + n_target * n_img) + 8 * n_target * n_img,
+            "k_good": 24 * n_target * n_img}
+
+
+def run_marker(args, cfg, rank, world, local):
+    import torch
+    from oracle import oracle as O  # the target's descriptors only (fixed input, untimed)
+    from ar_orbslam2_amd import synth
+    from ar_orbslam2_amd.marker import MarkerBatch
+    w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
+    S = max(1, args.streams)
+    target = synth.frame(w, h, 5, 0)
+    _, target_desc = O.cvorb_detect(target, O.cvorb_params(nf))
+    pipes, pools = [], []
+    for si in range(S):
+        mb = MarkerBatch(w, h, B, nf, device=local)
+        mb.set_target(target_desc)
+        stream_id = stream_of_rank(rank) * S + si
+        base = synth.canvas(w, h, stream=stream_id)
+        pool = []
+        for pi in range(args.pool):
+            fr = np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)])
+            pool.append(torch.from_numpy(fr).cuda())
+        pipes.append(mb)
+        pools.append(pool)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for i in range(args.warmup):
+        for p, pool in zip(pipes, pools):
+            p.run(pool[i % len(pool)].data_ptr(), B)
+    for p in pipes:
+        p.sync()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        for p, pool in zip(pipes, pools):
+            p.run(pool[i % len(pool)].data_ptr(), B)
+    for p in pipes:
+        p.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stages = {}
+    pipe = pipes[0]
+    if not args.no_profile:
+        pipe.profile(True)
+        for i in range(args.roofline_steps):
+            pipe.run(pools[0][i % len(pools[0])].data_ptr(), B)
+        pipe.sync()
+        stages = pipe.profile_read()
+        pipe.profile(False)
+    kp_counts, good_counts = pipe.results(B)
+    if (kp_counts < 0).any():
+        raise RuntimeError("a frame overflowed the per-level keypoint capacity")
+    elapsed = aggregate_elapsed(elapsed, world)
+    value = world * S * B * args.steps / elapsed
+    from ar_orbslam2_amd.marker import cvorb_params
+    lv = O.cvorb_levels(cvorb_params(nf), w, h)
+    levels = list(zip(lv["w"].tolist(), lv["h"].tolist()))
+    n_kp = int(kp_counts.sum())
+    alg = marker_bytes(levels, n_kp, B, len(target_desc))
+    roofline = None
+    if stages:
+        dom = max(stages, key=lambda k: stages[k][0])
+        ms, launches = stages[dom]
+        avg_s = ms / 1e3 / max(launches, 1)
+        a_bytes = alg.get(dom)
+        achieved = a_bytes / avg_s / 1e9
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 6),
+                    "traffic": pmc_traffic(args.pmc_dir, dom),
+                    "avg_launch_us": round(avg_s * 1e6, 2),
+                    "algorithmic_bytes_per_launch": a_bytes,
+                    "stages_ms_per_step": {k: round(v[0] / args.roofline_steps, 4)
+                                           for k, v in stages.items()},
+                    "stages_of": f"roofline pass: camera stream 0 alone, {args.roofline_steps} "
+                                 f"steps of {B} frames after the timed region"}
+    out = {
+        "metric": MARKER_METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B * S,
+                   "camera_streams_per_gpu": S, "frames_per_batch": B, "image": f"{w}x{h}",
+                   "nfeatures": nf, "target_descriptors": len(target_desc),
+                   "parallelism": f"{world} GPU(s) x {S} independent camera streams, no collective",
+                   "keypoints_per_frame": round(n_kp / B, 1),
+                   "good_matches_per_frame": round(float(good_counts.mean()), 1),
+                   "hamming_pairs_per_frame": round(n_kp / B * len(target_desc)),
+                   "timing": "hipGraph replay of the extraction + 2 matcher launches per batch"},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_marker(cfg, args.cpu_seconds, target_desc)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def aggregate_elapsed(elapsed, world):
     """Max over ranks: the job is as fast as its slowest GPU (RCCL/gloo all_reduce MAX)."""
     if world <= 1:
@@ -194,10 +338,16 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local))
 
+    cfg = CONFIGS[args.config]
+    if cfg.get("marker"):
+        run_marker(args, cfg, rank, world, local)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     from ar_orbslam2_amd import ORBextractor, Vocabulary, epipole, synth
     from ar_orbslam2_amd.pipeline import TUM1_K, FramePipeline, fundamental_from_pose
 
-    cfg = CONFIGS[args.config]
     w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
     voc = Vocabulary.synthetic()
     S = max(1, args.streams)
