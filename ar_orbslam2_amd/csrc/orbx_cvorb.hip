@@ -7,7 +7,7 @@
 // fixed launch sequence on the plan's stream (captured once into a hipGraph):
 //   k_pyramid      levels (cv::resize INTER_LINEAR from the previous level; shared with the
 //                  ORBextractor plan, orbx_extract.hip)
-//   k_cvfast       64x16 tiles of every level's border region [edge, w-edge) x [edge, h-edge):
+//   k_cvfast       64x32 tiles of every level's border region [edge, w-edge) x [edge, h-edge):
 //                  FAST-9/16 cornerScore at threshold 20 + whole-image 8-neighbour NMS
 //                  (cv::FAST(..., nonmax=true) followed by runByImageBorder) -> keep bitmaps
 //   k_cvselect     one wave per (image, level): raster-order compaction of the keep bitmaps,
@@ -56,7 +56,7 @@ __constant__ int c_cv_umax[kHalfPatch + 1];
 
 constexpr float kHarrisK = 0.04f;  // HARRIS_K (orb.cpp)
 constexpr int kFastTh = 20;        // computeKeyPoints: FastFeatureDetector fd(20, true)
-constexpr int kTW = 64, kTH = 16;  // k_cvfast tile
+constexpr int kTW = 64, kTH = 32;  // k_cvfast tile
 constexpr int kSelCap = 4096;      // k_cvselect: keypoints kept in LDS (more: global scratch)
 
 struct CvLevel {
@@ -91,74 +91,108 @@ __device__ __forceinline__ void xcd_block(int& bx, int& by) {
 // cv::FAST(level, keypoints, 20, true) keeps p when score(p) >= 20 and score(p) > V(q) for the
 // 8 neighbours, V(q) = score(q) if q is a corner at 20, else 0 (fast.cpp); then
 // runByImageBorder drops every keypoint outside [edge, w-edge) x [edge, h-edge) (edge >= 18,
-// so every neighbour of a kept pixel is a detection pixel).  A tile stages rows Y0-4..Y0+19
-// and columns X0-4..X0+67 (dword loads), scores the tile plus a 1-px ring into LDS (0 unless a
-// corner; compass-point pretest first: a 9-arc holds two consecutive compass points), then
-// one wave per row ballots the NMS survivors into the row's 64-bit keep word and stores the
-// survivors' scores.
+// so every neighbour of a kept pixel is a detection pixel).  A 64 x 32 tile stages rows
+// Y0-4..Y0+35 and columns X0-8..X0+71 (8-byte loads); the V window is the tile plus a 1-px
+// ring, restricted to [edge-1, w-edge] x [edge-1, h-edge].  The even-circle-point pretest runs
+// one pixel per lane with the compares as lane masks (fast_pretest), only its survivors are
+// queued (per wave, mbcnt ranks) and scored; the strict NMS is evaluated at the queued pixels
+// of the tile proper, survivors set their bit in the row's keep word (ds_or) and store their
+// score for k_cvselect.
 __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                                 const CvLevel* __restrict__ lv,
                                                 const CvTile* __restrict__ tiles,
                                                 uint64_t* __restrict__ bitmaps, int64_t bm_words,
                                                 uint8_t* __restrict__ smap) {
-  constexpr int SW = kTW + 8, SR = kTH + 8;  // staged bytes per row, rows
-  constexpr int QW = kTW + 2, QR = kTH + 2;  // score ring
-  __shared__ __align__(16) uint32_t s_in[SR * SW / 4];
-  __shared__ uint8_t s_sc[QR * QW];
+  constexpr int kInR = kTH + 8;           // staged rows Y0-4 .. Y0+kTH+3
+  constexpr int kInD = (kTW + 16) / 4;    // staged dwords: columns X0-8 .. X0+71
+  constexpr int kRowB = kInD * 4;         // staged row stride (bytes)
+  constexpr int kWinR = kTH + 2;          // V rows Y0-1 .. Y0+kTH
+  constexpr int kVS = kTW + 8;            // V row stride: columns X0-4 .. X0+67
+  constexpr int kQ = (kWinR + 3) / 4 * 64 + 64;  // per-wave queue bound (rows + ring pass)
+  __shared__ __align__(16) uint32_t s_in[kInR][kInD];
+  __shared__ __align__(16) uint32_t s_v32[kWinR * kVS / 4];
+  __shared__ uint16_t s_q[4][kQ + 64];
+  __shared__ uint64_t s_keep[kTH];
   int bx, img;
   xcd_block(bx, img);
   const CvTile T = tiles[bx];
   const CvLevel L = lv[T.level];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int X0 = T.tx * kTW, Y0 = L.ry0 + T.ty * kTH;
   const uint8_t* src = pyr + (int64_t)img * pyr_bytes + L.pyr_off;
-  const int tid = threadIdx.x;
-  const int pw = L.pitch >> 2;
-  for (int i = tid; i < SR * (SW / 4); i += 256) {
-    const int r = i / (SW / 4), c = i - r * (SW / 4);
-    const int y = min(max(Y0 - 4 + r, 0), L.h - 1);
-    const int cw = min(max((X0 >> 2) - 1 + c, 0), pw - 1);
-    s_in[i] = *(const uint32_t*)(src + (int64_t)y * L.pitch + 4 * cw);
+  for (int i = tid; i < kInR * (kInD / 2); i += 256) {
+    const int r = i / (kInD / 2), c = i - r * (kInD / 2);
+    const int y = min(max(Y0 + r - 4, 0), L.h - 1);
+    const int x = X0 - 8 + 8 * c;
+    *(uint2*)&s_in[r][2 * c] = (x >= 0 && x < L.pitch)
+                                   ? *(const uint2*)(src + (int64_t)y * L.pitch + x)
+                                   : make_uint2(0u, 0u);
   }
+  for (int i = tid; i < kWinR * kVS / 4; i += 256) s_v32[i] = 0;
+  if (tid < kTH) s_keep[tid] = 0;
   __syncthreads();
-  const uint8_t* S = (const uint8_t*)s_in;
   const int t = kFastTh;
-  for (int i = tid; i < QR * QW; i += 256) {
-    const int j = i / QW, c = i - j * QW;
-    const int x = X0 - 1 + c, y = Y0 - 1 + j;
-    int sc = 0;
-    if (x >= L.rx0 - 1 && x <= L.rx1 && y >= L.ry0 - 1 && y <= L.ry1) {
-      const uint8_t* p = S + (j + 3) * SW + (c + 3);
-      const int v = p[0];
-      const int d0 = v - p[3 * SW], d4 = v - p[3], d8 = v - p[-3 * SW], d12 = v - p[-3];
-      const bool dk0 = d0 > t, dk4 = d4 > t, dk8 = d8 > t, dk12 = d12 > t;
-      const bool br0 = d0 < -t, br4 = d4 < -t, br8 = d8 < -t, br12 = d12 < -t;
-      const bool pass = (dk0 && dk4) || (dk4 && dk8) || (dk8 && dk12) || (dk12 && dk0) ||
-                        (br0 && br4) || (br4 && br8) || (br8 && br12) || (br12 && br0);
-      if (pass) {
-        const int s = fast_score(S, SW, c + 3, j + 3);
-        sc = s >= t ? s : 0;
-      }
+  // V window: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, byte vx + 4
+  const int xlo = L.rx0 - 1, xhi = L.rx1, ylo = L.ry0 - 1, yhi = L.ry1;  // inclusive
+  uint16_t* q = s_q[wid];
+  int nq = 0;
+  const uint8_t* sin8 = (const uint8_t*)s_in;
+  auto enqueue = [&](uint64_t pass, int idx) {
+    q[(pass >> lane) & 1 ? nq + lane_rank(pass) : kQ + lane] = (uint16_t)idx;
+    nq += __popcll(pass);
+  };
+  const uint64_t col_ok = __ballot(X0 + lane >= xlo && X0 + lane <= xhi);
+  if (col_ok != 0) {
+    const int vy_lo = max(0, ylo - (Y0 - 1)), vy_hi = min(kWinR, yhi - (Y0 - 1) + 1);
+    for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)
+      enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 5, t, col_ok), vy * kVS + 4 + lane);
+  }
+  // ring columns X0-1 (vx 3) and X0+64 (vx 68)
+  for (int k0 = wid * 64; k0 < 2 * kWinR; k0 += 256) {
+    const int k = k0 + lane;
+    const int vy = min(k >> 1, kWinR - 1), vx = k & 1 ? 4 + kTW : 3;
+    const int x = X0 - 4 + vx, y = Y0 - 1 + vy;
+    const uint64_t ok = __ballot(k < 2 * kWinR && x >= xlo && x <= xhi && y >= ylo && y <= yhi);
+    if (ok != 0) enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + vx + 1, t, ok), vy * kVS + vx);
+  }
+  uint8_t* s_v = (uint8_t*)s_v32;
+  for (int j0 = 0; j0 < nq; j0 += 64) {
+    const int j = j0 + lane;
+    if (j < nq) {
+      const int i = q[j];
+      const int vy = i / kVS, vx = i - vy * kVS;
+      const int sc = fast_score(sin8, kRowB, vx + 4, vy + 3);
+      s_v[i] = (uint8_t)(sc >= t ? sc : 0);
     }
-    s_sc[i] = (uint8_t)sc;
   }
   __syncthreads();
-  const int lane = tid & 63, wave = tid >> 6;
-  const int x = X0 + lane;
-  uint64_t* bm = bitmaps + (int64_t)img * bm_words + L.bm_off;
   uint8_t* sm = smap + (int64_t)img * pyr_bytes + L.pyr_off;
-  for (int j = wave; j < kTH; j += 4) {
-    const int y = Y0 + j;
-    if (y >= L.ry1) break;  // wave-uniform
-    const uint8_t* q = s_sc + (j + 1) * QW + (lane + 1);
-    const int s = q[0];
-    bool keep = s > 0 && x >= L.rx0 && x < L.rx1;
-    if (keep) {
-      keep = s > q[-QW - 1] && s > q[-QW] && s > q[-QW + 1] && s > q[-1] && s > q[1] &&
-             s > q[QW - 1] && s > q[QW] && s > q[QW + 1];
+  for (int j0 = 0; j0 < nq; j0 += 64) {
+    const int j = j0 + lane;
+    if (j >= nq) break;
+    const int i = q[j];
+    const int vy = i / kVS, vx = i - vy * kVS;
+    const int tx = vx - 4, ty = vy - 1;
+    const int x = X0 + tx, y = Y0 + ty;
+    if (tx < 0 || tx >= kTW || ty < 0 || ty >= kTH || x < L.rx0 || x >= L.rx1 || y >= L.ry1)
+      continue;
+    const int v = s_v[i];
+    if (v == 0) continue;
+    const uint8_t* pu = s_v + i - kVS;
+    const uint8_t* pd = s_v + i + kVS;
+    const int nmax = max(max(max((int)pu[-1], (int)pu[0]), max((int)pu[1], (int)s_v[i - 1])),
+                         max(max((int)s_v[i + 1], (int)pd[-1]), max((int)pd[0], (int)pd[1])));
+    if (v > nmax) {
+      atomicOr((unsigned long long*)&s_keep[ty], 1ull << tx);
+      sm[(int64_t)y * L.pitch + x] = (uint8_t)v;
     }
-    const uint64_t m = __ballot(keep);
-    if (lane == 0) bm[(int64_t)y * L.bm_wpr + T.tx] = m;
-    if (keep) sm[(int64_t)y * L.pitch + x] = (uint8_t)s;
+  }
+  __syncthreads();
+  if (tid < kTH) {
+    const int y = Y0 + tid;
+    if (y < L.ry1)
+      bitmaps[(int64_t)img * bm_words + L.bm_off + (int64_t)y * L.bm_wpr + T.tx] = s_keep[tid];
   }
 }
 
@@ -353,19 +387,38 @@ __device__ int wave_retain_best(CvKey* a, int n, int n_points, uint32_t* Lpos, u
   return n_points + s.rtot;
 }
 
-// HarrisResponses(img, pts, 7, 0.04) for an integral keypoint (orb.cpp).
+// HarrisResponses(img, pts, 7, 0.04) for an integral keypoint (orb.cpp): the 9 x 9 window
+// (x-4 .. x+4, y-4 .. y+4) is loaded as 9 rows of three aligned dwords (the pitched level rows
+// are padded, so x+8 < pitch) and funnel-shifted to start at x-4; the sums are exact integers.
 __device__ float harris_response(const uint8_t* img, int step, int x, int y) {
-  const int r = 3;
   float scale = (float)((1 << 2) * 7) * 255.0f;
   scale = 1.0f / scale;
   const float scale_sq_sq = scale * scale * scale * scale;
-  const uint8_t* ptr0 = img + (y - r) * step + (x - r);
+  const int x0 = x - 4, xa = x0 & ~3, sh = x0 - xa;
+  int px[9][9];
+#pragma unroll
+  for (int r = 0; r < 9; r++) {
+    const uint32_t* rp = (const uint32_t*)(img + (int64_t)(y - 4 + r) * step + xa);
+    const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    const uint32_t d2 = w2 >> (8 * sh);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      px[r][c] = (d0 >> (8 * c)) & 255;
+      px[r][c + 4] = (d1 >> (8 * c)) & 255;
+    }
+    px[r][8] = d2 & 255;
+  }
   int a = 0, b = 0, c = 0;
-  for (int i = 0; i < 7; i++)
-    for (int j = 0; j < 7; j++) {
-      const uint8_t* p = ptr0 + i * step + j;
-      const int Ix = (p[1] - p[-1]) * 2 + (p[-step + 1] - p[-step - 1]) + (p[step + 1] - p[step - 1]);
-      const int Iy = (p[step] - p[-step]) * 2 + (p[step - 1] - p[-step - 1]) + (p[step + 1] - p[-step + 1]);
+#pragma unroll
+  for (int i = 1; i <= 7; i++)
+#pragma unroll
+    for (int j = 1; j <= 7; j++) {
+      const int Ix = (px[i][j + 1] - px[i][j - 1]) * 2 + (px[i - 1][j + 1] - px[i - 1][j - 1]) +
+                     (px[i + 1][j + 1] - px[i + 1][j - 1]);
+      const int Iy = (px[i + 1][j] - px[i - 1][j]) * 2 + (px[i + 1][j - 1] - px[i - 1][j - 1]) +
+                     (px[i + 1][j + 1] - px[i - 1][j + 1]);
       a += Ix * Ix;
       b += Iy * Iy;
       c += Ix * Iy;
@@ -397,16 +450,22 @@ __global__ __launch_bounds__(64) void k_cvselect(
     if (lane == 0) *oc = 0;
     return;
   }
+  // lane = region row: its keep words (nw <= 64, in registers 8 at a time), survivor count
   const uint64_t* bm = bitmaps + (int64_t)img * bm_words + L.bm_off;
   const int w0 = L.rx0 >> 6, nw = ((L.rx1 - 1) >> 6) - w0 + 1, nr = L.ry1 - L.ry0;
-  const int total = nw * nr;
+  auto row_words = [&](int r, int k0, uint64_t (&wv)[8]) {
+    const uint64_t* rp = bm + (int64_t)(L.ry0 + r) * L.bm_wpr + w0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) wv[k] = (r < nr && k0 + k < nw) ? rp[k0 + k] : 0ull;
+  };
   int n = 0;
-  for (int q0 = 0; q0 < total; q0 += 64) {
-    const int q = q0 + lane;
+  for (int r0 = 0; r0 < nr; r0 += 64) {
     int c = 0;
-    if (q < total) {
-      const int r = q / nw, k = q - r * nw;
-      c = __popcll(bm[(int64_t)(L.ry0 + r) * L.bm_wpr + w0 + k]);
+    for (int k0 = 0; k0 < nw; k0 += 8) {
+      uint64_t wv[8];
+      row_words(r0 + lane, k0, wv);
+#pragma unroll
+      for (int k = 0; k < 8; k++) c += __popcll(wv[k]);
     }
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     n += c;
@@ -422,32 +481,41 @@ __global__ __launch_bounds__(64) void k_cvselect(
     Lpos = gpos + (int64_t)img * cand_total + L.cand_off;
     Rpos = Lpos + (L.cand_cap + 1) / 2;
   }
-  // raster order: word q = row-major over (row, word), bits ascending
-  const uint8_t* sm = smap + (int64_t)img * pyr_bytes + L.pyr_off;
+  // raster order = row order (prefix over the rows' counts), then ascending x within a row
   int base = 0;
-  for (int q0 = 0; q0 < total; q0 += 64) {
-    const int q = q0 + lane;
-    uint64_t word = 0;
-    int r = 0, k = 0;
-    if (q < total) {
-      r = q / nw;
-      k = q - r * nw;
-      word = bm[(int64_t)(L.ry0 + r) * L.bm_wpr + w0 + k];
+  for (int r0 = 0; r0 < nr; r0 += 64) {
+    const int r = r0 + lane;
+    int c = 0;
+    for (int k0 = 0; k0 < nw; k0 += 8) {
+      uint64_t wv[8];
+      row_words(r, k0, wv);
+#pragma unroll
+      for (int k = 0; k < 8; k++) c += __popcll(wv[k]);
     }
-    const int c = __popcll(word);
     const int incl = wave_incl_scan(c);
     int pos = base + incl - c;
-    const int y = L.ry0 + r, xb = 64 * (w0 + k);
-    while (word) {
-      const int b = __ffsll((unsigned long long)word) - 1;
-      word &= word - 1;
-      const int x = xb + b;
-      CvKey e;
-      e.r = (float)sm[(int64_t)y * L.pitch + x];
-      e.k = ((uint32_t)y << 16) | (uint32_t)x;
-      a[pos++] = e;
+    const uint32_t yk = (uint32_t)(L.ry0 + r) << 16;
+    for (int k0 = 0; k0 < nw; k0 += 8) {
+      uint64_t wv[8];
+      row_words(r, k0, wv);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        uint64_t word = wv[k];
+        const int xb = 64 * (w0 + k0 + k);
+        while (word) {
+          const int bit = __ffsll((unsigned long long)word) - 1;
+          word &= word - 1;
+          a[pos++].k = yk | (uint32_t)(xb + bit);
+        }
+      }
     }
     base += __shfl(incl, 63);
+  }
+  __syncthreads();
+  const uint8_t* sm = smap + (int64_t)img * pyr_bytes + L.pyr_off;
+  for (int i = lane; i < n; i += 64) {
+    const uint32_t key = a[i].k;
+    a[i].r = (float)sm[(int64_t)(key >> 16) * L.pitch + (key & 0xFFFF)];
   }
   __syncthreads();
   const int feats = L.feats;

@@ -143,6 +143,39 @@ int launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint
 int launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur, int n,
                 hipStream_t s);
 
+// Even-point pretest for one pixel per lane (row stride RS of the staged bytes; c = top-left
+// byte of the pixel's 7x7 neighbourhood): lane mask of the pixels in ok that may be corners at
+// t.  Any 9-arc contains 4 cyclically consecutive even circle points, all darker or all
+// brighter; each point's compare is a v_cmp into a lane mask and, with A_k = D_k & D_k+1,
+// OR_k A_k & A_k+2 = (A0|A4)&(A2|A6) | (A1|A5)&(A3|A7) runs in the scalar unit.
+template <int RS>
+__device__ __forceinline__ uint64_t fast_pretest(const uint8_t* c, int t, uint64_t ok) {
+  const int v = c[3 * RS + 3];
+  const int lo = v - t, hi = v + t;
+  // even circle points in circle order: (0,3) (2,2) (3,0) (2,-2) (0,-3) (-2,-2) (-3,0) (-2,2)
+  const int e[8] = {c[6 * RS + 3], c[5 * RS + 5], c[3 * RS + 6], c[RS + 5],
+                    c[3],          c[RS + 1],     c[3 * RS],     c[5 * RS + 1]};
+  uint64_t pd[8], pb[8], dk[8], bk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    dk[k] = __ballot(e[k] < lo);
+    bk[k] = __ballot(e[k] > hi);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    pd[k] = dk[k] & dk[(k + 1) & 7];
+    pb[k] = bk[k] & bk[(k + 1) & 7];
+  }
+  const uint64_t any = ((pd[0] | pd[4]) & (pd[2] | pd[6])) | ((pd[1] | pd[5]) & (pd[3] | pd[7])) |
+                       ((pb[0] | pb[4]) & (pb[2] | pb[6])) | ((pb[1] | pb[5]) & (pb[3] | pb[7]));
+  return any & ok;
+}
+
+// rank of this lane among the set lanes of m
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
 // OpenCV 2.4 cornerScore<16> at (x, y) of a u8 image with row stride `stride`:
 // the pixel is a FAST-9/16 corner at threshold t iff the score is >= t.
 __device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, int y) {
