@@ -89,6 +89,29 @@ def pmc_traffic(pmc_dir, kernel):
     return round((tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024)
 
 
+def pmc_valu(pmc_dir, kernel, avg_launch_us):
+    """VALU-issue roofline of `kernel` from the SQ counter pass of this bench command
+    (sq_counters.csv: SQ_INSTS_VALU summed over a dispatch's waves).  A wave64 VALU instruction
+    occupies its SIMD's VALU for one quad-cycle (SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU on these
+    kernels), so the issue floor of a launch is INSTS_VALU * 4 / (1024 SIMDs * 2.4 GHz)."""
+    import csv
+    path = os.path.join(pmc_dir, "sq_counters.csv")
+    if not os.path.exists(path) or not avg_launch_us:
+        return None
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if r["Kernel_Name"].split("(")[0].endswith("::" + kernel)
+            and r["Counter_Name"] == "SQ_INSTS_VALU"]
+    if not vals:
+        return None
+    instr = sum(vals) / len(vals)
+    floor_us = instr * 4 / 1024 / 2400.0
+    return {"valu_instr_per_launch": round(instr), "issue_floor_us": round(floor_us, 2),
+            "frac": round(floor_us / avg_launch_us, 4),
+            "note": "integer stencil/popcount work: the VALU issue rate, not HBM, bounds it; "
+                    "floor = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz), frac = floor / "
+                    "avg_launch_us (" + os.path.relpath(path, ROOT) + ")"}
+
+
 def cpu_baseline(cfg, seconds):
     """The CPU oracle (orb_oracle.cc restating ORBextractor/ORBmatcher) on this host, 1 thread,
     on consecutive frames of the same synthetic stream: extract + SearchByBoW +
@@ -263,6 +286,7 @@ def run_marker(args, cfg, rank, world, local):
                     "traffic": pmc_traffic(args.pmc_dir, dom),
                     "avg_launch_us": round(avg_s * 1e6, 2),
                     "algorithmic_bytes_per_launch": a_bytes,
+                    "valu_roofline": pmc_valu(args.pmc_dir, dom, avg_s * 1e6),
                     "stages_ms_per_step": {k: round(v[0] / args.roofline_steps, 4)
                                            for k, v in stages.items()},
                     "stages_of": f"roofline pass: camera stream 0 alone, {args.roofline_steps} "
@@ -310,13 +334,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="frames per step (per GPU)")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="frames per step per camera stream")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
     ap.add_argument("--streams", type=int, default=3,
                     help="independent camera-stream pipelines per GPU, one HIP stream each "
                          "(kernels are latency-bound; concurrent streams fill the CUs the others leave idle)")
-    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01_pmc"),
+    ap.add_argument("--pmc-dir", default=None,
                     help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE CSVs of this bench command, used "
                          "for roofline.traffic (per launch of the dominant kernel)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -326,6 +351,9 @@ def main():
     ap.add_argument("--roofline-steps", type=int, default=5,
                     help="steps of the single-stream roofline pass (per-kernel HIP events)")
     args = ap.parse_args()
+    if args.pmc_dir is None:  # the committed PMC passes of this config's default command
+        args.pmc_dir = os.path.join(ROOT, "profiles",
+                                    "r01_pmc_ar" if args.config == "AR" else "r01_pmc")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -443,6 +471,7 @@ def main():
                                     os.path.relpath(args.pmc_dir, ROOT) + ")",
                     "avg_launch_us": round(avg_s * 1e6, 2),
                     "algorithmic_bytes_per_launch": a_bytes,
+                    "valu_roofline": pmc_valu(args.pmc_dir, dom, avg_s * 1e6),
                     "stages_ms_per_step": {k: round(v[0] / args.roofline_steps, 4)
                                            for k, v in stages.items()},
                     "stages_of": f"roofline pass: camera stream 0 alone, {args.roofline_steps} "

@@ -15,12 +15,14 @@ def load(path):
 
 
 if __name__ == "__main__":
-    base = sys.argv[1]
-    sq = load(f"{base}/pmc_sq/run_counter_collection.csv")
-    fe = load(f"{base}/pmc_fetch/run_counter_collection.csv")
-    wr = load(f"{base}/pmc_write/run_counter_collection.csv")
+    # usage: pmc_summary.py <pmc dir: sq_counters.csv, fetch_size.csv, write_size.csv>
+    #                       <rocprofv3 kernel_stats.csv of the same command>
+    base, stats = sys.argv[1], sys.argv[2]
+    sq = load(f"{base}/sq_counters.csv")
+    fe = load(f"{base}/fetch_size.csv")
+    wr = load(f"{base}/write_size.csv")
     dur = {}
-    for r in csv.DictReader(open(f"{base}/trace/run_kernel_stats.csv")):
+    for r in csv.DictReader(open(stats)):
         dur[r["Name"].split("(")[0].split("::")[-1]] = float(r["AverageNs"]) / 1e3
     print(f"{'kernel':16s} {'us':>7s} {'waves':>7s} {'valu/w':>7s} {'salu/w':>7s} {'lds/w':>6s} "
           f"{'wait%':>5s} {'valu_us':>7s} {'fetchMB':>8s} {'writeMB':>8s}")

@@ -6,7 +6,8 @@ a kernel includes launches that share the GPU with other streams' kernels; bench
 roofline kernel in a separate pass on stream 0 alone (its last `--roofline-steps` launches).
 This prints both the overall trace average and the average over those last launches.
 
-Usage: python3 scripts/roofline_check.py <trace dir> <bench json line file> [roofline_steps]"""
+Usage: python3 scripts/roofline_check.py <trace dir | kernel_trace.csv> <bench json line file>
+       [roofline_steps]"""
 import csv
 import json
 import sys
@@ -15,7 +16,9 @@ trace_dir, bench_file = sys.argv[1], sys.argv[2]
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 b = json.loads(open(bench_file).read().strip().splitlines()[-1])
 kern = b["roofline"]["kernel"]
-rows = [r for r in csv.DictReader(open(f"{trace_dir}/run_kernel_trace.csv"))
+import os
+path = trace_dir if trace_dir.endswith(".csv") else os.path.join(trace_dir, "run_kernel_trace.csv")
+rows = [r for r in csv.DictReader(open(path))
         if r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + kern)]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
