@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "../../include/orbx_pattern.h"
+#include "orbx_describe.h"
 #include "orbx_internal.h"
 #include "orbx_match.h"
 #include "orbx_math.h"
@@ -51,8 +52,8 @@
 namespace orbx {
 namespace cvorb {
 
-__constant__ int8_t c_cv_pattern[1024];
-__constant__ int c_cv_umax[kHalfPatch + 1];
+__constant__ int8_t c_cv_pattern[1024];            // bit_pattern_31_ (512 points)
+__constant__ IcMask c_cv_icmask;                   // IC_Angle row masks (umax, half 15)
 
 constexpr float kHarrisK = 0.04f;  // HARRIS_K (orb.cpp)
 constexpr int kFastTh = 20;        // computeKeyPoints: FastFeatureDetector fd(20, true)
@@ -623,21 +624,11 @@ __global__ __launch_bounds__(256) void k_cvdescribe(
     for (int k = 0; k < (BN + 31) / 32; k++)
       if (hl + 32 * k < BN) s_blr[hw][hl + 32 * k] = vb[k];
   }
-  constexpr int RS = 4 * RW, BS = 4 * BW;
-  const uint8_t* raw = (const uint8_t*)s_raw[hw] + 15 * RS + (cx - 4 * fr);
+  constexpr int BS = 4 * BW;
   const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - 4 * fb);
   int m10 = 0, m01 = 0;
-  if (active && hl < 31) {
-    const int u = hl - 15;
-    m10 = u * (int)raw[u];
-    for (int v = 1; v <= kHalfPatch; v++) {
-      const int d = c_cv_umax[v];
-      if (u < -d || u > d) continue;
-      const int vp = raw[u + v * RS], vm = raw[u - v * RS];
-      m10 += u * (vp + vm);
-      m01 += v * (vp - vm);
-    }
-  }
+  if (active && hl < 31)  // row v = hl - 15 of the circular patch
+    ic_row_moments(s_raw[hw] + hl * RW, (cx - 15) - 4 * fr, c_cv_icmask.m[hl], hl - 15, m10, m01);
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) {
     m10 += __shfl_xor(m10, o);
@@ -647,21 +638,16 @@ __global__ __launch_bounds__(256) void k_cvdescribe(
   const float angle = orbx_fast_atan2((float)m01, (float)m10);
   float ca, sb;
   cv_cos_sin(angle, &ca, &sb);
+  const uint8_t* bcb = bc - sample_bias(BS);
+  const float nsb = -sb;
   uint32_t byte = 0;
 #pragma unroll
   for (int m = 0; m < 8; m++) {
-    const int pair = hl * 8 + m;
-    int t[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const float px = (float)c_cv_pattern[pair * 4 + e * 2];
-      const float py = (float)c_cv_pattern[pair * 4 + e * 2 + 1];
-      const float xr = __fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sb));
-      const float yr = __fadd_rn(__fmul_rn(px, sb), __fmul_rn(py, ca));
-      const int col = (int)__builtin_rintf(xr), row = (int)__builtin_rintf(yr);
-      t[e] = bc[row * BS + col];
-    }
-    byte |= (uint32_t)(t[0] < t[1]) << m;
+    const int8_t* p8 = c_cv_pattern + (hl * 8 + m) * 4;  // (x0, y0, x1, y1) of pair 8 hl + m
+    const float4 pp = make_float4((float)p8[0], (float)p8[1], (float)p8[2], (float)p8[3]);
+    const int t0 = bcb[sample_offset(rotate_plain(pp.x, pp.y, ca, sb, nsb), BS)];
+    const int t1 = bcb[sample_offset(rotate_plain(pp.z, pp.w, ca, sb, nsb), BS)];
+    byte |= (uint32_t)(t0 < t1) << m;
   }
   int outpos = idx;
   for (int l = 0; l < level; l++) outpos += oc[l];
@@ -975,13 +961,14 @@ int plan_create(const orbx_cvorb_params& p, int w, int h, int max_batch, int dev
   if (hipSetDevice(device) != hipSuccess) return fail(ORBX_EDEVICE);
   if (hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(ORBX_EDEVICE);
-  if (hipMemcpyToSymbol(HIP_SYMBOL(c_cv_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)) != hipSuccess)
-    return fail(ORBX_EDEVICE);
   {
     orbx_params op{p.nfeatures, p.scale_factor, p.nlevels, 20, 7};
     Geometry t;
     build_tables(op, &t);  // umax for halfPatchSize 15 (orb.cpp computes it the same way)
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_cv_umax), t.umax, sizeof(t.umax)) != hipSuccess)
+    IcMask icm;
+    build_ic_mask(t.umax, &icm);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_cv_icmask), &icm, sizeof(icm)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_cv_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)) != hipSuccess)
       return fail(ORBX_EDEVICE);
   }
   rc = pyr_dev_create(g, &P->pd);

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/orbx_pattern.h"
+#include "orbx_describe.h"
 #include "orbx_internal.h"
 #include "orbx_math.h"
 
@@ -31,6 +32,7 @@ namespace orbx {
 
 __constant__ int8_t c_pattern[1024];
 __constant__ int c_umax[kHalfPatch + 1];
+__constant__ IcMask c_icmask;                   // IC_Angle row masks from umax
 
 // ------------------------------------------------------------------ helpers
 // Every level (level 0 copied in by k_pyramid) lives in the image's pitched pyramid block.
@@ -1302,22 +1304,13 @@ __global__ __launch_bounds__(256) void k_describe(
     for (int k = 0; k < (BN + 31) / 32; k++)
       if (hl + 32 * k < BN) s_blr[hw][hl + 32 * k] = vb[k];
   }
-  constexpr int RS = 4 * RW, BS = 4 * BW;
-  const uint8_t* raw = (const uint8_t*)s_raw[hw] + 15 * RS + (cx - 4 * fr);  // centre
+  constexpr int BS = 4 * BW;
   const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - 4 * fb);
-  // IC_Angle (ORBextractor.cc:73-98): lane hl < 31 is column u = hl - 15, rows v = 0..15
+  // IC_Angle (ORBextractor.cc:73-98): lane hl < 31 sums row v = hl - 15 of the circular patch
+  // (v_dot4_u32_u8 over the row's bytes masked to |u| <= umax[|v|])
   int m10 = 0, m01 = 0;
-  if (active && hl < 31) {
-    const int u = hl - 15;
-    m10 = __mul24(u, (int)raw[u]);
-    for (int v = 1; v <= kHalfPatch; v++) {
-      const int d = c_umax[v];
-      if (u < -d || u > d) continue;
-      const int vp = raw[u + __mul24(v, RS)], vm = raw[u - __mul24(v, RS)];
-      m10 += __mul24(u, vp + vm);
-      m01 += __mul24(v, vp - vm);
-    }
-  }
+  if (active && hl < 31)
+    ic_row_moments(s_raw[hw] + hl * RW, (cx - 15) - 4 * fr, c_icmask.m[hl], hl - 15, m10, m01);
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) {  // within the half-wave
     m10 += __shfl_xor(m10, o);
@@ -1329,20 +1322,20 @@ __global__ __launch_bounds__(256) void k_describe(
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float sn, cs;
   orbx_sincosf(angle * factorPI, &sn, &cs);
+  // rotated samples in packed f32 with the reference's fmaf pattern, rounded by the magic
+  // addend; the (row, col) -> byte offset bias is folded into the centre address
+  const uint8_t* bcb = bc - sample_bias(BS);
+  const float nsn = -sn;
   uint32_t byte = 0;
 #pragma unroll
   for (int m = 0; m < 8; m++) {
-    const int pair = hl * 8 + m;
-    int t[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const float px = (float)c_pattern[pair * 4 + e * 2];
-      const float py = (float)c_pattern[pair * 4 + e * 2 + 1];
-      const int row = (int)__builtin_rintf(__builtin_fmaf(px, sn, py * cs));
-      const int col = (int)__builtin_rintf(__builtin_fmaf(px, cs, -(py * sn)));
-      t[e] = bc[__mul24(row, BS) + col];
-    }
-    byte |= (uint32_t)(t[0] < t[1]) << m;
+    // (x0, y0, x1, y1) of pair 8 hl + m: int8 loads + cvt (a float table read per lane as
+    // 8 x dwordx4 made the kernel 30 % slower)
+    const int8_t* p8 = c_pattern + (hl * 8 + m) * 4;
+    const float4 pp = make_float4((float)p8[0], (float)p8[1], (float)p8[2], (float)p8[3]);
+    const int t0 = bcb[sample_offset(rotate_fma(pp.x, pp.y, cs, sn, nsn), BS)];
+    const int t1 = bcb[sample_offset(rotate_fma(pp.z, pp.w, cs, sn, nsn), BS)];
+    byte |= (uint32_t)(t0 < t1) << m;
   }
   int outpos = idx;
   for (int l = 0; l < level; l++) outpos += oc[l];
@@ -1582,6 +1575,11 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     return fail(ORBX_EDEVICE);
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)));
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), g.umax, sizeof(g.umax)));
+  {
+    IcMask icm;
+    build_ic_mask(g.umax, &icm);
+    ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), &icm, sizeof(icm)));
+  }
   const std::vector<BlurTile> tiles = blur_tiles(g);
   for (const CellGeom& c : g.cells)
     if (c.x1 - c.x0 > kCellMax || c.y1 - c.y0 > kCellMax) return fail(ORBX_EUNSUPPORTED);
