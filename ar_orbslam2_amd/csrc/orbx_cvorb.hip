@@ -7,7 +7,7 @@
 // fixed launch sequence on the plan's stream (captured once into a hipGraph):
 //   k_pyramid      levels (cv::resize INTER_LINEAR from the previous level; shared with the
 //                  ORBextractor plan, orbx_extract.hip)
-//   k_cvfast       64x32 tiles of every level's border region [edge, w-edge) x [edge, h-edge):
+//   k_cvfast       64x64 tiles of every level's border region [edge, w-edge) x [edge, h-edge):
 //                  FAST-9/16 cornerScore at threshold 20 + whole-image 8-neighbour NMS
 //                  (cv::FAST(..., nonmax=true) followed by runByImageBorder) -> keep bitmaps
 //   k_cvselect     one wave per (image, level): raster-order compaction of the keep bitmaps,
@@ -57,7 +57,7 @@ __constant__ IcMask c_cv_icmask;                   // IC_Angle row masks (umax, 
 
 constexpr float kHarrisK = 0.04f;  // HARRIS_K (orb.cpp)
 constexpr int kFastTh = 20;        // computeKeyPoints: FastFeatureDetector fd(20, true)
-constexpr int kTW = 64, kTH = 32;  // k_cvfast tile
+constexpr int kTW = 64, kTH = 64;  // k_cvfast tile
 constexpr int kSelCap = 4096;      // k_cvselect: keypoints kept in LDS (more: global scratch)
 
 struct CvLevel {
@@ -92,8 +92,8 @@ __device__ __forceinline__ void xcd_block(int& bx, int& by) {
 // cv::FAST(level, keypoints, 20, true) keeps p when score(p) >= 20 and score(p) > V(q) for the
 // 8 neighbours, V(q) = score(q) if q is a corner at 20, else 0 (fast.cpp); then
 // runByImageBorder drops every keypoint outside [edge, w-edge) x [edge, h-edge) (edge >= 18,
-// so every neighbour of a kept pixel is a detection pixel).  A 64 x 32 tile stages rows
-// Y0-4..Y0+35 and columns X0-8..X0+71 (8-byte loads); the V window is the tile plus a 1-px
+// so every neighbour of a kept pixel is a detection pixel).  A 64 x 64 tile stages rows
+// Y0-4..Y0+67 and columns X0-8..X0+71 (8-byte loads); the V window is the tile plus a 1-px
 // ring, restricted to [edge-1, w-edge] x [edge-1, h-edge].  The even-circle-point pretest runs
 // one pixel per lane with the compares as lane masks (fast_pretest), only its survivors are
 // queued (per wave, mbcnt ranks) and scored; the strict NMS is evaluated at the queued pixels
