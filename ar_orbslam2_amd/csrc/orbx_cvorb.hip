@@ -58,7 +58,7 @@ __constant__ IcMask c_cv_icmask;                   // IC_Angle row masks (umax, 
 constexpr float kHarrisK = 0.04f;  // HARRIS_K (orb.cpp)
 constexpr int kFastTh = 20;        // computeKeyPoints: FastFeatureDetector fd(20, true)
 constexpr int kTW = 64, kTH = 64;  // k_cvfast tile
-constexpr int kSelCap = 4096;      // k_cvselect: keypoints kept in LDS (more: global scratch)
+constexpr int kSelCap = 2560;  // k_cvselect: keypoints kept in LDS (30 KB: 5 waves per CU; more: global)
 
 struct CvLevel {
   int w, h, pitch, pyr_off;
@@ -224,21 +224,26 @@ struct Stoppers {
 // The swap sequence of a two-scan partition of [lo, hi): the left scan stops at elements with
 // ls(e), the right scan at rs(e); pair k = (k-th left stopper from lo, k-th right stopper from
 // hi - 1) swaps while the first is left of the second.  Lpos / Rpos hold up to (hi-lo)/2 ints.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// (For up to 64 chunks of 64 elements the first pass leaves each chunk's two stopper ballots
+// in lane `chunk` and the second pass reads them back with v_readlane instead of reloading
+// and re-testing the elements.)
 template <class LS, class RS>
 __device__ Stoppers wave_partition(CvKey* a, int lo, int hi, uint32_t* Lpos, uint32_t* Rpos,
                                    LS ls, RS rs) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1, le = lt | (1ull << lane);
+  const int nch = (hi - lo + 63) >> 6;
+  const bool cached = nch <= 64;
+  uint64_t myL = 0, myR = 0;
   int rtot = 0;
-  for (int p0 = lo; p0 < hi; p0 += 64) {
-    const int p = p0 + lane;
-    bool f = false;
-    if (p < hi) f = rs(a[p]);
-    rtot += __popcll(__ballot(f));
-  }
-  int lcnt = 0, rcnt = 0, K = 0, cutL = INT_MAX, cutR = hi;
-  for (int p0 = lo; p0 < hi; p0 += 64) {
-    const int p = p0 + lane;
+  for (int c = 0; c < nch; c++) {
+    const int p = lo + 64 * c + lane;
     bool lf = false, rf = false;
     if (p < hi) {
       const CvKey e = a[p];
@@ -246,6 +251,27 @@ __device__ Stoppers wave_partition(CvKey* a, int lo, int hi, uint32_t* Lpos, uin
       rf = rs(e);
     }
     const uint64_t lb = __ballot(lf), rb = __ballot(rf);
+    rtot += __popcll(rb);
+    if (lane == c) myL = lb, myR = rb;
+  }
+  int lcnt = 0, rcnt = 0, K = 0, cutL = INT_MAX, cutR = hi;
+  for (int c = 0; c < nch; c++) {
+    const int p0 = lo + 64 * c, p = p0 + lane;
+    uint64_t lb, rb;
+    if (cached) {
+      lb = readlane64(myL, c);
+      rb = readlane64(myR, c);
+    } else {
+      bool lf = false, rf = false;
+      if (p < hi) {
+        const CvKey e = a[p];
+        lf = ls(e);
+        rf = rs(e);
+      }
+      lb = __ballot(lf);
+      rb = __ballot(rf);
+    }
+    const bool lf = (lb >> lane) & 1, rf = (rb >> lane) & 1;
     const int lrank = lcnt + __popcll(lb & lt);
     const int rrank = rtot - (rcnt + __popcll(rb & le));
     const bool lsw = lf && rrank > lrank;
@@ -459,64 +485,66 @@ __global__ __launch_bounds__(64) void k_cvselect(
 #pragma unroll
     for (int k = 0; k < 8; k++) wv[k] = (r < nr && k0 + k < nw) ? rp[k0 + k] : 0ull;
   };
-  int n = 0;
-  for (int r0 = 0; r0 < nr; r0 += 64) {
-    int c = 0;
-    for (int k0 = 0; k0 < nw; k0 += 8) {
-      uint64_t wv[8];
-      row_words(r0 + lane, k0, wv);
+  // raster order = row order (prefix over the rows' counts), then ascending x within a row;
+  // keys go to LDS while they fit (the usual case), else the pass is repeated into the
+  // level's global scratch
+  auto emit = [&](CvKey* dst, int cap) {
+    int base = 0;
+    for (int r0 = 0; r0 < nr; r0 += 64) {
+      const int r = r0 + lane;
+      int c = 0;
+      for (int k0 = 0; k0 < nw; k0 += 8) {
+        uint64_t wv[8];
+        row_words(r, k0, wv);
 #pragma unroll
-      for (int k = 0; k < 8; k++) c += __popcll(wv[k]);
+        for (int k = 0; k < 8; k++) c += __popcll(wv[k]);
+      }
+      const int incl = wave_incl_scan(c);
+      int pos = base + incl - c;
+      const uint32_t yk = (uint32_t)(L.ry0 + r) << 16;
+      if (base + __shfl(incl, 63) <= cap) {  // wave-uniform
+        for (int k0 = 0; k0 < nw; k0 += 8) {
+          uint64_t wv[8];
+          row_words(r, k0, wv);
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            uint64_t word = wv[k];
+            const int xb = 64 * (w0 + k0 + k);
+            while (word) {
+              const int bit = __ffsll((unsigned long long)word) - 1;
+              word &= word - 1;
+              dst[pos++].k = yk | (uint32_t)(xb + bit);
+            }
+          }
+        }
+      }
+      base += __shfl(incl, 63);
     }
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    n += c;
-  }
-  CvKey* a;
-  uint32_t *Lpos, *Rpos;
-  if (n <= kSelCap) {
-    a = (CvKey*)s_sel;
-    Lpos = (uint32_t*)(s_sel + 8 * kSelCap);
-    Rpos = Lpos + kSelCap / 2;
-  } else {
+    return base;
+  };
+  CvKey* a = (CvKey*)s_sel;
+  uint32_t* Lpos = (uint32_t*)(s_sel + 8 * kSelCap);
+  uint32_t* Rpos = Lpos + kSelCap / 2;
+  int n = emit(a, kSelCap);
+  if (n > kSelCap) {
     a = gcand + (int64_t)img * cand_total + L.cand_off;
     Lpos = gpos + (int64_t)img * cand_total + L.cand_off;
     Rpos = Lpos + (L.cand_cap + 1) / 2;
-  }
-  // raster order = row order (prefix over the rows' counts), then ascending x within a row
-  int base = 0;
-  for (int r0 = 0; r0 < nr; r0 += 64) {
-    const int r = r0 + lane;
-    int c = 0;
-    for (int k0 = 0; k0 < nw; k0 += 8) {
-      uint64_t wv[8];
-      row_words(r, k0, wv);
-#pragma unroll
-      for (int k = 0; k < 8; k++) c += __popcll(wv[k]);
-    }
-    const int incl = wave_incl_scan(c);
-    int pos = base + incl - c;
-    const uint32_t yk = (uint32_t)(L.ry0 + r) << 16;
-    for (int k0 = 0; k0 < nw; k0 += 8) {
-      uint64_t wv[8];
-      row_words(r, k0, wv);
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        uint64_t word = wv[k];
-        const int xb = 64 * (w0 + k0 + k);
-        while (word) {
-          const int bit = __ffsll((unsigned long long)word) - 1;
-          word &= word - 1;
-          a[pos++].k = yk | (uint32_t)(xb + bit);
-        }
-      }
-    }
-    base += __shfl(incl, 63);
+    emit(a, INT_MAX);
   }
   __syncthreads();
   const uint8_t* sm = smap + (int64_t)img * pyr_bytes + L.pyr_off;
-  for (int i = lane; i < n; i += 64) {
-    const uint32_t key = a[i].k;
-    a[i].r = (float)sm[(int64_t)(key >> 16) * L.pitch + (key & 0xFFFF)];
+  for (int i0 = 0; i0 < n; i0 += 256) {  // four loads in flight per lane
+    uint32_t key[4];
+    int sc[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) key[u] = i0 + 64 * u + lane < n ? a[i0 + 64 * u + lane].k : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      sc[u] = i0 + 64 * u + lane < n ? sm[(int64_t)(key[u] >> 16) * L.pitch + (key[u] & 0xFFFF)] : 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (i0 + 64 * u + lane < n) a[i0 + 64 * u + lane].r = (float)sc[u];
   }
   __syncthreads();
   const int feats = L.feats;

@@ -433,7 +433,7 @@ int orbx_marker_profile_read(orbx_marker* mk, int32_t cap, char (*names)[32], do
 /* ------------------------------------------------------------------ test hooks (not product API) */
 /* The device computeOrbDescriptor rotation (float)cos/sin((double)(deg * (float)(CV_PI/180.f)))
  * for n host angles; and KeyPointsFilter::retainBest (orb.cpp's nth_element + partition) run by
- * the k_cvselect wave routine on one host array (in LDS when n <= 4096 unless force_global),
+ * the k_cvselect wave routine on one host array (in LDS when n <= 2560 unless force_global),
  * resp/ids rewritten in the retained order.  Used by tests/test_cvorb_gpu.py. */
 int orbx_debug_cvorb_cossin(const float* deg, int64_t n, float* c, float* s);
 int orbx_debug_retain_best(float* resp, uint32_t* ids, int32_t n, int32_t n_points,
