@@ -334,7 +334,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128,
+    ap.add_argument("--batch", type=int, default=256,
                     help="frames per step per camera stream")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
