@@ -793,8 +793,11 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
 // candidate order inside every node (DivideNode is a stable partition), so a node's retained
 // key is its max response with the lowest candidate index.  The final-refinement sort uses the
 // canonical (size, creation sequence) tie-break.
-constexpr int kOctNT = 256;
-constexpr int kOctRegKeys = 16;  // keys per thread kept in registers (levels of <= 4096 candidates)
+constexpr int kOctNT = 256;           // threads per (image, level) workgroup, and
+constexpr int kOctNTBig = 1024;       // for frames whose level-0 octree frame exceeds
+constexpr int kOctBigArea = 1 << 20;  // kOctBigArea px: a workgroup holds ~100 KB of LDS there
+                                      // (one per CU), so 1024 threads run its key passes 4x wide
+constexpr int kOctRegKeys = 16;       // keys per thread per register chunk
 
 struct OctNodes {
   int16_t *x0, *x1, *y0, *y1;
@@ -817,58 +820,81 @@ struct OctCtx {
 };
 
 // Where the octree keeps its keys (packed x:12 y:12 score:8) and their node labels.  Thread t
-// owns keys t, t + kOctNT, t + 2 kOctNT, ...
-//   RegKeys<R>: in registers (n <= R * kOctNT): no LDS for keys, more workgroups per CU, and
-//               the quadrant of each key is kept from the count pass to the relabel pass;
-//   MemKeys:    in global scratch (larger levels).
-template <int R>
+// owns keys t, t + NT, t + 2 NT, ... (NT threads); they are processed in chunks of kOctRegKeys
+// held in registers, slot r of chunk c being key t + NT (c kOctRegKeys + r).
+//   RegKeys<NT>: one chunk (n <= kOctRegKeys NT): keys and labels stay in registers for the
+//                whole tree, and the quadrant of each key is kept from the count pass to the
+//                relabel pass;
+//   MemKeys<NT>: larger levels, keys and labels in global scratch (L2-resident): every pass
+//                loads a chunk with all its loads in flight, works on the registers and stores
+//                the labels back (one load latency per chunk instead of one per key).
+template <int NT>
 struct RegKeys {
   static constexpr bool kRegs = true;
-  uint32_t key[R];
-  int lab[R];
+  uint32_t key[kOctRegKeys];
+  int lab[kOctRegKeys];
   uint32_t q2 = 0;  // 2 bits per key: quadrant inside its node (valid when the node splits)
   int n;
-  __device__ int nj() const { return R; }
-  __device__ uint32_t get_key(int j) const { return key[j]; }
-  __device__ int get_lab(int j) const { return lab[j]; }
-  __device__ void set_lab(int j, int v) { lab[j] = v; }
-  __device__ void set_q(int j, int q) { q2 = (q2 & ~(3u << (2 * j))) | ((uint32_t)q << (2 * j)); }
-  __device__ int get_q(int j, const OctNodes&, int) const { return (q2 >> (2 * j)) & 3; }
+  __device__ int nchunks() const { return 1; }
+  __device__ void load(int, bool) {}
+  __device__ void store_labs(int) {}
+  __device__ uint32_t get_key(int r) const { return key[r]; }
+  __device__ int get_lab(int r) const { return lab[r]; }
+  __device__ void set_lab(int r, int v) { lab[r] = v; }
+  __device__ void set_q(int r, int q) { q2 = (q2 & ~(3u << (2 * r))) | ((uint32_t)q << (2 * r)); }
+  __device__ int get_q(int r, const OctNodes&, int) const { return (q2 >> (2 * r)) & 3; }
 };
 
+template <int NT>
 struct MemKeys {
   static constexpr bool kRegs = false;
   uint32_t* keys;
   int* labs;
   int n;
-  __device__ int nj() const { return (n + kOctNT - 1) / kOctNT; }
-  __device__ uint32_t get_key(int j) const { return keys[threadIdx.x + kOctNT * j]; }
-  __device__ int get_lab(int j) const { return labs[threadIdx.x + kOctNT * j]; }
-  __device__ void set_lab(int j, int v) { labs[threadIdx.x + kOctNT * j] = v; }
+  uint32_t key[kOctRegKeys];
+  int lab[kOctRegKeys];
+  __device__ int nchunks() const { return (n + NT * kOctRegKeys - 1) / (NT * kOctRegKeys); }
+  __device__ void load(int c, bool want_labs) {
+#pragma unroll
+    for (int r = 0; r < kOctRegKeys; r++) {
+      const int k = threadIdx.x + NT * (c * kOctRegKeys + r);
+      key[r] = k < n ? keys[k] : 0u;
+      lab[r] = (want_labs && k < n) ? labs[k] : 0;
+    }
+  }
+  __device__ void store_labs(int c) {
+#pragma unroll
+    for (int r = 0; r < kOctRegKeys; r++) {
+      const int k = threadIdx.x + NT * (c * kOctRegKeys + r);
+      if (k < n) labs[k] = lab[r];
+    }
+  }
+  __device__ uint32_t get_key(int r) const { return key[r]; }
+  __device__ int get_lab(int r) const { return lab[r]; }
+  __device__ void set_lab(int r, int v) { lab[r] = v; }
   __device__ void set_q(int, int) {}
-  __device__ int get_q(int j, const OctNodes& cur, int nd) const {
-    return quad_of(get_key(j), cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
+  __device__ int get_q(int r, const OctNodes& cur, int nd) const {
+    return quad_of(key[r], cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
   }
 };
 
-// loop over this thread's keys: f(j, k) for k = tid + kOctNT j < n (unrolled for registers)
-template <class KS, class F>
-__device__ __forceinline__ void each_key(KS& ks, F f) {
-  if constexpr (KS::kRegs) {
+// every key of this thread: f(r, k) for key k < n in register slot r; `want_labs` loads a
+// chunk's labels with its keys, `labs_out` stores them back after it (MemKeys only)
+template <int NT, class KS, class F>
+__device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, F f) {
+  const int nc = ks.nchunks();
+  for (int c = 0; c < nc; c++) {
+    ks.load(c, want_labs);
 #pragma unroll
-    for (int j = 0; j < ks.nj(); j++) {
-      const int k = threadIdx.x + kOctNT * j;
-      if (k < ks.n) f(j, k);
+    for (int r = 0; r < kOctRegKeys; r++) {
+      const int k = threadIdx.x + NT * (c * kOctRegKeys + r);
+      if (k < ks.n) f(r, k);
     }
-  } else {
-    for (int j = 0; j < ks.nj(); j++) {
-      const int k = threadIdx.x + kOctNT * j;
-      if (k < ks.n) f(j, k);
-    }
+    if (labs_out) ks.store_labs(c);
   }
 }
 
-template <class KS>
+template <int NT, class KS>
 __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, KS& ks,
                                             const uint32_t* keys_mem) {
   const int tid = threadIdx.x;
@@ -880,7 +906,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   int* oc = X.oc;
   // 2. initial nodes (ORBextractor.cc:530-567)
   const int nini = G.nini;
-  for (int i = tid; i < nini; i += kOctNT) {
+  for (int i = tid; i < nini; i += NT) {
     A.x0[i] = (int16_t)G.ini_x[i];
     A.x1[i] = (int16_t)G.ini_x[i + 1];
     A.y0[i] = 0;
@@ -889,7 +915,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
     A.seq[i] = i;
   }
   __syncthreads();
-  each_key(ks, [&](int j, int) {
+  each_key<NT>(ks, false, true, [&](int j, int) {
     const float x = (float)(ks.get_key(j) & 0xFFF);
     const int ni = min((int)(x / G.hx), nini - 1);
     ks.set_lab(j, ni);
@@ -897,17 +923,17 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   });
   __syncthreads();
   // drop empty initial nodes, keep order
-  for (int i = tid; i < nini; i += kOctNT) t1[i] = A.cnt[i] > 0;
+  for (int i = tid; i < nini; i += NT) t1[i] = A.cnt[i] > 0;
   __syncthreads();
-  int size = block_scan_excl<kOctNT>(t1, nini, s_tmp);
-  for (int i = tid; i < nini; i += kOctNT)
+  int size = block_scan_excl<NT>(t1, nini, s_tmp);
+  for (int i = tid; i < nini; i += NT)
     if (A.cnt[i] > 0) {
       const int j = t1[i];
       B.x0[j] = A.x0[i]; B.x1[j] = A.x1[i]; B.y0[j] = A.y0[i]; B.y1[j] = A.y1[i];
       B.cnt[j] = A.cnt[i]; B.seq[j] = A.seq[i];
     }
   __syncthreads();
-  each_key(ks, [&](int j, int) { ks.set_lab(j, t1[ks.get_lab(j)]); });
+  each_key<NT>(ks, true, true, [&](int j, int) { ks.set_lab(j, t1[ks.get_lab(j)]); });
   __syncthreads();
   OctNodes cur = B, nxt = A;
   int seqc = nini;
@@ -915,13 +941,12 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   const int N = G.nfeat;
   for (int iter = 0; iter < 4096; iter++) {
     const int prevSize = size;
-    for (int i = tid; i < 4 * size; i += kOctNT) cc[i] = 0;
+    for (int i = tid; i < 4 * size; i += NT) cc[i] = 0;
     __syncthreads();
     // quadrant counts; keys are in cell order, so a wave's keys usually share one node and the
     // four counts are added with one atomic each instead of one per key
     const int lane = tid & 63;
-    auto count_one = [&](int j) {
-      const int k = tid + kOctNT * j;
+    auto count_one = [&](int j, int k) {
       int nd = -1, q = -1;
       if (k < n) {
         nd = ks.get_lab(j);
@@ -944,12 +969,11 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         atomicAdd(&cc[4 * nd + q], 1);
       }
     };
-    // every lane runs every j (the ballots need the whole wave)
-    if constexpr (KS::kRegs) {
+    // every lane runs every slot (the ballots need the whole wave)
+    for (int c = 0; c < ks.nchunks(); c++) {
+      ks.load(c, true);
 #pragma unroll
-      for (int j = 0; j < ks.nj(); j++) count_one(j);
-    } else {
-      for (int j = 0; j < ks.nj(); j++) count_one(j);
+      for (int j = 0; j < kOctRegKeys; j++) count_one(j, tid + NT * (c * kOctRegKeys + j));
     }
     __syncthreads();
     int T, newSize, nToExpand;
@@ -957,7 +981,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       // outer pass (list order): one packed scan gives childPre (bits 0-19), the rank among
       // undivided nodes (20-39) and the total of children with > 1 key (40-)
       uint64_t* pk = X.pk;
-      for (int i = tid; i < size; i += kOctNT) {
+      for (int i = tid; i < size; i += NT) {
         const bool e = cur.cnt[i] > 1;
         uint64_t ne = 0, nx = 0;
         if (e) {
@@ -971,12 +995,12 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         pk[i] = ne | ((uint64_t)!e << 20) | (nx << 40);
       }
       __syncthreads();
-      const uint64_t tot = block_scan_excl64<kOctNT>(pk, size, X.s_tmp64);
+      const uint64_t tot = block_scan_excl64<NT>(pk, size, X.s_tmp64);
       T = (int)(tot & 0xFFFFF);
       newSize = T + (int)((tot >> 20) & 0xFFFFF);
       nToExpand = (int)(tot >> 40);
       // base: divided -> T-1-childPre (child j at base-j); else newpos
-      for (int i = tid; i < size; i += kOctNT) {
+      for (int i = tid; i < size; i += NT) {
         const uint64_t e = pk[i];
         const int pre = (int)(e & 0xFFFFF), ndr = (int)((e >> 20) & 0xFFFFF);
         t1[i] = pre;
@@ -985,7 +1009,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       __syncthreads();
     } else {
       int nexp_local = 0;
-      for (int i = tid; i < size; i += kOctNT) {
+      for (int i = tid; i < size; i += NT) {
         const bool e = cur.cnt[i] > 1;
         int ne = 0;
         if (e) {
@@ -994,10 +1018,10 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         }
         t1[i] = ne;
       }
-      nToExpand = block_sum<kOctNT>(nexp_local, s_tmp);
+      nToExpand = block_sum<NT>(nexp_local, s_tmp);
       // final refinement: visit expandable nodes by (size desc, seq desc)
       int E_local = 0;
-      for (int i = tid; i < size; i += kOctNT) {
+      for (int i = tid; i < size; i += NT) {
         if (cur.cnt[i] > 1) {
           const int ci = cur.cnt[i], si = cur.seq[i];
           int r = 0;
@@ -1010,16 +1034,16 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
           E_local++;
         }
       }
-      const int E = block_sum<kOctNT>(E_local, s_tmp);
+      const int E = block_sum<NT>(E_local, s_tmp);
       // per visiting rank: nonEmpty -> childPre (exclusive scan over visiting order); t2 reused
-      for (int v = tid; v < E; v += kOctNT) t2[v] = t1[t3[v]];
+      for (int v = tid; v < E; v += NT) t2[v] = t1[t3[v]];
       __syncthreads();
       if (tid == 0) s_misc[0] = E > 0 ? E - 1 : -1;
       __syncthreads();
-      const int Tall = block_scan_excl<kOctNT>(t2, E, s_tmp);
+      const int Tall = block_scan_excl<NT>(t2, E, s_tmp);
       (void)Tall;
       // cut = first v with size + childPre_v + ne_v - (v+1) >= N
-      for (int v = tid; v < E; v += kOctNT) {
+      for (int v = tid; v < E; v += NT) {
         const int ne = t1[t3[v]];
         if (size + t2[v] + ne - (v + 1) >= N) atomicMin(&s_misc[0], v);
       }
@@ -1036,29 +1060,29 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       // divided flag & childPre per node: reuse t1 (keep nonEmpty in cc) -> store childPre
       // in t1 for divided nodes; t2 becomes divided flag per node (indexed by node).
       // First move childPre (indexed by v) into a per-node array (t4 holds rank).
-      for (int i = tid; i < size; i += kOctNT) {
+      for (int i = tid; i < size; i += NT) {
         const bool e = cur.cnt[i] > 1;
         const int r = e ? t4[i] : -1;
         t4[i] = (e && r <= cut) ? r : -1;  // rank if divided, else -1
       }
       __syncthreads();
-      for (int i = tid; i < size; i += kOctNT) {
+      for (int i = tid; i < size; i += NT) {
         const int r = t4[i];
         t1[i] = r >= 0 ? t2[r] : 0;  // childPre
       }
       __syncthreads();
-      for (int i = tid; i < size; i += kOctNT) {
+      for (int i = tid; i < size; i += NT) {
         t2[i] = t4[i] >= 0;
         t3[i] = !(t4[i] >= 0);
       }
       __syncthreads();
-      const int nd_total = block_scan_excl<kOctNT>(t3, size, s_tmp);
+      const int nd_total = block_scan_excl<NT>(t3, size, s_tmp);
       (void)nd_total;
-      for (int i = tid; i < size; i += kOctNT) t4[i] = t2[i] ? T - 1 - t1[i] : T + t3[i];
+      for (int i = tid; i < size; i += NT) t4[i] = t2[i] ? T - 1 - t1[i] : T + t3[i];
       __syncthreads();
     }
     // write next node arrays: t2 = divided, t1 = childPre, t4 = base
-    for (int i = tid; i < size; i += kOctNT) {
+    for (int i = tid; i < size; i += NT) {
       if (t2[i]) {
         const int x0 = cur.x0[i], x1 = cur.x1[i], y0 = cur.y0[i], y1 = cur.y1[i];
         const int xm = x0 + (x1 - x0 + 1) / 2, ym = y0 + (y1 - y0 + 1) / 2;
@@ -1085,7 +1109,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       }
     }
     // relabel keys
-    each_key(ks, [&](int j, int) {
+    each_key<NT>(ks, true, true, [&](int j, int) {
       const int nd = ks.get_lab(j);
       if (t2[nd]) {
         const int q = ks.get_q(j, cur, nd);
@@ -1113,14 +1137,14 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   }
   // 3. retain the best key per node (max response, first in candidate order)
   unsigned* best = (unsigned*)t1;
-  for (int i = tid; i < size; i += kOctNT) best[i] = 0;
+  for (int i = tid; i < size; i += NT) best[i] = 0;
   __syncthreads();
-  each_key(ks, [&](int j, int k) {
+  each_key<NT>(ks, true, false, [&](int j, int k) {
     const uint32_t key = ks.get_key(j);
     atomicMax(&best[ks.get_lab(j)], ((key >> 24) << 24) | (0xFFFFFFu - (unsigned)k));
   });
   __syncthreads();
-  for (int i = tid; i < size; i += kOctNT) {
+  for (int i = tid; i < size; i += NT) {
     const int k = (int)(0xFFFFFFu - (best[i] & 0xFFFFFFu));
     outk[i] = keys_mem[k];
   }
@@ -1128,14 +1152,14 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
 }
 
 
-__global__ __launch_bounds__(kOctNT) void k_octree(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree(
     const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
     const CellGeom* __restrict__ cells, const uint32_t* __restrict__ cand, int cand_total,
     uint32_t* __restrict__ lin, int* __restrict__ label, uint32_t* __restrict__ okey,
-    int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
-    int key_cap) {
+    int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap) {
   extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ int s_tmp[kOctNT / 64 + 1];
+  __shared__ int s_tmp[NT / 64 + 1];
   __shared__ int s_misc[8];
   const int level = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
   const LevelGeom& G = lv[level];
@@ -1167,64 +1191,76 @@ __global__ __launch_bounds__(kOctNT) void k_octree(
   int* cpre = (int*)take(4 * (cell_cap + 1));
   uint64_t* pk = (uint64_t*)take(8 * NC);
   int* s_slot = (int*)take(4 * cell_cap);
-  uint16_t* own = (uint16_t*)take(2 * key_cap);
-  __shared__ uint64_t s_tmp64[kOctNT / 64 + 1];
+  __shared__ uint64_t s_tmp64[NT / 64 + 1];
 
   // 1. gather candidates of this level in cell order (vToDistributeKeys): counts and slots of
-  // every cell in one round of loads, each key's cell from an owner table, then every key
-  // load in flight at once
+  // every cell in one round of loads, each key's cell by a binary search of the cell starts
+  // (all searches of a thread in lockstep), then every key load of a chunk in flight at once
   const int* cntv = cell_counts + (int64_t)img * ncells + G.cell_begin;
-  for (int i = tid; i < G.ncells; i += kOctNT) {
+  for (int i = tid; i < G.ncells; i += NT) {
     cpre[i] = cntv[i];
     s_slot[i] = cells[G.cell_begin + i].slot_off;
   }
   __syncthreads();
-  const int n = block_scan_excl<kOctNT>(cpre, G.ncells, s_tmp);
-  const uint32_t* cb = cand + (int64_t)img * cand_total;
-  uint32_t* keys = lin + (int64_t)img * cand_total + G.cand_off;
-  int* lab = label + (int64_t)img * cand_total + G.cand_off;
-  if (n <= key_cap) {
-    for (int c = tid; c < G.ncells; c += kOctNT) {
-      const int e = c + 1 < G.ncells ? cpre[c + 1] : n;
-      for (int k = cpre[c]; k < e; k++) own[k] = (uint16_t)c;
-    }
-  } else {
-    const int wid = tid >> 6, lane = tid & 63;
-    for (int c = wid; c < G.ncells; c += kOctNT / 64) {
-      const int e = c + 1 < G.ncells ? cpre[c + 1] : n, o = cpre[c];
-      for (int i = lane; i < e - o; i += 64) keys[o + i] = cb[s_slot[c] + i];
-    }
-  }
+  const int n = block_scan_excl<NT>(cpre, G.ncells, s_tmp);
+  if (tid == 0) cpre[G.ncells] = n;  // cell c holds keys cpre[c] .. cpre[c + 1] - 1
   __syncthreads();
   uint32_t* outk = okey + (int64_t)img * kp_total + G.kp_off;
   if (n == 0) {
     if (tid == 0) *oc = 0;
     return;
   }
-  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, pk, s_tmp64, outk, oc};
-  if (n <= key_cap) {  // keys + labels in registers: every pass stays on-chip
-    RegKeys<kOctRegKeys> ks;
-    ks.n = n;
+  const uint32_t* cb = cand + (int64_t)img * cand_total;
+  uint32_t* keys = lin + (int64_t)img * cand_total + G.cand_off;
+  int* lab = label + (int64_t)img * cand_total + G.cand_off;
+  int top = 1;  // largest power of two <= ncells
+  while (2 * top <= G.ncells) top *= 2;
+  // keys k0 + tid + NT j (j < kOctRegKeys), 0 past n; a key's cell is the last one starting at
+  // or before it (cells without keys share their successor's start)
+  auto load_keys = [&](int k0, uint32_t(&v)[kOctRegKeys]) {
+    int cs[kOctRegKeys];
+#pragma unroll
+    for (int j = 0; j < kOctRegKeys; j++) cs[j] = 0;
+    for (int st = top; st > 0; st >>= 1) {
+#pragma unroll
+      for (int j = 0; j < kOctRegKeys; j++) {
+        const int c = cs[j] + st;
+        if (c <= G.ncells && cpre[c] <= k0 + tid + NT * j) cs[j] = c;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kOctRegKeys; j++) {
-      const int k = tid + kOctNT * j;
-      uint32_t v = 0u;
-      if (k < n) {
-        const int c = own[k];
-        v = cb[s_slot[c] + k - cpre[c]];
-      }
-      ks.key[j] = v;
-      ks.lab[j] = 0;
+      const int k = k0 + tid + NT * j, c = cs[j];
+      v[j] = k < n ? cb[s_slot[c] + k - cpre[c]] : 0u;
     }
+  };
+  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, pk, s_tmp64, outk, oc};
+  if (n <= kOctRegKeys * NT) {  // keys + labels in registers: every pass stays on-chip
+    RegKeys<NT> ks;
+    ks.n = n;
+    load_keys(0, ks.key);
 #pragma unroll
     for (int j = 0; j < kOctRegKeys; j++) {  // the final lookup of retained keys reads lin
-      const int k = tid + kOctNT * j;
+      const int k = tid + NT * j;
+      ks.lab[j] = 0;
       if (k < n) keys[k] = ks.key[j];
     }
-    octree_core(G, X, ks, keys);
-  } else {
-    MemKeys ks{keys, lab, n};
-    octree_core(G, X, ks, keys);
+    octree_core<NT>(G, X, ks, keys);
+  } else {  // keys + labels in global scratch, processed in register chunks
+    for (int k0 = 0; k0 < n; k0 += NT * kOctRegKeys) {
+      uint32_t v[kOctRegKeys];
+      load_keys(k0, v);
+#pragma unroll
+      for (int j = 0; j < kOctRegKeys; j++) {
+        const int k = k0 + tid + NT * j;
+        if (k < n) keys[k] = v[j];
+      }
+    }
+    MemKeys<NT> ks;
+    ks.keys = keys;
+    ks.labs = lab;
+    ks.n = n;
+    octree_core<NT>(G, X, ks, keys);
   }
 }
 
@@ -1382,7 +1418,7 @@ struct orbx_plan {
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   size_t oct_smem = 0;
-  int key_cap = 0;
+  int oct_nt = 0;  // k_octree threads per workgroup (kOctNT or kOctNTBig)
   int cell_cap = 0;
   const uint8_t* last_in = nullptr;
   int last_n = 0;
@@ -1529,10 +1565,16 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                        P->d_cell_counts);
     pr.mark(P->stream, st_fb);
   }
-  hipLaunchKernelGGL(k_octree, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream, P->d_lv,
-                     P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total, P->d_lin,
-                     P->d_label, P->d_okey, P->d_ocount, g.kp_total, L, g.node_cap_max,
-                     P->cell_cap, P->key_cap);
+  if (P->oct_nt == kOctNTBig)
+    hipLaunchKernelGGL(k_octree<kOctNTBig>, dim3(L, n), dim3(kOctNTBig), P->oct_smem, P->stream,
+                       P->d_lv, P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total,
+                       P->d_lin, P->d_label, P->d_okey, P->d_ocount, g.kp_total, L,
+                       g.node_cap_max, P->cell_cap);
+  else
+    hipLaunchKernelGGL(k_octree<kOctNT>, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream,
+                       P->d_lv, P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total,
+                       P->d_lin, P->d_label, P->d_okey, P->d_ocount, g.kp_total, L,
+                       g.node_cap_max, P->cell_cap);
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
@@ -1627,14 +1669,15 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   const size_t NC = (size_t)g.node_cap_max;
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  P->key_cap = kOctRegKeys * kOctNT;
+  P->oct_nt = (int64_t)g.lv[0].W * g.lv[0].H > kOctBigArea ? kOctNTBig : kOctNT;
   P->oct_smem = 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
-                r16(4 * (P->cell_cap + 1)) + r16(8 * NC) + r16(4 * P->cell_cap) +
-                r16(2 * P->key_cap);
+                r16(4 * (P->cell_cap + 1)) + r16(8 * NC) + r16(4 * P->cell_cap);
   if (P->oct_smem > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
-  // keys and labels live in registers (up to kOctRegKeys * kOctNT per level, with a 16-bit
-  // owner cell per key in LDS for the gather) or in global scratch
-  if (hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+  // keys and labels live in registers (up to kOctRegKeys * oct_nt per level) or in global
+  // scratch
+  const void* oct_fn = P->oct_nt == kOctNTBig ? (const void*)k_octree<kOctNTBig>
+                                              : (const void*)k_octree<kOctNT>;
+  if (hipFuncSetAttribute(oct_fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)P->oct_smem) != hipSuccess)
     return fail(ORBX_EDEVICE);
   *out = P;

@@ -178,48 +178,35 @@ __device__ __forceinline__ int lane_rank(uint64_t m) {
 
 // OpenCV 2.4 cornerScore<16> at (x, y) of a u8 image with row stride `stride`:
 // the pixel is a FAST-9/16 corner at threshold t iff the score is >= t.
+// With d_k = v - c_k an arc's min d is v - max c and its max d is v - min c, so the score is
+// max(v - min_k maxc_k, max_k minc_k - v) - 1 over the 16 arcs of 9 points: the arc minima run
+// on packed u16 pairs (c, 255 - c), one v_pk_min_u16 per point and window step giving min c and
+// 255 - max c together.
+typedef unsigned short fast_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, int y) {
   const uint8_t* c = s + y * stride + x;
   const int v = c[0];
-  int d[16];
-  d[0] = v - c[3 * stride];
-  d[1] = v - c[3 * stride + 1];
-  d[2] = v - c[2 * stride + 2];
-  d[3] = v - c[stride + 3];
-  d[4] = v - c[3];
-  d[5] = v - c[-stride + 3];
-  d[6] = v - c[-2 * stride + 2];
-  d[7] = v - c[-3 * stride + 1];
-  d[8] = v - c[-3 * stride];
-  d[9] = v - c[-3 * stride - 1];
-  d[10] = v - c[-2 * stride - 2];
-  d[11] = v - c[-stride - 3];
-  d[12] = v - c[-3];
-  d[13] = v - c[stride - 3];
-  d[14] = v - c[2 * stride - 2];
-  d[15] = v - c[3 * stride - 1];
-  // sliding min/max over 9 consecutive circle points (wrap-around)
-  int mn2[16], mx2[16];
+  const int px[16] = {c[3 * stride],  c[3 * stride + 1],  c[2 * stride + 2],  c[stride + 3],
+                      c[3],           c[-stride + 3],     c[-2 * stride + 2], c[-3 * stride + 1],
+                      c[-3 * stride], c[-3 * stride - 1], c[-2 * stride - 2], c[-stride - 3],
+                      c[-3],          c[stride - 3],      c[2 * stride - 2],  c[3 * stride - 1]};
+  fast_u16x2 p[16], m2[16], m4[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn2[k] = min(d[k], d[(k + 1) & 15]);
-    mx2[k] = max(d[k], d[(k + 1) & 15]);
-  }
-  int mn4[16], mx4[16];
+  for (int k = 0; k < 16; k++)  // c | (255 - c) << 16 = 0xFF0000 - 65535 c: one v_mad_i32_i24
+    p[k] = __builtin_bit_cast(fast_u16x2, (uint32_t)(__mul24(px[k], -65535) + 0xFF0000));
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-  }
-  int q0 = -1000, q1 = 1000;
+  for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(p[k], p[(k + 1) & 15]);
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int a = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-    const int b = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-    q0 = max(q0, a);
-    q1 = min(q1, b);
-  }
-  return max(q0, -q1) - 1;
+  for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+  fast_u16x2 r = {0, 0};
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    r = __builtin_elementwise_max(
+        r, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]),
+                                     p[(k + 8) & 15]));
+  const uint32_t R = __builtin_bit_cast(uint32_t, r);
+  // low half: max_k (min c over arc k); high half: 255 - min_k (max c over arc k)
+  return max(v + (int)(R >> 16) - 255, (int)(R & 0xFFFFu) - v) - 1;
 }
 
 // Stage timing with HIP events recorded on the launching stream between kernels.  Marks are

@@ -352,8 +352,10 @@ def main():
                     help="steps of the single-stream roofline pass (per-kernel HIP events)")
     args = ap.parse_args()
     if args.pmc_dir is None:  # the committed PMC passes of this config's default command
+        # (never another config's: a missing directory reports traffic / VALU floor as null)
         args.pmc_dir = os.path.join(ROOT, "profiles",
-                                    "r01_pmc_ar" if args.config == "AR" else "r01_pmc")
+                                    "r01_pmc" if args.config == "C2" else
+                                    "r01_pmc_" + args.config.lower())
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

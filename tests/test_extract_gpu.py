@@ -109,3 +109,12 @@ def test_min_threshold_fallback_cells(contrast):
     img[:, :320] = 128 + (img[:, :320] - 128) // contrast
     kps = _compare(img.astype(np.uint8), 1000)
     assert len(kps) > 300
+
+
+@pytest.mark.parametrize("w,h,nf", [(1920, 1080, 4000), (1280, 960, 2000), (1024, 768, 1500)])
+def test_noise_octree_chunked_levels(w, h, nf):
+    """Uniform noise: tens of thousands of FAST candidates per level, so k_octree runs its
+    chunked global-scratch path (levels above 16 keys per thread) next to the register path,
+    with 1024-thread (level-0 octree frame above 1 Mpx) and 256-thread workgroups."""
+    rng = np.random.default_rng(w + h)
+    _compare(rng.integers(0, 256, (h, w), dtype=np.uint8), nf)
