@@ -622,6 +622,10 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
 }
 
 constexpr int kCompactCap = 30 * 30;  // survivors of a cell <= slot_cap (cells < 60 x 60)
+constexpr int kCompactK = 4;          // cells per wave: each round of loads covers all of them
+// k_fast_fallback queue counters, [2 img + fb_big] kFbStride ints apart: one 128-B line each (the
+// queues fill with one atomic per wave; on a shared line those atomics serialize)
+constexpr int kFbStride = 32;
 __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict__ vmap,
                                                       int64_t pyr_bytes,
                                                       const uint64_t* __restrict__ bitmaps,
@@ -632,60 +636,114 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
                                                       int* __restrict__ cell_counts,
                                                       int* __restrict__ fb_count,
                                                       int* __restrict__ fb_list) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bx, img;
   xcd_block(bx, img);
-  const int ci = bx * 4 + wid;
-  if (ci >= ncells) return;
-  const CellGeom C = cells[ci];  // one dependent load: everything below addresses from it
-  const int dr = C.y1 - C.y0 - 6, cx0 = C.x0 + 3, width = C.x1 - 3 - cx0;  // width <= 60
-  int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
-  if (dr <= 0 || width <= 0) {
-    if (lane == 0) *cnt_out = 0;
-    return;
-  }
-  const int sh = cx0 & 63;
-  const uint64_t wmask = width >= 64 ? ~0ull : ((1ull << width) - 1);
-  uint64_t bits = 0;
-  if (lane < dr) {
-    const uint64_t* row = bitmaps + (int64_t)img * bm_words + C.bm_row0 + lane * C.bm_wpr;
-    bits = row[0] >> sh;
-    if (sh && sh + width > 64) bits |= row[1] << (64 - sh);
-    bits &= wmask;
-  }
-  if (__ballot(bits != 0) == 0) {  // no keypoint at iniThFAST: k_fast_fallback takes the cell
-    if (lane == 0) {  // queue fb_big of the image: counts [2 img + fb_big], lists of ncells
-      const int qi = 2 * img + C.fb_big;
-      fb_list[(int64_t)qi * ncells + atomicAdd(fb_count + qi, 1)] = ci;
-    }
-    return;
-  }
-  // raster order: row prefix sum, then ascending x.  Each row lists its survivors (row, column)
-  // at its prefix slots in LDS; then lane s takes survivor s: one round of parallel V loads and
-  // coalesced key stores per 64 survivors.
-  __shared__ uint16_t s_rc[4][kCompactCap];
-  uint16_t* rc = s_rc[wid];
-  const int cnt = __popcll(bits);
-  int incl = cnt;
+  const int c0 = (bx * 4 + wid) * kCompactK;  // cells c0 .. c0 + kCompactK - 1 of this wave
+  if (c0 >= ncells) return;
+  // the cell's survivors (row << 8 | column) at their raster slots
+  __shared__ uint16_t s_rc[4][kCompactK][kCompactCap];
+  // round 1: the geometry of every cell of the wave
+  CellGeom C[kCompactK];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int n = __shfl_up(incl, o);
-    if (lane >= o) incl += n;
-  }
-  const int nout = __shfl(incl, 63);  // <= slot_cap <= kCompactCap
-  for (int pos = incl - cnt; bits; bits &= bits - 1)
-    rc[pos++] = (uint16_t)((lane << 8) | __builtin_ctzll(bits));
-  uint32_t* out = cand + (int64_t)img * cand_total + C.slot_off;
-  const uint8_t* V = vmap + (int64_t)img * pyr_bytes + C.v_row0;
-  for (int s0 = 0; s0 < nout; s0 += 64) {
-    const int si = s0 + lane;
-    if (si < nout) {
-      const int e = rc[si], r = e >> 8, k = e & 0xFF;
-      out[si] = cand_key(cx0 + k, C.y0 + 3 + r, (int)V[r * C.pitch + k]);
+  for (int j = 0; j < kCompactK; j++) C[j] = cells[min(c0 + j, ncells - 1)];
+  // round 2: every keep row (lane = detection row) of every cell
+  uint64_t bits[kCompactK];
+  int live[kCompactK];  // 1: in range with a detection region
+#pragma unroll
+  for (int j = 0; j < kCompactK; j++) {
+    const int dr = C[j].y1 - C[j].y0 - 6, cx0 = C[j].x0 + 3, width = C[j].x1 - 3 - cx0;  // <= 60
+    live[j] = c0 + j < ncells && dr > 0 && width > 0;
+    bits[j] = 0;
+    if (live[j] && lane < dr) {
+      const int sh = cx0 & 63;
+      const uint64_t* row = bitmaps + (int64_t)img * bm_words + C[j].bm_row0 + lane * C[j].bm_wpr;
+      uint64_t b = row[0] >> sh;
+      if (sh && sh + width > 64) b |= row[1] << (64 - sh);
+      bits[j] = b & (width >= 64 ? ~0ull : ((1ull << width) - 1));
     }
   }
-  if (lane == 0) *cnt_out = nout;
+  // raster order: row prefix sum, then ascending x; an empty cell is queued for
+  // k_fast_fallback (which writes its count), a cell outside the detection region counts 0
+  int nout[kCompactK], fbq[kCompactK];  // fbq: fallback queue of an empty cell, else -1
+#pragma unroll
+  for (int j = 0; j < kCompactK; j++) {
+    nout[j] = 0;
+    fbq[j] = -1;
+    const int ci = c0 + j;
+    if (ci >= ncells) continue;
+    int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
+    if (!live[j]) {
+      if (lane == 0) *cnt_out = 0;
+      continue;
+    }
+    uint64_t b = bits[j];
+    if (__ballot(b != 0) == 0) {  // no keypoint at iniThFAST: k_fast_fallback takes the cell
+      fbq[j] = C[j].fb_big;
+      continue;
+    }
+    const int cnt = __popcll(b);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int nn = __shfl_up(incl, o);
+      if (lane >= o) incl += nn;
+    }
+    nout[j] = __shfl(incl, 63);  // <= slot_cap <= kCompactCap
+    uint16_t* rc = s_rc[wid][j];
+    for (int pos = incl - cnt; b; b &= b - 1)
+      rc[pos++] = (uint16_t)((lane << 8) | __builtin_ctzll(b));
+    if (lane == 0) *cnt_out = nout[j];
+  }
+  // the empty cells join queue fb_big of the image (lists of ncells entries): one atomic per
+  // queue and wave
+#pragma unroll
+  for (int bq = 0; bq < 2; bq++) {
+    int m = 0;
+#pragma unroll
+    for (int j = 0; j < kCompactK; j++) m += fbq[j] == bq;
+    if (m == 0) continue;
+    const int qi = 2 * img + bq;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(fb_count + qi * kFbStride, m);
+    base = __shfl(base, 0);
+#pragma unroll
+    for (int j = 0; j < kCompactK; j++)
+      if (fbq[j] == bq) {
+        if (lane == 0) fb_list[(int64_t)qi * ncells + base] = c0 + j;
+        base++;
+      }
+  }
+  // round 3 (per 64 survivors of each cell): lane s takes survivor s of every cell, all V
+  // loads in flight, then the coalesced key stores
+  int nmax = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactK; j++) nmax = max(nmax, nout[j]);
+  for (int s0 = 0; s0 < nmax; s0 += 64) {
+    const int si = s0 + lane;
+    uint32_t key[kCompactK];
+#pragma unroll
+    for (int j = 0; j < kCompactK; j++) {
+      key[j] = 0;
+      if (si < nout[j]) {
+        const int e = s_rc[wid][j][si], r = e >> 8, k = e & 0xFF;
+        const uint8_t* V = vmap + (int64_t)img * pyr_bytes + C[j].v_row0;
+        key[j] = cand_key(C[j].x0 + 3 + k, C[j].y0 + 3 + r, (int)V[r * C[j].pitch + k]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kCompactK; j++)
+      if (si < nout[j]) cand[(int64_t)img * cand_total + C[j].slot_off + si] = key[j];
+  }
 }
+
+// a CellGeom as dwords (moved between lanes with readlane)
+constexpr int kCellWords = (int)(sizeof(CellGeom) / 4);
+struct CellWords {
+  uint32_t w[kCellWords];
+};
+static_assert(sizeof(CellWords) == sizeof(CellGeom), "CellGeom is whole dwords");
 
 // ---- k_fast_fallback: the cells queued by k_fast_compact, one wave each (kFbWG workgroups
 // per image walk the queue): cv::FAST with NMS at minThFAST on the cell image
@@ -700,7 +758,6 @@ constexpr int kFbWG = 16;  // workgroups per image
 template <int RS, int MAXR>
 __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict__ pyr,
                                                        int64_t pyr_bytes,
-                                                       const LevelGeom* __restrict__ lv,
                                                        const CellGeom* __restrict__ cells,
                                                        int ncells, const int* __restrict__ fb_count,
                                                        const int* __restrict__ fb_list, int min_th,
@@ -715,73 +772,90 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int img = blockIdx.y;
   const int qi = 2 * img + (RS > 44);  // this instance's queue (k_fast_compact)
-  const int nfb = fb_count[qi];
+  const int nfb = fb_count[qi * kFbStride];
   uint8_t* S = s_src[wid];
   uint8_t* V = s_vv[wid];
   uint16_t* q = s_q[wid];
   const int t1 = max(min_th, 1);
-  for (int k = blockIdx.x * 4 + wid; k < nfb; k += gridDim.x * 4) {  // wave-uniform
-    const int ci = fb_list[(int64_t)qi * ncells + k];
-    const CellGeom C = cells[ci];
-    const LevelGeom& G = lv[C.level];
-    const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
-    const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3 (fb_big)
-    const int dr = rows - 6, cw = cols - 6;            // > 0 (k_fast_compact)
-    // stage the ROI as aligned dwords (its first pixel lands at byte sh of each staged row;
-    // the 64-B pitch covers the last dword), four loads in flight per lane; zero the V map
-    // (rows dr + 2, columns cw + 2 with the ring)
-    const int a0 = C.x0 & ~3, sh = C.x0 & 3, words = (sh + cols + 3) >> 2;  // <= RS / 4
-    const uint8_t* srow = src + (int64_t)C.y0 * G.pitch + a0;
-    const int items = rows * words;
-    const float inv = 1.0f / (float)words;
-    for (int i0 = lane; i0 < items; i0 += 256) {
-      uint32_t v[4];
-      int rr[4], cc[4];
+  const int wv = blockIdx.x * 4 + wid, nw = gridDim.x * 4;  // wave-uniform
+  for (int kb = wv; kb < nfb; kb += 64 * nw) {
+    // this wave's next (up to) 64 queued cells in one round of loads: lane j holds queue entry
+    // kb + j nw and its CellGeom; iteration `it` reads its cell's fields from lane it
+    const int kl = kb + lane * nw;
+    int cil = 0;
+    CellWords gw = {};
+    if (kl < nfb) {
+      cil = fb_list[(int64_t)qi * ncells + kl];
+      gw = ((const CellWords*)cells)[cil];
+    }
+    const int nit = min(64, (nfb - kb + nw - 1) / nw);
+    for (int it = 0; it < nit; it++) {
+      const int ci = __builtin_amdgcn_readlane(cil, it);
+      CellWords cwd;
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        py_divmod(min(i0 + 64 * u, items - 1), words, inv, rr[u], cc[u]);
-        v[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr[u], G.pitch) + 4 * cc[u]);
+      for (int w = 0; w < kCellWords; w++) cwd.w[w] = __builtin_amdgcn_readlane(gw.w[w], it);
+      const CellGeom C = __builtin_bit_cast(CellGeom, cwd);
+      // the ROI origin (x0, y0) sits 3 rows and 3 columns before the first detection pixel
+      const uint8_t* src = pyr + (int64_t)img * pyr_bytes +  // the level's pixel (0, 0)
+                           (C.v_row0 - (C.y0 + 3) * C.pitch - (C.x0 + 3));
+      const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3 (fb_big)
+      const int dr = rows - 6, cw = cols - 6;            // > 0 (k_fast_compact)
+      // stage the ROI as aligned dwords (its first pixel lands at byte sh of each staged row;
+      // the 64-B pitch covers the last dword), four loads in flight per lane; zero the V map
+      // (rows dr + 2, columns cw + 2 with the ring)
+      const int a0 = C.x0 & ~3, sh = C.x0 & 3, words = (sh + cols + 3) >> 2;  // <= RS / 4
+      const uint8_t* srow = src + (int64_t)C.y0 * C.pitch + a0;
+      const int items = rows * words;
+      const float inv = 1.0f / (float)words;
+      for (int i0 = lane; i0 < items; i0 += 256) {
+        uint32_t v[4];
+        int rr[4], cc[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          py_divmod(min(i0 + 64 * u, items - 1), words, inv, rr[u], cc[u]);
+          v[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr[u], C.pitch) + 4 * cc[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) asm volatile("" : "+v"(v[u]));
+#pragma unroll
+        for (int u = 0; u < 4; u++) *(uint32_t*)(S + rr[u] * RS + 4 * cc[u]) = v[u];
       }
-#pragma unroll
-      for (int u = 0; u < 4; u++) asm volatile("" : "+v"(v[u]));
-#pragma unroll
-      for (int u = 0; u < 4; u++) *(uint32_t*)(S + rr[u] * RS + 4 * cc[u]) = v[u];
+      for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
+      const uint8_t* Sx = S + sh;  // pixel (r, c) of the ROI at Sx[r * RS + c]
+      const bool half = cw <= 32;  // wave-uniform
+      const int col = half ? lane & 31 : lane, sub = half ? lane >> 5 : 0, step = half ? 2 : 1;
+      // every candidate of the cell stays queued (row << 6 | column): scored in batches of 64,
+      // then the NMS runs at the queued pixels only (all others have V = 0)
+      int nq = 0;
+      for (int r0 = 0; r0 < dr; r0 += step) {
+        const int r = r0 + sub;
+        const uint64_t ok = __ballot(col < cw && r < dr);
+        const uint64_t pass = fast_pretest<RS>(Sx + min(r, dr - 1) * RS + col, min_th, ok);
+        q[(pass >> lane) & 1 ? nq + lane_rank(pass) : QCAP + lane] = (uint16_t)(r * 64 + col);
+        nq += __popcll(pass);
+      }
+      for (int j = lane; j < nq; j += 64) {
+        const int e = q[j], r = e >> 6, c = e & 63;
+        const int sc = fast_score(Sx, RS, c + 3, r + 3);
+        V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
+      }
+      if (lane < dr) s_rows[wid][lane] = 0;
+      // NMS at minThFAST; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
+      for (int j = lane; j < nq; j += 64) {
+        const int e = q[j], r = e >> 6, c = e & 63;
+        const uint8_t* p = V + (r + 1) * RS + c + 1;
+        const int v = p[0];
+        const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
+                             max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
+        if (v > (nmax > min_th ? nmax : t1))
+          atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
+      }
+      const uint64_t bits = lane < dr ? s_rows[wid][lane] : 0;
+      const uint8_t* Vr = V + (lane + 1) * RS + 1;
+      compact_rows(bits, lane, C.y0 + 3 + lane, C.x0 + 3,
+                   cand + (int64_t)img * cand_total + C.slot_off,
+                   cell_counts + (int64_t)img * ncells + ci, [&](int kk) { return (int)Vr[kk]; });
     }
-    for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
-    const uint8_t* Sx = S + sh;  // pixel (r, c) of the ROI at Sx[r * RS + c]
-    const bool half = cw <= 32;  // wave-uniform
-    const int col = half ? lane & 31 : lane, sub = half ? lane >> 5 : 0, step = half ? 2 : 1;
-    // every candidate of the cell stays queued (row << 6 | column): scored in batches of 64,
-    // then the NMS runs at the queued pixels only (all others have V = 0)
-    int nq = 0;
-    for (int r0 = 0; r0 < dr; r0 += step) {
-      const int r = r0 + sub;
-      const uint64_t ok = __ballot(col < cw && r < dr);
-      const uint64_t pass = fast_pretest<RS>(Sx + min(r, dr - 1) * RS + col, min_th, ok);
-      q[(pass >> lane) & 1 ? nq + lane_rank(pass) : QCAP + lane] = (uint16_t)(r * 64 + col);
-      nq += __popcll(pass);
-    }
-    for (int j = lane; j < nq; j += 64) {
-      const int e = q[j], r = e >> 6, c = e & 63;
-      const int sc = fast_score(Sx, RS, c + 3, r + 3);
-      V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
-    }
-    if (lane < dr) s_rows[wid][lane] = 0;
-    // NMS at minThFAST; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
-    for (int j = lane; j < nq; j += 64) {
-      const int e = q[j], r = e >> 6, c = e & 63;
-      const uint8_t* p = V + (r + 1) * RS + c + 1;
-      const int v = p[0];
-      const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
-                           max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
-      if (v > (nmax > min_th ? nmax : t1))
-        atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
-    }
-    const uint64_t bits = lane < dr ? s_rows[wid][lane] : 0;
-    const uint8_t* Vr = V + (lane + 1) * RS + 1;
-    compact_rows(bits, lane, C.y0 + 3 + lane, C.x0 + 3,
-                 cand + (int64_t)img * cand_total + C.slot_off,
-                 cell_counts + (int64_t)img * ncells + ci, [&](int kk) { return (int)Vr[kk]; });
   }
 }
 
@@ -1551,16 +1625,17 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                        g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
                        g.ini_th);
     pr.mark(P->stream, st_fs);
-    launch_fill_u32((uint32_t*)P->d_fb_count, 2 * (size_t)n, 0u, P->stream);
-    hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 3) / 4, n), dim3(256), 0, P->stream,
+    launch_fill_u32((uint32_t*)P->d_fb_count, 2 * kFbStride * (size_t)n, 0u, P->stream);
+    hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 4 * kCompactK - 1) / (4 * kCompactK), n),
+                       dim3(256), 0, P->stream,
                        P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
                        P->d_fb_list);
     pr.mark(P->stream, st_fast);
     hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
-                       P->d_pyr, g.pyr_bytes, P->d_lv, P->d_cells, ncells, P->d_fb_count,
+                       P->d_pyr, g.pyr_bytes, P->d_cells, ncells, P->d_fb_count,
                        P->d_fb_list, g.min_th, P->d_cand, g.cand_total, P->d_cell_counts);
     hipLaunchKernelGGL((k_fast_fallback<72, kCellMax>), dim3(kFbWG / 4, n), dim3(256), 0,
-                       P->stream, P->d_pyr, g.pyr_bytes, P->d_lv, P->d_cells, ncells,
+                       P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, ncells,
                        P->d_fb_count, P->d_fb_list, g.min_th, P->d_cand, g.cand_total,
                        P->d_cell_counts);
     pr.mark(P->stream, st_fb);
@@ -1650,7 +1725,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
-      dalloc(&P->d_fb_count, 2 * B) || dalloc(&P->d_fb_list, 2 * B * g.cells.size()) ||
+      dalloc(&P->d_fb_count, 2 * kFbStride * B) || dalloc(&P->d_fb_list, 2 * B * g.cells.size()) ||
       dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels) ||
       dalloc(&P->d_counts, B) || dalloc(&P->d_kps, B * g.kp_total) ||
       dalloc(&P->d_desc, B * g.kp_total * 32))
