@@ -6,13 +6,45 @@
 #   same command.  Everything lands in gpurun_out/$TAG/ with the layout of profiles/:
 #     <tag>_gpu_tests.txt, <tag>_bench.jsonl, <tag>_bench_ar.jsonl, <tag>_kernel_stats.csv,
 #     <tag>_kernel_stats_ar.csv, <tag>_pmc/{fetch_size,write_size,sq_counters}.csv, <tag>_pmc_ar/...
-# Usage: bash scripts/refresh_profiles.sh r01
+# With a second argument "configs" it does the same for C3 C4 C5 instead (PMC passes, bench line,
+# kernel stats: <tag>_pmc_c3/, <tag>_bench_c3.jsonl, <tag>_kernel_stats_c3.csv, ...), without the
+# tests; the two parts fit one gpurun call each.
+# Usage: bash scripts/refresh_profiles.sh r01 [configs]
 set -e -o pipefail
 TAG=${1:-r01}
+PART=${2:-main}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
-rm -rf $O && mkdir -p $O
 cd $R
+if [ "$PART" = configs ]; then
+  mkdir -p $O
+  for C in C3 C4 C5; do
+    c=$(echo $C | tr A-Z a-z)
+    (cd /tmp && export TMPDIR=/tmp && D=$O/${TAG}_pmc_$c && mkdir -p $D &&
+     timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/f -o run -- \
+       python3 $R/bench.py --config $C --no-cpu-baseline --steps 5 > /dev/null 2> $D/f.err &&
+     timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/w -o run -- \
+       python3 $R/bench.py --config $C --no-cpu-baseline --steps 5 > /dev/null 2> $D/w.err &&
+     timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
+       SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $D/s -o run -- \
+       python3 $R/bench.py --config $C --no-cpu-baseline --steps 5 > /dev/null 2> $D/s.err &&
+     cp $(find $D/f -name "*counter_collection.csv") $D/fetch_size.csv &&
+     cp $(find $D/w -name "*counter_collection.csv") $D/write_size.csv &&
+     cp $(find $D/s -name "*counter_collection.csv") $D/sq_counters.csv && rm -rf $D/f $D/w $D/s)
+    timeout -k 10 300 python -u bench.py --config $C --pmc-dir $O/${TAG}_pmc_$c \
+      > $O/${TAG}_bench_$c.jsonl 2> $O/bench_$c.err
+    cat $O/${TAG}_bench_$c.jsonl
+    (cd /tmp && export TMPDIR=/tmp &&
+     timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$c -o run -- \
+       python3 $R/bench.py --config $C --no-cpu-baseline --pmc-dir $O/${TAG}_pmc_$c \
+       > $O/${TAG}_bench_${c}_under_rocprof.jsonl 2> $O/trace_$c.err &&
+     cp $(find $O/trace_$c -name "*kernel_stats.csv") $O/${TAG}_kernel_stats_$c.csv &&
+     rm -rf $O/trace_$c)
+  done
+  echo done
+  exit 0
+fi
+rm -rf $O && mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
   > $O/${TAG}_gpu_tests.txt 2>&1
 tail -1 $O/${TAG}_gpu_tests.txt
