@@ -39,6 +39,7 @@ if [ "$PART" = configs ]; then
        python3 $R/bench.py --config $C --no-cpu-baseline --pmc-dir $O/${TAG}_pmc_$c \
        > $O/${TAG}_bench_${c}_under_rocprof.jsonl 2> $O/trace_$c.err &&
      cp $(find $O/trace_$c -name "*kernel_stats.csv") $O/${TAG}_kernel_stats_$c.csv &&
+     mkdir -p $O/traces && cp $(find $O/trace_$c -name "*kernel_trace.csv") $O/traces/kernel_trace_$c.csv &&
      rm -rf $O/trace_$c)
   done
   echo done

@@ -1,0 +1,116 @@
+"""Summaries of the committed round evidence under profiles/ (written by
+scripts/refresh_profiles.sh):
+
+  <tag>_roofline_check.txt  per config: the bench line's roofline kernel, its average launch
+                            duration from bench.py's HIP events (roofline pass, camera stream 0
+                            alone) against the rocprofv3 kernel trace of the same command
+                            (all dispatches: timed region with 3 concurrent streams + roofline
+                            pass; last 5 dispatches: the roofline pass itself)
+  <tag>_pmc_summary.txt     per config and kernel: trace average, waves, VALU / SALU / LDS
+                            instructions per wave, SQ_WAIT_ANY share, VALU issue floor and the
+                            FETCH_SIZE / WRITE_SIZE megabytes per dispatch
+
+Usage: python scripts/summarize_profiles.py [r01]
+"""
+from __future__ import annotations
+
+import collections
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = os.path.join(ROOT, "profiles")
+# config -> (suffix of the bench / kernel stats / trace files, suffix of the PMC dir)
+CONFIGS = {"C2": ("", ""), "AR": ("_ar", "_ar"), "C3": ("_c3", "_c3"), "C4": ("_c4", "_c4"),
+           "C5": ("_c5", "_c5")}
+VALU_US = 4 / (1024 * 2.4e3)  # us per wave-instruction at full issue (1024 SIMDs, 2.4 GHz)
+
+
+def short(name: str) -> str:
+    for ns in ("void ", "orbx::cvorb::", "orbx::", "(anonymous namespace)::"):
+        name = name.replace(ns, "")
+    return name.split("(")[0]
+
+
+def trace_durations(path):
+    d = collections.defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d[short(r["Kernel_Name"])].append(
+                (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    return {k: [dur for _, dur in sorted(v)] for k, v in d.items()}
+
+
+def counters(pmc_dir):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    calls = collections.defaultdict(set)
+    for fn in ("fetch_size.csv", "write_size.csv", "sq_counters.csv"):
+        path = os.path.join(pmc_dir, fn)
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                k = short(r["Kernel_Name"])
+                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                calls[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
+    return agg, calls
+
+
+def main(tag="r01"):
+    check, summ = [], []
+    for cfg, (sfx, psfx) in CONFIGS.items():
+        bench = os.path.join(P, f"{tag}_bench{sfx}.jsonl")
+        trace = os.path.join(P, "traces", f"kernel_trace{sfx}.csv")
+        if not (os.path.exists(bench) and os.path.exists(trace)):
+            continue
+        line = json.loads(open(bench).read().strip().splitlines()[-1])
+        rf = line["roofline"]
+        durs = trace_durations(trace)
+        k = rf["kernel"]
+        d = durs.get(k, [])
+        check.append(f"{cfg} ({line['config']['workload']}): {line['value']:.1f} frames/s")
+        check.append(f"  kernel {k}: {len(d)} dispatches")
+        if d:
+            check.append(f"    trace average, all dispatches (timed region with concurrent streams"
+                         f" + roofline pass): {sum(d) / len(d) / 1e3:.2f} us")
+            check.append(f"    trace average, last 5 dispatches (roofline pass, stream 0 alone): "
+                         f"{sum(d[-5:]) / len(d[-5:]) / 1e3:.2f} us")
+        check.append(f"    bench.py roofline avg_launch_us (HIP events, same pass): "
+                     f"{rf['avg_launch_us']:.2f} us")
+        vr = rf.get("valu_roofline") or {}
+        check.append(f"    HBM: achieved {rf.get('achieved')} GB/s of {rf['peak']} (frac "
+                     f"{rf.get('frac')}); VALU issue floor {vr.get('issue_floor_us')} us "
+                     f"(frac {vr.get('frac')})")
+        agg, calls = counters(os.path.join(P, f"{tag}_pmc{psfx}"))
+        summ.append(f"# {cfg}: per dispatch; us = rocprofv3 trace average of the bench command "
+                    f"(3 concurrent streams + roofline pass)")
+        summ.append(f"{'kernel':28s}{'us':>9s}{'waves':>9s}{'valu/w':>8s}{'salu/w':>8s}"
+                    f"{'lds/w':>7s}{'wait%':>6s}{'valu_us':>9s}{'fetchMB':>9s}{'writeMB':>9s}")
+        rows = []
+        for kn, dd in durs.items():
+            a = agg.get(kn, {})
+
+            def per(c):
+                n = len(calls.get((kn, c), ())) or 1
+                return a.get(c, 0.0) / n
+            w = per("SQ_WAVES") or 1.0
+            cyc = per("SQ_WAVE_CYCLES") or 1.0
+            rows.append((sum(dd) / len(dd) / 1e3, kn, per("SQ_WAVES"), per("SQ_INSTS_VALU") / w,
+                         per("SQ_INSTS_SALU") / w, per("SQ_INSTS_LDS") / w,
+                         100 * per("SQ_WAIT_ANY") / cyc, per("SQ_INSTS_VALU") * VALU_US,
+                         per("FETCH_SIZE") / 1024, per("WRITE_SIZE") / 1024))
+        for r in sorted(rows, reverse=True):
+            if r[1].startswith("__amd"):
+                continue
+            summ.append(f"{r[1][:27]:28s}{r[0]:9.1f}{r[2]:9.0f}{r[3]:8.0f}{r[4]:8.0f}{r[5]:7.0f}"
+                        f"{r[6]:6.0f}{r[7]:9.1f}{r[8]:9.1f}{r[9]:9.1f}")
+        summ.append("")
+    open(os.path.join(P, f"{tag}_roofline_check.txt"), "w").write("\n".join(check) + "\n")
+    open(os.path.join(P, f"{tag}_pmc_summary.txt"), "w").write("\n".join(summ))
+    print("\n".join(check))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
