@@ -69,24 +69,52 @@ def algorithmic_bytes(levels, n_kp, n_img):
     }
 
 
+# bytes per lane of the global loads of the kernels bench.py can name as roofline kernel (the
+# staged windows of k_fast_tile and k_cvfast: uint2 per lane); their stores are 8-B bitmap words
+# and 1-B survivor scores
+LOAD_WIDTH = {"k_fast_tile": 8, "k_cvfast": 8}
+
+
+def pmc_calibration():
+    """profiles/pmc_calibration.json (scripts/pmc_calibrate.py, tools/pmc_calib.hip): counter
+    bytes per true byte for streaming loads / stores of each width per lane, measured here."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "pmc_calibration.json")))
+    except (OSError, ValueError):
+        return None
+
+
 def pmc_traffic(pmc_dir, kernel):
     """HBM-side bytes per launch of `kernel` from separate rocprofv3 --pmc passes
-    (FETCH_SIZE, WRITE_SIZE, both in KB).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2→fabric
+    (FETCH_SIZE, WRITE_SIZE, both in KB).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2->fabric
     requests (Infinity-Cache hits included) and reads 1/2 of the bytes of 16-B-per-lane streaming
-    loads; these kernels use 1-4 B accesses, which the guide leaves uncalibrated, so the value is
-    reported uncorrected (FETCH_SIZE + WRITE_SIZE) x 1024."""
+    loads; other widths are to be calibrated in one's own access pattern, which
+    profiles/pmc_calibration.json holds (4- and 8-B loads: also 1/2; stores exact).  Returns
+    (bytes, note): FETCH_SIZE x 1024 / read factor of the kernel's load width +
+    WRITE_SIZE x 1024 / the 8-B store factor, or the uncorrected sum without a calibration."""
     import csv
     tot = {}
+    rel = os.path.relpath(pmc_dir, ROOT) if pmc_dir else None
     for name, counter in (("fetch_size.csv", "FETCH_SIZE"), ("write_size.csv", "WRITE_SIZE")):
-        path = os.path.join(pmc_dir, name)
+        path = os.path.join(pmc_dir, name) if pmc_dir else ""
         if not os.path.exists(path):
-            return None
+            return None, f"no PMC passes for this command ({rel})"
         vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
                 if r["Kernel_Name"].split("(")[0].endswith("::" + kernel) and r["Counter_Name"] == counter]
         if not vals:
-            return None
-        tot[counter] = sum(vals) / len(vals)
-    return round((tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024)
+            return None, f"kernel not in the PMC passes ({rel})"
+        tot[counter] = sum(vals) / len(vals) * 1024
+    cal = pmc_calibration()
+    w = LOAD_WIDTH.get(kernel)
+    rf = (cal or {}).get("read", {}).get(f"{w}B_per_lane") if w else None
+    wf = (cal or {}).get("write", {}).get("8B_per_lane")
+    if rf and wf:
+        return (round(tot["FETCH_SIZE"] / rf + tot["WRITE_SIZE"] / wf),
+                f"FETCH_SIZE*1024/{rf} + WRITE_SIZE*1024/{wf} per launch: rocprofv3 --pmc passes of "
+                f"this command ({rel}), corrected by profiles/pmc_calibration.json for {w}-B loads")
+    return (round(tot["FETCH_SIZE"] + tot["WRITE_SIZE"]),
+            f"uncorrected (FETCH_SIZE+WRITE_SIZE)*1024 per launch ({rel}; no calibration for "
+            f"this kernel's access width)")
 
 
 def pmc_valu(pmc_dir, kernel, avg_launch_us):
@@ -283,7 +311,8 @@ def run_marker(args, cfg, rank, world, local):
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 6),
-                    "traffic": pmc_traffic(args.pmc_dir, dom),
+                    "traffic": pmc_traffic(args.pmc_dir, dom)[0],
+                    "traffic_note": pmc_traffic(args.pmc_dir, dom)[1],
                     "avg_launch_us": round(avg_s * 1e6, 2),
                     "algorithmic_bytes_per_launch": a_bytes,
                     "valu_roofline": pmc_valu(args.pmc_dir, dom, avg_s * 1e6),
@@ -467,10 +496,8 @@ def main():
                     "achieved": round(achieved, 3) if achieved is not None else None,
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
-                    "traffic": pmc_traffic(args.pmc_dir, dom),
-                    "traffic_note": "uncorrected (FETCH_SIZE+WRITE_SIZE)*1024 per launch from "
-                                    "rocprofv3 --pmc passes of this command (" +
-                                    os.path.relpath(args.pmc_dir, ROOT) + ")",
+                    "traffic": pmc_traffic(args.pmc_dir, dom)[0],
+                    "traffic_note": pmc_traffic(args.pmc_dir, dom)[1],
                     "avg_launch_us": round(avg_s * 1e6, 2),
                     "algorithmic_bytes_per_launch": a_bytes,
                     "valu_roofline": pmc_valu(args.pmc_dir, dom, avg_s * 1e6),

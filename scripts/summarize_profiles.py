@@ -77,7 +77,12 @@ def main(tag="r01"):
                          f" + roofline pass): {sum(d) / len(d) / 1e3:.2f} us")
             check.append(f"    trace average, last 5 dispatches (roofline pass, stream 0 alone): "
                          f"{sum(d[-5:]) / len(d[-5:]) / 1e3:.2f} us")
-        check.append(f"    bench.py roofline avg_launch_us (HIP events, same pass): "
+        under = os.path.join(P, f"{tag}_bench{sfx}_under_rocprof.jsonl")
+        if os.path.exists(under):
+            ru = json.loads(open(under).read().strip().splitlines()[-1])["roofline"]
+            check.append(f"    bench.py roofline avg_launch_us of the traced run (HIP events, same "
+                         f"pass): {ru['avg_launch_us']:.2f} us")
+        check.append(f"    bench.py roofline avg_launch_us of the committed line (separate run): "
                      f"{rf['avg_launch_us']:.2f} us")
         vr = rf.get("valu_roofline") or {}
         check.append(f"    HBM: achieved {rf.get('achieved')} GB/s of {rf['peak']} (frac "
