@@ -40,6 +40,7 @@ EXPORTS = [
     "orbx_marker_destroy", "orbx_marker_set_target", "orbx_marker_run", "orbx_marker_sync",
     "orbx_marker_results", "orbx_marker_outputs", "orbx_marker_stream", "orbx_marker_profile",
     "orbx_marker_profile_read", "orbx_debug_cvorb_cossin", "orbx_debug_retain_best",
+    "orbx_debug_match_finish", "orbx_debug_sincosf",
 ]
 
 # == cv::DMatch (OpenCV 2.4): queryIdx, trainIdx, imgIdx, distance
@@ -105,14 +106,38 @@ class ProjLast(C.Structure):
 _lib = None
 
 
+def source_hash():
+    """(sha256 of the sources in liborbx.srclist order, the hash the build recorded)."""
+    import hashlib
+    lib_dir = os.path.dirname(LIB_PATH)
+    csrc = os.path.join(_HERE, "csrc")
+    try:
+        names = open(os.path.join(lib_dir, "liborbx.srclist")).read().split()
+        built = open(os.path.join(lib_dir, "liborbx.srchash")).read().strip()
+    except OSError:
+        return None, None
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(csrc, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest(), built
+
+
 def lib():
-    """Load liborbx.so; raises if the HIP library has not been built (no fallback)."""
+    """Load liborbx.so; raises if the HIP library has not been built (no fallback) or was built
+    from other sources than the ones in the tree (Makefile's liborbx.srchash)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; "
                 "g.build()'` (hipcc, gfx950). There is no CPU fallback.")
+        now, built = source_hash()
+        if now is None or now != built:
+            raise ImportError(
+                f"{LIB_PATH} is stale: it was built from other sources than "
+                f"ar_orbslam2_amd/csrc (hash {built} vs {now}); rebuild with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`.")
         _lib = C.CDLL(LIB_PATH)
         _lib.orbx_plan_stream.restype = C.c_void_p
         _lib.orbx_frames_stream.restype = C.c_void_p

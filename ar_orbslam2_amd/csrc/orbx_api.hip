@@ -17,6 +17,11 @@ extern "C" int orbx_plan_level_dims(const orbx_plan* P, int level, int* w, int* 
 extern "C" int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out,
                                         int64_t stride);
 
+// One ORBextractor: a batch-1 plan for the current image size plus pinned host staging.  A
+// call is one graph launch — pinned image -> HBM copy, the whole extraction, and one copy of
+// the plan's output block (count, keypoints, descriptors) back to pinned memory — and one
+// stream synchronisation; the caller's pageable image / output buffers are touched only by
+// host memcpy.
 struct orbx_extractor {
   orbx_params params{};
   Geometry tables;  // scale / sigma / features-per-level (no image size)
@@ -24,7 +29,23 @@ struct orbx_extractor {
   orbx_plan* plan = nullptr;
   int pw = 0, ph = 0;
   uint8_t* d_img = nullptr;
+  uint8_t* h_img = nullptr;  // pinned [h][w]
+  char* h_out = nullptr;     // pinned copy of the plan's output block
+  size_t kps_off = 0, desc_off = 0, out_bytes = 0;
+  GraphCache graphs;
   bool has_run = false;
+  void release() {
+    ORBX_RESOURCE_LOCK;
+    if (plan) graphs.clear((hipStream_t)orbx_plan_stream(plan));
+    if (plan) orbx_plan_destroy(plan);
+    if (d_img) (void)hipFree(d_img);
+    if (h_img) (void)hipHostFree(h_img);
+    if (h_out) (void)hipHostFree(h_out);
+    plan = nullptr;
+    d_img = h_img = nullptr;
+    h_out = nullptr;
+    pw = ph = 0;
+  }
 };
 
 extern "C" {
@@ -43,9 +64,9 @@ int orbx_extractor_create(const orbx_params* params, int hip_device, orbx_extrac
 }
 
 int orbx_extractor_destroy(orbx_extractor* ex) {
+  ORBX_RESOURCE_LOCK;
   if (!ex) return ORBX_OK;
-  if (ex->plan) orbx_plan_destroy(ex->plan);
-  if (ex->d_img) hipFree(ex->d_img);
+  ex->release();
   delete ex;
   return ORBX_OK;
 }
@@ -76,34 +97,47 @@ int orbx_extract(orbx_extractor* ex, const uint8_t* img, int32_t w, int32_t h, i
   if (!img || stride < w || cap < 0 || (cap > 0 && (!kps || !desc))) return ORBX_EINVAL;
   ORBX_HIP(hipSetDevice(ex->device));
   if (!ex->plan || ex->pw != w || ex->ph != h) {
-    if (ex->plan) orbx_plan_destroy(ex->plan);
-    ex->plan = nullptr;
-    if (ex->d_img) hipFree(ex->d_img);
-    ex->d_img = nullptr;
+    ORBX_RESOURCE_LOCK;
+    ex->release();
     int rc = orbx_plan_create(&ex->params, w, h, 1, ex->device, &ex->plan);
     if (rc != ORBX_OK) return rc;
-    ORBX_HIP(hipMalloc(&ex->d_img, (size_t)w * h));
+    plan_output_block(ex->plan, &ex->kps_off, &ex->desc_off, &ex->out_bytes);
+    if (hipMalloc(&ex->d_img, (size_t)w * h) != hipSuccess ||
+        hipHostMalloc(&ex->h_img, (size_t)w * h, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&ex->h_out, ex->out_bytes, hipHostMallocDefault) != hipSuccess) {
+      ex->release();
+      return ORBX_ENOMEM;
+    }
     ex->pw = w;
     ex->ph = h;
   }
   hipStream_t s = (hipStream_t)orbx_plan_stream(ex->plan);
-  ORBX_HIP(hipMemcpy2DAsync(ex->d_img, w, img, stride, w, h, hipMemcpyHostToDevice, s));
-  int rc = orbx_plan_extract(ex->plan, ex->d_img, 1);
-  if (rc != ORBX_OK) return rc;
   orbx_keypoint* d_kps;
   uint8_t* d_desc;
   int32_t* d_counts;
   orbx_plan_outputs(ex->plan, &d_kps, &d_desc, &d_counts);
-  int32_t n = 0;
-  ORBX_HIP(hipMemcpyAsync(&n, d_counts, 4, hipMemcpyDeviceToHost, s));
+  // the caller's image (a pageable cv::Mat) into pinned staging
+  if (stride == w) {
+    memcpy(ex->h_img, img, (size_t)w * h);
+  } else {
+    for (int y = 0; y < h; y++) memcpy(ex->h_img + (size_t)y * w, img + (size_t)y * stride, w);
+  }
+  int rc = run_graph(ex->graphs, s, ex->h_img, 1, [&]() -> int {
+    ORBX_HIP(hipMemcpyAsync(ex->d_img, ex->h_img, (size_t)w * h, hipMemcpyHostToDevice, s));
+    const int r = plan_enqueue(ex->plan, ex->d_img, 1, nullptr);
+    if (r != ORBX_OK) return r;
+    ORBX_HIP(hipMemcpyAsync(ex->h_out, d_counts, ex->out_bytes, hipMemcpyDeviceToHost, s));
+    return ORBX_OK;
+  });
+  if (rc != ORBX_OK) return rc;
   ORBX_HIP(hipStreamSynchronize(s));
   ex->has_run = true;
+  const int32_t n = *(const int32_t*)ex->h_out;
   *n_out = n;
   if (n > cap) return ORBX_ECAPACITY;
   if (n > 0) {
-    ORBX_HIP(hipMemcpyAsync(kps, d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipMemcpyAsync(desc, d_desc, (size_t)32 * n, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipStreamSynchronize(s));
+    memcpy(kps, ex->h_out + ex->kps_off, sizeof(orbx_keypoint) * n);
+    memcpy(desc, ex->h_out + ex->desc_off, (size_t)32 * n);
   }
   return ORBX_OK;
 }

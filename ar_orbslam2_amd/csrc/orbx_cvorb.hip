@@ -859,9 +859,7 @@ struct Plan {
   int *d_ocount = nullptr, *d_counts = nullptr;
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
-  hipGraphExec_t graph = nullptr;
-  const uint8_t* graph_in = nullptr;
-  int graph_n = -1;
+  GraphCache graphs;
   Profiler* prof = nullptr;  // owned by the caller
 };
 
@@ -874,7 +872,7 @@ int dalloc(T** p, size_t count) {
 
 void plan_destroy(Plan* P) {
   if (!P) return;
-  if (P->graph) (void)hipGraphExecDestroy(P->graph);
+  P->graphs.clear(P->stream);
   pyr_dev_destroy(&P->pd);
   void* bufs[] = {P->d_lv, P->d_tiles, P->d_pyr, P->d_blur, P->d_smap, P->d_bm, P->d_cand,
                   P->d_okey, P->d_pos, P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
@@ -1064,28 +1062,13 @@ int plan_run(Plan* P, const uint8_t* d_in, int n) {
   if (!P || !d_in || n <= 0 || n > P->max_batch) return ORBX_EINVAL;
   ORBX_HIP(hipSetDevice(P->device));
   if (P->prof && P->prof->on) return enqueue(P, d_in, n);
-  if (!(P->graph && P->graph_in == d_in && P->graph_n == n)) {
-    if (P->graph) {
-      hipGraphExecDestroy(P->graph);
-      P->graph = nullptr;
-    }
-    hipGraph_t gr;
-    ORBX_HIP(hipStreamBeginCapture(P->stream, hipStreamCaptureModeThreadLocal));
+  return run_graph(P->graphs, P->stream, d_in, n, [&] {
     Profiler* keep = P->prof;
     P->prof = nullptr;
-    int rc = enqueue(P, d_in, n);
+    const int rc = enqueue(P, d_in, n);
     P->prof = keep;
-    hipError_t e = hipStreamEndCapture(P->stream, &gr);
-    if (rc != ORBX_OK) return rc;
-    if (e != hipSuccess) return report_hip(e, "hipStreamEndCapture");
-    e = hipGraphInstantiate(&P->graph, gr, nullptr, nullptr, 0);
-    hipGraphDestroy(gr);
-    if (e != hipSuccess) return report_hip(e, "hipGraphInstantiate");
-    P->graph_in = d_in;
-    P->graph_n = n;
-  }
-  ORBX_HIP(hipGraphLaunch(P->graph, P->stream));
-  return ORBX_OK;
+    return rc;
+  });
 }
 
 int launch_bf(const uint8_t* d_query, int nq, const uint8_t* d_train, int64_t train_stride,
@@ -1167,6 +1150,7 @@ extern "C" {
 
 int orbx_cvorb_create(const orbx_cvorb_params* params, int32_t w, int32_t h, int32_t max_batch,
                       int hip_device, orbx_cvorb** out) {
+  ORBX_RESOURCE_LOCK;
   if (!params || !out || w <= 0 || h <= 0 || max_batch <= 0) return ORBX_EINVAL;
   *out = nullptr;
   if (!params_supported(*params)) return ORBX_EUNSUPPORTED;
@@ -1185,6 +1169,7 @@ int orbx_cvorb_create(const orbx_cvorb_params* params, int32_t w, int32_t h, int
 }
 
 int orbx_cvorb_destroy(orbx_cvorb* o) {
+  ORBX_RESOURCE_LOCK;
   if (!o) return ORBX_OK;
   plan_destroy(o->tp);
   plan_destroy(o->dp);
@@ -1403,6 +1388,7 @@ int orbx_debug_retain_best(float* resp, uint32_t* ids, int32_t n, int32_t n_poin
 
 int orbx_marker_create(const orbx_cvorb_params* params, int32_t w, int32_t h, int32_t max_batch,
                        int hip_device, orbx_marker** out) {
+  ORBX_RESOURCE_LOCK;
   if (!params || !out || w <= 0 || h <= 0 || max_batch <= 0) return ORBX_EINVAL;
   *out = nullptr;
   orbx_marker* M = new (std::nothrow) orbx_marker();
@@ -1423,6 +1409,7 @@ int orbx_marker_create(const orbx_cvorb_params* params, int32_t w, int32_t h, in
 }
 
 int orbx_marker_destroy(orbx_marker* M) {
+  ORBX_RESOURCE_LOCK;
   if (!M) return ORBX_OK;
   plan_destroy(M->plan);
   void* bufs[] = {M->d_target, M->d_best, M->d_matches, M->d_good, M->d_good_count};

@@ -1491,15 +1491,16 @@ struct orbx_plan {
   int *d_fb_count = nullptr, *d_fb_list = nullptr;  // k_fast_fallback queue per image
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
+  // counts, keypoints and descriptors share one allocation (d_counts is its base) so the
+  // drop-in path brings a frame's results back with one copy
+  size_t out_kps_off = 0, out_desc_off = 0, out_bytes = 0;
   size_t oct_smem = 0;
   int oct_nt = 0;  // k_octree threads per workgroup (kOctNT or kOctNTBig)
   int cell_cap = 0;
   const uint8_t* last_in = nullptr;
   int last_n = 0;
   // graph cache keyed by (input pointer, batch)
-  hipGraphExec_t graph = nullptr;
-  const uint8_t* graph_in = nullptr;
-  int graph_n = -1;
+  GraphCache graphs;
   Profiler prof;
 };
 
@@ -1668,6 +1669,7 @@ extern "C" {
 
 int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t max_batch,
                      int hip_device, orbx_plan** out) {
+  ORBX_RESOURCE_LOCK;
   if (!params || !out || w <= 0 || h <= 0 || max_batch <= 0) return ORBX_EINVAL;
   *out = nullptr;
   orbx_plan* P = new (std::nothrow) orbx_plan();
@@ -1726,10 +1728,19 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
       dalloc(&P->d_fb_count, 2 * kFbStride * B) || dalloc(&P->d_fb_list, 2 * B * g.cells.size()) ||
-      dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels) ||
-      dalloc(&P->d_counts, B) || dalloc(&P->d_kps, B * g.kp_total) ||
-      dalloc(&P->d_desc, B * g.kp_total * 32))
+      dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels))
     return fail(ORBX_ENOMEM);
+  {
+    auto r256 = [](size_t b) { return (b + 255) & ~size_t(255); };
+    P->out_kps_off = r256(4 * B);
+    P->out_desc_off = P->out_kps_off + r256(B * g.kp_total * sizeof(orbx_keypoint));
+    P->out_bytes = P->out_desc_off + B * g.kp_total * 32;
+    char* blk = nullptr;
+    if (dalloc(&blk, P->out_bytes)) return fail(ORBX_ENOMEM);
+    P->d_counts = (int*)blk;
+    P->d_kps = (orbx_keypoint*)(blk + P->out_kps_off);
+    P->d_desc = (uint8_t*)(blk + P->out_desc_off);
+  }
   auto up = [&](void* d, const void* h, size_t bytes) {
     return bytes ? hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) : hipSuccess;
   };
@@ -1760,11 +1771,12 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
 }
 
 int orbx_plan_destroy(orbx_plan* P) {
+  ORBX_RESOURCE_LOCK;
   if (!P) return ORBX_OK;
-  if (P->graph) hipGraphExecDestroy(P->graph);
+  P->graphs.clear(P->stream);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xtap,   P->d_ytap,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label, P->d_fb_count, P->d_fb_list,
-                  P->d_ocount, P->d_counts, P->d_kps, P->d_desc};
+                  P->d_ocount, P->d_counts /* base of kps and desc too */};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (P->stream) hipStreamDestroy(P->stream);
@@ -1784,25 +1796,8 @@ int orbx_plan_extract(orbx_plan* P, const uint8_t* d_imgs, int32_t n) {
   P->last_in = d_imgs;
   P->last_n = n;
   if (P->prof.on) return enqueue(P, d_imgs, n, &P->prof);
-  if (!(P->graph && P->graph_in == d_imgs && P->graph_n == n)) {
-    if (P->graph) {
-      hipGraphExecDestroy(P->graph);
-      P->graph = nullptr;
-    }
-    hipGraph_t gr;
-    ORBX_HIP(hipStreamBeginCapture(P->stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue(P, d_imgs, n, nullptr);
-    hipError_t e = hipStreamEndCapture(P->stream, &gr);
-    if (rc != ORBX_OK) return rc;
-    if (e != hipSuccess) return report_hip(e, "hipStreamEndCapture");
-    e = hipGraphInstantiate(&P->graph, gr, nullptr, nullptr, 0);
-    hipGraphDestroy(gr);
-    if (e != hipSuccess) return report_hip(e, "hipGraphInstantiate");
-    P->graph_in = d_imgs;
-    P->graph_n = n;
-  }
-  ORBX_HIP(hipGraphLaunch(P->graph, P->stream));
-  return ORBX_OK;
+  return run_graph(P->graphs, P->stream, d_imgs, n,
+                   [&] { return enqueue(P, d_imgs, n, nullptr); });
 }
 
 int orbx_plan_outputs(orbx_plan* P, orbx_keypoint** d_kps, uint8_t** d_desc, int32_t** d_counts) {
@@ -1864,7 +1859,38 @@ int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int
   return ORBX_OK;
 }
 
+// Test hook: the device sincosf port over a range of float bit patterns (orbx.h).
+__global__ void k_debug_sincosf(uint32_t lo, int64_t n, float* __restrict__ s, float* __restrict__ c) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float sv, cv;
+    orbx_sincosf(__uint_as_float(lo + (uint32_t)i), &sv, &cv);
+    s[i] = sv;
+    c[i] = cv;
+  }
+}
+
+int orbx_debug_sincosf(uint32_t lo, int64_t n, float* s, float* c) {
+  if (n < 0 || (n > 0 && (!s || !c)) || (uint64_t)lo + (uint64_t)n > 0x100000000ull)
+    return ORBX_EINVAL;
+  if (n == 0) return ORBX_OK;
+  float* d = nullptr;
+  {
+    ORBX_RESOURCE_LOCK;
+    ORBX_HIP(hipMalloc(&d, 8 * (size_t)n));
+  }
+  hipLaunchKernelGGL(k_debug_sincosf, dim3(4096), dim3(256), 0, 0, lo, n, d, d + n);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpy(s, d, 4 * (size_t)n, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(c, d + n, 4 * (size_t)n, hipMemcpyDeviceToHost);
+  {
+    ORBX_RESOURCE_LOCK;
+    (void)hipFree(d);
+  }
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "orbx_debug_sincosf");
+}
+
 }  // extern "C"
+
 
 namespace orbx {
 int plan_view(orbx_plan* P, PlanView* v) {
@@ -1879,6 +1905,13 @@ int plan_view(orbx_plan* P, PlanView* v) {
   v->d_pyr = P->d_pyr;
   v->pyr_bytes = P->g.pyr_bytes;
   v->d_lv = P->d_lv;
+  return ORBX_OK;
+}
+int plan_output_block(const orbx_plan* P, size_t* kps_off, size_t* desc_off, size_t* bytes) {
+  if (!P) return ORBX_EINVAL;
+  *kps_off = P->out_kps_off;
+  *desc_off = P->out_desc_off;
+  *bytes = P->out_bytes;
   return ORBX_OK;
 }
 int plan_enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {

@@ -76,17 +76,9 @@ struct orbx_frames {
   float F[9] = {0};
   float ex = 0, ey = 0;
   // graph cache, one executable graph per (input pointer, batch size)
-  struct GraphEntry {
-    const uint8_t* in;
-    int n;
-    hipGraphExec_t exec;
-  };
-  std::vector<GraphEntry> graphs;
+  GraphCache graphs;
   Profiler prof;
-  void drop_graphs() {
-    for (auto& g : graphs) hipGraphExecDestroy(g.exec);
-    graphs.clear();
-  }
+  void drop_graphs() { graphs.clear(v.stream); }
 };
 
 namespace {
@@ -130,6 +122,7 @@ int build_problems(orbx_frames* F, int n) {
     B.match = F->d_match + (int64_t)f * kp;
     B.count = F->d_bow_count + f;
     B.error = F->d_bow_count + F->bow_err_slot();
+    B.matched2 = nullptr;  // mode 0 reads the match array itself
     B.mode = 0;
     B.nnratio = F->bow_ratio;
     B.check_ori = F->bow_ori;
@@ -159,6 +152,7 @@ int build_problems(orbx_frames* F, int n) {
     T.m12 = F->d_m12 + (int64_t)f * kp;
     T.pairs = F->d_pairs + (int64_t)f * kp * 2;
     T.count = F->d_tri_count + f;
+    T.error = F->d_bow_count + F->bow_err_slot();
   }
   if (F->stereo) {
     std::vector<StereoProblem> sp(n);
@@ -237,6 +231,7 @@ extern "C" {
 static int frames_create(const orbx_params* p, int32_t w, int32_t h, int32_t max_batch,
                          const orbx_vocabulary* voc, int32_t levelsup, int stereo, float mb,
                          float mbf, int hip_device, orbx_frames** out) {
+  ORBX_RESOURCE_LOCK;
   if (!p || !out || !voc || levelsup < 0 || max_batch < 1) return ORBX_EINVAL;
   *out = nullptr;
   int voc_dev = 0;
@@ -317,6 +312,7 @@ int orbx_frames_create_stereo(const orbx_params* p, int32_t w, int32_t h, int32_
 }
 
 int orbx_frames_destroy(orbx_frames* F) {
+  ORBX_RESOURCE_LOCK;
   if (!F) return ORBX_OK;
   F->drop_graphs();
   void* ptrs[] = {F->d_lcounts, F->d_uright, F->d_depth, F->d_sad, F->d_row_off, F->d_row_idx,
@@ -372,24 +368,8 @@ int orbx_frames_run(orbx_frames* F, const uint8_t* d_imgs, int32_t n) {
     F->drop_graphs();
   }
   if (F->prof.on) return enqueue(F, d_imgs, n, &F->prof);
-  hipGraphExec_t exec = nullptr;
-  for (auto& g : F->graphs)
-    if (g.in == d_imgs && g.n == n) exec = g.exec;
-  if (!exec) {
-    if (F->graphs.size() >= 16) F->drop_graphs();
-    hipGraph_t gr;
-    ORBX_HIP(hipStreamBeginCapture(F->v.stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue(F, d_imgs, n, nullptr);
-    hipError_t e = hipStreamEndCapture(F->v.stream, &gr);
-    if (rc) return rc;
-    if (e != hipSuccess) return report_hip(e, "hipStreamEndCapture");
-    e = hipGraphInstantiate(&exec, gr, nullptr, nullptr, 0);
-    hipGraphDestroy(gr);
-    if (e != hipSuccess) return report_hip(e, "hipGraphInstantiate");
-    F->graphs.push_back({d_imgs, n, exec});
-  }
-  ORBX_HIP(hipGraphLaunch(exec, F->v.stream));
-  return ORBX_OK;
+  return run_graph(F->graphs, F->v.stream, d_imgs, n,
+                   [&] { return enqueue(F, d_imgs, n, nullptr); });
 }
 
 int orbx_frames_sync(orbx_frames* F) {

@@ -20,6 +20,16 @@ int report_hip(hipError_t e, const char* what) {
   return ORBX_EDEVICE;
 }
 
+std::recursive_mutex& resource_mutex() {
+  static std::recursive_mutex m;
+  return m;
+}
+
+int report(int code, const char* what) {
+  fprintf(stderr, "[orbx] error %d: %s\n", code, what);
+  return code;
+}
+
 // ORBextractor::ORBextractor (ORBextractor.cc:404-460)
 void build_tables(const orbx_params& p, Geometry* g) {
   const int L = p.nlevels;

@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -277,6 +278,78 @@ struct Profiler {
   } while (0)
 
 int report_hip(hipError_t e, const char* what);
+// logs a library-detected error (stderr) and returns `code`
+int report(int code, const char* what);
+
+// Process-wide lock around device resource changes (allocation, free, stream / symbol setup)
+// and stream capture.  ROCm may synchronise the device inside hipMalloc / hipFree, which
+// invalidates a capture running in another thread (hipErrorStreamCaptureInvalidated, seen with
+// several extractors on several host threads); captures and allocations therefore never
+// overlap.  Recursive: create functions call other create functions.
+std::recursive_mutex& resource_mutex();
+#define ORBX_RESOURCE_LOCK std::lock_guard<std::recursive_mutex> orbx_res_lock_(orbx::resource_mutex())
+
+// Executable graphs of one stream, keyed by (input pointer, batch): a caller that alternates
+// input buffers replays one graph per buffer instead of re-capturing.  Graphs are destroyed
+// only after the stream has drained (an exec may still be running).
+struct GraphCache {
+  struct Entry {
+    const void* in;
+    int n;
+    hipGraphExec_t exec;
+  };
+  std::vector<Entry> e;
+  static constexpr size_t kMax = 8;
+  hipGraphExec_t find(const void* in, int n) const {
+    for (const Entry& x : e)
+      if (x.in == in && x.n == n) return x.exec;
+    return nullptr;
+  }
+  void clear(hipStream_t s) {
+    if (e.empty()) return;
+    ORBX_RESOURCE_LOCK;
+    if (s) (void)hipStreamSynchronize(s);
+    for (Entry& x : e) (void)hipGraphExecDestroy(x.exec);
+    e.clear();
+  }
+  void add(const void* in, int n, hipGraphExec_t exec, hipStream_t s) {
+    if (e.size() >= kMax) clear(s);
+    e.push_back({in, n, exec});
+  }
+};
+
+// Captures what `enqueue()` puts on stream s into an executable graph; the partial graph of a
+// failed enqueue is destroyed.
+template <class Fn>
+int capture_graph(hipStream_t s, Fn&& enqueue, hipGraphExec_t* out) {
+  ORBX_RESOURCE_LOCK;
+  hipGraph_t gr = nullptr;
+  hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) return report_hip(e, "hipStreamBeginCapture");
+  const int rc = enqueue();
+  e = hipStreamEndCapture(s, &gr);
+  if (rc != ORBX_OK) {
+    if (e == hipSuccess && gr) (void)hipGraphDestroy(gr);
+    return rc;
+  }
+  if (e != hipSuccess) return report_hip(e, "hipStreamEndCapture");
+  e = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(gr);
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "hipGraphInstantiate");
+}
+
+// Replays the cached graph of (in, n) on s, capturing it first if needed.
+template <class Fn>
+int run_graph(GraphCache& cache, hipStream_t s, const void* in, int n, Fn&& enqueue) {
+  hipGraphExec_t exec = cache.find(in, n);
+  if (!exec) {
+    const int rc = capture_graph(s, enqueue, &exec);
+    if (rc != ORBX_OK) return rc;
+    cache.add(in, n, exec, s);
+  }
+  const hipError_t e = hipGraphLaunch(exec, s);
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "hipGraphLaunch");
+}
 
 // Internal plan access for the frame pipeline (orbx_frames.hip).
 struct PlanView {
@@ -293,5 +366,7 @@ struct PlanView {
 };
 int plan_view(orbx_plan* P, PlanView* v);
 int plan_enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof);
+// one allocation holds counts [max_batch] at 0, keypoints at kps_off, descriptors at desc_off
+int plan_output_block(const orbx_plan* P, size_t* kps_off, size_t* desc_off, size_t* bytes);
 
 }  // namespace orbx

@@ -40,7 +40,8 @@ struct BowProblem {
   DevSide s1, s2;
   int* match;  // pre-filled with -1
   int* count;
-  int* error;  // set to 1 when a node has more candidates than a wave tracks
+  int* error;  // bit 1 (ORBX_DEVERR_INDEX): a match index outside the other side
+  int* matched2;  // mode 1, nodes above kBowRegCands candidates: vbMatched2 flags [s2.n], zeroed
   int mode;
   float nnratio;
   int check_ori;
@@ -80,7 +81,15 @@ struct TriProblem {
   int* m12;    // [s1.n], pre-filled with -1
   int* pairs;  // [s1.n][2]
   int* count;
+  int* error;  // bit 1 (ORBX_DEVERR_INDEX): a match index outside KF2
 };
+
+// device error bits of the matcher problems: a finish kernel read a match index outside the
+// other side's features (stale or corrupt match array); the entry is dropped, never dereferenced
+constexpr int ORBX_DEVERR_INDEX = 2;
+// candidates per vocabulary node whose vbMatched2 flags k_bow_nodes keeps in a per-lane register
+// bitmap (64 chunks of 64); larger nodes keep them in global memory
+constexpr int kBowRegCands = 64 * 64;
 
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
 int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
@@ -94,35 +103,54 @@ int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_coun
 // LocalMapping and LoopClosing threads at once; each thread gets its own stream and buffers).
 struct Workspace {
   hipStream_t stream = nullptr;
-  char* d = nullptr;
+  char* d = nullptr;  // device buffer, cap bytes
+  char* h = nullptr;  // pinned host mirror, cap bytes: uploads and downloads go through it
   size_t cap = 0;
   int device = -1;
-  ~Workspace() {
+  void free_all() {
     if (d) (void)hipFree(d);
+    if (h) (void)hipHostFree(h);
+    d = nullptr;
+    h = nullptr;
+    cap = 0;
+  }
+  ~Workspace() {
+    ORBX_RESOURCE_LOCK;
+    free_all();
     if (stream) (void)hipStreamDestroy(stream);
   }
   int reserve(size_t bytes) {
     int dev = 0;
     (void)hipGetDevice(&dev);
+    if (device == dev && stream && bytes <= cap) return ORBX_OK;
+    ORBX_RESOURCE_LOCK;
     if (device != dev) {
-      if (d) (void)hipFree(d);
+      free_all();
       if (stream) (void)hipStreamDestroy(stream);
-      d = nullptr;
-      cap = 0;
       stream = nullptr;
       device = dev;
     }
     if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
       return ORBX_EDEVICE;
     if (bytes <= cap) return ORBX_OK;
-    if (d) (void)hipFree(d);
-    d = nullptr;
-    cap = std::max(bytes, cap * 2);
-    if (hipMalloc(&d, cap) != hipSuccess) {
-      cap = 0;
+    const size_t want = std::max(bytes, cap * 2);
+    free_all();
+    if (hipMalloc(&d, want) != hipSuccess ||
+        hipHostMalloc(&h, want, hipHostMallocDefault) != hipSuccess) {
+      free_all();
       return ORBX_ENOMEM;
     }
+    cap = want;
     return ORBX_OK;
+  }
+  // stages the packed host arrays through the pinned mirror and uploads them
+  hipError_t upload(const std::vector<char>& host, size_t bytes) {
+    memcpy(h, host.data(), bytes);
+    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+  }
+  // device range [off, off + bytes) into the same range of the pinned mirror
+  hipError_t download(size_t off, size_t bytes) {
+    return hipMemcpyAsync(h + off, d + off, bytes, hipMemcpyDeviceToHost, stream);
   }
 };
 extern thread_local Workspace tls_ws;

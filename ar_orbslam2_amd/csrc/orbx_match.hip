@@ -79,11 +79,13 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
   const int b = wave_lower_bound(P.s2.node_ids, nn2, id, lane);
   if (b >= nn2 || P.s2.node_ids[b] != id) return;
   const int f0 = P.s2.node_offsets[b], m = P.s2.node_offsets[b + 1] - f0;
-  if (m > 64 * 16) {  // more candidates than the per-lane matched bitmap holds
-    if (lane == 0) atomicOr(P.error, 1);
-    return;
-  }
   const bool kfkf = P.mode == 1;
+  // vbMatched2 / vpMapPointMatches[realIdxF] (ORBmatcher.cc:215-216, 598-599): a feature
+  // belongs to one node, so only this wave reads or sets the flags of the node's candidates.
+  // Up to kBowRegCands candidates they live in a register bitmap (bit c of lane l: candidate
+  // l + 64c); larger nodes (no limit in the reference) keep them in memory: mode 0 reads the
+  // output itself (match[i2] >= 0), mode 1 the zeroed matched2 flags.
+  const bool big = m > kBowRegCands;
   // candidate descriptors of chunk 0 stay in registers
   uint64_t reg[4] = {0, 0, 0, 0};
   int i2_0 = -1;
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
     reg[0] = p[0]; reg[1] = p[1]; reg[2] = p[2]; reg[3] = p[3];
     ok0 = !kfkf || !P.s2.valid || P.s2.valid[i2_0];
   }
-  uint32_t matched = 0;  // bit c: candidate lane + 64c already matched in this call
+  uint64_t matched = 0;  // bit c: candidate lane + 64c already matched in this call
   const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
   for (int c0 = a0; c0 < a1; c0 += 64) {
     // prefetch up to 64 KF features of the node (index, validity, descriptor) so the serial
@@ -121,14 +123,20 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
       int b1 = 256, bp = 0x7FFFFFFF, b2 = 256;
       for (int c = 0; c * 64 < m; c++) {
         const int jj = lane + 64 * c;
-        if (jj >= m || (matched >> c) & 1) continue;
+        if (jj >= m) continue;
+        if (!big && ((matched >> c) & 1)) continue;
+        const int i2 = c == 0 ? i2_0 : P.s2.node_feats[f0 + jj];
+        if (big && (kfkf ? __hip_atomic_load(P.matched2 + i2, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) != 0
+                         : __hip_atomic_load(P.match + i2, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) >= 0))
+          continue;
         int dist;
         if (c == 0) {
           if (!ok0) continue;
           uint64_t x[4] = {reg[0], reg[1], reg[2], reg[3]};
           dist = hamming_regs(d1, (const uint8_t*)x);
         } else {
-          const int i2 = P.s2.node_feats[f0 + jj];
           if (kfkf && P.s2.valid && !P.s2.valid[i2]) continue;
           dist = hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32);
         }
@@ -155,12 +163,20 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
       }
       const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
       if (pass && static_cast<float>(b1) < P.nnratio * static_cast<float>(b2)) {
-        if ((bp & 63) == lane) matched |= 1u << (bp >> 6);
+        if ((bp & 63) == lane) matched |= 1ull << (bp >> 6);
         if (lane == 0) {
           const int i2 = P.s2.node_feats[f0 + bp];
-          if (kfkf) P.match[i1] = i2;
-          else P.match[i2] = i1;
+          if (kfkf) {
+            P.match[i1] = i2;
+            if (big) __hip_atomic_store(P.matched2 + i2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else if (big) {
+            __hip_atomic_store(P.match + i2, i1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            P.match[i2] = i1;
+          }
         }
+        // the flag store completes before the next feature's scan reads it
+        if (big) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
       }
     }
   }
@@ -204,10 +220,11 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
   __syncthreads();
   const bool kfkf = P.mode == 1;
   const int n = kfkf ? side_n(P.s1) : side_n(P.s2);
+  const int n_other = kfkf ? side_n(P.s2) : side_n(P.s1);  // range of a match value
   if (P.check_ori) {
     for (int i = tid; i < n; i += 256) {
       const int m = P.match[i];
-      if (m < 0) continue;
+      if (m < 0 || m >= n_other) continue;
       const int bin = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m))
                             : rot_bin(side_angle(P.s1, m), side_angle(P.s2, i));
       atomicAdd(&hist[bin], 1);
@@ -220,6 +237,11 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
   for (int i = tid; i < n; i += 256) {
     const int m = P.match[i];
     if (m < 0) continue;
+    if (m >= n_other) {  // stale or corrupt index: report, drop, never dereference
+      atomicOr(P.error, ORBX_DEVERR_INDEX);
+      P.match[i] = -1;
+      continue;
+    }
     if (P.check_ori) {
       const int bin = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m))
                             : rot_bin(side_angle(P.s1, m), side_angle(P.s2, i));
@@ -342,13 +364,13 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
   __shared__ int s_ind[3];
   __shared__ int s_scan[257];
   const int tid = threadIdx.x;
-  const int n = tri_n(P.s1);
+  const int n = tri_n(P.s1), n2 = tri_n(P.s2);
   if (tid < kHISTO) hist[tid] = 0;
   __syncthreads();
   if (P.check_ori) {
     for (int i = tid; i < n; i += 256) {
       const int m = P.m12[i];
-      if (m >= 0) atomicAdd(&hist[rot_bin(P.s1.keys_un[i].angle, P.s2.keys_un[m].angle)], 1);
+      if (m >= 0 && m < n2) atomicAdd(&hist[rot_bin(P.s1.keys_un[i].angle, P.s2.keys_un[m].angle)], 1);
     }
     __syncthreads();
     if (tid == 0) three_maxima(hist, s_ind[0], s_ind[1], s_ind[2]);
@@ -360,6 +382,11 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
   int mine = 0;
   for (int i = beg; i < end; i++) {
     int m = P.m12[i];
+    if (m >= n2) {  // stale or corrupt index: report, drop, never dereference
+      if (P.error) atomicOr(P.error, ORBX_DEVERR_INDEX);
+      P.m12[i] = -1;
+      m = -1;
+    }
     if (m >= 0 && P.check_ori) {
       const int bin = rot_bin(P.s1.keys_un[i].angle, P.s2.keys_un[m].angle);
       if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
@@ -579,6 +606,7 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
   const size_t omatch = st.add(nullptr, (size_t)std::max(nout, 1) * 4);
   const size_t ocount = st.add(nullptr, 16);
   const size_t oprob = st.add(nullptr, sizeof(BowProblem));
+  const size_t omatched2 = st.add(nullptr, (size_t)std::max(s2->n, 1) * 4);  // mode 1, big nodes
   int rc = tls_ws.reserve(st.host.size());
   if (rc) return rc;
   char* base = tls_ws.d;
@@ -588,22 +616,23 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
   P.match = dptr<int>(base, omatch);
   P.count = dptr<int>(base, ocount);
   P.error = dptr<int>(base, ocount + 4);
+  P.matched2 = dptr<int>(base, omatched2);
   P.mode = mode;
   P.nnratio = nnratio;
   P.check_ori = check_ori;
   memcpy(st.host.data() + oprob, &P, sizeof(P));
   memset(st.host.data() + omatch, 0xFF, (size_t)std::max(nout, 1) * 4);
   memset(st.host.data() + ocount, 0, 16);
+  memset(st.host.data() + omatched2, 0, (size_t)std::max(s2->n, 1) * 4);
   hipStream_t s = tls_ws.stream;
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), st.host.size(), hipMemcpyHostToDevice, s));
+  ORBX_HIP(tls_ws.upload(st.host, st.host.size()));
   rc = launch_bow(dptr<BowProblem>(base, oprob), 1, s1->fv.n_nodes, s);
   if (rc) return rc;
-  int res[2] = {0, 0};
-  ORBX_HIP(hipMemcpyAsync(res, base + ocount, 8, hipMemcpyDeviceToHost, s));
-  if (nout > 0)
-    ORBX_HIP(hipMemcpyAsync(match_out, base + omatch, (size_t)nout * 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(tls_ws.download(omatch, ocount + 8 - omatch));  // match array and count / error
   ORBX_HIP(hipStreamSynchronize(s));
-  if (res[1]) return ORBX_EUNSUPPORTED;
+  const int* res = (const int*)(tls_ws.h + ocount);
+  if (res[1]) return report(ORBX_EDEVICE, "SearchByBoW: a match index outside the keyframe");
+  if (nout > 0) memcpy(match_out, tls_ws.h + omatch, (size_t)nout * 4);
   *nmatches = res[0];
   return ORBX_OK;
 }
@@ -685,20 +714,20 @@ int orbx_search_for_triangulation(const orbx_tri_side* k1, const orbx_tri_side* 
   P.m12 = dptr<int>(base, om12);
   P.pairs = dptr<int>(base, opairs);
   P.count = dptr<int>(base, ocount);
+  P.error = dptr<int>(base, ocount + 4);
   memcpy(st.host.data() + oprob, &P, sizeof(P));
   memset(st.host.data() + om12, 0xFF, (size_t)n1 * 4);
   memset(st.host.data() + ocount, 0, 16);
   hipStream_t s = tls_ws.stream;
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), st.host.size(), hipMemcpyHostToDevice, s));
+  ORBX_HIP(tls_ws.upload(st.host, st.host.size()));
   rc = launch_tri(dptr<TriProblem>(base, oprob), 1, k1->fv.n_nodes, s);
   if (rc) return rc;
-  int cnt = 0;
-  ORBX_HIP(hipMemcpyAsync(&cnt, base + ocount, 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(tls_ws.download(opairs, ocount + 8 - opairs));  // pairs and count / error
   ORBX_HIP(hipStreamSynchronize(s));
-  if (cnt > 0) {
-    ORBX_HIP(hipMemcpyAsync(pairs, base + opairs, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipStreamSynchronize(s));
-  }
+  const int* res = (const int*)(tls_ws.h + ocount);
+  if (res[1]) return report(ORBX_EDEVICE, "SearchForTriangulation: a match index outside KF2");
+  const int cnt = res[0];
+  if (cnt > 0) memcpy(pairs, tls_ws.h + opairs, (size_t)cnt * 8);
   *nmatches = cnt;
   return ORBX_OK;
 }
@@ -739,4 +768,58 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int3
   return ORBX_OK;
 }
 
+// Test hook: the finish step of SearchByBoW (kind 0: KF->Frame, match indexed by frame feature
+// with KF values < n1; kind 1: KF->KF, indexed by KF1 feature with values < n2) or of
+// SearchForTriangulation (kind 2: indexed by KF1 feature, values < n2) over a caller-given match
+// array, without the orientation check.  Out-of-range values are what a stale match array
+// would hold: the kernels must drop them (out[i] = -1) and report ORBX_EDEVICE, never read
+// through them.
+int orbx_debug_match_finish(int32_t kind, int32_t n1, int32_t n2, const int32_t* match,
+                            int32_t* out, int32_t* nmatches) {
+  if (kind < 0 || kind > 2 || n1 < 0 || n2 < 0 || !match || !out || !nmatches) return ORBX_EINVAL;
+  const int n = kind == 0 ? n2 : n1;
+  Stager st;
+  const size_t om = st.add(match, (size_t)std::max(n, 1) * 4);
+  const size_t ocount = st.add(nullptr, 16);
+  const size_t oprob = st.add(nullptr, std::max(sizeof(BowProblem), sizeof(TriProblem)));
+  const size_t opairs = st.add(nullptr, (size_t)std::max(n, 1) * 8);
+  memset(st.host.data() + ocount, 0, 16);
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  if (kind < 2) {
+    BowProblem P{};
+    P.s1.n = n1;
+    P.s2.n = n2;
+    P.match = dptr<int>(base, om);
+    P.count = dptr<int>(base, ocount);
+    P.error = dptr<int>(base, ocount + 4);
+    P.mode = kind;
+    memcpy(st.host.data() + oprob, &P, sizeof(P));
+  } else {
+    TriProblem P{};
+    P.s1.n = n1;
+    P.s2.n = n2;
+    P.m12 = dptr<int>(base, om);
+    P.pairs = dptr<int>(base, opairs);
+    P.count = dptr<int>(base, ocount);
+    P.error = dptr<int>(base, ocount + 4);
+    memcpy(st.host.data() + oprob, &P, sizeof(P));
+  }
+  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), st.host.size(), hipMemcpyHostToDevice, s));
+  if (kind < 2)
+    hipLaunchKernelGGL(k_bow_finish, dim3(1), dim3(256), 0, s, dptr<const BowProblem>(base, oprob));
+  else
+    hipLaunchKernelGGL(k_tri_finish, dim3(1), dim3(256), 0, s, dptr<const TriProblem>(base, oprob));
+  ORBX_HIP(hipGetLastError());
+  int res[2] = {0, 0};
+  ORBX_HIP(hipMemcpyAsync(res, base + ocount, 8, hipMemcpyDeviceToHost, s));
+  if (n > 0) ORBX_HIP(hipMemcpyAsync(out, base + om, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  ORBX_HIP(hipStreamSynchronize(s));
+  *nmatches = res[0];
+  return res[1] ? ORBX_EDEVICE : ORBX_OK;
+}
+
 }  // extern "C"
+

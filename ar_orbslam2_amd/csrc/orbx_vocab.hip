@@ -483,6 +483,7 @@ int vocab_view(const orbx_vocabulary* V, VocView* v, int* device) {
 // it (where the descent stops early), ranked by ascending id.
 int vocab_ranks(const orbx_vocabulary* Vc, int levelsup, const VocRanks** out) {
   orbx_vocabulary* V = const_cast<orbx_vocabulary*>(Vc);
+  ORBX_RESOURCE_LOCK;  // before V->m: frames_create holds it when it gets here
   std::lock_guard<std::mutex> lk(V->m);
   for (auto* r : V->ranks)
     if (r->levelsup == levelsup) {
@@ -534,6 +535,7 @@ int orbx_vocabulary_create(int32_t k, int32_t L, int32_t scoring, int32_t weight
                            int32_t n_nodes, const int32_t* parent, const uint8_t* is_leaf,
                            const uint8_t* desc, const double* weight, int32_t hip_device,
                            orbx_vocabulary** out) {
+  ORBX_RESOURCE_LOCK;
   if (!out) return ORBX_EINVAL;
   *out = nullptr;
   // the loader's header check (TemplatedVocabulary.h:1360-1364)
@@ -558,6 +560,7 @@ int orbx_vocabulary_create(int32_t k, int32_t L, int32_t scoring, int32_t weight
 }
 
 int orbx_vocabulary_load_text(const char* path, int32_t hip_device, orbx_vocabulary** out) {
+  ORBX_RESOURCE_LOCK;
   if (!path || !out) return ORBX_EINVAL;
   *out = nullptr;
   FILE* f = fopen(path, "r");
@@ -604,6 +607,7 @@ int orbx_vocabulary_load_text(const char* path, int32_t hip_device, orbx_vocabul
 }
 
 int orbx_vocabulary_destroy(orbx_vocabulary* voc) {
+  ORBX_RESOURCE_LOCK;
   delete voc;
   return ORBX_OK;
 }
@@ -650,7 +654,7 @@ int orbx_vocabulary_transform(const orbx_vocabulary* V, const uint8_t* desc, int
   if (rc) return rc;
   char* base = tls_ws.d;
   hipStream_t s = tls_ws.stream;
-  if (upload) ORBX_HIP(hipMemcpyAsync(base, st.host.data(), upload, hipMemcpyHostToDevice, s));
+  if (upload) ORBX_HIP(tls_ws.upload(st.host, upload));
   if (n > 0) {
     rc = launch_voc_transform(view, V->L - levelsup, R->d_rank_of_node, dptr<uint8_t>(base, od),
                               0, nullptr, n, n, dptr<uint32_t>(base, ow),
@@ -666,10 +670,9 @@ int orbx_vocabulary_transform(const orbx_vocabulary* V, const uint8_t* desc, int
                   R->d_rank_ids, dptr<uint32_t>(base, ofi), dptr<int>(base, ofo),
                   dptr<int>(base, off), 0, dptr<int>(base, ofn), 1, s);
   if (rc) return rc;
-  std::vector<char> back(st.host.size() - ow);
-  ORBX_HIP(hipMemcpyAsync(back.data(), base + ow, back.size(), hipMemcpyDeviceToHost, s));
+  ORBX_HIP(tls_ws.download(ow, st.host.size() - ow));
   ORBX_HIP(hipStreamSynchronize(s));
-  auto at = [&](size_t o) { return back.data() + (o - ow); };
+  auto at = [&](size_t o) { return (const char*)tls_ws.h + o; };
   const int nb = *(const int*)at(obn), nf = *(const int*)at(ofn);
   memcpy(bow_words, at(obw), (size_t)nb * 4);
   memcpy(bow_values, at(obv), (size_t)nb * 8);

@@ -2,23 +2,34 @@
 """Benchmark: frames/s of ORB extract + match (BASELINE.json metric) on MI355X.
 
 One step = one batch of `--batch` synthetic 640x480 frames (BASELINE.json configs[1], TUM
-fr1/xyz mono geometry, 1000 features) already resident in HBM, pushed through the whole
-device pipeline: ORBextractor (pyramid, FAST cells, octree, orientation, rBRIEF),
-Frame::ComputeBoW (full DBoW2 descent of the seeded k=10, L=6 vocabulary: word ids, BowVector,
-FeatureVector), SearchByBoW(prev-as-KF, cur) and SearchForTriangulation(prev-as-KF, cur-as-KF)
-(SURVEY §8d unit of work).  Multi-GPU: one process per GPU, each rank processes its
-own camera stream (weak scaling, no data-path collective; RCCL only carries the barrier and
-the max-over-ranks time).
+fr1/xyz mono geometry, 1000 features) per camera stream, already resident in HBM, pushed
+through the whole device pipeline: ORBextractor (pyramid, FAST cells, octree, orientation,
+rBRIEF), Frame::ComputeBoW (full DBoW2 descent of the seeded k=10, L=6 vocabulary: word ids,
+BowVector, FeatureVector), SearchByBoW(prev-as-KF, cur) and SearchForTriangulation(prev-as-KF,
+cur-as-KF) (SURVEY §8d unit of work).
+
+Multi-GPU: one process per GPU.  Camera streams are independent; global stream s
+runs on rank s mod G (the reference's only parallelism is one extractor per camera thread,
+ORB_SLAM2/src/Frame.cc:83-86), so there is no data-path collective: RCCL carries only the
+barrier and the max-over-ranks time.  Weak scaling (default): `--streams` camera streams per
+GPU.  Strong scaling: `--streams-total T` fixes the job's stream count over G GPUs.  Under
+torchrun the rank comes from RANK / LOCAL_RANK / WORLD_SIZE; `--gpus N` without WORLD_SIZE
+starts the N rank processes itself before anything touches the GPU.
 
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events on the
-pipeline stream over the timed region) and the CPU oracle baseline (rank 0, N=1 only).
+pipeline stream), the PCIe-upload-included rate, and the CPU oracle baseline (rank 0, N=1).
+`--dropin` measures the per-frame drop-in path instead (tools/orbx_dropin.cpp: host threads
+calling orbx_extract / orbx_vocabulary_transform / orbx_search_* one frame at a time).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,6 +40,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec ORB extract+match, 640×480 1000-feat; bit-exact descriptors"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PCIE_GEN5_X16_GBS = 63.0  # PCIe Gen5 x16 spec, one direction
+VALU_SIMDS = 1024         # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4           # MI355X peak engine clock
 CONFIGS = {
     "C2": dict(w=640, h=480, nfeatures=1000,
                workload="TUM fr1/xyz mono 640x480, 1000 features, 1xMI355X HIP extract+match"),
@@ -75,11 +89,9 @@ def algorithmic_bytes(levels, n_kp, n_img):
 LOAD_WIDTH = {"k_fast_tile": 8, "k_cvfast": 8}
 
 
-def pmc_calibration():
-    """profiles/pmc_calibration.json (scripts/pmc_calibrate.py, tools/pmc_calib.hip): counter
-    bytes per true byte for streaming loads / stores of each width per lane, measured here."""
+def _load_json(name):
     try:
-        return json.load(open(os.path.join(ROOT, "profiles", "pmc_calibration.json")))
+        return json.load(open(os.path.join(ROOT, "profiles", name)))
     except (OSError, ValueError):
         return None
 
@@ -89,9 +101,9 @@ def pmc_traffic(pmc_dir, kernel):
     (FETCH_SIZE, WRITE_SIZE, both in KB).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2->fabric
     requests (Infinity-Cache hits included) and reads 1/2 of the bytes of 16-B-per-lane streaming
     loads; other widths are to be calibrated in one's own access pattern, which
-    profiles/pmc_calibration.json holds (4- and 8-B loads: also 1/2; stores exact).  Returns
-    (bytes, note): FETCH_SIZE x 1024 / read factor of the kernel's load width +
-    WRITE_SIZE x 1024 / the 8-B store factor, or the uncorrected sum without a calibration."""
+    profiles/pmc_calibration.json holds (tools/pmc_calib.hip).  Returns (bytes, note):
+    FETCH_SIZE x 1024 / read factor of the kernel's load width + WRITE_SIZE x 1024 / the 8-B
+    store factor, or the uncorrected sum without a calibration."""
     import csv
     tot = {}
     rel = os.path.relpath(pmc_dir, ROOT) if pmc_dir else None
@@ -104,7 +116,7 @@ def pmc_traffic(pmc_dir, kernel):
         if not vals:
             return None, f"kernel not in the PMC passes ({rel})"
         tot[counter] = sum(vals) / len(vals) * 1024
-    cal = pmc_calibration()
+    cal = _load_json("pmc_calibration.json")
     w = LOAD_WIDTH.get(kernel)
     rf = (cal or {}).get("read", {}).get(f"{w}B_per_lane") if w else None
     wf = (cal or {}).get("write", {}).get("8B_per_lane")
@@ -117,11 +129,21 @@ def pmc_traffic(pmc_dir, kernel):
             f"this kernel's access width)")
 
 
+def valu_cycles():
+    """Cycles one wave64 VALU instruction occupies its SIMD when the SIMD is saturated.
+    MI355X_MICROARCH.md (SIMD-32: 'issues each VALU instruction over 2 cycles'; one wave alone
+    sustains 4).  profiles/valu_calibration.json (tools/valu_calib.hip, >= 2 waves per SIMD in
+    the integer instruction mix of these kernels) overrides the guide's figure when present."""
+    cal = _load_json("valu_calibration.json")
+    if cal and cal.get("cycles_per_valu_saturated"):
+        return float(cal["cycles_per_valu_saturated"]), "profiles/valu_calibration.json"
+    return 2.0, "MI355X_MICROARCH.md (2 cycles per wave64 VALU instruction on SIMD-32)"
+
+
 def pmc_valu(pmc_dir, kernel, avg_launch_us):
     """VALU-issue roofline of `kernel` from the SQ counter pass of this bench command
-    (sq_counters.csv: SQ_INSTS_VALU summed over a dispatch's waves).  A wave64 VALU instruction
-    occupies its SIMD's VALU for one quad-cycle (SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU on these
-    kernels), so the issue floor of a launch is INSTS_VALU * 4 / (1024 SIMDs * 2.4 GHz)."""
+    (sq_counters.csv: SQ_INSTS_VALU summed over a dispatch's waves): the launch cannot finish
+    before INSTS_VALU x c / (1024 SIMDs x 2.4 GHz), c from valu_cycles()."""
     import csv
     path = os.path.join(pmc_dir, "sq_counters.csv")
     if not os.path.exists(path) or not avg_launch_us:
@@ -132,73 +154,190 @@ def pmc_valu(pmc_dir, kernel, avg_launch_us):
     if not vals:
         return None
     instr = sum(vals) / len(vals)
-    floor_us = instr * 4 / 1024 / 2400.0
-    return {"valu_instr_per_launch": round(instr), "issue_floor_us": round(floor_us, 2),
-            "frac": round(floor_us / avg_launch_us, 4),
-            "note": "integer stencil/popcount work: the VALU issue rate, not HBM, bounds it; "
-                    "floor = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz), frac = floor / "
-                    "avg_launch_us (" + os.path.relpath(path, ROOT) + ")"}
+    c, src = valu_cycles()
+    floor_us = instr * c / VALU_SIMDS / (CLOCK_GHZ * 1e3)
+    return {"valu_instr_per_launch": round(instr), "cycles_per_instr": c,
+            "issue_floor_us": round(floor_us, 2), "frac": round(floor_us / avg_launch_us, 4),
+            "note": f"floor = SQ_INSTS_VALU x {c} cycles ({src}) / ({VALU_SIMDS} SIMDs x "
+                    f"{CLOCK_GHZ} GHz), frac = floor / avg_launch_us "
+                    f"({os.path.relpath(path, ROOT)})"}
 
 
-def cpu_baseline(cfg, seconds):
-    """The CPU oracle (orb_oracle.cc restating ORBextractor/ORBmatcher) on this host, 1 thread,
-    on consecutive frames of the same synthetic stream: extract + SearchByBoW +
-    SearchForTriangulation per frame."""
-    from oracle import oracle as O
-    from ar_orbslam2_amd import synth
-    from ar_orbslam2_amd.pipeline import TUM1_K, fundamental_from_pose
-    w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
-    p = O.params(nf)
-    t = O.tables(p, w, h)
-    from ar_orbslam2_amd.vocabulary import complete_tree
-    ndesc = sum(10 ** l for l in range(7))
-    voc = O.Vocabulary.from_nodes(10, 6, 0, 0, *complete_tree(
-        10, 6, np.random.default_rng(42).integers(0, 256, (ndesc, 32), dtype=np.uint8)))
-    F = fundamental_from_pose()
-    ex, ey = O.epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
-    stereo = cfg.get("stereo")
-    if stereo:
-        from ar_orbslam2_amd.stereo import stereo_params
-        mb, mbf = stereo_params(*stereo)
-        imgs = [synth.stereo_pair(w, h, i, 0) for i in range(16)]
-    else:
-        base = synth.canvas(w, h, 0)
-        imgs = [synth.frame(w, h, i, 0, base) for i in range(64)]
+def roofline_of(stages, alg, pmc_dir, steps, B):
+    """Roofline object of the dominant kernel (largest total time in the per-kernel HIP-event
+    pass).  The path is integer stencil / gather / popcount work: VALU issue bounds it, so
+    `bound` is "valu" and frac is the VALU-issue fraction when the SQ pass of this command
+    exists; the HBM fraction (algorithmic bytes / launch time vs 8 TB/s) is reported beside it."""
+    if not stages:
+        return None
+    dom = max(stages, key=lambda k: stages[k][0])
+    ms, launches = stages[dom]
+    avg_s = ms / 1e3 / max(launches, 1)
+    a_bytes = alg.get(dom)
+    achieved = (a_bytes / avg_s / 1e9) if a_bytes is not None else None
+    traffic, tnote = pmc_traffic(pmc_dir, dom)
+    valu = pmc_valu(pmc_dir, dom, avg_s * 1e6)
+    hbm = {"achieved": round(achieved, 3) if achieved is not None else None,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None}
+    out = {"bound": "hbm", "kernel": dom, **hbm, "traffic": traffic, "traffic_note": tnote,
+           "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": a_bytes}
+    if valu:
+        # VALU-issue roofline in the contract's fields; the HBM one kept under "hbm"
+        peak_ginstr = VALU_SIMDS * CLOCK_GHZ / valu["cycles_per_instr"]  # G wave-instr/s
+        out.update({"bound": "valu", "achieved": round(valu["valu_instr_per_launch"] / avg_s / 1e9, 3),
+                    "peak": round(peak_ginstr, 3), "unit": "G wave64 VALU instr/s",
+                    "frac": valu["frac"], "hbm": hbm})
+    out["valu_roofline"] = valu
+    out["stages_ms_per_step"] = {k: round(v[0] / steps, 4) for k, v in stages.items()}
+    out["stages_of"] = (f"roofline pass: camera stream 0 alone, {steps} steps of {B} frames "
+                        f"after the timed region")
+    return out
 
-    prev = None
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        img = imgs[n % len(imgs)]
-        u_right = None
-        if stereo:
-            kps, desc, pl, _ = O.extract(img[0], p, want_pyramid=True)
-            kr, dr, pr, _ = O.extract(img[1], p, want_pyramid=True)
-            u_right = O.stereo_matches(kps, desc, kr, dr, pl, pr, t["scale"], t["inv_scale"],
-                                       mb, mbf)[0]
+
+# ---------------------------------------------------------------------------- CPU baseline
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        libc.gnu_get_libc_version.restype = ctypes.c_char_p
+        glibc = libc.gnu_get_libc_version().decode()
+    except (OSError, AttributeError):
+        glibc = None
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    # the process's CPU share: on the GPU box the affinity mask shows the whole machine while
+    # OMP_NUM_THREADS (16 per GPU) states the share a job may use
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    if share > 0:
+        cores = min(cores, share)
+    return {"cpu_model": model or platform.processor() or platform.machine(),
+            "cores_available": cores, "glibc": glibc,
+            "glibc_note": "descriptor parity is defined against this glibc's sincosf "
+                          "(the reference calls sincosf; SURVEY App. C.2)"}
+
+
+class CpuUnit:
+    """The CPU oracle's unit of work (orb_oracle.cc restating ORBextractor/ORBmatcher, DBoW2
+    restatement): extract (x2 + ComputeStereoMatches for stereo) + ComputeBoW + SearchByBoW +
+    SearchForTriangulation against the previous frame of the same stream."""
+
+    def __init__(self, cfg, n_images=16, stream=0):
+        from oracle import oracle as O
+        from ar_orbslam2_amd import synth
+        from ar_orbslam2_amd.pipeline import TUM1_K, fundamental_from_pose
+        from ar_orbslam2_amd.vocabulary import complete_tree
+        self.O = O
+        self.cfg = cfg
+        w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
+        self.p = O.params(nf)
+        self.t = O.tables(self.p, w, h)
+        ndesc = sum(10 ** l for l in range(7))
+        self.voc = O.Vocabulary.from_nodes(10, 6, 0, 0, *complete_tree(
+            10, 6, np.random.default_rng(42).integers(0, 256, (ndesc, 32), dtype=np.uint8)))
+        self.F = fundamental_from_pose()
+        self.ex, self.ey = O.epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
+        self.stereo = cfg.get("stereo")
+        if self.stereo:
+            from ar_orbslam2_amd.stereo import stereo_params
+            self.mb, self.mbf = stereo_params(*self.stereo)
+            self.imgs = [synth.stereo_pair(w, h, i, stream) for i in range(n_images)]
         else:
-            kps, desc = O.extract(img, p)
-        b = voc.transform(desc, 4)  # Frame::ComputeBoW: BowVector + FeatureVector
-        r = np.random.default_rng(n)
+            base = synth.canvas(w, h, stream)
+            self.imgs = [synth.frame(w, h, i, stream, base) for i in range(n_images)]
+        self.prev = None
+        self.n = 0
+
+    def step(self):
+        O, t = self.O, self.t
+        img = self.imgs[self.n % len(self.imgs)]
+        u_right = None
+        if self.stereo:
+            kps, desc, pl, _ = O.extract(img[0], self.p, want_pyramid=True)
+            kr, dr, pr, _ = O.extract(img[1], self.p, want_pyramid=True)
+            u_right = O.stereo_matches(kps, desc, kr, dr, pl, pr, t["scale"], t["inv_scale"],
+                                       self.mb, self.mbf)[0]
+        else:
+            kps, desc = O.extract(img, self.p)
+        b = self.voc.transform(desc, 4)  # Frame::ComputeBoW: BowVector + FeatureVector
+        r = np.random.default_rng(self.n)
         cur = dict(desc=desc, angle=kps["angle"], keys=kps,
                    fv=(b["fv_ids"], b["fv_off"], b["fv_feats"]),
                    valid=(r.random(len(kps)) < 0.6).astype(np.uint8),
                    has_mp=(r.random(len(kps)) < 0.4).astype(np.uint8), u_right=u_right,
                    scale_factors=t["scale"], level_sigma2=t["sigma2"])
-        if prev is not None:
-            O.search_by_bow_kf_f(prev, dict(cur, valid=None), 0.7, True)
-            O.search_for_triangulation(prev, cur, F, ex, ey, False, 0.6, False)
-        prev = cur
+        if self.prev is not None:
+            O.search_by_bow_kf_f(self.prev, dict(cur, valid=None), 0.7, True)
+            O.search_for_triangulation(self.prev, cur, self.F, self.ex, self.ey, False, 0.6, False)
+        self.prev = cur
+        self.n += 1
+
+
+def _cpu_worker(unit, seconds, start_evt, q):
+    for _ in range(3):  # warm-up
+        unit.step()
+    start_evt.wait()
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        unit.step()
         n += 1
+    q.put((n, time.perf_counter() - t0))
+
+
+def cpu_baseline(cfg, seconds, mp_seconds, warmup=20, min_frames=200, max_seconds=40.0):
+    """SURVEY §8d CPU baseline, measured on this host before any GPU work of this process:
+    * one thread: `warmup` untimed frames, then frames timed one by one (steady clock) until
+      >= min_frames and >= `seconds` (or `max_seconds`); median and mean ms per frame, as
+      mono_tum.cc:113-121 reports tracking times;
+    * every available core (sched_getaffinity): one forked process per core, each its own
+      camera stream, aggregate frames/s over `mp_seconds` — the `value`."""
+    import multiprocessing as mp
+    info = host_info()
+    unit = CpuUnit(cfg)
+    for _ in range(warmup):
+        unit.step()
+    times = []
+    t0 = time.perf_counter()
+    while True:
+        a = time.perf_counter()
+        unit.step()
+        times.append(time.perf_counter() - a)
         el = time.perf_counter() - t0
-        if el >= seconds and n >= 4:
+        if (len(times) >= min_frames and el >= seconds) or el >= max_seconds:
             break
-    return dict(value=n / el, unit="frames/s", cores=1, kind="port",
-                sample=f"{n} consecutive {w}x{h} synthetic {'stereo ' if stereo else ''}frames, CPU "
-                       f"oracle (oracle/*.cc, g++ -O3 -march=x86-64-v3 -ffp-contract=off), 1 thread, "
-                       f"extract{' x2 + ComputeStereoMatches' if stereo else ''} + "
-                       f"ComputeBoW + SearchByBoW + SearchForTriangulation per frame, {el:.1f} s on "
-                       f"{platform.processor() or platform.machine()}")
+    times_ms = np.array(times) * 1e3
+    single = {"frames_per_s": round(len(times) / el, 3), "median_ms": round(float(np.median(times_ms)), 3),
+              "mean_ms": round(float(times_ms.mean()), 3), "timed_frames": len(times),
+              "warmup_frames": warmup}
+    P = info["cores_available"] or 1
+    ctx = mp.get_context("fork")  # no GPU work has happened in this process yet
+    start, q = ctx.Event(), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=(CpuUnit(cfg, 8, stream=1 + i), mp_seconds, start, q))
+             for i in range(P)]
+    for p in procs:
+        p.start()
+    time.sleep(0.5)
+    start.set()
+    res = [q.get(timeout=mp_seconds * 4 + 120) for _ in procs]
+    for p in procs:
+        p.join()
+    agg = sum(n for n, _ in res) / max(e for _, e in res)
+    stereo = cfg.get("stereo")
+    w, h = cfg["w"], cfg["h"]
+    unit_desc = (f"extract{' x2 + ComputeStereoMatches' if stereo else ''} + ComputeBoW + "
+                 f"SearchByBoW + SearchForTriangulation per frame")
+    return dict(value=round(agg, 3), unit="frames/s", cores=P, kind="port",
+                sample=f"{w}x{h} synthetic {'stereo ' if stereo else ''}frames, CPU oracle "
+                       f"(oracle/*.cc, g++ -O3 -march=x86-64-v3 -ffp-contract=off): {P} forked "
+                       f"processes x 1 thread, one camera stream each, {mp_seconds:.0f} s after 3 "
+                       f"warm-up frames ({sum(n for n, _ in res)} frames); {unit_desc}",
+                single_thread=single, **info)
 
 
 def cpu_baseline_marker(cfg, seconds, target_desc):
@@ -210,20 +349,26 @@ def cpu_baseline_marker(cfg, seconds, target_desc):
     base = synth.canvas(w, h, 0)
     imgs = [synth.frame(w, h, i, 0, base) for i in range(32)]
     p = O.cvorb_params(cfg["nfeatures"])
-    n = 0
+    for i in range(5):
+        O.good_matches(O.bf_match(target_desc, O.cvorb_detect(imgs[i], p)[1]))
+    times = []
     t0 = time.perf_counter()
     while True:
-        kps, desc = O.cvorb_detect(imgs[n % len(imgs)], p)
+        a = time.perf_counter()
+        kps, desc = O.cvorb_detect(imgs[len(times) % len(imgs)], p)
         O.good_matches(O.bf_match(target_desc, desc))
-        n += 1
+        times.append(time.perf_counter() - a)
         el = time.perf_counter() - t0
-        if el >= seconds and n >= 4:
+        if el >= seconds and len(times) >= 4:
             break
-    return dict(value=n / el, unit="frames/s", cores=1, kind="port",
-                sample=f"{n} consecutive {w}x{h} synthetic frames, CPU oracle (oracle/cvorb_oracle.cc, "
-                       f"g++ -O3 -march=x86-64-v3 -ffp-contract=off), 1 thread, cv::ORB + "
-                       f"BruteForceMatcher vs {len(target_desc)} target descriptors + good filter "
-                       f"per frame, {el:.1f} s on {platform.processor() or platform.machine()}")
+    ms = np.array(times) * 1e3
+    return dict(value=len(times) / el, unit="frames/s", cores=1, kind="port",
+                sample=f"{len(times)} consecutive {w}x{h} synthetic frames after 5 warm-up, CPU "
+                       f"oracle (oracle/cvorb_oracle.cc, g++ -O3 -march=x86-64-v3 "
+                       f"-ffp-contract=off), 1 thread, cv::ORB + BruteForceMatcher vs "
+                       f"{len(target_desc)} target descriptors + good filter per frame, {el:.1f} s",
+                median_ms=round(float(np.median(ms)), 3), mean_ms=round(float(ms.mean()), 3),
+                **host_info())
 
 
 def marker_bytes(levels, n_kp, n_img, n_target):
@@ -238,20 +383,178 @@ def marker_bytes(levels, n_kp, n_img, n_target):
             "k_good": 24 * n_target * n_img}
 
 
-def run_marker(args, cfg, rank, world, local):
+# ---------------------------------------------------------------------------- distribution
+def aggregate_elapsed(elapsed, world):
+    """Max over ranks: the job is as fast as its slowest GPU (RCCL/gloo all_reduce MAX)."""
+    if world <= 1:
+        return elapsed
     import torch
-    from oracle import oracle as O  # the target's descriptors only (fixed input, untimed)
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def streams_of_rank(rank, world, streams_per_gpu=1, streams_total=None):
+    """Global camera-stream ids processed by `rank` (stream s -> GPU s mod G, no
+    exchange).  Weak scaling: G x streams_per_gpu streams in the job; strong scaling: a fixed
+    `streams_total`, each rank taking the ids congruent to it mod G."""
+    total = streams_total if streams_total else world * max(1, streams_per_gpu)
+    return [s for s in range(total) if s % world == rank]
+
+
+def stream_of_rank(rank):
+    """First camera stream of a rank (one stream per rank)."""
+    return streams_of_rank(rank, rank + 1)[0]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n, argv):
+    """`--gpus N` without a launcher: start N rank processes (RANK = LOCAL_RANK = r, one GPU
+    each) and wait for them.  Called before this process touches the GPU; rank 0 prints the
+    JSON line.  Returns the worst exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+
+
+def init_dist(rank, world, local, backend):
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def gather_streams(streams, world):
+    if world <= 1:
+        return [streams]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, streams)
+    return out
+
+
+def run_dry(args, cfg, rank, world, streams):
+    """--dry-run: the launcher, stream sharding and max-over-ranks aggregation without device
+    work (gloo), for the CPU tests of the N>1 path."""
+    dist = init_dist(rank, world, rank, "gloo")
+    all_streams = gather_streams(streams, world)
+    B = args.batch
+    frames = sum(len(s) for s in all_streams) * B * args.steps
+    elapsed = aggregate_elapsed(0.01 * (1 + rank), world)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(frames / elapsed, 2), "unit": "frames/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong" if args.streams_total else "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic", "dry_run": True,
+            "config": {"workload": cfg["workload"], "streams_per_rank": all_streams,
+                       "frames_per_batch": B}}), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------- GPU legs
+def upload_pass(pipes, pools_host, B, steps, torch):
+    """PCIe-included rate: every step's frames start in pinned host memory and are copied to
+    HBM on one copy stream (double-buffered per camera stream, overlapped with the previous
+    batch's graph on the pipeline stream; one copy stream keeps the job within the box's 4
+    hardware queues: S pipeline streams + 1).  Also times the bare H2D of the same bytes."""
+    S = len(pipes)
+    nbytes = pools_host[0][0].numel()
+    dbuf = [[torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(2)]
+            for _ in range(S)]
+    cs_all = torch.cuda.Stream()
+    cstreams = [cs_all] * S
+    pstreams = [torch.cuda.ExternalStream(p.stream()) for p in pipes]
+    up = [[torch.cuda.Event() for _ in range(2)] for _ in range(S)]
+    done = [[torch.cuda.Event() for _ in range(2)] for _ in range(S)]
+
+    def step(i):
+        k = i % 2
+        for si, p in enumerate(pipes):
+            cs = cstreams[si]
+            cs.wait_event(done[si][k])  # the graph that last read dbuf[k] has finished
+            with torch.cuda.stream(cs):
+                dbuf[si][k].copy_(pools_host[si][i % len(pools_host[si])], non_blocking=True)
+                up[si][k].record(cs)
+            pstreams[si].wait_event(up[si][k])
+            p.run(dbuf[si][k].data_ptr(), B)
+            done[si][k].record(pstreams[si])
+
+    for i in range(2):
+        step(i)
+    for p in pipes:
+        p.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    for p in pipes:
+        p.sync()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # bare H2D of the same bytes (copy streams only)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(steps):
+        for si in range(S):
+            with torch.cuda.stream(cstreams[si]):
+                dbuf[si][i % 2].copy_(pools_host[si][i % len(pools_host[si])], non_blocking=True)
+    torch.cuda.synchronize()
+    el_copy = time.perf_counter() - t1
+    frames = S * B * steps
+    gbs = S * nbytes * steps / el / 1e9
+    copy_gbs = S * nbytes * steps / el_copy / 1e9
+    return {"value": round(frames / el, 2), "unit": "frames/s",
+            "h2d_GBs": round(gbs, 2), "h2d_copy_only_GBs": round(copy_gbs, 2),
+            "pcie_spec_GBs": PCIE_GEN5_X16_GBS,
+            "frac_of_pcie_spec": round(gbs / PCIE_GEN5_X16_GBS, 4),
+            "frac_of_copy_only": round(gbs / copy_gbs, 4),
+            "frames_ceiling_at_spec": round(PCIE_GEN5_X16_GBS * 1e9 / (nbytes / B), 1),
+            "note": "frames start in pinned host memory; H2D on one copy stream, "
+                    "double-buffered per camera stream, overlapped with the previous batch's graph"}
+
+
+def run_marker(args, cfg, rank, world, local, streams, dist):
+    import torch
     from ar_orbslam2_amd import synth
-    from ar_orbslam2_amd.marker import MarkerBatch
+    from ar_orbslam2_amd.marker import ORB, MarkerBatch, cvorb_params
     w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
-    S = max(1, args.streams)
+    S = len(streams)
+    # the target's descriptors come from the product cv::ORB (Marker::setTargetImage)
     target = synth.frame(w, h, 5, 0)
-    _, target_desc = O.cvorb_detect(target, O.cvorb_params(nf))
+    orb = ORB(nf, size=(w, h), device=local)
+    _, target_desc = orb(target)
+    orb.close()
     pipes, pools = [], []
-    for si in range(S):
+    for stream_id in streams:
         mb = MarkerBatch(w, h, B, nf, device=local)
         mb.set_target(target_desc)
-        stream_id = stream_of_rank(rank) * S + si
         base = synth.canvas(w, h, stream=stream_id)
         pool = []
         for pi in range(args.pool):
@@ -262,8 +565,7 @@ def run_marker(args, cfg, rank, world, local):
     torch.cuda.synchronize()
 
     def barrier():
-        if world > 1:
-            import torch.distributed as dist
+        if dist:
             dist.barrier()
 
     for i in range(args.warmup):
@@ -295,152 +597,73 @@ def run_marker(args, cfg, rank, world, local):
     if (kp_counts < 0).any():
         raise RuntimeError("a frame overflowed the per-level keypoint capacity")
     elapsed = aggregate_elapsed(elapsed, world)
-    value = world * S * B * args.steps / elapsed
-    from ar_orbslam2_amd.marker import cvorb_params
+    n_streams = args.streams_total or world * S
+    value = n_streams * B * args.steps / elapsed
+    from oracle import oracle as O  # level sizes only (host arithmetic tables)
     lv = O.cvorb_levels(cvorb_params(nf), w, h)
     levels = list(zip(lv["w"].tolist(), lv["h"].tolist()))
     n_kp = int(kp_counts.sum())
     alg = marker_bytes(levels, n_kp, B, len(target_desc))
-    roofline = None
-    if stages:
-        dom = max(stages, key=lambda k: stages[k][0])
-        ms, launches = stages[dom]
-        avg_s = ms / 1e3 / max(launches, 1)
-        a_bytes = alg.get(dom)
-        achieved = a_bytes / avg_s / 1e9
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 6),
-                    "traffic": pmc_traffic(args.pmc_dir, dom)[0],
-                    "traffic_note": pmc_traffic(args.pmc_dir, dom)[1],
-                    "avg_launch_us": round(avg_s * 1e6, 2),
-                    "algorithmic_bytes_per_launch": a_bytes,
-                    "valu_roofline": pmc_valu(args.pmc_dir, dom, avg_s * 1e6),
-                    "stages_ms_per_step": {k: round(v[0] / args.roofline_steps, 4)
-                                           for k, v in stages.items()},
-                    "stages_of": f"roofline pass: camera stream 0 alone, {args.roofline_steps} "
-                                 f"steps of {B} frames after the timed region"}
+    roofline = roofline_of(stages, alg, args.pmc_dir, args.roofline_steps, B)
     out = {
         "metric": MARKER_METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "scaling": "strong" if args.streams_total else "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
         "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B * S,
-                   "camera_streams_per_gpu": S, "frames_per_batch": B, "image": f"{w}x{h}",
+                   "camera_streams_per_gpu": S, "camera_streams_total": n_streams,
+                   "frames_per_batch": B, "image": f"{w}x{h}",
                    "nfeatures": nf, "target_descriptors": len(target_desc),
-                   "parallelism": f"{world} GPU(s) x {S} independent camera streams, no collective",
+                   "parallelism": f"{world} GPU(s), camera stream s on GPU s mod {world}, "
+                                  f"no collective",
                    "keypoints_per_frame": round(n_kp / B, 1),
                    "good_matches_per_frame": round(float(good_counts.mean()), 1),
                    "hamming_pairs_per_frame": round(n_kp / B * len(target_desc)),
                    "timing": "hipGraph replay of the extraction + 2 matcher launches per batch"},
         "roofline": roofline,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_marker(cfg, args.cpu_seconds, target_desc)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    return out, target_desc
 
 
-def aggregate_elapsed(elapsed, world):
-    """Max over ranks: the job is as fast as its slowest GPU (RCCL/gloo all_reduce MAX)."""
-    if world <= 1:
-        return elapsed
+def run_frames(args, cfg, rank, world, local, streams, dist):
     import torch
-    import torch.distributed as dist
-    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def stream_of_rank(rank):
-    """Camera stream s is processed by rank s (streams shard with no exchange)."""
-    return rank
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256,
-                    help="frames per step per camera stream")
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
-    ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
-    ap.add_argument("--streams", type=int, default=3,
-                    help="independent camera-stream pipelines per GPU, one HIP stream each "
-                         "(kernels are latency-bound; concurrent streams fill the CUs the others leave idle)")
-    ap.add_argument("--pmc-dir", default=None,
-                    help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE CSVs of this bench command, used "
-                         "for roofline.traffic (per launch of the dominant kernel)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true",
-                    help="skip the per-kernel roofline pass after the timed region")
-    ap.add_argument("--roofline-steps", type=int, default=5,
-                    help="steps of the single-stream roofline pass (per-kernel HIP events)")
-    args = ap.parse_args()
-    if args.pmc_dir is None:  # the committed PMC passes of this config's default command
-        # (never another config's: a missing directory reports traffic / VALU floor as null)
-        args.pmc_dir = os.path.join(ROOT, "profiles",
-                                    "r01_pmc" if args.config == "C2" else
-                                    "r01_pmc_" + args.config.lower())
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
-    torch.cuda.set_device(local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
-
-    cfg = CONFIGS[args.config]
-    if cfg.get("marker"):
-        run_marker(args, cfg, rank, world, local)
-        if world > 1:
-            dist.destroy_process_group()
-        return
-
     from ar_orbslam2_amd import ORBextractor, Vocabulary, epipole, synth
     from ar_orbslam2_amd.pipeline import TUM1_K, FramePipeline, fundamental_from_pose
 
     w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
-    voc = Vocabulary.synthetic()
-    S = max(1, args.streams)
+    voc = Vocabulary.synthetic(device=local)
+    S = len(streams)
     ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
-    pipes, pools = [], []
+    pipes, pools, pools_host = [], [], []
     stereo = None
     if cfg.get("stereo"):
         from ar_orbslam2_amd.stereo import stereo_params
         stereo = stereo_params(*cfg["stereo"])
-    for si in range(S):
+    for stream_id in streams:
         pipe = FramePipeline(w, h, B, voc, nf, device=local, stereo=stereo)
         pipe.seeded_masks(range(B))
         pipe.set_matching(fundamental_from_pose(), (ex, ey), bow_ratio=0.7, bow_check_ori=True,
                           tri_ratio=0.6, tri_check_ori=False)
         # synthetic frames of this camera stream, resident in HBM before timing
-        stream_id = stream_of_rank(rank) * S + si
-        pool = []
+        host = []
         if stereo:
             pairs = [synth.stereo_pair(w, h, t, stream_id) for t in range(min(B, 32))]
             for pi in range(args.pool):  # interleaved (left, right) images
-                fr = np.stack([im for i in range(B) for im in pairs[(pi * 7 + i) % len(pairs)]])
-                pool.append(torch.from_numpy(fr).cuda())
+                host.append(np.stack([im for i in range(B) for im in pairs[(pi * 7 + i) % len(pairs)]]))
         else:
             base = synth.canvas(w, h, stream=stream_id)
             for pi in range(args.pool):
-                fr = np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)])
-                pool.append(torch.from_numpy(fr).cuda())
+                host.append(np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)]))
+        pools.append([torch.from_numpy(fr).cuda() for fr in host])
+        pools_host.append([torch.from_numpy(fr).reshape(-1).pin_memory() for fr in host[:2]]
+                          if args.upload else None)
         pipes.append(pipe)
-        pools.append(pool)
     pipe = pipes[0]
     torch.cuda.synchronize()
 
     def barrier():
-        if world > 1:
+        if dist:
             dist.barrier()
 
     for i in range(args.warmup):
@@ -449,7 +672,7 @@ def main():
     for p in pipes:
         p.sync()
         if p.results(B)[3]:
-            raise RuntimeError("matcher reported a node larger than its per-wave capacity")
+            raise RuntimeError(f"frame pipeline reported device error {p.results(B)[3]}")
 
     # timed region: every camera stream replays its captured hipGraph, no per-kernel events
     barrier()
@@ -474,59 +697,192 @@ def main():
         pipe.sync()
         stages = pipe.profile_read()
         pipe.profile(False)
-    kp_counts, bow, tri, _ = pipe.results(B)
+    kp_counts, bow, tri, err = pipe.results(B)
+    if err:
+        raise RuntimeError(f"frame pipeline reported device error {err}")
+    upload = None
+    if args.upload:
+        del pools  # the device-resident pools are not needed any more
+        upload = upload_pass(pipes, pools_host, B, args.steps, torch)
 
     elapsed = aggregate_elapsed(elapsed, world)
-
-    frames = world * S * B * args.steps
-    value = frames / elapsed
-    ex_tables = ORBextractor(nf)
+    n_streams = args.streams_total or world * S
+    value = n_streams * B * args.steps / elapsed
+    ex_tables = ORBextractor(nf, device=local)
     levels = level_sizes(w, h, ex_tables.GetInverseScaleFactors())
     n_kp = int(kp_counts.sum())
     # stereo: both images of a frame are extracted (right keypoint count ~ left)
     alg = algorithmic_bytes(levels, 2 * n_kp if stereo else n_kp, 2 * B if stereo else B)
-    roofline = None
-    if stages:
-        dom = max(stages, key=lambda k: stages[k][0])
-        ms, launches = stages[dom]
-        avg_s = ms / 1e3 / max(launches, 1)
-        a_bytes = alg.get(dom)
-        achieved = (a_bytes / avg_s / 1e9) if a_bytes is not None else None
-        roofline = {"bound": "hbm", "kernel": dom,
-                    "achieved": round(achieved, 3) if achieved is not None else None,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
-                    "traffic": pmc_traffic(args.pmc_dir, dom)[0],
-                    "traffic_note": pmc_traffic(args.pmc_dir, dom)[1],
-                    "avg_launch_us": round(avg_s * 1e6, 2),
-                    "algorithmic_bytes_per_launch": a_bytes,
-                    "valu_roofline": pmc_valu(args.pmc_dir, dom, avg_s * 1e6),
-                    "stages_ms_per_step": {k: round(v[0] / args.roofline_steps, 4)
-                                           for k, v in stages.items()},
-                    "stages_of": f"roofline pass: camera stream 0 alone, {args.roofline_steps} "
-                                 f"steps of {B} frames after the timed region"}
-
+    roofline = roofline_of(stages, alg, args.pmc_dir, args.roofline_steps, B)
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "scaling": "strong" if args.streams_total else "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
         "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B * S,
-                   "camera_streams_per_gpu": S, "frames_per_batch": B,
+                   "camera_streams_per_gpu": S, "camera_streams_total": n_streams,
+                   "frames_per_batch": B,
                    "image": f"{w}x{h}", "images_per_frame": 2 if stereo else 1,
                    "nfeatures": nf, "nlevels": 8, "scale_factor": 1.2,
-                   "parallelism": f"{world} GPU(s) x {S} independent camera streams, no collective",
+                   "parallelism": f"{world} GPU(s), camera stream s on GPU s mod {world}, "
+                                  f"no collective",
                    "keypoints_per_frame": round(n_kp / B, 1),
                    "bow_matches_per_frame": round(float(bow.mean()), 1),
                    "triangulation_matches_per_frame": round(float(tri.mean()), 1),
                    "timing": "hipGraph replay; per-kernel HIP events only in the roofline pass"},
         "roofline": roofline,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    if upload:
+        out["pcie_upload_included"] = upload
+    return out
+
+
+class _nullctx:
+    def __init__(self, v):
+        self.v = v
+
+    def __enter__(self):
+        return self.v
+
+    def __exit__(self, *a):
+        return False
+
+
+def run_dropin(args, cfg, rank, world, local):
+    """--dropin: the per-frame path ORB-SLAM2 calls (Frame.cc:252-258 -> ORBextractor::operator(),
+    Frame::ComputeBoW, ORBmatcher::SearchByBoW / SearchForTriangulation one frame or keyframe
+    pair per call, Tracking.cc:1132-1136, LocalMapping.cc:238-241), driven by the C++ program
+    tools/orbx_dropin.cpp over liborbx.so from pageable host images (cv::Mat), K host threads
+    each with its own extractor (one per camera, like the reference's per-camera ORBextractor).
+    Runs as a child process; this process never touches the GPU."""
+    import tempfile
+    from ar_orbslam2_amd import synth
+    from ar_orbslam2_amd.vocabulary import complete_tree
+    exe = os.path.join(ROOT, "ar_orbslam2_amd", "_lib", "orbx_dropin")
+    if not os.path.exists(exe):
+        raise FileNotFoundError(f"{exe} missing: build with __graft_entry__.build()")
+    w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
+    n_img = 32
+    keep = args.dropin_dir
+    if keep:
+        os.makedirs(keep, exist_ok=True)
+    with (tempfile.TemporaryDirectory() if not keep else _nullctx(keep)) as td:
+        fr = np.stack([synth.frame(w, h, i, s) for s in range(args.threads) for i in range(n_img)])
+        fr.tofile(os.path.join(td, "frames.u8"))
+        ndesc = sum(10 ** l for l in range(7))
+        parent, is_leaf, desc, weight = complete_tree(
+            10, 6, np.random.default_rng(42).integers(0, 256, (ndesc, 32), dtype=np.uint8))
+        parent.astype(np.int32).tofile(os.path.join(td, "voc_parent.i32"))
+        is_leaf.astype(np.uint8).tofile(os.path.join(td, "voc_leaf.u8"))
+        desc.astype(np.uint8).tofile(os.path.join(td, "voc_desc.u8"))
+        weight.astype(np.float64).tofile(os.path.join(td, "voc_weight.f64"))
+        cmd = [exe, td, str(w), str(h), str(nf), str(n_img), str(args.threads),
+               str(args.warmup_frames), str(args.dropin_frames), str(local)]
+        if keep:  # inputs kept for a profiler run of the driver itself
+            with open(os.path.join(keep, "cmd.txt"), "w") as f:
+                f.write(" ".join(cmd[1:]) + "\n")
+        res = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if res.returncode != 0:
+        raise RuntimeError(f"orbx_dropin failed ({res.returncode}): {res.stderr[-2000:]}")
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    return {
+        "metric": METRIC + " (drop-in per-frame path, host images)", "value": d["fps"],
+        "unit": "frames/s", "n_gpus": 1, "steps": d["frames"], "warmup": args.warmup_frames,
+        "ms_per_step": d["mean_ms"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": cfg["workload"] + ", drop-in C ABI one frame per call",
+                   "host_threads": args.threads, "image": f"{w}x{h}", "nfeatures": nf},
+        "dropin": d,
+    }
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256,
+                    help="frames per step per camera stream")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="weak scaling: independent camera-stream pipelines per GPU, one HIP "
+                         "stream each (concurrent streams fill the CUs the serial stages leave idle)")
+    ap.add_argument("--streams-total", type=int, default=None,
+                    help="strong scaling: the job's camera-stream count, fixed over the GPUs "
+                         "(stream s on GPU s mod G); e.g. C5's 8 streams")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + sharding + aggregation only, no device work (gloo)")
+    ap.add_argument("--upload", dest="upload", action="store_true", default=True,
+                    help="also measure the rate with frames uploaded from pinned host memory")
+    ap.add_argument("--no-upload", dest="upload", action="store_false")
+    ap.add_argument("--dropin", action="store_true",
+                    help="measure the drop-in per-frame path (host images, one frame per call)")
+    ap.add_argument("--threads", type=int, default=4, help="--dropin host threads (cameras)")
+    ap.add_argument("--dropin-frames", type=int, default=500, help="--dropin frames per thread")
+    ap.add_argument("--warmup-frames", type=int, default=20, help="--dropin warm-up per thread")
+    ap.add_argument("--dropin-dir", default=None,
+                    help="--dropin: keep the driver's inputs (and its arguments in cmd.txt) here")
+    ap.add_argument("--pmc-dir", default=None,
+                    help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ CSVs of this bench command, "
+                         "used for roofline.traffic and the VALU-issue floor")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0,
+                    help="single-thread CPU baseline: at least this long and 200 frames")
+    ap.add_argument("--cpu-mp-seconds", type=float, default=6.0,
+                    help="all-cores CPU baseline window")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="skip the per-kernel roofline pass after the timed region")
+    ap.add_argument("--roofline-steps", type=int, default=5,
+                    help="steps of the single-stream roofline pass (per-kernel HIP events)")
+    args = ap.parse_args(argv)
+    if args.pmc_dir is None:  # the committed PMC passes of this config's default command
+        # (never another config's: a missing directory reports traffic / VALU floor as null)
+        args.pmc_dir = os.path.join(ROOT, "profiles",
+                                    "r02_pmc" if args.config == "C2" else
+                                    "r02_pmc_" + args.config.lower())
+    return args
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.dropin:
+        sys.exit(spawn_ranks(args.gpus, argv))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if args.streams_total is not None and args.streams_total < world:
+        raise SystemExit(f"--streams-total {args.streams_total} < {world} GPUs")
+    streams = streams_of_rank(rank, world, args.streams, args.streams_total)
+    cfg = CONFIGS[args.config]
+    if args.dry_run:
+        run_dry(args, cfg, rank, world, streams)
+        return
+    if args.dropin:
+        out = run_dropin(args, cfg, rank, world, local)
+        print(json.dumps(out), flush=True)
+        return
+    # the CPU baseline runs first, before this process touches the GPU (its all-cores leg
+    # forks one process per core) and without the GPU leg's host threads competing
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg.get("marker"):
+        cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_mp_seconds)
+    import torch
+    torch.cuda.set_device(local)
+    dist = init_dist(rank, world, local, "nccl")
+    if cfg.get("marker"):
+        out, target_desc = run_marker(args, cfg, rank, world, local, streams, dist)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_marker(cfg, args.cpu_seconds, target_desc)
+    else:
+        out = run_frames(args, cfg, rank, world, local, streams, dist)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist:
         dist.destroy_process_group()
 
 

@@ -438,6 +438,17 @@ int orbx_marker_profile_read(orbx_marker* mk, int32_t cap, char (*names)[32], do
 int orbx_debug_cvorb_cossin(const float* deg, int64_t n, float* c, float* s);
 int orbx_debug_retain_best(float* resp, uint32_t* ids, int32_t n, int32_t n_points,
                            int32_t force_global, int32_t* n_out);
+/* The finish step of SearchByBoW (kind 0 KF->Frame: match[n2] with values < n1; kind 1 KF->KF:
+ * match[n1], values < n2) or SearchForTriangulation (kind 2: m12[n1], values < n2) over a
+ * caller-given match array, orientation check off.  Out-of-range values (a stale match array)
+ * are dropped to -1 in out[] and reported as ORBX_EDEVICE; *nmatches counts the kept ones.
+ * Used by tests/test_match_gpu.py. */
+int orbx_debug_match_finish(int32_t kind, int32_t n1, int32_t n2, const int32_t* match,
+                            int32_t* out, int32_t* nmatches);
+/* The device glibc sincosf port of computeOrbDescriptor (ORBextractor.cc:103-104, orbx_math.h)
+ * for the n floats whose bit patterns are lo, lo+1, ...; s / c host arrays of n.  Used by
+ * tests/test_math_gpu.py (every float in [0, 2*pi] against the host libm). */
+int orbx_debug_sincosf(uint32_t lo, int64_t n, float* s, float* c);
 
 #ifdef __cplusplus
 }

@@ -159,6 +159,16 @@ def sincosf(x):
     return s.value, c.value
 
 
+def sincosf_bits(lo, n, threads=None):
+    """Host libm sincosf of the n floats with bit patterns lo, lo+1, ... -> (s, c) f32 arrays."""
+    s = np.empty(n, np.float32)
+    c = np.empty(n, np.float32)
+    import os
+    th = threads or min(16, len(os.sched_getaffinity(0)))
+    lib().oracle_sincosf_bits(C.c_uint32(lo), C.c_int64(n), _p(s), _p(c), C.c_int(th))
+    return s, c
+
+
 def fast_roi(roi, t):
     roi = np.ascontiguousarray(roi, np.uint8)
     rows, cols = roi.shape

@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstring>
 #include <list>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -802,6 +803,24 @@ void oracle_orb_descriptor(const uint8_t* blurred, int64_t stride, int cx, int c
   orb_descriptor(blurred, stride, cx, cy, angle, d);
 }
 void oracle_sincosf(float x, float* s, float* c) { sincosf(x, s, c); }
+// host libm sincosf over the floats with bit patterns lo .. lo+n-1 (reference outputs of the
+// device port's exhaustive test), on `threads` threads
+void oracle_sincosf_bits(uint32_t lo, int64_t n, float* s, float* c, int threads) {
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> th;
+  const int64_t per = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([=] {
+      const int64_t b = t * per, e = std::min(n, b + per);
+      for (int64_t i = b; i < e; i++) {
+        const uint32_t u = lo + (uint32_t)i;
+        float x;
+        memcpy(&x, &u, 4);
+        sincosf(x, s + i, c + i);
+      }
+    });
+  for (auto& x : th) x.join();
+}
 
 int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) {
   return descriptor_distance(a, b);

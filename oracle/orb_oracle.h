@@ -50,6 +50,7 @@ float oracle_ic_angle(const uint8_t* img, int64_t stride, int cx, int cy);
 void oracle_orb_descriptor(const uint8_t* blurred, int64_t stride, int cx, int cy, float angle,
                            uint8_t* desc32);
 void oracle_sincosf(float x, float* s, float* c);
+void oracle_sincosf_bits(uint32_t lo, int64_t n, float* s, float* c, int threads);
 
 /* matcher (ORBmatcher.cc) */
 int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);

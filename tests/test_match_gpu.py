@@ -141,3 +141,76 @@ def test_committed_match_goldens(golden_dir):
     _, p3 = ORBmatcher(0.6, False).SearchForTriangulation(ns(a, True), ns(b, True), MG.F_SHIFT,
                                                           False, (1e6, 1e6))
     assert np.array_equal(p3, np.load(os.path.join(golden_dir, "match_tri_pairs.npy")))
+
+
+def _big_node_sides(n, seed):
+    """n keyframe and n frame features in ONE vocabulary node (a dense, repetitive scene): frame
+    descriptors are permuted keyframe descriptors with 0-8 flipped bits (70 %) or random."""
+    rng = np.random.default_rng(seed)
+    d1 = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    perm = rng.permutation(n)
+    d2 = d1[perm].copy()
+    bits = np.unpackbits(d2, axis=1)
+    for i in range(n):
+        k = rng.integers(0, 9)
+        bits[i, rng.choice(256, k, replace=False)] ^= 1
+    d2 = np.packbits(bits, axis=1)
+    rand = rng.random(n) >= 0.7
+    d2[rand] = rng.integers(0, 256, (int(rand.sum()), 32), dtype=np.uint8)
+
+    def side(d, valid):
+        s = type("S", (), {})()
+        s.mDescriptors = d
+        s.mvKeys = s.mvKeysUn = np.zeros(n, O.KEYPOINT_DTYPE)
+        s.mvKeys["angle"] = rng.random(n).astype(np.float32) * 360
+        s.mFeatVec = (np.array([5], np.uint32), np.array([0, n], np.int32),
+                      np.arange(n, dtype=np.int32))
+        s.valid = valid
+        return s
+    return side(d1, (rng.random(n) < 0.6).astype(np.uint8)), side(d2, (rng.random(n) < 0.8).astype(np.uint8))
+
+
+@pytest.mark.parametrize("n", [1500, 5000])  # above the round-1 1024 limit; above the register bitmap
+def test_search_by_bow_single_huge_node(n):
+    """SearchByBoW has no node-size limit in the reference (ORBmatcher.cc:187-250, 557-622): a
+    node with thousands of candidates must give the oracle's matches (vbMatched2 semantics)."""
+    kf, f = _big_node_sides(n, n)
+    for ratio, ori in ((0.7, True), (0.9, False)):
+        n_ref, m_ref = O.search_by_bow_kf_f(_oracle_bow_side(kf), _oracle_bow_side(f, False),
+                                            ratio, ori)
+        fr = type("F", (), {})()
+        fr.mDescriptors, fr.mvKeys, fr.mFeatVec = f.mDescriptors, f.mvKeys, f.mFeatVec
+        got_n, got = ORBmatcher(ratio, ori).SearchByBoW(kf, fr)
+        assert got_n == n_ref and n_ref > 50
+        assert np.array_equal(got, m_ref)
+        f.is_keyframe = True
+        n_ref, m_ref = O.search_by_bow_kf_kf(_oracle_bow_side(kf), _oracle_bow_side(f), ratio, ori)
+        got_n, got = ORBmatcher(ratio, ori).SearchByBoW(kf, f)
+        del f.is_keyframe
+        assert got_n == n_ref and n_ref > 50
+        assert np.array_equal(got, m_ref)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_finish_kernels_reject_stale_indices(kind):
+    """A match array holding indices outside the other side (what a stale buffer would hold)
+    makes the finish kernels report ORBX_EDEVICE and drop those entries, never dereference
+    them (the round-1 C5 fault was an out-of-bounds read through such an index)."""
+    import ctypes as C
+    from ar_orbslam2_amd._ffi import lib, ptr
+    n1, n2 = 300, 200
+    n = n2 if kind == 0 else n1
+    other = n1 if kind == 0 else n2
+    rng = np.random.default_rng(kind)
+    match = np.where(rng.random(n) < 0.5, rng.integers(0, other, n), -1).astype(np.int32)
+    out = np.zeros(n, np.int32)
+    cnt = C.c_int32()
+    rc = lib().orbx_debug_match_finish(kind, n1, n2, ptr(match), ptr(out), C.byref(cnt))
+    assert rc == 0 and np.array_equal(out, match) and cnt.value == int((match >= 0).sum())
+    bad = match.copy()
+    bad[::7] = other + 10 ** np.arange(len(bad[::7])) % 1_000_000_007  # far out of range
+    bad[3] = 2 ** 31 - 1
+    rc = lib().orbx_debug_match_finish(kind, n1, n2, ptr(bad), ptr(out), C.byref(cnt))
+    assert rc == -3  # ORBX_EDEVICE
+    keep = np.where((bad >= 0) & (bad < other), bad, -1)
+    assert np.array_equal(out, keep) and cnt.value == int((keep >= 0).sum())

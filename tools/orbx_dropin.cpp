@@ -1,0 +1,267 @@
+// orbx_dropin — measures the drop-in per-frame path the way ORB-SLAM2 calls it (bench.py
+// --dropin).  K host threads, each one camera with its own extractor (the reference keeps one
+// ORBextractor per camera and runs the stereo pair's two on two threads, Frame.cc:83-86), push
+// pageable host images (cv::Mat) one frame per call through the C ABI:
+//   orbx_extract                    ORBextractor::operator()    Frame.cc:252-258, ORBextractor.cc:985-1045
+//   orbx_vocabulary_transform       Frame::ComputeBoW           Frame.cc:400-407
+//   orbx_search_by_bow_kf_f         SearchByBoW(KF*, F&)        Tracking.cc:1132-1136 (TrackReferenceKeyFrame)
+//   orbx_search_for_triangulation   SearchForTriangulation      LocalMapping.cc:238-241
+// with the previous frame of the same camera as the keyframe.  Prints one JSON line: aggregate
+// frames/s and per-frame latency (median / mean, as mono_tum.cc:113-121 reports tracking time),
+// per call.
+//
+// usage: orbx_dropin DIR W H NFEATURES N_IMG THREADS WARMUP FRAMES DEVICE
+//   DIR/frames.u8       THREADS x N_IMG x H x W u8 images
+//   DIR/voc_parent.i32, voc_leaf.u8, voc_desc.u8, voc_weight.f64   k=10, L=6 vocabulary nodes
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "orbx.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+std::vector<char> slurp(const std::string& path) {
+  std::vector<char> v;
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", path.c_str());
+    exit(2);
+  }
+  fseek(f, 0, SEEK_END);
+  const long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  v.resize((size_t)n);
+  if (n && fread(v.data(), 1, (size_t)n, f) != (size_t)n) {
+    fprintf(stderr, "short read %s\n", path.c_str());
+    exit(2);
+  }
+  fclose(f);
+  return v;
+}
+
+#define CK(x)                                                        \
+  do {                                                               \
+    int rc_ = (x);                                                   \
+    if (rc_ != ORBX_OK) {                                            \
+      fprintf(stderr, "%s failed: %d (line %d)\n", #x, rc_, __LINE__); \
+      exit(3);                                                       \
+    }                                                                \
+  } while (0)
+
+// One frame as the matchers see it (Frame / KeyFrame members the calls read).
+struct FrameData {
+  int n = 0;
+  std::vector<orbx_keypoint> kps;
+  std::vector<uint8_t> desc;
+  std::vector<float> angle;
+  std::vector<uint8_t> valid, has_mp;
+  std::vector<uint32_t> fv_ids, bow_words;
+  std::vector<int32_t> fv_off, fv_feats;
+  std::vector<double> bow_values;
+  std::vector<uint32_t> word_of, node_of;
+  int fv_n = 0, bow_n = 0;
+  void reserve(int cap) {
+    kps.resize(cap);
+    desc.resize((size_t)cap * 32);
+    angle.resize(cap);
+    valid.resize(cap);
+    has_mp.resize(cap);
+    fv_ids.resize(cap);
+    fv_off.resize(cap + 1);
+    fv_feats.resize(cap);
+    bow_words.resize(cap);
+    bow_values.resize(cap);
+    word_of.resize(cap);
+    node_of.resize(cap);
+  }
+  orbx_featvec fv() const { return {fv_n, fv_ids.data(), fv_off.data(), fv_feats.data()}; }
+};
+
+struct Stats {
+  std::vector<double> total, extract, bow, search_bow, search_tri;
+  long long matches_bow = 0, matches_tri = 0, keypoints = 0;
+};
+
+double median(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  const size_t m = v.size() / 2;
+  return v.size() % 2 ? v[m] : 0.5 * (v[m - 1] + v[m]);
+}
+double mean(const std::vector<double>& v) {
+  double s = 0;
+  for (double x : v) s += x;
+  return v.empty() ? 0 : s / v.size();
+}
+double pct(std::vector<double> v, double p) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, (size_t)(p * (v.size() - 1) + 0.5))];
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 10) {
+    fprintf(stderr, "usage: %s DIR W H NFEATURES N_IMG THREADS WARMUP FRAMES DEVICE\n", argv[0]);
+    return 1;
+  }
+  const std::string dir = argv[1];
+  const int W = atoi(argv[2]), H = atoi(argv[3]), NF = atoi(argv[4]), NIMG = atoi(argv[5]);
+  const int T = atoi(argv[6]), WARM = atoi(argv[7]), FR = atoi(argv[8]), DEV = atoi(argv[9]);
+  const std::vector<char> frames = slurp(dir + "/frames.u8");
+  if (frames.size() != (size_t)T * NIMG * W * H) {
+    fprintf(stderr, "frames.u8 has %zu bytes, expected %zu\n", frames.size(),
+            (size_t)T * NIMG * W * H);
+    return 2;
+  }
+  const std::vector<char> parent = slurp(dir + "/voc_parent.i32"), leaf = slurp(dir + "/voc_leaf.u8"),
+                          vdesc = slurp(dir + "/voc_desc.u8"), weight = slurp(dir + "/voc_weight.f64");
+  const int n_nodes = (int)(parent.size() / 4);
+  orbx_vocabulary* voc = nullptr;
+  CK(orbx_vocabulary_create(10, 6, ORBX_SCORE_L1, ORBX_WEIGHT_TF_IDF, n_nodes,
+                            (const int32_t*)parent.data(), (const uint8_t*)leaf.data(),
+                            (const uint8_t*)vdesc.data(), (const double*)weight.data(), DEV, &voc));
+
+  // SearchForTriangulation geometry: R = I, t = (0.10, 0.02, 0.05), TUM1 K
+  const float fx = 517.306408f, fy = 516.469215f, cx = 318.643040f, cy = 255.313989f;
+  const float tx = 0.10f, ty = 0.02f, tz = 0.05f;
+  const float Kinv[9] = {1 / fx, 0, -cx / fx, 0, 1 / fy, -cy / fy, 0, 0, 1};
+  const float Tx[9] = {0, -tz, ty, tz, 0, -tx, -ty, tx, 0};
+  float A[9], F12[9];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      float s = 0;
+      for (int k = 0; k < 3; k++) s += Tx[3 * r + k] * Kinv[3 * k + c];
+      A[3 * r + c] = s;
+    }
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      float s = 0;
+      for (int k = 0; k < 3; k++) s += Kinv[3 * k + r] * A[3 * k + c];  // Kinv^T * A
+      F12[3 * r + c] = s;
+    }
+  const float R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, tv[3] = {tx, ty, tz}, Cw[3] = {0, 0, 0};
+  float ex = 0, ey = 0;
+  CK(orbx_epipole(R, tv, Cw, fx, fy, cx, cy, &ex, &ey));
+
+  std::vector<Stats> stats(T);
+  std::atomic<int> ready{0};
+  std::atomic<bool> go{false};
+  std::vector<double> thread_wall(T, 0.0);
+  auto worker = [&](int t) {
+    orbx_params prm{NF, 1.2f, 8, 20, 7};
+    orbx_extractor* exr = nullptr;
+    CK(orbx_extractor_create(&prm, DEV, &exr));
+    float scale[8], sigma2[8];
+    int32_t nl = 0;
+    CK(orbx_extractor_tables(exr, &nl, scale, nullptr, sigma2, nullptr, nullptr));
+    const int cap = NF * 2 + 64;
+    FrameData fd[2];
+    fd[0].reserve(cap);
+    fd[1].reserve(cap);
+    std::vector<int32_t> match(cap), pairs((size_t)cap * 2);
+    Stats& st = stats[t];
+    uint32_t lcg = 0x9E3779B9u * (t + 1);
+    auto rnd = [&]() {
+      lcg = lcg * 1664525u + 1013904223u;
+      return (lcg >> 8) * (1.0f / 16777216.0f);
+    };
+    ready++;
+    while (!go.load()) std::this_thread::yield();
+    Clock::time_point t_start;
+    for (int f = 0; f < WARM + FR; f++) {
+      if (f == WARM) t_start = Clock::now();
+      FrameData& cur = fd[f & 1];
+      FrameData& prev = fd[(f + 1) & 1];
+      const uint8_t* img = (const uint8_t*)frames.data() + ((size_t)t * NIMG + f % NIMG) * W * H;
+      const auto a = Clock::now();
+      int32_t n = 0;
+      CK(orbx_extract(exr, img, W, H, W, cur.kps.data(), cur.desc.data(), cap, &n));
+      cur.n = n;
+      const auto b = Clock::now();
+      CK(orbx_vocabulary_transform(voc, cur.desc.data(), n, 4, cur.word_of.data(),
+                                   cur.node_of.data(), cur.bow_words.data(), cur.bow_values.data(),
+                                   &cur.bow_n, cur.fv_ids.data(), cur.fv_off.data(),
+                                   cur.fv_feats.data(), &cur.fv_n));
+      for (int i = 0; i < n; i++) {
+        cur.angle[i] = cur.kps[i].angle;
+        cur.valid[i] = rnd() < 0.6f;
+        cur.has_mp[i] = rnd() < 0.4f;
+      }
+      const auto c = Clock::now();
+      auto d = c, e = c;
+      int32_t nb = 0, nt = 0;
+      if (f > 0) {
+        orbx_bow_side kf{prev.n, prev.desc.data(), prev.angle.data(), prev.valid.data(), prev.fv()};
+        orbx_bow_side fr{cur.n, cur.desc.data(), cur.angle.data(), nullptr, cur.fv()};
+        CK(orbx_search_by_bow_kf_f(&kf, &fr, 0.7f, 1, match.data(), &nb));
+        d = Clock::now();
+        orbx_tri_side k1{prev.n, prev.desc.data(), prev.kps.data(), nullptr, prev.has_mp.data(),
+                         prev.fv(), scale, sigma2, nl};
+        orbx_tri_side k2{cur.n, cur.desc.data(), cur.kps.data(), nullptr, cur.has_mp.data(),
+                         cur.fv(), scale, sigma2, nl};
+        CK(orbx_search_for_triangulation(&k1, &k2, F12, ex, ey, 0, 0.6f, 0, pairs.data(), &nt));
+        e = Clock::now();
+      }
+      if (f >= WARM) {
+        auto ms = [](Clock::time_point x, Clock::time_point y) {
+          return std::chrono::duration<double, std::milli>(y - x).count();
+        };
+        st.total.push_back(ms(a, e));
+        st.extract.push_back(ms(a, b));
+        st.bow.push_back(ms(b, c));
+        st.search_bow.push_back(ms(c, d));
+        st.search_tri.push_back(ms(d, e));
+        st.matches_bow += nb;
+        st.matches_tri += nt;
+        st.keypoints += n;
+      }
+    }
+    thread_wall[t] = std::chrono::duration<double>(Clock::now() - t_start).count();
+    orbx_extractor_destroy(exr);
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++) th.emplace_back(worker, t);
+  while (ready.load() < T) std::this_thread::yield();
+  go = true;
+  for (auto& x : th) x.join();
+
+  Stats all;
+  for (auto& s : stats) {
+    all.total.insert(all.total.end(), s.total.begin(), s.total.end());
+    all.extract.insert(all.extract.end(), s.extract.begin(), s.extract.end());
+    all.bow.insert(all.bow.end(), s.bow.begin(), s.bow.end());
+    all.search_bow.insert(all.search_bow.end(), s.search_bow.begin(), s.search_bow.end());
+    all.search_tri.insert(all.search_tri.end(), s.search_tri.begin(), s.search_tri.end());
+    all.matches_bow += s.matches_bow;
+    all.matches_tri += s.matches_tri;
+    all.keypoints += s.keypoints;
+  }
+  const double wall = *std::max_element(thread_wall.begin(), thread_wall.end());
+  const double nfr = (double)all.total.size();
+  printf("{\"fps\": %.2f, \"frames\": %d, \"threads\": %d, \"wall_s\": %.4f, "
+         "\"median_ms\": %.4f, \"mean_ms\": %.4f, \"p90_ms\": %.4f, "
+         "\"per_call_median_ms\": {\"orbx_extract\": %.4f, \"orbx_vocabulary_transform\": %.4f, "
+         "\"orbx_search_by_bow_kf_f\": %.4f, \"orbx_search_for_triangulation\": %.4f}, "
+         "\"per_call_mean_ms\": {\"orbx_extract\": %.4f, \"orbx_vocabulary_transform\": %.4f, "
+         "\"orbx_search_by_bow_kf_f\": %.4f, \"orbx_search_for_triangulation\": %.4f}, "
+         "\"keypoints_per_frame\": %.1f, \"bow_matches_per_frame\": %.1f, "
+         "\"triangulation_matches_per_frame\": %.1f}\n",
+         nfr / wall, (int)nfr, T, wall, median(all.total), mean(all.total), pct(all.total, 0.9),
+         median(all.extract), median(all.bow), median(all.search_bow), median(all.search_tri),
+         mean(all.extract), mean(all.bow), mean(all.search_bow), mean(all.search_tri),
+         all.keypoints / nfr, all.matches_bow / nfr, all.matches_tri / nfr);
+  orbx_vocabulary_destroy(voc);
+  return 0;
+}

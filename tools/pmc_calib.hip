@@ -13,7 +13,7 @@ constexpr size_t kBytes = size_t(1) << 30;
 
 template <class T>
 __global__ __launch_bounds__(256) void calib_read(const T* __restrict__ src, size_t n,
-                                                  uint32_t* __restrict__ sink) {
+                                                  uint32_t* __restrict__ sink, uint32_t magic) {
   uint32_t acc = 0;
   for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
     const T v = src[i];
@@ -22,7 +22,10 @@ __global__ __launch_bounds__(256) void calib_read(const T* __restrict__ src, siz
     for (int k = 0; k < (int)(sizeof(T) >= 4 ? sizeof(T) / 4 : 1); k++)
       acc ^= sizeof(T) >= 4 ? w[k] : (uint32_t)(*(const uint8_t*)&v);
   }
-  if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;  // never true for the zero buffer: no stores
+  // never true for the zero buffer, so no stores; `magic` is a kernel argument so the compiler
+  // cannot prove the comparison false (a literal above 255 let it delete the whole 1-B loop,
+  // which is why round 1 saw FETCH_SIZE = 0 for 1-B loads)
+  if (acc == magic) sink[blockIdx.x] = acc;
 }
 
 template <class T>
@@ -48,9 +51,9 @@ int main() {
   CK(hipMemset(buf, 0, kBytes));
   CK(hipDeviceSynchronize());
   const dim3 grid(8192), block(256);
-  hipLaunchKernelGGL(calib_read<uint64_t>, grid, block, 0, 0, (const uint64_t*)buf, kBytes / 8, sink);
-  hipLaunchKernelGGL(calib_read<uint32_t>, grid, block, 0, 0, (const uint32_t*)buf, kBytes / 4, sink);
-  hipLaunchKernelGGL(calib_read<uint8_t>, grid, block, 0, 0, (const uint8_t*)buf, kBytes, sink);
+  hipLaunchKernelGGL(calib_read<uint64_t>, grid, block, 0, 0, (const uint64_t*)buf, kBytes / 8, sink, 0x9E3779B9u);
+  hipLaunchKernelGGL(calib_read<uint32_t>, grid, block, 0, 0, (const uint32_t*)buf, kBytes / 4, sink, 0x9E3779B9u);
+  hipLaunchKernelGGL(calib_read<uint8_t>, grid, block, 0, 0, (const uint8_t*)buf, kBytes, sink, 0x9E3779B9u);
   hipLaunchKernelGGL(calib_write<uint64_t>, grid, block, 0, 0, (uint64_t*)buf, kBytes / 8);
   hipLaunchKernelGGL(calib_write<uint32_t>, grid, block, 0, 0, (uint32_t*)buf, kBytes / 4);
   hipLaunchKernelGGL(calib_write<uint8_t>, grid, block, 0, 0, (uint8_t*)buf, kBytes);
