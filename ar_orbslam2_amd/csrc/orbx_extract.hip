@@ -466,6 +466,7 @@ struct FastTile {
   int16_t level, tx, ty, pad;
 };
 
+template <bool PAIR>
 __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ pyr,
                                                    int64_t pyr_bytes, uint8_t* __restrict__ vmap,
                                                    uint64_t* __restrict__ bitmaps,
@@ -480,8 +481,9 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   constexpr int kVS = kWinG * 4;          // V row stride (bytes)
   constexpr int kGroups = kWinR * kWinG;
   constexpr int kRowB = kInD * 4;         // staged row stride (bytes)
+  constexpr int kCS = 1;                  // bytes per staged column
   constexpr int kQ = (kWinR + 3) / 4 * 64 + 64;  // per-wave queue bound (rows + ring pass)
-  __shared__ __align__(16) uint32_t s_in[kInR][kInD];
+  __shared__ __align__(16) uint32_t s_in[kInR * kRowB / 4];
   __shared__ __align__(16) uint32_t s_v32[kWinR * kWinG];
   __shared__ uint16_t s_q[4][kQ + 64];
   int bx, img;
@@ -494,13 +496,15 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   const int X0 = T.tx * kFastT, Y0 = T.ty * kFastT;
   // staged window: rows Y0-4 .. Y0+67 clamped, 8-byte pieces of columns X0-8 .. X0+71 (zero
   // left of the image; the 64-B pitch covers the right side)
-  for (int i = tid; i < kInR * (kInD / 2); i += 256) {
-    const int r = i / (kInD / 2), c = i - r * (kInD / 2);
+  auto piece = [&](int r, int c) -> uint2 {
     const int y = min(max(Y0 + r - 4, 0), G.h - 1);
     const int x = X0 - 8 + 8 * c;
-    *(uint2*)&s_in[r][2 * c] = (x >= 0 && x < G.pitch)
-                                   ? *(const uint2*)(src + (int64_t)y * G.pitch + x)
+    return (x >= 0 && x < G.pitch) ? *(const uint2*)(src + (int64_t)y * G.pitch + x)
                                    : make_uint2(0u, 0u);
+  };
+  for (int i = tid; i < kInR * (kInD / 2); i += 256) {
+    const int r = i / (kInD / 2), c = i - r * (kInD / 2);
+    *(uint2*)&s_in[r * kInD + 2 * c] = piece(r, c);
   }
   for (int i = tid; i < kGroups; i += 256) s_v32[i] = 0;
   __syncthreads();
@@ -513,14 +517,25 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     q[(pass >> lane) & 1 ? nq + lane_rank(pass) : kQ + lane] = (uint16_t)idx;
     nq += __popcll(pass);
   };
-  // V window coordinates: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, byte vx + 4
-  // holds the pixel.  Tile columns: lane = column, one wave-uniform row per pass.
+  // V window coordinates: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, column vx + 4
+  // holds the pixel.  Tile columns: lane = column, one wave-uniform row (pair) per pass.
   const uint64_t col_ok = __ballot(X0 + lane >= xlo && X0 + lane < xhi);
   if (col_ok != 0) {
     const int vy_lo = max(0, ylo - (Y0 - 1)), vy_hi = min(kWinR, yhi - (Y0 - 1));
-    for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)  // rows = wid mod 4
-      enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th, col_ok),
-              vy * kVS + 4 + lane);
+    if constexpr (PAIR) {
+      // row pairs (vy, vy + 1), pair index = wid mod 4 (vy_lo is even, so vy + 1 <= 65)
+      for (int vy = vy_lo + 2 * wid; vy < vy_hi; vy += 8) {
+        uint64_t m0, m1;
+        fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th, col_ok,
+                             vy + 1 < vy_hi ? col_ok : 0, &m0, &m1);
+        enqueue(m0, vy * kVS + 4 + lane);
+        enqueue(m1, (vy + 1) * kVS + 4 + lane);
+      }
+    } else {
+      for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)  // rows = wid mod 4
+        enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th, col_ok),
+                vy * kVS + 4 + lane);
+    }
   }
   // ring columns X0-1 (vx 3) and X0+64 (vx 68): 2 * kWinR pixels, lane k = (row, side)
   for (int k0 = wid * 64; k0 < 2 * kWinR; k0 += 256) {
@@ -528,7 +543,8 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     const int vy = min(k >> 1, kWinR - 1), vx = k & 1 ? 4 + kFastT : 3;
     const int x = X0 - 4 + vx, y = Y0 - 1 + vy;
     const uint64_t ok = __ballot(k < 2 * kWinR && x >= xlo && x < xhi && y >= ylo && y < yhi);
-    if (ok != 0) enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + vx + 1, ini_th, ok), vy * kVS + vx);
+    if (ok != 0)
+      enqueue(fast_pretest<kRowB, kCS>(sin8 + vy * kRowB + (vx + 1) * kCS, ini_th, ok), vy * kVS + vx);
   }
   uint8_t* s_v = (uint8_t*)s_v32;
   for (int j0 = 0; j0 < nq; j0 += 64) {
@@ -536,7 +552,7 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     if (j < nq) {
       const int i = q[j];  // = vy * kVS + vx
       const int vy = i / kVS, vx = i - vy * kVS;
-      const int sc = fast_score((const uint8_t*)s_in, kInD * 4, vx + 4, vy + 3);
+      const int sc = fast_score<kCS>((const uint8_t*)s_in, kRowB, vx + 4, vy + 3);
       s_v[i] = (uint8_t)min(255, max(0, sc + 1));
     }
   }
@@ -1497,6 +1513,7 @@ struct orbx_plan {
   size_t oct_smem = 0;
   int oct_nt = 0;  // k_octree threads per workgroup (kOctNT or kOctNTBig)
   int cell_cap = 0;
+  bool fast_pair = true;  // k_fast_tile pretest on row pairs (ORBX_FAST_PAIR=0: one row per lane)
   const uint8_t* last_in = nullptr;
   int last_n = 0;
   // graph cache keyed by (input pointer, batch)
@@ -1622,7 +1639,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   }
   const int ncells = (int)g.cells.size();
   if (ncells > 0) {
-    hipLaunchKernelGGL(k_fast_tile, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
+    hipLaunchKernelGGL(P->fast_pair ? k_fast_tile<true> : k_fast_tile<false>, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
                        g.ini_th);
     pr.mark(P->stream, st_fs);
@@ -1684,6 +1701,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->params = *params;
   P->max_batch = max_batch;
   P->device = hip_device;
+  if (const char* e = getenv("ORBX_FAST_PAIR")) P->fast_pair = atoi(e) != 0;
   const Geometry& g = P->g;
   auto fail = [&](int code) {
     orbx_plan_destroy(P);

@@ -149,13 +149,13 @@ int launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_
 // t.  Any 9-arc contains 4 cyclically consecutive even circle points, all darker or all
 // brighter; each point's compare is a v_cmp into a lane mask and, with A_k = D_k & D_k+1,
 // OR_k A_k & A_k+2 = (A0|A4)&(A2|A6) | (A1|A5)&(A3|A7) runs in the scalar unit.
-template <int RS>
+template <int RS, int CS = 1>
 __device__ __forceinline__ uint64_t fast_pretest(const uint8_t* c, int t, uint64_t ok) {
-  const int v = c[3 * RS + 3];
+  const int v = c[3 * RS + 3 * CS];
   const int lo = v - t, hi = v + t;
   // even circle points in circle order: (0,3) (2,2) (3,0) (2,-2) (0,-3) (-2,-2) (-3,0) (-2,2)
-  const int e[8] = {c[6 * RS + 3], c[5 * RS + 5], c[3 * RS + 6], c[RS + 5],
-                    c[3],          c[RS + 1],     c[3 * RS],     c[5 * RS + 1]};
+  const int e[8] = {c[6 * RS + 3 * CS], c[5 * RS + 5 * CS], c[3 * RS + 6 * CS], c[RS + 5 * CS],
+                    c[3 * CS],          c[RS + CS],         c[3 * RS],          c[5 * RS + CS]};
   uint64_t pd[8], pb[8], dk[8], bk[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
@@ -172,6 +172,52 @@ __device__ __forceinline__ uint64_t fast_pretest(const uint8_t* c, int t, uint64
   return any & ok;
 }
 
+// The same pretest for two pixels per lane — rows r and r+1 of one column — in the 16-bit
+// halves of each dword, on the VALU operations that issue at full rate on gfx950 (32-bit add /
+// sub / and / or: 2 cycles per wave instruction where compares, min/max, shifts and packed
+// ops take 4; profiles/valu_calibration.json).  With C the centre pair, a circle-point pair E
+// and H = 0x80008000 (all values < 2^9, so no half borrows from the other):
+//   darker  e < v - t   <=>  bit 15 of each half of  (C + (0x8000 - t - 1)) - E     is set
+//   brighter e > v + t  <=>  bit 15 of each half of  (E | H) - (C + t + 1)          is set
+// and the arc logic of fast_pretest runs on those flag words with and / or.  Returns the lane
+// masks of rows r (low halves) and r+1 (high halves).
+// c: the top-left byte of the row-r pixel's 7 x 7 neighbourhood in bytes with row stride RS;
+// a pair (row r, row r + 1) is built with one v_perm.  (A staged row-pair dword layout that
+// makes each pair one ds_read_b32 measured slower: 515 vs 392 us per 256 C2 frames, from the
+// staging's extra VALU and the halved occupancy of its 23 KB window.)
+template <int RS>
+__device__ __forceinline__ uint32_t fast_pair(const uint8_t* p) {
+  return __builtin_amdgcn_perm((uint32_t)p[RS], (uint32_t)p[0], 0x0C040C00u);
+}
+template <int RS>
+__device__ __forceinline__ void fast_pretest2(const uint8_t* c, int t, uint64_t ok0, uint64_t ok1,
+                                              uint64_t* m0, uint64_t* m1) {
+  const uint32_t C = fast_pair<RS>(c + 3 * RS + 3);
+  const uint32_t rep = 0x10001u;
+  const uint32_t L = C + (uint32_t)(0x8000 - t - 1) * rep;
+  const uint32_t Hh = C + (uint32_t)(t + 1) * rep;
+  const uint32_t E[8] = {fast_pair<RS>(c + 6 * RS + 3), fast_pair<RS>(c + 5 * RS + 5),
+                         fast_pair<RS>(c + 3 * RS + 6), fast_pair<RS>(c + RS + 5),
+                         fast_pair<RS>(c + 3),          fast_pair<RS>(c + RS + 1),
+                         fast_pair<RS>(c + 3 * RS),     fast_pair<RS>(c + 5 * RS + 1)};
+  uint32_t D[8], B[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    D[k] = L - E[k];
+    B[k] = (E[k] | 0x80008000u) - Hh;
+  }
+  uint32_t pd[8], pb[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    pd[k] = D[k] & D[(k + 1) & 7];
+    pb[k] = B[k] & B[(k + 1) & 7];
+  }
+  const uint32_t any = ((pd[0] | pd[4]) & (pd[2] | pd[6])) | ((pd[1] | pd[5]) & (pd[3] | pd[7])) |
+                       ((pb[0] | pb[4]) & (pb[2] | pb[6])) | ((pb[1] | pb[5]) & (pb[3] | pb[7]));
+  *m0 = __ballot((any & 0x8000u) != 0) & ok0;
+  *m1 = __ballot((int32_t)any < 0) & ok1;
+}
+
 // rank of this lane among the set lanes of m
 __device__ __forceinline__ int lane_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -184,13 +230,16 @@ __device__ __forceinline__ int lane_rank(uint64_t m) {
 // on packed u16 pairs (c, 255 - c), one v_pk_min_u16 per point and window step giving min c and
 // 255 - max c together.
 typedef unsigned short fast_u16x2 __attribute__((ext_vector_type(2)));
+template <int CS = 1>  // bytes per column
 __device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, int y) {
-  const uint8_t* c = s + y * stride + x;
+  const uint8_t* c = s + y * stride + x * CS;
   const int v = c[0];
-  const int px[16] = {c[3 * stride],  c[3 * stride + 1],  c[2 * stride + 2],  c[stride + 3],
-                      c[3],           c[-stride + 3],     c[-2 * stride + 2], c[-3 * stride + 1],
-                      c[-3 * stride], c[-3 * stride - 1], c[-2 * stride - 2], c[-stride - 3],
-                      c[-3],          c[stride - 3],      c[2 * stride - 2],  c[3 * stride - 1]};
+  const int px[16] = {c[3 * stride],           c[3 * stride + CS],      c[2 * stride + 2 * CS],
+                      c[stride + 3 * CS],      c[3 * CS],               c[-stride + 3 * CS],
+                      c[-2 * stride + 2 * CS], c[-3 * stride + CS],     c[-3 * stride],
+                      c[-3 * stride - CS],     c[-2 * stride - 2 * CS], c[-stride - 3 * CS],
+                      c[-3 * CS],              c[stride - 3 * CS],      c[2 * stride - 2 * CS],
+                      c[3 * stride - CS]};
   fast_u16x2 p[16], m2[16], m4[16];
 #pragma unroll
   for (int k = 0; k < 16; k++)  // c | (255 - c) << 16 = 0xFF0000 - 65535 c: one v_mad_i32_i24

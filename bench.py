@@ -129,37 +129,49 @@ def pmc_traffic(pmc_dir, kernel):
             f"this kernel's access width)")
 
 
-def valu_cycles():
-    """Cycles one wave64 VALU instruction occupies its SIMD when the SIMD is saturated.
-    MI355X_MICROARCH.md (SIMD-32: 'issues each VALU instruction over 2 cycles'; one wave alone
-    sustains 4).  profiles/valu_calibration.json (tools/valu_calib.hip, >= 2 waves per SIMD in
-    the integer instruction mix of these kernels) overrides the guide's figure when present."""
-    cal = _load_json("valu_calibration.json")
-    if cal and cal.get("cycles_per_valu_saturated"):
-        return float(cal["cycles_per_valu_saturated"]), "profiles/valu_calibration.json"
-    return 2.0, "MI355X_MICROARCH.md (2 cycles per wave64 VALU instruction on SIMD-32)"
-
-
-def pmc_valu(pmc_dir, kernel, avg_launch_us):
-    """VALU-issue roofline of `kernel` from the SQ counter pass of this bench command
-    (sq_counters.csv: SQ_INSTS_VALU summed over a dispatch's waves): the launch cannot finish
-    before INSTS_VALU x c / (1024 SIMDs x 2.4 GHz), c from valu_cycles()."""
+def pmc_issue(pmc_dir, kernel, avg_launch_us):
+    """Issue-rate roofline of `kernel` from the SQ counter pass of this bench command
+    (sq_counters.csv, per-dispatch sums over the chip's SIMDs).  Measured on this MI355X with
+    tools/valu_calib.hip (profiles/valu_calibration.json): a wave64 VALU instruction occupies
+    its SIMD for one quad-cycle (4 cycles) except 32-bit add / sub / and / or / xor and f32 add /
+    fma, which dual-issue (2 cycles: SQ_ACTIVE_INST_VALU2 counts the quad-cycles in which two
+    VALU instructions issued), and a SALU instruction takes one quad-cycle of its SIMD's scalar
+    issue (SQ_INST_CYCLES_SALU == SQ_INSTS_SALU).  So a launch cannot finish before
+      VALU floor = (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) x 4 / (1024 SIMDs x 2.4 GHz)
+      SALU floor = SQ_INSTS_SALU x 4 / (1024 SIMDs x 2.4 GHz)
+    and the larger floor is the bound.  Older passes without SQ_ACTIVE_INST_VALU2 price every
+    VALU instruction at 4 cycles (the calibrated cost of all but the dual-issue ops)."""
     import csv
     path = os.path.join(pmc_dir, "sq_counters.csv")
     if not os.path.exists(path) or not avg_launch_us:
         return None
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if r["Kernel_Name"].split("(")[0].endswith("::" + kernel)
-            and r["Counter_Name"] == "SQ_INSTS_VALU"]
-    if not vals:
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if r["Kernel_Name"].split("(")[0].endswith("::" + kernel):
+            per.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    if "SQ_INSTS_VALU" not in per:
         return None
-    instr = sum(vals) / len(vals)
-    c, src = valu_cycles()
-    floor_us = instr * c / VALU_SIMDS / (CLOCK_GHZ * 1e3)
-    return {"valu_instr_per_launch": round(instr), "cycles_per_instr": c,
-            "issue_floor_us": round(floor_us, 2), "frac": round(floor_us / avg_launch_us, 4),
-            "note": f"floor = SQ_INSTS_VALU x {c} cycles ({src}) / ({VALU_SIMDS} SIMDs x "
-                    f"{CLOCK_GHZ} GHz), frac = floor / avg_launch_us "
+    avg = {k: sum(v) / len(v) for k, v in per.items()}
+    us_per_qc = 4 / VALU_SIMDS / (CLOCK_GHZ * 1e3)
+    if "SQ_ACTIVE_INST_VALU" in avg and "SQ_ACTIVE_INST_VALU2" in avg:
+        valu_qc = avg["SQ_ACTIVE_INST_VALU"] - avg["SQ_ACTIVE_INST_VALU2"]
+        how = "(SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) quad-cycles"
+    else:
+        valu_qc = avg["SQ_INSTS_VALU"]
+        how = "SQ_INSTS_VALU x 1 quad-cycle (no SQ_ACTIVE_INST_VALU2 in this pass)"
+    valu_us = valu_qc * us_per_qc
+    salu_us = avg.get("SQ_INSTS_SALU", 0.0) * us_per_qc
+    bound = "valu" if valu_us >= salu_us else "salu"
+    floor = max(valu_us, salu_us)
+    return {"valu_instr_per_launch": round(avg["SQ_INSTS_VALU"]),
+            "valu_quad_cycles_per_launch": round(valu_qc),
+            "salu_instr_per_launch": round(avg.get("SQ_INSTS_SALU", 0.0)),
+            "valu_floor_us": round(valu_us, 2), "salu_floor_us": round(salu_us, 2),
+            "issue_bound": bound, "issue_floor_us": round(floor, 2),
+            "frac": round(floor / avg_launch_us, 4),
+            "note": f"VALU floor = {how} x 4 cycles / ({VALU_SIMDS} SIMDs x {CLOCK_GHZ} GHz); "
+                    f"SALU floor = SQ_INSTS_SALU x 4 cycles / the same; frac = larger floor / "
+                    f"avg_launch_us; costs from profiles/valu_calibration.json "
                     f"({os.path.relpath(path, ROOT)})"}
 
 
@@ -176,19 +188,23 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     a_bytes = alg.get(dom)
     achieved = (a_bytes / avg_s / 1e9) if a_bytes is not None else None
     traffic, tnote = pmc_traffic(pmc_dir, dom)
-    valu = pmc_valu(pmc_dir, dom, avg_s * 1e6)
+    issue = pmc_issue(pmc_dir, dom, avg_s * 1e6)
     hbm = {"achieved": round(achieved, 3) if achieved is not None else None,
            "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None}
     out = {"bound": "hbm", "kernel": dom, **hbm, "traffic": traffic, "traffic_note": tnote,
            "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": a_bytes}
-    if valu:
-        # VALU-issue roofline in the contract's fields; the HBM one kept under "hbm"
-        peak_ginstr = VALU_SIMDS * CLOCK_GHZ / valu["cycles_per_instr"]  # G wave-instr/s
-        out.update({"bound": "valu", "achieved": round(valu["valu_instr_per_launch"] / avg_s / 1e9, 3),
-                    "peak": round(peak_ginstr, 3), "unit": "G wave64 VALU instr/s",
-                    "frac": valu["frac"], "hbm": hbm})
-    out["valu_roofline"] = valu
+    if issue:
+        # issue-rate roofline in the contract's fields (achieved / peak in SIMD quad-cycles of
+        # the binding unit per second); the HBM one kept under "hbm"
+        qc = (issue["valu_quad_cycles_per_launch"] if issue["issue_bound"] == "valu"
+              else issue["salu_instr_per_launch"])
+        peak_gqc = VALU_SIMDS * CLOCK_GHZ / 4  # G SIMD quad-cycles per second
+        out.update({"bound": issue["issue_bound"], "achieved": round(qc / avg_s / 1e9, 3),
+                    "peak": round(peak_gqc, 3),
+                    "unit": f"G {issue['issue_bound'].upper()} issue quad-cycles/s",
+                    "frac": issue["frac"], "hbm": hbm})
+    out["issue_roofline"] = issue
     out["stages_ms_per_step"] = {k: round(v[0] / steps, 4) for k, v in stages.items()}
     out["stages_of"] = (f"roofline pass: camera stream 0 alone, {steps} steps of {B} frames "
                         f"after the timed region")

@@ -34,8 +34,9 @@ def main():
             # counter bytes (KB x 1024) per true byte for this access width per lane
             f = round(float(r["Counter_Value"]) * 1024 / KNOWN, 4)
             out[kind][f"{WIDTH[t]}B_per_lane"] = f or None  # 0: no usable reading
-    out["note"] = ("1-B streaming loads reported FETCH_SIZE 0 for a 1 GiB pass (not understood; no "
-                   "roofline kernel streams 1-B loads), so that width stays uncalibrated")
+    out["note"] = ("round 1 read FETCH_SIZE 0 for the 1-B loads: the kernel compared its byte "
+                   "XOR against a literal above 255, so the compiler deleted the load loop; the "
+                   "comparison value is now a kernel argument (tools/pmc_calib.hip)")
     path = os.path.join(ROOT, "profiles", "pmc_calibration.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out))

@@ -9,10 +9,13 @@
 # With a second argument "configs" it does the same for C3 C4 C5 instead (PMC passes, bench line,
 # kernel stats: <tag>_pmc_c3/, <tag>_bench_c3.jsonl, <tag>_kernel_stats_c3.csv, ...), without the
 # tests; the two parts fit one gpurun call each.
-# Usage: bash scripts/refresh_profiles.sh r01 [configs]
+# Usage: bash scripts/refresh_profiles.sh r02 [configs]
 set -e -o pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
 PART=${2:-main}
+# issue-rate counters (8 SQ counters, one pass): dual-issued VALU quad-cycles and SALU
+# instructions give bench.py's issue floors (profiles/valu_calibration.json)
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS"
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 cd $R
@@ -25,8 +28,7 @@ if [ "$PART" = configs ]; then
        python3 $R/bench.py --config $C --no-cpu-baseline --steps 5 > /dev/null 2> $D/f.err &&
      timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/w -o run -- \
        python3 $R/bench.py --config $C --no-cpu-baseline --steps 5 > /dev/null 2> $D/w.err &&
-     timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
-       SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $D/s -o run -- \
+     timeout -s KILL 150 rocprofv3 --pmc $SQ --output-format csv -d $D/s -o run -- \
        python3 $R/bench.py --config $C --no-cpu-baseline --steps 5 > /dev/null 2> $D/s.err &&
      cp $(find $D/f -name "*counter_collection.csv") $D/fetch_size.csv &&
      cp $(find $D/w -name "*counter_collection.csv") $D/write_size.csv &&
@@ -57,8 +59,7 @@ pmc() {  # pmc <outdir> <bench args...>
     python3 $R/bench.py --no-cpu-baseline --steps 5 "$@" > /dev/null 2> $D/f.err
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/w -o run -- \
     python3 $R/bench.py --no-cpu-baseline --steps 5 "$@" > /dev/null 2> $D/w.err
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
-    SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $D/s -o run -- \
+  timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d $D/s -o run -- \
     python3 $R/bench.py --no-cpu-baseline --steps 5 "$@" > /dev/null 2> $D/s.err
   cp $(find $D/f -name "*counter_collection.csv") $D/fetch_size.csv
   cp $(find $D/w -name "*counter_collection.csv") $D/write_size.csv

@@ -25,7 +25,7 @@ P = os.path.join(ROOT, "profiles")
 # config -> (suffix of the bench / kernel stats / trace files, suffix of the PMC dir)
 CONFIGS = {"C2": ("", ""), "AR": ("_ar", "_ar"), "C3": ("_c3", "_c3"), "C4": ("_c4", "_c4"),
            "C5": ("_c5", "_c5")}
-VALU_US = 4 / (1024 * 2.4e3)  # us per wave-instruction at full issue (1024 SIMDs, 2.4 GHz)
+QC_US = 4 / (1024 * 2.4e3)  # us per SIMD quad-cycle of issue (1024 SIMDs, 2.4 GHz)
 
 
 def short(name: str) -> str:
@@ -58,7 +58,7 @@ def counters(pmc_dir):
     return agg, calls
 
 
-def main(tag="r01"):
+def main(tag="r02"):
     check, summ = [], []
     for cfg, (sfx, psfx) in CONFIGS.items():
         bench = os.path.join(P, f"{tag}_bench{sfx}.jsonl")
@@ -84,15 +84,20 @@ def main(tag="r01"):
                          f"pass): {ru['avg_launch_us']:.2f} us")
         check.append(f"    bench.py roofline avg_launch_us of the committed line (separate run): "
                      f"{rf['avg_launch_us']:.2f} us")
-        vr = rf.get("valu_roofline") or {}
-        check.append(f"    HBM: achieved {rf.get('achieved')} GB/s of {rf['peak']} (frac "
-                     f"{rf.get('frac')}); VALU issue floor {vr.get('issue_floor_us')} us "
-                     f"(frac {vr.get('frac')})")
+        vr = rf.get("issue_roofline") or rf.get("valu_roofline") or {}
+        hb = rf.get("hbm") or rf
+        check.append(f"    HBM: achieved {hb.get('achieved')} GB/s of {hb.get('peak')} (frac "
+                     f"{hb.get('frac')}); issue floors: VALU {vr.get('valu_floor_us')} us, SALU "
+                     f"{vr.get('salu_floor_us')} us, bound {vr.get('issue_bound')} (frac "
+                     f"{vr.get('frac')})")
         agg, calls = counters(os.path.join(P, f"{tag}_pmc{psfx}"))
         summ.append(f"# {cfg}: per dispatch; us = rocprofv3 trace average of the bench command "
                     f"(3 concurrent streams + roofline pass)")
+        summ.append("# valu_us / salu_us: issue floors per dispatch, (ACTIVE_INST_VALU - "
+                    "ACTIVE_INST_VALU2) x 4 and INSTS_SALU x 4 cycles over 1024 SIMDs at 2.4 GHz")
         summ.append(f"{'kernel':28s}{'us':>9s}{'waves':>9s}{'valu/w':>8s}{'salu/w':>8s}"
-                    f"{'lds/w':>7s}{'wait%':>6s}{'valu_us':>9s}{'fetchMB':>9s}{'writeMB':>9s}")
+                    f"{'lds/w':>7s}{'wait%':>6s}{'valu_us':>9s}{'salu_us':>9s}{'fetchMB':>9s}"
+                    f"{'writeMB':>9s}")
         rows = []
         for kn, dd in durs.items():
             a = agg.get(kn, {})
@@ -102,15 +107,17 @@ def main(tag="r01"):
                 return a.get(c, 0.0) / n
             w = per("SQ_WAVES") or 1.0
             cyc = per("SQ_WAVE_CYCLES") or 1.0
+            qc = (per("SQ_ACTIVE_INST_VALU") - per("SQ_ACTIVE_INST_VALU2")
+                  if "SQ_ACTIVE_INST_VALU2" in a else per("SQ_INSTS_VALU"))
             rows.append((sum(dd) / len(dd) / 1e3, kn, per("SQ_WAVES"), per("SQ_INSTS_VALU") / w,
                          per("SQ_INSTS_SALU") / w, per("SQ_INSTS_LDS") / w,
-                         100 * per("SQ_WAIT_ANY") / cyc, per("SQ_INSTS_VALU") * VALU_US,
+                         100 * per("SQ_WAIT_ANY") / cyc, qc * QC_US, per("SQ_INSTS_SALU") * QC_US,
                          per("FETCH_SIZE") / 1024, per("WRITE_SIZE") / 1024))
         for r in sorted(rows, reverse=True):
             if r[1].startswith("__amd"):
                 continue
             summ.append(f"{r[1][:27]:28s}{r[0]:9.1f}{r[2]:9.0f}{r[3]:8.0f}{r[4]:8.0f}{r[5]:7.0f}"
-                        f"{r[6]:6.0f}{r[7]:9.1f}{r[8]:9.1f}{r[9]:9.1f}")
+                        f"{r[6]:6.0f}{r[7]:9.1f}{r[8]:9.1f}{r[9]:9.1f}{r[10]:9.1f}")
         summ.append("")
     open(os.path.join(P, f"{tag}_roofline_check.txt"), "w").write("\n".join(check) + "\n")
     open(os.path.join(P, f"{tag}_pmc_summary.txt"), "w").write("\n".join(summ))

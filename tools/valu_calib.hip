@@ -29,7 +29,7 @@ constexpr int kChains = 8;
 constexpr int kUnroll = 16;
 
 template <int OP>
-__device__ __forceinline__ void op(uint32_t& a, uint64_t& a2, uint32_t b, uint64_t b2, uint32_t c, uint64_t msk) {
+__device__ __forceinline__ void op(uint32_t& a, uint64_t& a2, uint32_t b, uint64_t b2, uint32_t c, uint64_t msk, uint64_t& sa, uint32_t& s32) {
   if constexpr (OP == 0) { asm volatile("v_add_u32 %0, %0, %1" : "+v"(a) : "v"(b)); }
   if constexpr (OP == 1) { asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a) : "v"(b)); }
   if constexpr (OP == 2) { asm volatile("v_pk_sub_u16 %0, %0, %1" : "+v"(a) : "v"(b)); }
@@ -56,6 +56,10 @@ __device__ __forceinline__ void op(uint32_t& a, uint64_t& a2, uint32_t b, uint64
   if constexpr (OP == 23) { asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a) : "v"(b)); }
   if constexpr (OP == 24) { asm volatile("v_dot4_u32_u8 %0, %1, %2, %0" : "+v"(a) : "v"(b), "v"(c)); }
   if constexpr (OP == 25) { asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(a) : "v"(b)); }
+  if constexpr (OP == 26) { asm volatile("s_and_b64 %0, %0, %1" : "+s"(sa) : "s"(msk) : "scc"); }
+  if constexpr (OP == 27) { asm volatile("s_add_u32 %0, %0, %1" : "+s"(s32) : "s"((uint32_t)msk) : "scc"); }
+  if constexpr (OP == 28) { uint64_t m; asm volatile("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b)); asm volatile("s_and_b64 %0, %0, %1\n s_or_b64 %0, %0, %1" : "+s"(sa) : "s"(m) : "scc"); }
+  if constexpr (OP == 29) { asm volatile("v_add_u32 %0, %0, %2\n s_and_b64 %1, %1, %3" : "+v"(a), "+s"(sa) : "v"(b), "s"(msk) : "scc"); }
 }
 
 template <int OP>
@@ -68,6 +72,13 @@ __global__ __launch_bounds__(256) void k_valu(uint32_t* __restrict__ sink, int i
 #pragma unroll
   for (int k = 0; k < kChains; k++) a2[k] = ((uint64_t)a[k] << 32) | a[k];
   const uint64_t b2 = ((uint64_t)magic << 32) | threadIdx.x;
+  uint64_t sa[kChains];
+  uint32_t s32[kChains];
+#pragma unroll
+  for (int k = 0; k < kChains; k++) {
+    sa[k] = __builtin_amdgcn_readfirstlane(blockIdx.x + k) * 0x100000001ull;
+    s32[k] = __builtin_amdgcn_readfirstlane(blockIdx.x * 3 + k);
+  }
   const uint32_t b = blockIdx.x | 0x10001u, c = 0x05040100u ^ threadIdx.x;
   const uint64_t msk = ((uint64_t)magic << 32) | blockIdx.x;  // wave-uniform lane mask
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -75,18 +86,18 @@ __global__ __launch_bounds__(256) void k_valu(uint32_t* __restrict__ sink, int i
 #pragma unroll
     for (int u = 0; u < kUnroll; u++) {
 #pragma unroll
-      for (int k = 0; k < kChains; k++) op<OP>(a[k], a2[k], b, b2, c, msk);
+      for (int k = 0; k < kChains; k++) op<OP>(a[k], a2[k], b, b2, c, msk, sa[k], s32[k]);
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   uint32_t x = 0;
 #pragma unroll
-  for (int k = 0; k < kChains; k++) x ^= a[k] ^ (uint32_t)a2[k];
+  for (int k = 0; k < kChains; k++) x ^= a[k] ^ (uint32_t)a2[k] ^ (uint32_t)sa[k] ^ s32[k];
   if (x == magic) sink[blockIdx.x * 256 + threadIdx.x] = x;  // magic is a runtime value
   if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 4 + threadIdx.x / 64] = t1 - t0;
 }
 
-static const char* kNames[] = {"v_add_u32", "v_pk_max_u16", "v_pk_sub_u16", "v_perm_b32", "v_bfe_u32", "v_add3_u32", "v_cmp_gt_u32_e64", "v_cndmask_b32", "v_max_u32", "v_and_or_b32", "v_sub_u32", "v_and_b32", "v_or_b32", "v_xor_b32", "v_lshlrev_b32", "v_mov_b32", "v_add_f32", "v_fma_f32", "v_pk_add_f32", "v_mad_u32_u24", "v_cmp_gt_u32_vcc", "v_min3_u32", "v_lshl_or_b32", "v_pk_add_u16", "v_dot4_u32_u8", "v_bcnt_u32_b32"};
+static const char* kNames[] = {"v_add_u32", "v_pk_max_u16", "v_pk_sub_u16", "v_perm_b32", "v_bfe_u32", "v_add3_u32", "v_cmp_gt_u32_e64", "v_cndmask_b32", "v_max_u32", "v_and_or_b32", "v_sub_u32", "v_and_b32", "v_or_b32", "v_xor_b32", "v_lshlrev_b32", "v_mov_b32", "v_add_f32", "v_fma_f32", "v_pk_add_f32", "v_mad_u32_u24", "v_cmp_gt_u32_vcc", "v_min3_u32", "v_lshl_or_b32", "v_pk_add_u16", "v_dot4_u32_u8", "v_bcnt_u32_b32", "s_and_b64", "s_add_u32", "v_cmp_e64+2salu", "v_add_u32+s_and_b64"};
 
 template <int OP>
 int run(uint32_t* sink, unsigned long long* cyc, int waves_per_simd, int iters, bool print) {
@@ -132,6 +143,7 @@ int main() {
   unsigned long long* cyc = nullptr;
   CK(hipMalloc(&sink, 256 * 8 * 256 * 4));
   CK(hipMalloc(&cyc, 256 * 8 * 4 * 8));
+  setvbuf(stdout, nullptr, _IOLBF, 0);  // a line per run reaches the file even if a run stalls
   printf("{\"runs\": [\n");
   if (sweep<0>(sink, cyc) ||
       sweep<1>(sink, cyc) ||
@@ -158,7 +170,8 @@ int main() {
       sweep<22>(sink, cyc) ||
       sweep<23>(sink, cyc) ||
       sweep<24>(sink, cyc) ||
-      sweep<25>(sink, cyc))
+      sweep<25>(sink, cyc) ||
+      sweep<26>(sink, cyc) || sweep<27>(sink, cyc) || sweep<28>(sink, cyc) || sweep<29>(sink, cyc))
     return 1;
   printf("  {}]}\n");
   CK(hipFree(sink));
