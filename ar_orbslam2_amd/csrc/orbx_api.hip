@@ -16,6 +16,8 @@ using namespace orbx;
 extern "C" int orbx_plan_level_dims(const orbx_plan* P, int level, int* w, int* h);
 extern "C" int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out,
                                         int64_t stride);
+extern "C" int orbx_plan_level_download_buf(orbx_plan* P, int img, int level, uint8_t* out,
+                                            int64_t stride, int blurred);
 
 // One ORBextractor: a batch-1 plan for the current image size plus pinned host staging.  A
 // call is one graph launch — pinned image -> HBM copy, the whole extraction, and one copy of
@@ -153,6 +155,16 @@ int orbx_extractor_pyramid(orbx_extractor* ex, int32_t level, uint8_t* out, int6
   if (!out) return ORBX_OK;
   if (stride < lw) return ORBX_EINVAL;
   return orbx_plan_level_download(ex->plan, 0, level, out, stride);
+}
+
+// Test hook (orbx.h): the GaussianBlur'd level of the last extraction (ORBextractor.cc:1024-1026).
+int orbx_debug_extractor_blur(orbx_extractor* ex, int32_t level, uint8_t* out, int64_t stride) {
+  if (!ex || !ex->plan || !ex->has_run || !out) return ORBX_EINVAL;
+  int lw = 0, lh = 0;
+  int rc = orbx_plan_level_dims(ex->plan, level, &lw, &lh);
+  if (rc != ORBX_OK) return rc;
+  if (stride < lw) return ORBX_EINVAL;
+  return orbx_plan_level_download_buf(ex->plan, 0, level, out, stride, 1);
 }
 
 // Frame::ComputeStereoMatches (ORB_SLAM2/src/Frame.cc:471-643) on the last extraction of a

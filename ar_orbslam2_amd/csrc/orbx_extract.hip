@@ -339,7 +339,9 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
 // loads, border tiles byte-wise through reflect101.  Row pass in packed u16 (a row sum is at
 // most 255 * 257 = 65535): a thread makes 4 adjacent sums from the byte pairs of three dwords
 // (v_perm) with v_pk_add_u16 / v_pk_mad_u16, stored as 4 u16; column pass in 32 bits, 4
-// adjacent outputs per thread (7 x ds_read_b64, one dword store).
+// adjacent outputs per thread (7 x ds_read_b64, one dword store).  (Both passes in exact f32 on
+// the dual-issue add / fma measured slower, 303 vs 292 us per 256 C2 frames: the f32 row buffer
+// doubles the LDS traffic of the column pass, which then bounds the kernel.)
 constexpr int kBlurTW = 64, kBlurTH = 64;
 struct BlurTile {
   int16_t level, tx, ty, interior;
@@ -1866,15 +1868,20 @@ int orbx_plan_level_dims(const orbx_plan* P, int level, int* w, int* h) {
   return ORBX_OK;
 }
 
-int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int64_t stride) {
+int orbx_plan_level_download_buf(orbx_plan* P, int img, int level, uint8_t* out, int64_t stride,
+                                 int blurred) {
   if (!P || !P->last_in || img < 0 || img >= P->last_n || level < 0 || level >= P->g.nlevels)
     return ORBX_EINVAL;
   const LevelGeom& G = P->g.lv[level];
-  const uint8_t* src = P->d_pyr + (int64_t)img * P->g.pyr_bytes + G.pyr_off;
+  const uint8_t* src = (blurred ? P->d_blur : P->d_pyr) + (int64_t)img * P->g.pyr_bytes + G.pyr_off;
   ORBX_HIP(hipMemcpy2DAsync(out, stride, src, G.pitch, G.w, G.h, hipMemcpyDeviceToHost,
                             P->stream));
   ORBX_HIP(hipStreamSynchronize(P->stream));
   return ORBX_OK;
+}
+
+int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int64_t stride) {
+  return orbx_plan_level_download_buf(P, img, level, out, stride, 0);
 }
 
 // Test hook: the device sincosf port over a range of float bit patterns (orbx.h).

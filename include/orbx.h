@@ -449,6 +449,10 @@ int orbx_debug_match_finish(int32_t kind, int32_t n1, int32_t n2, const int32_t*
  * for the n floats whose bit patterns are lo, lo+1, ...; s / c host arrays of n.  Used by
  * tests/test_math_gpu.py (every float in [0, 2*pi] against the host libm). */
 int orbx_debug_sincosf(uint32_t lo, int64_t n, float* s, float* c);
+/* The GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) image of pyramid level `level` of the last
+ * orbx_extract call (ORBextractor.cc:1024-1026, computeDescriptors' working image), w x h of
+ * orbx_extractor_pyramid, into out with row stride `stride`.  Used by tests/test_extract_gpu.py. */
+int orbx_debug_extractor_blur(orbx_extractor* ex, int32_t level, uint8_t* out, int64_t stride);
 
 #ifdef __cplusplus
 }

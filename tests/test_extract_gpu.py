@@ -118,3 +118,40 @@ def test_noise_octree_chunked_levels(w, h, nf):
     with 1024-thread (level-0 octree frame above 1 Mpx) and 256-thread workgroups."""
     rng = np.random.default_rng(w + h)
     _compare(rng.integers(0, 256, (h, w), dtype=np.uint8), nf)
+
+
+def _blurred_levels(ex):
+    import ctypes as C
+    from ar_orbslam2_amd._ffi import lib, check, ptr
+    out = []
+    for l, lv in enumerate(ex.mvImagePyramid):
+        a = np.zeros_like(lv)
+        check("orbx_debug_extractor_blur",
+              lib().orbx_debug_extractor_blur(ex._h, C.c_int32(l), ptr(a), C.c_int64(a.shape[1])))
+        out.append((lv, a))
+    return out
+
+
+@pytest.mark.parametrize("w,h,kind", [(640, 480, "synth"), (1241, 376, "synth"), (643, 361, "noise"),
+                                      (517, 389, "flat255"), (401, 301, "steps")])
+def test_blur_every_pixel_matches_oracle(w, h, kind):
+    """k_blur (GaussianBlur 7x7 sigma 2, reflect-101, OpenCV 2.4 fixed point: SURVEY A.4)
+    pixel for pixel on every pyramid level against the oracle, including widths that are not a
+    multiple of 4 (the half-up scalar tail), saturating images and noise (rounding ties)."""
+    rng = np.random.default_rng(w * h)
+    if kind == "synth":
+        img = synth.frame(w, h, 3, 1)
+    elif kind == "noise":
+        img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    elif kind == "flat255":
+        img = np.full((h, w), 255, np.uint8)
+        img[::7, ::5] = 254
+    else:
+        img = np.repeat(np.repeat(rng.integers(0, 256, (h // 8 + 1, w // 8 + 1), dtype=np.uint8),
+                                  8, 0), 8, 1)[:h, :w].copy()
+    ex = ORBextractor(1000)
+    ex(img)
+    for l, (lv, got) in enumerate(_blurred_levels(ex)):
+        ref = O.gaussian7(lv)
+        bad = np.argwhere(got != ref)
+        assert bad.size == 0, f"level {l} ({lv.shape}): {len(bad)} blurred px differ, first {bad[:5]}"
