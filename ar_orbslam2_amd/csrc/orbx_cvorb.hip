@@ -146,8 +146,16 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
   const uint64_t col_ok = __ballot(X0 + lane >= xlo && X0 + lane <= xhi);
   if (col_ok != 0) {
     const int vy_lo = max(0, ylo - (Y0 - 1)), vy_hi = min(kWinR, yhi - (Y0 - 1) + 1);
-    for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)
-      enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 5, t, col_ok), vy * kVS + 4 + lane);
+    // row pairs (vy, vy + 1) on the dual-issue pretest (orbx_internal.h fast_pretest2), pair
+    // index = wid mod 4; vy_lo is 0, so the last pair's second row is at most kWinR - 1
+    // the lane's flag bits of interest: its column inside the detection region
+    const uint32_t fm = (X0 + lane >= xlo && X0 + lane <= xhi) ? 0x80008000u : 0u;
+    for (int vy = vy_lo + 2 * wid; vy < vy_hi; vy += 8) {
+      const uint32_t f = fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 5, t) &
+                         (vy + 1 < vy_hi ? fm : fm & 0x8000u);
+      wave_enqueue(q, nq, kQ, (f & 0x8000u) != 0, vy * kVS + 4 + lane, lane);
+      wave_enqueue(q, nq, kQ, (int32_t)f < 0, (vy + 1) * kVS + 4 + lane, lane);
+    }
   }
   // ring columns X0-1 (vx 3) and X0+64 (vx 68)
   for (int k0 = wid * 64; k0 < 2 * kWinR; k0 += 256) {

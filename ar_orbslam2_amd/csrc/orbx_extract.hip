@@ -526,12 +526,13 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     const int vy_lo = max(0, ylo - (Y0 - 1)), vy_hi = min(kWinR, yhi - (Y0 - 1));
     if constexpr (PAIR) {
       // row pairs (vy, vy + 1), pair index = wid mod 4 (vy_lo is even, so vy + 1 <= 65)
+      // the lane's flag bits of interest: its column inside the detection region
+      const uint32_t fm = (X0 + lane >= xlo && X0 + lane < xhi) ? 0x80008000u : 0u;
       for (int vy = vy_lo + 2 * wid; vy < vy_hi; vy += 8) {
-        uint64_t m0, m1;
-        fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th, col_ok,
-                             vy + 1 < vy_hi ? col_ok : 0, &m0, &m1);
-        enqueue(m0, vy * kVS + 4 + lane);
-        enqueue(m1, (vy + 1) * kVS + 4 + lane);
+        const uint32_t f = fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th) &
+                           (vy + 1 < vy_hi ? fm : fm & 0x8000u);
+        wave_enqueue(q, nq, kQ, (f & 0x8000u) != 0, vy * kVS + 4 + lane, lane);
+        wave_enqueue(q, nq, kQ, (int32_t)f < 0, (vy + 1) * kVS + 4 + lane, lane);
       }
     } else {
       for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)  // rows = wid mod 4
@@ -566,12 +567,16 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     // position inside its FAST cell (detection rows/columns 19 + i*cell ..): at the cell edges
     // a neighbour belongs to another cell ROI and counts as 0; bit 0 = left / up allowed,
     // bit 1 = right / down allowed
+    // (only columns / rows of the detection region matter: x - kEdge >= 0 there; the
+    // remainder by the float reciprocal, as py_divmod, instead of two integer divisions)
     const int wc = max(G.wcell, 1), x = X0 + tid;
-    const int rx = ((x - kEdge) % wc + wc) % wc;
+    int qx, rx;
+    py_divmod(max(x - kEdge, 0), wc, 1.0f / (float)wc, qx, rx);
     s_cm[tid] = (rx != 0 ? 1 : 0) | (rx != wc - 1 && x + 1 < xhi ? 2 : 0);
   } else if (tid < 2 * kFastT) {
     const int hc = max(G.hcell, 1), y = Y0 + tid - kFastT;
-    const int ry = ((y - kEdge) % hc + hc) % hc;
+    int qy, ry;
+    py_divmod(max(y - kEdge, 0), hc, 1.0f / (float)hc, qy, ry);
     s_rm[tid - kFastT] = (ry != 0 ? 1 : 0) | (ry != hc - 1 && y + 1 < yhi ? 2 : 0);
   }
   __syncthreads();

@@ -189,9 +189,9 @@ template <int RS>
 __device__ __forceinline__ uint32_t fast_pair(const uint8_t* p) {
   return __builtin_amdgcn_perm((uint32_t)p[RS], (uint32_t)p[0], 0x0C040C00u);
 }
+// Returns the flag word: bit 15 = the row-r pixel may be a corner, bit 31 = the row-r+1 pixel.
 template <int RS>
-__device__ __forceinline__ void fast_pretest2(const uint8_t* c, int t, uint64_t ok0, uint64_t ok1,
-                                              uint64_t* m0, uint64_t* m1) {
+__device__ __forceinline__ uint32_t fast_pretest2(const uint8_t* c, int t) {
   const uint32_t C = fast_pair<RS>(c + 3 * RS + 3);
   const uint32_t rep = 0x10001u;
   const uint32_t L = C + (uint32_t)(0x8000 - t - 1) * rep;
@@ -212,15 +212,24 @@ __device__ __forceinline__ void fast_pretest2(const uint8_t* c, int t, uint64_t 
     pd[k] = D[k] & D[(k + 1) & 7];
     pb[k] = B[k] & B[(k + 1) & 7];
   }
-  const uint32_t any = ((pd[0] | pd[4]) & (pd[2] | pd[6])) | ((pd[1] | pd[5]) & (pd[3] | pd[7])) |
-                       ((pb[0] | pb[4]) & (pb[2] | pb[6])) | ((pb[1] | pb[5]) & (pb[3] | pb[7]));
-  *m0 = __ballot((any & 0x8000u) != 0) & ok0;
-  *m1 = __ballot((int32_t)any < 0) & ok1;
+  return ((pd[0] | pd[4]) & (pd[2] | pd[6])) | ((pd[1] | pd[5]) & (pd[3] | pd[7])) |
+         ((pb[0] | pb[4]) & (pb[2] | pb[6])) | ((pb[1] | pb[5]) & (pb[3] | pb[7]));
 }
 
 // rank of this lane among the set lanes of m
 __device__ __forceinline__ int lane_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// Wave-local candidate queue: lanes with `pred` append `idx` in lane order (mbcnt rank); every
+// lane stores — the others into the wave's 64 spare slots past `spare` (no exec juggling).
+// Taking the lane's own predicate (not the lane's bit of the ballot) saves the 64-bit shift,
+// and and compare per row.
+__device__ __forceinline__ void wave_enqueue(uint16_t* q, int& nq, int spare, bool pred, int idx,
+                                             int lane) {
+  const uint64_t m = __ballot(pred);
+  q[pred ? nq + lane_rank(m) : spare + lane] = (uint16_t)idx;
+  nq += __popcll(m);
 }
 
 // OpenCV 2.4 cornerScore<16> at (x, y) of a u8 image with row stride `stride`:

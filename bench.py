@@ -96,6 +96,11 @@ def _load_json(name):
         return None
 
 
+def _kname_is(name, kernel):
+    """rocprofv3 Kernel_Name 'void orbx::k_fast_tile<true>(...)' is kernel 'k_fast_tile'."""
+    return name.split("(")[0].split("<")[0].endswith("::" + kernel)
+
+
 def pmc_traffic(pmc_dir, kernel):
     """HBM-side bytes per launch of `kernel` from separate rocprofv3 --pmc passes
     (FETCH_SIZE, WRITE_SIZE, both in KB).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2->fabric
@@ -112,7 +117,7 @@ def pmc_traffic(pmc_dir, kernel):
         if not os.path.exists(path):
             return None, f"no PMC passes for this command ({rel})"
         vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                if r["Kernel_Name"].split("(")[0].endswith("::" + kernel) and r["Counter_Name"] == counter]
+                if _kname_is(r["Kernel_Name"], kernel) and r["Counter_Name"] == counter]
         if not vals:
             return None, f"kernel not in the PMC passes ({rel})"
         tot[counter] = sum(vals) / len(vals) * 1024
@@ -147,7 +152,7 @@ def pmc_issue(pmc_dir, kernel, avg_launch_us):
         return None
     per = {}
     for r in csv.DictReader(open(path)):
-        if r["Kernel_Name"].split("(")[0].endswith("::" + kernel):
+        if _kname_is(r["Kernel_Name"], kernel):
             per.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     if "SQ_INSTS_VALU" not in per:
         return None
