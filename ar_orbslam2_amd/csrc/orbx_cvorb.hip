@@ -665,11 +665,11 @@ __global__ __launch_bounds__(256) void k_cvdescribe(
   int m10 = 0, m01 = 0;
   if (active && hl < 31)  // row v = hl - 15 of the circular patch
     ic_row_moments(s_raw[hw] + hl * RW, (cx - 15) - 4 * fr, c_cv_icmask.m[hl], hl - 15, m10, m01);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    m10 += __shfl_xor(m10, o);
-    m01 += __shfl_xor(m01, o);
-  }
+  // sums within the half-wave: 16-lane rows on DPP, then the two rows of the half
+  m10 = row16_sum(m10);
+  m01 = row16_sum(m01);
+  m10 += __shfl_xor(m10, 16);
+  m01 += __shfl_xor(m01, 16);
   if (!active) return;
   const float angle = orbx_fast_atan2((float)m01, (float)m10);
   float ca, sb;

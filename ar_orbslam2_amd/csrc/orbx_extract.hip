@@ -846,16 +846,19 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
       for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
       const uint8_t* Sx = S + sh;  // pixel (r, c) of the ROI at Sx[r * RS + c]
       const bool half = cw <= 32;  // wave-uniform
-      const int col = half ? lane & 31 : lane, sub = half ? lane >> 5 : 0, step = half ? 2 : 1;
+      const int col = half ? lane & 31 : lane, sub = half ? 2 * (lane >> 5) : 0, step = half ? 4 : 2;
       // every candidate of the cell stays queued (row << 6 | column): scored in batches of 64,
-      // then the NMS runs at the queued pixels only (all others have V = 0)
+      // then the NMS runs at the queued pixels only (all others have V = 0).  The pretest runs on
+      // row pairs (r, r + 1) per lane (fast_pretest2, dual-issue ops); a pair past the last
+      // detection row reads staged rows past the ROI, inside this workgroup's LDS, and is masked.
+      const uint32_t fm = col < cw ? 0x80008000u : 0u;
       int nq = 0;
       for (int r0 = 0; r0 < dr; r0 += step) {
         const int r = r0 + sub;
-        const uint64_t ok = __ballot(col < cw && r < dr);
-        const uint64_t pass = fast_pretest<RS>(Sx + min(r, dr - 1) * RS + col, min_th, ok);
-        q[(pass >> lane) & 1 ? nq + lane_rank(pass) : QCAP + lane] = (uint16_t)(r * 64 + col);
-        nq += __popcll(pass);
+        const uint32_t f = fast_pretest2<RS>(Sx + r * RS + col, min_th) &
+                           fm & ((r < dr ? 0x8000u : 0u) | (r + 1 < dr ? 0x80000000u : 0u));
+        wave_enqueue(q, nq, QCAP, (f & 0x8000u) != 0, r * 64 + col, lane);
+        wave_enqueue(q, nq, QCAP, (int32_t)f < 0, (r + 1) * 64 + col, lane);
       }
       for (int j = lane; j < nq; j += 64) {
         const int e = q[j], r = e >> 6, c = e & 63;
@@ -1444,11 +1447,11 @@ __global__ __launch_bounds__(256) void k_describe(
   int m10 = 0, m01 = 0;
   if (active && hl < 31)
     ic_row_moments(s_raw[hw] + hl * RW, (cx - 15) - 4 * fr, c_icmask.m[hl], hl - 15, m10, m01);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {  // within the half-wave
-    m10 += __shfl_xor(m10, o);
-    m01 += __shfl_xor(m01, o);
-  }
+  // sums within the half-wave: 16-lane rows on DPP, then the two rows of the half
+  m10 = row16_sum(m10);
+  m01 = row16_sum(m01);
+  m10 += __shfl_xor(m10, 16);
+  m01 += __shfl_xor(m01, 16);
   if (!active) return;
   const float angle = orbx_fast_atan2((float)m01, (float)m10);
   // descriptor on the blurred level: byte hl from pairs 8 hl .. 8 hl + 7, LSB first

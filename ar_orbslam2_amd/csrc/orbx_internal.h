@@ -221,6 +221,33 @@ __device__ __forceinline__ int lane_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
+// Cross-lane reductions on DPP moves (no LDS crossbar round trip, unlike __shfl_xor's
+// ds_bpermute): quad, half-row and row pairings give every lane of a 16-lane row the row's
+// result.  All lanes of the row must be active.
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int row16_sum(int v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  return v + dpp<0x140>(v);  // row_mirror
+}
+__device__ __forceinline__ uint32_t row16_min(uint32_t v) {
+  v = min(v, (uint32_t)dpp<0xB1>((int)v));
+  v = min(v, (uint32_t)dpp<0x4E>((int)v));
+  v = min(v, (uint32_t)dpp<0x141>((int)v));
+  return min(v, (uint32_t)dpp<0x140>((int)v));
+}
+// minimum over the 64 lanes, wave-uniform (the four row minima through readlane)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = row16_min(v);
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16),
+                 c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return min(min(a, b), min(c, d));
+}
+
 // Wave-local candidate queue: lanes with `pred` append `idx` in lane order (mbcnt rank); every
 // lane stores — the others into the wave's 64 spare slots past `spare` (no exec juggling).
 // Taking the lane's own predicate (not the lane's bit of the ballot) saves the 64-bit shift,

@@ -148,18 +148,16 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
           b2 = dist;
         }
       }
-      // wave merge of (best1, position, best2): keeps the first position of the minimum and the
-      // second order statistic, exactly what the sequential loop yields
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int ob1 = __shfl_xor(b1, o), obp = __shfl_xor(bp, o), ob2 = __shfl_xor(b2, o);
-        if (ob1 < b1 || (ob1 == b1 && obp < bp)) {
-          b2 = min(ob2, b1);
-          b1 = ob1;
-          bp = obp;
-        } else {
-          b2 = min(b2, ob1);
-        }
+      // wave merge of (best1, position, best2), what the sequential loop yields: the minimum
+      // of the key (best1 << 16 | position) is best1 at its first position; best2 is then the
+      // minimum over the lanes of best1, except the winning lane, which offers its own best2
+      {
+        const uint32_t key = ((uint32_t)b1 << 16) | (uint32_t)min(bp, 0xFFFF);
+        const uint32_t K = wave_min_u32(key);
+        const int B2 = (int)wave_min_u32(key == K ? (uint32_t)b2 : (uint32_t)b1);
+        b1 = (int)(K >> 16);
+        bp = (int)(K & 0xFFFFu);
+        b2 = B2;
       }
       const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
       if (pass && static_cast<float>(b1) < P.nnratio * static_cast<float>(b2)) {

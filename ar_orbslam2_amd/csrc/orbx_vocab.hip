@@ -102,8 +102,12 @@ __global__ __launch_bounds__(256) void k_voc_transform(VocView V, int nid_level,
       meta = V.cmeta[cb + c];
       key = dist * 64 + c;  // strict `d < best_d` over children in order: lowest c on ties
     }
+    if constexpr (G == 16) {
+      key = (int)row16_min((uint32_t)key);  // keys are >= 0
+    } else {
 #pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) key = min(key, __shfl_xor(key, o));
+      for (int o = G / 2; o > 0; o >>= 1) key = min(key, __shfl_xor(key, o));
+    }
     const int src = gbase + (key & 63);
     const int mx = __shfl(meta.x, src), my = __shfl(meta.y, src), mz = __shfl(meta.z, src),
               mw = __shfl(meta.w, src);
