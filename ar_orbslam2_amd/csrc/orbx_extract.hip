@@ -1119,16 +1119,25 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         t1[i] = ne;
       }
       nToExpand = block_sum<NT>(nexp_local, s_tmp);
-      // final refinement: visit expandable nodes by (size desc, seq desc)
+      // final refinement: visit expandable nodes by (size desc, seq desc).  A node's rank is
+      // the number of expandable nodes with a larger (size, seq) key; the keys are packed once
+      // into pk (size << 32 | seq, 0 for nodes that do not expand) so the all-pairs count is one
+      // broadcast 64-bit load and compare per node pair
+      uint64_t* pk = X.pk;
+      for (int i = tid; i < size; i += NT)
+        pk[i] = cur.cnt[i] > 1 ? ((uint64_t)cur.cnt[i] << 32) | (uint32_t)cur.seq[i] : 0;
+      __syncthreads();
       int E_local = 0;
       for (int i = tid; i < size; i += NT) {
-        if (cur.cnt[i] > 1) {
-          const int ci = cur.cnt[i], si = cur.seq[i];
+        const uint64_t ki = pk[i];
+        if (ki != 0) {
           int r = 0;
-          for (int j = 0; j < size; j++) {
-            const int cj = cur.cnt[j];
-            r += cj > 1 && (cj > ci || (cj == ci && cur.seq[j] > si));
+          int j = 0;
+          for (; j + 4 <= size; j += 4) {
+            const uint64_t a = pk[j], b = pk[j + 1], c = pk[j + 2], d = pk[j + 3];
+            r += (a > ki) + (b > ki) + (c > ki) + (d > ki);
           }
+          for (; j < size; j++) r += pk[j] > ki;
           t3[r] = i;  // vis[r] = node
           t4[i] = r;  // rank
           E_local++;
@@ -1257,11 +1266,12 @@ __global__ __launch_bounds__(NT) void k_octree(
     const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
     const CellGeom* __restrict__ cells, const uint32_t* __restrict__ cand, int cand_total,
     uint32_t* __restrict__ lin, int* __restrict__ label, uint32_t* __restrict__ okey,
-    int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap) {
+    int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
+    int level_base) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_tmp[NT / 64 + 1];
   __shared__ int s_misc[8];
-  const int level = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const int level = level_base + blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
   const LevelGeom& G = lv[level];
   int* oc = ocount + img * nlevels + level;
   if (G.ncells == 0) {
@@ -1520,8 +1530,12 @@ struct orbx_plan {
   // counts, keypoints and descriptors share one allocation (d_counts is its base) so the
   // drop-in path brings a frame's results back with one copy
   size_t out_kps_off = 0, out_desc_off = 0, out_bytes = 0;
-  size_t oct_smem = 0;
-  int oct_nt = 0;  // k_octree threads per workgroup (kOctNT or kOctNTBig)
+  // k_octree: levels below oct_split (level area > kOctBigArea) run 1024-thread workgroups
+  // with LDS for oct_nc_big nodes / oct_cc_big cells, the rest 256-thread ones sized for
+  // theirs, so small levels no longer hold a whole CU each
+  int oct_split = 0;
+  size_t oct_smem = 0, oct_smem_big = 0;
+  int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;
   int cell_cap = 0;
   bool fast_pair = true;  // k_fast_tile pretest on row pairs (ORBX_FAST_PAIR=0: one row per lane)
   const uint8_t* last_in = nullptr;
@@ -1668,16 +1682,18 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                        P->d_cell_counts);
     pr.mark(P->stream, st_fb);
   }
-  if (P->oct_nt == kOctNTBig)
-    hipLaunchKernelGGL(k_octree<kOctNTBig>, dim3(L, n), dim3(kOctNTBig), P->oct_smem, P->stream,
-                       P->d_lv, P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total,
-                       P->d_lin, P->d_label, P->d_okey, P->d_ocount, g.kp_total, L,
-                       g.node_cap_max, P->cell_cap);
-  else
-    hipLaunchKernelGGL(k_octree<kOctNT>, dim3(L, n), dim3(kOctNT), P->oct_smem, P->stream,
-                       P->d_lv, P->d_cell_counts, ncells, P->d_cells, P->d_cand, g.cand_total,
-                       P->d_lin, P->d_label, P->d_okey, P->d_ocount, g.kp_total, L,
-                       g.node_cap_max, P->cell_cap);
+  // levels [0, oct_split) on 1024-thread workgroups with the large LDS carve, the others on
+  // 256-thread ones sized for themselves (several per CU)
+  if (P->oct_split > 0)
+    hipLaunchKernelGGL(k_octree<kOctNTBig>, dim3(P->oct_split, n), dim3(kOctNTBig),
+                       P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
+                       P->d_cand, g.cand_total, P->d_lin, P->d_label, P->d_okey, P->d_ocount,
+                       g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0);
+  if (P->oct_split < L)
+    hipLaunchKernelGGL(k_octree<kOctNT>, dim3(L - P->oct_split, n), dim3(kOctNT), P->oct_smem,
+                       P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, P->d_cand,
+                       g.cand_total, P->d_lin, P->d_label, P->d_okey, P->d_ocount, g.kp_total, L,
+                       P->oct_nc, P->oct_cc, P->oct_split);
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
@@ -1781,19 +1797,40 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       up(P->d_ftiles, ftiles.data(), sizeof(FastTile) * ftiles.size()))
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
-  const size_t NC = (size_t)g.node_cap_max;
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  P->oct_nt = (int64_t)g.lv[0].W * g.lv[0].H > kOctBigArea ? kOctNTBig : kOctNT;
-  P->oct_smem = 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
-                r16(4 * (P->cell_cap + 1)) + r16(8 * NC) + r16(4 * P->cell_cap);
-  if (P->oct_smem > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
-  // keys and labels live in registers (up to kOctRegKeys * oct_nt per level) or in global
-  // scratch
-  const void* oct_fn = P->oct_nt == kOctNTBig ? (const void*)k_octree<kOctNTBig>
-                                              : (const void*)k_octree<kOctNT>;
-  if (hipFuncSetAttribute(oct_fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)P->oct_smem) != hipSuccess)
-    return fail(ORBX_EDEVICE);
+  auto oct_bytes = [&](size_t NC, size_t CC) {
+    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
+           r16(4 * (CC + 1)) + r16(8 * NC) + r16(4 * CC);
+  };
+  while (P->oct_split < g.nlevels && (int64_t)g.lv[P->oct_split].W * g.lv[P->oct_split].H > kOctBigArea)
+    P->oct_split++;
+  for (int l = 0; l < g.nlevels; l++) {
+    int& nc = l < P->oct_split ? P->oct_nc_big : P->oct_nc;
+    int& cc = l < P->oct_split ? P->oct_cc_big : P->oct_cc;
+    nc = std::max(nc, g.lv[l].node_cap);
+    cc = std::max(cc, g.lv[l].ncells);
+  }
+  P->oct_smem = oct_bytes(P->oct_nc, P->oct_cc);
+  P->oct_smem_big = P->oct_split ? oct_bytes(P->oct_nc_big, P->oct_cc_big) : 0;
+  if (std::max(P->oct_smem, P->oct_smem_big) > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
+  // keys and labels live in registers (up to kOctRegKeys * threads per level) or in global
+  // scratch.  The dynamic-LDS attribute is per function and shared by every plan of the
+  // process: only ever raised.
+  static size_t attr_small = 0, attr_big = 0;  // guarded by the resource lock
+  if (P->oct_smem > attr_small) {
+    if (hipFuncSetAttribute((const void*)k_octree<kOctNT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)P->oct_smem) != hipSuccess)
+      return fail(ORBX_EDEVICE);
+    attr_small = P->oct_smem;
+  }
+  if (P->oct_smem_big > attr_big) {
+    if (hipFuncSetAttribute((const void*)k_octree<kOctNTBig>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)P->oct_smem_big) != hipSuccess)
+      return fail(ORBX_EDEVICE);
+    attr_big = P->oct_smem_big;
+  }
   *out = P;
   return ORBX_OK;
 }
