@@ -62,14 +62,16 @@ def main(tag="r02"):
     check, summ = [], []
     for cfg, (sfx, psfx) in CONFIGS.items():
         bench = os.path.join(P, f"{tag}_bench{sfx}.jsonl")
-        trace = os.path.join(P, "traces", f"kernel_trace{sfx}.csv")
+        trace = os.path.join(P, "traces", f"{tag}_kernel_trace{sfx}.csv")
+        if not os.path.exists(trace):  # round-1 layout
+            trace = os.path.join(P, "traces", f"kernel_trace{sfx}.csv")
         if not (os.path.exists(bench) and os.path.exists(trace)):
             continue
         line = json.loads(open(bench).read().strip().splitlines()[-1])
         rf = line["roofline"]
         durs = trace_durations(trace)
         k = rf["kernel"]
-        d = durs.get(k, [])
+        d = durs.get(k) or next((v for kk, v in durs.items() if kk.startswith(k + "<")), [])
         check.append(f"{cfg} ({line['config']['workload']}): {line['value']:.1f} frames/s")
         check.append(f"  kernel {k}: {len(d)} dispatches")
         if d:
