@@ -1390,9 +1390,7 @@ __global__ __launch_bounds__(256) void k_describe(
     const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const uint32_t* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
-  // dwords per staged row: the raw 31-px rows span 8 or 9 dwords, the blurred 37-px rows 10;
-  // 12 keeps every staged row 16-byte aligned for the LDS stores
-  constexpr int RW = 12, BW = 12;
+  constexpr int RW = 10, BW = 11;  // dwords per staged row (31+3 / 37+3 bytes, rounded up)
   constexpr int RN = 31 * RW, BN = 37 * BW;
   __shared__ uint32_t s_raw[8][RN];
   __shared__ uint32_t s_blr[8][BN];
@@ -1428,37 +1426,29 @@ __global__ __launch_bounds__(256) void k_describe(
   const uint8_t* L = pyr + (int64_t)img * pyr_bytes + pyr_off;
   const uint8_t* Bp = blur + (int64_t)img * pyr_bytes + pyr_off;
   const int fr = (cx - 15) >> 2, lr = (cx + 15) >> 2;  // raw dword columns
-  const int fb = (cx - 18) >> 2;  // blurred dword columns (fb .. fb + 9)
+  const int fb = (cx - 18) >> 2, lb = (cx + 18) >> 2;  // blurred dword columns
   if (active) {
-    // one patch row per lane: its base address once, then dword loads at immediate offsets
-    // (the raw row's dwords fr .. fr + 7 always lie in the patch, fr + 8 when (cx - 15) & 3 >= 2;
-    // the blurred row's fb .. fb + 9 always).  Lanes 0-30: raw rows; lanes 0-31 then 0-4:
-    // blurred rows 0-31 and 32-36.
-    if (hl < 31) {
-      const uint32_t* src = (const uint32_t*)(L + (uint32_t)((cy - 15 + hl) * pitch + 4 * fr));
-      uint32_t v[9];
+    uint32_t vr[(RN + 31) / 32], vb[(BN + 31) / 32];
 #pragma unroll
-      for (int c = 0; c < 8; c++) v[c] = src[c];
-      v[8] = fr + 8 <= lr ? src[8] : 0u;
-      uint4* d = (uint4*)&s_raw[hw][hl * RW];
-      d[0] = make_uint4(v[0], v[1], v[2], v[3]);
-      d[1] = make_uint4(v[4], v[5], v[6], v[7]);
-      s_raw[hw][hl * RW + 8] = v[8];
+    for (int k = 0; k < (RN + 31) / 32; k++) {
+      const int i = hl + 32 * k, r = i / RW, c = i - r * RW;
+      vr[k] = (i < RN && fr + c <= lr)
+                  ? *(const uint32_t*)(L + (uint32_t)((cy - 15 + r) * pitch + 4 * (fr + c)))
+                  : 0u;
     }
 #pragma unroll
-    for (int r0 = 0; r0 < 37; r0 += 32) {
-      const int r = r0 + hl;
-      if (r < 37) {
-        const uint32_t* src = (const uint32_t*)(Bp + (uint32_t)((cy - 18 + r) * pitch + 4 * fb));
-        uint32_t v[10];
-#pragma unroll
-        for (int c = 0; c < 10; c++) v[c] = src[c];
-        uint4* d = (uint4*)&s_blr[hw][r * BW];
-        d[0] = make_uint4(v[0], v[1], v[2], v[3]);
-        d[1] = make_uint4(v[4], v[5], v[6], v[7]);
-        *(uint2*)&s_blr[hw][r * BW + 8] = make_uint2(v[8], v[9]);
-      }
+    for (int k = 0; k < (BN + 31) / 32; k++) {
+      const int i = hl + 32 * k, r = i / BW, c = i - r * BW;
+      vb[k] = (i < BN && fb + c <= lb)
+                  ? *(const uint32_t*)(Bp + (uint32_t)((cy - 18 + r) * pitch + 4 * (fb + c)))
+                  : 0u;
     }
+#pragma unroll
+    for (int k = 0; k < (RN + 31) / 32; k++)
+      if (hl + 32 * k < RN) s_raw[hw][hl + 32 * k] = vr[k];
+#pragma unroll
+    for (int k = 0; k < (BN + 31) / 32; k++)
+      if (hl + 32 * k < BN) s_blr[hw][hl + 32 * k] = vb[k];
   }
   constexpr int BS = 4 * BW;
   const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - 4 * fb);
