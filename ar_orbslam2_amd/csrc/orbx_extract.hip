@@ -568,15 +568,16 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     // a neighbour belongs to another cell ROI and counts as 0; bit 0 = left / up allowed,
     // bit 1 = right / down allowed
     // (only columns / rows of the detection region matter: x - kEdge >= 0 there; the
-    // remainder by the float reciprocal, as py_divmod, instead of two integer divisions)
+    // remainder by the hardware reciprocal, as py_divmod — which corrects the quotient by one
+    // either way — instead of two integer divisions)
     const int wc = max(G.wcell, 1), x = X0 + tid;
     int qx, rx;
-    py_divmod(max(x - kEdge, 0), wc, 1.0f / (float)wc, qx, rx);
+    py_divmod(max(x - kEdge, 0), wc, __builtin_amdgcn_rcpf((float)wc), qx, rx);
     s_cm[tid] = (rx != 0 ? 1 : 0) | (rx != wc - 1 && x + 1 < xhi ? 2 : 0);
   } else if (tid < 2 * kFastT) {
     const int hc = max(G.hcell, 1), y = Y0 + tid - kFastT;
     int qy, ry;
-    py_divmod(max(y - kEdge, 0), hc, 1.0f / (float)hc, qy, ry);
+    py_divmod(max(y - kEdge, 0), hc, __builtin_amdgcn_rcpf((float)hc), qy, ry);
     s_rm[tid - kFastT] = (ry != 0 ? 1 : 0) | (ry != hc - 1 && y + 1 < yhi ? 2 : 0);
   }
   __syncthreads();

@@ -195,7 +195,8 @@ __device__ __forceinline__ uint32_t fast_pretest2(const uint8_t* c, int t) {
   const uint32_t C = fast_pair<RS>(c + 3 * RS + 3);
   const uint32_t rep = 0x10001u;
   const uint32_t L = C + (uint32_t)(0x8000 - t - 1) * rep;
-  const uint32_t Hh = C + (uint32_t)(t + 1) * rep;
+  // (E | H) - (C + t + 1) == E - (C + t + 1 - H) (E has no bits at 15 / 31), one dual-issue sub
+  const uint32_t K = C + (uint32_t)(t + 1) * rep - 0x80008000u;
   const uint32_t E[8] = {fast_pair<RS>(c + 6 * RS + 3), fast_pair<RS>(c + 5 * RS + 5),
                          fast_pair<RS>(c + 3 * RS + 6), fast_pair<RS>(c + RS + 5),
                          fast_pair<RS>(c + 3),          fast_pair<RS>(c + RS + 1),
@@ -204,7 +205,7 @@ __device__ __forceinline__ uint32_t fast_pretest2(const uint8_t* c, int t) {
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     D[k] = L - E[k];
-    B[k] = (E[k] | 0x80008000u) - Hh;
+    B[k] = E[k] - K;
   }
   uint32_t pd[8], pb[8];
 #pragma unroll
@@ -262,10 +263,18 @@ __device__ __forceinline__ void wave_enqueue(uint16_t* q, int& nq, int spare, bo
 // OpenCV 2.4 cornerScore<16> at (x, y) of a u8 image with row stride `stride`:
 // the pixel is a FAST-9/16 corner at threshold t iff the score is >= t.
 // With d_k = v - c_k an arc's min d is v - max c and its max d is v - min c, so the score is
-// max(v - min_k maxc_k, max_k minc_k - v) - 1 over the 16 arcs of 9 points: the arc minima run
-// on packed u16 pairs (c, 255 - c), one v_pk_min_u16 per point and window step giving min c and
-// 255 - max c together.
-typedef unsigned short fast_u16x2 __attribute__((ext_vector_type(2)));
+// max(v - min_k maxc_k, max_k minc_k - v) - 1 over the 16 arcs of 9 points.  The arc minima run
+// on packed pairs (c, 255 - c) giving min c and 255 - max c together, held as the f16 bit
+// patterns 0x6400 + c (the halves 1024 + c, exact and ordered like c) so that gfx950's
+// three-input v_pk_minimum3_f16 / v_pk_maximum3_f16 apply: runs of 3, then arcs of 3 runs, then
+// the maximum over the arcs, 40 packed operations (the u16 two-input form took 80).
+typedef _Float16 fast_f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fast_f16x2 fast_min3(fast_f16x2 a, fast_f16x2 b, fast_f16x2 c) {
+  return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ fast_f16x2 fast_max3(fast_f16x2 a, fast_f16x2 b, fast_f16x2 c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
 template <int CS = 1>  // bytes per column
 __device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, int y) {
   const uint8_t* c = s + y * stride + x * CS;
@@ -276,23 +285,21 @@ __device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, i
                       c[-3 * stride - CS],     c[-2 * stride - 2 * CS], c[-stride - 3 * CS],
                       c[-3 * CS],              c[stride - 3 * CS],      c[2 * stride - 2 * CS],
                       c[3 * stride - CS]};
-  fast_u16x2 p[16], m2[16], m4[16];
+  fast_f16x2 p[16], m3[16], a[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++)  // c | (255 - c) << 16 = 0xFF0000 - 65535 c: one v_mad_i32_i24
-    p[k] = __builtin_bit_cast(fast_u16x2, (uint32_t)(__mul24(px[k], -65535) + 0xFF0000));
+  for (int k = 0; k < 16; k++)  // (0x6400 + c) | (0x6400 + 255 - c) << 16: one v_mad_i32_i24
+    p[k] = __builtin_bit_cast(fast_f16x2, (uint32_t)(__mul24(px[k], -65535) + 0x64FF6400));
 #pragma unroll
-  for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(p[k], p[(k + 1) & 15]);
+  for (int k = 0; k < 16; k++) m3[k] = fast_min3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
 #pragma unroll
-  for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-  fast_u16x2 r = {0, 0};
+  for (int k = 0; k < 16; k++) a[k] = fast_min3(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
+  fast_f16x2 r = fast_max3(a[0], a[1], a[2]);
 #pragma unroll
-  for (int k = 0; k < 16; k++)
-    r = __builtin_elementwise_max(
-        r, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]),
-                                     p[(k + 8) & 15]));
+  for (int k = 3; k < 15; k += 2) r = fast_max3(r, a[k], a[k + 1]);
+  r = __builtin_elementwise_maximum(r, a[15]);
   const uint32_t R = __builtin_bit_cast(uint32_t, r);
-  // low half: max_k (min c over arc k); high half: 255 - min_k (max c over arc k)
-  return max(v + (int)(R >> 16) - 255, (int)(R & 0xFFFFu) - v) - 1;
+  // low half: 0x6400 + max_k (min c over arc k); high half: 0x6400 + 255 - min_k (max c over arc k)
+  return max(v + (int)(R >> 16) - (0x6400 + 255), (int)(R & 0xFFFFu) - 0x6400 - v) - 1;
 }
 
 // Stage timing with HIP events recorded on the launching stream between kernels.  Marks are
