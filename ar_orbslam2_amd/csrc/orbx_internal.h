@@ -172,6 +172,47 @@ __device__ __forceinline__ uint64_t fast_pretest(const uint8_t* c, int t, uint64
   return any & ok;
 }
 
+// The nine pairs of fast_pretest2 (centre, then the even circle points) from LDS: row r by
+// ds_read_u8, row r + 1 by ds_read_u8_d16_hi (the byte lands in bits 16..23; with SRAM ECC on,
+// as on MI355X, a d16 load zeroes the other half rather than keeping it, so the two are merged
+// by a full-rate v_or instead of loading into one register).  The compiler assembles such pairs
+// with a quarter-rate v_perm each.  c must point into LDS.
+template <int RS>
+__device__ __forceinline__ void fast_pairs9(const uint8_t* c, uint32_t P[9]) {
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)c;
+  uint32_t H[9];
+  asm volatile(
+      "ds_read_u8 %0, %18 offset:%19\n\t"
+      "ds_read_u8_d16_hi %9, %18 offset:%28\n\t"
+      "ds_read_u8 %1, %18 offset:%20\n\t"
+      "ds_read_u8_d16_hi %10, %18 offset:%29\n\t"
+      "ds_read_u8 %2, %18 offset:%21\n\t"
+      "ds_read_u8_d16_hi %11, %18 offset:%30\n\t"
+      "ds_read_u8 %3, %18 offset:%22\n\t"
+      "ds_read_u8_d16_hi %12, %18 offset:%31\n\t"
+      "ds_read_u8 %4, %18 offset:%23\n\t"
+      "ds_read_u8_d16_hi %13, %18 offset:%32\n\t"
+      "ds_read_u8 %5, %18 offset:%24\n\t"
+      "ds_read_u8_d16_hi %14, %18 offset:%33\n\t"
+      "ds_read_u8 %6, %18 offset:%25\n\t"
+      "ds_read_u8_d16_hi %15, %18 offset:%34\n\t"
+      "ds_read_u8 %7, %18 offset:%26\n\t"
+      "ds_read_u8_d16_hi %16, %18 offset:%35\n\t"
+      "ds_read_u8 %8, %18 offset:%27\n\t"
+      "ds_read_u8_d16_hi %17, %18 offset:%36\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(P[0]), "=&v"(P[1]), "=&v"(P[2]), "=&v"(P[3]), "=&v"(P[4]), "=&v"(P[5]),
+        "=&v"(P[6]), "=&v"(P[7]), "=&v"(P[8]), "=&v"(H[0]), "=&v"(H[1]), "=&v"(H[2]),
+        "=&v"(H[3]), "=&v"(H[4]), "=&v"(H[5]), "=&v"(H[6]), "=&v"(H[7]), "=&v"(H[8])
+      : "v"(a), "i"(3 * RS + 3), "i"(6 * RS + 3), "i"(5 * RS + 5), "i"(3 * RS + 6), "i"(RS + 5),
+        "i"(3), "i"(RS + 1), "i"(3 * RS), "i"(5 * RS + 1), "i"(4 * RS + 3), "i"(7 * RS + 3),
+        "i"(6 * RS + 5), "i"(4 * RS + 6), "i"(2 * RS + 5), "i"(RS + 3), "i"(2 * RS + 1),
+        "i"(4 * RS), "i"(6 * RS + 1)
+      : "memory");
+#pragma unroll
+  for (int k = 0; k < 9; k++) P[k] |= H[k];
+}
+
 // The same pretest for two pixels per lane — rows r and r+1 of one column — in the 16-bit
 // halves of each dword, on the VALU operations that issue at full rate on gfx950 (32-bit add /
 // sub / and / or: 2 cycles per wave instruction where compares, min/max, shifts and packed
@@ -181,26 +222,21 @@ __device__ __forceinline__ uint64_t fast_pretest(const uint8_t* c, int t, uint64
 //   brighter e > v + t  <=>  bit 15 of each half of  (E | H) - (C + t + 1)          is set
 // and the arc logic of fast_pretest runs on those flag words with and / or.  Returns the lane
 // masks of rows r (low halves) and r+1 (high halves).
-// c: the top-left byte of the row-r pixel's 7 x 7 neighbourhood in bytes with row stride RS;
-// a pair (row r, row r + 1) is built with one v_perm.  (A staged row-pair dword layout that
+// c: the top-left byte (in LDS) of the row-r pixel's 7 x 7 neighbourhood with row stride RS;
+// the pairs (row r, row r + 1) come from fast_pairs9.  (A staged row-pair dword layout that
 // makes each pair one ds_read_b32 measured slower: 515 vs 392 us per 256 C2 frames, from the
 // staging's extra VALU and the halved occupancy of its 23 KB window.)
-template <int RS>
-__device__ __forceinline__ uint32_t fast_pair(const uint8_t* p) {
-  return __builtin_amdgcn_perm((uint32_t)p[RS], (uint32_t)p[0], 0x0C040C00u);
-}
 // Returns the flag word: bit 15 = the row-r pixel may be a corner, bit 31 = the row-r+1 pixel.
 template <int RS>
 __device__ __forceinline__ uint32_t fast_pretest2(const uint8_t* c, int t) {
-  const uint32_t C = fast_pair<RS>(c + 3 * RS + 3);
+  uint32_t P[9];
+  fast_pairs9<RS>(c, P);
+  const uint32_t C = P[0];
   const uint32_t rep = 0x10001u;
   const uint32_t L = C + (uint32_t)(0x8000 - t - 1) * rep;
   // (E | H) - (C + t + 1) == E - (C + t + 1 - H) (E has no bits at 15 / 31), one dual-issue sub
   const uint32_t K = C + (uint32_t)(t + 1) * rep - 0x80008000u;
-  const uint32_t E[8] = {fast_pair<RS>(c + 6 * RS + 3), fast_pair<RS>(c + 5 * RS + 5),
-                         fast_pair<RS>(c + 3 * RS + 6), fast_pair<RS>(c + RS + 5),
-                         fast_pair<RS>(c + 3),          fast_pair<RS>(c + RS + 1),
-                         fast_pair<RS>(c + 3 * RS),     fast_pair<RS>(c + 5 * RS + 1)};
+  const uint32_t* E = P + 1;
   uint32_t D[8], B[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
