@@ -336,12 +336,13 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
 // half-even (SSE2 f32 region x < 4*floor(w/4)) or half-up (scalar tail).  Values below 256
 // are exact in f32, so half-even rounding of m/65536 is done on the integer m.
 // Tile 64 x 64 outputs: interior tiles stage the (64+6) x 72 input window with aligned dword
-// loads, border tiles byte-wise through reflect101.  Row pass in packed u16 (a row sum is at
-// most 255 * 257 = 65535): a thread makes 4 adjacent sums from the byte pairs of three dwords
-// (v_perm) with v_pk_add_u16 / v_pk_mad_u16, stored as 4 u16; column pass in 32 bits, 4
-// adjacent outputs per thread (7 x ds_read_b64, one dword store).  (Both passes in exact f32 on
-// the dual-issue add / fma measured slower, 303 vs 292 us per 256 C2 frames: the f32 row buffer
-// doubles the LDS traffic of the column pass, which then bounds the kernel.)
+// loads, border tiles byte-wise through reflect101.  The separable sum is exact in integers, so
+// the column pass runs first, in packed u16 (a column sum is at most 255 * 257 = 65535), a
+// thread unpacking one dword column once for 4 output rows; the row pass then takes the 32-bit
+// products with v_dot2_u32_u16 on the stored u16 pairs, 4 per output.  (Row pass first, with the
+// column pass in 24-bit multiplies on extracted halves, issued 56 instead of 16 VALU per 4
+// outputs: 292 us per 256 C2 frames.  Both passes in exact f32 on the dual-issue add / fma
+// measured 303 us: the f32 buffer doubles the LDS traffic of the second pass.)
 constexpr int kBlurTW = 64, kBlurTH = 64;
 struct BlurTile {
   int16_t level, tx, ty, interior;
@@ -358,9 +359,12 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
                                               const LevelGeom* __restrict__ lv,
                                               const BlurTile* __restrict__ tiles) {
   constexpr int kWords = (kBlurTW + 8) / 4;  // window columns X0-4 .. X0+67
+  // staged row: 16-B pieces of columns X0-16 .. X0+79 (window dword c at c + 3), 28 dwords apart
+  // (112 B: rows 4 apart in the column pass land 48 banks on, not 8)
+  constexpr int kChunks = (kBlurTW + 32) / 16, kSt = 28;
   constexpr int kRows = kBlurTH + 6;         // window rows Y0-3 .. Y0+66
-  __shared__ __align__(16) uint32_t s_in[kRows][kWords];
-  __shared__ __align__(16) uint16_t s_row[kRows][kBlurTW];
+  __shared__ __align__(16) uint32_t s_in[kRows][kSt];
+  __shared__ __align__(16) uint32_t s_col[kBlurTH][kWords * 2];  // column sums, u16 pairs
   int bx, img;
   xcd_block(bx, img);
   const BlurTile T = tiles[bx];
@@ -372,9 +376,11 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
   const int X0 = T.tx * kBlurTW, Y0 = T.ty * kBlurTH;
   const int tid = threadIdx.x;
   if (T.interior) {
-    for (int i = tid; i < kRows * kWords; i += 256) {
-      const int r = i / kWords, c = i - r * kWords;
-      s_in[r][c] = *(const uint32_t*)(src + (int64_t)(Y0 + r - 3) * pitch + X0 - 4 + 4 * c);
+    // interior: X0 >= 64 and the pitch (a multiple of 64 past X0 + 67) covers X0 + 79
+    for (int i = tid; i < kRows * kChunks; i += 256) {
+      const int r = i / kChunks, c = i - r * kChunks;
+      *(uint4*)&s_in[r][4 * c] =
+          *(const uint4*)(src + (uint32_t)((Y0 + r - 3) * pitch + X0 - 16 + 16 * c));
     }
   } else {
     // border tile: each window row reflected once (reflect-101), whole dwords where the 4
@@ -392,49 +398,71 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
 #pragma unroll
         for (int k = 0; k < 4; k++) v |= (uint32_t)row[reflect101(min(x + k, w + 8), w)] << (8 * k);
       }
-      s_in[r][c] = v;
+      s_in[r][c + 3] = v;
     }
   }
   __syncthreads();
-  constexpr uint32_t k0 = 18, k1 = 34, k2 = 49, k3 = 55;
-  const blur_u16x2 K0 = {k0, k0}, K1 = {k1, k1}, K2 = {k2, k2}, K3 = {k3, k3};
-  for (int i = tid; i < kRows * (kBlurTW / 4); i += 256) {
-    const int r = i >> 4, q = i & 15;
-    // window bytes b_0 .. b_11 = X0+4q-4 .. X0+4q+7 of row r; U(i) = (b_i, b_i+1) as u16 pair
-    const uint32_t w0 = s_in[r][q], w1 = s_in[r][q + 1], w2 = s_in[r][q + 2];
-    const blur_u16x2 U1 = byte_pair(w1, w0, 0x0c020c01u), U2 = byte_pair(w1, w0, 0x0c030c02u),
-                     U3 = byte_pair(w1, w0, 0x0c040c03u), U4 = byte_pair(w1, w0, 0x0c050c04u),
-                     U5 = byte_pair(w2, w1, 0x0c020c01u), U6 = byte_pair(w2, w1, 0x0c030c02u),
-                     U7 = byte_pair(w2, w1, 0x0c040c03u), U8 = byte_pair(w2, w1, 0x0c050c04u),
-                     U9 = byte_pair(w2, w1, 0x0c060c05u);
-    // outputs at window bytes 4,5 and 6,7 (taps [18,34,49,55,49,34,18])
-    const blur_u16x2 s01 = (U1 + U7) * K0 + (U2 + U6) * K1 + (U3 + U5) * K2 + U4 * K3;
-    const blur_u16x2 s23 = (U3 + U9) * K0 + (U4 + U8) * K1 + (U5 + U7) * K2 + U6 * K3;
-    *(uint2*)&s_row[r][4 * q] =
-        make_uint2(__builtin_bit_cast(uint32_t, s01), __builtin_bit_cast(uint32_t, s23));
+  constexpr unsigned short k0 = 18, k1 = 34, k2 = 49, k3 = 55;
+  // column pass (the sum is separable and exact, so columns first gives the same m): a thread
+  // takes one window dword column and 4 output rows; its 10 input dwords unpack once into byte
+  // pairs (b0, b1) and (b2, b3), each output row is 7 packed u16 ops per pair (a column sum is
+  // at most 255 * 257 = 65535)
+  {
+    const blur_u16x2 K0 = {k0, k0}, K1 = {k1, k1}, K2 = {k2, k2}, K3 = {k3, k3};
+    for (int i = tid; i < kWords * (kBlurTH / 4); i += 256) {
+      const int rb = i / kWords, c = i - rb * kWords, r0 = 4 * rb;
+      blur_u16x2 U[10], V[10];
+#pragma unroll
+      for (int k = 0; k < 10; k++) {
+        const uint32_t w = s_in[r0 + k][c + 3];
+        U[k] = byte_pair(w, w, 0x0c010c00u);
+        V[k] = byte_pair(w, w, 0x0c030c02u);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const blur_u16x2 su = (U[j] + U[j + 6]) * K0 + (U[j + 1] + U[j + 5]) * K1 +
+                              (U[j + 2] + U[j + 4]) * K2 + U[j + 3] * K3;
+        const blur_u16x2 sv = (V[j] + V[j + 6]) * K0 + (V[j + 1] + V[j + 5]) * K1 +
+                              (V[j + 2] + V[j + 4]) * K2 + V[j + 3] * K3;
+        *(uint2*)&s_col[r0 + j][2 * c] =
+            make_uint2(__builtin_bit_cast(uint32_t, su), __builtin_bit_cast(uint32_t, sv));
+      }
+    }
   }
   __syncthreads();
+  // row pass: 4 adjacent outputs per thread from the 6 column-sum pairs P_j = (c[4q + 2j],
+  // c[4q + 2j + 1]) around them (window column i = x - X0 + 4), 4 v_dot2_u32_u16 per output with
+  // the taps laid over the pairs (even outputs start mid-pair)
+  const blur_u16x2 W0k0 = {0, k0}, Wk1k2 = {k1, k2}, Wk3k2 = {k3, k2}, Wk1k0 = {k1, k0},
+                   Wk0k1 = {k0, k1}, Wk2k3 = {k2, k3}, Wk2k1 = {k2, k1}, Wk00 = {k0, 0};
   for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
     const int r = i >> 4, q = i & 15;
     const int x = X0 + 4 * q, y = Y0 + r;
     if (x >= w || y >= h) continue;
-    uint2 R[7];
-#pragma unroll
-    for (int k = 0; k < 7; k++) R[k] = *(const uint2*)&s_row[r + k][4 * q];
-    // row sums <= 65535: pair sums < 2^24, 24-bit multiplies are exact
-    auto col7 = [&](int sh, bool hi) {
-      auto g = [&](int k) { return hi ? (R[k].y >> sh) & 0xFFFFu : (R[k].x >> sh) & 0xFFFFu; };
-      return (uint32_t)(__umul24(g(0) + g(6), k0) + __umul24(g(1) + g(5), k1) +
-                        __umul24(g(2) + g(4), k2) + __umul24(g(3), k3));
-    };
-    const uint32_t m[4] = {col7(0, false), col7(16, false), col7(0, true), col7(16, true)};
+    const uint2 A = *(const uint2*)&s_col[r][2 * q], B = *(const uint2*)&s_col[r][2 * q + 2],
+                C = *(const uint2*)&s_col[r][2 * q + 4];
+    const blur_u16x2 P0 = __builtin_bit_cast(blur_u16x2, A.x), P1 = __builtin_bit_cast(blur_u16x2, A.y),
+                     P2 = __builtin_bit_cast(blur_u16x2, B.x), P3 = __builtin_bit_cast(blur_u16x2, B.y),
+                     P4 = __builtin_bit_cast(blur_u16x2, C.x), P5 = __builtin_bit_cast(blur_u16x2, C.y);
+    auto d2 = [](blur_u16x2 p, blur_u16x2 k, uint32_t acc) { return __builtin_amdgcn_udot2(p, k, acc, false); };
+    const uint32_t m[4] = {d2(P3, Wk1k0, d2(P2, Wk3k2, d2(P1, Wk1k2, d2(P0, W0k0, 0u)))),
+                           d2(P4, Wk00, d2(P3, Wk2k1, d2(P2, Wk2k3, d2(P1, Wk0k1, 0u)))),
+                           d2(P4, Wk1k0, d2(P3, Wk3k2, d2(P2, Wk1k2, d2(P1, W0k0, 0u)))),
+                           d2(P5, Wk00, d2(P4, Wk2k1, d2(P3, Wk2k3, d2(P2, Wk0k1, 0u))))};
     // m / 65536 rounded half-even in the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up in
-    // the scalar tail (m + 0x8000); x is a multiple of 4, as is bxs: one test per group
-    const uint32_t even = x < bxs ? 1u : 0u;
-    uint32_t out = 0;
+    // the scalar tail (m + 0x8000); x is a multiple of 4, as is bxs: one test per group.
+    // Quotients <= 257: two per dword by one v_perm of the high halves, clamped by v_pk_min_u16,
+    // then the four low bytes gathered by one more v_perm
+    // (bit field of width 1 in the SSE2 region, 0 in the tail: v_bfe + v_add3 per output)
+    const uint32_t tail = x < bxs ? 0u : 1u;
+    uint32_t rq[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-      out |= min(255u, (m[k] + 0x8000u - (~(m[k] >> 16) & even)) >> 16) << (8 * k);
+    for (int k = 0; k < 4; k++) rq[k] = m[k] + (0x7FFFu + tail) + __builtin_amdgcn_ubfe(m[k], 16, 1u - tail);
+    const blur_u16x2 lim = {255, 255};
+    const blur_u16x2 h01 = __builtin_elementwise_min(byte_pair(rq[1], rq[0], 0x07060302u), lim),
+                     h23 = __builtin_elementwise_min(byte_pair(rq[3], rq[2], 0x07060302u), lim);
+    const uint32_t out = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, h23),
+                                               __builtin_bit_cast(uint32_t, h01), 0x06040200u);
     *(uint32_t*)(dst + (uint32_t)(y * pitch + x)) = out;  // bytes past w land in the row pad
   }
 }
@@ -1577,6 +1605,7 @@ static std::vector<BlurTile> blur_tiles(const Geometry& g) {
     for (int ty = 0; ty * kBlurTH < G.h; ty++)
       for (int tx = 0; tx * kBlurTW < G.w; tx++) {
         const int X0 = tx * kBlurTW, Y0 = ty * kBlurTH;
+        // (X0 >= 64 then, and the 64-B pitch covers k_blur's 16-B pieces up to X0 + 79)
         const bool interior = X0 >= 4 && X0 + kBlurTW + 4 <= G.w && Y0 >= 3 &&
                               Y0 + kBlurTH + 3 <= G.h;
         tiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, (int16_t)interior});
