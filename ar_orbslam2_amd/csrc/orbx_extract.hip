@@ -335,8 +335,8 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
 // (SURVEY A.4): integer row pass with taps [18,34,49,55,49,34,18], column pass rounded
 // half-even (SSE2 f32 region x < 4*floor(w/4)) or half-up (scalar tail).  Values below 256
 // are exact in f32, so half-even rounding of m/65536 is done on the integer m.
-// Tile 64 x 64 outputs: interior tiles stage the (64+6) x 72 input window with aligned dword
-// loads, border tiles byte-wise through reflect101.  The separable sum is exact in integers, so
+// Tile 64 x 64 outputs: tiles stage the (64+6) x 72 input window as aligned 16-B pieces, border
+// tiles reflecting rows and, byte-wise, the pieces crossing the left / right edge (reflect101).  The separable sum is exact in integers, so
 // the column pass runs first, in packed u16 (a column sum is at most 255 * 257 = 65535), a
 // thread unpacking one dword column once for 4 output rows; the row pass then takes the 32-bit
 // products with v_dot2_u32_u16 on the stored u16 pairs, 4 per output.  (Row pass first, with the
@@ -383,22 +383,32 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
           *(const uint4*)(src + (uint32_t)((Y0 + r - 3) * pitch + X0 - 16 + 16 * c));
     }
   } else {
-    // border tile: each window row reflected once (reflect-101), whole dwords where the 4
-    // bytes are inside the level, byte-wise reflect only for dwords crossing the left/right
-    // edge; dwords wholly past the last column any output reads (w + 2) stay unset
-    for (int i = tid; i < kRows * kWords; i += 256) {
-      const int r = i / kWords, c = i - r * kWords;
+    // border tile: each window row reflected once (reflect-101), whole 16-B pieces where they
+    // lie inside the level, byte-wise reflect only for the window dwords (3 .. 20) of a piece
+    // crossing the left / right edge; dwords wholly past the last column any output reads
+    // (w + 2) stay unset
+    for (int i = tid; i < kRows * kChunks; i += 256) {
+      const int r = i / kChunks, c = i - r * kChunks;
       const int y = reflect101(min(Y0 + r - 3, h + 8), h);
       const uint8_t* row = src + (int64_t)y * pitch;
-      const int x = X0 - 4 + 4 * c;
-      uint32_t v = 0;
-      if (x >= 0 && x + 4 <= w) {
-        v = *(const uint32_t*)(row + x);
-      } else if (x < w + 3) {
+      const int x = X0 - 16 + 16 * c;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (x >= 0 && x + 16 <= w) {
+        v = *(const uint4*)(row + x);
+      } else {
+        uint32_t d[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int k = 0; k < 4; k++) v |= (uint32_t)row[reflect101(min(x + k, w + 8), w)] << (8 * k);
+        for (int j = 0; j < 4; j++) {
+          const int dw = 4 * c + j, xd = x + 4 * j;
+          if (dw >= 3 && dw <= 20 && xd < w + 3) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              d[j] |= (uint32_t)row[reflect101(min(xd + k, w + 8), w)] << (8 * k);
+          }
+        }
+        v = make_uint4(d[0], d[1], d[2], d[3]);
       }
-      s_in[r][c + 3] = v;
+      *(uint4*)&s_in[r][4 * c] = v;
     }
   }
   __syncthreads();
