@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
                                                    const FastTile* __restrict__ tiles,
                                                    int ini_th) {
   constexpr int kInR = kFastT + 8;        // staged rows Y0-4 .. Y0+67
-  constexpr int kInD = (kFastT + 16) / 4; // staged dwords: columns X0-8 .. X0+71
+  constexpr int kInD = (kFastT + 32) / 4; // staged dwords: columns X0-16 .. X0+79 (16-B pieces)
   constexpr int kWinR = kFastT + 2;       // V rows Y0-1 .. Y0+64
   constexpr int kWinG = (kFastT + 8) / 4; // V column groups: X0-4 .. X0+67
   constexpr int kVS = kWinG * 4;          // V row stride (bytes)
@@ -534,17 +534,15 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   const LevelGeom& G = lv[T.level];
   const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
   const int X0 = T.tx * kFastT, Y0 = T.ty * kFastT;
-  // staged window: rows Y0-4 .. Y0+67 clamped, 8-byte pieces of columns X0-8 .. X0+71 (zero
-  // left of the image; the 64-B pitch covers the right side)
-  auto piece = [&](int r, int c) -> uint2 {
+  // staged window: rows Y0-4 .. Y0+67 clamped, 16-byte pieces of columns X0-16 .. X0+79 (zero
+  // left of the image and past the pitch, a multiple of 64 past X0 + 63)
+  for (int i = tid; i < kInR * (kInD / 4); i += 256) {
+    const int r = i / (kInD / 4), c = i - r * (kInD / 4);
     const int y = min(max(Y0 + r - 4, 0), G.h - 1);
-    const int x = X0 - 8 + 8 * c;
-    return (x >= 0 && x < G.pitch) ? *(const uint2*)(src + (int64_t)y * G.pitch + x)
-                                   : make_uint2(0u, 0u);
-  };
-  for (int i = tid; i < kInR * (kInD / 2); i += 256) {
-    const int r = i / (kInD / 2), c = i - r * (kInD / 2);
-    *(uint2*)&s_in[r * kInD + 2 * c] = piece(r, c);
+    const int x = X0 - 16 + 16 * c;
+    *(uint4*)&s_in[r * kInD + 4 * c] =
+        (x >= 0 && x < G.pitch) ? *(const uint4*)(src + (uint32_t)(__mul24(y, G.pitch) + x))
+                                : make_uint4(0u, 0u, 0u, 0u);
   }
   for (int i = tid; i < kGroups; i += 256) s_v32[i] = 0;
   __syncthreads();
@@ -557,7 +555,7 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     q[(pass >> lane) & 1 ? nq + lane_rank(pass) : kQ + lane] = (uint16_t)idx;
     nq += __popcll(pass);
   };
-  // V window coordinates: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, column vx + 4
+  // V window coordinates: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, column vx + 12
   // holds the pixel.  Tile columns: lane = column, one wave-uniform row (pair) per pass.
   const uint64_t col_ok = __ballot(X0 + lane >= xlo && X0 + lane < xhi);
   if (col_ok != 0) {
@@ -567,14 +565,14 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
       // the lane's flag bits of interest: its column inside the detection region
       const uint32_t fm = (X0 + lane >= xlo && X0 + lane < xhi) ? 0x80008000u : 0u;
       for (int vy = vy_lo + 2 * wid; vy < vy_hi; vy += 8) {
-        const uint32_t f = fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th) &
+        const uint32_t f = fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 13, ini_th) &
                            (vy + 1 < vy_hi ? fm : fm & 0x8000u);
         wave_enqueue(q, nq, kQ, (f & 0x8000u) != 0, vy * kVS + 4 + lane, lane);
         wave_enqueue(q, nq, kQ, (int32_t)f < 0, (vy + 1) * kVS + 4 + lane, lane);
       }
     } else {
       for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)  // rows = wid mod 4
-        enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 5, ini_th, col_ok),
+        enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 13, ini_th, col_ok),
                 vy * kVS + 4 + lane);
     }
   }
@@ -585,7 +583,7 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     const int x = X0 - 4 + vx, y = Y0 - 1 + vy;
     const uint64_t ok = __ballot(k < 2 * kWinR && x >= xlo && x < xhi && y >= ylo && y < yhi);
     if (ok != 0)
-      enqueue(fast_pretest<kRowB, kCS>(sin8 + vy * kRowB + (vx + 1) * kCS, ini_th, ok), vy * kVS + vx);
+      enqueue(fast_pretest<kRowB, kCS>(sin8 + vy * kRowB + (vx + 9) * kCS, ini_th, ok), vy * kVS + vx);
   }
   uint8_t* s_v = (uint8_t*)s_v32;
   for (int j0 = 0; j0 < nq; j0 += 64) {
@@ -593,7 +591,7 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
     if (j < nq) {
       const int i = q[j];  // = vy * kVS + vx
       const int vy = i / kVS, vx = i - vy * kVS;
-      const int sc = fast_score<kCS>((const uint8_t*)s_in, kRowB, vx + 4, vy + 3);
+      const int sc = fast_score<kCS>((const uint8_t*)s_in, kRowB, vx + 12, vy + 3);
       s_v[i] = (uint8_t)min(255, max(0, sc + 1));
     }
   }
