@@ -93,7 +93,7 @@ __device__ __forceinline__ void xcd_block(int& bx, int& by) {
 // 8 neighbours, V(q) = score(q) if q is a corner at 20, else 0 (fast.cpp); then
 // runByImageBorder drops every keypoint outside [edge, w-edge) x [edge, h-edge) (edge >= 18,
 // so every neighbour of a kept pixel is a detection pixel).  A 64 x 64 tile stages rows
-// Y0-4..Y0+67 and columns X0-8..X0+71 (8-byte loads); the V window is the tile plus a 1-px
+// Y0-4..Y0+67 and columns X0-16..X0+79 (16-byte loads); the V window is the tile plus a 1-px
 // ring, restricted to [edge-1, w-edge] x [edge-1, h-edge].  The even-circle-point pretest runs
 // one pixel per lane with the compares as lane masks (fast_pretest), only its survivors are
 // queued (per wave, mbcnt ranks) and scored; the strict NMS is evaluated at the queued pixels
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
                                                 uint64_t* __restrict__ bitmaps, int64_t bm_words,
                                                 uint8_t* __restrict__ smap) {
   constexpr int kInR = kTH + 8;           // staged rows Y0-4 .. Y0+kTH+3
-  constexpr int kInD = (kTW + 16) / 4;    // staged dwords: columns X0-8 .. X0+71
+  constexpr int kInD = (kTW + 32) / 4;    // staged dwords: columns X0-16 .. X0+79
   constexpr int kRowB = kInD * 4;         // staged row stride (bytes)
   constexpr int kWinR = kTH + 2;          // V rows Y0-1 .. Y0+kTH
   constexpr int kVS = kTW + 8;            // V row stride: columns X0-4 .. X0+67
@@ -122,19 +122,19 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int X0 = T.tx * kTW, Y0 = L.ry0 + T.ty * kTH;
   const uint8_t* src = pyr + (int64_t)img * pyr_bytes + L.pyr_off;
-  for (int i = tid; i < kInR * (kInD / 2); i += 256) {
-    const int r = i / (kInD / 2), c = i - r * (kInD / 2);
+  for (int i = tid; i < kInR * (kInD / 4); i += 256) {
+    const int r = i / (kInD / 4), c = i - r * (kInD / 4);
     const int y = min(max(Y0 + r - 4, 0), L.h - 1);
-    const int x = X0 - 8 + 8 * c;
-    *(uint2*)&s_in[r][2 * c] = (x >= 0 && x < L.pitch)
-                                   ? *(const uint2*)(src + (int64_t)y * L.pitch + x)
-                                   : make_uint2(0u, 0u);
+    const int x = X0 - 16 + 16 * c;
+    *(uint4*)&s_in[r][4 * c] = (x >= 0 && x < L.pitch)
+                                   ? *(const uint4*)(src + (uint32_t)(__mul24(y, L.pitch) + x))
+                                   : make_uint4(0u, 0u, 0u, 0u);
   }
   for (int i = tid; i < kWinR * kVS / 4; i += 256) s_v32[i] = 0;
   if (tid < kTH) s_keep[tid] = 0;
   __syncthreads();
   const int t = kFastTh;
-  // V window: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, byte vx + 4
+  // V window: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, byte vx + 12
   const int xlo = L.rx0 - 1, xhi = L.rx1, ylo = L.ry0 - 1, yhi = L.ry1;  // inclusive
   uint16_t* q = s_q[wid];
   int nq = 0;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
     // the lane's flag bits of interest: its column inside the detection region
     const uint32_t fm = (X0 + lane >= xlo && X0 + lane <= xhi) ? 0x80008000u : 0u;
     for (int vy = vy_lo + 2 * wid; vy < vy_hi; vy += 8) {
-      const uint32_t f = fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 5, t) &
+      const uint32_t f = fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 13, t) &
                          (vy + 1 < vy_hi ? fm : fm & 0x8000u);
       wave_enqueue(q, nq, kQ, (f & 0x8000u) != 0, vy * kVS + 4 + lane, lane);
       wave_enqueue(q, nq, kQ, (int32_t)f < 0, (vy + 1) * kVS + 4 + lane, lane);
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
     const int vy = min(k >> 1, kWinR - 1), vx = k & 1 ? 4 + kTW : 3;
     const int x = X0 - 4 + vx, y = Y0 - 1 + vy;
     const uint64_t ok = __ballot(k < 2 * kWinR && x >= xlo && x <= xhi && y >= ylo && y <= yhi);
-    if (ok != 0) enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + vx + 1, t, ok), vy * kVS + vx);
+    if (ok != 0) enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + vx + 9, t, ok), vy * kVS + vx);
   }
   uint8_t* s_v = (uint8_t*)s_v32;
   for (int j0 = 0; j0 < nq; j0 += 64) {
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
     if (j < nq) {
       const int i = q[j];
       const int vy = i / kVS, vx = i - vy * kVS;
-      const int sc = fast_score(sin8, kRowB, vx + 4, vy + 3);
+      const int sc = fast_score(sin8, kRowB, vx + 12, vy + 3);
       s_v[i] = (uint8_t)(sc >= t ? sc : 0);
     }
   }

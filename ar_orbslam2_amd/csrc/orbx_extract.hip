@@ -3,12 +3,13 @@
 //
 // One plan = one image size + one parameter set + a maximum batch.  A batch of images runs
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
-//   k_pyramid     level 0 copy + every level (cv::resize INTER_LINEAR), 2 launches, row bands
-//   k_blur        x 1            all levels, 64x16 LDS tiles         (GaussianBlur 7x7 s=2)
-//   k_fast_tile   x 1            64x64 tiles, all levels            (FAST score + cell-local NMS)
-//   k_fast_compact x 1           one wave per FAST cell             (fallback + ordered compaction)
-//   k_octree      x 1            one workgroup per (image, level)    (DistributeOctTree)
-//   k_describe    x 1            one wave per keypoint               (IC_Angle + rBRIEF)
+//   k_pyramid       2 launches   row bands               (level 0 copy + cv::resize INTER_LINEAR)
+//   k_blur          x 1          64x64 tiles, all levels (GaussianBlur 7x7 s=2)
+//   k_fast_tile     x 1          64x64 tiles, all levels (FAST score + cell-local NMS at iniThFAST)
+//   k_fast_compact  x 1          4 FAST cells per wave   (ordered compaction, fallback queue)
+//   k_fast_fallback x 1-2        queued cells            (the minThFAST retry)
+//   k_octree        x 2          (image, level)          (DistributeOctTree; big levels apart)
+//   k_describe      x 1          half-wave per keypoint  (IC_Angle + rBRIEF)
 // Level 0 is read in place from the caller's input buffer; levels >= 1 live in the pyramid
 // block.  Everything is integer or bit-exact float (see orbx_math.h); compiled with
 // -ffp-contract=off.
