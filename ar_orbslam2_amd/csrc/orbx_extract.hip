@@ -10,8 +10,8 @@
 //   k_fast_fallback x 1-2        queued cells            (the minThFAST retry)
 //   k_octree        x 2          (image, level)          (DistributeOctTree; big levels apart)
 //   k_describe      x 1          half-wave per keypoint  (IC_Angle + rBRIEF)
-// Level 0 is read in place from the caller's input buffer; levels >= 1 live in the pyramid
-// block.  Everything is integer or bit-exact float (see orbx_math.h); compiled with
+// The first k_pyramid launch copies level 0 from the caller's input into the pitched pyramid
+// block, where every level lives.  Everything is integer or bit-exact float (see orbx_math.h); compiled with
 // -ffp-contract=off.
 #include <hip/hip_runtime.h>
 
