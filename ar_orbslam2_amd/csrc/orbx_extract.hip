@@ -166,8 +166,9 @@ __device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
 // the rows the next level needs (Geometry::bands), so no band waits for another; a band keeps
 // its rows of the level just built in LDS (even levels in buffer A, odd ones at buf_b) and
 // reads the next level's sources there, so each level costs one barrier and the pyramid block
-// is only written, by the band that owns the row.  Work items are (row, 4-pixel column group)
-// pairs dealt round-robin over the kPyNT threads.
+// is only written, by the band that owns the row.  Work items are (strip of kPyStrip rows,
+// 4-pixel column group) pairs dealt round-robin over the kPyNT threads; along its strip an
+// item reuses the horizontal sums of the source row two consecutive output rows share.
 // i = r * n + c for 0 <= i < 2^20, 1 <= n: (i + 0.5) / n is >= 0.5 / n from an integer, so
 // the float quotient truncates to r; the two fix-ups are insurance.
 __device__ __forceinline__ void py_divmod(int i, int n, float inv_n, int& r, int& c) {
@@ -177,62 +178,48 @@ __device__ __forceinline__ void py_divmod(int i, int n, float inv_n, int& r, int
   if (c >= n) r++, c -= n;
 }
 
-// One resize work item: output row r (band-relative) and 4-pixel group at dx0, with its taps.
-struct PyItem {
-  int r, dx0;
-  int2 yt;
-  int4 t01, t23;
-};
-
-__device__ __forceinline__ PyItem py_load(int i, int ng, float inv_ng, const int2* __restrict__ xt,
-                                          const int2* __restrict__ yt, int dlo) {
-  PyItem it;
-  int g;
-  py_divmod(i, ng, inv_ng, it.r, g);
-  it.dx0 = 4 * g;
-  it.yt = yt[dlo + it.r];
-  it.t01 = *(const int4*)(xt + it.dx0);  // coef_x % 4 == 0 and runs padded: aligned, in range
-  it.t23 = *(const int4*)(xt + it.dx0 + 2);
-  return it;
-}
-
 __device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {  // a, b < 2^24
   return (uint32_t)(((uint64_t)(a & 0xFFFFFF) * (uint64_t)(b & 0xFFFFFF)) >> 32);
 }
 
-// Four output pixels of cv::resize INTER_LINEAR 8UC1.  Coefficients are in
-// [0, 2049] (checked in resize_tables), so every OpenCV saturation on the way is a no-op:
-// H = S0*a0 + S1*a1 < 2^19, H >> 4 < 32767, the mulhi sum <= 1020, results in [0, 255].
-// The taps carry a << 4, so g = H << 4 and (H >> 4) << 8 = g & ~0xFF: the SSE2 16-bit
-// _mm_mulhi_epi16(H >> 4, b) = ((H >> 4) * b) >> 16 = mulhi_u24((H >> 4) << 8, b << 8).
-__device__ __forceinline__ uint32_t py_resize4(const PyItem& it, const uint8_t* sb, int slo,
-                                               int spitch, int sh1, int vxs) {
-  const uint32_t b0 = it.yt.y & 0xFFFF, b1 = (uint32_t)it.yt.y >> 16;
-  const int ra = __mul24(min(max(it.yt.x, 0), sh1) - slo, spitch);
-  const int rb = __mul24(min(max(it.yt.x + 1, 0), sh1) - slo, spitch);
-  const int xs[4] = {it.t01.x, it.t01.z, it.t23.x, it.t23.z};
-  const uint32_t as[4] = {(uint32_t)it.t01.y, (uint32_t)it.t01.w, (uint32_t)it.t23.y,
-                          (uint32_t)it.t23.w};
-  uint32_t g0[4], g1[4];
+typedef unsigned short py_u16x2 __attribute__((ext_vector_type(2)));
+
+// Horizontal pass of cv::resize INTER_LINEAR 8UC1 for the 4 output pixels of one
+// column group on one source row: g = S0 * (a0 << 4) + S1 * (a1 << 4) (the taps carry << 4,
+// packed as u16 pairs), the source pair (S0, S1) one unaligned ds_read_u16 spread into u16
+// halves, the two products one v_dot2_u32_u16.  Coefficients are in [0, 2049] (checked in
+// resize_tables), so every OpenCV saturation on the way is a no-op: H = g >> 4 < 2^19.
+__device__ __forceinline__ void py_horiz(const uint8_t* row, const int (&xs)[4],
+                                         const uint32_t (&as)[4], uint32_t (&g)[4]) {
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t a0 = as[k] & 0xFFFF, a1 = as[k] >> 16;
-    g0[k] = __umul24(sb[ra + xs[k]], a0) + __umul24(sb[ra + xs[k] + 1], a1);
-    g1[k] = __umul24(sb[rb + xs[k]], a0) + __umul24(sb[rb + xs[k] + 1], a1);
+    const uint32_t p = __builtin_amdgcn_perm((uint32_t)row[xs[k] + 1], (uint32_t)row[xs[k]],
+                                             0x0c040c00u);  // (S0, S1)
+    g[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(py_u16x2, p),
+                                  __builtin_bit_cast(py_u16x2, as[k]), 0u, false);
   }
+}
+
+// Vertical pass for the 4 pixels from the horizontal sums of their two source rows.  SSE2
+// region: _mm_mulhi_epi16(H >> 4, b) = ((H >> 4) * b) >> 16 = mulhi_u24((H >> 4) << 8, b << 8)
+// with (H >> 4) << 8 = g & ~0xFF, the mulhi sum <= 1020, result (m + 2) >> 2; past vxs the
+// scalar (H0*b0 + H1*b1 + 2^21) >> 22.  Results are in [0, 255].
+__device__ __forceinline__ uint32_t py_vert(const uint32_t (&g0)[4], const uint32_t (&g1)[4],
+                                           uint32_t yb, int dx0, int vxs) {
+  const uint32_t b0 = yb & 0xFFFF, b1 = yb >> 16;
   uint32_t out = 0;
-  if (it.dx0 + 3 < vxs) {  // VResizeLinearVec_32s8u: the whole group in the SSE2 region
+  if (dx0 + 3 < vxs) {  // VResizeLinearVec_32s8u: the whole group in the SSE2 region
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t m = mulhi_u24(g0[k] & 0x7FFF00, b0 << 8) + mulhi_u24(g1[k] & 0x7FFF00, b1 << 8);
       out |= ((m + 2) >> 2) << (8 * k);
     }
-  } else {  // the row end: SSE2 up to vxs, then the scalar (H0*b0 + H1*b1 + 2^21) >> 22
+  } else {  // the row end: SSE2 up to vxs, then the scalar form
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t m = mulhi_u24(g0[k] & 0x7FFF00, b0 << 8) + mulhi_u24(g1[k] & 0x7FFF00, b1 << 8);
       const uint32_t vsc = (__umul24(g0[k] >> 4, b0) + __umul24(g1[k] >> 4, b1) + (1u << 21)) >> 22;
-      out |= (it.dx0 + k < vxs ? (m + 2) >> 2 : vsc) << (8 * k);
+      out |= (dx0 + k < vxs ? (m + 2) >> 2 : vsc) << (8 * k);
     }
   }
   return out;
@@ -306,26 +293,42 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
     uint8_t* db = s_pyr + (l & 1 ? buf_b : 0);
     uint8_t* dp = base + D.pyr_off;
     const int slo = B.lo[l - 1], dlo = B.lo[l], ng = (D.w + 3) >> 2;
-    const int items = max(0, B.hi[l] - dlo) * ng;
+    const int nr = max(0, B.hi[l] - dlo), nstrip = (nr + kPyStrip - 1) / kPyStrip;
+    const int items = nstrip * ng;
     const float inv_ng = 1.0f / (float)ng;
     const bool keep = l < l1;  // the stage's last level is not read back
     const int dpitch = D.pitch, spitch = S.pitch, sh1 = S.h - 1, vxs = D.vxs;
     const int own_lo = B.own_lo[l], own_hi = B.own_hi[l];
     const int2* xt = xtap + D.coef_x;
-    const int2* yt = ytap + D.coef_y;
-    for (int i = tid; i < items; i += 2 * kPyNT) {  // two items per thread in flight
-      const PyItem A = py_load(i, ng, inv_ng, xt, yt, dlo);
-      const PyItem C = py_load(min(i + kPyNT, items - 1), ng, inv_ng, xt, yt, dlo);
-      const uint32_t oa = py_resize4(A, sb, slo, spitch, sh1, vxs);
-      const uint32_t oc = py_resize4(C, sb, slo, spitch, sh1, vxs);
-      // pitch >= w + 4: bytes past w of the last group land in the row's pad
-      if (keep) *(uint32_t*)(db + __mul24(A.r, dpitch) + A.dx0) = oa;
-      if (dlo + A.r >= own_lo && dlo + A.r < own_hi)
-        *(uint32_t*)(dp + (uint32_t)__mul24(dlo + A.r, dpitch) + A.dx0) = oa;
-      if (i + kPyNT < items) {
-        if (keep) *(uint32_t*)(db + __mul24(C.r, dpitch) + C.dx0) = oc;
-        if (dlo + C.r >= own_lo && dlo + C.r < own_hi)
-          *(uint32_t*)(dp + (uint32_t)__mul24(dlo + C.r, dpitch) + C.dx0) = oc;
+    const int2* yt = ytap + D.coef_y + dlo;
+    // work item = (strip of kPyStrip output rows, 4-pixel column group): the taps are loaded
+    // once per item, and a source row's horizontal sums carry over to the next output row
+    // that reads it (scale 1.2: 1.2 horizontal passes per output row instead of 2)
+    for (int i = tid; i < items; i += kPyNT) {
+      int st, gi;
+      py_divmod(i, ng, inv_ng, st, gi);
+      const int dx0 = 4 * gi;
+      const int4 t01 = *(const int4*)(xt + dx0);  // coef_x % 4 == 0, runs padded: aligned, in range
+      const int4 t23 = *(const int4*)(xt + dx0 + 2);
+      const int xs[4] = {t01.x, t01.z, t23.x, t23.z};
+      const uint32_t as[4] = {(uint32_t)t01.y, (uint32_t)t01.w, (uint32_t)t23.y, (uint32_t)t23.w};
+      const int r0 = st * kPyStrip, r1 = min(nr, r0 + kPyStrip);
+      int prev = -1;
+      uint32_t gp[4] = {0u, 0u, 0u, 0u};
+      for (int r = r0; r < r1; r++) {
+        const int2 ty = yt[r];
+        const int ya = min(max(ty.x, 0), sh1), yb = min(max(ty.x + 1, 0), sh1);
+        if (ya != prev) py_horiz(sb + __mul24(ya - slo, spitch), xs, as, gp);
+        uint32_t g1[4];
+        py_horiz(sb + __mul24(yb - slo, spitch), xs, as, g1);
+        const uint32_t o = py_vert(gp, g1, (uint32_t)ty.y, dx0, vxs);
+        // pitch >= w + 4: bytes past w of the last group land in the row's pad
+        if (keep) *(uint32_t*)(db + __mul24(r, dpitch) + dx0) = o;
+        if (dlo + r >= own_lo && dlo + r < own_hi)
+          *(uint32_t*)(dp + (uint32_t)__mul24(dlo + r, dpitch) + dx0) = o;
+#pragma unroll
+        for (int k = 0; k < 4; k++) gp[k] = g1[k];
+        prev = yb;
       }
     }
   }

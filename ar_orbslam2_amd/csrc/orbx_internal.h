@@ -44,6 +44,10 @@ constexpr int kPyNT = ORBX_PY_NT;        // k_pyramid threads per workgroup
 constexpr int kPyStage0 = ORBX_PY_STAGE0;  // levels built by the first stage (from the input)
 constexpr int kPyStageN = ORBX_PY_STAGEN;  // levels per later stage (from the pyramid)
 constexpr int kPyMaxSmem = 64 * 1024;    // k_pyramid dynamic LDS bound (both buffers)
+#ifndef ORBX_PY_STRIP
+#define ORBX_PY_STRIP 4
+#endif
+constexpr int kPyStrip = ORBX_PY_STRIP;  // k_pyramid output rows per work item
 struct PyrBand {
   int lo[kMaxLevels], hi[kMaxLevels];      // rows of each level this band computes (with halo)
   int own_lo[kMaxLevels], own_hi[kMaxLevels];  // rows it writes to the pyramid (a partition)
