@@ -853,36 +853,66 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
       gw = ((const CellWords*)cells)[cil];
     }
     const int nit = min(64, (nfb - kb + nw - 1) / nw);
-    for (int it = 0; it < nit; it++) {
-      const int ci = __builtin_amdgcn_readlane(cil, it);
+    auto geom = [&](int it) {
       CellWords cwd;
 #pragma unroll
       for (int w = 0; w < kCellWords; w++) cwd.w[w] = __builtin_amdgcn_readlane(gw.w[w], it);
-      const CellGeom C = __builtin_bit_cast(CellGeom, cwd);
+      return __builtin_bit_cast(CellGeom, cwd);
+    };
+    // the ROI as aligned dwords (its first pixel lands at byte sh of each staged row; the 64-B
+    // pitch covers the last dword): lane item i = row * words + word.  When the largest ROI is
+    // at most kPf dwords per lane, the next cell's loads are issued before this cell is
+    // processed (their latency hides behind it) and land in LDS when it is done; an item past
+    // the ROI repeats the last one (same value, same place).
+    constexpr int kPf = (MAXR * (RS / 4) + 63) / 64;
+    constexpr bool kPrefetch = kPf <= 8;
+    uint32_t pv[kPrefetch ? kPf : 1], po[kPrefetch ? kPf : 1];
+    auto issue = [&](const CellGeom& C) {
+      const uint8_t* src = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - (C.y0 + 3) * C.pitch - (C.x0 + 3));
+      const int cols = C.x1 - C.x0, rows = C.y1 - C.y0;
+      const int a0 = C.x0 & ~3, words = ((C.x0 & 3) + cols + 3) >> 2;
+      const uint8_t* srow = src + (int64_t)C.y0 * C.pitch + a0;
+      const int items = rows * words;
+      const float inv = 1.0f / (float)words;
+#pragma unroll
+      for (int u = 0; u < (kPrefetch ? kPf : 1); u++) {
+        int rr, cc;
+        py_divmod(min(lane + 64 * u, items - 1), words, inv, rr, cc);
+        pv[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr, C.pitch) + 4 * cc);
+        po[u] = rr * RS + 4 * cc;
+      }
+    };
+    if (kPrefetch && nit > 0) issue(geom(0));
+    for (int it = 0; it < nit; it++) {
+      const int ci = __builtin_amdgcn_readlane(cil, it);
+      const CellGeom C = geom(it);
       // the ROI origin (x0, y0) sits 3 rows and 3 columns before the first detection pixel
       const uint8_t* src = pyr + (int64_t)img * pyr_bytes +  // the level's pixel (0, 0)
                            (C.v_row0 - (C.y0 + 3) * C.pitch - (C.x0 + 3));
       const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3 (fb_big)
       const int dr = rows - 6, cw = cols - 6;            // > 0 (k_fast_compact)
-      // stage the ROI as aligned dwords (its first pixel lands at byte sh of each staged row;
-      // the 64-B pitch covers the last dword), four loads in flight per lane; zero the V map
-      // (rows dr + 2, columns cw + 2 with the ring)
       const int a0 = C.x0 & ~3, sh = C.x0 & 3, words = (sh + cols + 3) >> 2;  // <= RS / 4
-      const uint8_t* srow = src + (int64_t)C.y0 * C.pitch + a0;
-      const int items = rows * words;
-      const float inv = 1.0f / (float)words;
-      for (int i0 = lane; i0 < items; i0 += 256) {
-        uint32_t v[4];
-        int rr[4], cc[4];
+      if constexpr (kPrefetch) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          py_divmod(min(i0 + 64 * u, items - 1), words, inv, rr[u], cc[u]);
-          v[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr[u], C.pitch) + 4 * cc[u]);
+        for (int u = 0; u < kPf; u++) *(uint32_t*)(S + po[u]) = pv[u];
+        if (it + 1 < nit) issue(geom(it + 1));
+      } else {  // four loads in flight per lane
+        const uint8_t* srow = src + (int64_t)C.y0 * C.pitch + a0;
+        const int items = rows * words;
+        const float inv = 1.0f / (float)words;
+        for (int i0 = lane; i0 < items; i0 += 256) {
+          uint32_t v[4];
+          int rr[4], cc[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            py_divmod(min(i0 + 64 * u, items - 1), words, inv, rr[u], cc[u]);
+            v[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr[u], C.pitch) + 4 * cc[u]);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; u++) asm volatile("" : "+v"(v[u]));
+#pragma unroll
+          for (int u = 0; u < 4; u++) *(uint32_t*)(S + rr[u] * RS + 4 * cc[u]) = v[u];
         }
-#pragma unroll
-        for (int u = 0; u < 4; u++) asm volatile("" : "+v"(v[u]));
-#pragma unroll
-        for (int u = 0; u < 4; u++) *(uint32_t*)(S + rr[u] * RS + 4 * cc[u]) = v[u];
       }
       for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
       const uint8_t* Sx = S + sh;  // pixel (r, c) of the ROI at Sx[r * RS + c]
