@@ -685,7 +685,10 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
   if (lane == 0) *cnt_out = nout;
 }
 
-constexpr int kCompactCap = 30 * 30;  // survivors of a cell <= slot_cap (cells < 60 x 60)
+// survivors of a cell staged in LDS for the coalesced round 3; a cell with more (at most
+// slot_cap: cells < 60 x 60) writes its keys from the row lanes directly.  A small stage keeps
+// the workgroup's LDS at 8 KB: occupancy, not issue, bounds this latency-chained kernel.
+constexpr int kCompactCap = 256;
 constexpr int kCompactK = 4;          // cells per wave: each round of loads covers all of them
 // k_fast_fallback queue counters, [2 img + fb_big] kFbStride ints apart: one 128-B line each (the
 // queues fill with one atomic per wave; on a shared line those atomics serialize)
@@ -754,11 +757,21 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
       const int nn = __shfl_up(incl, o);
       if (lane >= o) incl += nn;
     }
-    nout[j] = __shfl(incl, 63);  // <= slot_cap <= kCompactCap
-    uint16_t* rc = s_rc[wid][j];
-    for (int pos = incl - cnt; b; b &= b - 1)
-      rc[pos++] = (uint16_t)((lane << 8) | __builtin_ctzll(b));
-    if (lane == 0) *cnt_out = nout[j];
+    const int n = __shfl(incl, 63);  // <= slot_cap
+    if (lane == 0) *cnt_out = n;
+    if (n <= kCompactCap) {
+      nout[j] = n;
+      uint16_t* rc = s_rc[wid][j];
+      for (int pos = incl - cnt; b; b &= b - 1)
+        rc[pos++] = (uint16_t)((lane << 8) | __builtin_ctzll(b));
+    } else {  // rare: the row lanes write their keys themselves
+      const uint8_t* V = vmap + (int64_t)img * pyr_bytes + C[j].v_row0 + lane * C[j].pitch;
+      uint32_t* out = cand + (int64_t)img * cand_total + C[j].slot_off;
+      for (int pos = incl - cnt; b; b &= b - 1) {
+        const int k = __builtin_ctzll(b);
+        out[pos++] = cand_key(C[j].x0 + 3 + k, C[j].y0 + 3 + lane, (int)V[k]);
+      }
+    }
   }
   // the empty cells join queue fb_big of the image (lists of ncells entries): one atomic per
   // queue and wave
@@ -779,8 +792,8 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
         base++;
       }
   }
-  // round 3 (per 64 survivors of each cell): lane s takes survivor s of every cell, all V
-  // loads in flight, then the coalesced key stores
+  // round 3 (per 64 survivors of each LDS-staged cell): lane s takes survivor s of every cell,
+  // all V loads in flight, then the coalesced key stores
   int nmax = 0;
 #pragma unroll
   for (int j = 0; j < kCompactK; j++) nmax = max(nmax, nout[j]);

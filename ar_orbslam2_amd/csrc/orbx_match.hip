@@ -270,6 +270,13 @@ __device__ __forceinline__ bool epipolar_ok(float x1, float y1, float x2, float 
   return (double)dsqr < 3.84 * (double)sigma2;
 }
 
+// One wave per KF1 node.  The reference scans the KF2 node's features in order for each KF1
+// feature, keeping the last one at the running minimum distance that passes the checks
+// (ORBmatcher.cc:716-769): that is the candidate of largest node position among those at the
+// minimum passing distance, since a later equal distance replaces and a larger one never does.
+// So the scan of one KF1 feature splits over several lanes: with n1 KF1 features in the chunk,
+// G = 64 / n1 lanes per feature each scan every G-th staged KF2 feature, keeping the minimum of
+// (dist << 32 | ~position), and the G partial minima meet in an LDS atomic minimum.
 __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict__ probs) {
   const TriProblem& P = probs[blockIdx.y];
   const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -280,31 +287,34 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
   const int b = wave_lower_bound(P.s2.fv.node_ids, nn2, id, lane);
   if (b >= nn2 || P.s2.fv.node_ids[b] != id) return;
   const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
-  // KF2 node features are staged 64 at a time in this wave's LDS (descriptor, keypoint,
-  // stereo/map-point flags); every lane then scans them in node order for its KF1 feature
+  const int wv = threadIdx.x >> 6;
+  // KF2 features are staged 64 at a time in this wave's LDS (descriptor, keypoint,
+  // stereo/map-point flags); the KF1 features' best keys meet in LDS
   __shared__ uint64_t s_d[4][64][4];
   __shared__ float s_x[4][64], s_y[4][64];
   __shared__ int s_i2[4][64], s_oct[4][64];
-  const int wv = threadIdx.x >> 6;
+  __shared__ unsigned long long s_key[4][64];
   for (int pa0 = P.s1.fv.node_offsets[a]; pa0 < P.s1.fv.node_offsets[a + 1]; pa0 += 64) {
-    const int pa = pa0 + lane;
-    bool live = pa < P.s1.fv.node_offsets[a + 1];
-    int i1 = 0;
+    const int n1 = min(64, P.s1.fv.node_offsets[a + 1] - pa0);
+    const int G = 64 / n1;                        // lanes per KF1 feature (wave-uniform)
+    const int u = lane % n1, g = lane / n1;       // this lane: feature u, every G-th candidate from g
+    bool live = g < G;
+    int i1 = P.s1.fv.node_feats[pa0 + u];
     bool st1 = false;
-    orbx_keypoint kp1{};
-    uint64_t d1[4] = {0, 0, 0, 0};
     if (live) {
-      i1 = P.s1.fv.node_feats[pa];
       if (P.s1.has_mp && P.s1.has_mp[i1]) live = false;
       st1 = P.s1.u_right ? P.s1.u_right[i1] >= 0 : false;
       if (P.only_stereo && !st1) live = false;
     }
+    orbx_keypoint kp1{};
+    uint64_t d1[4] = {0, 0, 0, 0};
     if (live) {
       kp1 = P.s1.keys_un[i1];
       const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
       d1[0] = q[0]; d1[1] = q[1]; d1[2] = q[2]; d1[3] = q[3];
     }
-    int bestDist = kTH_LOW, bestIdx2 = -1;
+    s_key[wv][lane] = ~0ull;
+    unsigned long long best = ~0ull;
     for (int pb0 = f0; pb0 < f1; pb0 += 64) {
       const int nb = min(64, f1 - pb0);
       {  // stage chunk: entry skipped (i2 = -1) when it has a map point or fails only_stereo
@@ -327,16 +337,19 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
             s_oct[wv][lane] = kp2.octave | (st2 ? 0x10000 : 0);
           }
         }
-        if (lane < 64) s_i2[wv][lane] = i2;
+        s_i2[wv][lane] = i2;
       }
+      __builtin_amdgcn_wave_barrier();  // the chunk's LDS writes precede every lane's reads
       if (live) {
-        for (int j = 0; j < nb; j++) {
-          const int i2 = s_i2[wv][j];
-          if (i2 < 0) continue;
+        for (int j = g; j < nb; j += G) {
+          if (s_i2[wv][j] < 0) continue;
           const uint64_t* dd = s_d[wv][j];
           const int dist = __popcll(d1[0] ^ dd[0]) + __popcll(d1[1] ^ dd[1]) +
                            __popcll(d1[2] ^ dd[2]) + __popcll(d1[3] ^ dd[3]);
-          if (dist > kTH_LOW || dist > bestDist) continue;
+          if (dist > kTH_LOW) continue;
+          const unsigned long long key =
+              ((unsigned long long)dist << 32) | (uint32_t)~(pb0 - f0 + j);
+          if (key > best) continue;  // (dist > bestDist in the reference; equal: later wins)
           const int oc2 = s_oct[wv][j];
           const bool st2 = oc2 >> 16;
           const int oct2 = oc2 & 0xFFFF;
@@ -345,14 +358,18 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
             const float dex = P.ex - x2, dey = P.ey - y2;
             if (__builtin_fmaf(dex, dex, dey * dey) < 100 * P.s2.scale_factors[oct2]) continue;
           }
-          if (epipolar_ok(kp1.x, kp1.y, x2, y2, P.F, P.s2.level_sigma2[oct2])) {
-            bestIdx2 = i2;
-            bestDist = dist;
-          }
+          if (epipolar_ok(kp1.x, kp1.y, x2, y2, P.F, P.s2.level_sigma2[oct2])) best = key;
         }
       }
+      __builtin_amdgcn_wave_barrier();  // every lane's reads precede the next chunk's writes
     }
-    if (pa < P.s1.fv.node_offsets[a + 1] && live) P.m12[i1] = bestIdx2;
+    if (live) atomicMin(&s_key[wv][u], best);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < n1 && live) {
+      const unsigned long long key = s_key[wv][lane];
+      P.m12[i1] = key == ~0ull ? -1 : P.s2.fv.node_feats[f0 + (int)~(uint32_t)key];
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

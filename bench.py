@@ -361,35 +361,73 @@ def cpu_baseline(cfg, seconds, mp_seconds, warmup=20, min_frames=200, max_second
                 single_thread=single, **info)
 
 
-def cpu_baseline_marker(cfg, seconds, target_desc):
-    """The CPU oracle of the marker path (cvorb_oracle.cc), 1 thread: cv::ORB of the frame,
-    BruteForceMatcher match against the target, Marker::Match's good filter, per frame."""
-    from oracle import oracle as O
-    from ar_orbslam2_amd import synth
-    w, h = cfg["w"], cfg["h"]
-    base = synth.canvas(w, h, 0)
-    imgs = [synth.frame(w, h, i, 0, base) for i in range(32)]
-    p = O.cvorb_params(cfg["nfeatures"])
-    for i in range(5):
-        O.good_matches(O.bf_match(target_desc, O.cvorb_detect(imgs[i], p)[1]))
+class MarkerUnit:
+    """One marker-path frame of the CPU oracle (cvorb_oracle.cc): cv::ORB of the frame,
+    BruteForceMatcher match against the target's descriptors, Marker::Match's good filter.
+    The target is the one run_marker builds (synth.frame(w, h, 5, 0)); its oracle descriptors
+    are the GPU's (tests/test_cvorb_gpu.py)."""
+
+    def __init__(self, cfg, n_images=32, stream=0):
+        from oracle import oracle as O
+        from ar_orbslam2_amd import synth
+        self.O = O
+        w, h = cfg["w"], cfg["h"]
+        self.p = O.cvorb_params(cfg["nfeatures"])
+        self.target_desc = O.cvorb_detect(synth.frame(w, h, 5, 0), self.p)[1]
+        base = synth.canvas(w, h, stream)
+        self.imgs = [synth.frame(w, h, i, stream, base) for i in range(n_images)]
+        self.n = 0
+
+    def step(self):
+        O = self.O
+        desc = O.cvorb_detect(self.imgs[self.n % len(self.imgs)], self.p)[1]
+        O.good_matches(O.bf_match(self.target_desc, desc))
+        self.n += 1
+
+
+def cpu_baseline_marker(cfg, seconds, mp_seconds, warmup=5, min_frames=100, max_seconds=40.0):
+    """The marker path's CPU baseline, before any GPU work of this process, as cpu_baseline:
+    one thread timed frame by frame (median / mean ms), and `value` = every available core, one
+    forked process per core on its own camera stream."""
+    import multiprocessing as mp
+    info = host_info()
+    unit = MarkerUnit(cfg)
+    for _ in range(warmup):
+        unit.step()
     times = []
     t0 = time.perf_counter()
     while True:
         a = time.perf_counter()
-        kps, desc = O.cvorb_detect(imgs[len(times) % len(imgs)], p)
-        O.good_matches(O.bf_match(target_desc, desc))
+        unit.step()
         times.append(time.perf_counter() - a)
         el = time.perf_counter() - t0
-        if el >= seconds and len(times) >= 4:
+        if (len(times) >= min_frames and el >= seconds) or el >= max_seconds:
             break
     ms = np.array(times) * 1e3
-    return dict(value=len(times) / el, unit="frames/s", cores=1, kind="port",
-                sample=f"{len(times)} consecutive {w}x{h} synthetic frames after 5 warm-up, CPU "
-                       f"oracle (oracle/cvorb_oracle.cc, g++ -O3 -march=x86-64-v3 "
-                       f"-ffp-contract=off), 1 thread, cv::ORB + BruteForceMatcher vs "
-                       f"{len(target_desc)} target descriptors + good filter per frame, {el:.1f} s",
-                median_ms=round(float(np.median(ms)), 3), mean_ms=round(float(ms.mean()), 3),
-                **host_info())
+    single = {"frames_per_s": round(len(times) / el, 3), "median_ms": round(float(np.median(ms)), 3),
+              "mean_ms": round(float(ms.mean()), 3), "timed_frames": len(times),
+              "warmup_frames": warmup}
+    P = info["cores_available"] or 1
+    ctx = mp.get_context("fork")  # no GPU work has happened in this process yet
+    start, q = ctx.Event(), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=(MarkerUnit(cfg, 8, stream=1 + i), mp_seconds, start, q))
+             for i in range(P)]
+    for p in procs:
+        p.start()
+    time.sleep(0.5)
+    start.set()
+    res = [q.get(timeout=mp_seconds * 4 + 120) for _ in procs]
+    for p in procs:
+        p.join()
+    agg = sum(n for n, _ in res) / max(e for _, e in res)
+    w, h = cfg["w"], cfg["h"]
+    return dict(value=round(agg, 3), unit="frames/s", cores=P, kind="port",
+                sample=f"{w}x{h} synthetic frames, CPU oracle (oracle/cvorb_oracle.cc, g++ -O3 "
+                       f"-march=x86-64-v3 -ffp-contract=off): {P} forked processes x 1 thread, one "
+                       f"camera stream each, {mp_seconds:.0f} s after 3 warm-up frames "
+                       f"({sum(n for n, _ in res)} frames); cv::ORB + BruteForceMatcher vs "
+                       f"{len(unit.target_desc)} target descriptors + good filter per frame",
+                single_thread=single, **info)
 
 
 def marker_bytes(levels, n_kp, n_img, n_target):
@@ -888,15 +926,14 @@ def main(argv=None):
     # the CPU baseline runs first, before this process touches the GPU (its all-cores leg
     # forks one process per core) and without the GPU leg's host threads competing
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg.get("marker"):
-        cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_mp_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = (cpu_baseline_marker if cfg.get("marker") else cpu_baseline)(
+            cfg, args.cpu_seconds, args.cpu_mp_seconds)
     import torch
     torch.cuda.set_device(local)
     dist = init_dist(rank, world, local, "nccl")
     if cfg.get("marker"):
-        out, target_desc = run_marker(args, cfg, rank, world, local, streams, dist)
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline_marker(cfg, args.cpu_seconds, target_desc)
+        out, _ = run_marker(args, cfg, rank, world, local, streams, dist)
     else:
         out = run_frames(args, cfg, rank, world, local, streams, dist)
     if cpu is not None:
