@@ -74,7 +74,9 @@ def algorithmic_bytes(levels, n_kp, n_img):
         # two launches (levels 1-3 from the input, 4-7 from level 3): average launch
         "k_pyramid": (2 * P[0] * n_img + sum(per_resize)) / 2,
         "k_blur": 2 * sum(P) * n_img,
-        "k_fast_tile": sum(P) * n_img,                          # every level pixel read once
+        # every level pixel read once, its keep bit written (the 64-bit row words k_fast_compact
+        # reads back); the survivors' scores (~1 % of the pixels) are not counted
+        "k_fast_tile": sum(P) * n_img * 9 / 8,
         "k_fast_compact": sum(P) * n_img / 8,                   # 1 NMS bit per pixel
         "k_describe": 60 * n_kp,
         "k_voc_transform": 52 * n_kp,                          # desc in; word, rank, node, weight out
@@ -84,9 +86,9 @@ def algorithmic_bytes(levels, n_kp, n_img):
 
 
 # bytes per lane of the global loads of the kernels bench.py can name as roofline kernel (the
-# staged windows of k_fast_tile and k_cvfast: uint2 per lane); their stores are 8-B bitmap words
-# and 1-B survivor scores
-LOAD_WIDTH = {"k_fast_tile": 8, "k_cvfast": 8}
+# staged windows of k_fast_tile and k_cvfast: 16-B pieces per lane); their stores are 8-B bitmap
+# words and 1-B survivor scores
+LOAD_WIDTH = {"k_fast_tile": 16, "k_cvfast": 16}
 
 
 def _load_json(name):

@@ -28,12 +28,17 @@ def main():
                                     ("write_size.csv", "WRITE_SIZE", "write", "calib_write")):
         for r in csv.DictReader(open(os.path.join(D, fn))):
             name = r["Kernel_Name"]
-            if r["Counter_Name"] != counter or kern + "<" not in name:
+            if r["Counter_Name"] != counter:
                 continue
-            t = name.split("<", 1)[1].split(">", 1)[0]
+            if kern + "16(" in name:  # the uint4 kernels
+                width = 16
+            elif kern + "<" in name:
+                width = WIDTH[name.split("<", 1)[1].split(">", 1)[0]]
+            else:
+                continue
             # counter bytes (KB x 1024) per true byte for this access width per lane
             f = round(float(r["Counter_Value"]) * 1024 / KNOWN, 4)
-            out[kind][f"{WIDTH[t]}B_per_lane"] = f or None  # 0: no usable reading
+            out[kind][f"{width}B_per_lane"] = f or None  # 0: no usable reading
     out["note"] = ("round 1 read FETCH_SIZE 0 for the 1-B loads: the kernel compared its byte "
                    "XOR against a literal above 255, so the compiler deleted the load loop; the "
                    "comparison value is now a kernel argument (tools/pmc_calib.hip)")

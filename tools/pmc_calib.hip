@@ -34,6 +34,22 @@ __global__ __launch_bounds__(256) void calib_write(T* __restrict__ dst, size_t n
     dst[i] = (T)i;
 }
 
+// 16 B per lane (uint4): the staged windows of k_fast_tile / k_cvfast / k_blur
+__global__ __launch_bounds__(256) void calib_read16(const uint4* __restrict__ src, size_t n,
+                                                    uint32_t* __restrict__ sink, uint32_t magic) {
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const uint4 v = src[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == magic) sink[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void calib_write16(uint4* __restrict__ dst, size_t n) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    dst[i] = make_uint4((uint32_t)i, 0u, 0u, 0u);
+}
+
 #define CK(x)                                                          \
   do {                                                                 \
     hipError_t e_ = (x);                                               \
@@ -54,6 +70,8 @@ int main() {
   hipLaunchKernelGGL(calib_read<uint64_t>, grid, block, 0, 0, (const uint64_t*)buf, kBytes / 8, sink, 0x9E3779B9u);
   hipLaunchKernelGGL(calib_read<uint32_t>, grid, block, 0, 0, (const uint32_t*)buf, kBytes / 4, sink, 0x9E3779B9u);
   hipLaunchKernelGGL(calib_read<uint8_t>, grid, block, 0, 0, (const uint8_t*)buf, kBytes, sink, 0x9E3779B9u);
+  hipLaunchKernelGGL(calib_read16, grid, block, 0, 0, (const uint4*)buf, kBytes / 16, sink, 0x9E3779B9u);
+  hipLaunchKernelGGL(calib_write16, grid, block, 0, 0, (uint4*)buf, kBytes / 16);
   hipLaunchKernelGGL(calib_write<uint64_t>, grid, block, 0, 0, (uint64_t*)buf, kBytes / 8);
   hipLaunchKernelGGL(calib_write<uint32_t>, grid, block, 0, 0, (uint32_t*)buf, kBytes / 4);
   hipLaunchKernelGGL(calib_write<uint8_t>, grid, block, 0, 0, (uint8_t*)buf, kBytes);
