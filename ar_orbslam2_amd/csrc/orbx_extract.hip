@@ -873,58 +873,62 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
       return __builtin_bit_cast(CellGeom, cwd);
     };
     // the ROI as aligned dwords (its first pixel lands at byte sh of each staged row; the 64-B
-    // pitch covers the last dword): lane item i = row * words + word.  When the largest ROI is
-    // at most kPf dwords per lane, the next cell's loads are issued before this cell is
-    // processed (their latency hides behind it) and land in LDS when it is done; an item past
-    // the ROI repeats the last one (same value, same place).
-    constexpr int kPf = (MAXR * (RS / 4) + 63) / 64;
-    constexpr bool kPrefetch = kPf <= 8;
-    uint32_t pv[kPrefetch ? kPf : 1], po[kPrefetch ? kPf : 1];
+    // pitch covers the last dword).  Lane l stages word l % kW of rows l / kW + kG u (fixed
+    // per lane: no division per item); lanes past the cell's words or rows load nothing.  When
+    // the staged window fits kPf such rounds the next cell's loads are issued before this cell
+    // is processed (their latency hides behind it) and land in LDS when it is done.
+    constexpr int kW = RS / 4, kG = 64 / kW;              // words per staged row, rows per round
+    constexpr int kPf = (MAXR + kG - 1) / kG;              // rounds for the largest ROI
+    constexpr bool kPrefetch = kPf <= 9;
+    const int lrow = lane / kW, lword = lane - lrow * kW;   // compile-time divisor
+    const bool lane_ok = lrow < kG;
+    uint32_t pv[kPrefetch ? kPf : 1];
+    int prow = 0, pmask = 0;  // rows of the staged cell; bit u: round u loaded
     auto issue = [&](const CellGeom& C) {
-      const uint8_t* src = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - (C.y0 + 3) * C.pitch - (C.x0 + 3));
       const int cols = C.x1 - C.x0, rows = C.y1 - C.y0;
-      const int a0 = C.x0 & ~3, words = ((C.x0 & 3) + cols + 3) >> 2;
-      const uint8_t* srow = src + (int64_t)C.y0 * C.pitch + a0;
-      const int items = rows * words;
-      const float inv = 1.0f / (float)words;
+      const int words = ((C.x0 & 3) + cols + 3) >> 2;
+      const uint8_t* srow = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - 3 * C.pitch - 3) +
+                            (C.x0 & ~3) - C.x0;  // staged row 0, word 0
+      pmask = 0;
 #pragma unroll
       for (int u = 0; u < (kPrefetch ? kPf : 1); u++) {
-        int rr, cc;
-        py_divmod(min(lane + 64 * u, items - 1), words, inv, rr, cc);
-        pv[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr, C.pitch) + 4 * cc);
-        po[u] = rr * RS + 4 * cc;
+        const int r = lrow + kG * u;
+        if (lane_ok && lword < words && r < rows) {
+          pv[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(r, C.pitch) + 4 * lword);
+          pmask |= 1 << u;
+        }
       }
+      prow = rows;
     };
     if (kPrefetch && nit > 0) issue(geom(0));
     for (int it = 0; it < nit; it++) {
       const int ci = __builtin_amdgcn_readlane(cil, it);
       const CellGeom C = geom(it);
-      // the ROI origin (x0, y0) sits 3 rows and 3 columns before the first detection pixel
-      const uint8_t* src = pyr + (int64_t)img * pyr_bytes +  // the level's pixel (0, 0)
-                           (C.v_row0 - (C.y0 + 3) * C.pitch - (C.x0 + 3));
       const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3 (fb_big)
       const int dr = rows - 6, cw = cols - 6;            // > 0 (k_fast_compact)
-      const int a0 = C.x0 & ~3, sh = C.x0 & 3, words = (sh + cols + 3) >> 2;  // <= RS / 4
+      const int sh = C.x0 & 3, words = (sh + cols + 3) >> 2;  // <= RS / 4
       if constexpr (kPrefetch) {
 #pragma unroll
-        for (int u = 0; u < kPf; u++) *(uint32_t*)(S + po[u]) = pv[u];
+        for (int u = 0; u < kPf; u++)
+          if ((pmask >> u) & 1) *(uint32_t*)(S + (lrow + kG * u) * RS + 4 * lword) = pv[u];
         if (it + 1 < nit) issue(geom(it + 1));
-      } else {  // four loads in flight per lane
-        const uint8_t* srow = src + (int64_t)C.y0 * C.pitch + a0;
-        const int items = rows * words;
-        const float inv = 1.0f / (float)words;
-        for (int i0 = lane; i0 < items; i0 += 256) {
+      } else {  // four rounds of loads in flight per lane
+        const uint8_t* srow = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - 3 * C.pitch - 3) +
+                              (C.x0 & ~3) - C.x0;
+        for (int r0 = lrow; r0 < rows; r0 += 4 * kG) {
           uint32_t v[4];
-          int rr[4], cc[4];
 #pragma unroll
           for (int u = 0; u < 4; u++) {
-            py_divmod(min(i0 + 64 * u, items - 1), words, inv, rr[u], cc[u]);
-            v[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(rr[u], C.pitch) + 4 * cc[u]);
+            const int r = r0 + kG * u;
+            v[u] = (lane_ok && lword < words && r < rows)
+                       ? *(const uint32_t*)(srow + (uint32_t)__mul24(r, C.pitch) + 4 * lword)
+                       : 0u;
           }
 #pragma unroll
-          for (int u = 0; u < 4; u++) asm volatile("" : "+v"(v[u]));
-#pragma unroll
-          for (int u = 0; u < 4; u++) *(uint32_t*)(S + rr[u] * RS + 4 * cc[u]) = v[u];
+          for (int u = 0; u < 4; u++) {
+            const int r = r0 + kG * u;
+            if (lane_ok && lword < words && r < rows) *(uint32_t*)(S + r * RS + 4 * lword) = v[u];
+          }
         }
       }
       for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
