@@ -207,13 +207,7 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
 
 // ------------------------------------------------------------------ retainBest (one wave)
 __device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(v, o);
-    if (lane >= o) v += u;
-  }
-  return v;
+  return wave_scan_incl(v);
 }
 
 __device__ __forceinline__ void kswap(CvKey* a, int i, int j) {

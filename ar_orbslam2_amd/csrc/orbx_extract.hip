@@ -87,12 +87,7 @@ __device__ int block_scan_excl(int* a, int M, int* s_tmp) {
   int sum = 0;
   for (int i = beg; i < end; i++) sum += a[i];
   const int lane = t & 63, wid = t >> 6;
-  int v = sum;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int n = __shfl_up(v, off);
-    if (lane >= off) v += n;
-  }
+  const int v = wave_scan_incl(sum);
   __syncthreads();
   if (lane == 63) s_tmp[wid] = v;
   __syncthreads();
@@ -126,12 +121,7 @@ __device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
   uint64_t sum = 0;
   for (int i = beg; i < end; i++) sum += a[i];
   const int lane = t & 63, wid = t >> 6;
-  uint64_t v = sum;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint64_t n = __shfl_up(v, off);
-    if (lane >= off) v += n;
-  }
+  const uint64_t v = wave_scan_incl64(sum);
   __syncthreads();
   if (lane == 63) s_tmp[wid] = v;
   __syncthreads();
@@ -669,12 +659,7 @@ template <class VAt>
 __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int cx0,
                                              uint32_t* out, int* cnt_out, VAt v_at) {
   const int cnt = __popcll(bits);
-  int incl = cnt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int n = __shfl_up(incl, o);
-    if (lane >= o) incl += n;
-  }
+  const int incl = wave_scan_incl(cnt);
   int pos = incl - cnt;
   const int nout = __shfl(incl, 63);
   while (bits) {
@@ -751,12 +736,7 @@ __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict_
       continue;
     }
     const int cnt = __popcll(b);
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int nn = __shfl_up(incl, o);
-      if (lane >= o) incl += nn;
-    }
+    const int incl = wave_scan_incl(cnt);
     const int n = __shfl(incl, 63);  // <= slot_cap
     if (lane == 0) *cnt_out = n;
     if (n <= kCompactCap) {

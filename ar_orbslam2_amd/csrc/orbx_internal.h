@@ -281,6 +281,36 @@ __device__ __forceinline__ uint32_t row16_min(uint32_t v) {
   v = min(v, (uint32_t)dpp<0x141>((int)v));
   return min(v, (uint32_t)dpp<0x140>((int)v));
 }
+// Inclusive prefix sum over the 64 lanes on DPP moves (Hillis-Steele within each 16-lane row
+// with row_shr 1 / 2 / 4 / 8, then row_bcast 15 / 31 carry the row totals up), instead of six
+// ds_bpermute round trips.  Every lane of the wave must be active.
+template <int CTRL, int ROWS, bool BOUND>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {  // DPP move, 0 where there is no source
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, BOUND);
+}
+__device__ __forceinline__ int wave_scan_incl(int v) {
+  uint32_t u = (uint32_t)v;
+  u += dpp0<0x111, 0xF, true>(u);   // row_shr:1
+  u += dpp0<0x112, 0xF, true>(u);   // row_shr:2
+  u += dpp0<0x114, 0xF, true>(u);   // row_shr:4
+  u += dpp0<0x118, 0xF, true>(u);   // row_shr:8
+  u += dpp0<0x142, 0xA, false>(u);  // row_bcast:15 into rows 1 and 3
+  u += dpp0<0x143, 0xC, false>(u);  // row_bcast:31 into rows 2 and 3
+  return (int)u;
+}
+__device__ __forceinline__ uint64_t wave_scan_incl64(uint64_t v) {
+  auto step = [](uint64_t& x, auto mv) {
+    x += (uint64_t)mv((uint32_t)x) | ((uint64_t)mv((uint32_t)(x >> 32)) << 32);
+  };
+  step(v, [](uint32_t w) { return dpp0<0x111, 0xF, true>(w); });
+  step(v, [](uint32_t w) { return dpp0<0x112, 0xF, true>(w); });
+  step(v, [](uint32_t w) { return dpp0<0x114, 0xF, true>(w); });
+  step(v, [](uint32_t w) { return dpp0<0x118, 0xF, true>(w); });
+  step(v, [](uint32_t w) { return dpp0<0x142, 0xA, false>(w); });
+  step(v, [](uint32_t w) { return dpp0<0x143, 0xC, false>(w); });
+  return v;
+}
+
 // minimum over the 64 lanes, wave-uniform (the four row minima through readlane)
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   v = row16_min(v);

@@ -468,12 +468,7 @@ __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_o
     for (int b0 = 0; b0 < nb; b0 += 64) {
       const int b = b0 + tid;
       const int c = b < nb ? cnt[b] : 0;
-      int incl = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int x = __shfl_up(incl, o);
-        if (tid >= o) incl += x;
-      }
+      const int incl = wave_scan_incl(c);
       const uint64_t ne = __ballot(c > 0);
       const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0));

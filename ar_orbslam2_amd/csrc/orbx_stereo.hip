@@ -62,12 +62,7 @@ __global__ __launch_bounds__(256) void k_stereo_rows(const StereoProblem* __rest
   const int per = (nrows + 255) / 256;
   int sum = 0;
   for (int r = tid * per; r < min((tid + 1) * per, nrows); r++) sum += s_cnt[r];
-  int incl = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int x = __shfl_up(incl, o);
-    if (lane >= o) incl += x;
-  }
+  const int incl = wave_scan_incl(sum);
   if (lane == 63) s_tmp[wid] = incl;
   __syncthreads();
   int base = incl - sum;

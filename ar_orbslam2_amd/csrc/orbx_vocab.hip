@@ -141,12 +141,7 @@ __global__ __launch_bounds__(256) void k_voc_transform(VocView V, int nid_level,
 // ------------------------------------------------------------------ k_bowvec
 __device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int incl = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int x = __shfl_up(incl, o);
-    if (lane >= o) incl += x;
-  }
+  const int incl = wave_scan_incl(v);
   if (lane == 63) s_tmp[wid] = incl;
   __syncthreads();
   int base = 0, tot = 0;
