@@ -378,9 +378,9 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
     }
   } else {
     // border tile: each window row reflected once (reflect-101), whole 16-B pieces where they
-    // lie inside the level, byte-wise reflect only for the window dwords (3 .. 20) of a piece
-    // crossing the left / right edge; dwords wholly past the last column any output reads
-    // (w + 2) stay unset
+    // lie inside the level; in a piece crossing the left / right edge, whole dwords where they
+    // lie inside and a byte-wise reflect only for the window dwords (3 .. 20) that cross;
+    // dwords wholly past the last column any output reads (w + 2) stay unset
     for (int i = tid; i < kRows * kChunks; i += 256) {
       const int r = i / kChunks, c = i - r * kChunks;
       const int y = reflect101(min(Y0 + r - 3, h + 8), h);
@@ -389,15 +389,19 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (x >= 0 && x + 16 <= w) {
         v = *(const uint4*)(row + x);
-      } else {
+      } else {  // per window dword: whole inside the level, reflected byte-wise, or unused
         uint32_t d[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const int dw = 4 * c + j, xd = x + 4 * j;
           if (dw >= 3 && dw <= 20 && xd < w + 3) {
+            if (xd >= 0 && xd + 4 <= w) {
+              d[j] = *(const uint32_t*)(row + xd);
+            } else {
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-              d[j] |= (uint32_t)row[reflect101(min(xd + k, w + 8), w)] << (8 * k);
+              for (int k = 0; k < 4; k++)
+                d[j] |= (uint32_t)row[reflect101(min(xd + k, w + 8), w)] << (8 * k);
+            }
           }
         }
         v = make_uint4(d[0], d[1], d[2], d[3]);
