@@ -182,14 +182,21 @@ def pmc_issue(pmc_dir, kernel, avg_launch_us):
                     f"({os.path.relpath(path, ROOT)})"}
 
 
+AGGREGATE_STAGES = ("k_stereo", "k_bow", "k_tri")
+
+
 def roofline_of(stages, alg, pmc_dir, steps, B):
     """Roofline object of the dominant kernel (largest total time in the per-kernel HIP-event
     pass).  The path is integer stencil / gather / popcount work: VALU issue bounds it, so
     `bound` is "valu" and frac is the VALU-issue fraction when the SQ pass of this command
     exists; the HBM fraction (algorithmic bytes / launch time vs 8 TB/s) is reported beside it."""
-    if not stages:
+    # stages that time several kernels (the stereo copy + 3 kernels, the matchers' node and
+    # finish kernels) cannot be matched to one kernel's counters: the roofline kernel is the
+    # largest single-kernel stage
+    single = {k: v for k, v in stages.items() if k not in AGGREGATE_STAGES}
+    if not single:
         return None
-    dom = max(stages, key=lambda k: stages[k][0])
+    dom = max(single, key=lambda k: single[k][0])
     ms, launches = stages[dom]
     avg_s = ms / 1e3 / max(launches, 1)
     a_bytes = alg.get(dom)
