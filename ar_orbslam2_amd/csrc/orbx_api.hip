@@ -191,7 +191,7 @@ int orbx_stereo_matches(orbx_extractor* left, orbx_extractor* right, float mb, f
   const size_t ouse = st.add(nullptr, (size_t)kp * 4), odep = st.add(nullptr, (size_t)kp * 4),
                osad = st.add(nullptr, (size_t)kp * 4), ocnt = st.add(nullptr, 4),
                ooff = st.add(nullptr, ((size_t)nrows + 1) * 4),
-               oidx = st.add(nullptr, (size_t)row_cap * 4);
+               oidx = st.add(nullptr, (size_t)row_cap * 8);
   int rc = tls_ws.reserve(st.host.size());
   if (rc) return rc;
   char* base = tls_ws.d;
@@ -209,7 +209,7 @@ int orbx_stereo_matches(orbx_extractor* left, orbx_extractor* right, float mb, f
   P.depth = dptr<float>(base, odep);
   P.sad = dptr<int>(base, osad);
   P.row_off = dptr<int>(base, ooff);
-  P.row_idx = dptr<int>(base, oidx);
+  P.row_ent = dptr<uint2>(base, oidx);
   ORBX_HIP(hipMemcpyAsync(base + oprob, &P, sizeof(P), hipMemcpyHostToDevice, s));
   rc = launch_stereo(dptr<StereoProblem>(base, oprob), 1, vl.d_lv, vl.g->nlevels, nrows, row_cap,
                      kp, mb, mbf, s);

@@ -45,7 +45,7 @@ struct orbx_frames {
   float* d_depth = nullptr;   // [B][kp] mvDepth
   int* d_sad = nullptr;       // [B][kp]
   int* d_row_off = nullptr;   // [B][nrows + 1]
-  int* d_row_idx = nullptr;   // [B][row_cap]
+  uint2* d_row_idx = nullptr;  // [B][row_cap] row entries
   StereoProblem* d_sprob = nullptr;
   // per frame
   uint32_t* d_node_of = nullptr;  // [B][kp] FeatureVector node id
@@ -170,7 +170,7 @@ int build_problems(orbx_frames* F, int n) {
       S.depth = F->d_depth + (int64_t)f * kp;
       S.sad = F->d_sad + (int64_t)f * kp;
       S.row_off = F->d_row_off + (int64_t)f * (F->st_nrows + 1);
-      S.row_idx = F->d_row_idx + (int64_t)f * F->st_row_cap;
+      S.row_ent = F->d_row_idx + (int64_t)f * F->st_row_cap;
     }
     ORBX_HIP(hipMemcpy(F->d_sprob, sp.data(), sizeof(StereoProblem) * n, hipMemcpyHostToDevice));
   }

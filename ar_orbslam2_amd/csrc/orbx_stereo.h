@@ -23,7 +23,7 @@ struct StereoProblem {
   float* depth;   // [kp_cap] mvDepth
   int* sad;       // [kp_cap] SAD of the retained match, -1 otherwise
   int* row_off;   // scratch [nrows + 1]
-  int* row_idx;   // scratch [row_cap]
+  uint2* row_ent;  // scratch [row_cap]: right keypoint (index | octave << 16, x bits)
 };
 
 // Rows a right keypoint is registered in (Frame.cc:486-497) are at most this many.

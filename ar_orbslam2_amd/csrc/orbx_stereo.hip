@@ -8,9 +8,12 @@
 //                    reference's first-minimum over ascending right indices
 //   k_stereo_match   one wave per left keypoint: candidates of its row across lanes (octave
 //                    +-1, u window), Hamming minimum, then the 11 x 11 SAD slide over
-//                    incR = -5..5 (121 pixels across lanes, one wave reduction per shift; the
-//                    centred float windows of the reference have integer entries, so the
-//                    integer SAD equals cv::norm(IL, IR, NORM_L1) exactly), parabola fit in f32
+//                    incR = -5..5 (121 pixels across lanes, one DPP wave reduction per shift;
+//                    the centred float windows of the reference have integer entries, so the
+//                    integer SAD equals cv::norm(IL, IR, NORM_L1) exactly), parabola fit in f32.
+//                    Row entries carry the right keypoint's x and octave (no keypoint reload);
+//                    both windows are staged in LDS by aligned dword loads (two rounds, not 24
+//                    byte loads per lane: the vector memory pipeline bounded this kernel)
 //   k_stereo_filter  one workgroup per frame: median of the retained SADs by a two-level
 //                    histogram select, thDist = 1.5f*1.4f*median, invalidate SAD >= thDist
 //                    (Frame.cc:626-642)
@@ -83,15 +86,19 @@ __global__ __launch_bounds__(256) void k_stereo_rows(const StereoProblem* __rest
     const int minr = max((int)floorf(k.y - r), 0);
     for (int y = minr; y <= maxr; y++) {
       const int slot = atomicAdd(&s_cnt[y], 1);
-      if (slot < row_cap) P.row_idx[slot] = i;
+      if (slot < row_cap) P.row_ent[slot] = make_uint2((uint32_t)i | ((uint32_t)k.octave << 16),
+                                                       __float_as_uint(k.x));
     }
   }
 }
 
+// sum over the 64 lanes, wave-uniform: 16-lane row sums on DPP, then the four rows by readlane
+// (no ds_bpermute round trips: the SAD slide's 11 reductions are on the kernel's critical path).
+// Every lane must be active.
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = row16_sum(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+         __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 
 __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __restrict__ probs,
@@ -111,76 +118,110 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
   const int levelL = kpL.octave;
   const int row = (int)vL;  // vRowIndices[vL]: float -> index truncation
   bool ok = row >= 0 && row < nrows;
-  int bestDist = kTH_HIGH, bestIdxR = 0;
+  int bestDist = kTH_HIGH;
+  float uR0 = 0.0f;
   const float minU = uL - maxD, maxU = uL - minD;
   if (ok && maxU < 0) ok = false;
+  // the left window (IL) depends only on the left keypoint: its loads are issued here, ahead of
+  // the candidate search, so their latency overlaps it (addresses clamped into the level; the
+  // values are used only when the reference would take the window)
+  const LevelGeom& G = lv[levelL];
+  const float scaleFactor = G.inv_scale;
+  const float scaleduL = roundf(kpL.x * scaleFactor);
+  const float scaledvL = roundf(kpL.y * scaleFactor);
+  const int y0 = (int)scaledvL - kW, xl0 = (int)scaleduL - kW;
+  const bool left_in = y0 >= 0 && y0 + 2 * kW < G.h && xl0 >= 0 && xl0 + 2 * kW < G.w;
+  const int64_t pitch = G.pitch;
+  const uint8_t* PL = P.pyrL + G.pyr_off;
+  const uint8_t* PR = P.pyrR + G.pyr_off;
+  int yy[2], xx[2];
+  bool has[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int p = lane + 64 * k;
+    has[k] = p < (2 * kW + 1) * (2 * kW + 1);
+    yy[k] = has[k] ? p / (2 * kW + 1) : 0;
+    xx[k] = has[k] ? p - yy[k] * (2 * kW + 1) : 0;
+  }
+  // its 11 rows x 11 columns as 4 aligned dwords per row (lane < 44), kept in a register until
+  // the window is staged in LDS for the SAD; a dword starting at or past w is not read
+  const int al = xl0 & ~3, lo = xl0 - al;
+  uint32_t lw = 0u;
+  if (ok && left_in && lane < (2 * kW + 1) * 4 && al + 4 * (lane & 3) < G.w)
+    lw = *(const uint32_t*)(PL + (int64_t)(y0 + (lane >> 2)) * pitch + al + 4 * (lane & 3));
   if (ok) {
     const int c0 = P.row_off[row], c1 = P.row_off[row + 1];
     const uint64_t* q = (const uint64_t*)(P.dl + (int64_t)iL * 32);
     const uint64_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
     int key = INT_MAX;  // (distance << 16) | right index: first minimum in right-index order
+    float ukey = 0.0f;  // the u of this lane's best key (no reload of the winner's keypoint)
     for (int j = c0 + lane; j < c1; j += 64) {
-      const int iR = P.row_idx[j];
-      const orbx_keypoint kpR = P.kr[iR];
-      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-      const float uR = kpR.x;
+      const uint2 e = P.row_ent[j];  // (index | octave << 16, x): no keypoint reload
+      const int iR = (int)(e.x & 0xFFFFu), octR = (int)(e.x >> 16);
+      if (octR < levelL - 1 || octR > levelL + 1) continue;
+      const float uR = __uint_as_float(e.y);
       if (uR >= minU && uR <= maxU) {
         const uint64_t* r = (const uint64_t*)(P.dr + (int64_t)iR * 32);
         const int dist = __popcll(d0 ^ r[0]) + __popcll(d1 ^ r[1]) + __popcll(d2 ^ r[2]) +
                          __popcll(d3 ^ r[3]);
-        key = min(key, (dist << 16) | iR);
+        const int k2 = (dist << 16) | iR;
+        if (k2 < key) {
+          key = k2;
+          ukey = uR;
+        }
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) key = min(key, __shfl_xor(key, o));
-    if (key != INT_MAX && (key >> 16) < bestDist) {
-      bestDist = key >> 16;
-      bestIdxR = key & 0xFFFF;
+    const int kmin = (int)wave_min_u32((uint32_t)key);  // key >= 0: the same minimum
+    if (kmin != INT_MAX && (kmin >> 16) < bestDist) {
+      bestDist = kmin >> 16;
+      const uint64_t who = __ballot(key == kmin);  // (distance, index) keys are unique
+      uR0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ukey),
+                                                                (int)__builtin_ctzll(who)));
     }
     ok = bestDist < kTH_HIGH;
   }
   if (ok) {  // subpixel match by correlation (Frame.cc:555-618)
-    const LevelGeom& G = lv[levelL];
-    const float uR0 = P.kr[bestIdxR].x;
-    const float scaleFactor = G.inv_scale;
-    const float scaleduL = roundf(kpL.x * scaleFactor);
-    const float scaledvL = roundf(kpL.y * scaleFactor);
     const float scaleduR0 = roundf(uR0 * scaleFactor);
     const float iniu = scaleduR0 + kL - kW;
     const float endu = scaleduR0 + kL + kW + 1;
-    const int y0 = (int)scaledvL - kW, xl0 = (int)scaleduL - kW, xr = (int)scaleduR0;
+    const int xr = (int)scaleduR0;
     ok = !(iniu < 0 || endu >= G.w);
     // windows the reference would take with cv::Mat ranges (they assert inside the level)
-    if (ok && (y0 < 0 || y0 + 2 * kW >= G.h || xl0 < 0 || xl0 + 2 * kW >= G.w ||
-               xr - kL - kW < 0))
-      ok = false;
+    if (ok && (!left_in || xr - kL - kW < 0)) ok = false;
     if (ok) {
-      const uint8_t* PL = P.pyrL + G.pyr_off;
-      const uint8_t* PR = P.pyrR + G.pyr_off;
-      const int64_t pitch = G.pitch;
-      const int cL = PL[(int64_t)(y0 + kW) * pitch + xl0 + kW];
-      // centres of the 11 shifted right windows, one per lane, broadcast below
-      const int cRl = lane < 2 * kL + 1 ? PR[(int64_t)(y0 + kW) * pitch + xr + lane - kL] : 0;
-      int a[2], yy[2], xx[2];
-      bool has[2];
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const int p = lane + 64 * k;
-        has[k] = p < (2 * kW + 1) * (2 * kW + 1);
-        yy[k] = has[k] ? p / (2 * kW + 1) : 0;
-        xx[k] = has[k] ? p - yy[k] * (2 * kW + 1) : 0;
-        a[k] = has[k] ? (int)PL[(int64_t)(y0 + yy[k]) * pitch + xl0 + xx[k]] - cL : 0;
+      // the right window's 11 rows x 21 columns (xr - 10 .. xr + 10, every shift) staged in
+      // this wave's LDS by aligned dword loads (6 per row, 66 in all), instead of 22 byte
+      // loads per lane over 11 rows each; dwords starting at or past w stay unread (the
+      // window ends at xr + 10 <= w - 2; the pitch is >= w + 4)
+      __shared__ uint32_t s_rw[4][2 * kW + 1][6];
+      __shared__ uint32_t s_lw[4][2 * kW + 1][4];
+      const int wv = threadIdx.x >> 6;
+      if (lane < (2 * kW + 1) * 4) s_lw[wv][lane >> 2][lane & 3] = lw;
+      const int ar = (xr - 2 * kL) & ~3, ro = (xr - 2 * kL) - ar;  // ar >= 0: xr >= 10
+      for (int i = lane; i < (2 * kW + 1) * 6; i += 64) {  // 66 dwords: two rounds
+        const int rr = i / 6, dw = i - rr * 6;
+        s_rw[wv][rr][dw] = ar + 4 * dw < G.w
+                               ? *(const uint32_t*)(PR + (int64_t)(y0 + rr) * pitch + ar + 4 * dw)
+                               : 0u;
       }
+      __builtin_amdgcn_wave_barrier();
+      const uint8_t* rw = (const uint8_t*)s_rw[wv];  // byte (row, c) at rw[row * 24 + c]
+      const uint8_t* lwb = (const uint8_t*)s_lw[wv];  // byte (row, c) at lwb[row * 16 + c]
+      const int cL = lwb[kW * 16 + lo + kW];
+      int a[2];
+#pragma unroll
+      for (int k = 0; k < 2; k++) a[k] = has[k] ? (int)lwb[yy[k] * 16 + lo + xx[k]] - cL : 0;
       int vd[2 * kL + 1];
       int bestSad = INT_MAX, bestinc = 0;
 #pragma unroll
       for (int inc = -kL; inc <= kL; inc++) {
-        const int cR = __shfl(cRl, inc + kL);
+        // window column of (xx, inc): xr + inc - kW + xx - (xr - 10) = inc + kL + xx
+        const int cR = rw[kW * 24 + ro + inc + 2 * kL];  // the shifted window's centre
         int acc = 0;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
           if (has[k]) {
-            const int b = (int)PR[(int64_t)(y0 + yy[k]) * pitch + xr + inc - kW + xx[k]] - cR;
+            const int b = (int)rw[yy[k] * 24 + ro + inc + kL + xx[k]] - cR;
             acc += abs(a[k] - b);
           }
         }
