@@ -1462,7 +1462,10 @@ __global__ __launch_bounds__(256) void k_describe(
     const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const uint32_t* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
-  constexpr int RW = 10, BW = 11;  // dwords per staged row (31+3 / 37+3 bytes, rounded up)
+  // dwords per staged row: raw 31+3 bytes rounded up; blurred 16-B pieces from a 16-B aligned
+  // start (offset <= 15 plus 37 bytes: 13 dwords) — an odd stride, so the rBRIEF samples of
+  // different rows spread over the LDS banks
+  constexpr int RW = 10, BW = 13, BC = 4;  // BC: 16-B pieces per blurred row
   constexpr int RN = 31 * RW, BN = 37 * BW;
   __shared__ uint32_t s_raw[8][RN];
   __shared__ uint32_t s_blr[8][BN];
@@ -1498,9 +1501,10 @@ __global__ __launch_bounds__(256) void k_describe(
   const uint8_t* L = pyr + (int64_t)img * pyr_bytes + pyr_off;
   const uint8_t* Bp = blur + (int64_t)img * pyr_bytes + pyr_off;
   const int fr = (cx - 15) >> 2, lr = (cx + 15) >> 2;  // raw dword columns
-  const int fb = (cx - 18) >> 2, lb = (cx + 18) >> 2;  // blurred dword columns
+  const int ab = (cx - 18) & ~15, lb = ((cx + 18) & ~15) - ab;  // blurred first piece, last offset
   if (active) {
-    uint32_t vr[(RN + 31) / 32], vb[(BN + 31) / 32];
+    uint32_t vr[(RN + 31) / 32];
+    uint4 vb[(37 * BC + 31) / 32];
 #pragma unroll
     for (int k = 0; k < (RN + 31) / 32; k++) {
       const int i = hl + 32 * k, r = i / RW, c = i - r * RW;
@@ -1509,21 +1513,29 @@ __global__ __launch_bounds__(256) void k_describe(
                   : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < (BN + 31) / 32; k++) {
-      const int i = hl + 32 * k, r = i / BW, c = i - r * BW;
-      vb[k] = (i < BN && fb + c <= lb)
-                  ? *(const uint32_t*)(Bp + (uint32_t)((cy - 18 + r) * pitch + 4 * (fb + c)))
-                  : 0u;
+    for (int k = 0; k < (37 * BC + 31) / 32; k++) {  // 16-B pieces: 5 loads per lane, not 13
+      const int i = hl + 32 * k, r = i >> 2, c = i & 3;
+      vb[k] = (i < 37 * BC && 16 * c <= lb)
+                  ? *(const uint4*)(Bp + (uint32_t)((cy - 18 + r) * pitch + ab + 16 * c))
+                  : make_uint4(0u, 0u, 0u, 0u);
     }
 #pragma unroll
     for (int k = 0; k < (RN + 31) / 32; k++)
       if (hl + 32 * k < RN) s_raw[hw][hl + 32 * k] = vr[k];
 #pragma unroll
-    for (int k = 0; k < (BN + 31) / 32; k++)
-      if (hl + 32 * k < BN) s_blr[hw][hl + 32 * k] = vb[k];
+    for (int k = 0; k < (37 * BC + 31) / 32; k++) {
+      const int i = hl + 32 * k, r = i >> 2, c = i & 3;
+      if (i < 37 * BC) {
+        uint32_t* d = s_blr[hw] + r * BW + 4 * c;
+        d[0] = vb[k].x;
+        if (4 * c + 1 < BW) d[1] = vb[k].y;
+        if (4 * c + 2 < BW) d[2] = vb[k].z;
+        if (4 * c + 3 < BW) d[3] = vb[k].w;
+      }
+    }
   }
   constexpr int BS = 4 * BW;
-  const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - 4 * fb);
+  const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - ab);
   // IC_Angle (ORBextractor.cc:73-98): lane hl < 31 sums row v = hl - 15 of the circular patch
   // (v_dot4_u32_u8 over the row's bytes masked to |u| <= umax[|v|])
   int m10 = 0, m01 = 0;
