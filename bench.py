@@ -439,6 +439,18 @@ def cpu_baseline_marker(cfg, seconds, mp_seconds, warmup=5, min_frames=100, max_
                 single_thread=single, **info)
 
 
+def cvorb_level_sizes(params, w, h):
+    """cv::ORB 2.4 pyramid sizes (orb.cpp operator(): scale = (float)pow(scaleFactor, level),
+    size = cvRound(cols * (1 / scale))) — host arithmetic for the byte model, computed here so
+    that the product leg of bench.py never calls into oracle/."""
+    sf = float(params.scale_factor)
+    out = []
+    for lvl in range(params.nlevels):
+        inv = np.float32(1) / np.float32(sf ** (lvl - params.first_level))
+        out.append((int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))))
+    return out
+
+
 def marker_bytes(levels, n_kp, n_img, n_target):
     """Algorithmic bytes per launch of the marker-path kernels (same byte model as §8d; the
     matcher reads both descriptor sets once per frame)."""
@@ -667,9 +679,7 @@ def run_marker(args, cfg, rank, world, local, streams, dist):
     elapsed = aggregate_elapsed(elapsed, world)
     n_streams = args.streams_total or world * S
     value = n_streams * B * args.steps / elapsed
-    from oracle import oracle as O  # level sizes only (host arithmetic tables)
-    lv = O.cvorb_levels(cvorb_params(nf), w, h)
-    levels = list(zip(lv["w"].tolist(), lv["h"].tolist()))
+    levels = cvorb_level_sizes(cvorb_params(nf), w, h)
     n_kp = int(kp_counts.sum())
     alg = marker_bytes(levels, n_kp, B, len(target_desc))
     roofline = roofline_of(stages, alg, args.pmc_dir, args.roofline_steps, B)

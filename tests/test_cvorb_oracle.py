@@ -321,3 +321,17 @@ def test_extractor_empty_and_tiny():
     assert len(kps) == 0
     kps, desc = O.cvorb_detect(np.full((200, 200), 77, np.uint8), p)
     assert len(kps) == 0
+
+
+@pytest.mark.parametrize("size", [(640, 480), (1241, 376), (1920, 1080), (37, 41)])
+@pytest.mark.parametrize("sf,nl", [(1.2, 8), (1.5, 5), (2.0, 3)])
+def test_bench_cvorb_level_sizes_match_oracle(size, sf, nl):
+    """bench.py's own cv::ORB level sizes (the AR byte model; the product leg must not call
+    oracle/) equal the oracle's getScale / cvRound pyramid sizes."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from ar_orbslam2_amd.marker import cvorb_params
+    p = cvorb_params(500, sf, nl)
+    lv = O.cvorb_levels(p, *size)
+    assert bench.cvorb_level_sizes(p, *size) == list(zip(lv["w"].tolist(), lv["h"].tolist()))
