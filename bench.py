@@ -222,7 +222,26 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     out["stages_ms_per_step"] = {k: round(v[0] / steps, 4) for k, v in stages.items()}
     out["stages_of"] = (f"roofline pass: camera stream 0 alone, {steps} steps of {B} frames "
                         f"after the timed region")
+    out["extract_vs_match"] = phase_split(stages, steps, B)
     return out
+
+
+EXTRACT_STAGES = ("k_pyramid", "k_blur", "k_fast_tile", "k_fast_compact", "k_fast_fallback",
+                  "k_octree", "k_describe", "k_cvfast", "k_cvselect", "k_cvdescribe")
+
+
+def phase_split(stages, steps, B):
+    """SURVEY §8d asks for "extract" and "match" rates beside the combined one: the stage times
+    of the roofline pass (one camera stream alone) summed per phase, as ms per batch of B frames
+    and the frames/s one stream would reach on that phase alone (the timed region overlaps
+    several streams, so these do not add up to `value`)."""
+    ex = sum(v[0] for k, v in stages.items() if k in EXTRACT_STAGES) / steps
+    ma = sum(v[0] for k, v in stages.items() if k not in EXTRACT_STAGES) / steps
+    fps = lambda ms: round(B / (ms / 1e3), 1) if ms > 0 else None  # noqa: E731
+    return {"extract_ms_per_batch": round(ex, 4), "match_ms_per_batch": round(ma, 4),
+            "extract_frames_per_s_one_stream": fps(ex), "match_frames_per_s_one_stream": fps(ma),
+            "combined_frames_per_s_one_stream": fps(ex + ma),
+            "match_stages": sorted(k for k in stages if k not in EXTRACT_STAGES)}
 
 
 # ---------------------------------------------------------------------------- CPU baseline

@@ -121,3 +121,18 @@ def test_synthetic_frames_are_deterministic():
     a = synth.frame(64, 48, t=3, stream=1)
     b = synth.frame(64, 48, t=3, stream=1)
     assert np.array_equal(a, b) and a.dtype == np.uint8 and a.shape == (48, 64)
+
+
+def test_bench_extract_vs_match_split():
+    """bench.py's §8d phase split: extraction stages vs matcher stages of the roofline pass."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    st = {"k_pyramid": (1.0, 5), "k_fast_tile": (2.0, 5), "k_describe": (1.0, 5),
+          "k_voc_transform": (0.5, 5), "k_bow": (0.5, 5), "k_stereo": (1.0, 5)}
+    s = bench.phase_split(st, 5, 256)
+    assert s["extract_ms_per_batch"] == pytest.approx(0.8)
+    assert s["match_ms_per_batch"] == pytest.approx(0.4)
+    assert s["combined_frames_per_s_one_stream"] == pytest.approx(256 / 1.2e-3, rel=1e-6)
+    assert s["match_stages"] == ["k_bow", "k_stereo", "k_voc_transform"]
