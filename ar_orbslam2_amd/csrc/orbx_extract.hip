@@ -1343,7 +1343,9 @@ __global__ __launch_bounds__(NT) void k_octree(
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_tmp[NT / 64 + 1];
   __shared__ int s_misc[8];
-  const int level = level_base + blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  // grid (image, level): every image's largest level is dispatched first and the small levels
+  // last, so the launch does not end on one late large-level workgroup's serial pass chain
+  const int level = level_base + blockIdx.y, img = blockIdx.x, tid = threadIdx.x;
   const LevelGeom& G = lv[level];
   int* oc = ocount + img * nlevels + level;
   if (G.ncells == 0) {
@@ -1770,12 +1772,12 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   // levels [0, oct_split) on 1024-thread workgroups with the large LDS carve, the others on
   // 256-thread ones sized for themselves (several per CU)
   if (P->oct_split > 0)
-    hipLaunchKernelGGL(k_octree<kOctNTBig>, dim3(P->oct_split, n), dim3(kOctNTBig),
+    hipLaunchKernelGGL(k_octree<kOctNTBig>, dim3(n, P->oct_split), dim3(kOctNTBig),
                        P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
                        P->d_cand, g.cand_total, P->d_lin, P->d_label, P->d_okey, P->d_ocount,
                        g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0);
   if (P->oct_split < L)
-    hipLaunchKernelGGL(k_octree<kOctNT>, dim3(L - P->oct_split, n), dim3(kOctNT), P->oct_smem,
+    hipLaunchKernelGGL(k_octree<kOctNT>, dim3(n, L - P->oct_split), dim3(kOctNT), P->oct_smem,
                        P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, P->d_cand,
                        g.cand_total, P->d_lin, P->d_label, P->d_okey, P->d_ocount, g.kp_total, L,
                        P->oct_nc, P->oct_cc, P->oct_split);
