@@ -499,6 +499,9 @@ constexpr int kCellMax = 66;  // wCell, hCell < 60 (+6)
 //      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  Evaluated at the
 //      queued candidates only (one lane each); survivors set their bit in the row's 64-bit
 //      keep word in LDS (ds_or), which one thread per row and threshold then stores.
+// k_fast_fallback queue counters, [2 img + fb_big] kFbStride ints apart: one 128-B line each (the
+// queues fill with one atomic per wave; on a shared line those atomics serialize)
+constexpr int kFbStride = 32;
 constexpr int kFastT = 64;
 struct FastTile {
   int16_t level, tx, ty, pad;
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
                                                    int64_t bm_words,
                                                    const LevelGeom* __restrict__ lv,
                                                    const FastTile* __restrict__ tiles,
-                                                   int ini_th) {
+                                                   int ini_th, int* __restrict__ fb_count) {
   constexpr int kInR = kFastT + 8;        // staged rows Y0-4 .. Y0+67
   constexpr int kInD = (kFastT + 32) / 4; // staged dwords: columns X0-16 .. X0+79 (16-B pieces)
   constexpr int kWinR = kFastT + 2;       // V rows Y0-1 .. Y0+64
@@ -528,6 +531,9 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   xcd_block(bx, img);
   const FastTile T = tiles[bx];
   const int tid = threadIdx.x, lane = tid & 63;
+  // the image's two k_fast_fallback queue counters start at 0 (read by k_fast_compact, which
+  // runs after this launch): one tile per image clears them instead of a fill launch
+  if (bx == 0 && tid < 2 * kFbStride) fb_count[2 * kFbStride * img + tid] = 0;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar row math
   const LevelGeom& G = lv[T.level];
   const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
@@ -679,9 +685,6 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
 // the workgroup's LDS at 8 KB: occupancy, not issue, bounds this latency-chained kernel.
 constexpr int kCompactCap = 256;
 constexpr int kCompactK = 4;          // cells per wave: each round of loads covers all of them
-// k_fast_fallback queue counters, [2 img + fb_big] kFbStride ints apart: one 128-B line each (the
-// queues fill with one atomic per wave; on a shared line those atomics serialize)
-constexpr int kFbStride = 32;
 __global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict__ vmap,
                                                       int64_t pyr_bytes,
                                                       const uint64_t* __restrict__ bitmaps,
@@ -1623,6 +1626,7 @@ struct orbx_plan {
   size_t oct_smem = 0, oct_smem_big = 0;
   int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;
   int cell_cap = 0;
+  bool has_fb_big = false;  // some cell's ROI needs k_fast_fallback<72, kCellMax>
   bool fast_pair = true;  // k_fast_tile pretest on row pairs (ORBX_FAST_PAIR=0: one row per lane)
   const uint8_t* last_in = nullptr;
   int last_n = 0;
@@ -1752,9 +1756,8 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   if (ncells > 0) {
     hipLaunchKernelGGL(P->fast_pair ? k_fast_tile<true> : k_fast_tile<false>, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
-                       g.ini_th);
+                       g.ini_th, P->d_fb_count);
     pr.mark(P->stream, st_fs);
-    launch_fill_u32((uint32_t*)P->d_fb_count, 2 * kFbStride * (size_t)n, 0u, P->stream);
     hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 4 * kCompactK - 1) / (4 * kCompactK), n),
                        dim3(256), 0, P->stream,
                        P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
@@ -1763,7 +1766,8 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
     hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
                        P->d_pyr, g.pyr_bytes, P->d_cells, ncells, P->d_fb_count,
                        P->d_fb_list, g.min_th, P->d_cand, g.cand_total, P->d_cell_counts);
-    hipLaunchKernelGGL((k_fast_fallback<72, kCellMax>), dim3(kFbWG / 4, n), dim3(256), 0,
+    if (P->has_fb_big)  // (at C2 no cell is that large: 4,096 waves would only find it empty)
+      hipLaunchKernelGGL((k_fast_fallback<72, kCellMax>), dim3(kFbWG / 4, n), dim3(256), 0,
                        P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, ncells,
                        P->d_fb_count, P->d_fb_list, g.min_th, P->d_cand, g.cand_total,
                        P->d_cell_counts);
@@ -1816,6 +1820,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->device = hip_device;
   if (const char* e = getenv("ORBX_FAST_PAIR")) P->fast_pair = atoi(e) != 0;
   const Geometry& g = P->g;
+  for (const CellGeom& c : g.cells) P->has_fb_big |= c.fb_big != 0;
   auto fail = [&](int code) {
     orbx_plan_destroy(P);
     return code;
