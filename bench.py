@@ -44,7 +44,9 @@ PCIE_GEN5_X16_GBS = 63.0  # PCIe Gen5 x16 spec, one direction
 VALU_SIMDS = 1024         # 256 CUs x 4 SIMDs
 CLOCK_GHZ = 2.4           # MI355X peak engine clock
 CONFIGS = {
-    "C2": dict(w=640, h=480, nfeatures=1000,
+    # batch: frames per step per camera stream (C2: 3 x 512 measured 225.5k vs 3 x 256 222.3k
+    # frames/s, three alternating runs each on one box; the other configs keep 256)
+    "C2": dict(w=640, h=480, nfeatures=1000, batch=512,
                workload="TUM fr1/xyz mono 640x480, 1000 features, 1xMI355X HIP extract+match"),
     "C3": dict(w=752, h=480, nfeatures=1200, stereo=(47.90639384423901, 435.2046959714599),
                workload="EuRoC MH01 stereo geometry 2x752x480, 1200 features, stereo matching"),
@@ -899,8 +901,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256,
-                    help="frames per step per camera stream")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per step per camera stream (default: the config's, else 256)")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled")
     ap.add_argument("--streams", type=int, default=3,
@@ -934,6 +936,8 @@ def parse_args(argv=None):
     ap.add_argument("--roofline-steps", type=int, default=5,
                     help="steps of the single-stream roofline pass (per-kernel HIP events)")
     args = ap.parse_args(argv)
+    if args.batch is None:
+        args.batch = CONFIGS[args.config].get("batch", 256)
     if args.pmc_dir is None:  # the committed PMC passes of this config's default command
         # (never another config's: a missing directory reports traffic / VALU floor as null)
         args.pmc_dir = os.path.join(ROOT, "profiles",
