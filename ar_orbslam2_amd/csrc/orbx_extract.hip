@@ -1766,7 +1766,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
     hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
                        P->d_pyr, g.pyr_bytes, P->d_cells, ncells, P->d_fb_count,
                        P->d_fb_list, g.min_th, P->d_cand, g.cand_total, P->d_cell_counts);
-    if (P->has_fb_big)  // (at C2 no cell is that large: 4,096 waves would only find it empty)
+    if (P->has_fb_big)  // (a plan without such cells would launch waves that find the queue empty)
       hipLaunchKernelGGL((k_fast_fallback<72, kCellMax>), dim3(kFbWG / 4, n), dim3(256), 0,
                        P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, ncells,
                        P->d_fb_count, P->d_fb_list, g.min_th, P->d_cand, g.cand_total,
