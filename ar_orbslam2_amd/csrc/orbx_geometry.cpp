@@ -5,6 +5,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 
 #include "orbx_internal.h"
@@ -171,12 +172,19 @@ int build_pyramid(Geometry* g, std::string* why) {
   // ~2 rows per level below the top, so stages stay short.
   g->pyr_stages.clear();
   g->bands.clear();
+  // LDS bound of a band's two level buffers (ORBX_PY_MAX_SMEM overrides, for tuning only)
+  static const int py_max_smem = [] {
+    const char* e = getenv("ORBX_PY_MAX_SMEM");
+    const int v = e ? atoi(e) : 0;
+    return v >= 4096 && v <= kPyMaxSmemLimit ? v : kPyMaxSmem;
+  }();
   for (int l0 = 1; l0 < nl;) {
     PyrStage st;
     st.l0 = l0;
     st.l1 = std::min(nl - 1, l0 + (l0 == 1 ? kPyStage0 : kPyStageN) - 1);
     const int hs = g->lv[l0 - 1].h;
     std::vector<PyrBand> bands;
+    int smem_cap = py_max_smem;  // raised to kPyMaxSmemLimit for rows too wide for it
     for (int nb = std::max(1, hs / kPyBandH);; nb++) {
       bands.assign(nb, PyrBand{});
       int need[2] = {0, 0};
@@ -200,8 +208,13 @@ int build_pyramid(Geometry* g, std::string* why) {
       }
       st.buf_b = (need[0] + 15) & ~15;
       st.smem = st.buf_b + need[1];
-      if (st.smem <= kPyMaxSmem) break;
+      if (st.smem <= smem_cap) break;
       if (nb >= hs) {
+        if (smem_cap < kPyMaxSmemLimit) {  // one-row bands still too large: the larger carve
+          smem_cap = kPyMaxSmemLimit;
+          nb = std::max(1, hs / kPyBandH) - 1;
+          continue;
+        }
         if (why) *why = "image too wide for the pyramid bands";
         return ORBX_EUNSUPPORTED;
       }

@@ -43,7 +43,12 @@ constexpr int kPyBandH = ORBX_PY_BANDH;  // source-level rows per band (more if 
 constexpr int kPyNT = ORBX_PY_NT;        // k_pyramid threads per workgroup
 constexpr int kPyStage0 = ORBX_PY_STAGE0;  // levels built by the first stage (from the input)
 constexpr int kPyStageN = ORBX_PY_STAGEN;  // levels per later stage (from the pyramid)
-constexpr int kPyMaxSmem = 64 * 1024;    // k_pyramid dynamic LDS bound (both buffers)
+// k_pyramid dynamic LDS bound (both buffers): bands are narrowed until they fit.  40 KB keeps
+// four workgroups per CU; the 64 KB this was measured C4's pyramid at 0.76 vs 0.62 ms per 256
+// frames (wide 1241-px rows: two workgroups per CU), C2 0.31 vs 0.30 ms (32 KB: C4 0.65,
+// 24 KB: more recomputed band cones, C4 0.76)
+constexpr int kPyMaxSmem = 40 * 1024;
+constexpr int kPyMaxSmemLimit = 64 * 1024;
 #ifndef ORBX_PY_STRIP
 #define ORBX_PY_STRIP 4
 #endif
