@@ -136,3 +136,20 @@ def test_bench_extract_vs_match_split():
     assert s["match_ms_per_batch"] == pytest.approx(0.4)
     assert s["combined_frames_per_s_one_stream"] == pytest.approx(256 / 1.2e-3, rel=1e-6)
     assert s["match_stages"] == ["k_bow", "k_stereo", "k_voc_transform"]
+
+
+def test_summarizer_finds_roofline_pass():
+    """scripts/summarize_profiles.py: the roofline pass is the last run of >= 5 consecutive
+    dispatches on one stream (the timed region and the PCIe pass rotate over the streams)."""
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                        "summarize_profiles.py")
+    spec = importlib.util.spec_from_file_location("summarize_profiles", path)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    timed = [(700, s) for _ in range(4) for s in "123"]
+    solo = [(650 + i, "1") for i in range(5)]
+    pcie = [(720, s) for _ in range(3) for s in "123"]
+    assert m.solo_run(timed + solo + pcie) == [650, 651, 652, 653, 654]
+    assert m.solo_run(timed) == [700] * 5  # no solo run: the last dispatches
