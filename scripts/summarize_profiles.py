@@ -46,17 +46,19 @@ def trace_durations(path):
 
 
 def solo_run(d, steps=5):
-    """The roofline pass's dispatches: the last run of >= steps consecutive dispatches on one
-    stream (the timed region and the PCIe pass after it alternate over the camera streams)."""
+    """The roofline pass's dispatches: the first `steps` of the longest run of consecutive
+    dispatches on one stream.  The timed region before it and the PCIe pass after it rotate
+    over the camera streams (1, 2, 3, ...), so the run is the pass itself plus, at its end, the
+    PCIe pass's first dispatch when that lands on the same stream."""
     best, i = [], 0
     while i < len(d):
         j = i
         while j < len(d) and d[j][1] == d[i][1]:
             j += 1
-        if j - i >= steps:
-            best = [dur for dur, _ in d[j - steps:j]]
+        if j - i >= steps and j - i > len(best):
+            best = [dur for dur, _ in d[i:j]]
         i = j
-    return best or [dur for dur, _ in d[-steps:]]
+    return best[:steps] or [dur for dur, _ in d[-steps:]]
 
 
 def counters(pmc_dir):

@@ -139,8 +139,9 @@ def test_bench_extract_vs_match_split():
 
 
 def test_summarizer_finds_roofline_pass():
-    """scripts/summarize_profiles.py: the roofline pass is the last run of >= 5 consecutive
-    dispatches on one stream (the timed region and the PCIe pass rotate over the streams)."""
+    """scripts/summarize_profiles.py: the roofline pass is the start of the longest run of
+    dispatches on one stream (the timed region and the PCIe pass rotate over the streams, and
+    the PCIe pass's first dispatch may extend the run)."""
     import importlib.util
     import os
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
