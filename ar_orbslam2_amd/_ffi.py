@@ -106,38 +106,53 @@ class ProjLast(C.Structure):
 _lib = None
 
 
+# the options __graft_entry__.build() compiles with (csrc/Makefile BUILDFLAGS)
+DEFAULT_BUILDFLAGS = "ARCH=gfx950 EXTRA="
+
+
 def source_hash():
-    """(sha256 of the sources in liborbx.srclist order, the hash the build recorded)."""
+    """(sha256 of the sources in liborbx.srclist order and of the build-option line, the hash
+    the build recorded, that option line); (None, None, None) if any of them cannot be read."""
     import hashlib
     lib_dir = os.path.dirname(LIB_PATH)
     csrc = os.path.join(_HERE, "csrc")
     try:
         names = open(os.path.join(lib_dir, "liborbx.srclist")).read().split()
         built = open(os.path.join(lib_dir, "liborbx.srchash")).read().strip()
+        flags_path = os.path.join(lib_dir, "liborbx.buildflags")
+        h = hashlib.sha256()
+        for n in names:
+            with open(os.path.join(csrc, n), "rb") as f:
+                h.update(f.read())
+        with open(flags_path, "rb") as f:
+            flags = f.read()
+        h.update(flags)
     except OSError:
-        return None, None
-    h = hashlib.sha256()
-    for n in names:
-        with open(os.path.join(csrc, n), "rb") as f:
-            h.update(f.read())
-    return h.hexdigest(), built
+        return None, None, None
+    return h.hexdigest(), built, flags.decode(errors="replace").strip()
 
 
 def lib():
-    """Load liborbx.so; raises if the HIP library has not been built (no fallback) or was built
-    from other sources than the ones in the tree (Makefile's liborbx.srchash)."""
+    """Load liborbx.so; raises ImportError if the HIP library has not been built (no fallback),
+    was built from other sources than the ones in the tree (Makefile's liborbx.srchash), or with
+    other options than the default build (set ORBX_ALLOW_CUSTOM_BUILD=1 for experiments)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; "
                 "g.build()'` (hipcc, gfx950). There is no CPU fallback.")
-        now, built = source_hash()
+        now, built, flags = source_hash()
         if now is None or now != built:
             raise ImportError(
-                f"{LIB_PATH} is stale: it was built from other sources than "
-                f"ar_orbslam2_amd/csrc (hash {built} vs {now}); rebuild with "
+                f"{LIB_PATH} is stale or its sources are missing: it was built from other "
+                f"sources than ar_orbslam2_amd/csrc (hash {built} vs {now}); rebuild with "
                 "`python -c 'import __graft_entry__ as g; g.build()'`.")
+        if flags != DEFAULT_BUILDFLAGS and not os.environ.get("ORBX_ALLOW_CUSTOM_BUILD"):
+            raise ImportError(
+                f"{LIB_PATH} was built with non-default options ({flags!r}, default "
+                f"{DEFAULT_BUILDFLAGS!r}); rebuild with __graft_entry__.build() or set "
+                "ORBX_ALLOW_CUSTOM_BUILD=1.")
         _lib = C.CDLL(LIB_PATH)
         _lib.orbx_plan_stream.restype = C.c_void_p
         _lib.orbx_frames_stream.restype = C.c_void_p

@@ -109,7 +109,10 @@ __global__ __launch_bounds__(256) void k_cvfast(const uint8_t* __restrict__ pyr,
   constexpr int kRowB = kInD * 4;         // staged row stride (bytes)
   constexpr int kWinR = kTH + 2;          // V rows Y0-1 .. Y0+kTH
   constexpr int kVS = kTW + 8;            // V row stride: columns X0-4 .. X0+67
-  constexpr int kQ = (kWinR + 3) / 4 * 64 + 64;  // per-wave queue bound (rows + ring pass)
+  // per-wave queue bound: wave w pretests the row pairs starting at 2w mod 8, i.e. at most
+  // ceil(kWinR / 8) pairs = 2 * ceil(kWinR / 8) full rows, and wave 0 also takes one ring
+  // pass of 64 pixels (waves 1 and 2 take the rest of the ring, fewer rows)
+  constexpr int kQ = 2 * ((kWinR + 7) / 8) * 64 + 64;
   __shared__ __align__(16) uint32_t s_in[kInR][kInD];
   __shared__ __align__(16) uint32_t s_v32[kWinR * kVS / 4];
   __shared__ uint16_t s_q[4][kQ + 64];

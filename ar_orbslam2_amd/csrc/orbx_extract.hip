@@ -523,7 +523,10 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
   constexpr int kGroups = kWinR * kWinG;
   constexpr int kRowB = kInD * 4;         // staged row stride (bytes)
   constexpr int kCS = 1;                  // bytes per staged column
-  constexpr int kQ = (kWinR + 3) / 4 * 64 + 64;  // per-wave queue bound (rows + ring pass)
+  // per-wave queue bound: wave w pretests the row pairs starting at 2w mod 8, i.e. at most
+  // ceil(kWinR / 8) pairs = 2 * ceil(kWinR / 8) full rows, and wave 0 also takes one ring
+  // pass of 64 pixels (waves 1 and 2 take the rest of the ring, fewer rows)
+  constexpr int kQ = 2 * ((kWinR + 7) / 8) * 64 + 64;
   __shared__ __align__(16) uint32_t s_in[kInR * kRowB / 4];
   __shared__ __align__(16) uint32_t s_v32[kWinR * kWinG];
   __shared__ uint16_t s_q[4][kQ + 64];

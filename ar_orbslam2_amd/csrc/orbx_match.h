@@ -90,6 +90,10 @@ constexpr int ORBX_DEVERR_INDEX = 2;
 // candidates per vocabulary node whose vbMatched2 flags k_bow_nodes keeps in a per-lane register
 // bitmap (64 chunks of 64); larger nodes keep them in global memory
 constexpr int kBowRegCands = 64 * 64;
+// SearchByBoW's wave merge packs (best distance, node position) into 32 bits: side 2 of a
+// problem holds fewer than 2^23 features (the entry points reject more)
+constexpr int kBowMaxSide2 = 1 << 23;
+constexpr int kBowPosMask = kBowMaxSide2 - 1;
 
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
 int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);

@@ -149,14 +149,16 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
         }
       }
       // wave merge of (best1, position, best2), what the sequential loop yields: the minimum
-      // of the key (best1 << 16 | position) is best1 at its first position; best2 is then the
-      // minimum over the lanes of best1, except the winning lane, which offers its own best2
+      // of the key (best1 << 23 | position) is best1 at its first position; best2 is then the
+      // minimum over the lanes of best1, except the winning lane, which offers its own best2.
+      // best1 <= 256 takes 9 bits, a position < kBowMaxSide2 the other 23 (the host entry
+      // points reject larger sides; a lane without a candidate offers position 0x7FFFFF)
       {
-        const uint32_t key = ((uint32_t)b1 << 16) | (uint32_t)min(bp, 0xFFFF);
+        const uint32_t key = ((uint32_t)b1 << 23) | (uint32_t)min(bp, kBowPosMask);
         const uint32_t K = wave_min_u32(key);
         const int B2 = (int)wave_min_u32(key == K ? (uint32_t)b2 : (uint32_t)b1);
-        b1 = (int)(K >> 16);
-        bp = (int)(K & 0xFFFFu);
+        b1 = (int)(K >> 23);
+        bp = (int)(K & (uint32_t)kBowPosMask);
         b2 = B2;
       }
       const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
@@ -610,6 +612,7 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
             int mode, int32_t* match_out, int32_t* nmatches) {
   if (!side_ok(s1) || !side_ok(s2) || !match_out || !nmatches) return ORBX_EINVAL;
   if (!fv_ok(s1->fv, s1->n) || !fv_ok(s2->fv, s2->n)) return ORBX_EINVAL;
+  if (s2->n >= kBowMaxSide2) return report(ORBX_EUNSUPPORTED, "SearchByBoW: side 2 above 2^23 features");
   const int nout = mode == 1 ? s1->n : s2->n;
   Stager st;
   SideOffs o1 = stage_side(st, s1), o2 = stage_side(st, s2);

@@ -80,3 +80,14 @@ def stereo_pair(w, h, t=0, stream=0, disparity=(12, 20), base=None):
         noisy = img + rng.normal(0.0, 4.0, img.shape)
         out.append(np.clip(np.rint(noisy), 0, 255).astype(np.uint8))
     return out[0], out[1]
+
+
+# a 4 x 4 tile on which every pixel passes FAST's even-point pretest at threshold 20 (found by a
+# search over three-level tiles): the worst case for the FAST kernels' candidate queues
+DENSE_CORNER_TILE = np.array([[254, 0, 0, 254], [0, 254, 254, 127], [254, 0, 127, 254],
+                              [0, 254, 254, 127]], np.uint8)
+
+
+def dense_corners(w, h):
+    """A w x h frame tiled with DENSE_CORNER_TILE (every pixel a FAST pretest candidate)."""
+    return np.tile(DENSE_CORNER_TILE, (h // 4 + 1, w // 4 + 1))[:h, :w].copy()

@@ -698,7 +698,7 @@ def run_marker(args, cfg, rank, world, local, streams, dist):
     if (kp_counts < 0).any():
         raise RuntimeError("a frame overflowed the per-level keypoint capacity")
     elapsed = aggregate_elapsed(elapsed, world)
-    n_streams = args.streams_total or world * S
+    n_streams = sum(len(x) for x in gather_streams(list(streams), world))
     value = n_streams * B * args.steps / elapsed
     levels = cvorb_level_sizes(cvorb_params(nf), w, h)
     n_kp = int(kp_counts.sum())
@@ -725,49 +725,88 @@ def run_marker(args, cfg, rank, world, local, streams, dist):
     return out, target_desc
 
 
-def run_frames(args, cfg, rank, world, local, streams, dist):
+def _gen_pool(fn, n, threads=16):
+    """n synthetic frames fn(i) in order; numpy's generators and ufuncs release the GIL, so a
+    thread pool spreads the host-side generation over the job's CPU share."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max(1, min(threads, n))) as ex:
+        return list(ex.map(fn, range(n)))
+
+
+def make_frame_pipes(args, cfg, streams, local):
+    """The timed topology of run_frames: one FramePipeline (own HIP stream, captured hipGraphs)
+    per camera stream with SURVEY §8d's seeded masks and matcher settings, and `args.pool`
+    distinct batches of B frames of that stream resident in HBM.  Returns (pipes, pools,
+    pools_host): pools[s][k] is a device tensor, pools_host[s] the pinned copies of the first
+    two batches for the PCIe leg (None without --upload).  Each pipe carries `masks` (valid,
+    has_mp) and `epipole`.  tests/test_pipeline_gpu.py builds the same topology through this
+    function and checks its outputs against the oracle."""
     import torch
-    from ar_orbslam2_amd import ORBextractor, Vocabulary, epipole, synth
+    from ar_orbslam2_amd import Vocabulary, epipole, synth
     from ar_orbslam2_amd.pipeline import TUM1_K, FramePipeline, fundamental_from_pose
 
     w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
     voc = Vocabulary.synthetic(device=local)
-    S = len(streams)
     ex, ey = epipole(np.eye(3), [0.10, 0.02, 0.05], [0, 0, 0], *TUM1_K)
     pipes, pools, pools_host = [], [], []
     stereo = None
     if cfg.get("stereo"):
         from ar_orbslam2_amd.stereo import stereo_params
         stereo = stereo_params(*cfg["stereo"])
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
     for stream_id in streams:
         pipe = FramePipeline(w, h, B, voc, nf, device=local, stereo=stereo)
-        pipe.seeded_masks(range(B))
+        pipe.masks = pipe.seeded_masks(range(B))
+        pipe.epipole = (ex, ey)
         pipe.set_matching(fundamental_from_pose(), (ex, ey), bow_ratio=0.7, bow_check_ori=True,
                           tri_ratio=0.6, tri_check_ori=False)
         # synthetic frames of this camera stream, resident in HBM before timing
         host = []
         if stereo:
-            pairs = [synth.stereo_pair(w, h, t, stream_id) for t in range(min(B, 32))]
+            pairs = _gen_pool(lambda t: synth.stereo_pair(w, h, t, stream_id), min(B, 32), threads)
             for pi in range(args.pool):  # interleaved (left, right) images
                 host.append(np.stack([im for i in range(B) for im in pairs[(pi * 7 + i) % len(pairs)]]))
         else:
             base = synth.canvas(w, h, stream=stream_id)
+            allf = _gen_pool(lambda i: synth.frame(w, h, i, stream_id, base), args.pool * B, threads)
             for pi in range(args.pool):
-                host.append(np.stack([synth.frame(w, h, pi * B + i, stream_id, base) for i in range(B)]))
+                host.append(np.stack(allf[pi * B:(pi + 1) * B]))
+            del allf
         pools.append([torch.from_numpy(fr).cuda() for fr in host])
         pools_host.append([torch.from_numpy(fr).reshape(-1).pin_memory() for fr in host[:2]]
                           if args.upload else None)
         pipes.append(pipe)
-    pipe = pipes[0]
     torch.cuda.synchronize()
+    return pipes, pools, pools_host
+
+
+def replay_step(pipes, pools, B, i):
+    """One step of the timed region: every camera stream enqueues batch i mod pool (its
+    captured hipGraph for that input, replayed asynchronously on the pipeline's stream)."""
+    for p, pool in zip(pipes, pools):
+        p.run(pool[i % len(pool)].data_ptr(), B)
+
+
+def run_frames(args, cfg, rank, world, local, streams, dist):
+    import torch
+    from ar_orbslam2_amd import ORBextractor
+
+    w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
+    stereo = cfg.get("stereo")
+    S = len(streams)
+    pipes, pools, pools_host = make_frame_pipes(args, cfg, streams, local)
+    pipe = pipes[0]
 
     def barrier():
         if dist:
             dist.barrier()
 
+    # setup: one run per resident batch captures every (input, batch) hipGraph before the
+    # warm-up, so no capture lands in the timed region when the pool is larger than W
+    for i in range(len(pools[0])):
+        replay_step(pipes, pools, B, i)
     for i in range(args.warmup):
-        for p, pool in zip(pipes, pools):
-            p.run(pool[i % len(pool)].data_ptr(), B)
+        replay_step(pipes, pools, B, i)
     for p in pipes:
         p.sync()
         if p.results(B)[3]:
@@ -778,13 +817,15 @@ def run_frames(args, cfg, rank, world, local, streams, dist):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        for p, pool in zip(pipes, pools):
-            p.run(pool[i % len(pool)].data_ptr(), B)
+        replay_step(pipes, pools, B, i)
     for p in pipes:
         p.sync()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    for si, p in enumerate(pipes):
+        if p.results(B)[3]:
+            raise RuntimeError(f"camera stream {streams[si]}: device error {p.results(B)[3]}")
     # roofline pass (after timing): stream 0 alone with HIP events around every kernel on the
     # stream it launches on, so a kernel's event interval is its own duration (as rocprofv3
     # reports it) rather than a share of the concurrent streams
@@ -805,8 +846,12 @@ def run_frames(args, cfg, rank, world, local, streams, dist):
         upload = upload_pass(pipes, pools_host, B, args.steps, torch)
 
     elapsed = aggregate_elapsed(elapsed, world)
-    n_streams = args.streams_total or world * S
-    value = n_streams * B * args.steps / elapsed
+    # every rank's camera streams (stream s on rank s mod G); the job's frames are
+    # the sum over the ranks' streams
+    all_streams = gather_streams(list(streams), world)
+    n_streams = sum(len(x) for x in all_streams)
+    frames_total = n_streams * B * args.steps
+    value = frames_total / elapsed
     ex_tables = ORBextractor(nf, device=local)
     levels = level_sizes(w, h, ex_tables.GetInverseScaleFactors())
     n_kp = int(kp_counts.sum())
@@ -826,10 +871,14 @@ def run_frames(args, cfg, rank, world, local, streams, dist):
                    "nfeatures": nf, "nlevels": 8, "scale_factor": 1.2,
                    "parallelism": f"{world} GPU(s), camera stream s on GPU s mod {world}, "
                                   f"no collective",
+                   "streams_per_rank": all_streams, "frames_total": frames_total,
+                   "dist_backend": args.dist_backend if world > 1 else None,
+                   "same_device": bool(args.same_device),
                    "keypoints_per_frame": round(n_kp / B, 1),
                    "bow_matches_per_frame": round(float(bow.mean()), 1),
                    "triangulation_matches_per_frame": round(float(tri.mean()), 1),
-                   "timing": "hipGraph replay; per-kernel HIP events only in the roofline pass"},
+                   "timing": "hipGraph replay (every pool batch's graph captured in setup, "
+                             "before the warm-up); per-kernel HIP events only in the roofline pass"},
         "roofline": roofline,
     }
     if upload:
@@ -911,6 +960,12 @@ def parse_args(argv=None):
     ap.add_argument("--streams-total", type=int, default=None,
                     help="strong scaling: the job's camera-stream count, fixed over the GPUs "
                          "(stream s on GPU s mod G); e.g. C5's 8 streams")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for the barrier and the max-over-ranks time "
+                         "(nccl = RCCL; no data-path collective either way)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank uses device 0: rehearses the N>1 path on a one-GPU box "
+                         "(with --dist-backend gloo; RCCL refuses two ranks on one GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + sharding + aggregation only, no device work (gloo)")
     ap.add_argument("--upload", dest="upload", action="store_true", default=True,
@@ -953,7 +1008,9 @@ def main(argv=None):
         sys.exit(spawn_ranks(args.gpus, argv))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", str(rank)))
+    if args.same_device and args.dist_backend == "nccl" and world > 1:
+        raise SystemExit("--same-device needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
     if args.streams_total is not None and args.streams_total < world:
         raise SystemExit(f"--streams-total {args.streams_total} < {world} GPUs")
     streams = streams_of_rank(rank, world, args.streams, args.streams_total)
@@ -973,7 +1030,7 @@ def main(argv=None):
             cfg, args.cpu_seconds, args.cpu_mp_seconds)
     import torch
     torch.cuda.set_device(local)
-    dist = init_dist(rank, world, local, "nccl")
+    dist = init_dist(rank, world, local, args.dist_backend)
     if cfg.get("marker"):
         out, _ = run_marker(args, cfg, rank, world, local, streams, dist)
     else:

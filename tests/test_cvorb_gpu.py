@@ -93,6 +93,14 @@ def test_noise_many_candidates():
     _compare(img, nfeatures=5000, scoreType=M.FAST_SCORE)
 
 
+def test_dense_corner_pattern_fills_pretest_queues():
+    # every level-0 pixel passes the even-point pretest at 20 (tests/test_extract_gpu.py): the
+    # per-wave candidate queues of k_cvfast run full
+    img = synth.dense_corners(640, 480)
+    _compare(img)
+    _compare(img, scoreType=M.FAST_SCORE)
+
+
 def test_small_and_degenerate():
     assert _compare(np.zeros((0, 0), np.uint8)) == (None, None)
     kps, desc = _compare(np.full((200, 200), 77, np.uint8))

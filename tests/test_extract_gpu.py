@@ -155,3 +155,15 @@ def test_blur_every_pixel_matches_oracle(w, h, kind):
         ref = O.gaussian7(lv)
         bad = np.argwhere(got != ref)
         assert bad.size == 0, f"level {l} ({lv.shape}): {len(bad)} blurred px differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("w,h", [(640, 480), (1241, 376)])
+def test_dense_corner_pattern_fills_pretest_queues(w, h):
+    """Every level-0 pixel of the detection region is a pretest candidate, so each wave of
+    k_fast_tile enqueues every pixel of its rows plus its ring share: the per-wave queue bound
+    must hold that (the row-pair schedule puts 18 rows + 64 ring pixels on wave 0)."""
+    img = synth.dense_corners(w, h)
+    _compare(img, 1000)
+    # the same texture on half the frame next to a flat region (fallback cells beside full ones)
+    img[:, : w // 2] = 128
+    _compare(img, 1000)

@@ -236,3 +236,90 @@ def test_batch_keypoints_every_frame(w, h, nf, n):
         assert np.array_equal(kps_all[f, :k], kps), f
         assert np.array_equal(desc_all[f, :k], desc), f
     pipe.close()
+
+
+def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc):
+    """Frames `which` of the pipeline's last batch (host copy `frames`, n frames) against the
+    oracle: keypoints, descriptors, node / word ids, BowVector (f64 bits), SearchByBoW matches
+    and SearchForTriangulation pairs (frame f against (f - 1) mod n)."""
+    h, w = frames.shape[1:]
+    valid, has_mp = pipe.masks
+    ex, ey = pipe.epipole
+    F = fundamental_from_pose()
+    counts, bow, tri, err = pipe.results(n)
+    assert err == 0
+    cap = pipe.kp_cap
+    out, bo = pipe.device_outputs(), pipe.bow_outputs()
+    kps_all = d2h(out["kps"], n * cap * 28).view(KEYPOINT_DTYPE).reshape(n, cap)
+    desc_all = d2h(out["desc"], n * cap * 32).reshape(n, cap, 32)
+    nodes_all = d2h(out["node_of"], n * cap * 4).view(np.uint32).reshape(n, cap)
+    words_all = d2h(bo["bow_words"], n * cap * 4).view(np.uint32).reshape(n, cap)
+    vals_all = d2h(bo["bow_values"], n * cap * 8).view(np.float64).reshape(n, cap)
+    nw_all = d2h(bo["bow_n"], n * 4).view(np.int32)
+    word_of_all = d2h(bo["word_of"], n * cap * 4).view(np.uint32).reshape(n, cap)
+    match_all = d2h(out["bow_match"], n * cap * 4).view(np.int32).reshape(n, cap)
+    pairs_all = d2h(out["tri_pairs"], n * cap * 8).view(np.int32).reshape(n, cap, 2)
+    t = O.tables(O.params(nf), w, h)
+    ref = {}
+    for f in sorted(set(which) | {(f - 1) % n for f in which}):
+        kps, desc = O.extract(frames[f], O.params(nf))
+        k = len(kps)
+        assert counts[f] == k, f
+        assert np.array_equal(kps_all[f, :k], kps), f
+        assert np.array_equal(desc_all[f, :k], desc), f
+        r = oracle_voc.transform(desc, 4)
+        assert np.array_equal(nodes_all[f, :k], r["node_of"]), f
+        assert np.array_equal(word_of_all[f, :k], r["word_of"]), f
+        assert nw_all[f] == len(r["bow_words"]), f
+        assert np.array_equal(words_all[f, :nw_all[f]], r["bow_words"]), f
+        assert vals_all[f, :nw_all[f]].tobytes() == r["bow_values"].tobytes(), f
+        ref[f] = dict(desc=desc, angle=kps["angle"], keys=kps, fv=featvec(r["node_of"]),
+                      valid=valid[f, :k], has_mp=has_mp[f, :k], scale_factors=t["scale"],
+                      level_sigma2=t["sigma2"])
+    for f in which:
+        kf, cur = ref[(f - 1) % n], ref[f]
+        nb, mb = O.search_by_bow_kf_f(kf, dict(cur, valid=None), 0.7, True)
+        assert bow[f] == nb, f
+        assert np.array_equal(match_all[f, :len(cur["desc"])], mb), f
+        nt, pt = O.search_for_triangulation(kf, cur, F, ex, ey, False, 0.6, False)
+        assert tri[f] == nt, f
+        assert np.array_equal(pairs_all[f, :nt], pt), f
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("config,argv", [
+    ("C2", []),                                                  # 3 streams x 512, pool 4
+    ("C5", ["--streams-total", "8", "--pool", "2"]),             # 8 streams x 256 on one GPU
+])
+def test_bench_timed_topology_matches_oracle(config, argv):
+    """bench.py's timed configuration, built by bench's own make_frame_pipes / replay_step: the
+    headline C2 (three camera streams of 512 frames, a pool of 4 resident batches, every
+    stream's captured hipGraphs replayed interleaved across the three HIP streams) and C5's
+    single-GPU strong-scaling shape (8 streams of 256 frames).  After the setup captures, the
+    warm-up and 12 interleaved steps (the compared batch's graph has run 3 times), frames
+    {0, 1, 2, 254, 255, 256, 510, 511} (C5: {0, 1, 2, 127, 128, 254, 255}) of every stream equal
+    the oracle: keypoints, descriptors, BoW, SearchByBoW, SearchForTriangulation."""
+    import bench
+    args = bench.parse_args(["--config", config, "--no-upload", "--no-cpu-baseline"] + argv)
+    cfg = bench.CONFIGS[config]
+    streams = bench.streams_of_rank(0, 1, args.streams, args.streams_total)
+    B = args.batch
+    pipes, pools, _ = bench.make_frame_pipes(args, cfg, streams, 0)
+    steps = 12
+    for i in range(len(pools[0])):
+        bench.replay_step(pipes, pools, B, i)
+    for i in range(args.warmup):
+        bench.replay_step(pipes, pools, B, i)
+    for i in range(steps):
+        bench.replay_step(pipes, pools, B, i)
+    for p in pipes:
+        p.sync()
+    last = (steps - 1) % len(pools[0])
+    which = ([0, 1, 2, 254, 255, 256, 510, 511] if B == 512 else
+             [0, 1, 2, B // 2 - 1, B // 2, B - 2, B - 1])
+    _, oracle_voc = _vocabs()
+    for p, pool in zip(pipes, pools):
+        frames = pool[last].cpu().numpy()
+        _check_pipe_frames(p, frames, which, cfg["nfeatures"], B, oracle_voc)
+    for p in pipes:
+        p.close()
