@@ -28,6 +28,7 @@ EXPORTS = [
     "orbx_plan_profile", "orbx_plan_profile_read", "orbx_descriptor_distance",
     "orbx_search_by_bow_kf_f", "orbx_search_by_bow_kf_kf", "orbx_search_for_triangulation",
     "orbx_epipole", "orbx_search_by_projection", "orbx_search_by_projection_last",
+    "orbx_search_for_initialization", "orbx_fuse", "orbx_fuse_sim3",
     "orbx_stereo_matches", "orbx_vocabulary_load_text", "orbx_vocabulary_create",
     "orbx_vocabulary_destroy", "orbx_vocabulary_info", "orbx_vocabulary_transform",
     "orbx_frames_create", "orbx_frames_create_stereo", "orbx_frames_destroy",
@@ -97,6 +98,11 @@ class ProjPoints(C.Structure):
                 ("view_cos", C.c_void_p), ("desc", C.c_void_p)]
 
 
+class FusePoints(C.Structure):
+    _fields_ = [("n", C.c_int32), ("use", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
+                ("ur", C.c_void_p), ("pred_level", C.c_void_p), ("desc", C.c_void_p)]
+
+
 class ProjLast(C.Structure):
     _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
                 ("ur", C.c_void_p), ("octave", C.c_void_p), ("angle", C.c_void_p),
@@ -107,7 +113,7 @@ _lib = None
 
 
 # the options __graft_entry__.build() compiles with (csrc/Makefile BUILDFLAGS)
-DEFAULT_BUILDFLAGS = "ARCH=gfx950 EXTRA="
+DEFAULT_BUILDFLAGS = "ARCH=gfx950:sramecc+ EXTRA="
 
 
 def source_hash():

@@ -963,6 +963,144 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
   }
 }
 
+// ---- k_fast_cells: the whole per-cell FAST of ComputeKeyPointsOctTree (ORBextractor.cc:758-796)
+// in one wave per cell: the cell ROI is staged in the wave's LDS once; cv::FAST with NMS at
+// iniThFAST (:776-780) and, only if no keypoint survives, again at minThFAST on the same staged
+// pixels (:782-784); the survivors go to the cell's candidate slot in raster order.  FAST on the
+// cell ROI makes the NMS cell-local, so nothing outside the cell's detection pixels is scored,
+// and no score map or keep bitmap leaves the wave.
+//  (1) cardinal pretest (fast_cardinal2) on row pairs: lanes are columns (two half-waves of
+//      two rows each when the cell is at most 32 wide); each lane shifts its flag pair into a
+//      register, 8 steps at a time, and the wave compacts the flagged pixels into a queue
+//      (lane prefix sum, then each lane writes its own);
+//  (2) cornerScore<16> (fast_score) of the queued pixels into a zero-ringed V map (V = score + 1
+//      clamped; every other pixel has V = 0, equivalent in the NMS to a score below t);
+//  (3) the strict 8-neighbour NMS at the queued pixels with V > t, setting keep bits per row.
+// Instantiated for RS x MAXR staged windows as k_fast_fallback: <44, 44> (cells up to 38 wide /
+// high) and <72, 66> (any cell); `list` holds the instance's cells.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int RS, int MAXR>
+__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr,
+                                                    int64_t pyr_bytes,
+                                                    const CellGeom* __restrict__ cells,
+                                                    const int* __restrict__ list, int nlist,
+                                                    int ncells, int ini_th, int min_th,
+                                                    uint32_t* __restrict__ cand, int cand_total,
+                                                    int* __restrict__ cell_counts) {
+  // staged ROI (+ 4 rows the last pair step of a half-wave may read past it, masked)
+  __shared__ __align__(16) uint8_t s_src[4][(MAXR + 4) * RS];
+  __shared__ __align__(16) uint8_t s_vv[4][(MAXR - 4) * RS];
+  constexpr int QCAP = (MAXR - 6) * (RS - 9);  // detection pixels of the largest cell
+  __shared__ uint16_t s_q[4][QCAP];
+  __shared__ uint64_t s_rows[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bx, img;
+  xcd_block(bx, img);
+  const int li = bx * 4 + wid;
+  if (li >= nlist) return;  // wave-uniform; no workgroup barrier below
+  const int ci = list[li];
+  const CellGeom C = cells[ci];
+  uint8_t* S = s_src[wid];
+  uint8_t* V = s_vv[wid];
+  uint16_t* q = s_q[wid];
+  const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3
+  const int dr = rows - 6, cw = cols - 6;            // detection rows / columns
+  int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
+  if (dr <= 0 || cw <= 0) {
+    if (lane == 0) *cnt_out = 0;
+    return;
+  }
+  // the ROI as aligned dwords (its first pixel lands at byte sh of each staged row): lane l
+  // takes word l % kW of rows l / kW + kG u, all kPf loads in flight before the LDS stores
+  {
+    constexpr int kW = RS / 4, kG = 64 / kW, kPf = (MAXR + kG - 1) / kG;
+    const int lrow = lane / kW, lword = lane - lrow * kW;
+    const int words = ((C.x0 & 3) + cols + 3) >> 2;
+    const uint8_t* srow = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - 3 * C.pitch - 3) +
+                          (C.x0 & ~3) - C.x0;  // staged row 0, word 0
+    const bool ok = lrow < kG && lword < words;
+    uint32_t pv[kPf];
+#pragma unroll
+    for (int u = 0; u < kPf; u++) {
+      const int r = lrow + kG * u;
+      pv[u] = (ok && r < rows) ? *(const uint32_t*)(srow + (uint32_t)__mul24(r, C.pitch) + 4 * lword)
+                               : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kPf; u++) {
+      const int r = lrow + kG * u;
+      if (ok && r < rows) *(uint32_t*)(S + r * RS + 4 * lword) = pv[u];
+    }
+  }
+  for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
+  wave_sync();
+  const uint8_t* Sx = S + (C.x0 & 3);  // pixel (r, c) of the ROI at Sx[r * RS + c]
+  const bool half = cw <= 32;          // wave-uniform
+  const int col = half ? lane & 31 : lane, sub = half ? 2 * (lane >> 5) : 0, step = half ? 4 : 2;
+  const uint32_t fm = col < cw ? 0x80008000u : 0u;
+  int t = ini_th;
+  uint64_t bits = 0;  // this lane's keep row (lane = detection row)
+  for (int pass = 0; pass < 2; pass++) {
+    // (1) cardinal pretest at t, compacted into q (row << 6 | column)
+    int nq = 0;
+    for (int rc = 0; rc < dr; rc += 8 * step) {
+      const int nst = min(8, (dr - rc + step - 1) / step);  // wave-uniform
+      uint32_t acc = 0;  // step s's flags end at bits 15 - 2 (nst - 1 - s) and 31 - 2 (...)
+      for (int s = 0; s < nst; s++) {
+        const int r = rc + s * step + sub;
+        const uint32_t f = fast_cardinal2<RS>(Sx + r * RS + col, t) & fm &
+                           ((r < dr ? 0x8000u : 0u) | (r + 1 < dr ? 0x80000000u : 0u));
+        acc = (acc >> 2) | f;
+      }
+      const int cnt = __popc(acc);
+      const int incl = wave_scan_incl(cnt);
+      int pos = nq + incl - cnt;
+      nq += __builtin_amdgcn_readlane(incl, 63);
+      // bit b: step s = nst - 8 + (b & 15) / 2, row + 1 in the high half
+      const int rbase = rc + sub + step * (nst - 8);
+      while (acc) {
+        const int b = __builtin_ctz(acc);
+        acc &= acc - 1;
+        const int r = rbase + step * ((b & 15) >> 1) + (b >> 4);
+        q[pos++] = (uint16_t)((r << 6) | col);
+      }
+    }
+    wave_sync();
+    // (2) scores of the queued pixels (a fallback pass rescores the iniThFAST ones: same value)
+    for (int j = lane; j < nq; j += 64) {
+      const int e = q[j], r = e >> 6, c = e & 63;
+      const int sc = fast_score(Sx, RS, c + 3, r + 3);
+      V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
+    }
+    s_rows[wid][lane] = 0;
+    wave_sync();
+    // (3) NMS at t; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
+    const int t1 = max(t, 1);
+    for (int j = lane; j < nq; j += 64) {
+      const int e = q[j], r = e >> 6, c = e & 63;
+      const uint8_t* p = V + (r + 1) * RS + c + 1;
+      const int v = p[0];
+      if (v <= t1) continue;
+      const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
+                           max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
+      if (v > (nmax > t ? nmax : t1)) atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
+    }
+    wave_sync();
+    bits = lane < dr ? s_rows[wid][lane] : 0;
+    if (__ballot(bits != 0) != 0 || t == min_th) break;  // cell has keypoints, or retried
+    t = min_th;  // no keypoint at iniThFAST: FAST again at minThFAST (ORBextractor.cc:782-784)
+  }
+  const uint8_t* Vr = V + (lane + 1) * RS + 1;
+  compact_rows(bits, lane, C.y0 + 3 + lane, C.x0 + 3, cand + (int64_t)img * cand_total + C.slot_off,
+               cnt_out, [&](int kk) { return (int)Vr[kk]; });
+}
+
 // ------------------------------------------------------------------ k_octree
 // ORBextractor::DistributeOctTree (ORBextractor.cc:525-733) for one (image, level) per
 // workgroup.  The std::list is represented by node arrays kept in list order in LDS:
@@ -1630,6 +1768,10 @@ struct orbx_plan {
   int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;
   int cell_cap = 0;
   bool has_fb_big = false;  // some cell's ROI needs k_fast_fallback<72, kCellMax>
+  // k_fast_cells: the cells of its <44, 44> and <72, kCellMax> instances
+  int *d_cells_small = nullptr, *d_cells_big = nullptr;
+  int n_cells_small = 0, n_cells_big = 0;
+  bool fast_legacy = false;  // ORBX_FAST_LEGACY=1: k_fast_tile + k_fast_compact + k_fast_fallback
   bool fast_pair = true;  // k_fast_tile pretest on row pairs (ORBX_FAST_PAIR=0: one row per lane)
   const uint8_t* last_in = nullptr;
   int last_n = 0;
@@ -1743,7 +1885,8 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   const int st_pyr = pr.stage("k_pyramid"),
             st_blur = pr.stage("k_blur"), st_fs = pr.stage("k_fast_tile"),
             st_fast = pr.stage("k_fast_compact"), st_fb = pr.stage("k_fast_fallback"),
-            st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe");
+            st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe"),
+            st_fcell = pr.stage("k_fast_cells");
   pr.mark(P->stream, -1);
   for (const PyrStage& st : g.pyr_stages)
     hipLaunchKernelGGL(k_pyramid, dim3(st.nbands, n), dim3(kPyNT), st.smem, P->stream, d_in,
@@ -1756,7 +1899,19 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
     pr.mark(P->stream, st_blur);
   }
   const int ncells = (int)g.cells.size();
-  if (ncells > 0) {
+  if (ncells > 0 && !P->fast_legacy) {
+    if (P->n_cells_small > 0)
+      hipLaunchKernelGGL((k_fast_cells<44, 44>), dim3((P->n_cells_small + 3) / 4, n), dim3(256), 0,
+                         P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
+                         P->n_cells_small, ncells, g.ini_th, g.min_th, P->d_cand, g.cand_total,
+                         P->d_cell_counts);
+    if (P->n_cells_big > 0)
+      hipLaunchKernelGGL((k_fast_cells<72, kCellMax>), dim3((P->n_cells_big + 3) / 4, n), dim3(256),
+                         0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_big,
+                         P->n_cells_big, ncells, g.ini_th, g.min_th, P->d_cand, g.cand_total,
+                         P->d_cell_counts);
+    pr.mark(P->stream, st_fcell);
+  } else if (ncells > 0) {
     hipLaunchKernelGGL(P->fast_pair ? k_fast_tile<true> : k_fast_tile<false>, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
                        g.ini_th, P->d_fb_count);
@@ -1822,6 +1977,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->max_batch = max_batch;
   P->device = hip_device;
   if (const char* e = getenv("ORBX_FAST_PAIR")) P->fast_pair = atoi(e) != 0;
+  if (const char* e = getenv("ORBX_FAST_LEGACY")) P->fast_legacy = atoi(e) != 0;
   const Geometry& g = P->g;
   for (const CellGeom& c : g.cells) P->has_fb_big |= c.fb_big != 0;
   auto fail = [&](int code) {
@@ -1858,6 +2014,10 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   }
   P->nftiles = (int)ftiles.size();
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
+  std::vector<int> cells_small, cells_big;
+  for (int c = 0; c < (int)g.cells.size(); c++) (g.cells[c].fb_big ? cells_big : cells_small).push_back(c);
+  P->n_cells_small = (int)cells_small.size();
+  P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;
   if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, g.cells.size()) ||
       dalloc(&P->d_xtap, g.xtap.size() / 2) || dalloc(&P->d_ytap, g.ytap.size() / 2) ||
@@ -1867,7 +2027,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
       dalloc(&P->d_fb_count, 2 * kFbStride * B) || dalloc(&P->d_fb_list, 2 * B * g.cells.size()) ||
-      dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels))
+      dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels) ||
+      dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_big, cells_big.size()))
     return fail(ORBX_ENOMEM);
   {
     auto r256 = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1889,7 +2050,9 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       up(P->d_ytap, g.ytap.data(), 4 * g.ytap.size()) ||
       up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
       up(P->d_bands, g.bands.data(), sizeof(PyrBand) * g.bands.size()) ||
-      up(P->d_ftiles, ftiles.data(), sizeof(FastTile) * ftiles.size()))
+      up(P->d_ftiles, ftiles.data(), sizeof(FastTile) * ftiles.size()) ||
+      up(P->d_cells_small, cells_small.data(), 4 * cells_small.size()) ||
+      up(P->d_cells_big, cells_big.data(), 4 * cells_big.size()))
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
@@ -1936,7 +2099,8 @@ int orbx_plan_destroy(orbx_plan* P) {
   P->graphs.clear(P->stream);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xtap,   P->d_ytap,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label, P->d_fb_count, P->d_fb_list,
-                  P->d_ocount, P->d_counts /* base of kps and desc too */};
+                  P->d_ocount, P->d_cells_small, P->d_cells_big,
+                  P->d_counts /* base of kps and desc too */};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (P->stream) hipStreamDestroy(P->stream);

@@ -168,6 +168,60 @@ class ORBmatcher:
                                                        ptr(match), C.byref(nm)))
         return nm.value, match[:n].copy()
 
+    # -------------------------------------------------------------- monocular initialisation
+    def SearchForInitialization(self, F1, F2, vbPrevMatched, windowSize=10):
+        """ORBmatcher::SearchForInitialization (ORBmatcher.cc:405-523) on the GPU.
+
+        F1, F2: frames as for SearchByProjection (F1 needs only mvKeysUn and mDescriptors, F2
+        also its grid frame).  vbPrevMatched: float32 array (F1.N, 2), updated in place like the
+        reference's vector<cv::Point2f>&.  Returns (nmatches, vnMatches12)."""
+        f1, k1 = _proj_frame(F1, grid=False)
+        f2, k2 = _proj_frame(F2)
+        prev = vbPrevMatched
+        if not (isinstance(prev, np.ndarray) and prev.dtype == np.float32 and prev.flags.c_contiguous
+                and prev.shape == (f1.n, 2)):
+            raise ValueError("vbPrevMatched must be a C-contiguous float32 array of shape (N1, 2)")
+        m12 = np.zeros(max(f1.n, 1), np.int32)
+        nm = C.c_int32()
+        check("orbx_search_for_initialization",
+              lib().orbx_search_for_initialization(C.byref(f1), C.byref(f2), ptr(prev),
+                                                   C.c_int32(int(windowSize)),
+                                                   C.c_float(self.mfNNratio),
+                                                   C.c_int32(int(self.mbCheckOrientation)),
+                                                   ptr(m12), C.byref(nm)))
+        return nm.value, m12[:f1.n].copy()
+
+
+    # -------------------------------------------------------------- local mapping / loop closing
+    def Fuse(self, pKF, points, th=3.0, sim3=False):
+        """ORBmatcher::Fuse's per-point search on the GPU: Fuse(KeyFrame*, vector<MapPoint*>, th)
+        (ORBmatcher.cc:828-978) or, with sim3=True, Fuse(KeyFrame*, Scw, vpPoints, th,
+        vpReplacePoint) (:980-1103).
+
+        pKF: keyframe as for SearchByProjection's frame (mvKeysUn, mDescriptors, mvuRight, grid
+        frame, mvScaleFactors) plus mvInvLevelSigma2.  points: use, u, v, ur (not for sim3),
+        pred_level, desc — the caller's gates and projections (include/orbx.h).
+        Returns (nfused, best_idx, best_dist); the caller applies the replace / add-observation
+        step in point order as the reference does."""
+        kf, keep = _proj_frame(pKF)
+        spec = [("use", np.uint8), ("u", np.float32), ("v", np.float32), ("ur", np.float32),
+                ("pred_level", np.int32), ("desc", np.uint8)]
+        if sim3:
+            spec[3] = ("__none__", np.float32)
+        p, pk = _proj_struct(points, _ffi.FusePoints, spec)
+        bi = np.zeros(max(p.n, 1), np.int32)
+        bd = np.zeros(max(p.n, 1), np.int32)
+        nf = C.c_int32()
+        if sim3:
+            check("orbx_fuse_sim3",
+                  lib().orbx_fuse_sim3(C.byref(kf), C.byref(p), C.c_float(th), ptr(bi), ptr(bd),
+                                       C.byref(nf)))
+        else:
+            isg = np.ascontiguousarray(_get(pKF, "mvInvLevelSigma2", "inv_level_sigma2"), np.float32)
+            check("orbx_fuse",
+                  lib().orbx_fuse(C.byref(kf), ptr(isg), C.byref(p), C.c_float(th), ptr(bi), ptr(bd),
+                                  C.byref(nf)))
+        return nf.value, bi[:p.n].copy(), bd[:p.n].copy()
 
 
 def epipole(R2w, t2w, Cw, fx, fy, cx, cy):
@@ -188,9 +242,13 @@ def _get(obj, name, alt=None):
     return getattr(obj, alt, None) if v is None and alt else v
 
 
-def _proj_frame(F):
+def _proj_frame(F, grid=True):
     keys = np.ascontiguousarray(_get(F, "mvKeysUn", "keys_un"), KEYPOINT_DTYPE)
     desc = np.ascontiguousarray(_get(F, "mDescriptors", "desc"), np.uint8).reshape(-1, 32)
+    if not grid:  # only the keypoints and descriptors are read
+        s = _ffi.ProjFrame(len(keys), ptr(keys), ptr(desc), None, None, 0.0, 0.0, 0.0, 0.0, 0.0,
+                           0.0, None, 0)
+        return s, _Keep(keys=keys, desc=desc)
     ur = _get(F, "mvuRight", "u_right")
     ur = None if ur is None else np.ascontiguousarray(ur, np.float32)
     hm = _get(F, "has_mp_obs")

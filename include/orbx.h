@@ -217,6 +217,48 @@ int orbx_search_by_projection(const orbx_proj_frame* frame, const orbx_proj_poin
 int orbx_search_by_projection_last(const orbx_proj_frame* frame, const orbx_proj_last* last,
                                    float th, int32_t forward, int32_t backward,
                                    int32_t check_ori, int32_t* match, int32_t* nmatches);
+/* ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
+ * vector<int>& vnMatches12, int windowSize) (ORB_SLAM2/src/ORBmatcher.cc:405-523; called by
+ * Tracking::MonocularInitialization, Tracking.cc:953) of an ORBmatcher(nnratio, checkOri).
+ * f1 = the initial frame (n <= 65534, keys_un, desc; the rest unused), f2 = the current frame
+ * (keys_un, desc and its grid frame; u_right / has_mp_obs unused).  prev_matched: [f1->n][2]
+ * (x, y) = vbPrevMatched, updated in place as the reference updates it (:517-520);
+ * matches12[f1->n] = vnMatches12.  No limit on window size or feature density. */
+int orbx_search_for_initialization(const orbx_proj_frame* f1, const orbx_proj_frame* f2,
+                                   float* prev_matched, int32_t window_size, float nnratio,
+                                   int32_t check_ori, int32_t* matches12, int32_t* nmatches);
+
+/* ORBmatcher::Fuse, the per-point search of both overloads:
+ *   Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th)
+ *     (ORB_SLAM2/src/ORBmatcher.cc:828-978; LocalMapping::SearchInNeighbors, LocalMapping.cc:469,
+ *     495) -> orbx_fuse;
+ *   Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, float th,
+ *        vector<MapPoint*>& vpReplacePoint) (:980-1103; LoopClosing::SearchAndFuse) ->
+ *     orbx_fuse_sim3.
+ * kf = the keyframe: keys_un, desc, u_right (mvuRight; NULL = every entry -1), its grid frame
+ * (mnMinX.., mfGridElementWidthInv..) and mvScaleFactors.  Per point the caller evaluates the
+ * reference's gates before the search with its own cv::Mat code and passes use[i] = !isBad() &&
+ * not already in the keyframe && depth >= 0 && IsInImage(u, v) && minDistance <= dist3D <=
+ * maxDistance && PO.dot(Pn) >= 0.5 * dist3D (:849-888, :1008-1046), u, v (and ur = u - bf * invz,
+ * orbx_fuse only), pred_level = PredictScale(dist3D, mfLogScaleFactor) and the descriptor.
+ * The library runs KeyFrame::GetFeaturesInArea(u, v, th * mvScaleFactors[pred_level]), the
+ * level window, orbx_fuse's reprojection gates (inv_level_sigma2 = mvInvLevelSigma2) and the
+ * Hamming first minimum: best_idx[i] = bestIdx if bestDist <= TH_LOW else -1, best_dist[i] =
+ * bestDist (nullable).  *n_fused = points with best_idx >= 0.  The caller then applies the
+ * reference's replace / AddObservation step in point order (:954-974, :1084-1099), re-checking
+ * isBad() / IsInKeyFrame(pKF) at that point as the reference's loop does. */
+typedef struct {
+  int32_t n;
+  const uint8_t* use;
+  const float *u, *v, *ur;
+  const int32_t* pred_level;
+  const uint8_t* desc;         /* [n][32] */
+} orbx_fuse_points;
+int orbx_fuse(const orbx_proj_frame* kf, const float* inv_level_sigma2,
+              const orbx_fuse_points* points, float th, int32_t* best_idx, int32_t* best_dist,
+              int32_t* n_fused);
+int orbx_fuse_sim3(const orbx_proj_frame* kf, const orbx_fuse_points* points, float th,
+                   int32_t* best_idx, int32_t* best_dist, int32_t* n_fused);
 
 /* ------------------------------------------------------------------ stereo
  * Frame::ComputeStereoMatches (ORB_SLAM2/src/Frame.cc:471-643) on the last extraction of a

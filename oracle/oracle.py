@@ -460,6 +460,38 @@ def search_by_projection_last(f, last, th, forward, backward, check_ori):
     return n, match[:s.n].copy()
 
 
+def search_for_initialization(f1, f2, prev, nnratio, check_ori, window):
+    """ORBmatcher::SearchForInitialization (ORBmatcher.cc:405-523).  f1, f2: proj_frame dicts;
+    prev: (n1, 2) float32 vbPrevMatched.  Returns (nmatches, vnMatches12, updated prev)."""
+    s1, k1 = proj_frame(f1)
+    s2, k2 = proj_frame(f2)
+    pv = np.ascontiguousarray(prev, np.float32).reshape(-1, 2).copy()
+    m12 = np.zeros(max(s1.n, 1), np.int32)
+    n = lib().oracle_search_for_initialization(C.byref(s1), C.byref(s2), _p(pv), C.c_float(nnratio),
+                                               C.c_int(int(check_ori)), C.c_int(int(window)), _p(m12))
+    return n, m12[:s1.n].copy(), pv
+
+
+class FusePoints(C.Structure):
+    _fields_ = [("n", C.c_int32), ("use", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
+                ("ur", C.c_void_p), ("pred_level", C.c_void_p), ("desc", C.c_void_p)]
+
+
+def fuse(kf, inv_sigma2, pts, th, reproj=True):
+    """ORBmatcher::Fuse's per-point search (ORBmatcher.cc:828-978 / 980-1103).  Returns
+    (count, best_idx, best_dist)."""
+    s, keep = proj_frame(kf)
+    a = _arrs(pts, [("use", np.uint8), ("u", np.float32), ("v", np.float32), ("ur", np.float32),
+                    ("pred_level", np.int32), ("desc", np.uint8)])
+    p = FusePoints(len(a["use"]), *[_p(a[k]) for k in ("use", "u", "v", "ur", "pred_level", "desc")])
+    isg = np.ascontiguousarray(inv_sigma2, np.float32)
+    bi = np.zeros(max(p.n, 1), np.int32)
+    bd = np.zeros(max(p.n, 1), np.int32)
+    n = lib().oracle_fuse(C.byref(s), _p(isg), C.byref(p), C.c_float(th), C.c_int(int(reproj)),
+                          _p(bi), _p(bd))
+    return n, bi[:p.n].copy(), bd[:p.n].copy()
+
+
 # ---------------------------------------------------------------- AR marker path (cvorb_oracle.cc)
 DMATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
                          ("distance", "<f4")])

@@ -96,6 +96,11 @@ int oracle_search_by_projection(const orbx_proj_frame* F, const orbx_proj_points
                                 float nnratio, int32_t* match);
 int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_last* P, float th,
                                      int forward, int backward, int check_ori, int32_t* match);
+int oracle_search_for_initialization(const orbx_proj_frame* F1, const orbx_proj_frame* F2,
+                                     float* prev, float nnratio, int check_ori, int window,
+                                     int32_t* m12);
+int oracle_fuse(const orbx_proj_frame* KF, const float* inv_sigma2, const orbx_fuse_points* M,
+                float th, int reproj, int32_t* best_idx, int32_t* best_dist);
 
 /* AR marker path (cvorb_oracle.cc): cv::ORB 2.4 + BruteForceMatcher<HammingLUT> + the
  * Marker / AR-1.3 nearest-neighbour matchers */

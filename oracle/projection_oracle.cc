@@ -4,11 +4,17 @@
 //   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)   (ORBmatcher.cc:45-137)
 //   ORBmatcher::SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
 //                                                                          (ORBmatcher.cc:1331-1474)
+//   ORBmatcher::SearchForInitialization(Frame&, Frame&, vbPrevMatched, vnMatches12, windowSize)
+//                                                                          (ORBmatcher.cc:405-523)
+//   ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th)                     (ORBmatcher.cc:828-978)
+//   ORBmatcher::Fuse(KeyFrame*, Scw, vector<MapPoint*>, th, vpReplacePoint) (ORBmatcher.cc:980-1103)
+//   (the per-point search; KeyFrame::GetFeaturesInArea, KeyFrame.cc:518-558)
 // TEST INFRASTRUCTURE ONLY (see orb_oracle.h).  MapPoint state enters as plain arrays: the
 // caller evaluates mbTrackInView / isBad / the projections (Frame::isInFrustum, the pose
 // products) exactly as the reference does and passes the results; every MapPoint passed has
 // Observations() > 0, so a frame feature matched earlier in the same call is skipped by the
 // later ones, as in the reference.
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -231,6 +237,137 @@ int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_l
     }
   }
   return nmatches;
+}
+
+// SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize): prev[2 i1 .. 2 i1 + 1]
+// = vbPrevMatched[i1] (x, y), updated in place; m12[i1] = vnMatches12[i1].  Returns nmatches.
+// F1 uses n, keys_un, desc; F2 keys_un, desc and its grid frame.
+int oracle_search_for_initialization(const orbx_proj_frame* F1, const orbx_proj_frame* F2,
+                                     float* prev, float nnratio, int check_ori, int window,
+                                     int32_t* m12) {
+  Grid G;
+  assign_grid(F2, &G);
+  const int n1 = F1->n, n2 = F2->n;
+  int nmatches = 0;
+  for (int i = 0; i < n1; i++) m12[i] = -1;                     // :408
+  const int HISTO = 30;
+  std::vector<int> rotHist[30];                                  // :410-413
+  const float factor = 1.0f / HISTO;
+  std::vector<int> vMatchedDistance(n2, INT_MAX), vnMatches21(n2, -1);  // :415-416
+  const float r = (float)window;  // GetFeaturesInArea(const float& r) of the int windowSize
+  for (int i1 = 0; i1 < n1; i1++) {                              // :418-490
+    const orbx_keypoint& kp1 = F1->keys_un[i1];
+    const int level1 = kp1.octave;
+    if (level1 > 0) continue;
+    const std::vector<int> vIndices2 =
+        features_in_area(F2, G, prev[2 * i1], prev[2 * i1 + 1], r, level1, level1);
+    if (vIndices2.empty()) continue;
+    const uint8_t* d1 = F1->desc + (size_t)i1 * 32;
+    int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+    for (int i2 : vIndices2) {
+      const int dist = hamming(d1, F2->desc + (size_t)i2 * 32);
+      if (vMatchedDistance[i2] <= dist) continue;
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestIdx2 = i2;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= 50) {                                        // TH_LOW
+      if (bestDist < (float)bestDist2 * nnratio) {
+        if (vnMatches21[bestIdx2] >= 0) {
+          m12[vnMatches21[bestIdx2]] = -1;
+          nmatches--;
+        }
+        m12[i1] = bestIdx2;
+        vnMatches21[bestIdx2] = i1;
+        vMatchedDistance[bestIdx2] = bestDist;
+        nmatches++;
+        if (check_ori) {
+          float rot = F1->keys_un[i1].angle - F2->keys_un[bestIdx2].angle;
+          if (rot < 0.0) rot += 360.0f;
+          int bin = (int)std::round(rot * factor);
+          if (bin == HISTO) bin = 0;
+          rotHist[bin].push_back(i1);
+        }
+      }
+    }
+  }
+  if (check_ori) {                                               // :492-515
+    int hs[30];
+    for (int b = 0; b < HISTO; b++) hs[b] = (int)rotHist[b].size();
+    int ind1, ind2, ind3;
+    three_maxima(hs, HISTO, &ind1, &ind2, &ind3);
+    for (int b = 0; b < HISTO; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (int idx1 : rotHist[b])
+        if (m12[idx1] >= 0) {
+          m12[idx1] = -1;
+          nmatches--;
+        }
+    }
+  }
+  for (int i1 = 0; i1 < n1; i1++)                                // :517-520
+    if (m12[i1] >= 0) {
+      prev[2 * i1] = F2->keys_un[m12[i1]].x;
+      prev[2 * i1 + 1] = F2->keys_un[m12[i1]].y;
+    }
+  return nmatches;
+}
+
+// Fuse, both overloads: the per-point search (the caller evaluates the gates before it and
+// applies the replace / add-observation step after it).  reproj = 1: Fuse(KeyFrame*,
+// vector<MapPoint*>, th) with its reprojection gates, whose float expressions follow the
+// reference binary's contraction (e2 = fmaf(ex, ex, ey*ey), stereo fmaf(er, er, e2): RB
+// 0x7474c-0x74797, 0x7490b-0x74931); 0: the Sim3 overload.  best_idx[i] = bestIdx when
+// bestDist <= TH_LOW else -1, best_dist[i] = bestDist.  Returns the count of best_idx >= 0.
+int oracle_fuse(const orbx_proj_frame* KF, const float* inv_sigma2, const orbx_fuse_points* M,
+                float th, int reproj, int32_t* best_idx, int32_t* best_dist) {
+  Grid G;
+  assign_grid(KF, &G);
+  int nf = 0;
+  for (int i = 0; i < M->n; i++) {
+    const int none = reproj ? 256 : INT_MAX;  // :904, :1063
+    best_idx[i] = -1;
+    best_dist[i] = none;
+    if (!M->use[i]) continue;
+    const int nPredictedLevel = M->pred_level[i];
+    const float u = M->u[i], v = M->v[i];
+    const float radius = th * KF->scale_factors[nPredictedLevel];       // :893
+    const std::vector<int> vIndices = features_in_area(KF, G, u, v, radius, -1, -1);
+    if (vIndices.empty()) continue;
+    const uint8_t* dMP = M->desc + (size_t)i * 32;
+    int bestDist = none, bestIdx = -1;
+    for (int idx : vIndices) {
+      const orbx_keypoint& kp = KF->keys_un[idx];
+      const int kpLevel = kp.octave;
+      if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+      if (reproj) {
+        const float ex = u - kp.x, ey = v - kp.y;
+        if (KF->u_right && KF->u_right[idx] >= 0) {                    // :917-930
+          const float er = M->ur[i] - KF->u_right[idx];
+          const float e2 = std::fmaf(er, er, std::fmaf(ex, ex, ey * ey));
+          if (e2 * inv_sigma2[kpLevel] > 7.8) continue;
+        } else {                                                       // :931-941
+          const float e2 = std::fmaf(ex, ex, ey * ey);
+          if (e2 * inv_sigma2[kpLevel] > 5.99) continue;
+        }
+      }
+      const int dist = hamming(dMP, KF->desc + (size_t)idx * 32);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    best_dist[i] = bestDist;
+    if (bestDist <= 50) {                                              // TH_LOW
+      best_idx[i] = bestIdx;
+      nf++;
+    }
+  }
+  return nf;
 }
 
 }  // extern "C"

@@ -49,3 +49,48 @@ def scene(w=640, h=480, nf=1000, t=5, seed=0, stereo=False, mp_frac=0.1):
                 ur=(x - disp).astype(np.float32), octave=kp0["octave"].astype(np.int32),
                 angle=kp0["angle"].astype(np.float32), desc=desc)
     return F, pts, last
+
+
+def init_scene(w=640, h=480, nf=2000, t0=3, t1=6, jitter=0.0, seed=0):
+    """Monocular initialisation (Tracking::MonocularInitialization, Tracking.cc:922-960): the
+    initial frame and a later one from the 2*nFeatures initialisation extractor
+    (Tracking.cc:463-464), mvbPrevMatched = the initial keypoints' positions (:931),
+    optionally jittered as after earlier SearchForInitialization rounds."""
+    p = O.params(nf)
+    tb = O.tables(p, w, h)
+    base = synth.canvas(w, h, 4)
+    k1, d1 = O.extract(synth.frame(w, h, t0, 4, base), p)
+    k2, d2 = O.extract(synth.frame(w, h, t1, 4, base), p)
+    F1 = frame_dict(k1, d1, w, h, tb["scale"])
+    F2 = frame_dict(k2, d2, w, h, tb["scale"])
+    rng = np.random.default_rng(seed)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    if jitter:
+        prev = (prev + rng.normal(0, jitter, prev.shape)).astype(np.float32)
+    return F1, F2, prev
+
+
+def fuse_scene(w=640, h=480, nf=1000, t=5, seed=0, stereo=False, jitter=1.5):
+    """LocalMapping::SearchInNeighbors (LocalMapping.cc:469, 495) fusing map points into a
+    keyframe: the keyframe is frame t (oracle extraction, optional mvuRight), the points are
+    frame t-1's features carried to where they moved, with jittered projections (u, v, ur),
+    descriptors with a few bits flipped and a predicted level near their octave."""
+    F, _, _ = scene(w, h, nf, t, seed, stereo, mp_frac=0.0)
+    p = O.params(nf)
+    tb = O.tables(p, w, h)
+    base = synth.canvas(w, h, 2)
+    kp0, d0 = O.extract(synth.frame(w, h, t - 1, 2, base), p)
+    rng = np.random.default_rng(100 + seed)
+    n0 = len(kp0)
+    u = (kp0["x"] - 1 + rng.normal(0, jitter, n0)).astype(np.float32)
+    v = (kp0["y"] - 1 + rng.normal(0, jitter, n0)).astype(np.float32)
+    desc = d0.copy()
+    flips = rng.integers(0, 256, (n0, 8))
+    for k in range(8):
+        desc[np.arange(n0), flips[:, k] // 8] ^= (1 << (flips[:, k] % 8)).astype(np.uint8)
+    pts = dict(use=(rng.random(n0) < 0.9).astype(np.uint8), u=u, v=v,
+               ur=(u - rng.uniform(2, 30, n0)).astype(np.float32),
+               pred_level=np.clip(kp0["octave"] + rng.integers(-1, 2, n0), 0, 7).astype(np.int32),
+               desc=desc)
+    F["inv_level_sigma2"] = tb["inv_sigma2"]
+    return F, pts

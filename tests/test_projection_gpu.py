@@ -47,3 +47,70 @@ def test_projection_edge_cases():
     Lout = dict(L, u=L["u"] + 1000)
     n, _ = ORBmatcher(0.9).SearchByProjection(F, Lout, 7.0)
     assert n == 0
+
+
+@pytest.mark.parametrize("t1,jitter,nn,ori,window", [(6, 0.0, 0.9, True, 100), (4, 3.0, 0.9, True, 100),
+                                                     (9, 0.0, 0.7, False, 50), (5, 8.0, 1.0, True, 10)])
+def test_search_for_initialization(t1, jitter, nn, ori, window):
+    """SearchForInitialization (ORBmatcher.cc:405-523), as Tracking::MonocularInitialization
+    calls it (Tracking.cc:953: window 100, ORBmatcher(0.9, true)): vnMatches12, the count and the
+    updated vbPrevMatched equal the oracle's."""
+    from projdata import init_scene
+    F1, F2, prev = init_scene(t1=t1, jitter=jitter, seed=t1)
+    on, om, opv = O.search_for_initialization(F1, F2, prev, nn, ori, window)
+    pv = prev.copy()
+    n, m = ORBmatcher(nn, ori).SearchForInitialization(F1, F2, pv, window)
+    assert n == on and np.array_equal(m, om)
+    assert pv.tobytes() == opv.tobytes()
+    assert n > 100
+
+
+def test_search_for_initialization_edge_cases():
+    from projdata import init_scene
+    F1, F2, prev = init_scene()
+    # a window covering the whole frame: every level-0 feature of F2 (~430) is a candidate of
+    # each level-0 F1 feature, more than the candidate pool's first size (256 per point), so
+    # the call reruns with the pool sized to the total
+    assert (F2["keys_un"]["octave"] == 0).sum() > 300
+    sel = np.nonzero(F1["keys_un"]["octave"] == 0)[0][:20]
+    F1s = dict(F1, keys_un=F1["keys_un"][sel], desc=F1["desc"][sel])
+    p1 = prev[sel].copy()
+    on, om, opv = O.search_for_initialization(F1s, F2, p1, 0.9, True, 1000)
+    n, m = ORBmatcher(0.9, True).SearchForInitialization(F1s, F2, p1, 1000)
+    assert n == on and np.array_equal(m, om) and p1.tobytes() == opv.tobytes()
+    # empty frames
+    e1 = dict(F1, keys_un=F1["keys_un"][:0], desc=F1["desc"][:0])
+    n, m = ORBmatcher(0.9, True).SearchForInitialization(e1, F2, np.zeros((0, 2), np.float32), 100)
+    assert n == 0 and len(m) == 0
+    e2 = dict(F2, keys_un=F2["keys_un"][:0], desc=F2["desc"][:0])
+    pv = prev.copy()
+    n, m = ORBmatcher(0.9, True).SearchForInitialization(F1, e2, pv, 100)
+    assert n == 0 and (m == -1).all() and pv.tobytes() == prev.tobytes()
+
+
+@pytest.mark.parametrize("stereo,th,sim3,seed", [(False, 3.0, False, 0), (True, 3.0, False, 1),
+                                                 (True, 1.0, False, 2), (False, 10.0, True, 3),
+                                                 (True, 3.0, True, 4)])
+def test_fuse(stereo, th, sim3, seed):
+    """ORBmatcher::Fuse's per-point search, both overloads (ORBmatcher.cc:828-978, 980-1103):
+    best index and distance of every point equal the oracle's."""
+    from projdata import fuse_scene
+    K, P = fuse_scene(stereo=stereo, seed=seed)
+    on, obi, obd = O.fuse(K, K["inv_level_sigma2"], P, th, not sim3)
+    n, bi, bd = ORBmatcher(0.6, True).Fuse(K, P, th, sim3=sim3)
+    assert n == on and np.array_equal(bi, obi) and np.array_equal(bd, obd)
+    assert n > 100
+
+
+def test_fuse_edge_cases():
+    from projdata import fuse_scene
+    K, P = fuse_scene(w=376, h=240, nf=400)
+    e = {k: v[:0] for k, v in P.items()}
+    n, bi, bd = ORBmatcher().Fuse(K, e, 3.0)
+    assert n == 0 and len(bi) == 0
+    # no point passes the caller's gates
+    n, bi, bd = ORBmatcher().Fuse(K, dict(P, use=np.zeros_like(P["use"])), 3.0)
+    assert n == 0 and (bi == -1).all() and (bd == 256).all()
+    # projections outside the keyframe's grid
+    n, bi, _ = ORBmatcher().Fuse(K, dict(P, u=P["u"] + 5000), 3.0, sim3=True)
+    assert n == 0 and (bi == -1).all()

@@ -1,6 +1,7 @@
 """The tracking-search restatement (oracle/projection_oracle.cc) against a second restatement
 written here in Python/float32, line by line from ORB_SLAM2/src/Frame.cc:235-398 and
-ORB_SLAM2/src/ORBmatcher.cc:45-137, 1331-1474, 1604-1645.  CPU only."""
+ORB_SLAM2/src/ORBmatcher.cc:45-137, 405-523, 828-1103, 1331-1474, 1604-1645 and
+KeyFrame.cc:518-558.  CPU only."""
 import math
 
 import numpy as np
@@ -8,7 +9,7 @@ import pytest
 
 from oracle import oracle as O
 
-from projdata import scene
+from projdata import fuse_scene, init_scene, scene
 
 F32 = np.float32
 
@@ -196,3 +197,140 @@ def test_search_by_projection_last_frame(stereo, th, fwd, bwd, ori):
     pn, pm = py_last(F, L, th, fwd, bwd, ori)
     assert n == pn and np.array_equal(m, pm)
     assert n > 200
+
+
+def three_maxima(counts):
+    m1 = m2 = m3 = 0
+    i1 = i2 = i3 = -1
+    for b in range(30):
+        s = counts[b]
+        if s > m1:
+            m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, b
+        elif s > m2:
+            m3, m2, i3, i2 = m2, s, i2, b
+        elif s > m3:
+            m3, i3 = s, b
+    if m2 < F32(0.1) * F32(m1):
+        i2 = i3 = -1
+    elif m3 < F32(0.1) * F32(m1):
+        i3 = -1
+    return i1, i2, i3
+
+
+def py_init(F1, F2, prev, nnratio, ori, window):
+    """SearchForInitialization, ORBmatcher.cc:405-523 line by line."""
+    g = grid(F2)
+    n1, n2 = len(F1["keys_un"]), len(F2["keys_un"])
+    m12 = [-1] * n1
+    hist = [[] for _ in range(30)]
+    mdist = [2 ** 31 - 1] * n2
+    m21 = [-1] * n2
+    nm = 0
+    for i1 in range(n1):
+        lev = int(F1["keys_un"][i1]["octave"])
+        if lev > 0:
+            continue
+        idxs = in_area(F2, g, prev[i1, 0], prev[i1, 1], F32(window), lev, lev)
+        if not idxs:
+            continue
+        bd = bd2 = 2 ** 31 - 1
+        bi = -1
+        for i2 in idxs:
+            d = ham(F1["desc"][i1], F2["desc"][i2])
+            if mdist[i2] <= d:
+                continue
+            if d < bd:
+                bd2, bd, bi = bd, d, i2
+            elif d < bd2:
+                bd2 = d
+        if bd <= 50 and F32(bd) < F32(bd2) * F32(nnratio):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                nm -= 1
+            m12[i1] = bi
+            m21[bi] = i1
+            mdist[bi] = bd
+            nm += 1
+            if ori:
+                rot = F32(F32(F1["keys_un"][i1]["angle"]) - F32(F2["keys_un"][bi]["angle"]))
+                if rot < 0:
+                    rot = F32(rot + F32(360))
+                t = F32(rot * F32(F32(1) / F32(30)))
+                b = int(math.floor(abs(float(t)) + 0.5))
+                hist[0 if b == 30 else b].append(i1)
+    if ori:
+        keep = three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b not in keep:
+                for i1 in hist[b]:
+                    if m12[i1] >= 0:
+                        m12[i1] = -1
+                        nm -= 1
+    out = prev.copy()
+    for i1 in range(n1):
+        if m12[i1] >= 0:
+            out[i1] = (F2["keys_un"][m12[i1]]["x"], F2["keys_un"][m12[i1]]["y"])
+    return nm, np.array(m12, np.int32), out
+
+
+@pytest.mark.parametrize("t1,jitter,nn,ori,window", [(6, 0.0, 0.9, True, 100), (4, 3.0, 0.9, True, 100),
+                                                     (9, 0.0, 0.7, False, 50), (5, 8.0, 1.0, True, 10)])
+def test_search_for_initialization(t1, jitter, nn, ori, window):
+    F1, F2, prev = init_scene(t1=t1, jitter=jitter, seed=t1)
+    n, m, pv = O.search_for_initialization(F1, F2, prev, nn, ori, window)
+    pn, pm, ppv = py_init(F1, F2, prev, nn, ori, window)
+    assert n == pn and np.array_equal(m, pm)
+    assert pv.tobytes() == ppv.tobytes()
+    assert n > 100
+    assert (m >= 0).sum() == n
+
+
+def py_fuse(K, P, th, reproj):
+    """Fuse's per-point search, ORBmatcher.cc:845-975 (reproj) / 1003-1099, with the reference
+    binary's contraction of e2 emulated by exact float64 products rounded once."""
+    g = grid(K)
+    none = 256 if reproj else 2 ** 31 - 1
+    out_i, out_d = [], []
+    isg = K["inv_level_sigma2"]
+
+    def fma(a, b, c):  # float32 fused multiply-add: the exact double result rounded once
+        return F32(float(a) * float(b) + float(c))
+
+    for i in range(len(P["use"])):
+        bi, bd = -1, none
+        if P["use"][i]:
+            lev = int(P["pred_level"][i])
+            u, v = F32(P["u"][i]), F32(P["v"][i])
+            rad = F32(F32(th) * F32(K["scale_factors"][lev]))
+            for idx in in_area(K, g, u, v, rad):
+                k = K["keys_un"][idx]
+                kl = int(k["octave"])
+                if kl < lev - 1 or kl > lev:
+                    continue
+                if reproj:
+                    ex, ey = F32(u - F32(k["x"])), F32(v - F32(k["y"]))
+                    if K["u_right"] is not None and K["u_right"][idx] >= 0:
+                        er = F32(F32(P["ur"][i]) - F32(K["u_right"][idx]))
+                        e2 = fma(er, er, fma(ex, ex, F32(ey * ey)))
+                        if float(F32(e2 * F32(isg[kl]))) > 7.8:
+                            continue
+                    else:
+                        e2 = fma(ex, ex, F32(ey * ey))
+                        if float(F32(e2 * F32(isg[kl]))) > 5.99:
+                            continue
+                d = ham(P["desc"][i], K["desc"][idx])
+                if d < bd:
+                    bd, bi = d, idx
+        out_d.append(bd)
+        out_i.append(bi if bd <= 50 else -1)
+    return np.array(out_i, np.int32), np.array(out_d, np.int32)
+
+
+@pytest.mark.parametrize("stereo,th,reproj", [(False, 3.0, True), (True, 3.0, True),
+                                              (True, 1.0, True), (False, 10.0, False)])
+def test_fuse(stereo, th, reproj):
+    K, P = fuse_scene(stereo=stereo, seed=int(th))
+    n, bi, bd = O.fuse(K, K["inv_level_sigma2"], P, th, reproj)
+    pi, pd = py_fuse(K, P, th, reproj)
+    assert np.array_equal(bi, pi) and np.array_equal(bd, pd)
+    assert n == (pi >= 0).sum() and n > 100
