@@ -1,0 +1,63 @@
+// Frame_orbx.cc — the Frame / KeyFrame work the library runs on the GPU (see Frame_orbx.h):
+// Frame::ComputeBoW / KeyFrame::ComputeBoW (TemplatedVocabulary::transform, levelsup 4) and
+// Frame::ComputeStereoMatches.  Each returns false instead of failing, and the reference's body
+// runs then, so the callers' results are the reference's either way.
+#include <mutex>
+#include <vector>
+
+#include "Frame_orbx.h"
+#include "ORBextractor.h"
+
+namespace ORB_SLAM2 {
+
+namespace {
+std::mutex g_voc_mutex;
+orbx_vocabulary* g_voc = nullptr;
+}  // namespace
+
+bool orbx_load_vocabulary(const std::string& path) {
+  std::lock_guard<std::mutex> lock(g_voc_mutex);
+  if (g_voc) orbx_vocabulary_destroy(g_voc);
+  g_voc = nullptr;
+  return orbx_vocabulary_load_text(path.c_str(), /*hip_device*/ 0, &g_voc) == ORBX_OK;
+}
+
+bool orbx_compute_bow(const cv::Mat& descriptors, DBoW2::BowVector& bow, DBoW2::FeatureVector& fv) {
+  orbx_vocabulary* voc;
+  {
+    std::lock_guard<std::mutex> lock(g_voc_mutex);
+    voc = g_voc;
+  }
+  if (!voc) return false;
+  const int n = descriptors.rows;
+  const size_t m = (size_t)std::max(n, 1);
+  std::vector<uint32_t> bw(m), fi(m + 1);
+  std::vector<double> bv(m);
+  std::vector<int32_t> fo(m + 2), ff(m);
+  int32_t nb = 0, nf = 0;
+  if (orbx_vocabulary_transform(voc, descriptors.data, n, 4, nullptr, nullptr, bw.data(), bv.data(),
+                                &nb, fi.data(), fo.data(), ff.data(), &nf) != ORBX_OK)
+    return false;
+  bow.clear();
+  fv.clear();
+  for (int i = 0; i < nb; i++) bow.insert(bow.end(), std::make_pair(bw[i], bv[i]));  // ascending
+  for (int j = 0; j < nf; j++)
+    fv.insert(fv.end(), std::make_pair(fi[j], std::vector<unsigned int>(ff.begin() + fo[j],
+                                                                        ff.begin() + fo[j + 1])));
+  return true;
+}
+
+bool orbx_compute_stereo_matches(Frame& F) {
+  orbx_extractor* l = orbx_context_of(F.mpORBextractorLeft);
+  orbx_extractor* r = orbx_context_of(F.mpORBextractorRight);
+  if (!l || !r) return false;  // no device extraction to match on
+  std::vector<float> ur(std::max(F.N, 1)), depth(std::max(F.N, 1));
+  int32_t n = 0;
+  if (orbx_stereo_matches(l, r, F.mb, F.mbf, ur.data(), depth.data(), &n) != ORBX_OK || n != F.N)
+    return false;
+  F.mvuRight.assign(ur.begin(), ur.begin() + F.N);
+  F.mvDepth.assign(depth.begin(), depth.begin() + F.N);
+  return true;
+}
+
+}  // namespace ORB_SLAM2
