@@ -385,7 +385,7 @@ def cpu_baseline(cfg, seconds, mp_seconds, warmup=20, min_frames=200, max_second
                  f"SearchByBoW + SearchForTriangulation per frame")
     return dict(value=round(agg, 3), unit="frames/s", cores=P, kind="port",
                 sample=f"{w}x{h} synthetic {'stereo ' if stereo else ''}frames, CPU oracle "
-                       f"(oracle/*.cc, g++ -O3 -march=x86-64-v3 -ffp-contract=off): {P} forked "
+                       f"(oracle/*.cc, g++ -O3 -march=x86-64-v4 -mtune=znver3 -ffp-contract=off): {P} forked "
                        f"processes x 1 thread, one camera stream each, {mp_seconds:.0f} s after 3 "
                        f"warm-up frames ({sum(n for n, _ in res)} frames); {unit_desc}",
                 single_thread=single, **info)
@@ -453,7 +453,7 @@ def cpu_baseline_marker(cfg, seconds, mp_seconds, warmup=5, min_frames=100, max_
     w, h = cfg["w"], cfg["h"]
     return dict(value=round(agg, 3), unit="frames/s", cores=P, kind="port",
                 sample=f"{w}x{h} synthetic frames, CPU oracle (oracle/cvorb_oracle.cc, g++ -O3 "
-                       f"-march=x86-64-v3 -ffp-contract=off): {P} forked processes x 1 thread, one "
+                       f"-march=x86-64-v4 -mtune=znver3 -ffp-contract=off): {P} forked processes x 1 thread, one "
                        f"camera stream each, {mp_seconds:.0f} s after 3 warm-up frames "
                        f"({sum(n for n, _ in res)} frames); cv::ORB + BruteForceMatcher vs "
                        f"{len(unit.target_desc)} target descriptors + good filter per frame",
