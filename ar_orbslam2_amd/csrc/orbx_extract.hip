@@ -1223,8 +1223,9 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   // 2. initial nodes (ORBextractor.cc:530-567)
   const int nini = G.nini;
   for (int i = tid; i < nini; i += NT) {
-    A.x0[i] = (int16_t)G.ini_x[i];
-    A.x1[i] = (int16_t)G.ini_x[i + 1];
+    // ni.UL / ni.UR = cv::Point2i(hX * (float)i, 0): the float product truncated (:540-544)
+    A.x0[i] = (int16_t)(int)(G.hx * static_cast<float>(i));
+    A.x1[i] = (int16_t)(int)(G.hx * static_cast<float>(i + 1));
     A.y0[i] = 0;
     A.y1[i] = (int16_t)G.H;
     A.cnt[i] = 0;

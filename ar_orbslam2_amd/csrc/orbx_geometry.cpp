@@ -319,12 +319,11 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
       L.W = maxBX - minB;
       L.H = maxBY - minB;
       L.nini = (int)roundf(static_cast<float>(L.W) / L.H);
-      if (L.nini < 1 || L.nini > kMaxIni) {
-        if (why) *why = "octree initial column count out of range (extreme aspect ratio)";
+      if (L.nini < 1) {  // aspect below 1:2: the reference indexes vpIniNodes out of bounds
+        if (why) *why = "octree initial column count below 1 (portrait aspect under 1:2)";
         return ORBX_EUNSUPPORTED;
       }
       L.hx = static_cast<float>(L.W) / L.nini;
-      for (int i = 0; i <= L.nini; i++) L.ini_x[i] = (int)(L.hx * static_cast<float>(i));
       if (L.W >= 4096 || L.H >= 4096) {
         if (why) *why = "level too large for 12-bit key packing";
         return ORBX_EUNSUPPORTED;

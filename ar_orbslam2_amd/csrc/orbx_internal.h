@@ -20,7 +20,6 @@ constexpr int kMaxLevels = 16;
 constexpr int kEdge = 19;       // EDGE_THRESHOLD (ORBextractor.cc:71)
 constexpr int kPatch = 31;      // PATCH_SIZE (:69)
 constexpr int kHalfPatch = 15;  // HALF_PATCH_SIZE (:70)
-constexpr int kMaxIni = 64;     // initial octree columns supported (nIni)
 
 // Per pyramid level, computed on the host once per plan (ORBextractor.cc:404-460,
 // 735-757, 1047-1072).
@@ -78,8 +77,7 @@ struct LevelGeom {
   int cand_off, cand_cap;  // candidate region (keys) inside one image's candidate block
   int nfeat;               // mnFeaturesPerLevel
   int nini;                // DistributeOctTree initial columns
-  float hx;                // (float)(maxX-minX)/nIni
-  int ini_x[kMaxIni + 1];  // (int)(hX * i)
+  float hx;                // (float)(maxX-minX)/nIni; node i spans [(int)(hx*i), (int)(hx*(i+1)))
   int W, H;                // maxX-minX, maxY-minY (octree frame, origin at minBorder=16)
   int node_cap;            // max alive octree nodes: max(N+3, 4*nIni+4)
   int kp_off, kp_cap;      // per-image final keypoint slots for this level

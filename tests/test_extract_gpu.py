@@ -167,3 +167,14 @@ def test_dense_corner_pattern_fills_pretest_queues(w, h):
     # the same texture on half the frame next to a flat region (fallback cells beside full ones)
     img[:, : w // 2] = 128
     _compare(img, 1000)
+
+
+@pytest.mark.parametrize("w,h", [(4000, 70), (2600, 64)])
+def test_wide_frames_many_initial_octree_nodes(w, h):
+    """Panorama-like frames: DistributeOctTree starts from nIni = round(W / H) > 64 initial
+    nodes (ORBextractor.cc:530-567; 104 and 80 here) — round 2 returned ORBX_EUNSUPPORTED above
+    64, the reference has no limit."""
+    rng = np.random.default_rng(w)
+    img = synth.frame(w, h, 1, 3) if w <= 2600 else rng.integers(0, 256, (h, w), dtype=np.uint8)
+    kps = _compare(img, 1500)
+    assert len(kps) > 100
