@@ -984,6 +984,46 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef ORBX_FC_PAIR
+#define ORBX_FC_PAIR 1  // stage 1: two row-pair steps per LDS round trip
+#endif
+#ifndef ORBX_FC_SCORE2
+#define ORBX_FC_SCORE2 0  // scoring: two candidates per lane per round (measured slower: 0.637 vs 0.595 ms per 512 C2 frames)
+#endif
+// Stage 1 of one detection chunk (up to 8 steps of STEP rows per lane, two steps per LDS round
+// trip): the flags of step s end at bits 15 - 2 (nst - 1 - s) (row r) and 31 - 2 (...) (row
+// r + 1) of the returned word; the caller masks rows and columns outside the cell.
+template <int RS, int STEP>
+__device__ __forceinline__ uint32_t cardinal_chunk(const uint8_t* c0, int nst, int t) {
+  uint32_t acc = 0;
+  const uint8_t* c = c0;
+  int s = 0;
+  if constexpr (ORBX_FC_PAIR) {
+    for (; s + 2 <= nst; s += 2, c += 2 * STEP * RS) {
+      uint32_t f0, f1;
+      fast_cardinal2x2<RS, STEP * RS>(c, t, f0, f1);
+      acc = (acc >> 4) | (f0 >> 2) | f1;
+    }
+  } else {
+    for (; s + 1 < nst; s++, c += STEP * RS) acc = (acc >> 2) | fast_cardinal2<RS>(c, t);
+  }
+  if (s < nst) acc = (acc >> 2) | fast_cardinal2<RS>(c, t);
+  return acc;
+}
+
+// the odd bits of [lo, hi] (both odd, lo <= hi), 0 if hi < lo
+__device__ __forceinline__ uint32_t odd_bits(int lo, int hi) {
+  if (hi < lo) return 0u;
+  const uint32_t upto = hi >= 31 ? 0xFFFFFFFFu : ((2u << hi) - 1u);
+  return 0xAAAAAAAAu & upto & ~((1u << lo) - 1u);
+}
+
+// Each wave takes `cpw` consecutive cells of the list (neighbours: their ROIs share halo rows in
+// L2; at most kCellsPerWave, fewer when the launch has few cells, e.g. one drop-in frame); the
+// next cell's ROI loads are issued while the current one is processed, so their latency hides
+// behind it.
+constexpr int kCellsPerWave = 4;
+
 template <int RS, int MAXR>
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr,
                                                     int64_t pyr_bytes,
@@ -991,9 +1031,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                                                     const int* __restrict__ list, int nlist,
                                                     int ncells, int ini_th, int min_th,
                                                     uint32_t* __restrict__ cand, int cand_total,
-                                                    int* __restrict__ cell_counts) {
-  // staged ROI (+ 4 rows the last pair step of a half-wave may read past it, masked)
-  __shared__ __align__(16) uint8_t s_src[4][(MAXR + 4) * RS];
+                                                    int* __restrict__ cell_counts, int cpw) {
+  // staged ROI (+ the rows the last pair steps of a half-wave may read past it, masked)
+  __shared__ __align__(16) uint8_t s_src[4][(MAXR + 12) * RS];
   __shared__ __align__(16) uint8_t s_vv[4][(MAXR - 4) * RS];
   constexpr int QCAP = (MAXR - 6) * (RS - 9);  // detection pixels of the largest cell
   __shared__ uint16_t s_q[4][QCAP];
@@ -1002,103 +1042,125 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bx, img;
   xcd_block(bx, img);
-  const int li = bx * 4 + wid;
-  if (li >= nlist) return;  // wave-uniform; no workgroup barrier below
-  const int ci = list[li];
-  const CellGeom C = cells[ci];
+  const int l0 = (bx * 4 + wid) * cpw;
+  if (l0 >= nlist) return;  // wave-uniform; no workgroup barrier below
+  const int l1 = min(l0 + cpw, nlist);
   uint8_t* S = s_src[wid];
   uint8_t* V = s_vv[wid];
   uint16_t* q = s_q[wid];
-  const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3
-  const int dr = rows - 6, cw = cols - 6;            // detection rows / columns
-  int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
-  if (dr <= 0 || cw <= 0) {
-    if (lane == 0) *cnt_out = 0;
-    return;
-  }
-  // the ROI as aligned dwords (its first pixel lands at byte sh of each staged row): lane l
-  // takes word l % kW of rows l / kW + kG u, all kPf loads in flight before the LDS stores
-  {
-    constexpr int kW = RS / 4, kG = 64 / kW, kPf = (MAXR + kG - 1) / kG;
-    const int lrow = lane / kW, lword = lane - lrow * kW;
-    const int words = ((C.x0 & 3) + cols + 3) >> 2;
-    const uint8_t* srow = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - 3 * C.pitch - 3) +
-                          (C.x0 & ~3) - C.x0;  // staged row 0, word 0
-    const bool ok = lrow < kG && lword < words;
-    uint32_t pv[kPf];
+  const uint8_t* pimg = pyr + (int64_t)img * pyr_bytes;
+  // ROI staging as aligned dwords: lane l takes word l % kW of rows l / kW + kG u
+  constexpr int kW = RS / 4, kG = 64 / kW, kPf = (MAXR + kG - 1) / kG;
+  static_assert(63 / kW + kG * (kPf - 1) < MAXR + 12, "staging rows stay inside s_src");
+  const int lrow = lane / kW, lword = lane - lrow * kW;
+  uint32_t pv[kPf];
+  // every lane loads and stores every round, branch-free: rows past the ROI and words past its
+  // last one read clamped (in-level) addresses, and those staged bytes are never used (stage 1
+  // masks their flags, scores read only detection pixels' windows)
+  auto issue = [&](const CellGeom& C) {
+    const int rows = C.y1 - C.y0, words = ((C.x0 & 3) + (C.x1 - C.x0) + 3) >> 2;
+    const uint8_t* srow = pimg + (C.v_row0 - 3 * C.pitch - 3) + (C.x0 & ~3) - C.x0 +
+                          4 * min(lword, words - 1);
 #pragma unroll
-    for (int u = 0; u < kPf; u++) {
-      const int r = lrow + kG * u;
-      pv[u] = (ok && r < rows) ? *(const uint32_t*)(srow + (uint32_t)__mul24(r, C.pitch) + 4 * lword)
-                               : 0u;
-    }
+    for (int u = 0; u < kPf; u++)
+      pv[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(min(lrow + kG * u, rows - 1), C.pitch));
+  };
+  int ci = list[l0];
+  CellGeom C = cells[ci];
+  issue(C);
+  for (int li = l0; li < l1; li++) {
+    const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3
+    const int dr = rows - 6, cw = cols - 6;            // detection rows / columns
+    int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
+    // this cell's ROI into LDS (rows up to lrow + kG (kPf - 1) < MAXR + 12), then the next
+    // cell's loads in flight
+    wave_sync();  // the previous cell's reads of S are done
 #pragma unroll
-    for (int u = 0; u < kPf; u++) {
-      const int r = lrow + kG * u;
-      if (ok && r < rows) *(uint32_t*)(S + r * RS + 4 * lword) = pv[u];
+    for (int u = 0; u < kPf; u++) *(uint32_t*)(S + (lrow + kG * u) * RS + 4 * lword) = pv[u];
+    const CellGeom Cc = C;
+    const int cic = ci;
+    if (li + 1 < l1) {
+      ci = list[li + 1];
+      C = cells[ci];
+      issue(C);
     }
-  }
-  for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
-  wave_sync();
-  const uint8_t* Sx = S + (C.x0 & 3);  // pixel (r, c) of the ROI at Sx[r * RS + c]
-  const bool half = cw <= 32;          // wave-uniform
-  const int col = half ? lane & 31 : lane, sub = half ? 2 * (lane >> 5) : 0, step = half ? 4 : 2;
-  const uint32_t fm = col < cw ? 0x80008000u : 0u;
-  int t = ini_th;
-  uint64_t bits = 0;  // this lane's keep row (lane = detection row)
-  for (int pass = 0; pass < 2; pass++) {
-    // (1) cardinal pretest at t, compacted into q (row << 6 | column)
-    int nq = 0;
-    for (int rc = 0; rc < dr; rc += 8 * step) {
-      const int nst = min(8, (dr - rc + step - 1) / step);  // wave-uniform
-      uint32_t acc = 0;  // step s's flags end at bits 15 - 2 (nst - 1 - s) and 31 - 2 (...)
-      for (int s = 0; s < nst; s++) {
-        const int r = rc + s * step + sub;
-        const uint32_t f = fast_cardinal2<RS>(Sx + r * RS + col, t) & fm &
-                           ((r < dr ? 0x8000u : 0u) | (r + 1 < dr ? 0x80000000u : 0u));
-        acc = (acc >> 2) | f;
+    if (dr <= 0 || cw <= 0) {
+      if (lane == 0) *cnt_out = 0;
+      continue;
+    }
+    (void)cic;
+    for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
+    wave_sync();
+    const uint8_t* Sx = S + (Cc.x0 & 3);  // pixel (r, c) of the ROI at Sx[r * RS + c]
+    const bool half = cw <= 32;           // wave-uniform
+    const int col = half ? lane & 31 : lane, sub = half ? 2 * (lane >> 5) : 0, step = half ? 4 : 2;
+    const int lstep = half ? 2 : 1;       // log2(step)
+    const bool col_ok = col < cw;
+    int t = ini_th;
+    uint64_t bits = 0;  // this lane's keep row (lane = detection row)
+    for (int pass = 0; pass < 2; pass++) {
+      // (1) cardinal pretest at t, compacted into q (row << 6 | column)
+      int nq = 0;
+      for (int rc = 0; rc < dr; rc += 8 * step) {
+        const int nst = min(8, (dr - rc + step - 1) >> lstep);  // wave-uniform
+        uint32_t acc = half ? cardinal_chunk<RS, 4>(Sx + (rc + sub) * RS + col, nst, t)
+                            : cardinal_chunk<RS, 2>(Sx + rc * RS + col, nst, t);
+        // rows of this lane in the chunk: rc + sub + step s (+1 in the high half), s < nst;
+        // step s's bits sit at 15 - 2 (nst - 1 - s): keep rows < dr and columns < cw
+        const int lo = 17 - 2 * nst;
+        const int nlo = min(nst, max(0, dr - rc - sub + step - 1) >> lstep);
+        const int nhi = min(nst, max(0, dr - rc - sub + step - 2) >> lstep);
+        acc &= col_ok ? odd_bits(lo, lo + 2 * nlo - 2) | (odd_bits(lo, lo + 2 * nhi - 2) << 16) : 0u;
+        const int cnt = __popc(acc);
+        const int incl = wave_scan_incl(cnt);
+        int pos = nq + incl - cnt;
+        nq += __builtin_amdgcn_readlane(incl, 63);
+        // bit b: step s = nst - 8 + (b & 15) / 2, row + 1 in the high half
+        const int rbase = rc + sub + step * (nst - 8);
+        while (acc) {
+          const int b = __builtin_ctz(acc);
+          acc &= acc - 1;
+          const int r = rbase + step * ((b & 15) >> 1) + (b >> 4);
+          q[pos++] = (uint16_t)((r << 6) | col);
+        }
       }
-      const int cnt = __popc(acc);
-      const int incl = wave_scan_incl(cnt);
-      int pos = nq + incl - cnt;
-      nq += __builtin_amdgcn_readlane(incl, 63);
-      // bit b: step s = nst - 8 + (b & 15) / 2, row + 1 in the high half
-      const int rbase = rc + sub + step * (nst - 8);
-      while (acc) {
-        const int b = __builtin_ctz(acc);
-        acc &= acc - 1;
-        const int r = rbase + step * ((b & 15) >> 1) + (b >> 4);
-        q[pos++] = (uint16_t)((r << 6) | col);
+      wave_sync();
+      // (2) scores of the queued pixels, two per lane per round so their loads overlap (a
+      // fallback pass rescores the iniThFAST ones: same value)
+      for (int j = lane; j < nq; j += ORBX_FC_SCORE2 ? 128 : 64) {
+        const int j2 = ORBX_FC_SCORE2 && j + 64 < nq ? j + 64 : j;
+        const int e0 = q[j], e1 = q[j2];
+        const int r0 = e0 >> 6, c0 = e0 & 63, r1 = e1 >> 6, c1 = e1 & 63;
+        const int sc0 = fast_score(Sx, RS, c0 + 3, r0 + 3);
+        V[(r0 + 1) * RS + c0 + 1] = (uint8_t)min(255, max(0, sc0 + 1));
+        if (ORBX_FC_SCORE2) {
+          const int sc1 = fast_score(Sx, RS, c1 + 3, r1 + 3);
+          V[(r1 + 1) * RS + c1 + 1] = (uint8_t)min(255, max(0, sc1 + 1));
+        }
       }
+      s_rows[wid][lane] = 0;
+      wave_sync();
+      // (3) NMS at t; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
+      const int t1 = max(t, 1);
+      for (int j = lane; j < nq; j += 64) {
+        const int e = q[j], r = e >> 6, c = e & 63;
+        const uint8_t* p = V + (r + 1) * RS + c + 1;
+        const int v = p[0];
+        if (v <= t1) continue;
+        const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
+                             max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
+        if (v > (nmax > t ? nmax : t1)) atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
+      }
+      wave_sync();
+      bits = lane < dr ? s_rows[wid][lane] : 0;
+      if (__ballot(bits != 0) != 0 || t == min_th) break;  // cell has keypoints, or retried
+      t = min_th;  // no keypoint at iniThFAST: FAST again at minThFAST (ORBextractor.cc:782-784)
     }
-    wave_sync();
-    // (2) scores of the queued pixels (a fallback pass rescores the iniThFAST ones: same value)
-    for (int j = lane; j < nq; j += 64) {
-      const int e = q[j], r = e >> 6, c = e & 63;
-      const int sc = fast_score(Sx, RS, c + 3, r + 3);
-      V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
-    }
-    s_rows[wid][lane] = 0;
-    wave_sync();
-    // (3) NMS at t; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
-    const int t1 = max(t, 1);
-    for (int j = lane; j < nq; j += 64) {
-      const int e = q[j], r = e >> 6, c = e & 63;
-      const uint8_t* p = V + (r + 1) * RS + c + 1;
-      const int v = p[0];
-      if (v <= t1) continue;
-      const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
-                           max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
-      if (v > (nmax > t ? nmax : t1)) atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
-    }
-    wave_sync();
-    bits = lane < dr ? s_rows[wid][lane] : 0;
-    if (__ballot(bits != 0) != 0 || t == min_th) break;  // cell has keypoints, or retried
-    t = min_th;  // no keypoint at iniThFAST: FAST again at minThFAST (ORBextractor.cc:782-784)
+    const uint8_t* Vr = V + (lane + 1) * RS + 1;
+    compact_rows(bits, lane, Cc.y0 + 3 + lane, Cc.x0 + 3,
+                 cand + (int64_t)img * cand_total + Cc.slot_off, cnt_out,
+                 [&](int kk) { return (int)Vr[kk]; });
   }
-  const uint8_t* Vr = V + (lane + 1) * RS + 1;
-  compact_rows(bits, lane, C.y0 + 3 + lane, C.x0 + 3, cand + (int64_t)img * cand_total + C.slot_off,
-               cnt_out, [&](int kk) { return (int)Vr[kk]; });
 }
 
 // ------------------------------------------------------------------ k_octree
@@ -1773,6 +1835,7 @@ struct orbx_plan {
   int *d_cells_small = nullptr, *d_cells_big = nullptr;
   int n_cells_small = 0, n_cells_big = 0;
   bool fast_legacy = false;  // ORBX_FAST_LEGACY=1: k_fast_tile + k_fast_compact + k_fast_fallback
+  int fc_cpw = 0;            // ORBX_FC_CPW: k_fast_cells cells per wave (experiments; 0 = auto)
   bool fast_pair = true;  // k_fast_tile pretest on row pairs (ORBX_FAST_PAIR=0: one row per lane)
   const uint8_t* last_in = nullptr;
   int last_n = 0;
@@ -1901,16 +1964,20 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   }
   const int ncells = (int)g.cells.size();
   if (ncells > 0 && !P->fast_legacy) {
+    // cells per wave: up to kCellsPerWave while the launch keeps >= 16 k waves in flight
+    int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
+    if (P->fc_cpw > 0) cpw = P->fc_cpw;
     if (P->n_cells_small > 0)
-      hipLaunchKernelGGL((k_fast_cells<44, 44>), dim3((P->n_cells_small + 3) / 4, n), dim3(256), 0,
+      hipLaunchKernelGGL((k_fast_cells<44, 44>),
+                         dim3((P->n_cells_small + 4 * cpw - 1) / (4 * cpw), n), dim3(256), 0,
                          P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
                          P->n_cells_small, ncells, g.ini_th, g.min_th, P->d_cand, g.cand_total,
-                         P->d_cell_counts);
+                         P->d_cell_counts, cpw);
     if (P->n_cells_big > 0)
       hipLaunchKernelGGL((k_fast_cells<72, kCellMax>), dim3((P->n_cells_big + 3) / 4, n), dim3(256),
                          0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_big,
                          P->n_cells_big, ncells, g.ini_th, g.min_th, P->d_cand, g.cand_total,
-                         P->d_cell_counts);
+                         P->d_cell_counts, 1);
     pr.mark(P->stream, st_fcell);
   } else if (ncells > 0) {
     hipLaunchKernelGGL(P->fast_pair ? k_fast_tile<true> : k_fast_tile<false>, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
@@ -1979,6 +2046,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->device = hip_device;
   if (const char* e = getenv("ORBX_FAST_PAIR")) P->fast_pair = atoi(e) != 0;
   if (const char* e = getenv("ORBX_FAST_LEGACY")) P->fast_legacy = atoi(e) != 0;
+  if (const char* e = getenv("ORBX_FC_CPW")) P->fc_cpw = std::max(0, std::min(kCellsPerWave, atoi(e)));
   const Geometry& g = P->g;
   for (const CellGeom& c : g.cells) P->has_fb_big |= c.fb_big != 0;
   auto fail = [&](int code) {

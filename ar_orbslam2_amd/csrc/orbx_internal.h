@@ -316,6 +316,68 @@ __device__ __forceinline__ uint32_t fast_cardinal2(const uint8_t* c, int t) {
   return (((D[0] | D[2]) & (D[1] | D[3])) | ((B[0] | B[2]) & (B[1] | B[3]))) & 0x80008000u;
 }
 
+// fast_cardinal2 for two row pairs at once, the second D bytes below the first (D = the step
+// between pairs times the row stride): the 20 LDS loads are issued together and waited for once,
+// so a wave exposes one LDS latency per two steps.
+template <int RS, int D>
+__device__ __forceinline__ void fast_cardinal2x2(const uint8_t* c, int t, uint32_t& f0,
+                                                 uint32_t& f1) {
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)c;
+  uint32_t P[10], H[10];
+  asm volatile(
+      "ds_read_u8 %0, %20 offset:%21\n\t"
+      "ds_read_u8_d16_hi %10, %20 offset:%26\n\t"
+      "ds_read_u8 %1, %20 offset:%22\n\t"
+      "ds_read_u8_d16_hi %11, %20 offset:%27\n\t"
+      "ds_read_u8 %2, %20 offset:%23\n\t"
+      "ds_read_u8_d16_hi %12, %20 offset:%28\n\t"
+      "ds_read_u8 %3, %20 offset:%24\n\t"
+      "ds_read_u8_d16_hi %13, %20 offset:%29\n\t"
+      "ds_read_u8 %4, %20 offset:%25\n\t"
+      "ds_read_u8_d16_hi %14, %20 offset:%30\n\t"
+      "ds_read_u8 %5, %20 offset:%31\n\t"
+      "ds_read_u8_d16_hi %15, %20 offset:%36\n\t"
+      "ds_read_u8 %6, %20 offset:%32\n\t"
+      "ds_read_u8_d16_hi %16, %20 offset:%37\n\t"
+      "ds_read_u8 %7, %20 offset:%33\n\t"
+      "ds_read_u8_d16_hi %17, %20 offset:%38\n\t"
+      "ds_read_u8 %8, %20 offset:%34\n\t"
+      "ds_read_u8_d16_hi %18, %20 offset:%39\n\t"
+      "ds_read_u8 %9, %20 offset:%35\n\t"
+      "ds_read_u8_d16_hi %19, %20 offset:%40\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(P[0]), "=&v"(P[1]), "=&v"(P[2]), "=&v"(P[3]), "=&v"(P[4]), "=&v"(P[5]),
+        "=&v"(P[6]), "=&v"(P[7]), "=&v"(P[8]), "=&v"(P[9]), "=&v"(H[0]), "=&v"(H[1]),
+        "=&v"(H[2]), "=&v"(H[3]), "=&v"(H[4]), "=&v"(H[5]), "=&v"(H[6]), "=&v"(H[7]),
+        "=&v"(H[8]), "=&v"(H[9])
+      : "v"(a), "i"(3 * RS + 3), "i"(6 * RS + 3), "i"(3 * RS + 6), "i"(3), "i"(3 * RS),
+        "i"(4 * RS + 3), "i"(7 * RS + 3), "i"(4 * RS + 6), "i"(RS + 3), "i"(4 * RS),
+        "i"(D + 3 * RS + 3), "i"(D + 6 * RS + 3), "i"(D + 3 * RS + 6), "i"(D + 3), "i"(D + 3 * RS),
+        "i"(D + 4 * RS + 3), "i"(D + 7 * RS + 3), "i"(D + 4 * RS + 6), "i"(D + RS + 3),
+        "i"(D + 4 * RS)
+      : "memory");
+  const uint32_t rep = 0x10001u;
+  uint32_t f[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    uint32_t Q[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) Q[k] = P[5 * h + k] | H[5 * h + k];
+    const uint32_t C = Q[0];
+    const uint32_t L = C + (uint32_t)(0x8000 - t - 1) * rep;
+    const uint32_t K = C + (uint32_t)(t + 1) * rep - 0x80008000u;
+    uint32_t Dk[4], Bk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      Dk[k] = L - Q[k + 1];
+      Bk[k] = Q[k + 1] - K;
+    }
+    f[h] = (((Dk[0] | Dk[2]) & (Dk[1] | Dk[3])) | ((Bk[0] | Bk[2]) & (Bk[1] | Bk[3]))) & 0x80008000u;
+  }
+  f0 = f[0];
+  f1 = f[1];
+}
+
 // rank of this lane among the set lanes of m
 __device__ __forceinline__ int lane_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));

@@ -76,9 +76,11 @@ def algorithmic_bytes(levels, n_kp, n_img):
         # two launches (levels 1-3 from the input, 4-7 from level 3): average launch
         "k_pyramid": (2 * P[0] * n_img + sum(per_resize)) / 2,
         "k_blur": 2 * sum(P) * n_img,
-        # every level pixel read once, its keep bit written (the 64-bit row words k_fast_compact
-        # reads back); the survivors' scores (~1 % of the pixels) are not counted
-        "k_fast_tile": sum(P) * n_img * 9 / 8,
+        # SURVEY §8d's FAST term: every level pixel read once (the per-cell kernel writes only
+        # the cells' keys, 4 B per candidate, ~1 % of the pixels: not counted)
+        "k_fast_cells": sum(P) * n_img,
+        # the round-2 tile path (ORBX_FAST_LEGACY=1), same model
+        "k_fast_tile": sum(P) * n_img,
         "k_fast_compact": sum(P) * n_img / 8,                   # 1 NMS bit per pixel
         "k_describe": 60 * n_kp,
         "k_voc_transform": 52 * n_kp,                          # desc in; word, rank, node, weight out
@@ -88,9 +90,9 @@ def algorithmic_bytes(levels, n_kp, n_img):
 
 
 # bytes per lane of the global loads of the kernels bench.py can name as roofline kernel (the
-# staged windows of k_fast_tile and k_cvfast: 16-B pieces per lane); their stores are 8-B bitmap
-# words and 1-B survivor scores
-LOAD_WIDTH = {"k_fast_tile": 16, "k_cvfast": 16}
+# staged windows of k_fast_tile and k_cvfast: 16-B pieces per lane; k_fast_cells: the cell ROI
+# as aligned dwords); the stores are 8-B bitmap words / 1-B scores (tile) and 4-B keys (cells)
+LOAD_WIDTH = {"k_fast_tile": 16, "k_cvfast": 16, "k_fast_cells": 4}
 
 
 def _load_json(name):
@@ -192,6 +194,8 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     pass).  The path is integer stencil / gather / popcount work: VALU issue bounds it, so
     `bound` is "valu" and frac is the VALU-issue fraction when the SQ pass of this command
     exists; the HBM fraction (algorithmic bytes / launch time vs 8 TB/s) is reported beside it."""
+    # stages not launched in this configuration (the other FAST path) are dropped
+    stages = {k: v for k, v in stages.items() if v[1] > 0}
     # stages that time several kernels (the stereo copy + 3 kernels, the matchers' node and
     # finish kernels) cannot be matched to one kernel's counters: the roofline kernel is the
     # largest single-kernel stage
@@ -228,7 +232,8 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     return out
 
 
-EXTRACT_STAGES = ("k_pyramid", "k_blur", "k_fast_tile", "k_fast_compact", "k_fast_fallback",
+EXTRACT_STAGES = ("k_pyramid", "k_blur", "k_fast_cells", "k_fast_tile", "k_fast_compact",
+                  "k_fast_fallback",
                   "k_octree", "k_describe", "k_cvfast", "k_cvselect", "k_cvdescribe")
 
 
