@@ -311,7 +311,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
           c.bm_row0 = (int)(L.bm_off + (int64_t)(c.y0 + 3) * L.bm_wpr + ((c.x0 + 3) >> 6));
           c.v_row0 = (int)(L.pyr_off + (int64_t)(c.y0 + 3) * L.pitch + c.x0 + 3);
           c.bm_wpr = (int16_t)L.bm_wpr;
-          c.pitch = (int16_t)L.pitch;
+          c.pitch = L.pitch;
           g->cells.push_back(c);
         }
       }

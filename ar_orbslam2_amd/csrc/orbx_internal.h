@@ -94,9 +94,11 @@ struct CellGeom {
   // k_fast_compact addressing of the first detection row (per image): its keep-bitmap word
   // holding column x0 + 3, and its V byte at column x0 + 3; with the level's row strides
   int bm_row0, v_row0;
-  int16_t bm_wpr, pitch;
-  int pad;
+  int16_t bm_wpr, pad16;
+  int pitch;  // a whole aligned dword: k_fast_cells reads the next cell's geometry with scalar
+              // loads (an int16 field here became a vector load whose wait it exposed per cell)
 };
+static_assert(sizeof(CellGeom) == 40, "CellGeom layout");
 
 struct Geometry {
   int w = 0, h = 0, nlevels = 0;
