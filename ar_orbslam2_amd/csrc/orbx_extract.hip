@@ -663,14 +663,39 @@ __global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ p
 // iniThFAST (ORBextractor.cc:780) in raster order (row prefix sum, then ascending x) into the
 // cell's candidate slot, keys relative to minBorder = 16.  A cell without any is queued for
 // k_fast_fallback (the minThFAST retry, ORBextractor.cc:782-784).
-__device__ __forceinline__ uint32_t cand_key(int x, int y, int v) {
-  return (uint32_t)(x - (kEdge - 3)) | ((uint32_t)(y - (kEdge - 3)) << 12) | ((uint32_t)(v - 1) << 24);
+// Candidate keys: position in the octree frame (level coordinates - minBorder + 3) and FAST
+// score - 1.  Plans whose octree frames fit 4095 px pack x:12 y:12 score:8 into a u32; wider
+// ones (Geometry::wide_keys) use a u64 with x:16 y:16 and the score at bit 32.
+template <class K>
+struct KeyFmt;
+template <>
+struct KeyFmt<uint32_t> {
+  static __device__ __forceinline__ uint32_t make(int x, int y, int v) {
+    return (uint32_t)(x - (kEdge - 3)) | ((uint32_t)(y - (kEdge - 3)) << 12) | ((uint32_t)(v - 1) << 24);
+  }
+  static __device__ __forceinline__ int x(uint32_t k) { return (int)(k & 0xFFF); }
+  static __device__ __forceinline__ int y(uint32_t k) { return (int)((k >> 12) & 0xFFF); }
+  static __device__ __forceinline__ unsigned score(uint32_t k) { return k >> 24; }
+};
+template <>
+struct KeyFmt<uint64_t> {
+  static __device__ __forceinline__ uint64_t make(int x, int y, int v) {
+    return (uint64_t)((uint32_t)(x - (kEdge - 3)) | ((uint32_t)(y - (kEdge - 3)) << 16)) |
+           ((uint64_t)(uint32_t)(v - 1) << 32);
+  }
+  static __device__ __forceinline__ int x(uint64_t k) { return (int)(k & 0xFFFF); }
+  static __device__ __forceinline__ int y(uint64_t k) { return (int)((k >> 16) & 0xFFFF); }
+  static __device__ __forceinline__ unsigned score(uint64_t k) { return (unsigned)(k >> 32); }
+};
+
+__device__ __forceinline__ uint32_t cand_key(int x, int y, int v) {  // the legacy FAST kernels
+  return KeyFmt<uint32_t>::make(x, y, v);
 }
 
 // raster-order compaction of a cell's keep rows (lane = detection row): out slot, count
-template <class VAt>
+template <class K, class VAt>
 __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int cx0,
-                                             uint32_t* out, int* cnt_out, VAt v_at) {
+                                             K* out, int* cnt_out, VAt v_at) {
   const int cnt = __popcll(bits);
   const int incl = wave_scan_incl(cnt);
   int pos = incl - cnt;
@@ -678,7 +703,7 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
   while (bits) {
     const int k = __builtin_ctzll(bits);
     bits &= bits - 1;
-    out[pos++] = cand_key(cx0 + k, y, v_at(k));
+    out[pos++] = KeyFmt<K>::make(cx0 + k, y, v_at(k));
   }
   if (lane == 0) *cnt_out = nout;
 }
@@ -1024,13 +1049,13 @@ __device__ __forceinline__ uint32_t odd_bits(int lo, int hi) {
 // behind it.
 constexpr int kCellsPerWave = 4;
 
-template <int RS, int MAXR>
+template <int RS, int MAXR, class K>
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr,
                                                     int64_t pyr_bytes,
                                                     const CellGeom* __restrict__ cells,
                                                     const int* __restrict__ list, int nlist,
                                                     int ncells, int ini_th, int min_th,
-                                                    uint32_t* __restrict__ cand, int cand_total,
+                                                    K* __restrict__ cand, int cand_total,
                                                     int* __restrict__ cell_counts, int cpw) {
   // staged ROI (+ the rows the last pair steps of a half-wave may read past it, masked)
   __shared__ __align__(16) uint8_t s_src[4][(MAXR + 12) * RS];
@@ -1182,8 +1207,9 @@ struct OctNodes {
   int *cnt, *seq;
 };
 
-__device__ __forceinline__ int quad_of(uint32_t key, int x0, int x1, int y0, int y1) {
-  const int x = key & 0xFFF, y = (key >> 12) & 0xFFF;
+template <class K>
+__device__ __forceinline__ int quad_of(K key, int x0, int x1, int y0, int y1) {
+  const int x = KeyFmt<K>::x(key), y = KeyFmt<K>::y(key);
   const int xm = x0 + (x1 - x0 + 1) / 2;  // ceil((float)(UR.x-UL.x)/2)
   const int ym = y0 + (y1 - y0 + 1) / 2;
   return x < xm ? (y < ym ? 0 : 2) : (y < ym ? 1 : 3);
@@ -1193,11 +1219,11 @@ struct OctCtx {
   OctNodes A, B;
   int *cc, *t1, *t2, *t3, *t4, *s_tmp, *s_misc;
   uint64_t *pk, *s_tmp64;
-  uint32_t* outk;
+  void* outk;  // K[] of the level's retained keys
   int* oc;
 };
 
-// Where the octree keeps its keys (packed x:12 y:12 score:8) and their node labels.  Thread t
+// Where the octree keeps its keys (KeyFmt<K>) and their node labels.  Thread t
 // owns keys t, t + NT, t + 2 NT, ... (NT threads); they are processed in chunks of kOctRegKeys
 // held in registers, slot r of chunk c being key t + NT (c kOctRegKeys + r).
 //   RegKeys<NT>: one chunk (n <= kOctRegKeys NT): keys and labels stay in registers for the
@@ -1206,37 +1232,39 @@ struct OctCtx {
 //   MemKeys<NT>: larger levels, keys and labels in global scratch (L2-resident): every pass
 //                loads a chunk with all its loads in flight, works on the registers and stores
 //                the labels back (one load latency per chunk instead of one per key).
-template <int NT>
+template <int NT, class K>
 struct RegKeys {
+  using Key = K;
   static constexpr bool kRegs = true;
-  uint32_t key[kOctRegKeys];
+  K key[kOctRegKeys];
   int lab[kOctRegKeys];
   uint32_t q2 = 0;  // 2 bits per key: quadrant inside its node (valid when the node splits)
   int n;
   __device__ int nchunks() const { return 1; }
   __device__ void load(int, bool) {}
   __device__ void store_labs(int) {}
-  __device__ uint32_t get_key(int r) const { return key[r]; }
+  __device__ K get_key(int r) const { return key[r]; }
   __device__ int get_lab(int r) const { return lab[r]; }
   __device__ void set_lab(int r, int v) { lab[r] = v; }
   __device__ void set_q(int r, int q) { q2 = (q2 & ~(3u << (2 * r))) | ((uint32_t)q << (2 * r)); }
   __device__ int get_q(int r, const OctNodes&, int) const { return (q2 >> (2 * r)) & 3; }
 };
 
-template <int NT>
+template <int NT, class K>
 struct MemKeys {
+  using Key = K;
   static constexpr bool kRegs = false;
-  uint32_t* keys;
+  K* keys;
   int* labs;
   int n;
-  uint32_t key[kOctRegKeys];
+  K key[kOctRegKeys];
   int lab[kOctRegKeys];
   __device__ int nchunks() const { return (n + NT * kOctRegKeys - 1) / (NT * kOctRegKeys); }
   __device__ void load(int c, bool want_labs) {
 #pragma unroll
     for (int r = 0; r < kOctRegKeys; r++) {
       const int k = threadIdx.x + NT * (c * kOctRegKeys + r);
-      key[r] = k < n ? keys[k] : 0u;
+      key[r] = k < n ? keys[k] : K(0);
       lab[r] = (want_labs && k < n) ? labs[k] : 0;
     }
   }
@@ -1247,7 +1275,7 @@ struct MemKeys {
       if (k < n) labs[k] = lab[r];
     }
   }
-  __device__ uint32_t get_key(int r) const { return key[r]; }
+  __device__ K get_key(int r) const { return key[r]; }
   __device__ int get_lab(int r) const { return lab[r]; }
   __device__ void set_lab(int r, int v) { lab[r] = v; }
   __device__ void set_q(int, int) {}
@@ -1274,13 +1302,14 @@ __device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, 
 
 template <int NT, class KS>
 __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, KS& ks,
-                                            const uint32_t* keys_mem) {
+                                            const typename KS::Key* keys_mem) {
+  using K = typename KS::Key;
   const int tid = threadIdx.x;
   const int n = ks.n;
   OctNodes A = X.A, B = X.B;
   int *cc = X.cc, *t1 = X.t1, *t2 = X.t2, *t3 = X.t3, *t4 = X.t4, *s_tmp = X.s_tmp,
       *s_misc = X.s_misc;
-  uint32_t* outk = X.outk;
+  K* outk = (K*)X.outk;
   int* oc = X.oc;
   // 2. initial nodes (ORBextractor.cc:530-567)
   const int nini = G.nini;
@@ -1295,7 +1324,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   }
   __syncthreads();
   each_key<NT>(ks, false, true, [&](int j, int) {
-    const float x = (float)(ks.get_key(j) & 0xFFF);
+    const float x = (float)KeyFmt<K>::x(ks.get_key(j));
     const int ni = min((int)(x / G.hx), nini - 1);
     ks.set_lab(j, ni);
     atomicAdd(&A.cnt[ni], 1);
@@ -1528,8 +1557,8 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   for (int i = tid; i < size; i += NT) best[i] = 0;
   __syncthreads();
   each_key<NT>(ks, true, false, [&](int j, int k) {
-    const uint32_t key = ks.get_key(j);
-    atomicMax(&best[ks.get_lab(j)], ((key >> 24) << 24) | (0xFFFFFFu - (unsigned)k));
+    const K key = ks.get_key(j);
+    atomicMax(&best[ks.get_lab(j)], (KeyFmt<K>::score(key) << 24) | (0xFFFFFFu - (unsigned)k));
   });
   __syncthreads();
   for (int i = tid; i < size; i += NT) {
@@ -1540,11 +1569,11 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
 }
 
 
-template <int NT>
+template <int NT, class K>
 __global__ __launch_bounds__(NT) void k_octree(
     const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
-    const CellGeom* __restrict__ cells, const uint32_t* __restrict__ cand, int cand_total,
-    uint32_t* __restrict__ lin, int* __restrict__ label, uint32_t* __restrict__ okey,
+    const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
+    K* __restrict__ lin, int* __restrict__ label, K* __restrict__ okey,
     int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
     int level_base) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -1596,19 +1625,19 @@ __global__ __launch_bounds__(NT) void k_octree(
   const int n = block_scan_excl<NT>(cpre, G.ncells, s_tmp);
   if (tid == 0) cpre[G.ncells] = n;  // cell c holds keys cpre[c] .. cpre[c + 1] - 1
   __syncthreads();
-  uint32_t* outk = okey + (int64_t)img * kp_total + G.kp_off;
+  K* outk = okey + (int64_t)img * kp_total + G.kp_off;
   if (n == 0) {
     if (tid == 0) *oc = 0;
     return;
   }
-  const uint32_t* cb = cand + (int64_t)img * cand_total;
-  uint32_t* keys = lin + (int64_t)img * cand_total + G.cand_off;
+  const K* cb = cand + (int64_t)img * cand_total;
+  K* keys = lin + (int64_t)img * cand_total + G.cand_off;
   int* lab = label + (int64_t)img * cand_total + G.cand_off;
   int top = 1;  // largest power of two <= ncells
   while (2 * top <= G.ncells) top *= 2;
   // keys k0 + tid + NT j (j < kOctRegKeys), 0 past n; a key's cell is the last one starting at
   // or before it (cells without keys share their successor's start)
-  auto load_keys = [&](int k0, uint32_t(&v)[kOctRegKeys]) {
+  auto load_keys = [&](int k0, K(&v)[kOctRegKeys]) {
     int cs[kOctRegKeys];
 #pragma unroll
     for (int j = 0; j < kOctRegKeys; j++) cs[j] = 0;
@@ -1622,12 +1651,12 @@ __global__ __launch_bounds__(NT) void k_octree(
 #pragma unroll
     for (int j = 0; j < kOctRegKeys; j++) {
       const int k = k0 + tid + NT * j, c = cs[j];
-      v[j] = k < n ? cb[s_slot[c] + k - cpre[c]] : 0u;
+      v[j] = k < n ? cb[s_slot[c] + k - cpre[c]] : K(0);
     }
   };
   OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, pk, s_tmp64, outk, oc};
   if (n <= kOctRegKeys * NT) {  // keys + labels in registers: every pass stays on-chip
-    RegKeys<NT> ks;
+    RegKeys<NT, K> ks;
     ks.n = n;
     load_keys(0, ks.key);
 #pragma unroll
@@ -1639,7 +1668,7 @@ __global__ __launch_bounds__(NT) void k_octree(
     octree_core<NT>(G, X, ks, keys);
   } else {  // keys + labels in global scratch, processed in register chunks
     for (int k0 = 0; k0 < n; k0 += NT * kOctRegKeys) {
-      uint32_t v[kOctRegKeys];
+      K v[kOctRegKeys];
       load_keys(k0, v);
 #pragma unroll
       for (int j = 0; j < kOctRegKeys; j++) {
@@ -1647,7 +1676,7 @@ __global__ __launch_bounds__(NT) void k_octree(
         if (k < n) keys[k] = v[j];
       }
     }
-    MemKeys<NT> ks;
+    MemKeys<NT, K> ks;
     ks.keys = keys;
     ks.labs = lab;
     ks.n = n;
@@ -1666,9 +1695,10 @@ struct KpOffsets {  // per-level first keypoint slot (LevelGeom::kp_off), by val
   int off[kMaxLevels + 1];
 };
 
+template <class K>
 __global__ __launch_bounds__(256) void k_describe(
     const uint8_t* __restrict__ pyr, int64_t pyr_bytes, const uint8_t* __restrict__ blur,
-    const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const uint32_t* __restrict__ okey,
+    const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const K* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
   // dwords per staged row: raw 31+3 bytes rounded up; blurred 16-B pieces from a 16-B aligned
@@ -1697,14 +1727,14 @@ __global__ __launch_bounds__(256) void k_describe(
   // the count, the key and the level's fields in one round of loads, pinned in registers (a
   // rematerialised load of G per patch row would serialise the patch loads behind it)
   int noc = oc[level];
-  uint32_t key = okey[(int64_t)img * kp_total + min(slot, kp_total - 1)];
+  K key = okey[(int64_t)img * kp_total + min(slot, kp_total - 1)];
   int pitch = G.pitch, pyr_off = (int)G.pyr_off;
   float lscale = G.scale, lsize = G.size;
   asm volatile("" : "+v"(noc), "+v"(key), "+v"(pitch), "+v"(pyr_off), "+v"(lscale), "+v"(lsize));
   const bool active = slot < kp_total && idx < noc;  // uniform within the half-wave
   if (!active) key = 0;
-  const int cx = active ? (int)(key & 0xFFF) + (kEdge - 3) : 0;
-  const int cy = active ? (int)((key >> 12) & 0xFFF) + (kEdge - 3) : 0;
+  const int cx = active ? KeyFmt<K>::x(key) + (kEdge - 3) : 0;
+  const int cy = active ? KeyFmt<K>::y(key) + (kEdge - 3) : 0;
   // stage both patches with aligned dword loads issued together: the raw 31 x 31 patch
   // (IC_Angle, radius 15) and the blurred 37 x 37 patch (rBRIEF samples, radius <= 18)
   const uint8_t* L = pyr + (int64_t)img * pyr_bytes + pyr_off;
@@ -1786,7 +1816,7 @@ __global__ __launch_bounds__(256) void k_describe(
     k.y = level ? (float)(cy) * lscale : (float)cy;
     k.size = lsize;
     k.angle = angle;
-    k.response = (float)(key >> 24);
+    k.response = (float)KeyFmt<K>::score(key);
     k.octave = level;
     k.class_id = -1;
     kps[o] = k;
@@ -1815,7 +1845,8 @@ struct orbx_plan {
   uint8_t* d_vmap = nullptr;
   uint64_t* d_bitmaps = nullptr;
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
-  uint32_t *d_cand = nullptr, *d_lin = nullptr, *d_okey = nullptr;
+  // candidate keys, the octree's gathered keys and the retained keys: u32 or u64 (wide_keys)
+  void *d_cand = nullptr, *d_lin = nullptr, *d_okey = nullptr;
   int *d_cell_counts = nullptr, *d_label = nullptr, *d_ocount = nullptr, *d_counts = nullptr;
   int *d_fb_count = nullptr, *d_fb_list = nullptr;  // k_fast_fallback queue per image
   orbx_keypoint* d_kps = nullptr;
@@ -1941,9 +1972,53 @@ int orbx::launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, 
 
 namespace {
 
-int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
+// k_fast_cells, k_octree and k_describe on K-wide candidate keys (KeyFmt)
+template <class K>
+void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, int st_desc) {
   const Geometry& g = P->g;
   const int L = g.nlevels;
+  const int ncells = (int)g.cells.size();
+  K *cand = (K*)P->d_cand, *lin = (K*)P->d_lin, *okey = (K*)P->d_okey;
+  if (ncells > 0 && !P->fast_legacy) {
+    // cells per wave: up to kCellsPerWave while the launch keeps >= 16 k waves in flight
+    int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
+    if (P->fc_cpw > 0) cpw = P->fc_cpw;
+    if (P->n_cells_small > 0)
+      hipLaunchKernelGGL((k_fast_cells<44, 44, K>),
+                         dim3((P->n_cells_small + 4 * cpw - 1) / (4 * cpw), n), dim3(256), 0,
+                         P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
+                         P->n_cells_small, ncells, g.ini_th, g.min_th, cand, g.cand_total,
+                         P->d_cell_counts, cpw);
+    if (P->n_cells_big > 0)
+      hipLaunchKernelGGL((k_fast_cells<72, kCellMax, K>), dim3((P->n_cells_big + 3) / 4, n), dim3(256),
+                         0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_big,
+                         P->n_cells_big, ncells, g.ini_th, g.min_th, cand, g.cand_total,
+                         P->d_cell_counts, 1);
+    pr.mark(P->stream, st_fcell);
+  }
+  // levels [0, oct_split) on 1024-thread workgroups with the large LDS carve, the others on
+  // 256-thread ones sized for themselves (several per CU)
+  if (P->oct_split > 0)
+    hipLaunchKernelGGL((k_octree<kOctNTBig, K>), dim3(n, P->oct_split), dim3(kOctNTBig),
+                       P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
+                       cand, g.cand_total, lin, P->d_label, okey, P->d_ocount,
+                       g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0);
+  if (P->oct_split < L)
+    hipLaunchKernelGGL((k_octree<kOctNT, K>), dim3(n, L - P->oct_split), dim3(kOctNT), P->oct_smem,
+                       P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, cand,
+                       g.cand_total, lin, P->d_label, okey, P->d_ocount, g.kp_total, L,
+                       P->oct_nc, P->oct_cc, P->oct_split);
+  pr.mark(P->stream, st_oct);
+  KpOffsets ko{};
+  for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
+  hipLaunchKernelGGL(k_describe<K>, dim3((g.kp_total + 7) / 8, n), dim3(256), 0, P->stream,
+                     P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, ko, okey, P->d_ocount,
+                     g.kp_total, P->d_kps, P->d_desc, P->d_counts);
+  pr.mark(P->stream, st_desc);
+}
+
+int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
+  const Geometry& g = P->g;
   Profiler dummy;
   Profiler& pr = prof ? *prof : dummy;
   const int st_pyr = pr.stage("k_pyramid"),
@@ -1963,61 +2038,31 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
     pr.mark(P->stream, st_blur);
   }
   const int ncells = (int)g.cells.size();
-  if (ncells > 0 && !P->fast_legacy) {
-    // cells per wave: up to kCellsPerWave while the launch keeps >= 16 k waves in flight
-    int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
-    if (P->fc_cpw > 0) cpw = P->fc_cpw;
-    if (P->n_cells_small > 0)
-      hipLaunchKernelGGL((k_fast_cells<44, 44>),
-                         dim3((P->n_cells_small + 4 * cpw - 1) / (4 * cpw), n), dim3(256), 0,
-                         P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
-                         P->n_cells_small, ncells, g.ini_th, g.min_th, P->d_cand, g.cand_total,
-                         P->d_cell_counts, cpw);
-    if (P->n_cells_big > 0)
-      hipLaunchKernelGGL((k_fast_cells<72, kCellMax>), dim3((P->n_cells_big + 3) / 4, n), dim3(256),
-                         0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_big,
-                         P->n_cells_big, ncells, g.ini_th, g.min_th, P->d_cand, g.cand_total,
-                         P->d_cell_counts, 1);
-    pr.mark(P->stream, st_fcell);
-  } else if (ncells > 0) {
+  if (ncells > 0 && P->fast_legacy) {
+    uint32_t* cand = (uint32_t*)P->d_cand;  // (legacy plans are never wide_keys)
     hipLaunchKernelGGL(P->fast_pair ? k_fast_tile<true> : k_fast_tile<false>, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
                        g.ini_th, P->d_fb_count);
     pr.mark(P->stream, st_fs);
     hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 4 * kCompactK - 1) / (4 * kCompactK), n),
                        dim3(256), 0, P->stream,
-                       P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, P->d_cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
+                       P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
                        P->d_fb_list);
     pr.mark(P->stream, st_fast);
     hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
                        P->d_pyr, g.pyr_bytes, P->d_cells, ncells, P->d_fb_count,
-                       P->d_fb_list, g.min_th, P->d_cand, g.cand_total, P->d_cell_counts);
+                       P->d_fb_list, g.min_th, cand, g.cand_total, P->d_cell_counts);
     if (P->has_fb_big)  // (a plan without such cells would launch waves that find the queue empty)
       hipLaunchKernelGGL((k_fast_fallback<72, kCellMax>), dim3(kFbWG / 4, n), dim3(256), 0,
                        P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, ncells,
-                       P->d_fb_count, P->d_fb_list, g.min_th, P->d_cand, g.cand_total,
+                       P->d_fb_count, P->d_fb_list, g.min_th, cand, g.cand_total,
                        P->d_cell_counts);
     pr.mark(P->stream, st_fb);
   }
-  // levels [0, oct_split) on 1024-thread workgroups with the large LDS carve, the others on
-  // 256-thread ones sized for themselves (several per CU)
-  if (P->oct_split > 0)
-    hipLaunchKernelGGL(k_octree<kOctNTBig>, dim3(n, P->oct_split), dim3(kOctNTBig),
-                       P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
-                       P->d_cand, g.cand_total, P->d_lin, P->d_label, P->d_okey, P->d_ocount,
-                       g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0);
-  if (P->oct_split < L)
-    hipLaunchKernelGGL(k_octree<kOctNT>, dim3(n, L - P->oct_split), dim3(kOctNT), P->oct_smem,
-                       P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, P->d_cand,
-                       g.cand_total, P->d_lin, P->d_label, P->d_okey, P->d_ocount, g.kp_total, L,
-                       P->oct_nc, P->oct_cc, P->oct_split);
-  pr.mark(P->stream, st_oct);
-  KpOffsets ko{};
-  for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
-  hipLaunchKernelGGL(k_describe, dim3((g.kp_total + 7) / 8, n), dim3(256), 0, P->stream,
-                     P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, ko, P->d_okey, P->d_ocount,
-                     g.kp_total, P->d_kps, P->d_desc, P->d_counts);
-  pr.mark(P->stream, st_desc);
+  if (g.wide_keys)
+    enqueue_keyed<uint64_t>(P, n, pr, st_fcell, st_oct, st_desc);
+  else
+    enqueue_keyed<uint32_t>(P, n, pr, st_fcell, st_oct, st_desc);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return report_hip(e, "extract launch");
   return ORBX_OK;
@@ -2088,15 +2133,19 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->n_cells_small = (int)cells_small.size();
   P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;
+  if (g.wide_keys && P->fast_legacy) return fail(ORBX_EUNSUPPORTED);  // 32-bit keys only
+  const size_t ksz = g.wide_keys ? 8 : 4;  // bytes per candidate key
   if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, g.cells.size()) ||
       dalloc(&P->d_xtap, g.xtap.size() / 2) || dalloc(&P->d_ytap, g.ytap.size() / 2) ||
       dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_bands, g.bands.size()) || dalloc(&P->d_ftiles, ftiles.size()) ||
-      dalloc(&P->d_vmap, B * g.pyr_bytes) || dalloc(&P->d_bitmaps, B * g.bm_words) ||
+      dalloc(&P->d_vmap, P->fast_legacy ? B * g.pyr_bytes : 1) ||
+      dalloc(&P->d_bitmaps, P->fast_legacy ? B * g.bm_words : 1) ||
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
-      dalloc(&P->d_cand, B * g.cand_total) || dalloc(&P->d_lin, B * g.cand_total) ||
+      dalloc((char**)&P->d_cand, B * g.cand_total * ksz) ||
+      dalloc((char**)&P->d_lin, B * g.cand_total * ksz) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
       dalloc(&P->d_fb_count, 2 * kFbStride * B) || dalloc(&P->d_fb_list, 2 * B * g.cells.size()) ||
-      dalloc(&P->d_okey, B * g.kp_total) || dalloc(&P->d_ocount, B * g.nlevels) ||
+      dalloc((char**)&P->d_okey, B * g.kp_total * ksz) || dalloc(&P->d_ocount, B * g.nlevels) ||
       dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_big, cells_big.size()))
     return fail(ORBX_ENOMEM);
   {
@@ -2144,17 +2193,21 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   // scratch.  The dynamic-LDS attribute is per function and shared by every plan of the
   // process: only ever raised.
   static size_t attr_small = 0, attr_big = 0;  // guarded by the resource lock
+  auto raise = [](const void* f32, const void* f64, size_t bytes) {
+    return hipFuncSetAttribute(f32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
+               hipSuccess &&
+           hipFuncSetAttribute(f64, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
+               hipSuccess;
+  };
   if (P->oct_smem > attr_small) {
-    if (hipFuncSetAttribute((const void*)k_octree<kOctNT>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)P->oct_smem) != hipSuccess)
+    if (!raise((const void*)k_octree<kOctNT, uint32_t>, (const void*)k_octree<kOctNT, uint64_t>,
+               P->oct_smem))
       return fail(ORBX_EDEVICE);
     attr_small = P->oct_smem;
   }
   if (P->oct_smem_big > attr_big) {
-    if (hipFuncSetAttribute((const void*)k_octree<kOctNTBig>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)P->oct_smem_big) != hipSuccess)
+    if (!raise((const void*)k_octree<kOctNTBig, uint32_t>,
+               (const void*)k_octree<kOctNTBig, uint64_t>, P->oct_smem_big))
       return fail(ORBX_EDEVICE);
     attr_big = P->oct_smem_big;
   }

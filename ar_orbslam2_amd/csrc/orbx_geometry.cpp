@@ -253,6 +253,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
   g->min_th = std::min(std::max(p.min_th_fast, 0), 255);
   g->cells.clear();
   g->bm_words = 0;
+  g->wide_keys = false;
   for (int l = 0; l < p.nlevels; l++) {
     LevelGeom& L = g->lv[l];
     L = LevelGeom{};
@@ -324,10 +325,13 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
         return ORBX_EUNSUPPORTED;
       }
       L.hx = static_cast<float>(L.W) / L.nini;
-      if (L.W >= 4096 || L.H >= 4096) {
-        if (why) *why = "level too large for 12-bit key packing";
+      // candidate keys: x:12 y:12 in a u32 up to 4095 px, x:16 y:16 in a u64 above (the
+      // node and cell bounds are int16)
+      if (L.W > 32767 || L.H > 32767) {
+        if (why) *why = "level wider or taller than 32767 px";
         return ORBX_EUNSUPPORTED;
       }
+      g->wide_keys |= L.W >= 4096 || L.H >= 4096;
     }
     L.ncells = (int)g->cells.size() - L.cell_begin;
     L.cand_cap = cand - L.cand_off;

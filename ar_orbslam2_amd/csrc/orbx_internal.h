@@ -118,6 +118,7 @@ struct Geometry {
   int cand_total = 0;                 // per image candidate keys
   int kp_total = 0;                   // per image final keypoint slots
   int node_cap_max = 0;
+  bool wide_keys = false;             // an octree frame >= 4096 px: 64-bit candidate keys
   float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
   int feats[kMaxLevels];
   int umax[kHalfPatch + 1];

@@ -178,3 +178,14 @@ def test_wide_frames_many_initial_octree_nodes(w, h):
     img = synth.frame(w, h, 1, 3) if w <= 2600 else rng.integers(0, 256, (h, w), dtype=np.uint8)
     kps = _compare(img, 1500)
     assert len(kps) > 100
+
+
+@pytest.mark.parametrize("w,h,nf", [(4400, 500, 2000), (4200, 4200, 4000)])
+def test_levels_wider_than_4095_px(w, h, nf):
+    """Octree frames of 4096 px and more (level 0 of a frame wider or taller than ~4134 px)
+    switch the plan to 64-bit candidate keys (x:16 y:16 score:8); round 2 returned
+    ORBX_EUNSUPPORTED there, the reference has no limit (ORBextractor.cc:1047-1072, 525-733)."""
+    img = synth.frame(w, h, 1, 3)
+    kps = _compare(img, nf)
+    assert len(kps) > nf // 2
+    assert (kps["x"] > 4096).any() if w > 4096 else True
