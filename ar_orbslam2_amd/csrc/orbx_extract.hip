@@ -1201,6 +1201,7 @@ constexpr int kOctNTBig = 1024;       // for frames whose level-0 octree frame e
 constexpr int kOctBigArea = 1 << 20;  // kOctBigArea px: a workgroup holds ~100 KB of LDS there
                                       // (one per CU), so 1024 threads run its key passes 4x wide
 constexpr int kOctRegKeys = 16;       // keys per thread per register chunk
+constexpr size_t kOctMaxSmem = 150 * 1024;  // dynamic LDS of one octree workgroup
 
 struct OctNodes {
   int16_t *x0, *x1, *y0, *y1;
@@ -1575,7 +1576,7 @@ __global__ __launch_bounds__(NT) void k_octree(
     const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
     K* __restrict__ lin, int* __restrict__ label, K* __restrict__ okey,
     int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
-    int level_base) {
+    int level_base, int* __restrict__ cell_scr) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_tmp[NT / 64 + 1];
   __shared__ int s_misc[8];
@@ -1608,9 +1609,12 @@ __global__ __launch_bounds__(NT) void k_octree(
   int* t2 = (int*)take(4 * NC);
   int* t3 = (int*)take(4 * NC);
   int* t4 = (int*)take(4 * NC);
-  int* cpre = (int*)take(4 * (cell_cap + 1));
+  // per-cell key starts and slots: in LDS, or (cell_cap == 0: levels with too many cells for
+  // it) in this (image, level)'s part of cell_scr, [2 (ncells + nlevels)] ints per image
+  int* cpre = cell_cap > 0 ? (int*)take(4 * (cell_cap + 1))
+                           : cell_scr + (int64_t)img * 2 * (ncells + nlevels) + 2 * (G.cell_begin + level);
   uint64_t* pk = (uint64_t*)take(8 * NC);
-  int* s_slot = (int*)take(4 * cell_cap);
+  int* s_slot = cell_cap > 0 ? (int*)take(4 * cell_cap) : cpre + G.ncells + 1;
   __shared__ uint64_t s_tmp64[NT / 64 + 1];
 
   // 1. gather candidates of this level in cell order (vToDistributeKeys): counts and slots of
@@ -1859,7 +1863,8 @@ struct orbx_plan {
   // theirs, so small levels no longer hold a whole CU each
   int oct_split = 0;
   size_t oct_smem = 0, oct_smem_big = 0;
-  int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;
+  int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;  // oct_cc* 0: cells in d_cell_scr
+  int* d_cell_scr = nullptr;
   int cell_cap = 0;
   bool has_fb_big = false;  // some cell's ROI needs k_fast_fallback<72, kCellMax>
   // k_fast_cells: the cells of its <44, 44> and <72, kCellMax> instances
@@ -2002,12 +2007,12 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
     hipLaunchKernelGGL((k_octree<kOctNTBig, K>), dim3(n, P->oct_split), dim3(kOctNTBig),
                        P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
                        cand, g.cand_total, lin, P->d_label, okey, P->d_ocount,
-                       g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0);
+                       g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0, P->d_cell_scr);
   if (P->oct_split < L)
     hipLaunchKernelGGL((k_octree<kOctNT, K>), dim3(n, L - P->oct_split), dim3(kOctNT), P->oct_smem,
                        P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, cand,
                        g.cand_total, lin, P->d_label, okey, P->d_ocount, g.kp_total, L,
-                       P->oct_nc, P->oct_cc, P->oct_split);
+                       P->oct_nc, P->oct_cc, P->oct_split, P->d_cell_scr);
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
@@ -2176,7 +2181,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   auto oct_bytes = [&](size_t NC, size_t CC) {
     return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
-           r16(4 * (CC + 1)) + r16(8 * NC) + r16(4 * CC);
+           (CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0) + r16(8 * NC);
   };
   while (P->oct_split < g.nlevels && (int64_t)g.lv[P->oct_split].W * g.lv[P->oct_split].H > kOctBigArea)
     P->oct_split++;
@@ -2186,9 +2191,15 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     nc = std::max(nc, g.lv[l].node_cap);
     cc = std::max(cc, g.lv[l].ncells);
   }
+  // a level with more cells than fit beside its nodes keeps its cell table in global scratch
+  if (oct_bytes(P->oct_nc, P->oct_cc) > kOctMaxSmem) P->oct_cc = 0;
+  if (oct_bytes(P->oct_nc_big, P->oct_cc_big) > kOctMaxSmem) P->oct_cc_big = 0;
+  if ((P->oct_cc == 0 || (P->oct_split && P->oct_cc_big == 0)) &&
+      dalloc(&P->d_cell_scr, B * 2 * (g.cells.size() + g.nlevels)))
+    return fail(ORBX_ENOMEM);
   P->oct_smem = oct_bytes(P->oct_nc, P->oct_cc);
   P->oct_smem_big = P->oct_split ? oct_bytes(P->oct_nc_big, P->oct_cc_big) : 0;
-  if (std::max(P->oct_smem, P->oct_smem_big) > 150 * 1024) return fail(ORBX_EUNSUPPORTED);
+  if (std::max(P->oct_smem, P->oct_smem_big) > kOctMaxSmem) return fail(ORBX_EUNSUPPORTED);
   // keys and labels live in registers (up to kOctRegKeys * threads per level) or in global
   // scratch.  The dynamic-LDS attribute is per function and shared by every plan of the
   // process: only ever raised.
@@ -2221,7 +2232,7 @@ int orbx_plan_destroy(orbx_plan* P) {
   P->graphs.clear(P->stream);
   void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xtap,   P->d_ytap,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
                   P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label, P->d_fb_count, P->d_fb_list,
-                  P->d_ocount, P->d_cells_small, P->d_cells_big,
+                  P->d_ocount, P->d_cells_small, P->d_cells_big, P->d_cell_scr,
                   P->d_counts /* base of kps and desc too */};
   for (void* p : ptrs)
     if (p) hipFree(p);

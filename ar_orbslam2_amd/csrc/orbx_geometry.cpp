@@ -145,13 +145,11 @@ int build_pyramid(Geometry* g, std::string* why) {
     }
     if (l > 0) {
       const LevelGeom& P = g->lv[l - 1];
-      // cv::resize switches INTER_LINEAR to INTER_AREA at an exact 2x2 decimation; not
-      // implemented (the reference configurations use scaleFactor 1.2).
-      const double sx = 1. / ((double)L.w / P.w), sy = 1. / ((double)L.h / P.h);
-      if (fabs(sx - 2) < 2.2e-16 && fabs(sy - 2) < 2.2e-16) {
-        if (why) *why = "exact 2x decimation (INTER_AREA path)";
-        return ORBX_EUNSUPPORTED;
-      }
+      // cv::resize (OpenCV 2.4.9, the version the reference links) switches INTER_LINEAR to
+      // the fast INTER_AREA path at an exact 2x2 decimation: (a + b + c + d + 2) >> 2 per
+      // output pixel.  The linear taps at that scale are 1024 / 1024 in both passes, and both
+      // of OpenCV's vertical paths (SSE2 mulhi of the >>4 sums, scalar >>22) round that same
+      // way, so the tables below produce it unchanged (tests/test_oracle_kat.py).
       if (!resize_tables(P.w, P.h, L.w, L.h, g, &L)) {
         if (why) *why = "resize coefficients outside [0, 2048]";
         return ORBX_EUNSUPPORTED;
@@ -335,6 +333,10 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     }
     L.ncells = (int)g->cells.size() - L.cell_begin;
     L.cand_cap = cand - L.cand_off;
+    if (L.cand_cap >= (1 << 24)) {  // k_octree's retention packs a level's key index in 24 bits
+      if (why) *why = "level candidate capacity exceeds 2^24";
+      return ORBX_EUNSUPPORTED;
+    }
     ncmax = std::max(ncmax, L.ncells);
     L.node_cap = L.ncells ? std::max(L.nfeat + 3, 4 * L.nini + 4) : 1;
     L.kp_off = kp;
@@ -342,10 +344,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     kp += L.kp_cap;
     g->node_cap_max = std::max(g->node_cap_max, L.node_cap);
   }
-  if (cand >= (1 << 24)) {
-    if (why) *why = "candidate capacity exceeds 2^24";
-    return ORBX_EUNSUPPORTED;
-  }
+
   g->cand_total = cand;
   g->kp_total = kp;
   (void)ncmax;

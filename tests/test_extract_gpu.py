@@ -189,3 +189,13 @@ def test_levels_wider_than_4095_px(w, h, nf):
     kps = _compare(img, nf)
     assert len(kps) > nf // 2
     assert (kps["x"] > 4096).any() if w > 4096 else True
+
+
+@pytest.mark.parametrize("w,h,nlevels", [(640, 480, 6), (752, 480, 8)])
+def test_scale_factor_exactly_two(w, h, nlevels):
+    """scaleFactor 2: cv::resize takes its fast INTER_AREA path at the exact 2x2 decimations
+    (OpenCV 2.4.9), which the linear taps reproduce (tests/test_oracle_kat.py); round 2 returned
+    ORBX_EUNSUPPORTED here.  752 x 480 mixes exact levels with non-exact ones (47 -> 24)."""
+    img = synth.frame(w, h, 1, 3)
+    kps = _compare(img, 1000, scale=2.0, nlevels=nlevels)
+    assert len(kps) > 300

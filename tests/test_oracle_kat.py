@@ -121,6 +121,20 @@ def test_resize_vertical_paths_differ_only_by_one():
     assert np.abs(out - ref).max() <= 1.01
 
 
+@pytest.mark.parametrize("w,h", [(640, 480), (100, 60), (74, 38), (2, 2), (36, 1000)])
+def test_exact_2x_decimation_is_area_fast(w, h):
+    """OpenCV 2.4.9 (the version the reference links: ORB_SLAM2/build/CMakeFiles/ORB_SLAM2.dir/
+    link.txt) runs cv::resize INTER_LINEAR at an exact 2x2 decimation as the fast INTER_AREA
+    path, (a + b + c + d + 2) >> 2 per pixel.  The linear restatement gives the same bytes there
+    (taps 1024 / 1024 in both passes, both vertical paths), so scaleFactor 2 needs no path of
+    its own."""
+    src = np.random.default_rng(w * h).integers(0, 256, (h, w), dtype=np.uint8)
+    got = O.resize_linear(src, w // 2, h // 2)
+    s = src.astype(np.int32)
+    area = (s[0::2, 0::2] + s[0::2, 1::2] + s[1::2, 0::2] + s[1::2, 1::2] + 2) >> 2
+    assert np.array_equal(got, area.astype(np.uint8))
+
+
 @pytest.mark.parametrize("y,x,deg", [(0, 1, 0.0), (1, 0, 90.0), (0, -1, 180.0), (-1, 0, 270.0),
                                      (0, 0, 0.0)])
 def test_fast_atan2_axes(y, x, deg):
