@@ -132,7 +132,7 @@ int orbx_extract(orbx_extractor* ex, const uint8_t* img, int32_t w, int32_t h, i
     return ORBX_OK;
   });
   if (rc != ORBX_OK) return rc;
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   ex->has_run = true;
   const int32_t n = *(const int32_t*)ex->h_out;
   *n_out = n;
@@ -216,12 +216,12 @@ int orbx_stereo_matches(orbx_extractor* left, orbx_extractor* right, float mb, f
   if (rc) return rc;
   int32_t n = 0;
   ORBX_HIP(hipMemcpyAsync(&n, vl.d_counts, 4, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   (void)ocnt;
   if (n > 0) {
     ORBX_HIP(hipMemcpyAsync(uright, base + ouse, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipMemcpyAsync(depth, base + odep, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipStreamSynchronize(s));
+    ORBX_HIP(orbx::wait_stream(s));
   }
   if (n_out) *n_out = n;
   return ORBX_OK;

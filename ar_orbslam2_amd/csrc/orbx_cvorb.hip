@@ -1214,14 +1214,14 @@ int orbx_cvorb_detect(orbx_cvorb* o, const uint8_t* img, int32_t w, int32_t h, i
   if (rc != ORBX_OK) return rc;
   int32_t n = 0;
   ORBX_HIP(hipMemcpyAsync(&n, P->d_counts, 4, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   if (n < 0) return ORBX_ECAPACITY;  // cannot happen with exact capacity
   *n_out = n;
   if (n > cap) return ORBX_ECAPACITY;
   if (n > 0) {
     ORBX_HIP(hipMemcpyAsync(kps, P->d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipMemcpyAsync(desc, P->d_desc, (size_t)32 * n, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipStreamSynchronize(s));
+    ORBX_HIP(orbx::wait_stream(s));
   }
   return ORBX_OK;
 }
@@ -1242,7 +1242,7 @@ int orbx_cvorb_outputs(orbx_cvorb* o, orbx_keypoint** d_kps, uint8_t** d_desc,
 
 int orbx_cvorb_sync(orbx_cvorb* o) {
   if (!o) return ORBX_EINVAL;
-  ORBX_HIP(hipStreamSynchronize(o->tp->stream));
+  ORBX_HIP(orbx::wait_stream(o->tp->stream));
   return ORBX_OK;
 }
 
@@ -1267,7 +1267,7 @@ int orbx_bf_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_
   if (rc) return rc;
   std::vector<int2> best(nq);
   ORBX_HIP(hipMemcpyAsync(best.data(), base + ob, (size_t)nq * 8, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   for (int i = 0; i < nq; i++) out[i] = {i, best[i].x, 0, (float)best[i].y};
   *n_out = nq;
   return ORBX_OK;
@@ -1319,7 +1319,7 @@ int orbx_nn_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_
     ORBX_HIP(hipMemcpyAsync(best.data(), base + ob, (size_t)nq * 8, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipMemcpyAsync(second.data(), base + os, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipMemcpyAsync(ext, base + oe, 8, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipStreamSynchronize(s));
+    ORBX_HIP(orbx::wait_stream(s));
   } else {
     for (int i = 0; i < nq; i++) best[i] = make_int2(-1, INT_MAX), second[i] = INT_MAX;
   }
@@ -1428,7 +1428,7 @@ int orbx_marker_destroy(orbx_marker* M) {
 int orbx_marker_set_target(orbx_marker* M, const uint8_t* desc, int32_t n) {
   if (!M || n < 0 || (n > 0 && !desc)) return ORBX_EINVAL;
   ORBX_HIP(hipSetDevice(M->device));
-  ORBX_HIP(hipStreamSynchronize(M->plan->stream));
+  ORBX_HIP(orbx::wait_stream(M->plan->stream));
   if (n > M->match_cap) {
     void* bufs[] = {M->d_target, M->d_best, M->d_matches, M->d_good};
     for (void* b : bufs)
@@ -1464,7 +1464,7 @@ int orbx_marker_run(orbx_marker* M, const uint8_t* d_imgs, int32_t n) {
 
 int orbx_marker_sync(orbx_marker* M) {
   if (!M) return ORBX_EINVAL;
-  ORBX_HIP(hipStreamSynchronize(M->plan->stream));
+  ORBX_HIP(orbx::wait_stream(M->plan->stream));
   return ORBX_OK;
 }
 
@@ -1475,7 +1475,7 @@ int orbx_marker_results(orbx_marker* M, int32_t n, int32_t* kp_counts, int32_t* 
     ORBX_HIP(hipMemcpyAsync(kp_counts, M->plan->d_counts, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
   if (good_counts)
     ORBX_HIP(hipMemcpyAsync(good_counts, M->d_good_count, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   return ORBX_OK;
 }
 

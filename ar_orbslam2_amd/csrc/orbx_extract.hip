@@ -2085,6 +2085,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   orbx_plan* P = new (std::nothrow) orbx_plan();
   if (!P) return ORBX_ENOMEM;
   std::string why;
+  P->g.py_band_h = max_batch <= kPyFewImages ? kPyBandHSmall : kPyBandH;
   int rc = build_geometry(*params, w, h, &P->g, &why);
   if (rc != ORBX_OK) {
     fprintf(stderr, "[orbx] plan %dx%d unsupported: %s\n", w, h, why.c_str());
@@ -2134,7 +2135,11 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->nftiles = (int)ftiles.size();
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
   std::vector<int> cells_small, cells_big;
-  for (int c = 0; c < (int)g.cells.size(); c++) (g.cells[c].fb_big ? cells_big : cells_small).push_back(c);
+  // a few-image plan runs every cell in the <72, kCellMax> instance: one launch instead of two
+  // on the drop-in path's one-frame chain (either instance handles any cell)
+  const bool one_fast_launch = max_batch <= kPyFewImages;
+  for (int c = 0; c < (int)g.cells.size(); c++)
+    (g.cells[c].fb_big || one_fast_launch ? cells_big : cells_small).push_back(c);
   P->n_cells_small = (int)cells_small.size();
   P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;

@@ -5,6 +5,8 @@
 #include <math.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cstdlib>
 #include <cstdio>
 
@@ -19,6 +21,23 @@ static inline int cv_round(double v) { return (int)nearbyint(v); }  // cvRound: 
 int report_hip(hipError_t e, const char* what) {
   fprintf(stderr, "[orbx] HIP error %d (%s) at %s\n", (int)e, hipGetErrorString(e), what);
   return ORBX_EDEVICE;
+}
+
+hipError_t wait_stream(hipStream_t s) {
+  static const long spin_us = [] {
+    const char* e = getenv("ORBX_SPIN_US");
+    return e ? std::max(0L, atol(e)) : 2000L;
+  }();
+  if (spin_us > 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e != hipErrorNotReady) return e;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
+      std::this_thread::yield();
+    }
+  }
+  return hipStreamSynchronize(s);
 }
 
 std::recursive_mutex& resource_mutex() {
@@ -183,7 +202,7 @@ int build_pyramid(Geometry* g, std::string* why) {
     const int hs = g->lv[l0 - 1].h;
     std::vector<PyrBand> bands;
     int smem_cap = py_max_smem;  // raised to kPyMaxSmemLimit for rows too wide for it
-    for (int nb = std::max(1, hs / kPyBandH);; nb++) {
+    for (int nb = std::max(1, hs / g->py_band_h);; nb++) {
       bands.assign(nb, PyrBand{});
       int need[2] = {0, 0};
       for (int b = 0; b < nb; b++) {
@@ -210,7 +229,7 @@ int build_pyramid(Geometry* g, std::string* why) {
       if (nb >= hs) {
         if (smem_cap < kPyMaxSmemLimit) {  // one-row bands still too large: the larger carve
           smem_cap = kPyMaxSmemLimit;
-          nb = std::max(1, hs / kPyBandH) - 1;
+          nb = std::max(1, hs / g->py_band_h) - 1;
           continue;
         }
         if (why) *why = "image too wide for the pyramid bands";
@@ -225,7 +244,7 @@ int build_pyramid(Geometry* g, std::string* why) {
   }
   if (nl == 1) {  // level 0 alone: one copy stage
     PyrStage st{1, 0, 0, 0, 0, 0};
-    const int nb = std::max(1, g->lv[0].h / kPyBandH);
+    const int nb = std::max(1, g->lv[0].h / g->py_band_h);
     for (int b = 0; b < nb; b++) {
       PyrBand B{};
       B.own_lo[0] = B.lo[0] = (int)((int64_t)b * g->lv[0].h / nb);

@@ -39,6 +39,13 @@ constexpr int kHalfPatch = 15;  // HALF_PATCH_SIZE (:70)
 #define ORBX_PY_STAGEN 4
 #endif
 constexpr int kPyBandH = ORBX_PY_BANDH;  // source-level rows per band (more if LDS is short)
+#ifndef ORBX_PY_BANDH_SMALL
+#define ORBX_PY_BANDH_SMALL 8
+#endif
+// plans of at most kPyFewImages images (the drop-in extractor's batch of 1) use short bands:
+// more workgroups for one image's latency-chained level builds
+constexpr int kPyBandHSmall = ORBX_PY_BANDH_SMALL;
+constexpr int kPyFewImages = 4;
 constexpr int kPyNT = ORBX_PY_NT;        // k_pyramid threads per workgroup
 constexpr int kPyStage0 = ORBX_PY_STAGE0;  // levels built by the first stage (from the input)
 constexpr int kPyStageN = ORBX_PY_STAGEN;  // levels per later stage (from the pyramid)
@@ -119,6 +126,7 @@ struct Geometry {
   int kp_total = 0;                   // per image final keypoint slots
   int node_cap_max = 0;
   bool wide_keys = false;             // an octree frame >= 4096 px: 64-bit candidate keys
+  int py_band_h = kPyBandH;           // k_pyramid source rows per band (set before building)
   float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
   int feats[kMaxLevels];
   int umax[kHalfPatch + 1];
@@ -564,6 +572,11 @@ struct Profiler {
   } while (0)
 
 int report_hip(hipError_t e, const char* what);
+// Waits for a stream's work on the one-call (drop-in) paths: polls hipStreamQuery for up to
+// ORBX_SPIN_US microseconds (default 2000; 0 = block at once) before a blocking
+// hipStreamSynchronize — a blocking wait adds the runtime's interrupt wake-up latency to every
+// call, which for calls whose GPU work takes ~50-200 us is a large share.
+hipError_t wait_stream(hipStream_t s);
 // logs a library-detected error (stderr) and returns `code`
 int report(int code, const char* what);
 

@@ -86,15 +86,24 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
   // l + 64c); larger nodes (no limit in the reference) keep them in memory: mode 0 reads the
   // output itself (match[i2] >= 0), mode 1 the zeroed matched2 flags.
   const bool big = m > kBowRegCands;
-  // candidate descriptors of chunk 0 stay in registers
-  uint64_t reg[4] = {0, 0, 0, 0};
-  int i2_0 = -1;
-  bool ok0 = false;
-  if (lane < m) {
-    i2_0 = P.s2.node_feats[f0 + lane];
-    const uint64_t* p = (const uint64_t*)(P.s2.desc + (int64_t)i2_0 * 32);
-    reg[0] = p[0]; reg[1] = p[1]; reg[2] = p[2]; reg[3] = p[3];
-    ok0 = !kfkf || !P.s2.valid || P.s2.valid[i2_0];
+  // the candidates of chunks 0 .. kBowDescChunks-1 (positions lane + 64 c) stay in registers
+  // for the whole node: descriptor, index and validity (bit c of okr); later chunks of a larger
+  // node are read from memory per KF feature
+  uint64_t reg[kBowDescChunks][4];
+  int i2r[kBowDescChunks];
+  uint32_t okr = 0;
+#pragma unroll
+  for (int c = 0; c < kBowDescChunks; c++) {
+    const int jj = lane + 64 * c;
+    reg[c][0] = reg[c][1] = reg[c][2] = reg[c][3] = 0;
+    i2r[c] = -1;
+    if (jj < m) {
+      const int i2 = P.s2.node_feats[f0 + jj];
+      const uint64_t* p = (const uint64_t*)(P.s2.desc + (int64_t)i2 * 32);
+      reg[c][0] = p[0]; reg[c][1] = p[1]; reg[c][2] = p[2]; reg[c][3] = p[3];
+      i2r[c] = i2;
+      if (!kfkf || !P.s2.valid || P.s2.valid[i2]) okr |= 1u << c;
+    }
   }
   uint64_t matched = 0;  // bit c: candidate lane + 64c already matched in this call
   const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
@@ -121,25 +130,8 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
       const uint64_t d1[4] = {(uint64_t)__shfl((long long)dl0, j), (uint64_t)__shfl((long long)dl1, j),
                               (uint64_t)__shfl((long long)dl2, j), (uint64_t)__shfl((long long)dl3, j)};
       int b1 = 256, bp = 0x7FFFFFFF, b2 = 256;
-      for (int c = 0; c * 64 < m; c++) {
-        const int jj = lane + 64 * c;
-        if (jj >= m) continue;
-        if (!big && ((matched >> c) & 1)) continue;
-        const int i2 = c == 0 ? i2_0 : P.s2.node_feats[f0 + jj];
-        if (big && (kfkf ? __hip_atomic_load(P.matched2 + i2, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) != 0
-                         : __hip_atomic_load(P.match + i2, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) >= 0))
-          continue;
-        int dist;
-        if (c == 0) {
-          if (!ok0) continue;
-          uint64_t x[4] = {reg[0], reg[1], reg[2], reg[3]};
-          dist = hamming_regs(d1, (const uint8_t*)x);
-        } else {
-          if (kfkf && P.s2.valid && !P.s2.valid[i2]) continue;
-          dist = hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32);
-        }
+      // candidates in position order (lane + 64 c ascending per lane): strict < keeps the first
+      auto offer = [&](int dist, int jj) {
         if (dist < b1) {
           b2 = b1;
           b1 = dist;
@@ -147,6 +139,33 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
         } else if (dist < b2) {
           b2 = dist;
         }
+      };
+#pragma unroll
+      for (int c = 0; c < kBowDescChunks; c++) {
+        if (c * 64 >= m) break;  // wave-uniform
+        const int jj = lane + 64 * c;
+        if (!((okr >> c) & 1)) continue;
+        if (!big && ((matched >> c) & 1)) continue;
+        if (big && (kfkf ? __hip_atomic_load(P.matched2 + i2r[c], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) != 0
+                         : __hip_atomic_load(P.match + i2r[c], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) >= 0))
+          continue;
+        offer(__popcll(d1[0] ^ reg[c][0]) + __popcll(d1[1] ^ reg[c][1]) +
+                  __popcll(d1[2] ^ reg[c][2]) + __popcll(d1[3] ^ reg[c][3]), jj);
+      }
+      for (int c = kBowDescChunks; c * 64 < m; c++) {
+        const int jj = lane + 64 * c;
+        if (jj >= m) continue;
+        if (!big && ((matched >> c) & 1)) continue;
+        const int i2 = P.s2.node_feats[f0 + jj];
+        if (big && (kfkf ? __hip_atomic_load(P.matched2 + i2, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) != 0
+                         : __hip_atomic_load(P.match + i2, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) >= 0))
+          continue;
+        if (kfkf && P.s2.valid && !P.s2.valid[i2]) continue;
+        offer(hamming_regs(d1, P.s2.desc + (int64_t)i2 * 32), jj);
       }
       // wave merge of (best1, position, best2), what the sequential loop yields: the minimum
       // of the key (best1 << 23 | position) is best1 at its first position; best2 is then the
@@ -642,7 +661,7 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
   rc = launch_bow(dptr<BowProblem>(base, oprob), 1, s1->fv.n_nodes, s);
   if (rc) return rc;
   ORBX_HIP(tls_ws.download(omatch, ocount + 8 - omatch));  // match array and count / error
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   const int* res = (const int*)(tls_ws.h + ocount);
   if (res[1]) return report(ORBX_EDEVICE, "SearchByBoW: a match index outside the keyframe");
   if (nout > 0) memcpy(match_out, tls_ws.h + omatch, (size_t)nout * 4);
@@ -736,7 +755,7 @@ int orbx_search_for_triangulation(const orbx_tri_side* k1, const orbx_tri_side* 
   rc = launch_tri(dptr<TriProblem>(base, oprob), 1, k1->fv.n_nodes, s);
   if (rc) return rc;
   ORBX_HIP(tls_ws.download(opairs, ocount + 8 - opairs));  // pairs and count / error
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   const int* res = (const int*)(tls_ws.h + ocount);
   if (res[1]) return report(ORBX_EDEVICE, "SearchForTriangulation: a match index outside KF2");
   const int cnt = res[0];
@@ -777,7 +796,7 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int3
                      dptr<int>(base, oo));
   ORBX_HIP(hipGetLastError());
   ORBX_HIP(hipMemcpyAsync(out, base + oo, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   return ORBX_OK;
 }
 
@@ -829,7 +848,7 @@ int orbx_debug_match_finish(int32_t kind, int32_t n1, int32_t n2, const int32_t*
   int res[2] = {0, 0};
   ORBX_HIP(hipMemcpyAsync(res, base + ocount, 8, hipMemcpyDeviceToHost, s));
   if (n > 0) ORBX_HIP(hipMemcpyAsync(out, base + om, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   *nmatches = res[0];
   return res[1] ? ORBX_EDEVICE : ORBX_OK;
 }

@@ -744,7 +744,7 @@ int run_projection(const orbx_proj_frame* f, ProjPointsDev P, const std::vector<
     const int nout = ic ? ic->n1 : f->n;
     if (nout > 0)
       ORBX_HIP(hipMemcpyAsync(match, base + omatch, 4 * (size_t)nout, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipStreamSynchronize(s));
+    ORBX_HIP(orbx::wait_stream(s));
     if ((size_t)(unsigned)used > pool_cap) {  // some list did not fit: rerun with the total
       pool_cap = (size_t)(unsigned)used;
       continue;
@@ -752,7 +752,7 @@ int run_projection(const orbx_proj_frame* f, ProjPointsDev P, const std::vector<
     if (ic && ic->n1 > 0) {
       ORBX_HIP(hipMemcpyAsync(ic->prev_out, base + offs[9], 8 * (size_t)ic->n1,
                               hipMemcpyDeviceToHost, s));
-      ORBX_HIP(hipStreamSynchronize(s));
+      ORBX_HIP(orbx::wait_stream(s));
     }
     if (nmatches) *nmatches = nm;
     return ORBX_OK;
@@ -799,7 +799,7 @@ int run_fuse(const orbx_proj_frame* kf, const float* inv_sigma2, const orbx_fuse
   ORBX_HIP(hipGetLastError());
   std::vector<int2> best(std::max<size_t>(n, 1));
   if (n) ORBX_HIP(hipMemcpyAsync(best.data(), base + obest, 8 * n, hipMemcpyDeviceToHost, s));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   int nf = 0;
   for (size_t i = 0; i < n; i++) {
     best_idx[i] = best[i].x;

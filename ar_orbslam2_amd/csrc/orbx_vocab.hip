@@ -680,7 +680,7 @@ int orbx_vocabulary_transform(const orbx_vocabulary* V, const uint8_t* desc, int
                   dptr<int>(base, off), 0, dptr<int>(base, ofn), 1, s);
   if (rc) return rc;
   ORBX_HIP(tls_ws.download(ow, st.host.size() - ow));
-  ORBX_HIP(hipStreamSynchronize(s));
+  ORBX_HIP(orbx::wait_stream(s));
   auto at = [&](size_t o) { return (const char*)tls_ws.h + o; };
   const int nb = *(const int*)at(obn), nf = *(const int*)at(ofn);
   memcpy(bow_words, at(obw), (size_t)nb * 4);
