@@ -108,6 +108,46 @@ int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_coun
 // d_ids is [nimg][nb], d_off is [nimg][nb + 1], d_feats is [nimg][feats_stride].
 
 // ------------------------------------------------------------------ host-pointer ABI helpers
+// Growable pinned host buffer (pageable fallback if pinning fails); new bytes read as zero.
+struct PinnedBuf {
+  char* p = nullptr;
+  size_t n = 0, cap = 0;
+  bool pinned = false;
+  char* data() { return p; }
+  const char* data() const { return p; }
+  size_t size() const { return n; }
+  void resize(size_t m) {
+    if (m > cap) grow(std::max(m, 2 * cap + 4096));
+    if (m > n) memset(p + n, 0, m - n);
+    n = m;
+  }
+  void grow(size_t want) {
+    ORBX_RESOURCE_LOCK;
+    char* q = nullptr;
+    const bool pin = hipHostMalloc(&q, want, hipHostMallocDefault) == hipSuccess;
+    if (!pin) q = (char*)malloc(want);
+    if (!q) abort();  // host memory exhausted
+    if (n) memcpy(q, p, n);
+    release();
+    p = q;
+    cap = want;
+    pinned = pin;
+  }
+  void release() {
+    if (p) {
+      if (pinned) (void)hipHostFree(p);
+      else free(p);
+    }
+    p = nullptr;
+    cap = 0;
+  }
+  ~PinnedBuf() {
+    ORBX_RESOURCE_LOCK;
+    release();
+  }
+};
+extern thread_local PinnedBuf tls_stage;
+
 // Per-thread device workspace (ORBmatcher / the vocabulary are called from the Tracking,
 // LocalMapping and LoopClosing threads at once; each thread gets its own stream and buffers).
 struct Workspace {
@@ -152,10 +192,9 @@ struct Workspace {
     cap = want;
     return ORBX_OK;
   }
-  // stages the packed host arrays through the pinned mirror and uploads them
-  hipError_t upload(const std::vector<char>& host, size_t bytes) {
-    memcpy(h, host.data(), bytes);
-    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+  // uploads the packed host arrays (a Stager's pinned buffer: one DMA, no host copy)
+  hipError_t upload(const PinnedBuf& host, size_t bytes) {
+    return hipMemcpyAsync(d, host.data(), bytes, hipMemcpyHostToDevice, stream);
   }
   // device range [off, off + bytes) into the same range of the pinned mirror
   hipError_t download(size_t off, size_t bytes) {
@@ -164,9 +203,13 @@ struct Workspace {
 };
 extern thread_local Workspace tls_ws;
 
-// Packs host arrays into one staging buffer, uploaded with one copy.
+// Packs host arrays into one staging buffer, uploaded with one copy.  The buffer is the
+// calling thread's pinned arena (one Stager per thread at a time: every entry point stages,
+// uploads and waits for its stream before returning), so the upload is a DMA from it.
 struct Stager {
-  std::vector<char> host;
+  PinnedBuf& host;
+  Stager() : host(tls_stage) { host.n = 0; }
+  Stager(const Stager&) = delete;
   size_t add(const void* p, size_t bytes) {
     const size_t off = (host.size() + 15) & ~size_t(15);
     host.resize(off + bytes);

@@ -228,6 +228,8 @@ __device__ void three_maxima(const int* h, int& ind1, int& ind2, int& ind3) {
 
 // Rotation consistency filter + count.  Entries: mode 0 indexed by F feature (value = KF idx),
 // mode 1 / triangulation indexed by side-1 feature (value = side-2 idx).
+constexpr int kFinishRegs = 8;  // entries per thread per gather round (n <= 2048: one round)
+
 __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict__ probs) {
   const BowProblem& P = probs[blockIdx.x];
   __shared__ int hist[kHISTO];
@@ -240,36 +242,66 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
   const bool kfkf = P.mode == 1;
   const int n = kfkf ? side_n(P.s1) : side_n(P.s2);
   const int n_other = kfkf ? side_n(P.s2) : side_n(P.s1);  // range of a match value
-  if (P.check_ori) {
-    for (int i = tid; i < n; i += 256) {
-      const int m = P.match[i];
-      if (m < 0 || m >= n_other) continue;
-      const int bin = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m))
-                            : rot_bin(side_angle(P.s1, m), side_angle(P.s2, i));
-      atomicAdd(&hist[bin], 1);
+  const bool ori = P.check_ori;
+  // entries i0 + tid + 256 r (r < kFinishRegs): the matches, then the angle pairs, each with
+  // every load of the round in flight
+  int m[kFinishRegs], bin[kFinishRegs];
+  auto gather = [&](int i0) {
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) {
+      const int i = i0 + tid + 256 * r;
+      m[r] = i < n ? P.match[i] : -1;
     }
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) {
+      const int i = i0 + tid + 256 * r;
+      if (m[r] >= n_other) {  // stale or corrupt index: report, drop, never dereference
+        atomicOr(P.error, ORBX_DEVERR_INDEX);
+        P.match[i] = -1;
+        m[r] = -1;
+      }
+      bin[r] = -1;
+      if (ori && m[r] >= 0)
+        bin[r] = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m[r]))
+                      : rot_bin(side_angle(P.s1, m[r]), side_angle(P.s2, i));
+    }
+  };
+  auto filter = [&](int i0) {  // after ComputeThreeMaxima: drop the other bins, count the rest
+    int c = 0;
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) {
+      if (m[r] < 0) continue;
+      if (ori && bin[r] != s_ind[0] && bin[r] != s_ind[1] && bin[r] != s_ind[2]) {
+        P.match[i0 + tid + 256 * r] = -1;
+        continue;
+      }
+      c++;
+    }
+    return c;
+  };
+  const bool one_round = n <= 256 * kFinishRegs;
+  for (int i0 = 0; i0 < n || i0 == 0; i0 += 256 * kFinishRegs) {
+    gather(i0);
+    if (ori) {
+#pragma unroll
+      for (int r = 0; r < kFinishRegs; r++)
+        if (bin[r] >= 0) atomicAdd(&hist[bin[r]], 1);
+    }
+    if (one_round) break;
+  }
+  if (ori) {
     __syncthreads();
     if (tid == 0) three_maxima(hist, s_ind[0], s_ind[1], s_ind[2]);
     __syncthreads();
   }
   int local = 0;
-  for (int i = tid; i < n; i += 256) {
-    const int m = P.match[i];
-    if (m < 0) continue;
-    if (m >= n_other) {  // stale or corrupt index: report, drop, never dereference
-      atomicOr(P.error, ORBX_DEVERR_INDEX);
-      P.match[i] = -1;
-      continue;
+  if (one_round) {
+    local = filter(0);
+  } else {
+    for (int i0 = 0; i0 < n; i0 += 256 * kFinishRegs) {
+      gather(i0);
+      local += filter(i0);
     }
-    if (P.check_ori) {
-      const int bin = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m))
-                            : rot_bin(side_angle(P.s1, m), side_angle(P.s2, i));
-      if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
-        P.match[i] = -1;
-        continue;
-      }
-    }
-    local++;
   }
   atomicAdd(&s_cnt, local);
   __syncthreads();
@@ -398,7 +430,7 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
   const TriProblem& P = probs[blockIdx.x];
   __shared__ int hist[kHISTO];
   __shared__ int s_ind[3];
-  __shared__ int s_scan[257];
+  __shared__ int s_scan[4];
   const int tid = threadIdx.x;
   const int n = tri_n(P.s1), n2 = tri_n(P.s2);
   if (tid < kHISTO) hist[tid] = 0;
@@ -432,19 +464,17 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
     }
     mine += m >= 0;
   }
-  s_scan[tid] = mine;
+  // exclusive scan of the per-thread counts (DPP wave scans + the 4 wave totals)
+  const int lane = tid & 63, wid = tid >> 6;
+  const int incl = wave_scan_incl(mine);
+  if (lane == 63) s_scan[wid] = incl;
   __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int t = 0; t < 256; t++) {
-      const int x = s_scan[t];
-      s_scan[t] = acc;
-      acc += x;
-    }
-    s_scan[256] = acc;
+  int pos = incl - mine, total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    pos += w < wid ? s_scan[w] : 0;
+    total += s_scan[w];
   }
-  __syncthreads();
-  int pos = s_scan[tid];
   for (int i = beg; i < end; i++) {
     const int m = P.m12[i];
     if (m >= 0) {
@@ -453,7 +483,7 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
       pos++;
     }
   }
-  if (tid == 0) *P.count = s_scan[256];
+  if (tid == 0) *P.count = total;
 }
 
 // ------------------------------------------------------------------ vocabulary + FeatureVector
@@ -468,13 +498,19 @@ __global__ __launch_bounds__(256) void k_csr(const uint32_t* __restrict__ node_o
                                              const uint32_t* __restrict__ rank_ids,
                                              uint32_t* __restrict__ node_ids,
                                              int* __restrict__ offsets, int* __restrict__ feats,
-                                             int64_t feats_stride, int* __restrict__ n_nodes) {
+                                             int64_t feats_stride, int* __restrict__ n_nodes,
+                                             int stage_cap) {
   extern __shared__ int sm[];
   int* cnt = sm;       // nb
   int* cur = sm + nb;  // nb
   const int img = blockIdx.x, tid = threadIdx.x;
   const int n = counts ? counts[img] : n_fixed;
   const uint32_t* nodes = node_of + img * node_stride;
+  if (n <= stage_cap) {  // the image's node ids into LDS in one coalesced round
+    uint32_t* s_nodes = (uint32_t*)(sm + 2 * nb);
+    for (int i = tid; i < n; i += 256) s_nodes[i] = nodes[i];
+    nodes = s_nodes;
+  }
   uint32_t* oid = node_ids + (int64_t)img * nb;        // [img][nb]
   int* ooff = offsets + (int64_t)img * (nb + 1);       // [img][nb + 1]
   int* of = feats + img * feats_stride;                // [img][feats_stride]
@@ -562,16 +598,22 @@ int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_coun
                uint32_t id_lo, int nb, const uint32_t* d_rank_ids, uint32_t* d_ids, int* d_off,
                int* d_feats, int64_t feats_stride, int* d_nn, int nimg, hipStream_t s) {
   if (nimg <= 0) return ORBX_OK;
-  const size_t smem = (size_t)(2 * nb) * 4;
+  size_t smem = (size_t)(2 * nb) * 4;
   if (smem > 64 * 1024) return ORBX_EUNSUPPORTED;
+  // the node ids staged in LDS too when the per-image capacity fits beside the buckets
+  const int64_t per_img = std::max<int64_t>(feats_stride, n_fixed);  // features per image, at most
+  const int stage_cap = smem + (size_t)per_img * 4 <= 32 * 1024 ? (int)per_img : 0;
+  smem += (size_t)stage_cap * 4;
   hipLaunchKernelGGL(k_csr, dim3(nimg), dim3(256), smem, s, d_node_of, node_stride, d_counts,
-                     n_fixed, id_lo, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride, d_nn);
+                     n_fixed, id_lo, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride, d_nn,
+                     stage_cap);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_csr");
 }
 
 // ------------------------------------------------------------------ host-pointer ABI
 thread_local Workspace tls_ws;
+thread_local PinnedBuf tls_stage;
 
 }  // namespace orbx
 
