@@ -124,13 +124,20 @@ int orbx_extract(orbx_extractor* ex, const uint8_t* img, int32_t w, int32_t h, i
   } else {
     for (int y = 0; y < h; y++) memcpy(ex->h_img + (size_t)y * w, img + (size_t)y * stride, w);
   }
-  int rc = run_graph(ex->graphs, s, ex->h_img, 1, [&]() -> int {
+  auto enqueue = [&]() -> int {
     ORBX_HIP(hipMemcpyAsync(ex->d_img, ex->h_img, (size_t)w * h, hipMemcpyHostToDevice, s));
     const int r = plan_enqueue(ex->plan, ex->d_img, 1, nullptr);
     if (r != ORBX_OK) return r;
     ORBX_HIP(hipMemcpyAsync(ex->h_out, d_counts, ex->out_bytes, hipMemcpyDeviceToHost, s));
     return ORBX_OK;
-  });
+  };
+  // one captured graph per input (default), or the launches themselves (ORBX_DROPIN_GRAPH=0):
+  // a graph launch costs the host more before the first node starts than the first launch does
+  static const bool use_graph = [] {
+    const char* e = getenv("ORBX_DROPIN_GRAPH");
+    return !e || atoi(e) != 0;
+  }();
+  int rc = use_graph ? run_graph(ex->graphs, s, ex->h_img, 1, enqueue) : enqueue();
   if (rc != ORBX_OK) return rc;
   ORBX_HIP(orbx::wait_stream(s));
   ex->has_run = true;

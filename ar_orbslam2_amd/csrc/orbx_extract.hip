@@ -1865,6 +1865,7 @@ struct orbx_plan {
   size_t oct_smem = 0, oct_smem_big = 0;
   int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;  // oct_cc* 0: cells in d_cell_scr
   int* d_cell_scr = nullptr;
+  int oct_nt = kOctNT;  // threads of the levels below oct_split (ORBX_OCT_NT_FEW: 512 for few-image plans)
   int cell_cap = 0;
   bool has_fb_big = false;  // some cell's ROI needs k_fast_fallback<72, kCellMax>
   // k_fast_cells: the cells of its <44, 44> and <72, kCellMax> instances
@@ -2008,11 +2009,13 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
                        P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
                        cand, g.cand_total, lin, P->d_label, okey, P->d_ocount,
                        g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0, P->d_cell_scr);
-  if (P->oct_split < L)
-    hipLaunchKernelGGL((k_octree<kOctNT, K>), dim3(n, L - P->oct_split), dim3(kOctNT), P->oct_smem,
+  if (P->oct_split < L) {
+    auto kern = P->oct_nt == 512 ? k_octree<512, K> : k_octree<kOctNT, K>;
+    hipLaunchKernelGGL(kern, dim3(n, L - P->oct_split), dim3(P->oct_nt), P->oct_smem,
                        P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, cand,
                        g.cand_total, lin, P->d_label, okey, P->d_ocount, g.kp_total, L,
                        P->oct_nc, P->oct_cc, P->oct_split, P->d_cell_scr);
+  }
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
@@ -2098,6 +2101,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (const char* e = getenv("ORBX_FAST_PAIR")) P->fast_pair = atoi(e) != 0;
   if (const char* e = getenv("ORBX_FAST_LEGACY")) P->fast_legacy = atoi(e) != 0;
   if (const char* e = getenv("ORBX_FC_CPW")) P->fc_cpw = std::max(0, std::min(kCellsPerWave, atoi(e)));
+  if (const char* e = getenv("ORBX_OCT_NT_FEW"))
+    if (max_batch <= kPyFewImages && atoi(e) == 512) P->oct_nt = 512;
   const Geometry& g = P->g;
   for (const CellGeom& c : g.cells) P->has_fb_big |= c.fb_big != 0;
   auto fail = [&](int code) {
@@ -2217,6 +2222,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   };
   if (P->oct_smem > attr_small) {
     if (!raise((const void*)k_octree<kOctNT, uint32_t>, (const void*)k_octree<kOctNT, uint64_t>,
+               P->oct_smem) ||
+        !raise((const void*)k_octree<512, uint32_t>, (const void*)k_octree<512, uint64_t>,
                P->oct_smem))
       return fail(ORBX_EDEVICE);
     attr_small = P->oct_smem;
