@@ -9,9 +9,11 @@
 # With a second argument "configs" it does the same for C3 C4 C5 instead (PMC passes, bench line,
 # kernel stats: <tag>_pmc_c3/, <tag>_bench_c3.jsonl, <tag>_kernel_stats_c3.csv, ...), without the
 # tests; the two parts fit one gpurun call each.
-# Usage: bash scripts/refresh_profiles.sh r02 [configs]
+# PMC passes are compacted to one row per (kernel, counter) (scripts/pmc_compact.py); the
+# kernel traces stay under gpurun_out/$TAG/traces (scripts/summarize_profiles.py reads them there).
+# Usage: bash scripts/refresh_profiles.sh r03 [configs]
 set -e -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 PART=${2:-main}
 # issue-rate counters (8 SQ counters, one pass): dual-issued VALU quad-cycles and SALU
 # instructions give bench.py's issue floors (profiles/valu_calibration.json)
@@ -32,7 +34,8 @@ if [ "$PART" = configs ]; then
        python3 $R/bench.py --config $C --no-cpu-baseline --steps 5 > /dev/null 2> $D/s.err &&
      cp $(find $D/f -name "*counter_collection.csv") $D/fetch_size.csv &&
      cp $(find $D/w -name "*counter_collection.csv") $D/write_size.csv &&
-     cp $(find $D/s -name "*counter_collection.csv") $D/sq_counters.csv && rm -rf $D/f $D/w $D/s)
+     cp $(find $D/s -name "*counter_collection.csv") $D/sq_counters.csv && rm -rf $D/f $D/w $D/s &&
+     python3 $R/scripts/pmc_compact.py $D)
     timeout -k 10 300 python -u bench.py --config $C --pmc-dir $O/${TAG}_pmc_$c \
       > $O/${TAG}_bench_$c.jsonl 2> $O/bench_$c.err
     cat $O/${TAG}_bench_$c.jsonl
@@ -65,6 +68,7 @@ pmc() {  # pmc <outdir> <bench args...>
   cp $(find $D/w -name "*counter_collection.csv") $D/write_size.csv
   cp $(find $D/s -name "*counter_collection.csv") $D/sq_counters.csv
   rm -rf $D/f $D/w $D/s
+  python3 $R/scripts/pmc_compact.py $D
 }
 pmc $O/${TAG}_pmc
 pmc $O/${TAG}_pmc_ar --config AR

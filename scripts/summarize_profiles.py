@@ -62,8 +62,11 @@ def solo_run(d, steps=5):
 
 
 def counters(pmc_dir):
+    """kernel -> counter -> sum over dispatches, and (kernel, counter) -> dispatches; reads the
+    per-dispatch rocprofv3 layout and the compact one of scripts/pmc_compact.py"""
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    calls = collections.defaultdict(set)
+    ids = collections.defaultdict(set)
+    counts = collections.Counter()
     for fn in ("fetch_size.csv", "write_size.csv", "sq_counters.csv"):
         path = os.path.join(pmc_dir, fn)
         if not os.path.exists(path):
@@ -71,8 +74,14 @@ def counters(pmc_dir):
         with open(path) as f:
             for r in csv.DictReader(f):
                 k = short(r["Kernel_Name"])
-                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-                calls[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
+                if "Dispatches" in r:  # compact: mean per dispatch of one full kernel name
+                    n = int(r["Dispatches"])
+                    agg[k][r["Counter_Name"]] += float(r["Counter_Value"]) * n
+                    counts[(k, r["Counter_Name"])] += n
+                else:
+                    agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                    ids[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
+    calls = {key: range(counts[key] + len(ids.get(key, ()))) for key in set(counts) | set(ids)}
     return agg, calls
 
 
@@ -83,6 +92,8 @@ def main(tag="r02"):
         trace = os.path.join(P, "traces", f"{tag}_kernel_trace{sfx}.csv")
         if not os.path.exists(trace):  # round-1 layout
             trace = os.path.join(P, "traces", f"kernel_trace{sfx}.csv")
+        if not os.path.exists(trace):  # round 3 on: traces stay in gpurun_out (not committed)
+            trace = os.path.join(ROOT, "gpurun_out", tag, "traces", f"kernel_trace{sfx}.csv")
         if not (os.path.exists(bench) and os.path.exists(trace)):
             continue
         line = json.loads(open(bench).read().strip().splitlines()[-1])

@@ -154,3 +154,49 @@ def test_summarizer_finds_roofline_pass():
     pcie = [(720, s) for _ in range(3) for s in "123"]
     assert m.solo_run(timed + solo + pcie) == [650, 651, 652, 653, 654]
     assert m.solo_run(timed) == [700] * 5  # no solo run: the last dispatches
+
+
+def test_pmc_compaction_keeps_bench_readings(tmp_path):
+    """scripts/pmc_compact.py rewrites a --pmc pass to one row per (kernel, counter) holding the
+    mean per dispatch: bench.py's traffic and issue readings and the summarizer's per-dispatch
+    sums are unchanged (the committed round-3 passes are compact)."""
+    import csv
+    import importlib.util
+    import os
+    import shutil
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rows = []
+    for d, (kn, vals) in enumerate([("void orbx::k_fast_cells<44, 44, unsigned int>(x)", (10., 14.)),
+                                    ("void orbx::k_fast_cells<72, 66, unsigned int>(x)", (2., 4.)),
+                                    ("orbx::k_blur(x)", (7., 9.))]):
+        for i, v in enumerate(vals):
+            for c, scale in (("FETCH_SIZE", 1.0), ("WRITE_SIZE", 0.5)):
+                rows.append({"Dispatch_Id": str(10 * d + i), "Kernel_Name": kn, "Counter_Name": c,
+                             "Counter_Value": str(v * scale)})
+    full, comp = tmp_path / "full", tmp_path / "comp"
+    full.mkdir()
+    for name, c in (("fetch_size.csv", "FETCH_SIZE"), ("write_size.csv", "WRITE_SIZE")):
+        with open(full / name, "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(rows[0]))
+            w.writeheader()
+            w.writerows(r for r in rows if r["Counter_Name"] == c)
+    shutil.copytree(full, comp)
+    spec = importlib.util.spec_from_file_location("pmc_compact", os.path.join(root, "scripts", "pmc_compact.py"))
+    pc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pc)
+    pc.compact(str(comp / "fetch_size.csv"))
+    pc.compact(str(comp / "write_size.csv"))
+    assert len(list(csv.DictReader(open(comp / "fetch_size.csv")))) == 3
+    sys.path.insert(0, root)
+    import bench
+    assert bench.pmc_traffic(str(full), "k_fast_cells")[0] == bench.pmc_traffic(str(comp), "k_fast_cells")[0]
+    spec = importlib.util.spec_from_file_location("summarize_profiles",
+                                                  os.path.join(root, "scripts", "summarize_profiles.py"))
+    sm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sm)
+    a1, c1 = sm.counters(str(full))
+    a2, c2 = sm.counters(str(comp))
+    for k in a1:
+        for c in a1[k]:
+            assert a1[k][c] == pytest.approx(a2[k][c]) and len(c1[(k, c)]) == len(c2[(k, c)])
