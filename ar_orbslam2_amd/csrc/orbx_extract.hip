@@ -348,153 +348,130 @@ __device__ __forceinline__ blur_u16x2 byte_pair(uint32_t hi, uint32_t lo, uint32
   return __builtin_bit_cast(blur_u16x2, __builtin_amdgcn_perm(hi, lo, sel));
 }
 
-// One 16-B piece (window row r, piece c: columns X0-16+16c .. +15) of a tile's staged window.
-// Interior tiles read it whole; border tiles reflect the row once (reflect-101) and, in a piece
-// crossing the left / right edge, take whole dwords where they lie inside and reflect byte-wise
-// only the window dwords (3 .. 20) that cross; dwords wholly past the last column any output
-// reads (w + 2) stay zero.
-__device__ __forceinline__ uint4 blur_piece(const uint8_t* src, int pitch, int w, int h, int X0,
-                                            int Y0, bool interior, int r, int c) {
-  if (interior)  // X0 >= 64 and the pitch (a multiple of 64 past X0 + 67) covers X0 + 79
-    return *(const uint4*)(src + (uint32_t)((Y0 + r - 3) * pitch + X0 - 16 + 16 * c));
-  const int y = reflect101(min(Y0 + r - 3, h + 8), h);
-  const uint8_t* row = src + (int64_t)y * pitch;
-  const int x = X0 - 16 + 16 * c;
-  if (x >= 0 && x + 16 <= w) return *(const uint4*)(row + x);
-  uint32_t d[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int dw = 4 * c + j, xd = x + 4 * j;
-    if (dw >= 3 && dw <= 20 && xd < w + 3) {
-      if (xd >= 0 && xd + 4 <= w) {
-        d[j] = *(const uint32_t*)(row + xd);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) d[j] |= (uint32_t)row[reflect101(min(xd + k, w + 8), w)] << (8 * k);
-      }
-    }
-  }
-  return make_uint4(d[0], d[1], d[2], d[3]);
-}
-
-// A workgroup blurs `tpw` consecutive tiles of one image: the next tile's window is loaded into
-// registers while the current tile's column and row passes run, and stored to LDS after them.
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                               uint8_t* __restrict__ blur,
                                               const LevelGeom* __restrict__ lv,
-                                              const BlurTile* __restrict__ tiles, int ntiles,
-                                              int tpw) {
+                                              const BlurTile* __restrict__ tiles) {
   constexpr int kWords = (kBlurTW + 8) / 4;  // window columns X0-4 .. X0+67
   // staged row: 16-B pieces of columns X0-16 .. X0+79 (window dword c at c + 3), 28 dwords apart
   // (112 B: rows 4 apart in the column pass land 48 banks on, not 8)
   constexpr int kChunks = (kBlurTW + 32) / 16, kSt = 28;
   constexpr int kRows = kBlurTH + 6;         // window rows Y0-3 .. Y0+66
-  constexpr int kItems = kRows * kChunks, kPer = (kItems + 255) / 256;
   __shared__ __align__(16) uint32_t s_in[kRows][kSt];
   __shared__ __align__(16) uint32_t s_col[kBlurTH][kWords * 2];  // column sums, u16 pairs
   int bx, img;
   xcd_block(bx, img);
-  const int t_beg = bx * tpw, t_end = min(t_beg + tpw, ntiles);
-  if (t_beg >= ntiles) return;  // (workgroup-uniform)
+  const BlurTile T = tiles[bx];
+  const LevelGeom& G = lv[T.level];
+  int pitch = G.pitch, w = G.w, h = G.h, bxs = G.bxs, pyr_off = (int)G.pyr_off;
+  asm volatile("" : "+s"(pitch), "+s"(w), "+s"(h), "+s"(bxs), "+s"(pyr_off));
+  const uint8_t* src = pyr + (int64_t)img * pyr_bytes + pyr_off;
+  uint8_t* dst = blur + (int64_t)img * pyr_bytes + pyr_off;
+  const int X0 = T.tx * kBlurTW, Y0 = T.ty * kBlurTH;
   const int tid = threadIdx.x;
-  const uint8_t* pimg = pyr + (int64_t)img * pyr_bytes;
-  uint8_t* bimg = blur + (int64_t)img * pyr_bytes;
-  uint4 pv[kPer];
-  auto fetch = [&](int t) {  // tile t's window pieces into registers
-    const BlurTile T = tiles[t];
-    const LevelGeom& G = lv[T.level];
-    const uint8_t* src = pimg + G.pyr_off;
-    const int X0 = T.tx * kBlurTW, Y0 = T.ty * kBlurTH;
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-      const int i = min(tid + 256 * u, kItems - 1);  // (past the end: the last piece again)
+  if (T.interior) {
+    // interior: X0 >= 64 and the pitch (a multiple of 64 past X0 + 67) covers X0 + 79
+    for (int i = tid; i < kRows * kChunks; i += 256) {
       const int r = i / kChunks, c = i - r * kChunks;
-      pv[u] = blur_piece(src, G.pitch, G.w, G.h, X0, Y0, T.interior != 0, r, c);
+      *(uint4*)&s_in[r][4 * c] =
+          *(const uint4*)(src + (uint32_t)((Y0 + r - 3) * pitch + X0 - 16 + 16 * c));
     }
-  };
-  auto stage = [&]() {
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-      const int i = min(tid + 256 * u, kItems - 1);
+  } else {
+    // border tile: each window row reflected once (reflect-101), whole 16-B pieces where they
+    // lie inside the level; in a piece crossing the left / right edge, whole dwords where they
+    // lie inside and a byte-wise reflect only for the window dwords (3 .. 20) that cross;
+    // dwords wholly past the last column any output reads (w + 2) stay unset
+    for (int i = tid; i < kRows * kChunks; i += 256) {
       const int r = i / kChunks, c = i - r * kChunks;
-      *(uint4*)&s_in[r][4 * c] = pv[u];
-    }
-  };
-  fetch(t_beg);
-  stage();
-  for (int t = t_beg; t < t_end; t++) {
-    const BlurTile T = tiles[t];
-    const LevelGeom& G = lv[T.level];
-    int pitch = G.pitch, w = G.w, h = G.h, bxs = G.bxs, pyr_off = (int)G.pyr_off;
-    asm volatile("" : "+s"(pitch), "+s"(w), "+s"(h), "+s"(bxs), "+s"(pyr_off));
-    uint8_t* dst = bimg + pyr_off;
-    const int X0 = T.tx * kBlurTW, Y0 = T.ty * kBlurTH;
-    __syncthreads();  // tile t's window is in s_in; the previous tile's row pass is done
-    if (t + 1 < t_end) fetch(t + 1);  // in flight during this tile's two passes
-    constexpr unsigned short k0 = 18, k1 = 34, k2 = 49, k3 = 55;
-    // column pass (the sum is separable and exact, so columns first gives the same m): a thread
-    // takes one window dword column and 4 output rows; its 10 input dwords unpack once into byte
-    // pairs (b0, b1) and (b2, b3), each output row is 7 packed u16 ops per pair (a column sum is
-    // at most 255 * 257 = 65535)
-    {
-      const blur_u16x2 K0 = {k0, k0}, K1 = {k1, k1}, K2 = {k2, k2}, K3 = {k3, k3};
-      for (int i = tid; i < kWords * (kBlurTH / 4); i += 256) {
-        const int rb = i / kWords, c = i - rb * kWords, r0 = 4 * rb;
-        blur_u16x2 U[10], V[10];
-  #pragma unroll
-        for (int k = 0; k < 10; k++) {
-          const uint32_t w = s_in[r0 + k][c + 3];
-          U[k] = byte_pair(w, w, 0x0c010c00u);
-          V[k] = byte_pair(w, w, 0x0c030c02u);
-        }
-  #pragma unroll
+      const int y = reflect101(min(Y0 + r - 3, h + 8), h);
+      const uint8_t* row = src + (int64_t)y * pitch;
+      const int x = X0 - 16 + 16 * c;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (x >= 0 && x + 16 <= w) {
+        v = *(const uint4*)(row + x);
+      } else {  // per window dword: whole inside the level, reflected byte-wise, or unused
+        uint32_t d[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
         for (int j = 0; j < 4; j++) {
-          const blur_u16x2 su = (U[j] + U[j + 6]) * K0 + (U[j + 1] + U[j + 5]) * K1 +
-                                (U[j + 2] + U[j + 4]) * K2 + U[j + 3] * K3;
-          const blur_u16x2 sv = (V[j] + V[j + 6]) * K0 + (V[j + 1] + V[j + 5]) * K1 +
-                                (V[j + 2] + V[j + 4]) * K2 + V[j + 3] * K3;
-          *(uint2*)&s_col[r0 + j][2 * c] =
-              make_uint2(__builtin_bit_cast(uint32_t, su), __builtin_bit_cast(uint32_t, sv));
+          const int dw = 4 * c + j, xd = x + 4 * j;
+          if (dw >= 3 && dw <= 20 && xd < w + 3) {
+            if (xd >= 0 && xd + 4 <= w) {
+              d[j] = *(const uint32_t*)(row + xd);
+            } else {
+#pragma unroll
+              for (int k = 0; k < 4; k++)
+                d[j] |= (uint32_t)row[reflect101(min(xd + k, w + 8), w)] << (8 * k);
+            }
+          }
         }
+        v = make_uint4(d[0], d[1], d[2], d[3]);
+      }
+      *(uint4*)&s_in[r][4 * c] = v;
+    }
+  }
+  __syncthreads();
+  constexpr unsigned short k0 = 18, k1 = 34, k2 = 49, k3 = 55;
+  // column pass (the sum is separable and exact, so columns first gives the same m): a thread
+  // takes one window dword column and 4 output rows; its 10 input dwords unpack once into byte
+  // pairs (b0, b1) and (b2, b3), each output row is 7 packed u16 ops per pair (a column sum is
+  // at most 255 * 257 = 65535)
+  {
+    const blur_u16x2 K0 = {k0, k0}, K1 = {k1, k1}, K2 = {k2, k2}, K3 = {k3, k3};
+    for (int i = tid; i < kWords * (kBlurTH / 4); i += 256) {
+      const int rb = i / kWords, c = i - rb * kWords, r0 = 4 * rb;
+      blur_u16x2 U[10], V[10];
+#pragma unroll
+      for (int k = 0; k < 10; k++) {
+        const uint32_t w = s_in[r0 + k][c + 3];
+        U[k] = byte_pair(w, w, 0x0c010c00u);
+        V[k] = byte_pair(w, w, 0x0c030c02u);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const blur_u16x2 su = (U[j] + U[j + 6]) * K0 + (U[j + 1] + U[j + 5]) * K1 +
+                              (U[j + 2] + U[j + 4]) * K2 + U[j + 3] * K3;
+        const blur_u16x2 sv = (V[j] + V[j + 6]) * K0 + (V[j + 1] + V[j + 5]) * K1 +
+                              (V[j + 2] + V[j + 4]) * K2 + V[j + 3] * K3;
+        *(uint2*)&s_col[r0 + j][2 * c] =
+            make_uint2(__builtin_bit_cast(uint32_t, su), __builtin_bit_cast(uint32_t, sv));
       }
     }
-    __syncthreads();
-    // row pass: 4 adjacent outputs per thread from the 6 column-sum pairs P_j = (c[4q + 2j],
-    // c[4q + 2j + 1]) around them (window column i = x - X0 + 4), 4 v_dot2_u32_u16 per output with
-    // the taps laid over the pairs (even outputs start mid-pair)
-    const blur_u16x2 W0k0 = {0, k0}, Wk1k2 = {k1, k2}, Wk3k2 = {k3, k2}, Wk1k0 = {k1, k0},
-                     Wk0k1 = {k0, k1}, Wk2k3 = {k2, k3}, Wk2k1 = {k2, k1}, Wk00 = {k0, 0};
-    for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
-      const int r = i >> 4, q = i & 15;
-      const int x = X0 + 4 * q, y = Y0 + r;
-      if (x >= w || y >= h) continue;
-      const uint2 A = *(const uint2*)&s_col[r][2 * q], B = *(const uint2*)&s_col[r][2 * q + 2],
-                  C = *(const uint2*)&s_col[r][2 * q + 4];
-      const blur_u16x2 P0 = __builtin_bit_cast(blur_u16x2, A.x), P1 = __builtin_bit_cast(blur_u16x2, A.y),
-                       P2 = __builtin_bit_cast(blur_u16x2, B.x), P3 = __builtin_bit_cast(blur_u16x2, B.y),
-                       P4 = __builtin_bit_cast(blur_u16x2, C.x), P5 = __builtin_bit_cast(blur_u16x2, C.y);
-      auto d2 = [](blur_u16x2 p, blur_u16x2 k, uint32_t acc) { return __builtin_amdgcn_udot2(p, k, acc, false); };
-      const uint32_t m[4] = {d2(P3, Wk1k0, d2(P2, Wk3k2, d2(P1, Wk1k2, d2(P0, W0k0, 0u)))),
-                             d2(P4, Wk00, d2(P3, Wk2k1, d2(P2, Wk2k3, d2(P1, Wk0k1, 0u)))),
-                             d2(P4, Wk1k0, d2(P3, Wk3k2, d2(P2, Wk1k2, d2(P1, W0k0, 0u)))),
-                             d2(P5, Wk00, d2(P4, Wk2k1, d2(P3, Wk2k3, d2(P2, Wk0k1, 0u))))};
-      // m / 65536 rounded half-even in the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up in
-      // the scalar tail (m + 0x8000); x is a multiple of 4, as is bxs: one test per group.
-      // Quotients <= 257: two per dword by one v_perm of the high halves, clamped by v_pk_min_u16,
-      // then the four low bytes gathered by one more v_perm
-      // (bit field of width 1 in the SSE2 region, 0 in the tail: v_bfe + v_add3 per output)
-      const uint32_t tail = x < bxs ? 0u : 1u;
-      uint32_t rq[4];
-  #pragma unroll
-      for (int k = 0; k < 4; k++) rq[k] = m[k] + (0x7FFFu + tail) + __builtin_amdgcn_ubfe(m[k], 16, 1u - tail);
-      const blur_u16x2 lim = {255, 255};
-      const blur_u16x2 h01 = __builtin_elementwise_min(byte_pair(rq[1], rq[0], 0x07060302u), lim),
-                       h23 = __builtin_elementwise_min(byte_pair(rq[3], rq[2], 0x07060302u), lim);
-      const uint32_t out = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, h23),
-                                                 __builtin_bit_cast(uint32_t, h01), 0x06040200u);
-      *(uint32_t*)(dst + (uint32_t)(y * pitch + x)) = out;  // bytes past w land in the row pad
-    }
-    if (t + 1 < t_end) stage();  // (s_in is free: the column pass finished before the barrier)
+  }
+  __syncthreads();
+  // row pass: 4 adjacent outputs per thread from the 6 column-sum pairs P_j = (c[4q + 2j],
+  // c[4q + 2j + 1]) around them (window column i = x - X0 + 4), 4 v_dot2_u32_u16 per output with
+  // the taps laid over the pairs (even outputs start mid-pair)
+  const blur_u16x2 W0k0 = {0, k0}, Wk1k2 = {k1, k2}, Wk3k2 = {k3, k2}, Wk1k0 = {k1, k0},
+                   Wk0k1 = {k0, k1}, Wk2k3 = {k2, k3}, Wk2k1 = {k2, k1}, Wk00 = {k0, 0};
+  for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
+    const int r = i >> 4, q = i & 15;
+    const int x = X0 + 4 * q, y = Y0 + r;
+    if (x >= w || y >= h) continue;
+    const uint2 A = *(const uint2*)&s_col[r][2 * q], B = *(const uint2*)&s_col[r][2 * q + 2],
+                C = *(const uint2*)&s_col[r][2 * q + 4];
+    const blur_u16x2 P0 = __builtin_bit_cast(blur_u16x2, A.x), P1 = __builtin_bit_cast(blur_u16x2, A.y),
+                     P2 = __builtin_bit_cast(blur_u16x2, B.x), P3 = __builtin_bit_cast(blur_u16x2, B.y),
+                     P4 = __builtin_bit_cast(blur_u16x2, C.x), P5 = __builtin_bit_cast(blur_u16x2, C.y);
+    auto d2 = [](blur_u16x2 p, blur_u16x2 k, uint32_t acc) { return __builtin_amdgcn_udot2(p, k, acc, false); };
+    const uint32_t m[4] = {d2(P3, Wk1k0, d2(P2, Wk3k2, d2(P1, Wk1k2, d2(P0, W0k0, 0u)))),
+                           d2(P4, Wk00, d2(P3, Wk2k1, d2(P2, Wk2k3, d2(P1, Wk0k1, 0u)))),
+                           d2(P4, Wk1k0, d2(P3, Wk3k2, d2(P2, Wk1k2, d2(P1, W0k0, 0u)))),
+                           d2(P5, Wk00, d2(P4, Wk2k1, d2(P3, Wk2k3, d2(P2, Wk0k1, 0u))))};
+    // m / 65536 rounded half-even in the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up in
+    // the scalar tail (m + 0x8000); x is a multiple of 4, as is bxs: one test per group.
+    // Quotients <= 257: two per dword by one v_perm of the high halves, clamped by v_pk_min_u16,
+    // then the four low bytes gathered by one more v_perm
+    // (bit field of width 1 in the SSE2 region, 0 in the tail: v_bfe + v_add3 per output)
+    const uint32_t tail = x < bxs ? 0u : 1u;
+    uint32_t rq[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) rq[k] = m[k] + (0x7FFFu + tail) + __builtin_amdgcn_ubfe(m[k], 16, 1u - tail);
+    const blur_u16x2 lim = {255, 255};
+    const blur_u16x2 h01 = __builtin_elementwise_min(byte_pair(rq[1], rq[0], 0x07060302u), lim),
+                     h23 = __builtin_elementwise_min(byte_pair(rq[3], rq[2], 0x07060302u), lim);
+    const uint32_t out = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, h23),
+                                               __builtin_bit_cast(uint32_t, h01), 0x06040200u);
+    *(uint32_t*)(dst + (uint32_t)(y * pitch + x)) = out;  // bytes past w land in the row pad
   }
 }
 
@@ -1927,14 +1904,6 @@ int orbx::launch_fill_u32(uint32_t* p, size_t n, uint32_t v, hipStream_t s) {
   return ORBX_OK;
 }
 
-// k_blur tiles per workgroup: up to kBlurTPW while the launch keeps >= 4096 workgroups
-#ifndef ORBX_BLUR_TPW
-#define ORBX_BLUR_TPW 8
-#endif
-static int blur_tiles_per_wg(int ntiles, int n) {
-  return std::max(1, std::min(ORBX_BLUR_TPW, (int)((int64_t)ntiles * n / 4096)));
-}
-
 // Blur tiles over every level (the blurred pyramid has the pyramid's pitched layout).
 static std::vector<BlurTile> blur_tiles(const Geometry& g) {
   std::vector<BlurTile> tiles;
@@ -2000,11 +1969,9 @@ int orbx::launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in
 
 int orbx::launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur,
                       int n, hipStream_t s) {
-  if (d.ntiles > 0) {
-    const int tpw = blur_tiles_per_wg(d.ntiles, n);
-    hipLaunchKernelGGL(k_blur, dim3((d.ntiles + tpw - 1) / tpw, n), dim3(256), 0, s, d_pyr,
-                       g.pyr_bytes, d_blur, d.d_lv, (const BlurTile*)d.d_tiles, d.ntiles, tpw);
-  }
+  if (d.ntiles > 0)
+    hipLaunchKernelGGL(k_blur, dim3(d.ntiles, n), dim3(256), 0, s, d_pyr, g.pyr_bytes, d_blur,
+                       d.d_lv, (const BlurTile*)d.d_tiles);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_blur");
 }
@@ -2074,9 +2041,8 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
                        P->d_xtap, P->d_ytap, st.buf_b);
   pr.mark(P->stream, st_pyr);
   if (P->ntiles > 0) {
-    const int tpw = blur_tiles_per_wg(P->ntiles, n);
-    hipLaunchKernelGGL(k_blur, dim3((P->ntiles + tpw - 1) / tpw, n), dim3(256), 0, P->stream,
-                       P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles, P->ntiles, tpw);
+    hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
+                       g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles);
     pr.mark(P->stream, st_blur);
   }
   const int ncells = (int)g.cells.size();
