@@ -269,12 +269,6 @@ __global__ __launch_bounds__(256) void k_bowvec(int must, int l1, int tf,
   __syncthreads();
   uint32_t* ow = out_words + img * out_stride;
   double* ov = out_vals + img * out_stride;
-  // the values also go to LDS for the ordered normalisation pass: into the radix counters'
-  // region (free now) when they fit, padded with zeros to a multiple of 8 (adding +0.0 or
-  // fma(0, 0, norm) leaves the running norm unchanged)
-  constexpr int kValLds = 4 * kRadixB * 4 / 8;  // doubles in the counters' region
-  const bool val_lds = must && nu + 16 <= kValLds;  // (the pass reads 8 past the padding)
-  double* s_val = (double*)s_cnt;
   for (int o = tid; o < nu; o += 256) {
     const int a = s_pos[o], b = s_pos[o + 1];
     double v = wt[(uint32_t)s_a[a]];  // insert(value_type(id, w)) of the first occurrence
@@ -283,41 +277,39 @@ __global__ __launch_bounds__(256) void k_bowvec(int must, int l1, int tf,
     if (tf && !must) v /= (double)nu;  // TemplatedVocabulary.h:1165-1172
     ow[o] = (uint32_t)(s_a[a] >> 32);
     ov[o] = v;
-    if (val_lds) s_val[o] = v;
   }
   if (tid == 0) out_n[img] = nu;
   if (!must) return;
-  if (val_lds) {
-    if (tid < 8) s_val[nu + tid] = 0.0;
-  } else {
-    __syncthreads();
-    // the values back into LDS (over the pong keys) for the ordered normalisation pass
-    s_val = (double*)s_b;
-    for (int o = tid; o < nu; o += 256) s_val[o] = ov[o];
-    if (tid < 8) s_val[nu + tid] = 0.0;  // (past s_b's cap doubles: the free counters)
-  }
+  __syncthreads();
+  // the values back into LDS (over the pong keys) for the ordered normalisation pass
+  double* s_val = (double*)s_b;
+  for (int o = tid; o < nu; o += 256) s_val[o] = ov[o];
   __syncthreads();
   if (tid == 0) {  // BowVector::normalize: one ordered pass over the words
-    // (the adds stay in word order; the next 8 values load while the current 8 are added)
+    // (the adds stay in word order; LDS reads are batched 8 at a time)
     double norm = 0.0;
-    double v[8], w[8];
+    int o = 0;
+    if (l1) {
+      for (; o + 8 <= nu; o += 8) {
+        double v[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) v[j] = s_val[j];
-    for (int o = 0; o < nu; o += 8) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) w[j] = s_val[o + 8 + j];  // (zeros / unused past the end)
-      if (l1) {
+        for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
 #pragma unroll
         for (int j = 0; j < 8; j++) norm += fabs(v[j]);
-      } else {
-        // built -O3 -march=native (Thirdparty/DBoW2/CMakeLists.txt): `norm += v * v` contracts
+      }
+      for (; o < nu; o++) norm += fabs(s_val[o]);
+    } else {
+      // built -O3 -march=native (Thirdparty/DBoW2/CMakeLists.txt): `norm += v * v` contracts
+      for (; o + 8 <= nu; o += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
 #pragma unroll
         for (int j = 0; j < 8; j++) norm = fma(v[j], v[j], norm);
       }
-#pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = w[j];
+      for (; o < nu; o++) norm = fma(s_val[o], s_val[o], norm);
+      norm = sqrt(norm);
     }
-    if (!l1) norm = sqrt(norm);
     s_norm = norm;
   }
   __syncthreads();
