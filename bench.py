@@ -1001,8 +1001,8 @@ def parse_args(argv=None):
     if args.pmc_dir is None:  # the committed PMC passes of this config's default command
         # (never another config's: a missing directory reports traffic / VALU floor as null)
         args.pmc_dir = os.path.join(ROOT, "profiles",
-                                    "r02_pmc" if args.config == "C2" else
-                                    "r02_pmc_" + args.config.lower())
+                                    "r03_pmc" if args.config == "C2" else
+                                    "r03_pmc_" + args.config.lower())
     return args
 
 
