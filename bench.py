@@ -122,11 +122,15 @@ def pmc_traffic(pmc_dir, kernel):
         path = os.path.join(pmc_dir, name) if pmc_dir else ""
         if not os.path.exists(path):
             return None, f"no PMC passes for this command ({rel})"
-        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                if _kname_is(r["Kernel_Name"], kernel) and r["Counter_Name"] == counter]
-        if not vals:
+        # one "launch" of a stage spans every instance of the kernel (k_fast_cells<44, 44> and
+        # <72, 66> per step): mean per instance over its dispatches, summed over the instances
+        per = {}
+        for r in csv.DictReader(open(path)):
+            if _kname_is(r["Kernel_Name"], kernel) and r["Counter_Name"] == counter:
+                per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+        if not per:
             return None, f"kernel not in the PMC passes ({rel})"
-        tot[counter] = sum(vals) / len(vals) * 1024
+        tot[counter] = sum(sum(v) / len(v) for v in per.values()) * 1024
     cal = _load_json("pmc_calibration.json")
     w = LOAD_WIDTH.get(kernel)
     rf = (cal or {}).get("read", {}).get(f"{w}B_per_lane") if w else None
@@ -156,13 +160,15 @@ def pmc_issue(pmc_dir, kernel, avg_launch_us):
     path = os.path.join(pmc_dir, "sq_counters.csv")
     if not os.path.exists(path) or not avg_launch_us:
         return None
-    per = {}
+    per = {}  # counter -> instance (full kernel name) -> values per dispatch
     for r in csv.DictReader(open(path)):
         if _kname_is(r["Kernel_Name"], kernel):
-            per.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            per.setdefault(r["Counter_Name"], {}).setdefault(r["Kernel_Name"], []).append(
+                float(r["Counter_Value"]))
     if "SQ_INSTS_VALU" not in per:
         return None
-    avg = {k: sum(v) / len(v) for k, v in per.items()}
+    # per stage launch: mean per instance, summed over the kernel's instances
+    avg = {k: sum(sum(v) / len(v) for v in inst.values()) for k, inst in per.items()}
     us_per_qc = 4 / VALU_SIMDS / (CLOCK_GHZ * 1e3)
     if "SQ_ACTIVE_INST_VALU" in avg and "SQ_ACTIVE_INST_VALU2" in avg:
         valu_qc = avg["SQ_ACTIVE_INST_VALU"] - avg["SQ_ACTIVE_INST_VALU2"]

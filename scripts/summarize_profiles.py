@@ -90,23 +90,27 @@ def main(tag="r02"):
     for cfg, (sfx, psfx) in CONFIGS.items():
         bench = os.path.join(P, f"{tag}_bench{sfx}.jsonl")
         trace = os.path.join(P, "traces", f"{tag}_kernel_trace{sfx}.csv")
-        if not os.path.exists(trace):  # round-1 layout
-            trace = os.path.join(P, "traces", f"kernel_trace{sfx}.csv")
         if not os.path.exists(trace):  # round 3 on: traces stay in gpurun_out (not committed)
             trace = os.path.join(ROOT, "gpurun_out", tag, "traces", f"kernel_trace{sfx}.csv")
+        if not os.path.exists(trace) and tag == "r01":  # round-1 layout
+            trace = os.path.join(P, "traces", f"kernel_trace{sfx}.csv")
         if not (os.path.exists(bench) and os.path.exists(trace)):
             continue
         line = json.loads(open(bench).read().strip().splitlines()[-1])
         rf = line["roofline"]
         durs = trace_durations(trace)
         k = rf["kernel"]
-        d = durs.get(k) or next((v for kk, v in durs.items() if kk.startswith(k + "<")), [])
+        # every instance of the kernel (k_fast_cells runs a <44, 44> and a <72, 66> launch per
+        # step; bench.py's stage, one "launch", spans both): durations summed per step
+        inst = [v for kk, v in sorted(durs.items()) if kk == k or kk.startswith(k + "<")]
         check.append(f"{cfg} ({line['config']['workload']}): {line['value']:.1f} frames/s")
-        check.append(f"  kernel {k}: {len(d)} dispatches")
-        if d:
-            solo, alld = solo_run(d), [dur for dur, _ in d]
+        check.append(f"  kernel {k}: {sum(len(v) for v in inst)} dispatches"
+                     + (f" ({len(inst)} instances, summed per step)" if len(inst) > 1 else ""))
+        if inst:
+            solo = [sum(x) for x in zip(*(solo_run(v) for v in inst))]
+            alld = sum(sum(dur for dur, _ in v) / len(v) for v in inst)
             check.append(f"    trace average, all dispatches (timed region with concurrent streams"
-                         f" + roofline pass + PCIe pass): {sum(alld) / len(alld) / 1e3:.2f} us")
+                         f" + roofline pass + PCIe pass): {alld / 1e3:.2f} us")
             check.append(f"    trace average, roofline pass (5 consecutive dispatches on one "
                          f"stream, camera stream 0 alone): {sum(solo) / len(solo) / 1e3:.2f} us")
         under = os.path.join(P, f"{tag}_bench{sfx}_under_rocprof.jsonl")
