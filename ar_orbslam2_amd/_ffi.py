@@ -33,6 +33,7 @@ EXPORTS = [
     "orbx_search_by_bow_kf_f", "orbx_search_by_bow_kf_kf", "orbx_search_for_triangulation",
     "orbx_epipole", "orbx_search_by_projection", "orbx_search_by_projection_last",
     "orbx_search_for_initialization", "orbx_fuse", "orbx_fuse_sim3",
+    "orbx_search_by_projection_kf", "orbx_search_by_projection_sim3", "orbx_search_by_sim3",
     "orbx_stereo_matches", "orbx_vocabulary_load_text", "orbx_vocabulary_create",
     "orbx_vocabulary_destroy", "orbx_vocabulary_info", "orbx_vocabulary_transform",
     "orbx_frames_create", "orbx_frames_create_stereo", "orbx_frames_destroy",

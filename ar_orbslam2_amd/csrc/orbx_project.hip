@@ -59,9 +59,14 @@ struct ProjFrameDev {
 };
 
 // mode 0: local-map points (SearchByProjection(F, vpMapPoints, th)); 1: last frame;
-// 2: SearchForInitialization (x, y = vbPrevMatched, level = F1 octave, th = windowSize)
+// 2: SearchForInitialization (x, y = vbPrevMatched, level = F1 octave, th = windowSize);
+// 3: relocalization (SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist): level = the
+//    predicted level, window levels +-1, angle = the keyframe keypoint's);
+// 4: loop closing (SearchByProjection(pKF, Scw, vpPoints, vpMatched, th): the keyframe's grid,
+//    levels [predicted - 1, predicted])
 struct ProjPointsDev {
   int mode;
+  int max_dist;         // accepted best distance (modes 1, 3, 4): TH_HIGH, ORBdist, TH_LOW
   int n;
   const uint8_t* use;   // track (mode 0) / valid (mode 1)
   const float *x, *y, *xr;
@@ -143,9 +148,20 @@ __global__ __launch_bounds__(256) void k_proj_cand(ProjFrameDev F, ProjPointsDev
     if (P.forward) minLevel = oct, maxLevel = -1;
     else if (P.backward) minLevel = 0, maxLevel = oct;
     else minLevel = oct - 1, maxLevel = oct + 1;
-  } else if (go) {  // GetFeaturesInArea(prev.x, prev.y, windowSize, level1, level1) (:425)
+  } else if (go && P.mode == 2) {  // GetFeaturesInArea(prev.x, prev.y, windowSize, level1, level1) (:425)
     rs = P.th;
     minLevel = maxLevel = P.level[p];
+  } else if (go && P.mode == 3) {
+    if (x < F.min_x || x > F.max_x || y < F.min_y || y > F.max_y) go = false;  // :1512-1515
+    const int lev = P.level[p];
+    rs = P.th * F.scale[lev];  // :1530-1532
+    minLevel = lev - 1;
+    maxLevel = lev + 1;
+  } else if (go) {  // mode 4: the level test sits in the reference's loop (:364-367), same set
+    const int lev = P.level[p];
+    rs = P.th * F.scale[lev];  // :354-356
+    minLevel = lev - 1;
+    maxLevel = lev;
   }
   int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
   if (go) {  // GetFeaturesInArea window (Frame.cc:337-351)
@@ -214,7 +230,7 @@ __global__ __launch_bounds__(256) void k_proj_cand(ProjFrameDev F, ProjPointsDev
       // static per-candidate filters of the searches; the order slot is kept either way
       int dist = 256;
       bool ok = P.mode == 2 || !(F.has_mp_obs && F.has_mp_obs[idx]);
-      if (ok && P.mode != 2 && F.u_right && F.u_right[idx] > 0) {
+      if (ok && P.mode <= 1 && F.u_right && F.u_right[idx] > 0) {
         const float er = fabsf((P.mode == 0 ? P.xr[p] : xr) - F.u_right[idx]);
         ok = !(er > (P.mode == 0 ? r * F.scale[P.level[p]] : rs));
       }
@@ -262,7 +278,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjFrameDev F, ProjPointsD
     for (int o = 32; o > 0; o >>= 1) key1 = min(key1, __shfl_xor(key1, o));
     if (key1 == INT_MAX) continue;
     const int bestDist = key1 >> 22, bestPos = key1 & 0x3FFFFF;
-    if (bestDist > kTH_HIGH) continue;
+    if (bestDist > (P.mode == 0 ? kTH_HIGH : P.max_dist)) continue;
     const int4 best = lst[bestPos];
     if (P.mode == 0) {
       // second: first minimum of {the best among candidates before bestPos} followed by the
@@ -296,7 +312,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjFrameDev F, ProjPointsD
     if (lane == 0) {
       match[best.x] = p;
       s_claim[best.x >> 5] |= 1u << (best.x & 31);
-      if (P.mode == 1 && P.check_ori) {
+      if ((P.mode == 1 || P.mode == 3) && P.check_ori) {
         float rot = P.angle[p] - F.keys[best.x].angle;
         if (rot < 0.0) rot += 360.0f;
         int bin = (int)roundf(rot * factor);
@@ -307,7 +323,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjFrameDev F, ProjPointsD
     nm++;
     __syncthreads();
   }
-  if (P.mode == 1 && P.check_ori) {
+  if ((P.mode == 1 || P.mode == 3) && P.check_ori) {
     __syncthreads();
     int ind1 = -1, ind2 = -1, ind3 = -1;  // ComputeThreeMaxima (ORBmatcher.cc:1604-1645)
     int max1 = 0, max2 = 0, max3 = 0;
@@ -500,6 +516,7 @@ struct FusePointsDev {
   const uint8_t* desc;
   float th;
   int reproj;  // 1: Fuse(KeyFrame*, vector<MapPoint*>, th); 0: Fuse(KeyFrame*, Scw, ...)
+  int max_dist;  // accepted best distance: TH_LOW (Fuse), TH_HIGH (SearchBySim3)
   float inv_sigma2[kMaxLevels];
 };
 
@@ -583,7 +600,7 @@ __global__ __launch_bounds__(256) void k_fuse(ProjFrameDev F, FusePointsDev P,
   const int idx = __shfl(kidx, __builtin_ctzll(win));
   if (lane == 0) {
     if (K == INT_MAX) best[p] = make_int2(-1, none_dist);
-    else best[p] = make_int2((K >> 22) <= kTH_LOW ? idx : -1, K >> 22);  // (:955, :1085)
+    else best[p] = make_int2((K >> 22) <= P.max_dist ? idx : -1, K >> 22);  // (:955, :1085, :1212)
   }
 }
 
@@ -597,6 +614,23 @@ struct Staged {
   ProjFrameDev F;
   size_t cell, ids, off, feats, nn, begin, lists, cnts, err, match, nmatch;
 };
+
+// SearchBySim3's agreement (ORBmatcher.cc:1305-1326): KF1 point i1's best KF2 feature idx2 is
+// kept when KF2 point idx2's best KF1 feature is i1.  best12 / best21: k_fuse results of the two
+// directions (index or -1); m12[i1] = idx2 or -1; *nfound = the kept count.
+__global__ __launch_bounds__(256) void k_sim3_agree(const int2* __restrict__ best12, int n1,
+                                                    const int2* __restrict__ best21, int n2,
+                                                    int* __restrict__ m12, int* __restrict__ nfound) {
+  const int i1 = blockIdx.x * 256 + threadIdx.x;
+  int keep = 0;
+  if (i1 < n1) {
+    const int idx2 = best12[i1].x;
+    keep = idx2 >= 0 && idx2 < n2 && best21[idx2].x == i1;
+    m12[i1] = keep ? idx2 : -1;
+  }
+  const int c = __popcll(__ballot(keep));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(nfound, c);
+}
 
 // The frame's arrays and its grid (Frame::AssignFeaturesToGrid: k_grid_cells, k_csr,
 // k_grid_dense) in one workspace: offsets of the uploaded arrays and of the grid scratch.
@@ -791,6 +825,7 @@ int run_fuse(const orbx_proj_frame* kf, const float* inv_sigma2, const orbx_fuse
   P.desc = dptr<uint8_t>(base, odesc);
   P.th = th;
   P.reproj = reproj;
+  P.max_dist = kTH_LOW;
   for (int l = 0; l < kMaxLevels; l++)
     P.inv_sigma2[l] = reproj && l < kf->nlevels ? inv_sigma2[l] : 1.f;
   if (m->n > 0)
@@ -807,6 +842,71 @@ int run_fuse(const orbx_proj_frame* kf, const float* inv_sigma2, const orbx_fuse
     nf += best[i].x >= 0;
   }
   if (n_fused) *n_fused = nf;
+  return ORBX_OK;
+}
+
+// SearchBySim3: both keyframes and both point sets in one upload, the two grids, the two
+// per-point searches (k_fuse without reprojection gates, TH_HIGH) and the agreement.
+int run_sim3(const orbx_proj_frame* kf1, const orbx_proj_frame* kf2, const orbx_fuse_points* m12,
+             const orbx_fuse_points* m21, float th, int32_t* matches12, int32_t* n_found) {
+  Stager st;
+  GridOffs g1, g2;
+  stage_frame(st, kf1, &g1);
+  stage_frame(st, kf2, &g2);
+  struct Offs { size_t use, u, v, lev, desc; } o[2];
+  const orbx_fuse_points* ms[2] = {m12, m21};
+  for (int k = 0; k < 2; k++) {
+    const size_t n = (size_t)ms[k]->n;
+    o[k].use = st.add(ms[k]->use, n);
+    o[k].u = st.add(ms[k]->u, 4 * n);
+    o[k].v = st.add(ms[k]->v, 4 * n);
+    o[k].lev = st.add(ms[k]->pred_level, 4 * n);
+    o[k].desc = st.add(ms[k]->desc, 32 * n);
+  }
+  const size_t upload = st.host.size();
+  stage_grid(st, kf1, &g1);
+  stage_grid(st, kf2, &g2);
+  const size_t ob12 = st.add(nullptr, 8 * (size_t)std::max(m12->n, 1)),
+               ob21 = st.add(nullptr, 8 * (size_t)std::max(m21->n, 1)),
+               om12 = st.add(nullptr, 4 * (size_t)std::max(m12->n, 1)), ofound = st.add(nullptr, 4);
+  int rc = tls_ws.reserve(st.host.size());
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), upload, hipMemcpyHostToDevice, s));
+  ORBX_HIP(hipMemsetAsync(base + ofound, 0, 4, s));
+  ProjFrameDev F1{}, F2{};
+  rc = launch_grid(kf1, base, g1, false, s, &F1);
+  if (rc) return rc;
+  rc = launch_grid(kf2, base, g2, false, s, &F2);
+  if (rc) return rc;
+  // points of KF1 searched in KF2's grid, points of KF2 in KF1's
+  for (int k = 0; k < 2; k++) {
+    FusePointsDev P{};
+    P.n = ms[k]->n;
+    P.use = dptr<uint8_t>(base, o[k].use);
+    P.u = dptr<float>(base, o[k].u);
+    P.v = dptr<float>(base, o[k].v);
+    P.ur = nullptr;
+    P.level = dptr<int>(base, o[k].lev);
+    P.desc = dptr<uint8_t>(base, o[k].desc);
+    P.th = th;
+    P.reproj = 0;
+    P.max_dist = kTH_HIGH;
+    for (int l = 0; l < kMaxLevels; l++) P.inv_sigma2[l] = 1.f;
+    if (P.n > 0)
+      hipLaunchKernelGGL(k_fuse, dim3((P.n + 3) / 4), dim3(256), 0, s, k == 0 ? F2 : F1, P,
+                         dptr<int2>(base, k == 0 ? ob12 : ob21));
+  }
+  if (m12->n > 0)
+    hipLaunchKernelGGL(k_sim3_agree, dim3((m12->n + 255) / 256), dim3(256), 0, s,
+                       dptr<const int2>(base, ob12), m12->n, dptr<const int2>(base, ob21), m21->n,
+                       dptr<int>(base, om12), dptr<int>(base, ofound));
+  ORBX_HIP(hipGetLastError());
+  ORBX_HIP(tls_ws.download(om12, ofound + 4 - om12));
+  ORBX_HIP(orbx::wait_stream(s));
+  if (m12->n > 0) memcpy(matches12, tls_ws.h + om12, 4 * (size_t)m12->n);
+  *n_found = *(const int*)(tls_ws.h + ofound);
   return ORBX_OK;
 }
 
@@ -857,6 +957,7 @@ int orbx_search_by_projection_last(const orbx_proj_frame* f, const orbx_proj_las
     if (l->valid[i] && (l->octave[i] < 0 || l->octave[i] >= f->nlevels)) return ORBX_EINVAL;
   ProjPointsDev P{};
   P.mode = 1;
+  P.max_dist = kTH_HIGH;
   P.n = l->n;
   P.th = th;
   P.forward = forward;
@@ -896,6 +997,48 @@ int orbx_search_for_initialization(const orbx_proj_frame* f1, const orbx_proj_fr
                          f1->desc, f1->keys_un, prev_matched},
                         {n, 4 * n, 4 * n, 0, 4 * n, 0, 0, 32 * n, sizeof(orbx_keypoint) * n, 8 * n},
                         matches12, nmatches, &ic);
+}
+
+int orbx_search_by_projection_kf(const orbx_proj_frame* f, const orbx_proj_last* k, float th,
+                                 int32_t orb_dist, int32_t check_ori, int32_t* match,
+                                 int32_t* nmatches) {
+  if (!frame_ok(f) || !k || k->n < 0 || (f->n > 0 && !match)) return ORBX_EINVAL;
+  if (k->n > 0 && (!k->valid || !k->u || !k->v || !k->octave || !k->angle || !k->desc))
+    return ORBX_EINVAL;
+  for (int i = 0; i < k->n; i++)
+    if (k->valid[i] && (k->octave[i] < 0 || k->octave[i] >= f->nlevels)) return ORBX_EINVAL;
+  ProjPointsDev P{};
+  P.mode = 3;
+  P.max_dist = orb_dist;
+  P.n = k->n;
+  P.th = th;
+  P.check_ori = check_ori;
+  const size_t n = (size_t)k->n;
+  return run_projection(f, P, {k->valid, k->u, k->v, nullptr, k->octave, nullptr, k->angle, k->desc},
+                        {n, 4 * n, 4 * n, 0, 4 * n, 0, 4 * n, 32 * n}, match, nmatches);
+}
+
+int orbx_search_by_projection_sim3(const orbx_proj_frame* kf, const orbx_fuse_points* m,
+                                   float th, int32_t* match, int32_t* nmatches) {
+  if (!fuse_args_ok(kf, m, match, false) || (kf->n > 0 && !match)) return ORBX_EINVAL;
+  ProjPointsDev P{};
+  P.mode = 4;
+  P.max_dist = kTH_LOW;
+  P.n = m->n;
+  P.th = th;
+  const size_t n = (size_t)m->n;
+  return run_projection(kf, P, {m->use, m->u, m->v, nullptr, m->pred_level, nullptr, nullptr, m->desc},
+                        {n, 4 * n, 4 * n, 0, 4 * n, 0, 0, 32 * n}, match, nmatches);
+}
+
+int orbx_search_by_sim3(const orbx_proj_frame* kf1, const orbx_proj_frame* kf2,
+                        const orbx_fuse_points* points12, const orbx_fuse_points* points21,
+                        float th, int32_t* matches12, int32_t* n_found) {
+  if (!n_found || !fuse_args_ok(kf2, points12, matches12, false) ||
+      !fuse_args_ok(kf1, points21, matches12, false))
+    return ORBX_EINVAL;
+  if (points12->n != kf1->n || points21->n != kf2->n) return ORBX_EINVAL;  // one point per keypoint
+  return run_sim3(kf1, kf2, points12, points21, th, matches12, n_found);
 }
 
 int orbx_fuse(const orbx_proj_frame* kf, const float* inv_level_sigma2,

@@ -223,6 +223,62 @@ class ORBmatcher:
                                   C.byref(nf)))
         return nf.value, bi[:p.n].copy(), bd[:p.n].copy()
 
+    # -------------------------------------------------------------- relocalization / loop closing
+    _SIM3_SPEC = [("use", np.uint8), ("u", np.float32), ("v", np.float32), ("__none__", np.float32),
+                  ("pred_level", np.int32), ("desc", np.uint8)]
+
+    def SearchByProjectionKF(self, CurrentFrame, kf_points, th, ORBdist):
+        """SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, sAlreadyFound, th, ORBdist)
+        (ORBmatcher.cc:1475-1602, Tracking::Relocalization) on the GPU.
+
+        CurrentFrame: as for SearchByProjection, with `has_mp_obs` = mvpMapPoints[i] != NULL.
+        kf_points: valid, u, v (projection into the current frame), octave (the predicted
+        level), angle (pKF->mvKeysUn[i].angle), desc — include/orbx.h.
+        Returns (nmatches, match) with match[f] = keyframe index or -1."""
+        fr, keep = _proj_frame(CurrentFrame)
+        p, pk = _proj_struct(kf_points, _ffi.ProjLast, [
+            ("valid", np.uint8), ("u", np.float32), ("v", np.float32), ("__none__", np.float32),
+            ("octave", np.int32), ("angle", np.float32), ("desc", np.uint8)])
+        match = np.zeros(max(fr.n, 1), np.int32)
+        nm = C.c_int32()
+        check("orbx_search_by_projection_kf",
+              lib().orbx_search_by_projection_kf(C.byref(fr), C.byref(p), C.c_float(th),
+                                                 C.c_int32(int(ORBdist)),
+                                                 C.c_int32(int(self.mbCheckOrientation)),
+                                                 ptr(match), C.byref(nm)))
+        return nm.value, match[:fr.n].copy()
+
+    def SearchByProjectionSim3(self, pKF, points, th):
+        """SearchByProjection(KeyFrame* pKF, cv::Mat Scw, vpPoints, vpMatched, int th)
+        (ORBmatcher.cc:290-403, loop closing) on the GPU.  pKF: keyframe with `has_mp_obs` =
+        vpMatched[i] != NULL; points: use, u, v, pred_level, desc (the caller's Scw projection
+        and gates).  Returns (nmatches, match) with match[f] = point index assigned to keyframe
+        feature f in this call, else -1."""
+        kf, keep = _proj_frame(pKF)
+        p, pk = _proj_struct(points, _ffi.FusePoints, self._SIM3_SPEC)
+        match = np.zeros(max(kf.n, 1), np.int32)
+        nm = C.c_int32()
+        check("orbx_search_by_projection_sim3",
+              lib().orbx_search_by_projection_sim3(C.byref(kf), C.byref(p), C.c_float(th),
+                                                   ptr(match), C.byref(nm)))
+        return nm.value, match[:kf.n].copy()
+
+    def SearchBySim3(self, pKF1, pKF2, points12, points21, th):
+        """SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:1105-1329)
+        on the GPU.  points12: KF1's map points projected into KF2 (one per KF1 keypoint: use,
+        u, v, pred_level, desc), points21: KF2's into KF1.  Returns (nFound, m12) with m12[i1]
+        = idx2 where both directions agree, else -1."""
+        k1, keep1 = _proj_frame(pKF1)
+        k2, keep2 = _proj_frame(pKF2)
+        p12, pk12 = _proj_struct(points12, _ffi.FusePoints, self._SIM3_SPEC)
+        p21, pk21 = _proj_struct(points21, _ffi.FusePoints, self._SIM3_SPEC)
+        m12 = np.zeros(max(p12.n, 1), np.int32)
+        nf = C.c_int32()
+        check("orbx_search_by_sim3",
+              lib().orbx_search_by_sim3(C.byref(k1), C.byref(k2), C.byref(p12), C.byref(p21),
+                                        C.c_float(th), ptr(m12), C.byref(nf)))
+        return nf.value, m12[:p12.n].copy()
+
 
 def epipole(R2w, t2w, Cw, fx, fy, cx, cy):
     ex, ey = C.c_float(), C.c_float()

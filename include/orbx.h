@@ -228,6 +228,20 @@ int orbx_search_for_initialization(const orbx_proj_frame* f1, const orbx_proj_fr
                                    float* prev_matched, int32_t window_size, float nnratio,
                                    int32_t check_ori, int32_t* matches12, int32_t* nmatches);
 
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
+ * sAlreadyFound, const float th, const int ORBdist) (ORB_SLAM2/src/ORBmatcher.cc:1475-1602;
+ * Tracking::Relocalization, Tracking.cc:1441-1468) of an ORBmatcher(nnratio, checkOri).
+ * frame = CurrentFrame with has_mp_obs[f] = mvpMapPoints[f] != NULL (here any map point blocks a
+ * feature, observed or not; u_right unused).  kf_points: one entry per keyframe map point i,
+ * valid[i] = pMP && !isBad() && !sAlreadyFound.count(pMP) && minDistance <= dist3D <=
+ * maxDistance, u, v its projection into the current frame (the reference's cv::Mat pose
+ * products), octave = PredictScale(dist3D, mfLogScaleFactor), angle = pKF->mvKeysUn[i].angle,
+ * desc = GetDescriptor(); ur unused.  The window is the predicted level +-1, the first minimum
+ * is kept when <= orb_dist, then the rotation filter.  match[f] = the keyframe index whose map
+ * point is assigned to current feature f in this call, else -1. */
+int orbx_search_by_projection_kf(const orbx_proj_frame* frame, const orbx_proj_last* kf_points,
+                                 float th, int32_t orb_dist, int32_t check_ori, int32_t* match,
+                                 int32_t* nmatches);
 /* ORBmatcher::Fuse, the per-point search of both overloads:
  *   Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th)
  *     (ORB_SLAM2/src/ORBmatcher.cc:828-978; LocalMapping::SearchInNeighbors, LocalMapping.cc:469,
@@ -259,6 +273,30 @@ int orbx_fuse(const orbx_proj_frame* kf, const float* inv_level_sigma2,
               int32_t* n_fused);
 int orbx_fuse_sim3(const orbx_proj_frame* kf, const orbx_fuse_points* points, float th,
                    int32_t* best_idx, int32_t* best_dist, int32_t* n_fused);
+/* ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints,
+ * vector<MapPoint*>& vpMatched, int th) (ORB_SLAM2/src/ORBmatcher.cc:290-403;
+ * LoopClosing::ComputeSim3 / CorrectLoop): kf = the keyframe (keys_un, desc, grid frame,
+ * mvScaleFactors) with has_mp_obs[f] = vpMatched[f] != NULL on entry.  points: use[i] =
+ * !isBad() && not in spAlreadyFound && depth >= 0 && IsInImage(u, v) && minDistance <= dist <=
+ * maxDistance && PO.dot(Pn) >= 0.5 * dist (:318-352, evaluated by the caller with Scw), u, v,
+ * pred_level = PredictScale(dist, mfLogScaleFactor), desc; ur unused.  match[f] = the point
+ * index assigned to keyframe feature f in this call (vpMatched[f] = vpPoints[match[f]]), else
+ * -1; *nmatches as the reference returns. */
+int orbx_search_by_projection_sim3(const orbx_proj_frame* kf, const orbx_fuse_points* points,
+                                   float th, int32_t* match, int32_t* nmatches);
+/* ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12,
+ * const float& s12, const cv::Mat& R12, const cv::Mat& t12, const float th)
+ * (ORB_SLAM2/src/ORBmatcher.cc:1105-1329; LoopClosing::ComputeSim3, LoopClosing.cc:305):
+ * kf1 / kf2 the two keyframes (keys_un, desc, grid frame, mvScaleFactors).  points12 = KF1's
+ * map points projected into KF2 (n = kf1->n, one per keypoint i1: use[i1] = pMP &&
+ * !vbAlreadyMatched1[i1] && !isBad() && depth >= 0 && pKF2->IsInImage(u, v) && minDistance <=
+ * dist3D <= maxDistance, u, v, pred_level = PredictScale(dist3D, pKF2->mfLogScaleFactor),
+ * desc), points21 = KF2's into KF1 (n = kf2->n, the same gates with vbAlreadyMatched2).
+ * matches12[i1] = idx2 where the two directions agree (the caller sets vpMatches12[i1] =
+ * vpMapPoints2[idx2]), else -1 (entry left as it was); *n_found as the reference returns. */
+int orbx_search_by_sim3(const orbx_proj_frame* kf1, const orbx_proj_frame* kf2,
+                        const orbx_fuse_points* points12, const orbx_fuse_points* points21,
+                        float th, int32_t* matches12, int32_t* n_found);
 
 /* ------------------------------------------------------------------ stereo
  * Frame::ComputeStereoMatches (ORB_SLAM2/src/Frame.cc:471-643) on the last extraction of a

@@ -492,6 +492,53 @@ def fuse(kf, inv_sigma2, pts, th, reproj=True):
     return n, bi[:p.n].copy(), bd[:p.n].copy()
 
 
+def _fuse_points(pts):
+    a = _arrs(pts, [("use", np.uint8), ("u", np.float32), ("v", np.float32), ("ur", np.float32),
+                    ("pred_level", np.int32), ("desc", np.uint8)])
+    return FusePoints(len(a["use"]), *[_p(a[k]) for k in ("use", "u", "v", "ur", "pred_level", "desc")]), a
+
+
+def search_by_projection_kf(f, kf_points, th, orb_dist, check_ori):
+    """ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
+    (ORBmatcher.cc:1475-1602).  f: proj_frame dict whose has_mp_obs = mvpMapPoints != NULL;
+    kf_points: valid, u, v, octave (predicted level), angle, desc.  Returns (n, match)."""
+    s, keep = proj_frame(f)
+    a = _arrs(kf_points, [("valid", np.uint8), ("u", np.float32), ("v", np.float32),
+                          ("ur", np.float32), ("octave", np.int32), ("angle", np.float32),
+                          ("desc", np.uint8)])
+    p = ProjLast(len(a["valid"]), *[_p(a[k]) for k in ("valid", "u", "v", "ur", "octave", "angle",
+                                                        "desc")])
+    match = np.zeros(max(s.n, 1), np.int32)
+    n = lib().oracle_search_by_projection_kf(C.byref(s), C.byref(p), C.c_float(th),
+                                             C.c_int(int(orb_dist)), C.c_int(int(check_ori)),
+                                             _p(match))
+    return n, match[:s.n].copy()
+
+
+def search_by_projection_sim3(kf, pts, th):
+    """ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)
+    (ORBmatcher.cc:290-403).  kf: proj_frame dict whose has_mp_obs = vpMatched != NULL; pts:
+    use, u, v, pred_level, desc.  Returns (n, match)."""
+    s, keep = proj_frame(kf)
+    p, a = _fuse_points(pts)
+    match = np.zeros(max(s.n, 1), np.int32)
+    n = lib().oracle_search_by_projection_sim3(C.byref(s), C.byref(p), C.c_float(th), _p(match))
+    return n, match[:s.n].copy()
+
+
+def search_by_sim3(kf1, kf2, pts12, pts21, th):
+    """ORBmatcher::SearchBySim3 (ORBmatcher.cc:1105-1329).  pts12: KF1's points projected into
+    KF2 (one per KF1 keypoint), pts21: KF2's into KF1.  Returns (nFound, m12)."""
+    s1, k1 = proj_frame(kf1)
+    s2, k2 = proj_frame(kf2)
+    p12, a12 = _fuse_points(pts12)
+    p21, a21 = _fuse_points(pts21)
+    m12 = np.zeros(max(p12.n, 1), np.int32)
+    n = lib().oracle_search_by_sim3(C.byref(s1), C.byref(s2), C.byref(p12), C.byref(p21),
+                                    C.c_float(th), _p(m12))
+    return n, m12[:p12.n].copy()
+
+
 # ---------------------------------------------------------------- AR marker path (cvorb_oracle.cc)
 DMATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
                          ("distance", "<f4")])

@@ -99,6 +99,13 @@ int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_l
 int oracle_search_for_initialization(const orbx_proj_frame* F1, const orbx_proj_frame* F2,
                                      float* prev, float nnratio, int check_ori, int window,
                                      int32_t* m12);
+int oracle_search_by_projection_kf(const orbx_proj_frame* F, const orbx_proj_last* P, float th,
+                                   int ORBdist, int check_ori, int32_t* match);
+int oracle_search_by_projection_sim3(const orbx_proj_frame* KF, const orbx_fuse_points* M,
+                                     float th, int32_t* match);
+int oracle_search_by_sim3(const orbx_proj_frame* KF1, const orbx_proj_frame* KF2,
+                          const orbx_fuse_points* M12, const orbx_fuse_points* M21, float th,
+                          int32_t* m12);
 int oracle_fuse(const orbx_proj_frame* KF, const float* inv_sigma2, const orbx_fuse_points* M,
                 float th, int reproj, int32_t* best_idx, int32_t* best_dist);
 

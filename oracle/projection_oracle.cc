@@ -9,6 +9,10 @@
 //   ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th)                     (ORBmatcher.cc:828-978)
 //   ORBmatcher::Fuse(KeyFrame*, Scw, vector<MapPoint*>, th, vpReplacePoint) (ORBmatcher.cc:980-1103)
 //   (the per-point search; KeyFrame::GetFeaturesInArea, KeyFrame.cc:518-558)
+//   ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
+//                                                                          (ORBmatcher.cc:1475-1602)
+//   ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:290-403)
+//   ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)    (ORBmatcher.cc:1105-1329)
 // TEST INFRASTRUCTURE ONLY (see orb_oracle.h).  MapPoint state enters as plain arrays: the
 // caller evaluates mbTrackInView / isBad / the projections (Frame::isInFrustum, the pose
 // products) exactly as the reference does and passes the results; every MapPoint passed has
@@ -368,6 +372,161 @@ int oracle_fuse(const orbx_proj_frame* KF, const float* inv_sigma2, const orbx_f
     }
   }
   return nf;
+}
+
+// SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (relocalization): F's
+// has_mp_obs = mvpMapPoints[i] != NULL on entry; P: valid (pMP, !isBad, not already found, the
+// distance-invariance gate), u, v, octave = the predicted level, angle = pKF->mvKeysUn[i].angle,
+// desc.  match[f] = the keyframe index whose map point was assigned to f, else -1.
+int oracle_search_by_projection_kf(const orbx_proj_frame* F, const orbx_proj_last* P, float th,
+                                   int ORBdist, int check_ori, int32_t* match) {
+  Grid G;
+  assign_grid(F, &G);
+  std::vector<uint8_t> has(F->n, 0);  // CurrentFrame.mvpMapPoints[i2] != NULL
+  for (int i = 0; i < F->n; i++) {
+    match[i] = -1;
+    if (F->has_mp_obs && F->has_mp_obs[i]) has[i] = 1;
+  }
+  const int HISTO = 30;
+  const float factor = 1.0f / HISTO;
+  std::vector<int> rotHist[30];
+  int nmatches = 0;
+  for (int i = 0; i < P->n; i++) {
+    if (!P->valid[i]) continue;
+    const float u = P->u[i], v = P->v[i];
+    if (u < F->min_x || u > F->max_x) continue;  // :1512-1515
+    if (v < F->min_y || v > F->max_y) continue;
+    const int nPredictedLevel = P->octave[i];
+    const float radius = th * F->scale_factors[nPredictedLevel];  // :1530
+    const std::vector<int> vIndices2 =
+        features_in_area(F, G, u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1);
+    if (vIndices2.empty()) continue;
+    const uint8_t* dMP = P->desc + (size_t)i * 32;
+    int bestDist = 256, bestIdx2 = -1;
+    for (int i2 : vIndices2) {
+      if (has[i2]) continue;  // :1546-1547
+      const int dist = hamming(dMP, F->desc + (size_t)i2 * 32);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = i2;
+      }
+    }
+    if (bestDist <= ORBdist) {  // :1560-1576
+      has[bestIdx2] = 1;
+      match[bestIdx2] = i;
+      nmatches++;
+      if (check_ori) {
+        float rot = P->angle[i] - F->keys_un[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == HISTO) bin = 0;
+        rotHist[bin].push_back(bestIdx2);
+      }
+    }
+  }
+  if (check_ori) {  // :1582-1598
+    int hs[30];
+    for (int b = 0; b < HISTO; b++) hs[b] = (int)rotHist[b].size();
+    int ind1, ind2, ind3;
+    three_maxima(hs, HISTO, &ind1, &ind2, &ind3);
+    for (int b = 0; b < HISTO; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (int idx : rotHist[b]) {
+        match[idx] = -1;
+        nmatches--;
+      }
+    }
+  }
+  return nmatches;
+}
+
+// SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (loop closing): KF's has_mp_obs =
+// vpMatched[f] != NULL on entry; M: use (the gates of :318-352), u, v, pred_level, desc.
+// match[f] = the point index assigned to keyframe feature f in this call, else -1.
+int oracle_search_by_projection_sim3(const orbx_proj_frame* KF, const orbx_fuse_points* M,
+                                     float th, int32_t* match) {
+  Grid G;
+  assign_grid(KF, &G);
+  std::vector<uint8_t> matched(KF->n, 0);  // vpMatched[idx] != NULL
+  for (int i = 0; i < KF->n; i++) {
+    match[i] = -1;
+    if (KF->has_mp_obs && KF->has_mp_obs[i]) matched[i] = 1;
+  }
+  int nmatches = 0;
+  for (int iMP = 0; iMP < M->n; iMP++) {
+    if (!M->use[iMP]) continue;
+    const int nPredictedLevel = M->pred_level[iMP];
+    const float radius = th * KF->scale_factors[nPredictedLevel];  // :354-356
+    // KeyFrame::GetFeaturesInArea(u, v, radius): no level window (KeyFrame.cc:518-558)
+    const std::vector<int> vIndices = features_in_area(KF, G, M->u[iMP], M->v[iMP], radius, -1, -1);
+    if (vIndices.empty()) continue;
+    const uint8_t* dMP = M->desc + (size_t)iMP * 32;
+    int bestDist = 256, bestIdx = -1;
+    for (int idx : vIndices) {
+      if (matched[idx]) continue;  // :360-361
+      const int kpLevel = KF->keys_un[idx].octave;
+      if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;  // :364-367
+      const int dist = hamming(dMP, KF->desc + (size_t)idx * 32);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= 50) {  // TH_LOW (:384-388)
+      matched[bestIdx] = 1;
+      match[bestIdx] = iMP;
+      nmatches++;
+    }
+  }
+  return nmatches;
+}
+
+// SearchBySim3 (:1105-1329): one direction's per-point search (KeyFrame::GetFeaturesInArea, the
+// level window [pred - 1, pred], first minimum from INT_MAX, accepted when <= TH_HIGH).
+static void sim3_direction(const orbx_proj_frame* KF, const orbx_fuse_points* M, float th,
+                           std::vector<int>* vnMatch) {
+  Grid G;
+  assign_grid(KF, &G);
+  vnMatch->assign(M->n, -1);
+  for (int i = 0; i < M->n; i++) {
+    if (!M->use[i]) continue;
+    const int nPredictedLevel = M->pred_level[i];
+    const float radius = th * KF->scale_factors[nPredictedLevel];  // :1183, :1258
+    const std::vector<int> vIndices = features_in_area(KF, G, M->u[i], M->v[i], radius, -1, -1);
+    if (vIndices.empty()) continue;
+    const uint8_t* dMP = M->desc + (size_t)i * 32;
+    int bestDist = INT_MAX, bestIdx = -1;
+    for (int idx : vIndices) {
+      const int kl = KF->keys_un[idx].octave;
+      if (kl < nPredictedLevel - 1 || kl > nPredictedLevel) continue;
+      const int dist = hamming(dMP, KF->desc + (size_t)idx * 32);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= 100) (*vnMatch)[i] = bestIdx;  // TH_HIGH
+  }
+}
+
+// m12[i1] = idx2 where both directions agree (vpMatches12[i1] = vpMapPoints2[idx2]), else -1.
+// Returns nFound.  M12: KF1's points projected into KF2 (n = KF1->n); M21: KF2's into KF1.
+int oracle_search_by_sim3(const orbx_proj_frame* KF1, const orbx_proj_frame* KF2,
+                          const orbx_fuse_points* M12, const orbx_fuse_points* M21, float th,
+                          int32_t* m12) {
+  std::vector<int> vnMatch1, vnMatch2;
+  sim3_direction(KF2, M12, th, &vnMatch1);
+  sim3_direction(KF1, M21, th, &vnMatch2);
+  int nFound = 0;
+  for (int i1 = 0; i1 < M12->n; i1++) {  // :1305-1326
+    m12[i1] = -1;
+    const int idx2 = vnMatch1[i1];
+    if (idx2 >= 0 && idx2 < M21->n && vnMatch2[idx2] == i1) {
+      m12[i1] = idx2;
+      nFound++;
+    }
+  }
+  return nFound;
 }
 
 }  // extern "C"

@@ -94,3 +94,56 @@ def fuse_scene(w=640, h=480, nf=1000, t=5, seed=0, stereo=False, jitter=1.5):
                desc=desc)
     F["inv_level_sigma2"] = tb["inv_sigma2"]
     return F, pts
+
+
+def reloc_scene(w=640, h=480, nf=1000, t=5, seed=0):
+    """Tracking::Relocalization (Tracking.cc:1441-1468): the current frame (with the map points
+    SearchByBoW / an earlier pass already assigned: mvpMapPoints != NULL blocks a feature) and a
+    candidate keyframe's map points projected into it; octave = the predicted level, angle = the
+    keyframe keypoint's."""
+    F, _, last = scene(w, h, nf, t, seed, stereo=False, mp_frac=0.15)
+    F["u_right"] = None
+    rng = np.random.default_rng(200 + seed)
+    n0 = len(last["valid"])
+    pts = dict(last, octave=np.clip(last["octave"] + rng.integers(-1, 2, n0), 0, 7).astype(np.int32))
+    return F, pts
+
+
+def loop_scene(w=640, h=480, nf=1000, t=5, seed=0):
+    """LoopClosing::ComputeSim3 / CorrectLoop's SearchByProjection(pKF, Scw, vpPoints, vpMatched,
+    th): the keyframe with vpMatched already set for some features, the loop's map points
+    projected with Scw."""
+    K, P = fuse_scene(w, h, nf, t, seed, stereo=False)
+    rng = np.random.default_rng(300 + seed)
+    K["has_mp_obs"] = (rng.random(len(K["keys_un"])) < 0.1).astype(np.uint8)
+    K["u_right"] = None
+    return K, P
+
+
+def sim3_scene(w=640, h=480, nf=1000, t=5, seed=0):
+    """LoopClosing::ComputeSim3's SearchBySim3 (LoopClosing.cc:305): KF1 = frame t-1, KF2 =
+    frame t of the synthetic sequence (features move by (-1, -1)); KF1's map points projected
+    into KF2 near where their features moved and KF2's projected back, one entry per keypoint,
+    with descriptor bit flips, jitter and predicted levels near the octave."""
+    p = O.params(nf)
+    tb = O.tables(p, w, h)
+    base = synth.canvas(w, h, 2)
+    k1, d1 = O.extract(synth.frame(w, h, t - 1, 2, base), p)
+    k2, d2 = O.extract(synth.frame(w, h, t, 2, base), p)
+    K1 = frame_dict(k1, d1, w, h, tb["scale"])
+    K2 = frame_dict(k2, d2, w, h, tb["scale"])
+    rng = np.random.default_rng(400 + seed)
+
+    def project(kp, desc, dxy):
+        n = len(kp)
+        d = desc.copy()
+        flips = rng.integers(0, 256, (n, 6))
+        for k in range(6):
+            d[np.arange(n), flips[:, k] // 8] ^= (1 << (flips[:, k] % 8)).astype(np.uint8)
+        return dict(use=(rng.random(n) < 0.85).astype(np.uint8),
+                    u=(kp["x"] + dxy + rng.normal(0, 1.0, n)).astype(np.float32),
+                    v=(kp["y"] + dxy + rng.normal(0, 1.0, n)).astype(np.float32),
+                    ur=np.zeros(n, np.float32),
+                    pred_level=np.clip(kp["octave"] + rng.integers(-1, 2, n), 0, 7).astype(np.int32),
+                    desc=d)
+    return K1, K2, project(k1, d1, -1.0), project(k2, d2, 1.0)

@@ -114,3 +114,62 @@ def test_fuse_edge_cases():
     # projections outside the keyframe's grid
     n, bi, _ = ORBmatcher().Fuse(K, dict(P, u=P["u"] + 5000), 3.0, sim3=True)
     assert n == 0 and (bi == -1).all()
+
+
+@pytest.mark.parametrize("th,orb_dist,ori", [(10.0, 100, True), (10.0, 50, False), (5.0, 64, True)])
+def test_search_by_projection_relocalization(th, orb_dist, ori):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1475-1602),
+    as Tracking::Relocalization calls it (th 10 / ORBdist 100, then th 3 / 64): match array and
+    count equal the oracle's."""
+    from projdata import reloc_scene
+    F, L = reloc_scene(seed=int(th) + orb_dist)
+    on, om = O.search_by_projection_kf(F, L, th, orb_dist, ori)
+    n, m = ORBmatcher(0.75, ori).SearchByProjectionKF(F, L, th, orb_dist)
+    assert n == on and np.array_equal(m, om)
+    assert n > 100
+
+
+@pytest.mark.parametrize("th,seed", [(10.0, 0), (5.0, 1)])
+def test_search_by_projection_sim3(th, seed):
+    """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:290-403)."""
+    from projdata import loop_scene
+    K, P = loop_scene(seed=seed)
+    on, om = O.search_by_projection_sim3(K, P, th)
+    n, m = ORBmatcher(0.75, True).SearchByProjectionSim3(K, P, th)
+    assert n == on and np.array_equal(m, om)
+    assert n > 100
+
+
+@pytest.mark.parametrize("th,seed", [(7.5, 0), (3.0, 1)])
+def test_search_by_sim3(th, seed):
+    """SearchBySim3 (ORBmatcher.cc:1105-1329; LoopClosing::ComputeSim3, th 7.5): both directions'
+    searches and the agreement equal the oracle's."""
+    from projdata import sim3_scene
+    K1, K2, P12, P21 = sim3_scene(seed=seed)
+    on, om = O.search_by_sim3(K1, K2, P12, P21, th)
+    n, m = ORBmatcher(0.75, True).SearchBySim3(K1, K2, P12, P21, th)
+    assert n == on and np.array_equal(m, om)
+    assert n > 100
+
+
+def test_relocalization_and_loop_searches_edge_cases():
+    from projdata import loop_scene, reloc_scene, sim3_scene
+    F, L = reloc_scene()
+    mt = ORBmatcher(0.75, True)
+    # every current feature already holds a map point: nothing can be assigned
+    n, m = mt.SearchByProjectionKF(dict(F, has_mp_obs=np.ones(len(F["keys_un"]), np.uint8)), L, 10, 100)
+    assert n == 0 and (m == -1).all()
+    # no valid keyframe point / ORBdist 0
+    n, _ = mt.SearchByProjectionKF(F, dict(L, valid=np.zeros_like(L["valid"])), 10, 100)
+    assert n == 0
+    on, om = O.search_by_projection_kf(F, L, 10, 0, True)
+    n, m = mt.SearchByProjectionKF(F, L, 10, 0)
+    assert n == on and np.array_equal(m, om)
+    K, P = loop_scene()
+    e = {k: v[:0] for k, v in P.items()}
+    n, m = mt.SearchByProjectionSim3(K, e, 10)
+    assert n == 0 and (m == -1).all()
+    K1, K2, P12, P21 = sim3_scene()
+    # nothing usable in one direction: no agreement
+    n, m = mt.SearchBySim3(K1, K2, P12, dict(P21, use=np.zeros_like(P21["use"])), 7.5)
+    assert n == 0 and (m == -1).all()

@@ -334,3 +334,160 @@ def test_fuse(stereo, th, reproj):
     pi, pd = py_fuse(K, P, th, reproj)
     assert np.array_equal(bi, pi) and np.array_equal(bd, pd)
     assert n == (pi >= 0).sum() and n > 100
+
+
+def _rot_bin(a_point, a_feat):
+    rot = F32(F32(a_point) - F32(a_feat))
+    if rot < 0:
+        rot = F32(rot + F32(360))
+    t = F32(rot * F32(F32(1) / F32(30)))
+    b = int(math.floor(abs(float(t)) + 0.5))
+    return 0 if b == 30 else b
+
+
+def _keep_three_maxima(hist, match, nm):
+    """ComputeThreeMaxima (ORBmatcher.cc:1604-1645) and the removal of the other bins."""
+    m1 = m2 = m3 = 0
+    i1 = i2 = i3 = -1
+    for b in range(30):
+        s = len(hist[b])
+        if s > m1:
+            m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, b
+        elif s > m2:
+            m3, m2, i3, i2 = m2, s, i2, b
+        elif s > m3:
+            m3, i3 = s, b
+    if m2 < F32(0.1) * F32(m1):
+        i2 = i3 = -1
+    elif m3 < F32(0.1) * F32(m1):
+        i3 = -1
+    for b in range(30):
+        if b not in (i1, i2, i3):
+            for idx in hist[b]:
+                match[idx] = -1
+                nm -= 1
+    return nm
+
+
+def py_reloc(F, L, th, orb_dist, ori):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist), ORBmatcher.cc:1475-1602."""
+    g = grid(F)
+    n = len(F["keys_un"])
+    has = [bool(F["has_mp_obs"][i]) for i in range(n)]
+    match = [-1] * n
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for i in range(len(L["valid"])):
+        if not L["valid"][i]:
+            continue
+        u, v = F32(L["u"][i]), F32(L["v"][i])
+        if u < F["min_x"] or u > F["max_x"] or v < F["min_y"] or v > F["max_y"]:
+            continue
+        lev = int(L["octave"][i])
+        rad = F32(F32(th) * F32(F["scale_factors"][lev]))
+        bd, bi = 256, -1
+        for idx in in_area(F, g, u, v, rad, lev - 1, lev + 1):
+            if has[idx]:
+                continue
+            d = ham(L["desc"][i], F["desc"][idx])
+            if d < bd:
+                bd, bi = d, idx
+        if bd <= orb_dist:
+            has[bi] = True
+            match[bi] = i
+            nm += 1
+            if ori:
+                hist[_rot_bin(L["angle"][i], F["keys_un"][bi]["angle"])].append(bi)
+    if ori:
+        nm = _keep_three_maxima(hist, match, nm)
+    return nm, np.array(match, np.int32)
+
+
+def py_proj_sim3(K, P, th):
+    """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th), ORBmatcher.cc:290-403."""
+    g = grid(K)
+    n = len(K["keys_un"])
+    matched = [bool(K["has_mp_obs"][i]) for i in range(n)]
+    match = [-1] * n
+    nm = 0
+    for i in range(len(P["use"])):
+        if not P["use"][i]:
+            continue
+        lev = int(P["pred_level"][i])
+        rad = F32(F32(th) * F32(K["scale_factors"][lev]))
+        bd, bi = 256, -1
+        for idx in in_area(K, g, F32(P["u"][i]), F32(P["v"][i]), rad):
+            if matched[idx]:
+                continue
+            kl = int(K["keys_un"][idx]["octave"])
+            if kl < lev - 1 or kl > lev:
+                continue
+            d = ham(P["desc"][i], K["desc"][idx])
+            if d < bd:
+                bd, bi = d, idx
+        if bd <= 50:
+            matched[bi] = True
+            match[bi] = i
+            nm += 1
+    return nm, np.array(match, np.int32)
+
+
+def py_search_by_sim3(K1, K2, P12, P21, th):
+    """SearchBySim3, ORBmatcher.cc:1105-1329 (the two per-point searches and the agreement)."""
+    def direction(K, P):
+        g = grid(K)
+        out = []
+        for i in range(len(P["use"])):
+            best = -1
+            if P["use"][i]:
+                lev = int(P["pred_level"][i])
+                rad = F32(F32(th) * F32(K["scale_factors"][lev]))
+                bd, bi = 2 ** 31 - 1, -1
+                for idx in in_area(K, g, F32(P["u"][i]), F32(P["v"][i]), rad):
+                    kl = int(K["keys_un"][idx]["octave"])
+                    if kl < lev - 1 or kl > lev:
+                        continue
+                    d = ham(P["desc"][i], K["desc"][idx])
+                    if d < bd:
+                        bd, bi = d, idx
+                if bd <= 100:
+                    best = bi
+            out.append(best)
+        return out
+    v1, v2 = direction(K2, P12), direction(K1, P21)
+    m12 = [-1] * len(v1)
+    for i1, idx2 in enumerate(v1):
+        if idx2 >= 0 and v2[idx2] == i1:
+            m12[i1] = idx2
+    m12 = np.array(m12, np.int32)
+    return int((m12 >= 0).sum()), m12
+
+
+@pytest.mark.parametrize("th,orb_dist,ori", [(10.0, 100, True), (10.0, 50, False), (5.0, 64, True)])
+def test_search_by_projection_relocalization(th, orb_dist, ori):
+    from projdata import reloc_scene
+    F, L = reloc_scene(seed=int(th) + orb_dist)
+    n, m = O.search_by_projection_kf(F, L, th, orb_dist, ori)
+    pn, pm = py_reloc(F, L, th, orb_dist, ori)
+    assert n == pn and np.array_equal(m, pm)
+    assert n > 100
+
+
+@pytest.mark.parametrize("th,seed", [(10.0, 0), (5.0, 1)])
+def test_search_by_projection_sim3(th, seed):
+    from projdata import loop_scene
+    K, P = loop_scene(seed=seed)
+    n, m = O.search_by_projection_sim3(K, P, th)
+    pn, pm = py_proj_sim3(K, P, th)
+    assert n == pn and np.array_equal(m, pm)
+    assert n > 100
+
+
+@pytest.mark.parametrize("th,seed", [(7.5, 0), (3.0, 1)])
+def test_search_by_sim3(th, seed):
+    from projdata import sim3_scene
+    K1, K2, P12, P21 = sim3_scene(seed=seed)
+    n, m = O.search_by_sim3(K1, K2, P12, P21, th)
+    pn, pm = py_search_by_sim3(K1, K2, P12, P21, th)
+    assert n == pn and np.array_equal(m, pm)
+    assert n > 100
