@@ -5,10 +5,10 @@
 // library's source list (-I<repo>/include -I<repo>/include/compat, -I ORB_SLAM2/src for the
 // host file), link -lorbx.
 //
-// GPU: SearchByBoW (both), SearchForTriangulation, SearchByProjection (local map, last frame),
-// SearchForInitialization, Fuse (both: the per-point search; the replace / add-observation step
-// stays here, in the reference's order).  The relocalisation and Sim3 projections and
-// SearchBySim3 are forwarded to the reference's own code (ORBmatcherHost).  Every GPU call falls
+// GPU: SearchByBoW (both), SearchForTriangulation, SearchByProjection (all four: local map, last
+// frame, relocalisation, loop-closing Sim3), SearchForInitialization, SearchBySim3, Fuse (both:
+// the per-point search; the replace / add-observation step stays here, in the reference's
+// order).  Only DescriptorDistance on single pairs stays on the host.  Every GPU call falls
 // back to the reference's code on a device error (logged once), so callers see the reference's
 // results either way.  MapPoint pointers become masks before a call and come back from the
 // returned indices after it.  Reentrant: Tracking, LocalMapping and LoopClosing call these at
@@ -294,25 +294,211 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
   return nm;
 }
 
-// relocalisation (:1475-1602) and loop detection (:290-403) projections: the reference's code
+// SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (:1475-1602,
+// Tracking::Relocalization): the projection and gates with the reference's cv::Mat code
+// (:1477-1526), the search on the GPU.  Any map point of the current frame blocks its feature.
 int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
                                    const std::set<MapPoint*>& sAlreadyFound, const float th,
                                    const int ORBdist) {
-  return ORBmatcherHost(mfNNratio, mbCheckOrientation)
-      .SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist);
+  const cv::Mat Rcw = CurrentFrame.mTcw.rowRange(0, 3).colRange(0, 3);
+  const cv::Mat tcw = CurrentFrame.mTcw.rowRange(0, 3).col(3);
+  const cv::Mat Ow = -Rcw.t() * tcw;
+  const std::vector<MapPoint*> vpMPs = pKF->GetMapPointMatches();
+  const int nk = (int)vpMPs.size(), m = std::max(nk, 1);
+  std::vector<uint8_t> valid(m, 0), has(std::max(CurrentFrame.N, 1)), desc(32 * (size_t)m);
+  std::vector<float> u(m), v(m), ang(m);
+  std::vector<int32_t> lev(m);
+  for (int i = 0; i < nk; i++) {
+    MapPoint* pMP = vpMPs[i];
+    if (!pMP || pMP->isBad() || sAlreadyFound.count(pMP)) continue;
+    cv::Mat x3Dw = pMP->GetWorldPos();
+    cv::Mat x3Dc = Rcw * x3Dw + tcw;
+    const float xc = x3Dc.at<float>(0);
+    const float yc = x3Dc.at<float>(1);
+    const float invzc = 1.0 / x3Dc.at<float>(2);
+    u[i] = CurrentFrame.fx * xc * invzc + CurrentFrame.cx;
+    v[i] = CurrentFrame.fy * yc * invzc + CurrentFrame.cy;
+    // (the image-bounds test runs in the library, as the reference's next lines)
+    cv::Mat PO = x3Dw - Ow;
+    const float dist3D = cv::norm(PO);
+    const float maxDistance = pMP->GetMaxDistanceInvariance();
+    const float minDistance = pMP->GetMinDistanceInvariance();
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    lev[i] = pMP->PredictScale(dist3D, CurrentFrame.mfLogScaleFactor);
+    ang[i] = pKF->mvKeysUn[i].angle;
+    const cv::Mat d = pMP->GetDescriptor();
+    std::copy(d.data, d.data + 32, desc.begin() + 32 * i);
+    valid[i] = 1;
+  }
+  for (int i = 0; i < CurrentFrame.N; i++) has[i] = CurrentFrame.mvpMapPoints[i] != NULL;
+  orbx_proj_frame fr = frame_view(CurrentFrame, has.data());
+  fr.u_right = nullptr;
+  const orbx_proj_last pts{nk, valid.data(), u.data(), v.data(), nullptr, lev.data(), ang.data(),
+                           desc.data()};
+  std::vector<int32_t> match(std::max(CurrentFrame.N, 1));
+  int32_t nm = 0;
+  const int rc = orbx_search_by_projection_kf(&fr, &pts, th, ORBdist, mbCheckOrientation,
+                                              match.data(), &nm);
+  if (rc != ORBX_OK) {
+    log_fallback("orbx_search_by_projection_kf", rc);
+    return ORBmatcherHost(mfNNratio, mbCheckOrientation)
+        .SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist);
+  }
+  for (int i = 0; i < CurrentFrame.N; i++)
+    if (match[i] >= 0) CurrentFrame.mvpMapPoints[i] = vpMPs[match[i]];
+  return nm;
 }
 
+// SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (:290-403, loop closing): the Sim3
+// decomposition, projection and gates with the reference's code (:292-352), the search on the GPU
 int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
                                    std::vector<MapPoint*>& vpMatched, int th) {
-  return ORBmatcherHost(mfNNratio, mbCheckOrientation)
-      .SearchByProjection(pKF, Scw, vpPoints, vpMatched, th);
+  const float& fx = pKF->fx;
+  const float& fy = pKF->fy;
+  const float& cx = pKF->cx;
+  const float& cy = pKF->cy;
+  cv::Mat sRcw = Scw.rowRange(0, 3).colRange(0, 3);
+  const float scw = std::sqrt(sRcw.row(0).dot(sRcw.row(0)));
+  cv::Mat Rcw = sRcw / scw;
+  cv::Mat tcw = Scw.rowRange(0, 3).col(3) / scw;
+  cv::Mat Ow = -Rcw.t() * tcw;
+  std::set<MapPoint*> spAlreadyFound(vpMatched.begin(), vpMatched.end());
+  spAlreadyFound.erase(static_cast<MapPoint*>(NULL));
+  const int np = (int)vpPoints.size(), m = std::max(np, 1);
+  std::vector<uint8_t> use(m, 0), desc(32 * (size_t)m), matched(std::max(pKF->N, 1));
+  std::vector<float> u(m), v(m);
+  std::vector<int32_t> lev(m);
+  for (int i = 0; i < np; i++) {
+    MapPoint* pMP = vpPoints[i];
+    if (pMP->isBad() || spAlreadyFound.count(pMP)) continue;
+    cv::Mat p3Dw = pMP->GetWorldPos();
+    cv::Mat p3Dc = Rcw * p3Dw + tcw;
+    if (p3Dc.at<float>(2) < 0.0) continue;
+    const float invz = 1 / p3Dc.at<float>(2);
+    const float x = p3Dc.at<float>(0) * invz;
+    const float y = p3Dc.at<float>(1) * invz;
+    u[i] = fx * x + cx;
+    v[i] = fy * y + cy;
+    if (!pKF->IsInImage(u[i], v[i])) continue;
+    const float maxDistance = pMP->GetMaxDistanceInvariance();
+    const float minDistance = pMP->GetMinDistanceInvariance();
+    cv::Mat PO = p3Dw - Ow;
+    const float dist = cv::norm(PO);
+    if (dist < minDistance || dist > maxDistance) continue;
+    cv::Mat Pn = pMP->GetNormal();
+    if (PO.dot(Pn) < 0.5 * dist) continue;
+    lev[i] = pMP->PredictScale(dist, pKF->mfLogScaleFactor);
+    const cv::Mat d = pMP->GetDescriptor();
+    std::copy(d.data, d.data + 32, desc.begin() + 32 * i);
+    use[i] = 1;
+  }
+  for (int i = 0; i < pKF->N; i++) matched[i] = vpMatched[i] != NULL;
+  orbx_proj_frame kf = keyframe_view(pKF);
+  kf.has_mp_obs = matched.data();
+  const orbx_fuse_points pts{np, use.data(), u.data(), v.data(), nullptr, lev.data(), desc.data()};
+  std::vector<int32_t> match(std::max(pKF->N, 1));
+  int32_t nm = 0;
+  const int rc = orbx_search_by_projection_sim3(&kf, &pts, (float)th, match.data(), &nm);
+  if (rc != ORBX_OK) {
+    log_fallback("orbx_search_by_projection_sim3", rc);
+    return ORBmatcherHost(mfNNratio, mbCheckOrientation)
+        .SearchByProjection(pKF, Scw, vpPoints, vpMatched, th);
+  }
+  for (int i = 0; i < pKF->N; i++)
+    if (match[i] >= 0) vpMatched[i] = vpPoints[match[i]];
+  return nm;
 }
 
+// SearchBySim3 (:1105-1329; LoopClosing::ComputeSim3): both directions' projections and gates
+// with the reference's code (:1108-1180, :1208-1255), the searches and the agreement on the GPU
 int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12,
                              const float& s12, const cv::Mat& R12, const cv::Mat& t12,
                              const float th) {
-  return ORBmatcherHost(mfNNratio, mbCheckOrientation)
-      .SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th);
+  const float& fx = pKF1->fx;
+  const float& fy = pKF1->fy;
+  const float& cx = pKF1->cx;
+  const float& cy = pKF1->cy;
+  cv::Mat R1w = pKF1->GetRotation();
+  cv::Mat t1w = pKF1->GetTranslation();
+  cv::Mat R2w = pKF2->GetRotation();
+  cv::Mat t2w = pKF2->GetTranslation();
+  cv::Mat sR12 = s12 * R12;
+  cv::Mat sR21 = (1.0 / s12) * R12.t();
+  cv::Mat t21 = -sR21 * t12;
+  const std::vector<MapPoint*> vpMapPoints1 = pKF1->GetMapPointMatches();
+  const std::vector<MapPoint*> vpMapPoints2 = pKF2->GetMapPointMatches();
+  const int N1 = (int)vpMapPoints1.size(), N2 = (int)vpMapPoints2.size();
+  std::vector<bool> vbAlreadyMatched1(N1, false), vbAlreadyMatched2(N2, false);
+  for (int i = 0; i < N1; i++) {
+    MapPoint* pMP = vpMatches12[i];
+    if (pMP) {
+      vbAlreadyMatched1[i] = true;
+      const int idx2 = pMP->GetIndexInKeyFrame(pKF2);
+      if (idx2 >= 0 && idx2 < N2) vbAlreadyMatched2[idx2] = true;
+    }
+  }
+  struct Side {
+    std::vector<uint8_t> use, desc;
+    std::vector<float> u, v;
+    std::vector<int32_t> lev;
+  } sd[2];
+  // direction 0: KF1's points into KF2 (p3Dc2 = sR21 (R1w p + t1w) + t21); 1: KF2's into KF1
+  for (int k = 0; k < 2; k++) {
+    const std::vector<MapPoint*>& vp = k == 0 ? vpMapPoints1 : vpMapPoints2;
+    const std::vector<bool>& already = k == 0 ? vbAlreadyMatched1 : vbAlreadyMatched2;
+    KeyFrame* pTo = k == 0 ? pKF2 : pKF1;
+    const int n = (int)vp.size(), m = std::max(n, 1);
+    Side& S = sd[k];
+    S.use.assign(m, 0);
+    S.desc.assign(32 * (size_t)m, 0);
+    S.u.assign(m, 0.f);
+    S.v.assign(m, 0.f);
+    S.lev.assign(m, 0);
+    for (int i = 0; i < n; i++) {
+      MapPoint* pMP = vp[i];
+      if (!pMP || already[i] || pMP->isBad()) continue;
+      cv::Mat p3Dw = pMP->GetWorldPos();
+      cv::Mat p3Dc;
+      if (k == 0) {  // the reference's two statements (:1160-1161, :1235-1236)
+        cv::Mat p3Dc1 = R1w * p3Dw + t1w;
+        p3Dc = sR21 * p3Dc1 + t21;
+      } else {
+        cv::Mat p3Dc2 = R2w * p3Dw + t2w;
+        p3Dc = sR12 * p3Dc2 + t12;
+      }
+      if (p3Dc.at<float>(2) < 0.0) continue;
+      const float invz = 1.0 / p3Dc.at<float>(2);
+      const float x = p3Dc.at<float>(0) * invz;
+      const float y = p3Dc.at<float>(1) * invz;
+      S.u[i] = fx * x + cx;
+      S.v[i] = fy * y + cy;
+      if (!pTo->IsInImage(S.u[i], S.v[i])) continue;
+      const float maxDistance = pMP->GetMaxDistanceInvariance();
+      const float minDistance = pMP->GetMinDistanceInvariance();
+      const float dist3D = cv::norm(p3Dc);
+      if (dist3D < minDistance || dist3D > maxDistance) continue;
+      S.lev[i] = pMP->PredictScale(dist3D, pTo->mfLogScaleFactor);
+      const cv::Mat d = pMP->GetDescriptor();
+      std::copy(d.data, d.data + 32, S.desc.begin() + 32 * i);
+      S.use[i] = 1;
+    }
+  }
+  const orbx_proj_frame k1 = keyframe_view(pKF1), k2 = keyframe_view(pKF2);
+  const orbx_fuse_points p12{N1, sd[0].use.data(), sd[0].u.data(), sd[0].v.data(), nullptr,
+                             sd[0].lev.data(), sd[0].desc.data()};
+  const orbx_fuse_points p21{N2, sd[1].use.data(), sd[1].u.data(), sd[1].v.data(), nullptr,
+                             sd[1].lev.data(), sd[1].desc.data()};
+  std::vector<int32_t> m12(std::max(N1, 1));
+  int32_t nFound = 0;
+  const int rc = orbx_search_by_sim3(&k1, &k2, &p12, &p21, th, m12.data(), &nFound);
+  if (rc != ORBX_OK) {
+    log_fallback("orbx_search_by_sim3", rc);
+    return ORBmatcherHost(mfNNratio, mbCheckOrientation)
+        .SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th);
+  }
+  for (int i1 = 0; i1 < N1; i1++)  // (:1305-1326)
+    if (m12[i1] >= 0) vpMatches12[i1] = vpMapPoints2[m12[i1]];
+  return nFound;
 }
 
 // ------------------------------------------------------------------ SearchForInitialization
