@@ -1570,8 +1570,15 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
 }
 
 
+#ifndef ORBX_OCT_WAVES
+#define ORBX_OCT_WAVES 0  // amdgpu_waves_per_eu floor for k_octree (0: the compiler's choice)
+#endif
 template <int NT, class K>
-__global__ __launch_bounds__(NT) void k_octree(
+__global__ __launch_bounds__(NT)
+#if ORBX_OCT_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(ORBX_OCT_WAVES)))
+#endif
+void k_octree(
     const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
     const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
     K* __restrict__ lin, int* __restrict__ label, K* __restrict__ okey,
