@@ -64,6 +64,36 @@ def test_invalid_arguments_are_reported():
         A.ORBextractor(1000, 1.2, 0)
 
 
+def test_search_entry_points_reject_bad_arguments_without_a_gpu():
+    """Argument checks of the projection-family entry points run before any device work
+    (null structs, a predicted level outside the pyramid, SearchBySim3 point sets that are not
+    one per keypoint): ORBX_EINVAL (-1)."""
+    lib = A.lib()
+    n = C.c_int32()
+    assert lib.orbx_search_by_projection_kf(None, None, C.c_float(10), 100, 1, None, C.byref(n)) == -1
+    assert lib.orbx_search_by_projection_sim3(None, None, C.c_float(10), None, C.byref(n)) == -1
+    assert lib.orbx_search_by_sim3(None, None, None, None, C.c_float(7.5), None, C.byref(n)) == -1
+    scale = np.ones(8, np.float32)
+    kp = np.zeros(2, A.KEYPOINT_DTYPE)
+    desc = np.zeros((2, 32), np.uint8)
+    fr = _ffi.ProjFrame(2, kp.ctypes.data, desc.ctypes.data, None, None, 0.0, 0.0, 640.0, 480.0,
+                        0.1, 0.1, scale.ctypes.data, 8)
+    use = np.ones(1, np.uint8)
+    u = np.zeros(1, np.float32)
+    lev = np.array([9], np.int32)  # outside the 8-level pyramid
+    pd = np.zeros((1, 32), np.uint8)
+    pts = _ffi.FusePoints(1, use.ctypes.data, u.ctypes.data, u.ctypes.data, None, lev.ctypes.data,
+                          pd.ctypes.data)
+    match = np.zeros(2, np.int32)
+    assert lib.orbx_search_by_projection_sim3(C.byref(fr), C.byref(pts), C.c_float(10),
+                                              match.ctypes.data, C.byref(n)) == -1
+    lev[0] = 0
+    m12 = np.zeros(2, np.int32)
+    # one point for a 2-keypoint keyframe: not one entry per keypoint
+    assert lib.orbx_search_by_sim3(C.byref(fr), C.byref(fr), C.byref(pts), C.byref(pts),
+                                   C.c_float(7.5), m12.ctypes.data, C.byref(n)) == -1
+
+
 def test_empty_image_returns_untouched():
     ex = A.ORBextractor()
     assert ex(np.zeros((0, 0), np.uint8)) == (None, None)
