@@ -1012,6 +1012,12 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef ORBX_FC_PAIR
 #define ORBX_FC_PAIR 1  // stage 1: two row-pair steps per LDS round trip
 #endif
+#ifndef ORBX_FC_MAXR
+#define ORBX_FC_MAXR 42  // rows of the small k_fast_cells instance's ROI (44: round 3's first form)
+#endif
+#ifndef ORBX_FC_ROWS_ALIAS
+#define ORBX_FC_ROWS_ALIAS 1  // keep rows in the staging buffer's slack (0: their own 512 B)
+#endif
 #ifndef ORBX_FC_SCORE2
 #define ORBX_FC_SCORE2 0  // scoring: two candidates per lane per round (measured slower: 0.637 vs 0.595 ms per 512 C2 frames)
 #endif
@@ -1062,9 +1068,22 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
   __shared__ __align__(16) uint8_t s_vv[4][(MAXR - 4) * RS];
   constexpr int QCAP = (MAXR - 6) * (RS - 9);  // detection pixels of the largest cell
   __shared__ uint16_t s_q[4][QCAP];
-  __shared__ uint64_t s_rows[4][64];
+#if ORBX_FC_ROWS_ALIAS
+  // the keep bits per detection row live in the last 512 B of the wave's staging buffer: slack
+  // rows past any ROI (the pretest reads them only masked; a cell is staged before its NMS and
+  // its bits are in registers before the next cell is staged)
+  static_assert((MAXR + 12) * RS - 512 >= MAXR * RS, "keep rows past every ROI row");
+  static_assert(((MAXR + 12) * RS - 512) % 8 == 0, "keep rows 8-B aligned");
+#else
+  __shared__ uint64_t s_rows_sep[4][64];
+#endif
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if ORBX_FC_ROWS_ALIAS
+  uint64_t* const krows = (uint64_t*)(s_src[wid] + (MAXR + 12) * RS - 512);
+#else
+  uint64_t* const krows = s_rows_sep[wid];
+#endif
   int bx, img;
   xcd_block(bx, img);
   const int l0 = (bx * 4 + wid) * cpw;
@@ -1163,7 +1182,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
           V[(r1 + 1) * RS + c1 + 1] = (uint8_t)min(255, max(0, sc1 + 1));
         }
       }
-      s_rows[wid][lane] = 0;
+      krows[lane] = 0;
       wave_sync();
       // (3) NMS at t; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
       const int t1 = max(t, 1);
@@ -1174,10 +1193,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         if (v <= t1) continue;
         const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
                              max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
-        if (v > (nmax > t ? nmax : t1)) atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
+        if (v > (nmax > t ? nmax : t1)) atomicOr((unsigned long long*)&krows[r], 1ull << c);
       }
       wave_sync();
-      bits = lane < dr ? s_rows[wid][lane] : 0;
+      bits = lane < dr ? krows[lane] : 0;
       if (__ballot(bits != 0) != 0 || t == min_th) break;  // cell has keypoints, or retried
       t = min_th;  // no keypoint at iniThFAST: FAST again at minThFAST (ORBextractor.cc:782-784)
     }
@@ -1997,7 +2016,7 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
     int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
     if (P->fc_cpw > 0) cpw = P->fc_cpw;
     if (P->n_cells_small > 0)
-      hipLaunchKernelGGL((k_fast_cells<44, 44, K>),
+      hipLaunchKernelGGL((k_fast_cells<44, ORBX_FC_MAXR, K>),
                          dim3((P->n_cells_small + 4 * cpw - 1) / (4 * cpw), n), dim3(256), 0,
                          P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
                          P->n_cells_small, ncells, g.ini_th, g.min_th, cand, g.cand_total,
@@ -2150,8 +2169,13 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   // a few-image plan runs every cell in the <72, kCellMax> instance: one launch instead of two
   // on the drop-in path's one-frame chain (either instance handles any cell)
   const bool one_fast_launch = max_batch <= kPyFewImages;
-  for (int c = 0; c < (int)g.cells.size(); c++)
-    (g.cells[c].fb_big || one_fast_launch ? cells_big : cells_small).push_back(c);
+  // the <44, ORBX_FC_MAXR> instance takes ROIs up to 41 + its alignment slack wide and
+  // ORBX_FC_MAXR rows high
+  for (int c = 0; c < (int)g.cells.size(); c++) {
+    const CellGeom& C = g.cells[c];
+    const bool small = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= ORBX_FC_MAXR;
+    (small && !one_fast_launch ? cells_small : cells_big).push_back(c);
+  }
   P->n_cells_small = (int)cells_small.size();
   P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;
