@@ -1589,14 +1589,16 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
 }
 
 
+// 256-thread instances: at least 6 waves per SIMD (the compiler's choice was 104 VGPRs, 4 waves;
+// 6 costs a few spilled registers and took C2's octree 0.154 -> 0.124 ms per 512 frames; 7 / 8
+// spill more and were slower); the 1024-thread instance keeps its registers (a cap slowed C5's
+// level-0 trees).  ORBX_OCT_WAVES overrides the floor for experiments.
 #ifndef ORBX_OCT_WAVES
-#define ORBX_OCT_WAVES 0  // amdgpu_waves_per_eu floor for k_octree (0: the compiler's choice)
+#define ORBX_OCT_WAVES 6
 #endif
 template <int NT, class K>
 __global__ __launch_bounds__(NT)
-#if ORBX_OCT_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(ORBX_OCT_WAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(NT <= 256 ? ORBX_OCT_WAVES : 1)))
 void k_octree(
     const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
     const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
