@@ -1733,11 +1733,10 @@ __global__ __launch_bounds__(256) void k_describe(
     const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const K* __restrict__ okey,
     const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
-  // dwords per staged row (odd strides, so the samples of different rows spread over the LDS
-  // banks): raw 31 + 3 bytes; blurred 16-B pieces from a 16-B aligned start, stored two dwords
-  // to the left when the patch starts 8 or more bytes into the first piece (offset <= 7 plus 37
-  // bytes: 11 dwords).  21.9 KB per workgroup: 7 workgroups per CU (13 / 10 dwords: 6)
-  constexpr int RW = 9, BW = 11, BC = 4;  // BC: 16-B pieces per blurred row
+  // dwords per staged row: raw 31+3 bytes rounded up; blurred 16-B pieces from a 16-B aligned
+  // start (offset <= 15 plus 37 bytes: 13 dwords) — an odd stride, so the rBRIEF samples of
+  // different rows spread over the LDS banks
+  constexpr int RW = 10, BW = 13, BC = 4;  // BC: 16-B pieces per blurred row
   constexpr int RN = 31 * RW, BN = 37 * BW;
   __shared__ uint32_t s_raw[8][RN];
   __shared__ uint32_t s_blr[8][BN];
@@ -1774,7 +1773,6 @@ __global__ __launch_bounds__(256) void k_describe(
   const uint8_t* Bp = blur + (int64_t)img * pyr_bytes + pyr_off;
   const int fr = (cx - 15) >> 2, lr = (cx + 15) >> 2;  // raw dword columns
   const int ab = (cx - 18) & ~15, lb = ((cx + 18) & ~15) - ab;  // blurred first piece, last offset
-  const int bsh = (cx - 18) - ab >= 8 ? 2 : 0;  // dwords the staged blurred rows are shifted left
   if (active) {
     uint32_t vr[(RN + 31) / 32];
     uint4 vb[(37 * BC + 31) / 32];
@@ -1799,17 +1797,16 @@ __global__ __launch_bounds__(256) void k_describe(
     for (int k = 0; k < (37 * BC + 31) / 32; k++) {
       const int i = hl + 32 * k, r = i >> 2, c = i & 3;
       if (i < 37 * BC) {
-        uint32_t* d = s_blr[hw] + r * BW;
-        const int j0 = 4 * c - bsh;  // staged dword of the piece's first dword
-        if (j0 >= 0 && j0 < BW) d[j0] = vb[k].x;
-        if (j0 + 1 >= 0 && j0 + 1 < BW) d[j0 + 1] = vb[k].y;
-        if (j0 + 2 >= 0 && j0 + 2 < BW) d[j0 + 2] = vb[k].z;
-        if (j0 + 3 < BW) d[j0 + 3] = vb[k].w;
+        uint32_t* d = s_blr[hw] + r * BW + 4 * c;
+        d[0] = vb[k].x;
+        if (4 * c + 1 < BW) d[1] = vb[k].y;
+        if (4 * c + 2 < BW) d[2] = vb[k].z;
+        if (4 * c + 3 < BW) d[3] = vb[k].w;
       }
     }
   }
   constexpr int BS = 4 * BW;
-  const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - ab) - 4 * bsh;
+  const uint8_t* bc = (const uint8_t*)s_blr[hw] + 18 * BS + (cx - ab);
   // IC_Angle (ORBextractor.cc:73-98): lane hl < 31 sums row v = hl - 15 of the circular patch
   // (v_dot4_u32_u8 over the row's bytes masked to |u| <= umax[|v|])
   int m10 = 0, m01 = 0;
