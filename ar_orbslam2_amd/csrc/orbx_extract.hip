@@ -1220,6 +1220,10 @@ constexpr int kOctNTBig = 1024;       // for frames whose level-0 octree frame e
 constexpr int kOctBigArea = 1 << 20;  // kOctBigArea px: a workgroup holds ~100 KB of LDS there
                                       // (one per CU), so 1024 threads run its key passes 4x wide
 constexpr int kOctRegKeys = 16;       // keys per thread per register chunk
+#ifndef ORBX_OCT_BATCH
+#define ORBX_OCT_BATCH 8
+#endif
+constexpr int kOctBatch = ORBX_OCT_BATCH;  // node-info loads in flight per key pass round
 constexpr size_t kOctMaxSmem = 150 * 1024;  // dynamic LDS of one octree workgroup
 
 struct OctNodes {
@@ -1227,17 +1231,25 @@ struct OctNodes {
   int *cnt, *seq;
 };
 
-template <class K>
-__device__ __forceinline__ int quad_of(K key, int x0, int x1, int y0, int y1) {
-  const int x = KeyFmt<K>::x(key), y = KeyFmt<K>::y(key);
+// A node's split point packed for the key passes (one LDS load per key): xm in bits 0-15, ym in
+// 16-30 (levels are < 32768 px), bit 31 set when the node holds more than one key
+__device__ __forceinline__ uint32_t node_info(int cnt, int x0, int x1, int y0, int y1) {
   const int xm = x0 + (x1 - x0 + 1) / 2;  // ceil((float)(UR.x-UL.x)/2)
   const int ym = y0 + (y1 - y0 + 1) / 2;
-  return x < xm ? (y < ym ? 0 : 2) : (y < ym ? 1 : 3);
+  return (cnt > 1 ? 0x80000000u : 0u) | (uint32_t)xm | ((uint32_t)ym << 16);
+}
+
+// quadrant of a key in its node: 0 UL, 1 UR, 2 BL, 3 BR (DivideNode, ORBextractor.cc:487-522)
+template <class K>
+__device__ __forceinline__ int quad_of(K key, uint32_t info) {
+  const int x = KeyFmt<K>::x(key), y = KeyFmt<K>::y(key);
+  return (x >= (int)(info & 0xFFFFu)) | ((y >= (int)((info >> 16) & 0x7FFFu)) << 1);
 }
 
 struct OctCtx {
   OctNodes A, B;
   int *cc, *t1, *t2, *t3, *t4, *s_tmp, *s_misc;
+  uint32_t* ninfo;  // node_info() of the current nodes
   uint64_t *pk, *s_tmp64;
   void* outk;  // K[] of the level's retained keys
   int* oc;
@@ -1267,7 +1279,7 @@ struct RegKeys {
   __device__ int get_lab(int r) const { return lab[r]; }
   __device__ void set_lab(int r, int v) { lab[r] = v; }
   __device__ void set_q(int r, int q) { q2 = (q2 & ~(3u << (2 * r))) | ((uint32_t)q << (2 * r)); }
-  __device__ int get_q(int r, const OctNodes&, int) const { return (q2 >> (2 * r)) & 3; }
+  __device__ int get_q(int r, uint32_t) const { return (q2 >> (2 * r)) & 3; }
 };
 
 template <int NT, class K>
@@ -1299,9 +1311,7 @@ struct MemKeys {
   __device__ int get_lab(int r) const { return lab[r]; }
   __device__ void set_lab(int r, int v) { lab[r] = v; }
   __device__ void set_q(int, int) {}
-  __device__ int get_q(int r, const OctNodes& cur, int nd) const {
-    return quad_of(key[r], cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
-  }
+  __device__ int get_q(int r, uint32_t info) const { return quad_of(key[r], info); }
 };
 
 // every key of this thread: f(r, k) for key k < n in register slot r; `want_labs` loads a
@@ -1318,6 +1328,15 @@ __device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, 
     }
     if (labs_out) ks.store_labs(c);
   }
+}
+
+// What a key of node i becomes after a pass: its new label is base - pre[q], pre[q] = the node's
+// non-empty quadrants before the key's quadrant q (children are pushed in quadrant order); bits
+// 2q..2q+1 hold pre[q] (pre[0] = 0), zero for a node that is not divided, and bits 8- the base
+__device__ __forceinline__ int relabel_info(int base, int divided, const int* ccn) {
+  if (!divided) return base << 8;
+  const int p1 = ccn[0] > 0, p2 = p1 + (ccn[1] > 0), p3 = p2 + (ccn[2] > 0);
+  return (base << 8) | (p1 << 2) | (p2 << 4) | (p3 << 6);
 }
 
 template <int NT, class KS>
@@ -1370,16 +1389,18 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   for (int iter = 0; iter < 4096; iter++) {
     const int prevSize = size;
     for (int i = tid; i < 4 * size; i += NT) cc[i] = 0;
+    for (int i = tid; i < size; i += NT)
+      X.ninfo[i] = node_info(cur.cnt[i], cur.x0[i], cur.x1[i], cur.y0[i], cur.y1[i]);
     __syncthreads();
     // quadrant counts; keys are in cell order, so a wave's keys usually share one node and the
     // four counts are added with one atomic each instead of one per key
     const int lane = tid & 63;
-    auto count_one = [&](int j, int k) {
+    auto count_one = [&](int j, int k, uint32_t info) {
       int nd = -1, q = -1;
       if (k < n) {
         nd = ks.get_lab(j);
-        if (cur.cnt[nd] > 1) {
-          q = quad_of(ks.get_key(j), cur.x0[nd], cur.x1[nd], cur.y0[nd], cur.y1[nd]);
+        if (info >> 31) {
+          q = quad_of(ks.get_key(j), info);
           ks.set_q(j, q);
         }
       }
@@ -1397,11 +1418,20 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         atomicAdd(&cc[4 * nd + q], 1);
       }
     };
-    // every lane runs every slot (the ballots need the whole wave)
+    // every lane runs every slot (the ballots need the whole wave); a chunk's node infos are
+    // loaded together before its first atomic, one LDS latency per chunk instead of per key
     for (int c = 0; c < ks.nchunks(); c++) {
       ks.load(c, true);
 #pragma unroll
-      for (int j = 0; j < kOctRegKeys; j++) count_one(j, tid + NT * (c * kOctRegKeys + j));
+      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
+        uint32_t inf[kOctBatch];
+#pragma unroll
+        for (int j = 0; j < kOctBatch; j++)
+          inf[j] = tid + NT * (c * kOctRegKeys + j0 + j) < n ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
+#pragma unroll
+        for (int j = 0; j < kOctBatch; j++)
+          count_one(j0 + j, tid + NT * (c * kOctRegKeys + j0 + j), inf[j]);
+      }
     }
     __syncthreads();
     int T, newSize, nToExpand;
@@ -1432,7 +1462,9 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         const uint64_t e = pk[i];
         const int pre = (int)(e & 0xFFFFF), ndr = (int)((e >> 20) & 0xFFFFF);
         t1[i] = pre;
-        t4[i] = t2[i] ? T - 1 - pre : T + ndr;
+        const int base = t2[i] ? T - 1 - pre : T + ndr;
+        t4[i] = base;
+        t3[i] = relabel_info(base, t2[i], cc + 4 * i);
       }
       __syncthreads();
     } else {
@@ -1515,10 +1547,14 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       __syncthreads();
       const int nd_total = block_scan_excl<NT>(t3, size, s_tmp);
       (void)nd_total;
-      for (int i = tid; i < size; i += NT) t4[i] = t2[i] ? T - 1 - t1[i] : T + t3[i];
+      for (int i = tid; i < size; i += NT) {
+        const int base = t2[i] ? T - 1 - t1[i] : T + t3[i];
+        t4[i] = base;
+        t3[i] = relabel_info(base, t2[i], cc + 4 * i);
+      }
       __syncthreads();
     }
-    // write next node arrays: t2 = divided, t1 = childPre, t4 = base
+    // write next node arrays: t2 = divided, t1 = childPre, t4 = base, t3 = relabel_info
     for (int i = tid; i < size; i += NT) {
       if (t2[i]) {
         const int x0 = cur.x0[i], x1 = cur.x1[i], y0 = cur.y0[i], y1 = cur.y1[i];
@@ -1545,18 +1581,27 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
       }
     }
-    // relabel keys
-    each_key<NT>(ks, true, true, [&](int j, int) {
-      const int nd = ks.get_lab(j);
-      if (t2[nd]) {
-        const int q = ks.get_q(j, cur, nd);
-        int c = 0;
-        for (int qq = 0; qq < q; qq++) c += cc[4 * nd + qq] > 0;
-        ks.set_lab(j, t4[nd] - c);
-      } else {
-        ks.set_lab(j, t4[nd]);
+    // relabel keys: a chunk's relabel infos (and, for keys in memory, node infos) in one round
+    // of loads
+    for (int c = 0; c < ks.nchunks(); c++) {
+      ks.load(c, true);
+#pragma unroll
+      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
+        uint32_t rl[kOctBatch], inf[kOctBatch];
+#pragma unroll
+        for (int j = 0; j < kOctBatch; j++) {
+          const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
+          rl[j] = v ? (uint32_t)t3[ks.get_lab(j0 + j)] : 0u;
+          inf[j] = (!KS::kRegs && v) ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kOctBatch; j++)
+          if (tid + NT * (c * kOctRegKeys + j0 + j) < n)
+            ks.set_lab(j0 + j, (int)(rl[j] >> 8) -
+                                   (int)((rl[j] >> (2 * ks.get_q(j0 + j, inf[j]))) & 3u));
       }
-    });
+      ks.store_labs(c);
+    }
     __syncthreads();
     {
       OctNodes tmp = cur;
@@ -1637,6 +1682,7 @@ void k_octree(
   int* t2 = (int*)take(4 * NC);
   int* t3 = (int*)take(4 * NC);
   int* t4 = (int*)take(4 * NC);
+  uint32_t* ninfo = (uint32_t*)take(4 * NC);
   // per-cell key starts and slots: in LDS, or (cell_cap == 0: levels with too many cells for
   // it) in this (image, level)'s part of cell_scr, [2 (ncells + nlevels)] ints per image
   int* cpre = cell_cap > 0 ? (int*)take(4 * (cell_cap + 1))
@@ -1686,7 +1732,7 @@ void k_octree(
       v[j] = k < n ? cb[s_slot[c] + k - cpre[c]] : K(0);
     }
   };
-  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, pk, s_tmp64, outk, oc};
+  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, ninfo, pk, s_tmp64, outk, oc};
   if (n <= kOctRegKeys * NT) {  // keys + labels in registers: every pass stays on-chip
     RegKeys<NT, K> ks;
     ks.n = n;
@@ -2223,7 +2269,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   auto oct_bytes = [&](size_t NC, size_t CC) {
-    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 4 * r16(4 * NC) +
+    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 5 * r16(4 * NC) +
            (CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0) + r16(8 * NC);
   };
   while (P->oct_split < g.nlevels && (int64_t)g.lv[P->oct_split].W * g.lv[P->oct_split].H > kOctBigArea)
