@@ -1261,7 +1261,7 @@ int orbx_bf_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_
   if (rc) return rc;
   char* base = tls_ws.d;
   hipStream_t s = tls_ws.stream;
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), ob, hipMemcpyHostToDevice, s));
+  ORBX_HIP(host_copy(base, st.host.data(), ob, st.host.pinned, hipMemcpyHostToDevice, s));
   rc = launch_bf(dptr<uint8_t>(base, oq), nq, dptr<uint8_t>(base, ot), 0, dptr<int>(base, oc), 1,
                  dptr<int2>(base, ob), nullptr, nullptr, s);
   if (rc) return rc;
@@ -1312,7 +1312,7 @@ int orbx_nn_match(const uint8_t* query, int32_t nq, const uint8_t* train, int32_
     if (rc) return rc;
     char* base = tls_ws.d;
     hipStream_t s = tls_ws.stream;
-    ORBX_HIP(hipMemcpyAsync(base, st.host.data(), ob, hipMemcpyHostToDevice, s));
+    ORBX_HIP(host_copy(base, st.host.data(), ob, st.host.pinned, hipMemcpyHostToDevice, s));
     rc = launch_bf(dptr<uint8_t>(base, oq), nq, dptr<uint8_t>(base, ot), 0, dptr<int>(base, oc),
                    1, dptr<int2>(base, ob), dptr<int>(base, os), dptr<int>(base, oe), s);
     if (rc) return rc;

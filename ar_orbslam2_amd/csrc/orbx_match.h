@@ -108,6 +108,14 @@ int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_coun
 // d_ids is [nimg][nb], d_off is [nimg][nb + 1], d_feats is [nimg][feats_stride].
 
 // ------------------------------------------------------------------ host-pointer ABI helpers
+// bytes between device memory and pinned host memory by a kernel on stream s (orbx_match.hip)
+hipError_t queue_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
+// the same when the host side is pinned, else an asynchronous hipMemcpy
+inline hipError_t host_copy(void* dst, const void* src, size_t bytes, bool pinned,
+                            hipMemcpyKind kind, hipStream_t s) {
+  return pinned ? queue_copy(dst, src, bytes, s) : hipMemcpyAsync(dst, src, bytes, kind, s);
+}
+
 // Growable pinned host buffer (pageable fallback if pinning fails); new bytes read as zero.
 struct PinnedBuf {
   char* p = nullptr;
@@ -192,13 +200,14 @@ struct Workspace {
     cap = want;
     return ORBX_OK;
   }
-  // uploads the packed host arrays (a Stager's pinned buffer: one DMA, no host copy)
+  // uploads the packed host arrays (a Stager's pinned buffer: one copy kernel reading it, no
+  // host copy; a DMA when pinning failed)
   hipError_t upload(const PinnedBuf& host, size_t bytes) {
-    return hipMemcpyAsync(d, host.data(), bytes, hipMemcpyHostToDevice, stream);
+    return host_copy(d, host.data(), bytes, host.pinned, hipMemcpyHostToDevice, stream);
   }
   // device range [off, off + bytes) into the same range of the pinned mirror
   hipError_t download(size_t off, size_t bytes) {
-    return hipMemcpyAsync(h + off, d + off, bytes, hipMemcpyDeviceToHost, stream);
+    return queue_copy(h + off, d + off, bytes, stream);
   }
 };
 extern thread_local Workspace tls_ws;

@@ -611,6 +611,30 @@ int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_coun
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_csr");
 }
 
+// Copies on the compute queue (one of the ends pinned host memory, read or written over PCIe by
+// the kernel itself): an asynchronous copy outside a graph goes to a DMA engine, and a
+// DMA -> kernel -> DMA chain waits ~10 us at each engine switch, which for the per-frame calls'
+// few-KB payloads is longer than the copies
+__global__ __launch_bounds__(256) void k_copy(uint8_t* __restrict__ dst,
+                                              const uint8_t* __restrict__ src, size_t n) {
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x, stride = (size_t)gridDim.x * 256;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+    const size_t n16 = n >> 4;
+    for (size_t i = t; i < n16; i += stride) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (size_t i = (n16 << 4) + t; i < n; i += stride) dst[i] = src[i];
+  } else {
+    for (size_t i = t; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+hipError_t queue_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((bytes + 4095) / 4096, 256);
+  hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, s, (uint8_t*)dst,
+                     (const uint8_t*)src, bytes);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ host-pointer ABI
 thread_local Workspace tls_ws;
 thread_local PinnedBuf tls_stage;
@@ -833,7 +857,7 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int3
   if (rc) return rc;
   char* base = tls_ws.d;
   hipStream_t s = tls_ws.stream;
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), oo, hipMemcpyHostToDevice, s));
+  ORBX_HIP(host_copy(base, st.host.data(), oo, st.host.pinned, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_distance, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)(base + oa), (const uint8_t*)(base + ob), n,
                      dptr<int>(base, oo));
   ORBX_HIP(hipGetLastError());
@@ -881,7 +905,7 @@ int orbx_debug_match_finish(int32_t kind, int32_t n1, int32_t n2, const int32_t*
     P.error = dptr<int>(base, ocount + 4);
     memcpy(st.host.data() + oprob, &P, sizeof(P));
   }
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), st.host.size(), hipMemcpyHostToDevice, s));
+  ORBX_HIP(host_copy(base, st.host.data(), st.host.size(), st.host.pinned, hipMemcpyHostToDevice, s));
   if (kind < 2)
     hipLaunchKernelGGL(k_bow_finish, dim3(1), dim3(256), 0, s, dptr<const BowProblem>(base, oprob));
   else

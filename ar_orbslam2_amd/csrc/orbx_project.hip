@@ -734,7 +734,7 @@ int run_projection(const orbx_proj_frame* f, ProjPointsDev P, const std::vector<
     if (rc) return rc;
     char* base = tls_ws.d;
     hipStream_t s = tls_ws.stream;
-    ORBX_HIP(hipMemcpyAsync(base, st.host.data(), upload, hipMemcpyHostToDevice, s));
+    ORBX_HIP(host_copy(base, st.host.data(), upload, st.host.pinned, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemsetAsync(base + oused, 0, 16, s));
     ProjFrameDev F{};
     rc = launch_grid(f, base, go, !ic, s, &F);
@@ -811,7 +811,7 @@ int run_fuse(const orbx_proj_frame* kf, const float* inv_sigma2, const orbx_fuse
   if (rc) return rc;
   char* base = tls_ws.d;
   hipStream_t s = tls_ws.stream;
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), upload, hipMemcpyHostToDevice, s));
+  ORBX_HIP(host_copy(base, st.host.data(), upload, st.host.pinned, hipMemcpyHostToDevice, s));
   ProjFrameDev F{};
   rc = launch_grid(kf, base, go, reproj != 0, s, &F);
   if (rc) return rc;
@@ -873,7 +873,7 @@ int run_sim3(const orbx_proj_frame* kf1, const orbx_proj_frame* kf2, const orbx_
   if (rc) return rc;
   char* base = tls_ws.d;
   hipStream_t s = tls_ws.stream;
-  ORBX_HIP(hipMemcpyAsync(base, st.host.data(), upload, hipMemcpyHostToDevice, s));
+  ORBX_HIP(host_copy(base, st.host.data(), upload, st.host.pinned, hipMemcpyHostToDevice, s));
   ORBX_HIP(hipMemsetAsync(base + ofound, 0, 4, s));
   ProjFrameDev F1{}, F2{};
   rc = launch_grid(kf1, base, g1, false, s, &F1);
