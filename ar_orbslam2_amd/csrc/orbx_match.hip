@@ -106,6 +106,13 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
     }
   }
   uint64_t matched = 0;  // bit c: candidate lane + 64c already matched in this call
+  // Without `big`, the matches of register candidates are stored after the loops (a global
+  // store inside the serial per-feature loop made the next feature wait for its completion):
+  // mode 0 keeps the KF feature matched to candidate lane + 64 c in mval[c] of the candidate's
+  // lane, mode 1 the candidate index matched to a prefetched KF feature in res_l of its lane
+  int mval[kBowDescChunks];
+#pragma unroll
+  for (int c = 0; c < kBowDescChunks; c++) mval[c] = -1;
   const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
   for (int c0 = a0; c0 < a1; c0 += 64) {
     // prefetch up to 64 KF features of the node (index, validity, descriptor) so the serial
@@ -122,6 +129,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
         dl0 = q[0]; dl1 = q[1]; dl2 = q[2]; dl3 = q[3];
       }
     }
+    int res_l = -1;
     uint64_t okm = __ballot(ok_l);
     while (okm) {
       const int j = __builtin_ctzll(okm);
@@ -182,23 +190,43 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
       }
       const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
       if (pass && static_cast<float>(b1) < P.nnratio * static_cast<float>(b2)) {
-        if ((bp & 63) == lane) matched |= 1ull << (bp >> 6);
-        if (lane == 0) {
-          const int i2 = P.s2.node_feats[f0 + bp];
-          if (kfkf) {
-            P.match[i1] = i2;
-            if (big) __hip_atomic_store(P.matched2 + i2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } else if (big) {
-            __hip_atomic_store(P.match + i2, i1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } else {
-            P.match[i2] = i1;
+        const int cb = bp >> 6, lb = bp & 63;  // wave-uniform
+        if (lb == lane) matched |= 1ull << cb;
+        if (big) {
+          if (lane == 0) {
+            const int i2 = P.s2.node_feats[f0 + bp];
+            if (kfkf) {
+              P.match[i1] = i2;
+              __hip_atomic_store(P.matched2 + i2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+              __hip_atomic_store(P.match + i2, i1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
+          // the flag store completes before the next feature's scan reads it
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        } else if (cb < kBowDescChunks) {
+          if (kfkf) {
+            int i2c = i2r[0];
+#pragma unroll
+            for (int c = 1; c < kBowDescChunks; c++) i2c = cb == c ? i2r[c] : i2c;
+            const int i2 = __builtin_amdgcn_readlane(i2c, lb);
+            if (lane == j) res_l = i2;
+          } else if (lane == lb) {
+#pragma unroll
+            for (int c = 0; c < kBowDescChunks; c++) mval[c] = cb == c ? i1 : mval[c];
+          }
+        } else if (lane == lb) {  // a candidate past the register chunks: stored now
+          const int i2 = P.s2.node_feats[f0 + bp];
+          if (kfkf) P.match[i1] = i2;
+          else P.match[i2] = i1;
         }
-        // the flag store completes before the next feature's scan reads it
-        if (big) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
       }
     }
+    if (res_l >= 0) P.match[i1_l] = res_l;
   }
+#pragma unroll
+  for (int c = 0; c < kBowDescChunks; c++)
+    if (mval[c] >= 0) P.match[i2r[c]] = mval[c];
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:1604-1645)
