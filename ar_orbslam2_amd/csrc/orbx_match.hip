@@ -272,7 +272,8 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
   const int n_other = kfkf ? side_n(P.s2) : side_n(P.s1);  // range of a match value
   const bool ori = P.check_ori;
   // entries i0 + tid + 256 r (r < kFinishRegs): the matches, then the angle pairs, each with
-  // every load of the round in flight
+  // every load of the round in flight (the stores of dropped entries come after the loads:
+  // between them they kept the compiler from batching the angle loads)
   int m[kFinishRegs], bin[kFinishRegs];
   auto gather = [&](int i0) {
 #pragma unroll
@@ -280,18 +281,27 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
       const int i = i0 + tid + 256 * r;
       m[r] = i < n ? P.match[i] : -1;
     }
+    uint32_t bad = 0;
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) {
+      if (m[r] >= n_other) {  // stale or corrupt index: report, drop, never dereference
+        bad |= 1u << r;
+        m[r] = -1;
+      }
+    }
 #pragma unroll
     for (int r = 0; r < kFinishRegs; r++) {
       const int i = i0 + tid + 256 * r;
-      if (m[r] >= n_other) {  // stale or corrupt index: report, drop, never dereference
-        atomicOr(P.error, ORBX_DEVERR_INDEX);
-        P.match[i] = -1;
-        m[r] = -1;
-      }
       bin[r] = -1;
       if (ori && m[r] >= 0)
         bin[r] = kfkf ? rot_bin(side_angle(P.s1, i), side_angle(P.s2, m[r]))
                       : rot_bin(side_angle(P.s1, m[r]), side_angle(P.s2, i));
+    }
+    if (bad) {
+      atomicOr(P.error, ORBX_DEVERR_INDEX);
+#pragma unroll
+      for (int r = 0; r < kFinishRegs; r++)
+        if ((bad >> r) & 1) P.match[i0 + tid + 256 * r] = -1;
     }
   };
   auto filter = [&](int i0) {  // after ComputeThreeMaxima: drop the other bins, count the rest
@@ -463,10 +473,26 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
   const int n = tri_n(P.s1), n2 = tri_n(P.s2);
   if (tid < kHISTO) hist[tid] = 0;
   __syncthreads();
+  // rounds of kFinishRegs entries per thread, every load of a round in flight before its
+  // atomics and stores
   if (P.check_ori) {
-    for (int i = tid; i < n; i += 256) {
-      const int m = P.m12[i];
-      if (m >= 0 && m < n2) atomicAdd(&hist[rot_bin(P.s1.keys_un[i].angle, P.s2.keys_un[m].angle)], 1);
+    for (int i0 = tid; i0 < n; i0 += 256 * kFinishRegs) {
+      int m[kFinishRegs];
+      float a1[kFinishRegs], a2[kFinishRegs];
+#pragma unroll
+      for (int r = 0; r < kFinishRegs; r++) {
+        const int i = i0 + 256 * r;
+        m[r] = i < n ? P.m12[i] : -1;
+      }
+#pragma unroll
+      for (int r = 0; r < kFinishRegs; r++) {
+        const bool ok = m[r] >= 0 && m[r] < n2;
+        a1[r] = ok ? P.s1.keys_un[i0 + 256 * r].angle : 0.f;
+        a2[r] = ok ? P.s2.keys_un[m[r]].angle : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < kFinishRegs; r++)
+        if (m[r] >= 0 && m[r] < n2) atomicAdd(&hist[rot_bin(a1[r], a2[r])], 1);
     }
     __syncthreads();
     if (tid == 0) three_maxima(hist, s_ind[0], s_ind[1], s_ind[2]);
@@ -476,21 +502,33 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
   const int per = (n + 255) / 256;
   const int beg = min(tid * per, n), end = min(beg + per, n);
   int mine = 0;
-  for (int i = beg; i < end; i++) {
-    int m = P.m12[i];
-    if (m >= n2) {  // stale or corrupt index: report, drop, never dereference
-      if (P.error) atomicOr(P.error, ORBX_DEVERR_INDEX);
-      P.m12[i] = -1;
-      m = -1;
-    }
-    if (m >= 0 && P.check_ori) {
-      const int bin = rot_bin(P.s1.keys_un[i].angle, P.s2.keys_un[m].angle);
-      if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
-        P.m12[i] = -1;
-        m = -1;
+  for (int b0 = beg; b0 < end; b0 += kFinishRegs) {
+    int m[kFinishRegs], bin[kFinishRegs];
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) m[r] = b0 + r < end ? P.m12[b0 + r] : -1;
+    uint32_t bad = 0;
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++)
+      if (m[r] >= n2) {  // stale or corrupt index: report, drop, never dereference
+        bad |= 1u << r;
+        m[r] = -1;
       }
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++)
+      bin[r] = (m[r] >= 0 && P.check_ori)
+                   ? rot_bin(P.s1.keys_un[b0 + r].angle, P.s2.keys_un[m[r]].angle)
+                   : -1;
+    if (bad && P.error) atomicOr(P.error, ORBX_DEVERR_INDEX);
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) {
+      if (m[r] >= 0 && P.check_ori && bin[r] != s_ind[0] && bin[r] != s_ind[1] &&
+          bin[r] != s_ind[2]) {
+        bad |= 1u << r;
+        m[r] = -1;
+      }
+      if ((bad >> r) & 1) P.m12[b0 + r] = -1;
+      mine += m[r] >= 0;
     }
-    mine += m >= 0;
   }
   // exclusive scan of the per-thread counts (DPP wave scans + the 4 wave totals)
   const int lane = tid & 63, wid = tid >> 6;
@@ -503,12 +541,17 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
     pos += w < wid ? s_scan[w] : 0;
     total += s_scan[w];
   }
-  for (int i = beg; i < end; i++) {
-    const int m = P.m12[i];
-    if (m >= 0) {
-      P.pairs[2 * pos] = i;
-      P.pairs[2 * pos + 1] = m;
-      pos++;
+  for (int b0 = beg; b0 < end; b0 += kFinishRegs) {
+    int m[kFinishRegs];
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) m[r] = b0 + r < end ? P.m12[b0 + r] : -1;
+#pragma unroll
+    for (int r = 0; r < kFinishRegs; r++) {
+      if (m[r] >= 0) {
+        P.pairs[2 * pos] = b0 + r;
+        P.pairs[2 * pos + 1] = m[r];
+        pos++;
+      }
     }
   }
   if (tid == 0) *P.count = total;
