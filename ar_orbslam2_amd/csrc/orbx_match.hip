@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -464,6 +465,110 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
   }
 }
 
+// Latency form of k_tri_nodes for calls with few problems (the per-keyframe-pair drop-in call),
+// where one wave per node leaves the GPU idle behind the largest node: one workgroup per KF1
+// node, the KF2 node staged 256 features at a time for the whole workgroup and G = 256 / n1
+// lanes per KF1 feature, so a node's scan is spread over four times as many lanes.  Same keys,
+// same LDS minimum, same result.
+__global__ __launch_bounds__(256) void k_tri_nodes_wg(const TriProblem* __restrict__ probs) {
+  const TriProblem& P = probs[blockIdx.y];
+  const int a = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (a >= tri_nodes(P.s1)) return;
+  __shared__ uint64_t s_d[256][4];
+  __shared__ float s_x[256], s_y[256];
+  __shared__ int s_i2[256], s_oct[256];
+  __shared__ unsigned long long s_key[64];
+  __shared__ int s_b;
+  const uint32_t id = P.s1.fv.node_ids[a];
+  if (tid < 64) {
+    const int nn2 = tri_nodes(P.s2);
+    const int b = wave_lower_bound(P.s2.fv.node_ids, nn2, id, lane);
+    if (lane == 0) s_b = b < nn2 && P.s2.fv.node_ids[b] == id ? b : -1;
+  }
+  __syncthreads();
+  const int b = s_b;
+  if (b < 0) return;  // workgroup-uniform
+  const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
+  const int a1 = P.s1.fv.node_offsets[a + 1];
+  for (int pa0 = P.s1.fv.node_offsets[a]; pa0 < a1; pa0 += 64) {
+    const int n1 = min(64, a1 - pa0);
+    const int G = 256 / n1;                    // lanes per KF1 feature
+    const int u = tid % n1, g = tid / n1;
+    bool live = g < G;
+    const int i1 = P.s1.fv.node_feats[pa0 + u];
+    bool st1 = false;
+    if (live) {
+      if (P.s1.has_mp && P.s1.has_mp[i1]) live = false;
+      st1 = P.s1.u_right ? P.s1.u_right[i1] >= 0 : false;
+      if (P.only_stereo && !st1) live = false;
+    }
+    orbx_keypoint kp1{};
+    uint64_t d1[4] = {0, 0, 0, 0};
+    if (live) {
+      kp1 = P.s1.keys_un[i1];
+      const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
+      d1[0] = q[0]; d1[1] = q[1]; d1[2] = q[2]; d1[3] = q[3];
+    }
+    if (tid < 64) s_key[tid] = ~0ull;
+    unsigned long long best = ~0ull;
+    for (int pb0 = f0; pb0 < f1; pb0 += 256) {
+      const int nb = min(256, f1 - pb0);
+      __syncthreads();  // the previous chunk's reads (and the key reset) are done
+      {
+        int i2 = -1;
+        if (tid < nb) {
+          i2 = P.s2.fv.node_feats[pb0 + tid];
+          const bool st2 = P.s2.u_right ? P.s2.u_right[i2] >= 0 : false;
+          if ((P.s2.has_mp && P.s2.has_mp[i2]) || (P.only_stereo && !st2)) {  // (:728)
+            i2 = -1;
+          } else {
+            const uint64_t* q = (const uint64_t*)(P.s2.desc + (int64_t)i2 * 32);
+            s_d[tid][0] = q[0];
+            s_d[tid][1] = q[1];
+            s_d[tid][2] = q[2];
+            s_d[tid][3] = q[3];
+            const orbx_keypoint kp2 = P.s2.keys_un[i2];
+            s_x[tid] = kp2.x;
+            s_y[tid] = kp2.y;
+            s_oct[tid] = kp2.octave | (st2 ? 0x10000 : 0);
+          }
+        }
+        s_i2[tid] = i2;
+      }
+      __syncthreads();
+      if (live) {
+        for (int j = g; j < nb; j += G) {
+          if (s_i2[j] < 0) continue;
+          const uint64_t* dd = s_d[j];
+          const int dist = __popcll(d1[0] ^ dd[0]) + __popcll(d1[1] ^ dd[1]) +
+                           __popcll(d1[2] ^ dd[2]) + __popcll(d1[3] ^ dd[3]);
+          if (dist > kTH_LOW) continue;
+          const unsigned long long key =
+              ((unsigned long long)dist << 32) | (uint32_t)~(pb0 - f0 + j);
+          if (key > best) continue;
+          const int oc2 = s_oct[j];
+          const bool st2 = oc2 >> 16;
+          const int oct2 = oc2 & 0xFFFF;
+          const float x2 = s_x[j], y2 = s_y[j];
+          if (!st1 && !st2) {
+            const float dex = P.ex - x2, dey = P.ey - y2;
+            if (__builtin_fmaf(dex, dex, dey * dey) < 100 * P.s2.scale_factors[oct2]) continue;
+          }
+          if (epipolar_ok(kp1.x, kp1.y, x2, y2, P.F, P.s2.level_sigma2[oct2])) best = key;
+        }
+      }
+    }
+    if (live && best != ~0ull) atomicMin(&s_key[u], best);
+    __syncthreads();
+    if (tid < n1 && live) {  // g == 0: the feature's own liveness
+      const unsigned long long key = s_key[tid];
+      P.m12[i1] = key == ~0ull ? -1 : P.s2.fv.node_feats[f0 + (int)~(uint32_t)key];
+    }
+    __syncthreads();  // s_key is reset for the next KF1 chunk
+  }
+}
+
 __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict__ probs) {
   const TriProblem& P = probs[blockIdx.x];
   __shared__ int hist[kHISTO];
@@ -656,9 +761,19 @@ int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_bow");
 }
 
+// calls with at most kTriWgProbs keyframe pairs use the workgroup-per-node form
+// (ORBX_TRI_WG_PROBS overrides the limit for experiments)
+constexpr int kTriWgProbs = 4;
+
 int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s) {
   if (nprob <= 0) return ORBX_OK;
-  if (max_nodes1 > 0)
+  static const int wg_probs = [] {
+    const char* e = getenv("ORBX_TRI_WG_PROBS");
+    return e ? atoi(e) : kTriWgProbs;
+  }();
+  if (max_nodes1 > 0 && nprob <= wg_probs)
+    hipLaunchKernelGGL(k_tri_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
+  else if (max_nodes1 > 0)
     hipLaunchKernelGGL(k_tri_nodes, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
   hipLaunchKernelGGL(k_tri_finish, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();
