@@ -205,12 +205,21 @@ int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
                             F->d_node_of, F->d_wt_of, kp, n, s);
   if (rc) return rc;
   pr.mark(s, st_fv);
-  rc = launch_bowvec(F->scoring, F->weighting, F->d_word_of, F->d_wt_of, kp, fcounts(F), 0, kp,
-                     F->d_bow_words, F->d_bow_vals, kp, F->d_bow_n, n, s);
-  if (rc) return rc;
-  pr.mark(s, st_bv);
-  rc = launch_csr(F->d_rank_of, kp, fcounts(F), 0, 0, F->nb, F->ranks->d_rank_ids, F->d_ids,
-                  F->d_off, F->d_feats, kp, F->d_nn, n, s);
+  // BowVector + FeatureVector in one launch (k_bowfv, stage "k_bowvec"), else the two kernels
+  rc = launch_bowfv(F->scoring, F->weighting, F->vv.n_words, F->d_word_of, F->d_rank_of,
+                    F->d_wt_of, kp, fcounts(F), 0, kp, F->d_bow_words, F->d_bow_vals, kp,
+                    F->d_bow_n, F->nb, F->ranks->d_rank_ids, F->d_ids, F->d_off, F->d_feats, kp,
+                    F->d_nn, n, s);
+  if (rc == ORBX_EUNSUPPORTED) {
+    rc = launch_bowvec(F->scoring, F->weighting, F->d_word_of, F->d_wt_of, kp, fcounts(F), 0, kp,
+                       F->d_bow_words, F->d_bow_vals, kp, F->d_bow_n, n, s);
+    if (rc) return rc;
+    pr.mark(s, st_bv);
+    rc = launch_csr(F->d_rank_of, kp, fcounts(F), 0, 0, F->nb, F->ranks->d_rank_ids, F->d_ids,
+                    F->d_off, F->d_feats, kp, F->d_nn, n, s);
+  } else if (rc == ORBX_OK) {
+    pr.mark(s, st_bv);
+  }
   if (rc) return rc;
   pr.mark(s, st_csr);
   launch_fill_u32((uint32_t*)F->d_match, (size_t)n * kp, 0xFFFFFFFFu, s);

@@ -43,5 +43,15 @@ int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
                   const double* d_weight_of, int64_t in_stride, const int* d_counts, int n_fixed,
                   int max_n, uint32_t* d_words, double* d_values, int64_t out_stride,
                   int* d_nwords, int nimg, hipStream_t s);
+// BowVector (as launch_bowvec) and FeatureVector CSR (as launch_csr with id_lo 0 over
+// d_rank_ids) of every image in one launch (k_bowfv).  ORBX_EUNSUPPORTED when it does not apply
+// (more than 4096 features, ids too wide, no rank table, ORBX_BOWFV=0): the caller then runs
+// launch_bowvec + launch_csr.
+int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word_of,
+                 const uint32_t* d_rank_of, const double* d_weight_of, int64_t in_stride,
+                 const int* d_counts, int n_fixed, int max_n, uint32_t* d_words, double* d_values,
+                 int64_t out_stride, int* d_nwords, int nb, const uint32_t* d_rank_ids,
+                 uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride, int* d_nn,
+                 int nimg, hipStream_t s);
 
 }  // namespace orbx

@@ -10,7 +10,10 @@
 //                    in LDS, per-word weight sums in feature order (BowVector::addWeight /
 //                    addIfNotExist, BowVector.cpp:38-62), then the scoring's L1/L2
 //                    normalisation as one ordered pass (BowVector::normalize, :66-98)
-// The FeatureVector CSR reuses k_csr (orbx_match.hip) over the node ranks built here.
+//   k_bowfv          one workgroup per image of up to 4096 features: the BowVector above and
+//                    the FeatureVector CSR together, from two in-register bitonic sorts merged
+//                    by rank (one launch instead of k_bowvec + k_csr)
+// Otherwise the FeatureVector CSR reuses k_csr (orbx_match.hip) over the node ranks built here.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -372,6 +375,318 @@ int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_bowvec");
 }
 
+// ------------------------------------------------------------------ k_bowfv
+// BowVector and FeatureVector of an image in one workgroup, for images of at most 256 * NPL
+// features whose word ids and FeatureVector ranks fit beside a feature index in 32 bits.  Both
+// orders are stable sorts of (key << IB | feature) words — word for the BowVector
+// (BowVector::addWeight / addIfNotExist in feature order, BowVector.cpp:38-62), FeatureVector
+// rank for the node lists (FeatureVector::addFeature, FeatureVector.cpp:31-45) — so both are
+// sorts of distinct 32-bit keys:
+//  (1) every wave sorts its 64 * NPL keys of each order in registers (bitonic network: NPL keys
+//      per lane, partners inside a lane or across lanes by DPP / swizzle / bpermute);
+//  (2) the four sorted runs merge by rank: a key's place = its place in its run + the keys
+//      below it in the three other runs (branch-free binary searches in LDS);
+//  (3) wave 0 finds the word runs, sums their weights in feature order and runs the scoring's
+//      ordered normalisation (BowVector::normalize, :66-98), while wave 1 writes the
+//      FeatureVector CSR (node ids, offsets, features).
+// It replaces k_bowvec + k_csr (a radix sort with ~15 workgroup barriers, and a wave-serial
+// bucket placement) where it applies: one launch and three barriers per image.
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (M == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad [1,0,3,2]
+  } else if constexpr (M == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad [2,3,0,1]
+  } else if constexpr (M < 32) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));  // xor within 32
+  } else {
+    return (uint32_t)__shfl_xor((int)v, M);
+  }
+}
+
+// Bitonic sort of a wave's 64 * NPL keys of two independent arrays (ascending; element
+// e = lane * NPL + r).  Stage (k, j): e meets e ^ j, ascending where e & k == 0.
+template <int NPL, int K, int J>
+__device__ __forceinline__ void bitonic_stage(uint32_t (&a)[NPL], uint32_t (&b)[NPL], int lane) {
+  if constexpr (J < NPL) {
+#pragma unroll
+    for (int r = 0; r < NPL; r++) {
+      if (r & J) continue;
+      const bool asc = K < NPL ? (r & K) == 0 : ((lane * NPL) & K) == 0;
+      const uint32_t la = min(a[r], a[r | J]), ha = max(a[r], a[r | J]);
+      const uint32_t lb = min(b[r], b[r | J]), hb = max(b[r], b[r | J]);
+      a[r] = asc ? la : ha;
+      a[r | J] = asc ? ha : la;
+      b[r] = asc ? lb : hb;
+      b[r | J] = asc ? hb : lb;
+    }
+  } else {
+    constexpr int LJ = J / NPL;
+    const bool takemin = (((lane * NPL) & K) == 0) == ((lane & LJ) == 0);
+    uint32_t ya[NPL], yb[NPL];
+#pragma unroll
+    for (int r = 0; r < NPL; r++) {
+      ya[r] = lane_xor<LJ>(a[r]);
+      yb[r] = lane_xor<LJ>(b[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < NPL; r++) {
+      a[r] = takemin ? min(a[r], ya[r]) : max(a[r], ya[r]);
+      b[r] = takemin ? min(b[r], yb[r]) : max(b[r], yb[r]);
+    }
+  }
+}
+
+template <int NPL, int K, int J>
+__device__ __forceinline__ void bitonic_js(uint32_t (&a)[NPL], uint32_t (&b)[NPL], int lane) {
+  bitonic_stage<NPL, K, J>(a, b, lane);
+  if constexpr (J > 1) bitonic_js<NPL, K, J / 2>(a, b, lane);
+}
+
+template <int NPL, int K>
+__device__ __forceinline__ void bitonic_ks(uint32_t (&a)[NPL], uint32_t (&b)[NPL], int lane) {
+  bitonic_js<NPL, K, K / 2>(a, b, lane);
+  if constexpr (K < 64 * NPL) bitonic_ks<NPL, 2 * K>(a, b, lane);
+}
+
+constexpr uint32_t kBowSent = 0xFFFFFFFFu;  // no key (padding, stopped word): sorts last
+
+template <int NPL>
+__global__ __launch_bounds__(256) void k_bowfv(int must, int l1, int tf,
+                                               const uint32_t* __restrict__ word_of,
+                                               const uint32_t* __restrict__ rank_of,
+                                               const double* __restrict__ weight_of,
+                                               int64_t in_stride, const int* __restrict__ counts,
+                                               int n_fixed, uint32_t* __restrict__ out_words,
+                                               double* __restrict__ out_vals, int64_t out_stride,
+                                               int* __restrict__ out_n, int nb,
+                                               const uint32_t* __restrict__ rank_ids,
+                                               uint32_t* __restrict__ node_ids,
+                                               int* __restrict__ offsets, int* __restrict__ feats,
+                                               int64_t feats_stride, int* __restrict__ n_nodes) {
+  constexpr int R = 64 * NPL, CAP = 4 * R;
+  constexpr int IB = __builtin_ctz(CAP);
+  constexpr uint32_t IMASK = (1u << IB) - 1u;
+  extern __shared__ __align__(16) uint32_t smb[];
+  uint32_t* runA = smb;             // [CAP] the four sorted runs (word keys)
+  uint32_t* runB = smb + CAP;       // [CAP] (rank keys)
+  uint32_t* mA = smb + 2 * CAP;     // [CAP] merged
+  uint32_t* mB = smb + 3 * CAP;     // [CAP]
+  int* s_start = (int*)(smb + 4 * CAP);  // [CAP + 1] word run starts
+  double* s_val = (double*)smb;     // [CAP] over the runs, after the merge
+  __shared__ int s_cnt[2][4];
+  const int img = blockIdx.x, lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = counts ? counts[img] : n_fixed;
+  const uint32_t* wo = word_of + img * in_stride;
+  const uint32_t* ro = rank_of + img * in_stride;
+  uint32_t a[NPL], b[NPL];
+  int ca = 0, cb = 0;
+#pragma unroll
+  for (int r = 0; r < NPL; r++) {
+    const int i = wid * R + lane * NPL + r;
+    const uint32_t w = i < n ? wo[i] : kBowSent, k = i < n ? ro[i] : kBowSent;
+    a[r] = w != kBowSent ? (w << IB) | (uint32_t)i : kBowSent;
+    b[r] = k != kBowSent ? (k << IB) | (uint32_t)i : kBowSent;
+    ca += a[r] != kBowSent;
+    cb += b[r] != kBowSent;
+  }
+  ca = wave_scan_incl(ca);
+  cb = wave_scan_incl(cb);
+  if (lane == 63) {
+    s_cnt[0][wid] = ca;
+    s_cnt[1][wid] = cb;
+  }
+  bitonic_ks<NPL, 2>(a, b, lane);
+#pragma unroll
+  for (int r = 0; r < NPL; r++) {
+    runA[wid * R + lane * NPL + r] = a[r];
+    runB[wid * R + lane * NPL + r] = b[r];
+  }
+  __syncthreads();
+  const int m_a = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
+  const int m_b = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
+  {  // merge by rank: keys are distinct, so a key's place is unique
+    int pa[NPL], pb[NPL];
+#pragma unroll
+    for (int r = 0; r < NPL; r++) pa[r] = pb[r] = lane * NPL + r;
+#pragma unroll
+    for (int o = 1; o < 4; o++) {
+      const int w2 = (wid + o) & 3;
+      const uint32_t* qa = runA + w2 * R;
+      const uint32_t* qb = runB + w2 * R;
+      int la[NPL], lb[NPL];
+#pragma unroll
+      for (int r = 0; r < NPL; r++) la[r] = lb[r] = 0;
+#pragma unroll
+      for (int st = R / 2; st > 0; st >>= 1) {  // la = min(keys below, R - 1)
+#pragma unroll
+        for (int r = 0; r < NPL; r++) {
+          la[r] += qa[la[r] + st - 1] < a[r] ? st : 0;
+          lb[r] += qb[lb[r] + st - 1] < b[r] ? st : 0;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NPL; r++) {
+        pa[r] += la[r] + (qa[la[r]] < a[r]);
+        pb[r] += lb[r] + (qb[lb[r]] < b[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NPL; r++) {
+      if (a[r] != kBowSent) mA[pa[r]] = a[r];
+      if (b[r] != kBowSent) mB[pb[r]] = b[r];
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1;
+  if (wid == 0) {  // BowVector: runs of equal words, weights in feature order
+    const double* wt = weight_of + img * in_stride;
+    int nu = 0;
+    for (int c0 = 0; c0 < m_a; c0 += 64) {
+      const int j = c0 + lane;
+      const bool valid = j < m_a;
+      const uint32_t x = valid ? mA[j] : 0u, px = valid && j > 0 ? mA[j - 1] : 0u;
+      const bool st = valid && (j == 0 || (x >> IB) != (px >> IB));
+      const uint64_t ball = __ballot(st);
+      if (st) s_start[nu + __popcll(ball & lt)] = j;
+      nu += __popcll(ball);
+    }
+    if (lane == 0) s_start[nu] = m_a;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t* ow = out_words + img * out_stride;
+    double* ov = out_vals + img * out_stride;
+    for (int o = lane; o < nu; o += 64) {
+      const int s0 = s_start[o], s1 = s_start[o + 1];
+      const uint32_t x = mA[s0];
+      double v = wt[x & IMASK];  // insert(value_type(id, w)) of the first occurrence
+      if (tf)
+        for (int j = s0 + 1; j < s1; j++) v += wt[mA[j] & IMASK];  // addWeight, feature order
+      if (tf && !must) v /= (double)nu;  // TemplatedVocabulary.h:1165-1172
+      ow[o] = x >> IB;
+      if (must)
+        s_val[o] = v;
+      else
+        ov[o] = v;
+    }
+    if (lane == 0) out_n[img] = nu;
+    if (must) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double norm = 0.0;
+      if (lane == 0) {  // BowVector::normalize: one ordered pass over the words
+        int o = 0;
+        if (l1) {
+          for (; o + 8 <= nu; o += 8) {
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
+#pragma unroll
+            for (int j = 0; j < 8; j++) norm += fabs(v[j]);
+          }
+          for (; o < nu; o++) norm += fabs(s_val[o]);
+        } else {
+          // built -O3 -march=native (Thirdparty/DBoW2/CMakeLists.txt): `norm += v * v` contracts
+          for (; o + 8 <= nu; o += 8) {
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
+#pragma unroll
+            for (int j = 0; j < 8; j++) norm = fma(v[j], v[j], norm);
+          }
+          for (; o < nu; o++) norm = fma(s_val[o], s_val[o], norm);
+          norm = sqrt(norm);
+        }
+      }
+      norm = __shfl(norm, 0);
+      for (int o = lane; o < nu; o += 64) ov[o] = norm > 0.0 ? s_val[o] / norm : s_val[o];
+    }
+  } else if (wid == 1) {  // FeatureVector CSR: node runs of the rank order
+    uint32_t* oid = node_ids + (int64_t)img * nb;
+    int* ooff = offsets + (int64_t)img * (nb + 1);
+    int* of = feats + img * feats_stride;
+    int nn = 0;
+    for (int c0 = 0; c0 < m_b; c0 += 64) {
+      const int j = c0 + lane;
+      const bool valid = j < m_b;
+      const uint32_t x = valid ? mB[j] : 0u, px = valid && j > 0 ? mB[j - 1] : 0u;
+      const bool st = valid && (j == 0 || (x >> IB) != (px >> IB));
+      const uint64_t ball = __ballot(st);
+      if (st) {
+        const int q = nn + __popcll(ball & lt);
+        oid[q] = rank_ids[x >> IB];
+        ooff[q] = j;
+      }
+      if (valid) of[j] = (int)(x & IMASK);
+      nn += __popcll(ball);
+    }
+    if (lane == 0) {
+      ooff[nn] = m_b;
+      n_nodes[img] = nn;
+    }
+  }
+}
+
+template <int NPL>
+static int launch_bowfv_t(int must, int l1, int tf, const uint32_t* d_word_of,
+                          const uint32_t* d_rank_of, const double* d_weight_of, int64_t in_stride,
+                          const int* d_counts, int n_fixed, uint32_t* d_words, double* d_values,
+                          int64_t out_stride, int* d_nwords, int nb, const uint32_t* d_rank_ids,
+                          uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride,
+                          int* d_nn, int nimg, hipStream_t s) {
+  constexpr int CAP = 256 * NPL;
+  constexpr size_t smem = (size_t)CAP * 20 + 16;  // runs, merged orders, run starts
+  if constexpr (smem > 64 * 1024) {
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+      attr = hipFuncSetAttribute((const void*)k_bowfv<NPL>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    });
+    if (attr != hipSuccess) return report_hip(attr, "hipFuncSetAttribute(k_bowfv)");
+  }
+  hipLaunchKernelGGL(k_bowfv<NPL>, dim3(nimg), dim3(256), smem, s, must, l1, tf, d_word_of,
+                     d_rank_of, d_weight_of, in_stride, d_counts, n_fixed, d_words, d_values,
+                     out_stride, d_nwords, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride,
+                     d_nn);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_bowfv");
+}
+
+int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word_of,
+                 const uint32_t* d_rank_of, const double* d_weight_of, int64_t in_stride,
+                 const int* d_counts, int n_fixed, int max_n, uint32_t* d_words, double* d_values,
+                 int64_t out_stride, int* d_nwords, int nb, const uint32_t* d_rank_ids,
+                 uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride, int* d_nn,
+                 int nimg, hipStream_t s) {
+  static const bool enabled = [] {
+    const char* e = getenv("ORBX_BOWFV");
+    return !e || atoi(e) != 0;
+  }();
+  if (!enabled || !d_rank_ids || nb < 1) return ORBX_EUNSUPPORTED;
+  if (nimg <= 0) return ORBX_OK;
+  const int must = scoring != ORBX_SCORE_DOT_PRODUCT;
+  const int l1 = scoring != ORBX_SCORE_L2;
+  const int tf = weighting == ORBX_WEIGHT_TF_IDF || weighting == ORBX_WEIGHT_TF;
+  // keys (id << IB | feature) stay below the sentinel: id < 2^(32 - IB) - 1
+  auto fits = [&](int cap, int ib) {
+    const int64_t lim = ((int64_t)1 << (32 - ib)) - 1;
+    return max_n <= cap && n_words < lim && nb < lim;
+  };
+#define ORBX_BOWFV_ARGS                                                                        \
+  must, l1, tf, d_word_of, d_rank_of, d_weight_of, in_stride, d_counts, n_fixed, d_words,     \
+      d_values, out_stride, d_nwords, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride, d_nn, \
+      nimg, s
+  if (fits(1024, 10)) return launch_bowfv_t<4>(ORBX_BOWFV_ARGS);
+  if (fits(2048, 11)) return launch_bowfv_t<8>(ORBX_BOWFV_ARGS);
+  if (fits(4096, 12)) return launch_bowfv_t<16>(ORBX_BOWFV_ARGS);
+#undef ORBX_BOWFV_ARGS
+  return ORBX_EUNSUPPORTED;
+}
+
 // ------------------------------------------------------------------ host side
 namespace {
 
@@ -671,13 +986,20 @@ int orbx_vocabulary_transform(const orbx_vocabulary* V, const uint8_t* desc, int
                               dptr<double>(base, owt), 0, 1, s);
     if (rc) return rc;
   }
-  rc = launch_bowvec(V->scoring, V->weighting, dptr<uint32_t>(base, ow), dptr<double>(base, owt),
-                     0, nullptr, n, n, dptr<uint32_t>(base, obw), dptr<double>(base, obv), 0,
-                     dptr<int>(base, obn), 1, s);
-  if (rc) return rc;
-  rc = launch_csr(dptr<uint32_t>(base, orank), 0, nullptr, n, 0, std::max(R->nb, 1),
-                  R->d_rank_ids, dptr<uint32_t>(base, ofi), dptr<int>(base, ofo),
-                  dptr<int>(base, off), 0, dptr<int>(base, ofn), 1, s);
+  rc = launch_bowfv(V->scoring, V->weighting, V->n_words, dptr<uint32_t>(base, ow),
+                    dptr<uint32_t>(base, orank), dptr<double>(base, owt), 0, nullptr, n, n,
+                    dptr<uint32_t>(base, obw), dptr<double>(base, obv), 0, dptr<int>(base, obn),
+                    R->nb, R->d_rank_ids, dptr<uint32_t>(base, ofi), dptr<int>(base, ofo),
+                    dptr<int>(base, off), 0, dptr<int>(base, ofn), 1, s);
+  if (rc == ORBX_EUNSUPPORTED) {
+    rc = launch_bowvec(V->scoring, V->weighting, dptr<uint32_t>(base, ow),
+                       dptr<double>(base, owt), 0, nullptr, n, n, dptr<uint32_t>(base, obw),
+                       dptr<double>(base, obv), 0, dptr<int>(base, obn), 1, s);
+    if (rc) return rc;
+    rc = launch_csr(dptr<uint32_t>(base, orank), 0, nullptr, n, 0, std::max(R->nb, 1),
+                    R->d_rank_ids, dptr<uint32_t>(base, ofi), dptr<int>(base, ofo),
+                    dptr<int>(base, off), 0, dptr<int>(base, ofn), 1, s);
+  }
   if (rc) return rc;
   ORBX_HIP(tls_ws.download(ow, st.host.size() - ow));
   ORBX_HIP(orbx::wait_stream(s));
