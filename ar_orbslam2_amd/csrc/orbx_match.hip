@@ -70,10 +70,11 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {
 }
 
 // ------------------------------------------------------------------ SearchByBoW
-__global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict__ probs) {
-  const BowProblem& P = probs[blockIdx.y];
-  const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+// One wave per KF node a of problem pi (every lane of the wave active; the problem read through
+// the kernel's __restrict__ pointer, so its fields stay in scalar registers across the stores)
+__device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ probs, const int pi,
+                                              const int a, const int lane) {
+  const BowProblem& P = probs[pi];
   if (a >= side_nodes(P.s1)) return;
   const uint32_t id = P.s1.node_ids[a];
   const int nn2 = side_nodes(P.s2);
@@ -228,6 +229,203 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict_
 #pragma unroll
   for (int c = 0; c < kBowDescChunks; c++)
     if (mval[c] >= 0) P.match[i2r[c]] = mval[c];
+}
+
+__global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict__ probs) {
+  bow_node_wave(probs, blockIdx.y, blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+}
+
+// Latency form of k_bow_nodes for calls with few problems (the per-frame drop-in call), where
+// one wave per node leaves the GPU idle behind the node with the longest serial loop: one
+// workgroup per KF node of at most kBwgCands candidates, and no serial loop.  The greedy scan
+// (each KF feature in node order takes its best candidate not matched by an earlier one,
+// ORBmatcher.cc:187-250 / 557-622) is solved as a triangular fixed point:
+//  (1) every KF feature's kBwgK smallest (distance << 8 | position) keys over all candidates,
+//      the candidates split over the four waves (partial lists merged by wave 0), distances
+//      kept in LDS;
+//  (2) wave 0 (lane = KF feature) repeats "take the first two keys of my list whose candidate
+//      no lower lane claims" until no lane's claim changes.  Feature k's outcome depends only on
+//      the claims of features < k, so iteration t settles features < t and the fixed point is
+//      the sequential result; a feature whose list runs out of unclaimed keys while more valid
+//      candidates exist rescans its distance row.
+constexpr int kBwgCands = 128;  // claim masks: two u64
+constexpr int kBwgK = 8;
+constexpr uint32_t kBwgSent = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void topk_insert(uint32_t (&L)[kBwgK], uint32_t key) {
+#pragma unroll
+  for (int q = 0; q < kBwgK; q++) {
+    const uint32_t lo = min(L[q], key);
+    key = max(L[q], key);
+    L[q] = lo;
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_or_excl(uint32_t u) {  // OR over the lanes below
+  u |= dpp0<0x111, 0xF, true>(u);   // row_shr:1
+  u |= dpp0<0x112, 0xF, true>(u);   // row_shr:2
+  u |= dpp0<0x114, 0xF, true>(u);   // row_shr:4
+  u |= dpp0<0x118, 0xF, true>(u);   // row_shr:8
+  u |= dpp0<0x142, 0xA, false>(u);  // row_bcast:15
+  u |= dpp0<0x143, 0xC, false>(u);  // row_bcast:31
+  const int lane = threadIdx.x & 63;
+  const uint32_t below = (uint32_t)__shfl((int)u, lane > 0 ? lane - 1 : 0);
+  return lane > 0 ? below : 0u;
+}
+
+__device__ __forceinline__ uint64_t wave_or_all64(uint64_t v) {  // OR over the wave
+  const uint32_t lo = wave_or_excl((uint32_t)v) | (uint32_t)v;
+  const uint32_t hi = wave_or_excl((uint32_t)(v >> 32)) | (uint32_t)(v >> 32);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, 63) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32);
+}
+
+__device__ __forceinline__ bool claimed(uint64_t m0, uint64_t m1, int pos) {
+  return ((pos < 64 ? m0 >> pos : m1 >> (pos - 64)) & 1) != 0;
+}
+
+__global__ __launch_bounds__(256) void k_bow_nodes_wg(const BowProblem* __restrict__ probs) {
+  const BowProblem& P = probs[blockIdx.y];
+  const int a = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a >= side_nodes(P.s1)) return;
+  __shared__ uint64_t s_cd[kBwgCands][4];
+  __shared__ int s_ci2[kBwgCands];
+  __shared__ uint16_t s_dist[64][kBwgCands + 2];  // odd dword row stride
+  __shared__ uint32_t s_list[4][kBwgK][64];
+  __shared__ int s_b, s_nv;
+  const uint32_t id = P.s1.node_ids[a];
+  if (tid < 64) {
+    const int nn2 = side_nodes(P.s2);
+    const int b = wave_lower_bound(P.s2.node_ids, nn2, id, lane);
+    if (lane == 0) s_b = b < nn2 && P.s2.node_ids[b] == id ? b : -1;
+  }
+  __syncthreads();
+  const int b = s_b;
+  if (b < 0) return;  // workgroup-uniform
+  const int f0 = P.s2.node_offsets[b], m = P.s2.node_offsets[b + 1] - f0;
+  if (m > kBwgCands) {  // the wave form (no candidate limit)
+    if (wid == 0) bow_node_wave(probs, blockIdx.y, a, lane);
+    return;
+  }
+  const bool kfkf = P.mode == 1;
+  if (tid < 64) {  // candidates: descriptor, index, validity (mode 1: pMP2 of KF2)
+    int nv = 0;
+    for (int j0 = 0; j0 < m; j0 += 64) {
+      const int j = j0 + lane;
+      int i2 = -1;
+      if (j < m) {
+        i2 = P.s2.node_feats[f0 + j];
+        const uint64_t* q = (const uint64_t*)(P.s2.desc + (int64_t)i2 * 32);
+        s_cd[j][0] = q[0];
+        s_cd[j][1] = q[1];
+        s_cd[j][2] = q[2];
+        s_cd[j][3] = q[3];
+        if (kfkf && P.s2.valid && !P.s2.valid[i2]) i2 = -1;
+        s_ci2[j] = i2;
+      }
+      nv += __popcll(__ballot(i2 >= 0));
+    }
+    if (lane == 0) s_nv = nv;
+  }
+  __syncthreads();
+  const int nv = s_nv;
+  const int mq = (m + 3) >> 2, jb = wid * mq, je = min(m, jb + mq);
+  uint64_t M0 = 0, M1 = 0;  // candidates claimed by earlier chunks (wave 0)
+  const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
+  for (int c0 = a0; c0 < a1; c0 += 64) {
+    const int k = c0 + lane;
+    int i1 = -1;
+    bool ok1 = false;
+    uint64_t d1[4] = {0, 0, 0, 0};
+    if (k < a1) {
+      i1 = P.s1.node_feats[k];
+      ok1 = !P.s1.valid || P.s1.valid[i1];
+      if (ok1) {
+        const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
+        d1[0] = q[0]; d1[1] = q[1]; d1[2] = q[2]; d1[3] = q[3];
+      }
+    }
+    uint32_t L[kBwgK];
+#pragma unroll
+    for (int q = 0; q < kBwgK; q++) L[q] = kBwgSent;
+    for (int j = jb; j < je; j++) {  // this wave's quarter, in position order
+      if (s_ci2[j] < 0) continue;    // uniform
+      const int d = __popcll(d1[0] ^ s_cd[j][0]) + __popcll(d1[1] ^ s_cd[j][1]) +
+                    __popcll(d1[2] ^ s_cd[j][2]) + __popcll(d1[3] ^ s_cd[j][3]);
+      s_dist[lane][j] = (uint16_t)d;
+      topk_insert(L, ((uint32_t)d << 8) | (uint32_t)j);
+    }
+#pragma unroll
+    for (int q = 0; q < kBwgK; q++) s_list[wid][q][lane] = L[q];
+    __syncthreads();
+    if (wid == 0) {
+      for (int w = 1; w < 4; w++) {  // merge the other waves' lists (sorted: stop at the first miss)
+        for (int q = 0; q < kBwgK; q++) {
+          const uint32_t e = s_list[w][q][lane];
+          if (e >= L[kBwgK - 1]) break;
+          topk_insert(L, e);
+        }
+      }
+      const bool more = nv > kBwgK;  // the lists may not hold every valid candidate
+      int out = -1;
+      for (;;) {
+        const uint64_t mine0 = out >= 0 && out < 64 ? 1ull << out : 0ull;
+        const uint64_t mine1 = out >= 64 ? 1ull << (out - 64) : 0ull;
+        const uint64_t E0 = M0 | wave_or_excl((uint32_t)mine0) |
+                            ((uint64_t)wave_or_excl((uint32_t)(mine0 >> 32)) << 32);
+        const uint64_t E1 = M1 | wave_or_excl((uint32_t)mine1) |
+                            ((uint64_t)wave_or_excl((uint32_t)(mine1 >> 32)) << 32);
+        int nout = -1;
+        if (ok1) {
+          int b1 = 256, bp = -1, b2 = 256, found = 0;
+#pragma unroll
+          for (int q = 0; q < kBwgK; q++) {
+            const uint32_t e = L[q];
+            if (found == 2 || e == kBwgSent) continue;
+            const int pos = (int)(e & 0xFF);
+            if (claimed(E0, E1, pos)) continue;
+            if (found == 0) {
+              b1 = (int)(e >> 8);
+              bp = pos;
+            } else {
+              b2 = (int)(e >> 8);
+            }
+            found++;
+          }
+          if (found < 2 && more) {  // the next unclaimed key lies past the list: the whole row
+            b1 = 256, bp = -1, b2 = 256;
+            for (int j = 0; j < m; j++) {
+              if (s_ci2[j] < 0 || claimed(E0, E1, j)) continue;
+              const int d = s_dist[lane][j];
+              if (d < b1) {
+                b2 = b1;
+                b1 = d;
+                bp = j;
+              } else if (d < b2) {
+                b2 = d;
+              }
+            }
+          }
+          const bool pass = kfkf ? b1 < kTH_LOW : b1 <= kTH_LOW;
+          if (bp >= 0 && pass && static_cast<float>(b1) < P.nnratio * static_cast<float>(b2))
+            nout = bp;
+        }
+        const bool changed = __ballot(nout != out) != 0;
+        out = nout;
+        if (!changed) break;
+      }
+      if (out >= 0) {
+        const int i2 = s_ci2[out];
+        if (kfkf) P.match[i1] = i2;
+        else P.match[i2] = i1;
+      }
+      M0 |= wave_or_all64(out >= 0 && out < 64 ? 1ull << out : 0ull);
+      M1 |= wave_or_all64(out >= 64 ? 1ull << (out - 64) : 0ull);
+    }
+    __syncthreads();  // s_list / s_dist are rewritten by the next chunk
+  }
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:1604-1645)
@@ -752,9 +950,19 @@ __global__ void k_distance(const uint8_t* a, const uint8_t* b, int n, int* out) 
 }
 
 // ------------------------------------------------------------------ launchers
+// calls with at most kBowWgProbs problems use the workgroup-per-node SearchByBoW
+// (ORBX_BOW_WG_PROBS overrides the limit for experiments)
+constexpr int kBowWgProbs = 4;
+
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s) {
   if (nprob <= 0) return ORBX_OK;
-  if (max_nodes1 > 0)
+  static const int wg_probs = [] {
+    const char* e = getenv("ORBX_BOW_WG_PROBS");
+    return e ? atoi(e) : kBowWgProbs;
+  }();
+  if (max_nodes1 > 0 && nprob <= wg_probs)
+    hipLaunchKernelGGL(k_bow_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
+  else if (max_nodes1 > 0)
     hipLaunchKernelGGL(k_bow_nodes, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
   hipLaunchKernelGGL(k_bow_finish, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();

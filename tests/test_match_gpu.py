@@ -191,6 +191,69 @@ def test_search_by_bow_single_huge_node(n):
         assert np.array_equal(got, m_ref)
 
 
+def _contested_sides(n1, n2, palette, seed, chain=False):
+    """n1 keyframe and n2 frame features in one vocabulary node, all descriptors a few bits away
+    from one of `palette` base descriptors: many keyframe features want the same candidates,
+    distances tie, and late features find their best candidates already matched."""
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, (palette, 32), dtype=np.uint8)
+
+    def draw(which, flips):
+        bits = np.unpackbits(base[which], axis=1)
+        for i in range(len(which)):
+            bits[i, rng.choice(256, flips(i), replace=False)] ^= 1
+        return np.packbits(bits, axis=1)
+
+    def side(d, valid):
+        n = len(d)
+        s = type("S", (), {})()
+        s.mDescriptors = d
+        s.mvKeys = s.mvKeysUn = np.zeros(n, O.KEYPOINT_DTYPE)
+        s.mvKeys["angle"] = rng.random(n).astype(np.float32) * 360
+        s.mFeatVec = (np.array([5], np.uint32), np.array([0, n], np.int32),
+                      np.arange(n, dtype=np.int32))
+        s.valid = valid
+        return s
+    # frame: n2 / palette copies of every base, 0-8 bits off; keyframe: bases 0-3 bits off.
+    # chain: copy c of a base is exactly c bits off and the keyframe features are the bases, so
+    # successive keyframe features of a base claim its copies one after the other (past the
+    # workgroup form's 8-key lists)
+    if chain:
+        return (side(draw(rng.integers(0, palette, n1), lambda i: 0), np.ones(n1, np.uint8)),
+                side(draw(np.arange(n2) % palette, lambda i: i // palette), np.ones(n2, np.uint8)))
+    return (side(draw(rng.integers(0, palette, n1), lambda i: rng.integers(0, 4)),
+                 (rng.random(n1) < 0.8).astype(np.uint8)),
+            side(draw(np.arange(n2) % palette, lambda i: rng.integers(0, 9)),
+                 (rng.random(n2) < 0.8).astype(np.uint8)))
+
+
+@pytest.mark.parametrize("n1,n2,palette,chain", [
+    (100, 128, 8, False), (200, 60, 4, False), (64, 128, 128, False), (130, 100, 16, False),
+    (90, 7, 2, False), (10, 128, 1, False), (40, 40, 2, True), (100, 128, 4, True),
+    (70, 120, 1, True)])
+def test_search_by_bow_contested_nodes(n1, n2, palette, chain):
+    """Nodes of at most 128 candidates (the one-problem calls' workgroup form): more keyframe
+    features than a wave, tied distances and best candidates claimed by earlier features — the
+    greedy order of ORBmatcher.cc:187-250 / 557-622 must come out exactly."""
+    kf, f = _contested_sides(n1, n2, palette, 1000 * n1 + n2, chain)
+    for ratio, ori in ((0.7, True), (0.9, False), (1.0, False)):
+        n_ref, m_ref = O.search_by_bow_kf_f(_oracle_bow_side(kf), _oracle_bow_side(f, False),
+                                            ratio, ori)
+        fr = type("F", (), {})()
+        fr.mDescriptors, fr.mvKeys, fr.mFeatVec = f.mDescriptors, f.mvKeys, f.mFeatVec
+        got_n, got = ORBmatcher(ratio, ori).SearchByBoW(kf, fr)
+        assert got_n == n_ref
+        assert np.array_equal(got, m_ref)
+        f.is_keyframe = True
+        n_ref2, m_ref = O.search_by_bow_kf_kf(_oracle_bow_side(kf), _oracle_bow_side(f), ratio, ori)
+        got_n, got = ORBmatcher(ratio, ori).SearchByBoW(kf, f)
+        del f.is_keyframe
+        assert got_n == n_ref2
+        assert np.array_equal(got, m_ref)
+        if ratio == 1.0 and palette <= 16:
+            assert n_ref > (8 if chain else 0)
+
+
 @pytest.mark.parametrize("kind", [0, 1, 2])
 def test_finish_kernels_reject_stale_indices(kind):
     """A match array holding indices outside the other side (what a stale buffer would hold)
