@@ -1,5 +1,5 @@
-"""GPU parity of the DBoW2 vocabulary (orbx_vocabulary_*: loader, k_voc_transform, k_bowvec,
-k_csr) against the CPU restatement (oracle/dbow2_oracle.cc): word ids, FeatureVector node ids,
+"""GPU parity of the DBoW2 vocabulary (orbx_vocabulary_*: loader, k_voc_transform, k_bowfv, and
+k_bowvec + k_csr above 4,096 features) against the CPU restatement (oracle/dbow2_oracle.cc): word ids, FeatureVector node ids,
 BowVector word ids and f64 values bit for bit, FeatureVector CSR."""
 import numpy as np
 import pytest
@@ -51,6 +51,22 @@ def test_random_irregular_trees(seed, k, depth, n):
         f[: n // 2] = arrays[2][rng.integers(0, len(arrays[2]), n // 2)]
         f[: n // 4, 0] ^= 1
     for levelsup in (1, 2, depth):
+        _same(g.transform_full(f, levelsup), o.transform(f, levelsup))
+
+
+@pytest.mark.parametrize("n", [1024, 1025, 2048, 2049, 4096])
+@pytest.mark.parametrize("scoring,weighting", [(0, 0), (1, 1), (4, 0)])
+def test_bowfv_capacity_edges(n, scoring, weighting):
+    """k_bowfv's three instances (up to 1,024 / 2,048 / 4,096 features per image) at and past
+    their capacities, with repeated words (near-duplicate node descriptors)."""
+    arrays = random_tree(7, k=10, depth=3)
+    g = Vocabulary.from_nodes(10, 4, scoring, weighting, *arrays)
+    o = O.Vocabulary.from_nodes(10, 4, scoring, weighting, *arrays)
+    rng = np.random.default_rng(n)
+    f = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    f[: n // 2] = arrays[2][rng.integers(0, len(arrays[2]), n // 2)]
+    f[: n // 4, 0] ^= 1
+    for levelsup in (1, 3):
         _same(g.transform_full(f, levelsup), o.transform(f, levelsup))
 
 
