@@ -42,6 +42,8 @@ struct BowProblem {
   int* count;
   int* error;  // bit 1 (ORBX_DEVERR_INDEX): a match index outside the other side
   int* matched2;  // mode 1, nodes above kBowRegCands candidates: vbMatched2 flags [s2.n], zeroed
+  int* done;      // nullable, zeroed: k_bow_nodes_wg's finished-workgroup counter (the last one
+                  // runs the finish); null: k_bow_finish is launched after it
   int mode;
   float nnratio;
   int check_ori;
@@ -82,6 +84,7 @@ struct TriProblem {
   int* pairs;  // [s1.n][2]
   int* count;
   int* error;  // bit 1 (ORBX_DEVERR_INDEX): a match index outside KF2
+  int* done;   // nullable, zeroed: k_tri_nodes_wg's finished-workgroup counter (as BowProblem)
 };
 
 // device error bits of the matcher problems: a finish kernel read a match index outside the
@@ -100,8 +103,12 @@ constexpr int kBowDescChunks = ORBX_BOW_CHUNKS;
 constexpr int kBowMaxSide2 = 1 << 23;
 constexpr int kBowPosMask = kBowMaxSide2 - 1;
 
-int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
-int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s);
+// fused_finish: every problem's `done` counter is set and zeroed, and a call taking the
+// workgroup-per-node kernel runs the finish in its last workgroup instead of a second launch
+int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
+               bool fused_finish = false);
+int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
+               bool fused_finish = false);
 int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,
                uint32_t id_lo, int nb, const uint32_t* d_rank_ids, uint32_t* d_ids, int* d_off,
                int* d_feats, int64_t feats_stride, int* d_nn, int nimg, hipStream_t s);

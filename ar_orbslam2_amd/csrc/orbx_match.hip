@@ -69,6 +69,10 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {
   return bin;
 }
 
+__device__ __forceinline__ void bow_finish(const BowProblem* __restrict__ probs, const int pi);
+__device__ __forceinline__ void tri_finish(const TriProblem* __restrict__ probs, const int pi);
+__device__ __forceinline__ bool last_workgroup(int* done);
+
 // ------------------------------------------------------------------ SearchByBoW
 // One wave per KF node a of problem pi (every lane of the wave active; the problem read through
 // the kernel's __restrict__ pointer, so its fields stay in scalar registers across the stores)
@@ -284,7 +288,7 @@ __device__ __forceinline__ bool claimed(uint64_t m0, uint64_t m1, int pos) {
   return ((pos < 64 ? m0 >> pos : m1 >> (pos - 64)) & 1) != 0;
 }
 
-__global__ __launch_bounds__(256) void k_bow_nodes_wg(const BowProblem* __restrict__ probs) {
+__device__ __forceinline__ void bow_nodes_wg(const BowProblem* __restrict__ probs) {
   const BowProblem& P = probs[blockIdx.y];
   const int a = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -428,6 +432,11 @@ __global__ __launch_bounds__(256) void k_bow_nodes_wg(const BowProblem* __restri
   }
 }
 
+__global__ __launch_bounds__(256) void k_bow_nodes_wg(const BowProblem* __restrict__ probs) {
+  bow_nodes_wg(probs);
+  if (probs[blockIdx.y].done && last_workgroup(probs[blockIdx.y].done)) bow_finish(probs, blockIdx.y);
+}
+
 // ComputeThreeMaxima (ORBmatcher.cc:1604-1645)
 __device__ void three_maxima(const int* h, int& ind1, int& ind2, int& ind3) {
   int max1 = 0, max2 = 0, max3 = 0;
@@ -457,8 +466,8 @@ __device__ void three_maxima(const int* h, int& ind1, int& ind2, int& ind3) {
 // mode 1 / triangulation indexed by side-1 feature (value = side-2 idx).
 constexpr int kFinishRegs = 8;  // entries per thread per gather round (n <= 2048: one round)
 
-__global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict__ probs) {
-  const BowProblem& P = probs[blockIdx.x];
+__device__ __forceinline__ void bow_finish(const BowProblem* __restrict__ probs, const int pi) {
+  const BowProblem& P = probs[pi];
   __shared__ int hist[kHISTO];
   __shared__ int s_ind[3];
   __shared__ int s_cnt;
@@ -543,6 +552,26 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict
   atomicAdd(&s_cnt, local);
   __syncthreads();
   if (tid == 0) *P.count = s_cnt;
+}
+
+__global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict__ probs) {
+  bow_finish(probs, blockIdx.x);
+}
+
+// The last workgroup of a node kernel to finish (counted in *done, zeroed by the host) runs the
+// problem's finish: one launch fewer on the latency path.  Stores of every workgroup are made
+// visible device-wide before its count (release), and read after the last count (acquire).
+__device__ __forceinline__ bool last_workgroup(int* done) {
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(done, 1) == (int)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return false;
+  __threadfence();
+  return true;
 }
 
 // ------------------------------------------------------------------ SearchForTriangulation
@@ -668,7 +697,7 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
 // node, the KF2 node staged 256 features at a time for the whole workgroup and G = 256 / n1
 // lanes per KF1 feature, so a node's scan is spread over four times as many lanes.  Same keys,
 // same LDS minimum, same result.
-__global__ __launch_bounds__(256) void k_tri_nodes_wg(const TriProblem* __restrict__ probs) {
+__device__ __forceinline__ void tri_nodes_wg(const TriProblem* __restrict__ probs) {
   const TriProblem& P = probs[blockIdx.y];
   const int a = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -767,8 +796,13 @@ __global__ __launch_bounds__(256) void k_tri_nodes_wg(const TriProblem* __restri
   }
 }
 
-__global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict__ probs) {
-  const TriProblem& P = probs[blockIdx.x];
+__global__ __launch_bounds__(256) void k_tri_nodes_wg(const TriProblem* __restrict__ probs) {
+  tri_nodes_wg(probs);
+  if (probs[blockIdx.y].done && last_workgroup(probs[blockIdx.y].done)) tri_finish(probs, blockIdx.y);
+}
+
+__device__ __forceinline__ void tri_finish(const TriProblem* __restrict__ probs, const int pi) {
+  const TriProblem& P = probs[pi];
   __shared__ int hist[kHISTO];
   __shared__ int s_ind[3];
   __shared__ int s_scan[4];
@@ -858,6 +892,10 @@ __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict
     }
   }
   if (tid == 0) *P.count = total;
+}
+
+__global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict__ probs) {
+  tri_finish(probs, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ vocabulary + FeatureVector
@@ -954,17 +992,20 @@ __global__ void k_distance(const uint8_t* a, const uint8_t* b, int n, int* out) 
 // (ORBX_BOW_WG_PROBS overrides the limit for experiments)
 constexpr int kBowWgProbs = 4;
 
-int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s) {
+int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
+               bool fused_finish) {
   if (nprob <= 0) return ORBX_OK;
   static const int wg_probs = [] {
     const char* e = getenv("ORBX_BOW_WG_PROBS");
     return e ? atoi(e) : kBowWgProbs;
   }();
-  if (max_nodes1 > 0 && nprob <= wg_probs)
+  const bool wg = max_nodes1 > 0 && nprob <= wg_probs;
+  if (wg)
     hipLaunchKernelGGL(k_bow_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
   else if (max_nodes1 > 0)
     hipLaunchKernelGGL(k_bow_nodes, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
-  hipLaunchKernelGGL(k_bow_finish, dim3(nprob), dim3(256), 0, s, d_probs);
+  if (!(wg && fused_finish))  // else the node kernel's last workgroup ran it
+    hipLaunchKernelGGL(k_bow_finish, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_bow");
 }
@@ -973,17 +1014,20 @@ int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t
 // (ORBX_TRI_WG_PROBS overrides the limit for experiments)
 constexpr int kTriWgProbs = 4;
 
-int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s) {
+int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
+               bool fused_finish) {
   if (nprob <= 0) return ORBX_OK;
   static const int wg_probs = [] {
     const char* e = getenv("ORBX_TRI_WG_PROBS");
     return e ? atoi(e) : kTriWgProbs;
   }();
-  if (max_nodes1 > 0 && nprob <= wg_probs)
+  const bool wg = max_nodes1 > 0 && nprob <= wg_probs;
+  if (wg)
     hipLaunchKernelGGL(k_tri_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
   else if (max_nodes1 > 0)
     hipLaunchKernelGGL(k_tri_nodes, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
-  hipLaunchKernelGGL(k_tri_finish, dim3(nprob), dim3(256), 0, s, d_probs);
+  if (!(wg && fused_finish))  // else the node kernel's last workgroup ran it
+    hipLaunchKernelGGL(k_tri_finish, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_tri");
 }
@@ -1109,6 +1153,7 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
   P.count = dptr<int>(base, ocount);
   P.error = dptr<int>(base, ocount + 4);
   P.matched2 = dptr<int>(base, omatched2);
+  P.done = dptr<int>(base, ocount + 8);
   P.mode = mode;
   P.nnratio = nnratio;
   P.check_ori = check_ori;
@@ -1118,7 +1163,7 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
   memset(st.host.data() + omatched2, 0, (size_t)std::max(s2->n, 1) * 4);
   hipStream_t s = tls_ws.stream;
   ORBX_HIP(tls_ws.upload(st.host, st.host.size()));
-  rc = launch_bow(dptr<BowProblem>(base, oprob), 1, s1->fv.n_nodes, s);
+  rc = launch_bow(dptr<BowProblem>(base, oprob), 1, s1->fv.n_nodes, s, true);
   if (rc) return rc;
   ORBX_HIP(tls_ws.download(omatch, ocount + 8 - omatch));  // match array and count / error
   ORBX_HIP(orbx::wait_stream(s));
@@ -1207,12 +1252,13 @@ int orbx_search_for_triangulation(const orbx_tri_side* k1, const orbx_tri_side* 
   P.pairs = dptr<int>(base, opairs);
   P.count = dptr<int>(base, ocount);
   P.error = dptr<int>(base, ocount + 4);
+  P.done = dptr<int>(base, ocount + 8);
   memcpy(st.host.data() + oprob, &P, sizeof(P));
   memset(st.host.data() + om12, 0xFF, (size_t)n1 * 4);
   memset(st.host.data() + ocount, 0, 16);
   hipStream_t s = tls_ws.stream;
   ORBX_HIP(tls_ws.upload(st.host, st.host.size()));
-  rc = launch_tri(dptr<TriProblem>(base, oprob), 1, k1->fv.n_nodes, s);
+  rc = launch_tri(dptr<TriProblem>(base, oprob), 1, k1->fv.n_nodes, s, true);
   if (rc) return rc;
   ORBX_HIP(tls_ws.download(opairs, ocount + 8 - opairs));  // pairs and count / error
   ORBX_HIP(orbx::wait_stream(s));

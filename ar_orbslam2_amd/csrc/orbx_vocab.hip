@@ -386,9 +386,10 @@ int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
 //      per lane, partners inside a lane or across lanes by DPP / swizzle / bpermute);
 //  (2) the four sorted runs merge by rank: a key's place = its place in its run + the keys
 //      below it in the three other runs (branch-free binary searches in LDS);
-//  (3) wave 0 finds the word runs, sums their weights in feature order and runs the scoring's
-//      ordered normalisation (BowVector::normalize, :66-98), while wave 1 writes the
-//      FeatureVector CSR (node ids, offsets, features).
+//  (3) waves 0 / 1 find the word / node runs in LDS; the workgroup sums each word's weights in
+//      feature order (weights staged in LDS with the keys) and writes the FeatureVector CSR
+//      (node ids, offsets, features); one lane runs the scoring's ordered normalisation
+//      (BowVector::normalize, :66-98).
 // It replaces k_bowvec + k_csr (a radix sort with ~15 workgroup barriers, and a wave-serial
 // bucket placement) where it applies: one launch and three barriers per image.
 template <int M>
@@ -468,18 +469,24 @@ __global__ __launch_bounds__(256) void k_bowfv(int must, int l1, int tf,
   constexpr int IB = __builtin_ctz(CAP);
   constexpr uint32_t IMASK = (1u << IB) - 1u;
   extern __shared__ __align__(16) uint32_t smb[];
-  uint32_t* runA = smb;             // [CAP] the four sorted runs (word keys)
-  uint32_t* runB = smb + CAP;       // [CAP] (rank keys)
-  uint32_t* mA = smb + 2 * CAP;     // [CAP] merged
-  uint32_t* mB = smb + 3 * CAP;     // [CAP]
-  int* s_start = (int*)(smb + 4 * CAP);  // [CAP + 1] word run starts
-  double* s_val = (double*)smb;     // [CAP] over the runs, after the merge
+  uint32_t* runA = smb;                      // [CAP] the four sorted runs (word keys)
+  uint32_t* runB = smb + CAP;                // [CAP] (rank keys)
+  uint32_t* mA = smb + 2 * CAP;              // [CAP] merged
+  uint32_t* mB = smb + 3 * CAP;              // [CAP]
+  double* s_wt = (double*)(smb + 4 * CAP);   // [CAP] feature weights
+  int* s_start = (int*)(smb + 6 * CAP);      // [CAP + 1] word run starts
+  int* s_nstart = (int*)(smb + 7 * CAP + 4); // [CAP + 1] node run starts
+  double* s_val = (double*)smb;              // [CAP] over the runs, after the merge
   __shared__ int s_cnt[2][4];
-  const int img = blockIdx.x, lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __shared__ int s_nu, s_nn;
+  __shared__ double s_norm;
+  const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = counts ? counts[img] : n_fixed;
   const uint32_t* wo = word_of + img * in_stride;
   const uint32_t* ro = rank_of + img * in_stride;
+  const double* wt = weight_of + img * in_stride;
+  for (int i = tid; i < n; i += 256) s_wt[i] = wt[i];  // coalesced; read after the merge barrier
   uint32_t a[NPL], b[NPL];
   int ca = 0, cb = 0;
 #pragma unroll
@@ -539,95 +546,94 @@ __global__ __launch_bounds__(256) void k_bowfv(int must, int l1, int tf,
     }
   }
   __syncthreads();
+  // run starts from LDS alone: wave 0 the words (BowVector entries), wave 1 the FeatureVector
+  // nodes
   const uint64_t lt = (1ull << lane) - 1;
-  if (wid == 0) {  // BowVector: runs of equal words, weights in feature order
-    const double* wt = weight_of + img * in_stride;
-    int nu = 0;
-    for (int c0 = 0; c0 < m_a; c0 += 64) {
+  if (wid < 2) {
+    const uint32_t* mk = wid == 0 ? mA : mB;
+    const int mm = wid == 0 ? m_a : m_b;
+    int* starts = wid == 0 ? s_start : s_nstart;
+    int cnt = 0;
+    for (int c0 = 0; c0 < mm; c0 += 64) {
       const int j = c0 + lane;
-      const bool valid = j < m_a;
-      const uint32_t x = valid ? mA[j] : 0u, px = valid && j > 0 ? mA[j - 1] : 0u;
+      const bool valid = j < mm;
+      const uint32_t x = valid ? mk[j] : 0u, px = valid && j > 0 ? mk[j - 1] : 0u;
       const bool st = valid && (j == 0 || (x >> IB) != (px >> IB));
       const uint64_t ball = __ballot(st);
-      if (st) s_start[nu + __popcll(ball & lt)] = j;
-      nu += __popcll(ball);
+      if (st) starts[cnt + __popcll(ball & lt)] = j;
+      cnt += __popcll(ball);
     }
-    if (lane == 0) s_start[nu] = m_a;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t* ow = out_words + img * out_stride;
-    double* ov = out_vals + img * out_stride;
-    for (int o = lane; o < nu; o += 64) {
-      const int s0 = s_start[o], s1 = s_start[o + 1];
-      const uint32_t x = mA[s0];
-      double v = wt[x & IMASK];  // insert(value_type(id, w)) of the first occurrence
-      if (tf)
-        for (int j = s0 + 1; j < s1; j++) v += wt[mA[j] & IMASK];  // addWeight, feature order
-      if (tf && !must) v /= (double)nu;  // TemplatedVocabulary.h:1165-1172
-      ow[o] = x >> IB;
-      if (must)
-        s_val[o] = v;
-      else
-        ov[o] = v;
+    if (lane == 0) {
+      starts[cnt] = mm;
+      if (wid == 0) s_nu = cnt;
+      else s_nn = cnt;
     }
-    if (lane == 0) out_n[img] = nu;
-    if (must) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      double norm = 0.0;
-      if (lane == 0) {  // BowVector::normalize: one ordered pass over the words
-        int o = 0;
-        if (l1) {
-          for (; o + 8 <= nu; o += 8) {
-            double v[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
-#pragma unroll
-            for (int j = 0; j < 8; j++) norm += fabs(v[j]);
-          }
-          for (; o < nu; o++) norm += fabs(s_val[o]);
-        } else {
-          // built -O3 -march=native (Thirdparty/DBoW2/CMakeLists.txt): `norm += v * v` contracts
-          for (; o + 8 <= nu; o += 8) {
-            double v[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
-#pragma unroll
-            for (int j = 0; j < 8; j++) norm = fma(v[j], v[j], norm);
-          }
-          for (; o < nu; o++) norm = fma(s_val[o], s_val[o], norm);
-          norm = sqrt(norm);
-        }
-      }
-      norm = __shfl(norm, 0);
-      for (int o = lane; o < nu; o += 64) ov[o] = norm > 0.0 ? s_val[o] / norm : s_val[o];
-    }
-  } else if (wid == 1) {  // FeatureVector CSR: node runs of the rank order
+  }
+  __syncthreads();
+  const int nu = s_nu, nn = s_nn;
+  // the whole workgroup: word weights summed in feature order (LDS), the CSR written out
+  uint32_t* ow = out_words + img * out_stride;
+  double* ov = out_vals + img * out_stride;
+  for (int o = tid; o < nu; o += 256) {
+    const int s0 = s_start[o], s1 = s_start[o + 1];
+    const uint32_t x = mA[s0];
+    double v = s_wt[x & IMASK];  // insert(value_type(id, w)) of the first occurrence
+    if (tf)
+      for (int j = s0 + 1; j < s1; j++) v += s_wt[mA[j] & IMASK];  // addWeight, feature order
+    if (tf && !must) v /= (double)nu;  // TemplatedVocabulary.h:1165-1172
+    ow[o] = x >> IB;
+    if (must)
+      s_val[o] = v;
+    else
+      ov[o] = v;
+  }
+  {
     uint32_t* oid = node_ids + (int64_t)img * nb;
     int* ooff = offsets + (int64_t)img * (nb + 1);
     int* of = feats + img * feats_stride;
-    int nn = 0;
-    for (int c0 = 0; c0 < m_b; c0 += 64) {
-      const int j = c0 + lane;
-      const bool valid = j < m_b;
-      const uint32_t x = valid ? mB[j] : 0u, px = valid && j > 0 ? mB[j - 1] : 0u;
-      const bool st = valid && (j == 0 || (x >> IB) != (px >> IB));
-      const uint64_t ball = __ballot(st);
-      if (st) {
-        const int q = nn + __popcll(ball & lt);
-        oid[q] = rank_ids[x >> IB];
-        ooff[q] = j;
-      }
-      if (valid) of[j] = (int)(x & IMASK);
-      nn += __popcll(ball);
+    for (int q = tid; q < nn; q += 256) {
+      const int j = s_nstart[q];
+      oid[q] = rank_ids[mB[j] >> IB];
+      ooff[q] = j;
     }
-    if (lane == 0) {
+    for (int j = tid; j < m_b; j += 256) of[j] = (int)(mB[j] & IMASK);
+    if (tid == 0) {
       ooff[nn] = m_b;
       n_nodes[img] = nn;
+      out_n[img] = nu;
     }
   }
+  if (!must) return;
+  __syncthreads();
+  if (tid == 0) {  // BowVector::normalize: one ordered pass over the words (LDS reads 8 ahead)
+    double norm = 0.0;
+    int o = 0;
+    if (l1) {
+      for (; o + 8 <= nu; o += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) norm += fabs(v[j]);
+      }
+      for (; o < nu; o++) norm += fabs(s_val[o]);
+    } else {
+      // built -O3 -march=native (Thirdparty/DBoW2/CMakeLists.txt): `norm += v * v` contracts
+      for (; o + 8 <= nu; o += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = s_val[o + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) norm = fma(v[j], v[j], norm);
+      }
+      for (; o < nu; o++) norm = fma(s_val[o], s_val[o], norm);
+      norm = sqrt(norm);
+    }
+    s_norm = norm;
+  }
+  __syncthreads();
+  const double norm = s_norm;
+  for (int o = tid; o < nu; o += 256) ov[o] = norm > 0.0 ? s_val[o] / norm : s_val[o];
 }
 
 template <int NPL>
@@ -638,7 +644,7 @@ static int launch_bowfv_t(int must, int l1, int tf, const uint32_t* d_word_of,
                           uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride,
                           int* d_nn, int nimg, hipStream_t s) {
   constexpr int CAP = 256 * NPL;
-  constexpr size_t smem = (size_t)CAP * 20 + 16;  // runs, merged orders, run starts
+  constexpr size_t smem = (size_t)CAP * 32 + 32;  // runs, merged orders, weights, run starts
   if constexpr (smem > 64 * 1024) {
     static std::once_flag once;
     static hipError_t attr = hipSuccess;
