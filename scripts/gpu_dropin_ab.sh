@@ -1,22 +1,16 @@
 #!/bin/bash
-# Drop-in A/B: parity tests of the per-call paths, then bench.py --dropin lines (1 / 4 / 8
-# threads, and 1 thread with extra environment per item).  Usage:
-#   bash scripts/gpu_dropin_ab.sh TAG [name:ENV=V,...]...
+# Drop-in A/B: the parity tests of the extraction paths with the defaults, then the one-thread
+# drop-in line under each setting of two environment switches, alternated.
+# Usage: bash scripts/gpu_dropin_ab.sh TAG VAR1 VAR2 [tests...]
 set -o pipefail
-T=${1:-dab}; shift
-O=gpurun_out/$T; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_extract_gpu.py tests/test_match_gpu.py tests/test_vocab_gpu.py tests/test_threads_gpu.py -m gpu -q -x \
-  --timeout 300 --timeout-method thread > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
-tail -1 $O/tests.txt
-run() {  # name threads [ENV=V...]
-  local n=$1 t=$2; shift 2
-  env "$@" timeout -k 10 200 python -u bench.py --dropin --threads $t --dropin-frames 300 > $O/$n.json 2> $O/$n.err || { tail -5 $O/$n.err; exit 2; }
-  python3 -c "import json,sys; d=json.load(open('$O/$n.json')); x=d['dropin']; print('$n', round(d['value']), x['median_ms'], x['per_call_median_ms'])"
-}
-run t1 1
-run t4 4
-run t8 8
-for item in "$@"; do
-  name=${item%%:*}; envs=${item#*:}
-  run $name 1 ${envs//,/ }
+T=$1; A=$2; B=$3; shift 3
+mkdir -p gpurun_out/$T
+timeout -k 10 500 python -u -m pytest ${@:-tests} -m gpu -q -x --timeout 240 --timeout-method thread \
+  > gpurun_out/$T/tests.txt 2>&1 || { tail -30 gpurun_out/$T/tests.txt; exit 1; }
+tail -1 gpurun_out/$T/tests.txt
+for rep in 1 2; do
+  for a in 1 0; do for b in 1 0; do
+    env $A=$a $B=$b timeout -k 10 200 python bench.py --dropin --threads 1 --dropin-frames 400 > gpurun_out/$T/d$a$b.json 2> gpurun_out/$T/d$a$b.err || exit 4
+    python -c "import json; d=json.load(open('gpurun_out/$T/d$a$b.json')); print('$A=$a $B=$b', d['value'], d['dropin']['median_ms'], d['dropin']['per_call_median_ms']['orbx_extract'])"
+  done; done
 done
