@@ -223,7 +223,7 @@ int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
   if (rc) return rc;
   pr.mark(s, st_csr);
   launch_fill_u32((uint32_t*)F->d_match, (size_t)n * kp, 0xFFFFFFFFu, s);
-  rc = launch_bow(F->d_bprob, n, F->nb, s);
+  rc = launch_bow(F->d_bprob, n, F->nb, s, false, kp / std::max(F->nb, 1));
   if (rc) return rc;
   pr.mark(s, st_bow);
   launch_fill_u32((uint32_t*)F->d_m12, (size_t)n * kp, 0xFFFFFFFFu, s);

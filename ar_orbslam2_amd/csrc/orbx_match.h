@@ -105,8 +105,11 @@ constexpr int kBowPosMask = kBowMaxSide2 - 1;
 
 // fused_finish: every problem's `done` counter is set and zeroed, and a call taking the
 // workgroup-per-node kernel runs the finish in its last workgroup instead of a second launch
+// feats_per_node: features per frame over vocabulary nodes (a hint: at kBowWideNode and above
+// the batched kernel keeps 4 candidate chunks in registers)
+constexpr int kBowWideNode = 32;
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
-               bool fused_finish = false);
+               bool fused_finish = false, int feats_per_node = 0);
 int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
                bool fused_finish = false);
 int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_counts, int n_fixed,

@@ -76,6 +76,7 @@ __device__ __forceinline__ bool last_workgroup(int* done);
 // ------------------------------------------------------------------ SearchByBoW
 // One wave per KF node a of problem pi (every lane of the wave active; the problem read through
 // the kernel's __restrict__ pointer, so its fields stay in scalar registers across the stores)
+template <int CH>
 __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ probs, const int pi,
                                               const int a, const int lane) {
   const BowProblem& P = probs[pi];
@@ -92,14 +93,14 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
   // l + 64c); larger nodes (no limit in the reference) keep them in memory: mode 0 reads the
   // output itself (match[i2] >= 0), mode 1 the zeroed matched2 flags.
   const bool big = m > kBowRegCands;
-  // the candidates of chunks 0 .. kBowDescChunks-1 (positions lane + 64 c) stay in registers
+  // the candidates of chunks 0 .. CH-1 (positions lane + 64 c) stay in registers
   // for the whole node: descriptor, index and validity (bit c of okr); later chunks of a larger
   // node are read from memory per KF feature
-  uint64_t reg[kBowDescChunks][4];
-  int i2r[kBowDescChunks];
+  uint64_t reg[CH][4];
+  int i2r[CH];
   uint32_t okr = 0;
 #pragma unroll
-  for (int c = 0; c < kBowDescChunks; c++) {
+  for (int c = 0; c < CH; c++) {
     const int jj = lane + 64 * c;
     reg[c][0] = reg[c][1] = reg[c][2] = reg[c][3] = 0;
     i2r[c] = -1;
@@ -116,9 +117,9 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
   // store inside the serial per-feature loop made the next feature wait for its completion):
   // mode 0 keeps the KF feature matched to candidate lane + 64 c in mval[c] of the candidate's
   // lane, mode 1 the candidate index matched to a prefetched KF feature in res_l of its lane
-  int mval[kBowDescChunks];
+  int mval[CH];
 #pragma unroll
-  for (int c = 0; c < kBowDescChunks; c++) mval[c] = -1;
+  for (int c = 0; c < CH; c++) mval[c] = -1;
   const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
   for (int c0 = a0; c0 < a1; c0 += 64) {
     // prefetch up to 64 KF features of the node (index, validity, descriptor) so the serial
@@ -155,7 +156,7 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
         }
       };
 #pragma unroll
-      for (int c = 0; c < kBowDescChunks; c++) {
+      for (int c = 0; c < CH; c++) {
         if (c * 64 >= m) break;  // wave-uniform
         const int jj = lane + 64 * c;
         if (!((okr >> c) & 1)) continue;
@@ -168,7 +169,7 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
         offer(__popcll(d1[0] ^ reg[c][0]) + __popcll(d1[1] ^ reg[c][1]) +
                   __popcll(d1[2] ^ reg[c][2]) + __popcll(d1[3] ^ reg[c][3]), jj);
       }
-      for (int c = kBowDescChunks; c * 64 < m; c++) {
+      for (int c = CH; c * 64 < m; c++) {
         const int jj = lane + 64 * c;
         if (jj >= m) continue;
         if (!big && ((matched >> c) & 1)) continue;
@@ -210,16 +211,16 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
           }
           // the flag store completes before the next feature's scan reads it
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-        } else if (cb < kBowDescChunks) {
+        } else if (cb < CH) {
           if (kfkf) {
             int i2c = i2r[0];
 #pragma unroll
-            for (int c = 1; c < kBowDescChunks; c++) i2c = cb == c ? i2r[c] : i2c;
+            for (int c = 1; c < CH; c++) i2c = cb == c ? i2r[c] : i2c;
             const int i2 = __builtin_amdgcn_readlane(i2c, lb);
             if (lane == j) res_l = i2;
           } else if (lane == lb) {
 #pragma unroll
-            for (int c = 0; c < kBowDescChunks; c++) mval[c] = cb == c ? i1 : mval[c];
+            for (int c = 0; c < CH; c++) mval[c] = cb == c ? i1 : mval[c];
           }
         } else if (lane == lb) {  // a candidate past the register chunks: stored now
           const int i2 = P.s2.node_feats[f0 + bp];
@@ -231,12 +232,16 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
     if (res_l >= 0) P.match[i1_l] = res_l;
   }
 #pragma unroll
-  for (int c = 0; c < kBowDescChunks; c++)
+  for (int c = 0; c < CH; c++)
     if (mval[c] >= 0) P.match[i2r[c]] = mval[c];
 }
 
+// CH candidate chunks of 64 in registers: kBowDescChunks (2), or 4 for frames whose vocabulary
+// nodes hold many features (C5's 4,000 per frame: 0.62 -> 0.52 ms per 256 frames; at C2's 1,000
+// the extra registers cost occupancy: 0.113 -> 0.138 ms)
+template <int CH>
 __global__ __launch_bounds__(256) void k_bow_nodes(const BowProblem* __restrict__ probs) {
-  bow_node_wave(probs, blockIdx.y, blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+  bow_node_wave<CH>(probs, blockIdx.y, blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
 }
 
 // Latency form of k_bow_nodes for calls with few problems (the per-frame drop-in call), where
@@ -310,7 +315,7 @@ __device__ __forceinline__ void bow_nodes_wg(const BowProblem* __restrict__ prob
   if (b < 0) return;  // workgroup-uniform
   const int f0 = P.s2.node_offsets[b], m = P.s2.node_offsets[b + 1] - f0;
   if (m > kBwgCands) {  // the wave form (no candidate limit)
-    if (wid == 0) bow_node_wave(probs, blockIdx.y, a, lane);
+    if (wid == 0) bow_node_wave<kBowDescChunks>(probs, blockIdx.y, a, lane);
     return;
   }
   const bool kfkf = P.mode == 1;
@@ -993,7 +998,7 @@ __global__ void k_distance(const uint8_t* a, const uint8_t* b, int n, int* out) 
 constexpr int kBowWgProbs = 4;
 
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
-               bool fused_finish) {
+               bool fused_finish, int feats_per_node) {
   if (nprob <= 0) return ORBX_OK;
   static const int wg_probs = [] {
     const char* e = getenv("ORBX_BOW_WG_PROBS");
@@ -1002,8 +1007,11 @@ int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t
   const bool wg = max_nodes1 > 0 && nprob <= wg_probs;
   if (wg)
     hipLaunchKernelGGL(k_bow_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
+  else if (max_nodes1 > 0 && feats_per_node >= kBowWideNode)
+    hipLaunchKernelGGL(k_bow_nodes<4>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
   else if (max_nodes1 > 0)
-    hipLaunchKernelGGL(k_bow_nodes, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
+    hipLaunchKernelGGL(k_bow_nodes<kBowDescChunks>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256),
+                       0, s, d_probs);
   if (!(wg && fused_finish))  // else the node kernel's last workgroup ran it
     hipLaunchKernelGGL(k_bow_finish, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();
