@@ -82,6 +82,25 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
   const BowProblem& P = probs[pi];
   if (a >= side_nodes(P.s1)) return;
   const uint32_t id = P.s1.node_ids[a];
+  // the KF node's first 64 features (index, validity, descriptor: one round of loads) are in
+  // flight during the frame node lookup
+  const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
+  int i1_l = -1;
+  bool ok_l = false;
+  uint64_t dl0 = 0, dl1 = 0, dl2 = 0, dl3 = 0;
+  auto load_kf = [&](int c0) {
+    const int my = c0 + lane;
+    i1_l = -1;
+    ok_l = false;
+    dl0 = dl1 = dl2 = dl3 = 0;
+    if (my < a1) {
+      i1_l = P.s1.node_feats[my];
+      ok_l = !P.s1.valid || P.s1.valid[i1_l];
+      const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1_l * 32);
+      dl0 = q[0]; dl1 = q[1]; dl2 = q[2]; dl3 = q[3];
+    }
+  };
+  load_kf(a0);
   const int nn2 = side_nodes(P.s2);
   const int b = wave_lower_bound(P.s2.node_ids, nn2, id, lane);
   if (b >= nn2 || P.s2.node_ids[b] != id) return;
@@ -120,22 +139,10 @@ __device__ __forceinline__ void bow_node_wave(const BowProblem* __restrict__ pro
   int mval[CH];
 #pragma unroll
   for (int c = 0; c < CH; c++) mval[c] = -1;
-  const int a0 = P.s1.node_offsets[a], a1 = P.s1.node_offsets[a + 1];
   for (int c0 = a0; c0 < a1; c0 += 64) {
-    // prefetch up to 64 KF features of the node (index, validity, descriptor) so the serial
-    // per-feature loop below only shuffles registers
-    const int my = c0 + lane;
-    int i1_l = -1;
-    bool ok_l = false;
-    uint64_t dl0 = 0, dl1 = 0, dl2 = 0, dl3 = 0;
-    if (my < a1) {
-      i1_l = P.s1.node_feats[my];
-      ok_l = !P.s1.valid || P.s1.valid[i1_l];
-      if (ok_l) {
-        const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1_l * 32);
-        dl0 = q[0]; dl1 = q[1]; dl2 = q[2]; dl3 = q[3];
-      }
-    }
+    // up to 64 KF features of the node (index, validity, descriptor) in registers, so the
+    // serial per-feature loop below only shuffles registers
+    if (c0 != a0) load_kf(c0);
     int res_l = -1;
     uint64_t okm = __ballot(ok_l);
     while (okm) {
@@ -606,11 +613,6 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
   const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (a >= tri_nodes(P.s1)) return;
-  const uint32_t id = P.s1.fv.node_ids[a];
-  const int nn2 = tri_nodes(P.s2);
-  const int b = wave_lower_bound(P.s2.fv.node_ids, nn2, id, lane);
-  if (b >= nn2 || P.s2.fv.node_ids[b] != id) return;
-  const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
   const int wv = threadIdx.x >> 6;
   // KF2 features are staged 64 at a time in this wave's LDS (descriptor, keypoint,
   // stereo/map-point flags); the KF1 features' best keys meet in LDS
@@ -618,44 +620,56 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
   __shared__ float s_x[4][64], s_y[4][64];
   __shared__ int s_i2[4][64], s_oct[4][64];
   __shared__ unsigned long long s_key[4][64];
-  for (int pa0 = P.s1.fv.node_offsets[a]; pa0 < P.s1.fv.node_offsets[a + 1]; pa0 += 64) {
-    const int n1 = min(64, P.s1.fv.node_offsets[a + 1] - pa0);
-    const int G = 64 / n1;                        // lanes per KF1 feature (wave-uniform)
-    const int u = lane % n1, g = lane / n1;       // this lane: feature u, every G-th candidate from g
-    bool live = g < G;
-    int i1 = P.s1.fv.node_feats[pa0 + u];
-    bool st1 = false;
-    if (live) {
-      if (P.s1.has_mp && P.s1.has_mp[i1]) live = false;
-      st1 = P.s1.u_right ? P.s1.u_right[i1] >= 0 : false;
-      if (P.only_stereo && !st1) live = false;
-    }
-    orbx_keypoint kp1{};
-    uint64_t d1[4] = {0, 0, 0, 0};
-    if (live) {
-      kp1 = P.s1.keys_un[i1];
-      const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
-      d1[0] = q[0]; d1[1] = q[1]; d1[2] = q[2]; d1[3] = q[3];
-    }
+  const int a0 = P.s1.fv.node_offsets[a], a1 = P.s1.fv.node_offsets[a + 1];
+  // a KF1 chunk: this lane's feature u (every G-th candidate from g), its flags, keypoint and
+  // descriptor in one round of loads (all depend on the feature index only)
+  int n1, G, u, g, i1;
+  bool live, st1;
+  orbx_keypoint kp1;
+  uint64_t d1[4];
+  auto load_kf1 = [&](int pa0) {
+    n1 = min(64, a1 - pa0);
+    G = 64 / n1;  // lanes per KF1 feature (wave-uniform)
+    u = lane % n1;
+    g = lane / n1;
+    i1 = P.s1.fv.node_feats[pa0 + u];
+    const bool hm = P.s1.has_mp && P.s1.has_mp[i1];
+    st1 = P.s1.u_right ? P.s1.u_right[i1] >= 0 : false;
+    kp1 = P.s1.keys_un[i1];
+    const uint64_t* q = (const uint64_t*)(P.s1.desc + (int64_t)i1 * 32);
+    d1[0] = q[0]; d1[1] = q[1]; d1[2] = q[2]; d1[3] = q[3];
+    live = g < G && !hm && !(P.only_stereo && !st1);
+  };
+  if (a0 < a1) load_kf1(a0);  // in flight during the KF2 node lookup
+  const uint32_t id = P.s1.fv.node_ids[a];
+  const int nn2 = tri_nodes(P.s2);
+  const int b = wave_lower_bound(P.s2.fv.node_ids, nn2, id, lane);
+  if (b >= nn2 || P.s2.fv.node_ids[b] != id) return;
+  const int f0 = P.s2.fv.node_offsets[b], f1 = P.s2.fv.node_offsets[b + 1];
+  for (int pa0 = a0; pa0 < a1; pa0 += 64) {
+    if (pa0 != a0) load_kf1(pa0);
     s_key[wv][lane] = ~0ull;
     unsigned long long best = ~0ull;
     for (int pb0 = f0; pb0 < f1; pb0 += 64) {
       const int nb = min(64, f1 - pb0);
-      {  // stage chunk: entry skipped (i2 = -1) when it has a map point or fails only_stereo
+      {  // stage chunk: entry skipped (i2 = -1) when it has a map point or fails only_stereo;
+         // the flags, descriptor and keypoint load together
         int i2 = -1;
         if (lane < nb) {
           i2 = P.s2.fv.node_feats[pb0 + lane];
           const bool st2 = P.s2.u_right ? P.s2.u_right[i2] >= 0 : false;
+          const bool hm2 = P.s2.has_mp && P.s2.has_mp[i2];
+          const uint64_t* q = (const uint64_t*)(P.s2.desc + (int64_t)i2 * 32);
+          const uint64_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+          const orbx_keypoint kp2 = P.s2.keys_un[i2];
           // `vbMatched2[idx2] || pMP2` (:728): vbMatched2 is never set in this function
-          if ((P.s2.has_mp && P.s2.has_mp[i2]) || (P.only_stereo && !st2)) {
+          if (hm2 || (P.only_stereo && !st2)) {
             i2 = -1;
           } else {
-            const uint64_t* q = (const uint64_t*)(P.s2.desc + (int64_t)i2 * 32);
-            s_d[wv][lane][0] = q[0];
-            s_d[wv][lane][1] = q[1];
-            s_d[wv][lane][2] = q[2];
-            s_d[wv][lane][3] = q[3];
-            const orbx_keypoint kp2 = P.s2.keys_un[i2];
+            s_d[wv][lane][0] = q0;
+            s_d[wv][lane][1] = q1;
+            s_d[wv][lane][2] = q2;
+            s_d[wv][lane][3] = q3;
             s_x[wv][lane] = kp2.x;
             s_y[wv][lane] = kp2.y;
             s_oct[wv][lane] = kp2.octave | (st2 ? 0x10000 : 0);
