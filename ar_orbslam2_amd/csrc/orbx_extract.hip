@@ -147,6 +147,9 @@ __device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
 }
 
 // ------------------------------------------------------------------ k_pyramid
+#ifndef ORBX_PY_LOADS
+#define ORBX_PY_LOADS 4  // 16-B source chunks per thread in flight while a band is staged
+#endif
 // ComputePyramid (ORBextractor.cc:1047-1072) in a few launches (Geometry::pyr_stages): the first
 // copies level 0 into the 64-B pitched pyramid block (every later kernel reads aligned dwords)
 // and builds levels 1..3, the next ones build four levels each from the last level stored.
@@ -239,20 +242,20 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
     if ((w & 15) == 0) {  // 16-byte chunks, four per thread in flight
       const int nch = w >> 4, items = nr * nch;
       const float inv = 1.0f / (float)nch;
-      for (int i0 = tid; i0 < items; i0 += 4 * kPyNT) {
+      for (int i0 = tid; i0 < items; i0 += ORBX_PY_LOADS * kPyNT) {
         // past the end a thread repeats the last chunk: identical bytes to identical places
-        uint4 v[4];
-        int rr[4], cc[4];
+        uint4 v[ORBX_PY_LOADS];
+        int rr[ORBX_PY_LOADS], cc[ORBX_PY_LOADS];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < ORBX_PY_LOADS; u++) {
           py_divmod(min(i0 + kPyNT * u, items - 1), nch, inv, rr[u], cc[u]);
           v[u] = *(const uint4*)(src + (int64_t)(lo + rr[u]) * w + 16 * cc[u]);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++)  // pin the loads here: all four in flight together
+        for (int u = 0; u < ORBX_PY_LOADS; u++)  // pin the loads here: all four in flight together
           asm volatile("" : "+v"(v[u].x), "+v"(v[u].y), "+v"(v[u].z), "+v"(v[u].w));
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < ORBX_PY_LOADS; u++) {
           const int y = lo + rr[u];
           *(uint4*)(sdst + __mul24(rr[u], pitch) + 16 * cc[u]) = v[u];
           if (y >= own_lo && y < own_hi) *(uint4*)(dst + (uint32_t)__mul24(y, pitch) + 16 * cc[u]) = v[u];
