@@ -46,15 +46,16 @@ CLOCK_GHZ = 2.4           # MI355X peak engine clock
 CONFIGS = {
     # batch: frames per step per camera stream (C2: 3 x 512 measured 225.5k vs 3 x 256 222.3k
     # frames/s, three alternating runs each on one box; C3 / C4: 512 vs 256 107.6-108.1k vs
-    # 106.4-106.6k and 71.0-71.3k vs 70.8-71.0k, two runs each (scripts/gpu_batch_ab.sh); C5 keeps
-    # 256, the shape of its 8-stream timed-topology parity test; AR below)
+    # 106.4-106.6k and 71.0-71.3k vs 70.8-71.0k, C5 44.2-44.5k vs 43.7-44.0k, two runs each
+    # (scripts/gpu_batch_ab.sh); AR below)
     "C2": dict(w=640, h=480, nfeatures=1000, batch=512,
                workload="TUM fr1/xyz mono 640x480, 1000 features, 1xMI355X HIP extract+match"),
     "C3": dict(w=752, h=480, nfeatures=1200, stereo=(47.90639384423901, 435.2046959714599), batch=512,
                workload="EuRoC MH01 stereo geometry 2x752x480, 1200 features, stereo matching"),
     "C4": dict(w=1241, h=376, nfeatures=2000, stereo=(386.1448, 718.856), batch=512,
                workload="KITTI 00 stereo geometry 2x1241x376, 2000 features, stereo matching"),
-    "C5": dict(w=1920, h=1080, nfeatures=4000, workload="synthetic 1920x1080, 4000 features"),
+    "C5": dict(w=1920, h=1080, nfeatures=4000, batch=512,
+               workload="synthetic 1920x1080, 4000 features"),
     # the AR marker path (Marker::Match: cv::ORB 2.4 HARRIS 500 features on
     # the frame, BruteForceMatcher<HammingLUT> against the target's descriptors, good filter)
     # AR: 512 vs 256 frames per batch 282.8-283.1k vs 272.0-275.0k frames/s, two runs each

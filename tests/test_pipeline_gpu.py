@@ -289,7 +289,7 @@ def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc):
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("config,argv", [
     ("C2", []),                                                  # 3 streams x 512, pool 4
-    ("C5", ["--streams-total", "8", "--pool", "2"]),             # 8 streams x 256 on one GPU
+    ("C5", ["--streams-total", "8", "--pool", "2", "--batch", "256"]),  # 8 streams x 256, one GPU
 ])
 def test_bench_timed_topology_matches_oracle(config, argv):
     """bench.py's timed configuration, built by bench's own make_frame_pipes / replay_step: the
