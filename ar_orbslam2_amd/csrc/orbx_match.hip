@@ -1018,10 +1018,14 @@ int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t
     const char* e = getenv("ORBX_BOW_WG_PROBS");
     return e ? atoi(e) : kBowWgProbs;
   }();
+  static const int wide_node = [] {  // ORBX_BOW_WIDE_NODE overrides kBowWideNode (experiments)
+    const char* e = getenv("ORBX_BOW_WIDE_NODE");
+    return e ? atoi(e) : kBowWideNode;
+  }();
   const bool wg = max_nodes1 > 0 && nprob <= wg_probs;
   if (wg)
     hipLaunchKernelGGL(k_bow_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
-  else if (max_nodes1 > 0 && feats_per_node >= kBowWideNode)
+  else if (max_nodes1 > 0 && feats_per_node >= wide_node)
     hipLaunchKernelGGL(k_bow_nodes<4>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
   else if (max_nodes1 > 0)
     hipLaunchKernelGGL(k_bow_nodes<kBowDescChunks>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256),
