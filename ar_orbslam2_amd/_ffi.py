@@ -111,7 +111,7 @@ class FusePoints(C.Structure):
 class ProjLast(C.Structure):
     _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
                 ("ur", C.c_void_p), ("octave", C.c_void_p), ("angle", C.c_void_p),
-                ("desc", C.c_void_p)]
+                ("desc", C.c_void_p), ("blocks", C.c_void_p)]
 
 
 _lib = None

@@ -76,6 +76,8 @@ struct ProjPointsDev {
   const uint8_t* desc;
   float th, nnratio;
   int forward, backward, check_ori;
+  const uint8_t* blocks;  // mode 1: the point has observations, its feature blocks later points
+  int2* log;              // modes 1 / 3 with check_ori: (feature, bin) of every assignment
 };
 
 __global__ __launch_bounds__(256) void k_grid_cells(ProjFrameDev F, uint32_t* __restrict__ cell) {
@@ -311,13 +313,16 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjFrameDev F, ProjPointsD
     }
     if (lane == 0) {
       match[best.x] = p;
-      s_claim[best.x >> 5] |= 1u << (best.x & 31);
+      // a point without observations leaves its feature open to later points, which may take
+      // it over (ORBmatcher.cc:1406-1408)
+      if (!P.blocks || P.blocks[p]) s_claim[best.x >> 5] |= 1u << (best.x & 31);
       if ((P.mode == 1 || P.mode == 3) && P.check_ori) {
         float rot = P.angle[p] - F.keys[best.x].angle;
         if (rot < 0.0) rot += 360.0f;
         int bin = (int)roundf(rot * factor);
         if (bin == kHisto) bin = 0;
         s_hist[bin]++;
+        P.log[nm] = make_int2(best.x, bin);  // rotHist[bin].push_back(bestIdx2)
       }
     }
     nm++;
@@ -341,16 +346,13 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjFrameDev F, ProjPointsD
     }
     if (max2 < 0.1f * (float)max1) ind2 = ind3 = -1;
     else if (max3 < 0.1f * (float)max1) ind3 = -1;
+    // every pushed entry of a bin outside the three maxima: its feature loses its point and
+    // nmatches drops by one per entry (:1459-1468; a feature taken over twice has two entries)
     int removed = 0;
-    for (int i = lane; i < F.n; i += 64) {
-      const int p = match[i];
-      if (p < 0) continue;
-      float rot = P.angle[p] - F.keys[i].angle;
-      if (rot < 0.0) rot += 360.0f;
-      int bin = (int)roundf(rot * factor);
-      if (bin == kHisto) bin = 0;
-      if (bin != ind1 && bin != ind2 && bin != ind3) {
-        match[i] = -1;
+    for (int k = lane; k < nm; k += 64) {
+      const int2 e = P.log[k];
+      if (e.y != ind1 && e.y != ind2 && e.y != ind3) {
+        match[e.x] = -1;
         removed++;
       }
     }
@@ -725,7 +727,7 @@ int run_projection(const orbx_proj_frame* f, ProjPointsDev P, const std::vector<
     const size_t olists = st.add(nullptr, sizeof(int4) * pool_cap),
                  obases = st.add(nullptr, 4 * (size_t)np), ocnt = st.add(nullptr, 4 * (size_t)np),
                  oused = st.add(nullptr, 16), omatch = st.add(nullptr, 4 * (size_t)std::max(n, np)),
-                 onm = st.add(nullptr, 4);
+                 onm = st.add(nullptr, 4), olog = st.add(nullptr, 8 * (size_t)np);
     // SearchForInitialization state: in LDS when it fits one workgroup, else global scratch
     const size_t init_words = ic ? (size_t)f->n + 2 * (size_t)ic->n1 : 0;
     const bool init_lds = init_words * 4 <= 150 * 1024;
@@ -749,6 +751,8 @@ int run_projection(const orbx_proj_frame* f, ProjPointsDev P, const std::vector<
     Q.view_cos = src[5] ? dptr<float>(base, offs[5]) : nullptr;
     Q.angle = src[6] ? dptr<float>(base, offs[6]) : nullptr;
     Q.desc = dptr<uint8_t>(base, offs[7]);
+    Q.blocks = src.size() > 10 && src[10] ? dptr<uint8_t>(base, offs[10]) : nullptr;
+    Q.log = dptr<int2>(base, olog);
     if (P.n > 0)
       hipLaunchKernelGGL(k_proj_cand, dim3((P.n + 3) / 4), dim3(256), 0, s, F, Q,
                          dptr<int4>(base, olists), dptr<int>(base, obases), dptr<int>(base, ocnt),
@@ -964,8 +968,11 @@ int orbx_search_by_projection_last(const orbx_proj_frame* f, const orbx_proj_las
   P.backward = backward;
   P.check_ori = check_ori;
   const size_t n = (size_t)l->n;
-  return run_projection(f, P, {l->valid, l->u, l->v, l->ur, l->octave, nullptr, l->angle, l->desc},
-                        {n, 4 * n, 4 * n, 4 * n, 4 * n, 0, 4 * n, 32 * n}, match, nmatches);
+  return run_projection(f, P,
+                        {l->valid, l->u, l->v, l->ur, l->octave, nullptr, l->angle, l->desc,
+                         nullptr, nullptr, l->blocks},
+                        {n, 4 * n, 4 * n, 4 * n, 4 * n, 0, 4 * n, 32 * n, 0, 0, n}, match,
+                        nmatches);
 }
 
 int orbx_search_for_initialization(const orbx_proj_frame* f1, const orbx_proj_frame* f2,

@@ -138,7 +138,8 @@ class ORBmatcher:
         points with `proj_x` — local-map points (SearchByProjection(F, vpMapPoints, th)):
            track, proj_x, proj_y, proj_xr, pred_level, view_cos, desc.
         points with `u` — the last frame (SearchByProjection(CurrentFrame, LastFrame, th,
-           bMono)): valid, u, v, ur, octave, angle, desc; forward / backward are bForward /
+           bMono)): valid, u, v, ur, octave, angle, desc and optionally blocks
+           (pMP->Observations() > 0; absent = all); forward / backward are bForward /
            bBackward (both False when bMono).
         Returns (nmatches, match) with match[f] = point / last-frame index or -1."""
         fr, keep = _proj_frame(F)
@@ -159,7 +160,8 @@ class ORBmatcher:
                 forward = backward = False
             p, pk = _proj_struct(points, _ffi.ProjLast, [
                 ("valid", np.uint8), ("u", np.float32), ("v", np.float32), ("ur", np.float32),
-                ("octave", np.int32), ("angle", np.float32), ("desc", np.uint8)])
+                ("octave", np.int32), ("angle", np.float32), ("desc", np.uint8),
+                ("blocks", np.uint8)])
             check("orbx_search_by_projection_last",
                   lib().orbx_search_by_projection_last(C.byref(fr), C.byref(p), C.c_float(th),
                                                        C.c_int32(int(forward)),

@@ -795,6 +795,52 @@ def make_frame_pipes(args, cfg, streams, local):
     return pipes, pools, pools_host
 
 
+def _d2h(ptr, nbytes):
+    """Device bytes at `ptr` (a pipeline output) to a host u8 array (hipMemcpy D2H)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = np.zeros(nbytes, np.uint8)
+    rc = hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr),
+                       ctypes.c_size_t(nbytes), 2)
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy D2H failed ({rc})")
+    return out
+
+
+def dump_verify_frames(out_dir, rank, stream_id, pipe, batch, B, stereo):
+    """--verify-frames: this rank's first camera stream, the batch its last timed step ran —
+    frames {0, B-1} with their keyframes {B-1, B-2} (frame f is matched against (f - 1) mod B):
+    input images, keypoints, descriptors, (stereo) mvuRight / mvDepth, SearchByBoW matches,
+    SearchForTriangulation pairs and the masks, to out_dir/rank{rank}.npz.  Every rank's outputs
+    can then be checked against the oracle (tests/test_distributed_gpu.py), not only rank 0's
+    counts."""
+    from ar_orbslam2_amd import KEYPOINT_DTYPE
+    pipe.sync()
+    cap = pipe.kp_cap
+    ni = 2 * B if stereo else B
+    counts, bow, tri, err = pipe.results(B)
+    out = pipe.device_outputs()
+    ids = [B - 2, B - 1, 0]
+    imgs = batch.cpu().numpy()
+    img_rows = [j for f in ids for j in ((2 * f, 2 * f + 1) if stereo else (f,))]
+    kps = _d2h(out["kps"], ni * cap * 28).view(KEYPOINT_DTYPE).reshape(ni, cap)
+    desc = _d2h(out["desc"], ni * cap * 32).reshape(ni, cap, 32)
+    match = _d2h(out["bow_match"], B * cap * 4).view(np.int32).reshape(B, cap)
+    pairs = _d2h(out["tri_pairs"], B * cap * 8).view(np.int32).reshape(B, cap, 2)
+    valid, has_mp = pipe.masks
+    d = dict(rank=rank, stream=stream_id, batch=B, stereo=int(stereo), frame_ids=np.array(ids),
+             err=err, counts=counts[ids], images=imgs[img_rows], kps=kps[img_rows],
+             desc=desc[img_rows], bow=bow[[0, B - 1]], match=match[[0, B - 1]],
+             tri=tri[[0, B - 1]], pairs=pairs[[0, B - 1]], valid=valid[ids], has_mp=has_mp[ids],
+             epipole=np.array(pipe.epipole, np.float32))
+    if stereo:
+        so = pipe.stereo_outputs()
+        d["uright"] = _d2h(so["uright"], B * cap * 4).view(np.float32).reshape(B, cap)[ids]
+        d["depth"] = _d2h(so["depth"], B * cap * 4).view(np.float32).reshape(B, cap)[ids]
+    os.makedirs(out_dir, exist_ok=True)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **d)
+
+
 def replay_step(pipes, pools, B, i):
     """One step of the timed region: every camera stream enqueues batch i mod pool (its
     captured hipGraph for that input, replayed asynchronously on the pipeline's stream)."""
@@ -841,6 +887,9 @@ def run_frames(args, cfg, rank, world, local, streams, dist):
     for si, p in enumerate(pipes):
         if p.results(B)[3]:
             raise RuntimeError(f"camera stream {streams[si]}: device error {p.results(B)[3]}")
+    if args.verify_frames:
+        dump_verify_frames(args.verify_frames, rank, streams[0], pipes[0],
+                           pools[0][(args.steps - 1) % len(pools[0])], B, bool(stereo))
     # roofline pass (after timing): stream 0 alone with HIP events around every kernel on the
     # stream it launches on, so a kernel's event interval is its own duration (as rocprofv3
     # reports it) rather than a share of the concurrent streams
@@ -941,7 +990,7 @@ def run_dropin(args, cfg, rank, world, local):
         desc.astype(np.uint8).tofile(os.path.join(td, "voc_desc.u8"))
         weight.astype(np.float64).tofile(os.path.join(td, "voc_weight.f64"))
         cmd = [exe, td, str(w), str(h), str(nf), str(n_img), str(args.threads),
-               str(args.warmup_frames), str(args.dropin_frames), str(local)]
+               str(args.warmup_frames), str(args.dropin_frames), str(local), args.dropin_mode]
         if keep:  # inputs kept for a profiler run of the driver itself
             with open(os.path.join(keep, "cmd.txt"), "w") as f:
                 f.write(" ".join(cmd[1:]) + "\n")
@@ -954,8 +1003,12 @@ def run_dropin(args, cfg, rank, world, local):
         "unit": "frames/s", "n_gpus": 1, "steps": d["frames"], "warmup": args.warmup_frames,
         "ms_per_step": d["mean_ms"], "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": cfg["workload"] + ", drop-in C ABI one frame per call",
-                   "host_threads": args.threads, "image": f"{w}x{h}", "nfeatures": nf},
+        "config": {"workload": cfg["workload"] + (", drop-in C ABI one frame per call"
+                                                  if args.dropin_mode == "capi" else
+                                                  ", drop-in through the reference-side shims' "
+                                                  "per-call marshalling, one frame per call"),
+                   "host_threads": args.threads, "image": f"{w}x{h}", "nfeatures": nf,
+                   "dropin_mode": args.dropin_mode},
         "dropin": d,
     }
 
@@ -988,11 +1041,19 @@ def parse_args(argv=None):
     ap.add_argument("--no-upload", dest="upload", action="store_false")
     ap.add_argument("--dropin", action="store_true",
                     help="measure the drop-in per-frame path (host images, one frame per call)")
+    ap.add_argument("--dropin-mode", default="capi", choices=["capi", "shim"],
+                    help="--dropin: call the C ABI directly (capi) or replay the reference-side "
+                         "shims' per-call marshalling around it (shim: std::map BoW / "
+                         "FeatureVector, MapPoint masks, per-call buffers; include/compat)")
     ap.add_argument("--threads", type=int, default=4, help="--dropin host threads (cameras)")
     ap.add_argument("--dropin-frames", type=int, default=500, help="--dropin frames per thread")
     ap.add_argument("--warmup-frames", type=int, default=20, help="--dropin warm-up per thread")
     ap.add_argument("--dropin-dir", default=None,
                     help="--dropin: keep the driver's inputs (and its arguments in cmd.txt) here")
+    ap.add_argument("--verify-frames", default=None, metavar="DIR",
+                    help="after the timed region, every rank dumps frames {0, B-1} of its first "
+                         "camera stream (inputs, keypoints, descriptors, matches) to "
+                         "DIR/rank<r>.npz for an oracle check of that rank's outputs")
     ap.add_argument("--pmc-dir", default=None,
                     help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ CSVs of this bench command, "
                          "used for roofline.traffic and the VALU-issue floor")

@@ -2,6 +2,7 @@
 // Frame::ComputeBoW / KeyFrame::ComputeBoW (TemplatedVocabulary::transform, levelsup 4) and
 // Frame::ComputeStereoMatches.  Each returns false instead of failing, and the reference's body
 // runs then, so the callers' results are the reference's either way.
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -11,19 +12,24 @@
 namespace ORB_SLAM2 {
 
 namespace {
+// The device vocabulary is shared: a transform running in one thread keeps the vocabulary it
+// started with alive while another thread loads a new one (the last holder destroys it).
 std::mutex g_voc_mutex;
-orbx_vocabulary* g_voc = nullptr;
+std::shared_ptr<orbx_vocabulary> g_voc;
 }  // namespace
 
 bool orbx_load_vocabulary(const std::string& path) {
+  orbx_vocabulary* v = nullptr;
+  const bool ok = orbx_vocabulary_load_text(path.c_str(), /*hip_device*/ 0, &v) == ORBX_OK;
+  std::shared_ptr<orbx_vocabulary> nv;
+  if (ok) nv.reset(v, orbx_vocabulary_destroy);
   std::lock_guard<std::mutex> lock(g_voc_mutex);
-  if (g_voc) orbx_vocabulary_destroy(g_voc);
-  g_voc = nullptr;
-  return orbx_vocabulary_load_text(path.c_str(), /*hip_device*/ 0, &g_voc) == ORBX_OK;
+  g_voc = nv;
+  return ok;
 }
 
 bool orbx_compute_bow(const cv::Mat& descriptors, DBoW2::BowVector& bow, DBoW2::FeatureVector& fv) {
-  orbx_vocabulary* voc;
+  std::shared_ptr<orbx_vocabulary> voc;
   {
     std::lock_guard<std::mutex> lock(g_voc_mutex);
     voc = g_voc;
@@ -35,7 +41,7 @@ bool orbx_compute_bow(const cv::Mat& descriptors, DBoW2::BowVector& bow, DBoW2::
   std::vector<double> bv(m);
   std::vector<int32_t> fo(m + 2), ff(m);
   int32_t nb = 0, nf = 0;
-  if (orbx_vocabulary_transform(voc, descriptors.data, n, 4, nullptr, nullptr, bw.data(), bv.data(),
+  if (orbx_vocabulary_transform(voc.get(), descriptors.data, n, 4, nullptr, nullptr, bw.data(), bv.data(),
                                 &nb, fi.data(), fo.data(), ff.data(), &nf) != ORBX_OK)
     return false;
   bow.clear();
@@ -50,11 +56,20 @@ bool orbx_compute_bow(const cv::Mat& descriptors, DBoW2::BowVector& bow, DBoW2::
 bool orbx_compute_stereo_matches(Frame& F) {
   orbx_extractor* l = orbx_context_of(F.mpORBextractorLeft);
   orbx_extractor* r = orbx_context_of(F.mpORBextractorRight);
-  if (!l || !r) return false;  // no device extraction to match on
+  if (!l || !r) {
+    // an extraction served by the host: the reference's body runs on mvImagePyramid, which the
+    // device extraction (if any) exports now
+    orbx_materialize_pyramid(F.mpORBextractorLeft);
+    orbx_materialize_pyramid(F.mpORBextractorRight);
+    return false;
+  }
   std::vector<float> ur(std::max(F.N, 1)), depth(std::max(F.N, 1));
   int32_t n = 0;
-  if (orbx_stereo_matches(l, r, F.mb, F.mbf, ur.data(), depth.data(), &n) != ORBX_OK || n != F.N)
+  if (orbx_stereo_matches(l, r, F.mb, F.mbf, ur.data(), depth.data(), &n) != ORBX_OK || n != F.N) {
+    orbx_materialize_pyramid(F.mpORBextractorLeft);  // the host body reads mvImagePyramid
+    orbx_materialize_pyramid(F.mpORBextractorRight);
     return false;
+  }
   F.mvuRight.assign(ur.begin(), ur.begin() + F.N);
   F.mvDepth.assign(depth.begin(), depth.begin() + F.N);
   return true;

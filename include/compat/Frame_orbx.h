@@ -36,5 +36,11 @@ bool orbx_compute_stereo_matches(Frame& F);
 
 // ORBextractor_orbx.cc: the device context of an extractor whose last call ran on the GPU
 ::orbx_extractor* orbx_context_of(const ORBextractor* self);
+// ORBextractor_orbx.cc: mvImagePyramid (ORBextractor.h:88) is exported from HBM lazily — its
+// only reader, Frame::ComputeStereoMatches, runs on the device (orbx_compute_stereo_matches).
+// This copies the last device extraction's levels into mvImagePyramid; it is a no-op when they
+// are already there (or the last call ran on the host, which fills them itself).  Returns false
+// on a device error.  Code reading mvImagePyramid elsewhere calls it first.
+bool orbx_materialize_pyramid(ORBextractor* self);
 
 }  // namespace ORB_SLAM2

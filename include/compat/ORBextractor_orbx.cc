@@ -9,11 +9,14 @@
 //
 // Behaviour per ORBextractor.cc:985-1045: an empty image leaves the outputs untouched; keypoints
 // (cv::KeyPoint == orbx_keypoint, 28 B) and descriptors bit-exact with the reference (the
-// library's parity tests); mvImagePyramid holds the levels of the last call.  On a device error
-// the call is served by the reference's own code (ORBextractorHost), once logged.
+// library's parity tests); mvImagePyramid is exported from HBM on demand
+// (orbx_materialize_pyramid, Frame_orbx.h: its only reader, Frame::ComputeStereoMatches, runs on
+// the device).  On a device error the call is served by the reference's own code
+// (ORBextractorHost), once logged.
 #include <cstdio>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "ORBextractor.h"
 #include "Frame_orbx.h"
@@ -30,7 +33,9 @@ struct ExtractorCtx {
   orbx_extractor* ex = nullptr;
   orbx_params p{};
   ORBextractorHost* host = nullptr;  // built on the first fallback
+  bool create_failed = false;        // no device context: every call goes to the host
   bool last_on_device = false;       // the last call's results are resident on the GPU
+  bool pyramid_exported = false;     // mvImagePyramid holds the last device call's levels
 };
 
 std::mutex g_mutex;
@@ -53,9 +58,13 @@ ExtractorCtx& ctx_of(const ORBextractor* self, const orbx_params& p) {
     delete c.host;
     c = ExtractorCtx{};
   }
-  if (!c.ex) {
+  if (c.create_failed && !same_params(c.p, p)) c = ExtractorCtx{};
+  if (!c.ex && !c.create_failed) {  // one attempt per (object, parameters), not one per frame
     c.p = p;
-    if (orbx_extractor_create(&p, /*hip_device*/ 0, &c.ex) != ORBX_OK) c.ex = nullptr;
+    if (orbx_extractor_create(&p, /*hip_device*/ 0, &c.ex) != ORBX_OK) {
+      c.ex = nullptr;
+      c.create_failed = true;
+    }
   }
   return c;
 }
@@ -65,6 +74,19 @@ void log_once(const char* what, int rc) {
   std::call_once(f, [&] {
     fprintf(stderr, "[orbx] %s failed (%d): falling back to the host ORBextractor\n", what, rc);
   });
+}
+
+// mvImagePyramid from the device: level sizes, then one download per level
+int export_pyramid(orbx_extractor* ex, int nlevels, std::vector<cv::Mat>& pyr) {
+  int rc = ORBX_OK;
+  for (int l = 0; l < nlevels && rc == ORBX_OK; ++l) {
+    int32_t w = 0, h = 0;
+    rc = orbx_extractor_pyramid(ex, l, nullptr, 0, &w, &h);
+    if (rc != ORBX_OK) break;
+    pyr[l].create(h, w, CV_8U);
+    rc = orbx_extractor_pyramid(ex, l, pyr[l].data, (int64_t)pyr[l].step, &w, &h);
+  }
+  return rc;
 }
 
 }  // namespace
@@ -129,19 +151,11 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask,
         cv::Mat out = _descriptors.getMat();
         d.rowRange(0, n).copyTo(out);
       }
-      // mvImagePyramid (ORBextractor.h:88): read by Frame::ComputeStereoMatches only
-      for (int l = 0; l < nlevels && rc == ORBX_OK; ++l) {
-        int32_t w = 0, h = 0;
-        rc = orbx_extractor_pyramid(c.ex, l, nullptr, 0, &w, &h);
-        if (rc != ORBX_OK) break;
-        mvImagePyramid[l].create(h, w, CV_8U);
-        rc = orbx_extractor_pyramid(c.ex, l, mvImagePyramid[l].data,
-                                    (int64_t)mvImagePyramid[l].step, &w, &h);
-      }
-      if (rc == ORBX_OK) {
-        c.last_on_device = true;
-        return;
-      }
+      // mvImagePyramid (ORBextractor.h:88) is read by Frame::ComputeStereoMatches only, which
+      // runs on the device: it is exported on demand (orbx_materialize_pyramid), not per call
+      c.last_on_device = true;
+      c.pyramid_exported = false;
+      return;
     }
   }
   c.last_on_device = false;
@@ -165,6 +179,27 @@ orbx_extractor* orbx_context_of(const ORBextractor* self) {
   std::lock_guard<std::mutex> lock(g_mutex);
   auto it = g_ctx.find(self);
   return it == g_ctx.end() || !it->second.last_on_device ? nullptr : it->second.ex;
+}
+
+bool orbx_materialize_pyramid(ORBextractor* self) {
+  if (!self) return false;
+  orbx_extractor* ex;
+  {
+    std::lock_guard<std::mutex> lock(g_mutex);
+    auto it = g_ctx.find(self);
+    if (it == g_ctx.end() || !it->second.last_on_device || it->second.pyramid_exported)
+      return true;  // host-served call (levels already there) or already exported
+    ex = it->second.ex;
+  }
+  // the extractor is not reentrant (ORBextractor.h), so its owner's thread is the only writer
+  const int rc = export_pyramid(ex, self->GetLevels(), self->mvImagePyramid);
+  if (rc != ORBX_OK) {
+    log_once("orbx_extractor_pyramid", rc);
+    return false;
+  }
+  std::lock_guard<std::mutex> lock(g_mutex);
+  g_ctx[self].pyramid_exported = true;
+  return true;
 }
 
 }  // namespace ORB_SLAM2

@@ -15,7 +15,9 @@
 // once (System.cc:90-95); the library keeps a stream and workspace per thread.
 #include <cmath>
 #include <cstdio>
+#include <map>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "KeyFrame.h"
@@ -32,11 +34,18 @@ const int ORBmatcher::HISTO_LENGTH = 30;
 
 namespace {
 
+// One message per entry point (the first fallback of each search is logged, not only the
+// first of the whole matcher), and a count per entry point for the caller's diagnostics.
 void log_fallback(const char* what, int rc) {
-  static std::once_flag f;
-  std::call_once(f, [&] {
+  static std::mutex mu;
+  static std::map<std::string, long> seen;
+  long count;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    count = ++seen[what];
+  }
+  if (count == 1)
     fprintf(stderr, "[orbx] %s failed (%d): falling back to the host ORBmatcher\n", what, rc);
-  });
 }
 
 // DBoW2::FeatureVector (std::map, node ids ascending) as CSR
@@ -251,7 +260,8 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
   const bool bForward = tlc.at<float>(2) > CurrentFrame.mb && !bMono;
   const bool bBackward = -tlc.at<float>(2) > CurrentFrame.mb && !bMono;
   const int nl = LastFrame.N;
-  std::vector<uint8_t> valid(std::max(nl, 1)), has(std::max(CurrentFrame.N, 1));
+  std::vector<uint8_t> valid(std::max(nl, 1)), blocks(std::max(nl, 1)),
+      has(std::max(CurrentFrame.N, 1));
   std::vector<float> u(std::max(nl, 1)), v(std::max(nl, 1)), ur(std::max(nl, 1)),
       ang(std::max(nl, 1));
   std::vector<int32_t> oct(std::max(nl, 1));
@@ -273,13 +283,16 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
     ang[i] = LastFrame.mvKeysUn[i].angle;
     const cv::Mat d = pMP->GetDescriptor();
     std::copy(d.data, d.data + 32, desc.begin() + 32 * i);
+    // Tracking::UpdateLastFrame's visual-odometry points have no observations: their feature
+    // stays open to later points (:1406-1408)
+    blocks[i] = pMP->Observations() > 0;
     valid[i] = 1;
   }
   for (int i = 0; i < CurrentFrame.N; i++)
     has[i] = CurrentFrame.mvpMapPoints[i] && CurrentFrame.mvpMapPoints[i]->Observations() > 0;
   const orbx_proj_frame fr = frame_view(CurrentFrame, has.data());
-  const orbx_proj_last last{nl, valid.data(), u.data(), v.data(), ur.data(), oct.data(),
-                            ang.data(), desc.data()};
+  const orbx_proj_last last{nl,        valid.data(), u.data(),    v.data(),     ur.data(),
+                            oct.data(), ang.data(),   desc.data(), blocks.data()};
   std::vector<int32_t> match(std::max(CurrentFrame.N, 1));
   int32_t nm = 0;
   const int rc = orbx_search_by_projection_last(&fr, &last, th, bForward, bBackward,
@@ -333,8 +346,8 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
   for (int i = 0; i < CurrentFrame.N; i++) has[i] = CurrentFrame.mvpMapPoints[i] != NULL;
   orbx_proj_frame fr = frame_view(CurrentFrame, has.data());
   fr.u_right = nullptr;
-  const orbx_proj_last pts{nk, valid.data(), u.data(), v.data(), nullptr, lev.data(), ang.data(),
-                           desc.data()};
+  const orbx_proj_last pts{nk,         valid.data(), u.data(),    v.data(), nullptr,
+                           lev.data(), ang.data(),   desc.data(), nullptr};  // any point blocks
   std::vector<int32_t> match(std::max(CurrentFrame.N, 1));
   int32_t nm = 0;
   const int rc = orbx_search_by_projection_kf(&fr, &pts, th, ORBdist, mbCheckOrientation,

@@ -197,7 +197,13 @@ typedef struct {
  * LastFrame.mvpMapPoints[i] && !mvbOutlier[i] && invzc >= 0; u, v the projection into the
  * current frame and ur = u - mbf*invzc (ORBmatcher.cc:1364-1383, evaluated by the caller with
  * the reference's cv::Mat pose products); octave = LastFrame.mvKeys[i].octave, angle =
- * LastFrame.mvKeysUn[i].angle, desc = pMP->GetDescriptor(). */
+ * LastFrame.mvKeysUn[i].angle, desc = pMP->GetDescriptor().
+ * blocks[i] = pMP->Observations() > 0 (NULL = every point has observations).  A current-frame
+ * feature assigned a point without observations (the visual-odometry points
+ * Tracking::UpdateLastFrame adds, Tracking.cc:1181-1221) is not skipped by later points
+ * (ORBmatcher.cc:1406-1408): a later point may take it over, and nmatches and the rotation
+ * histogram count both assignments, as in the reference.  orbx_search_by_projection_kf ignores
+ * blocks (any map point blocks there, :1544). */
 typedef struct {
   int32_t n;
   const uint8_t* valid;
@@ -205,6 +211,7 @@ typedef struct {
   const int32_t* octave;
   const float* angle;
   const uint8_t* desc;         /* [n][32] */
+  const uint8_t* blocks;       /* [n], nullable */
 } orbx_proj_last;
 /* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
  * (ORB_SLAM2/src/ORBmatcher.cc:45-137): match[f] = index of the point assigned to frame

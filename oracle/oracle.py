@@ -407,7 +407,7 @@ class ProjPoints(C.Structure):
 class ProjLast(C.Structure):
     _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
                 ("ur", C.c_void_p), ("octave", C.c_void_p), ("angle", C.c_void_p),
-                ("desc", C.c_void_p)]
+                ("desc", C.c_void_p), ("blocks", C.c_void_p)]
 
 
 def _arrs(d, spec):
@@ -450,9 +450,10 @@ def search_by_projection(f, pts, th, nnratio):
 def search_by_projection_last(f, last, th, forward, backward, check_ori):
     s, keep = proj_frame(f)
     a = _arrs(last, [("valid", np.uint8), ("u", np.float32), ("v", np.float32), ("ur", np.float32),
-                     ("octave", np.int32), ("angle", np.float32), ("desc", np.uint8)])
+                     ("octave", np.int32), ("angle", np.float32), ("desc", np.uint8),
+                     ("blocks", np.uint8)])
     p = ProjLast(len(a["valid"]), *[_p(a[k]) for k in ("valid", "u", "v", "ur", "octave", "angle",
-                                                        "desc")])
+                                                        "desc", "blocks")])
     match = np.zeros(max(s.n, 1), np.int32)
     n = lib().oracle_search_by_projection_last(C.byref(s), C.byref(p), C.c_float(th),
                                                C.c_int(int(forward)), C.c_int(int(backward)),

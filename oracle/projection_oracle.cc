@@ -15,9 +15,10 @@
 //   ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)    (ORBmatcher.cc:1105-1329)
 // TEST INFRASTRUCTURE ONLY (see orb_oracle.h).  MapPoint state enters as plain arrays: the
 // caller evaluates mbTrackInView / isBad / the projections (Frame::isInFrustum, the pose
-// products) exactly as the reference does and passes the results; every MapPoint passed has
-// Observations() > 0, so a frame feature matched earlier in the same call is skipped by the
-// later ones, as in the reference.
+// products) exactly as the reference does and passes the results.  A frame feature matched
+// earlier in the same call is skipped by the later points when its point has Observations() > 0
+// (every point of the local-map and keyframe searches; per point `blocks` in the last-frame
+// search, whose visual-odometry points have none, Tracking.cc:1181-1221).
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -216,7 +217,8 @@ int oracle_search_by_projection_last(const orbx_proj_frame* F, const orbx_proj_l
     }
     if (bestDist <= 100) {
       match[bestIdx2] = i;
-      claimed[bestIdx2] = 1;
+      // the feature blocks later points only if its point has observations (:1406-1408)
+      if (!P->blocks || P->blocks[i]) claimed[bestIdx2] = 1;
       nmatches++;
       if (check_ori) {
         float rot = P->angle[i] - F->keys_un[bestIdx2].angle;

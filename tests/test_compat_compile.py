@@ -43,7 +43,7 @@ def test_shim_calls_are_exported():
         src = open(os.path.join(ROOT, "include", "compat", shim)).read()
         called |= set(re.findall(r"\b(orbx_[a-z0-9_]+)\s*\(", src))
     # the shims' own helpers (defined in the shim files) are not library symbols
-    own = {"orbx_context_of", "orbx_load_vocabulary", "orbx_compute_bow",
+    own = {"orbx_context_of", "orbx_materialize_pyramid", "orbx_load_vocabulary", "orbx_compute_bow",
            "orbx_compute_stereo_matches", "orbx_marker_orb", "orbx_marker_good_matches"}
     hdr = open(os.path.join(ROOT, "include", "orbx.h")).read()
     types = set(re.findall(r"\b(orbx_\w+);", hdr))  # typedef names (sizeof(orbx_keypoint) ...)

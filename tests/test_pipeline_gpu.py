@@ -238,11 +238,28 @@ def test_batch_keypoints_every_frame(w, h, nf, n):
     pipe.close()
 
 
-def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc):
-    """Frames `which` of the pipeline's last batch (host copy `frames`, n frames) against the
-    oracle: keypoints, descriptors, node / word ids, BowVector (f64 bits), SearchByBoW matches
-    and SearchForTriangulation pairs (frame f against (f - 1) mod n)."""
+_ORACLE_MEMO = {}
+
+
+def _oracle_extract(img, nf, pyramid=False):
+    """O.extract of one image, memoised by content (the stereo pools repeat 32 pairs)."""
+    import hashlib
+    key = (hashlib.sha1(img.tobytes()).hexdigest(), img.shape, nf, pyramid)
+    if key not in _ORACLE_MEMO:
+        if len(_ORACLE_MEMO) > 256:
+            _ORACLE_MEMO.clear()
+        _ORACLE_MEMO[key] = O.extract(img, O.params(nf), want_pyramid=pyramid)
+    return _ORACLE_MEMO[key]
+
+
+def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc, stereo=None):
+    """Frames `which` of the pipeline's last batch (host copy `frames`: n frames, or 2n
+    interleaved (left, right) images with `stereo` = (mb, mbf)) against the oracle: keypoints and
+    descriptors (both images of a stereo frame), mvuRight / mvDepth (ComputeStereoMatches,
+    Frame.cc:471-643), node / word ids, BowVector (f64 bits), SearchByBoW matches and
+    SearchForTriangulation pairs with mvuRight (frame f against (f - 1) mod n)."""
     h, w = frames.shape[1:]
+    ni = 2 * n if stereo else n
     valid, has_mp = pipe.masks
     ex, ey = pipe.epipole
     F = fundamental_from_pose()
@@ -250,8 +267,8 @@ def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc):
     assert err == 0
     cap = pipe.kp_cap
     out, bo = pipe.device_outputs(), pipe.bow_outputs()
-    kps_all = d2h(out["kps"], n * cap * 28).view(KEYPOINT_DTYPE).reshape(n, cap)
-    desc_all = d2h(out["desc"], n * cap * 32).reshape(n, cap, 32)
+    kps_all = d2h(out["kps"], ni * cap * 28).view(KEYPOINT_DTYPE).reshape(ni, cap)
+    desc_all = d2h(out["desc"], ni * cap * 32).reshape(ni, cap, 32)
     nodes_all = d2h(out["node_of"], n * cap * 4).view(np.uint32).reshape(n, cap)
     words_all = d2h(bo["bow_words"], n * cap * 4).view(np.uint32).reshape(n, cap)
     vals_all = d2h(bo["bow_values"], n * cap * 8).view(np.float64).reshape(n, cap)
@@ -259,14 +276,32 @@ def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc):
     word_of_all = d2h(bo["word_of"], n * cap * 4).view(np.uint32).reshape(n, cap)
     match_all = d2h(out["bow_match"], n * cap * 4).view(np.int32).reshape(n, cap)
     pairs_all = d2h(out["tri_pairs"], n * cap * 8).view(np.int32).reshape(n, cap, 2)
+    if stereo:
+        so = pipe.stereo_outputs()
+        ur_all = d2h(so["uright"], n * cap * 4).view(np.float32).reshape(n, cap)
+        dp_all = d2h(so["depth"], n * cap * 4).view(np.float32).reshape(n, cap)
     t = O.tables(O.params(nf), w, h)
     ref = {}
     for f in sorted(set(which) | {(f - 1) % n for f in which}):
-        kps, desc = O.extract(frames[f], O.params(nf))
+        if stereo:
+            kps, desc, pl, _ = _oracle_extract(frames[2 * f], nf, True)
+            kr, dr, pr, _ = _oracle_extract(frames[2 * f + 1], nf, True)
+            assert np.array_equal(kps_all[2 * f + 1, :len(kr)], kr), f
+            assert np.array_equal(desc_all[2 * f + 1, :len(kr)], dr), f
+            li = 2 * f
+        else:
+            kps, desc = _oracle_extract(frames[f], nf)
+            li = f
         k = len(kps)
         assert counts[f] == k, f
-        assert np.array_equal(kps_all[f, :k], kps), f
-        assert np.array_equal(desc_all[f, :k], desc), f
+        assert np.array_equal(kps_all[li, :k], kps), f
+        assert np.array_equal(desc_all[li, :k], desc), f
+        ur = None
+        if stereo:
+            ur, dp, _ = O.stereo_matches(kps, desc, kr, dr, pl, pr, t["scale"], t["inv_scale"],
+                                         *stereo)
+            assert ur_all[f, :k].tobytes() == ur.tobytes(), f
+            assert dp_all[f, :k].tobytes() == dp.tobytes(), f
         r = oracle_voc.transform(desc, 4)
         assert np.array_equal(nodes_all[f, :k], r["node_of"]), f
         assert np.array_equal(word_of_all[f, :k], r["word_of"]), f
@@ -276,6 +311,8 @@ def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc):
         ref[f] = dict(desc=desc, angle=kps["angle"], keys=kps, fv=featvec(r["node_of"]),
                       valid=valid[f, :k], has_mp=has_mp[f, :k], scale_factors=t["scale"],
                       level_sigma2=t["sigma2"])
+        if stereo:
+            ref[f]["u_right"] = ur
     for f in which:
         kf, cur = ref[(f - 1) % n], ref[f]
         nb, mb = O.search_by_bow_kf_f(kf, dict(cur, valid=None), 0.7, True)
@@ -286,25 +323,31 @@ def _check_pipe_frames(pipe, frames, which, nf, n, oracle_voc):
         assert np.array_equal(pairs_all[f, :nt], pt), f
 
 
-@pytest.mark.timeout(900)
+@pytest.mark.timeout(1100)
 @pytest.mark.parametrize("config,argv", [
     ("C2", []),                                                  # 3 streams x 512, pool 4
+    ("C3", []),                                                  # 3 streams x 512 stereo pairs
+    ("C4", []),                                                  # 3 streams x 512 stereo pairs
+    ("C5", []),                                                  # 3 streams x 512
     ("C5", ["--streams-total", "8", "--pool", "2", "--batch", "256"]),  # 8 streams x 256, one GPU
 ])
 def test_bench_timed_topology_matches_oracle(config, argv):
-    """bench.py's timed configuration, built by bench's own make_frame_pipes / replay_step: the
-    headline C2 (three camera streams of 512 frames, a pool of 4 resident batches, every
-    stream's captured hipGraphs replayed interleaved across the three HIP streams) and C5's
-    single-GPU strong-scaling shape (8 streams of 256 frames).  After the setup captures, the
-    warm-up and 12 interleaved steps (the compared batch's graph has run 3 times), frames
-    {0, 1, 2, 254, 255, 256, 510, 511} (C5: {0, 1, 2, 127, 128, 254, 255}) of every stream equal
-    the oracle: keypoints, descriptors, BoW, SearchByBoW, SearchForTriangulation."""
+    """bench.py's timed configuration, built by bench's own make_frame_pipes / replay_step, for
+    every bench config: C2 / C3 / C4 / C5 at their defaults (three camera streams of 512 frames
+    — C3 / C4 frames are (left, right) pairs — a pool of 4 resident batches, every stream's
+    captured hipGraphs replayed interleaved across the three HIP streams) and C5's single-GPU
+    strong-scaling shape (8 streams of 256 frames).  After the setup captures, the warm-up and 12
+    interleaved steps (the compared batch's graph has run 3 times), frames
+    {0, 1, 2, 255, 256, 510, 511} (C5 x 256: {0, 1, 2, 127, 128, 254, 255}) of every stream equal
+    the oracle: keypoints and descriptors (both images for stereo), mvuRight / mvDepth, BoW,
+    SearchByBoW, SearchForTriangulation (Frame.cc:66-122, 471-643)."""
     import bench
     args = bench.parse_args(["--config", config, "--no-upload", "--no-cpu-baseline"] + argv)
     cfg = bench.CONFIGS[config]
     streams = bench.streams_of_rank(0, 1, args.streams, args.streams_total)
     B = args.batch
     pipes, pools, _ = bench.make_frame_pipes(args, cfg, streams, 0)
+    print(f"[{config}] pipelines and pools built", flush=True)
     steps = 12
     for i in range(len(pools[0])):
         bench.replay_step(pipes, pools, B, i)
@@ -315,11 +358,18 @@ def test_bench_timed_topology_matches_oracle(config, argv):
     for p in pipes:
         p.sync()
     last = (steps - 1) % len(pools[0])
-    which = ([0, 1, 2, 254, 255, 256, 510, 511] if B == 512 else
+    which = ([0, 1, 2, 255, 256, 510, 511] if B == 512 else
              [0, 1, 2, B // 2 - 1, B // 2, B - 2, B - 1])
+    stereo = None
+    if cfg.get("stereo"):
+        from ar_orbslam2_amd.stereo import stereo_params
+        stereo = stereo_params(*cfg["stereo"])
     _, oracle_voc = _vocabs()
-    for p, pool in zip(pipes, pools):
+    for si, (p, pool) in enumerate(zip(pipes, pools)):
         frames = pool[last].cpu().numpy()
-        _check_pipe_frames(p, frames, which, cfg["nfeatures"], B, oracle_voc)
+        _check_pipe_frames(p, frames, which, cfg["nfeatures"], B, oracle_voc, stereo)
+        print(f"[{config}] stream {si}: frames {which} equal the oracle", flush=True)
     for p in pipes:
         p.close()
+    del pools
+    torch.cuda.empty_cache()

@@ -33,6 +33,22 @@ def test_search_by_projection_last_frame(stereo, th, fwd, bwd, ori):
     assert n > 200
 
 
+@pytest.mark.parametrize("stereo,th,fwd,bwd,ori", [(True, 7.0, 0, 0, True), (True, 15.0, 1, 0, True),
+                                                  (False, 7.0, 0, 0, False), (True, 7.0, 0, 1, True),
+                                                  (False, 30.0, 0, 0, True)])
+def test_search_by_projection_last_frame_vo_points(stereo, th, fwd, bwd, ori):
+    """Last-frame points without observations (Tracking::UpdateLastFrame's visual-odometry
+    points, Tracking.cc:1181-1221) do not block their feature (ORBmatcher.cc:1406-1408): later
+    points take it over, nmatches and the rotation histogram count every assignment."""
+    from test_projection_oracle import last_with_vo_points
+    F, _, L = scene(stereo=stereo, seed=int(th) + fwd)
+    L2 = last_with_vo_points(L, int(th))
+    n, m = ORBmatcher(0.9, ori).SearchByProjection(F, L2, th, forward=fwd, backward=bwd)
+    on, om = O.search_by_projection_last(F, L2, th, fwd, bwd, ori)
+    assert n == on and np.array_equal(m, om)
+    assert (om >= len(L["valid"])).any()  # some copies took their feature over
+
+
 def test_projection_edge_cases():
     F, P, L = scene(w=376, h=240, nf=400)
     # no points

@@ -102,13 +102,15 @@ def py_local(F, P, th, nnratio):
     return nm, np.array(match, np.int32)
 
 
-def py_last(F, L, th, fwd, bwd, ori):
+def py_last(F, L, th, fwd, bwd, ori, stats=None):
     g = grid(F)
     n = len(F["keys_un"])
     claimed = [bool(F["has_mp_obs"][i]) for i in range(n)]
+    blocks = L.get("blocks")
     match = [-1] * n
     hist = [[] for _ in range(30)]
     nm = 0
+    takeovers = 0
     for i in range(len(L["valid"])):
         if not L["valid"][i]:
             continue
@@ -134,8 +136,10 @@ def py_last(F, L, th, fwd, bwd, ori):
             if d < bd:
                 bd, bi = d, idx
         if bd <= 100:
-            match[bi] = i
-            claimed[bi] = True
+            takeovers += match[bi] >= 0
+            match[bi] = i  # CurrentFrame.mvpMapPoints[bestIdx2] = pMP (:1431)
+            # only a point with observations makes later points skip the feature (:1406-1408)
+            claimed[bi] = blocks is None or bool(blocks[i])
             nm += 1
             if ori:
                 rot = F32(F32(L["angle"][i]) - F32(F["keys_un"][bi]["angle"]))
@@ -164,6 +168,8 @@ def py_last(F, L, th, fwd, bwd, ori):
                 for idx in hist[b]:
                     match[idx] = -1
                     nm -= 1
+    if stats is not None:
+        stats["takeovers"] = takeovers
     return nm, np.array(match, np.int32)
 
 
@@ -197,6 +203,35 @@ def test_search_by_projection_last_frame(stereo, th, fwd, bwd, ori):
     pn, pm = py_last(F, L, th, fwd, bwd, ori)
     assert n == pn and np.array_equal(m, pm)
     assert n > 200
+
+
+def last_with_vo_points(L, seed):
+    """The last frame as Tracking::UpdateLastFrame leaves it for stereo / RGB-D
+    (Tracking.cc:1181-1221): some of its points are visual-odometry points with no observations.
+    Every point is listed twice so that a feature one of them wins stays open to its copy."""
+    rng = np.random.default_rng(seed)
+    L2 = {k: (None if v is None else np.concatenate([v, v])) for k, v in L.items()}
+    L2["blocks"] = (rng.random(len(L2["valid"])) < 0.5).astype(np.uint8)
+    return L2
+
+
+@pytest.mark.parametrize("stereo,th,fwd,bwd,ori", [(True, 7.0, 0, 0, True), (True, 15.0, 1, 0, True),
+                                                  (False, 7.0, 0, 0, False), (True, 7.0, 0, 1, True)])
+def test_search_by_projection_last_frame_vo_points(stereo, th, fwd, bwd, ori):
+    """ORBmatcher.cc:1406-1408: a feature assigned a point without observations is not skipped
+    by later points; the later point takes it over and nmatches / rotHist count both."""
+    F, _, L = scene(stereo=stereo, seed=int(th) + fwd)
+    L2 = last_with_vo_points(L, int(th))
+    n, m = O.search_by_projection_last(F, L2, th, fwd, bwd, ori)
+    st = {}
+    pn, pm = py_last(F, L2, th, fwd, bwd, ori, st)
+    assert n == pn and np.array_equal(m, pm)
+    assert st["takeovers"] > 50
+    # every point blocking is the same search as blocks = NULL
+    L2["blocks"][:] = 1
+    n1, m1 = O.search_by_projection_last(F, L2, th, fwd, bwd, ori)
+    n0, m0 = O.search_by_projection_last(F, dict(L2, blocks=None), th, fwd, bwd, ori)
+    assert n1 == n0 and np.array_equal(m1, m0)
 
 
 def three_maxima(counts):

@@ -10,7 +10,23 @@
 // frames/s and per-frame latency (median / mean, as mono_tum.cc:113-121 reports tracking time),
 // per call.
 //
-// usage: orbx_dropin DIR W H NFEATURES N_IMG THREADS WARMUP FRAMES DEVICE
+// MODE "capi" (default) calls the C ABI directly with buffers reused across frames.  MODE
+// "shim" replays what the reference-side shims (include/compat/*.cc) do around each call, so the
+// number is what Frame.cc:252-258 / Tracking.cc:1132-1136 / LocalMapping.cc:238-241 would see
+// with the shims linked in — everything but OpenCV itself, which is not in this image:
+//   ORBextractor_orbx.cc   a fresh keypoint vector and a cap x 32 descriptor block per call
+//                          (cv::Mat d), then descriptors.create(n, 32) + the row copy; no pyramid
+//                          export (mvImagePyramid is materialised on demand, mono never does)
+//   Frame_orbx.cc          per-call output vectors, then BowVector / FeatureVector as the
+//                          reference's std::maps (map<WordId, double>, map<NodeId,
+//                          vector<unsigned>>)
+//   ORBmatcher_orbx.cc     GetMapPointMatches() copies, the validity masks (isBad per point),
+//                          angles, the std::map FeatureVectors -> CSR for both sides, the match
+//                          vector back to MapPoint pointers; SearchForTriangulation's
+//                          GetMapPoint(i) per feature under the keyframe's feature mutex and the
+//                          vector<pair<size_t, size_t>> result
+//
+// usage: orbx_dropin DIR W H NFEATURES N_IMG THREADS WARMUP FRAMES DEVICE [MODE]
 //   DIR/frames.u8       THREADS x N_IMG x H x W u8 images
 //   DIR/voc_parent.i32, voc_leaf.u8, voc_desc.u8, voc_weight.f64   k=10, L=6 vocabulary nodes
 #include <algorithm>
@@ -20,8 +36,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "orbx.h"
@@ -87,6 +106,142 @@ struct FrameData {
   orbx_featvec fv() const { return {fv_n, fv_ids.data(), fv_off.data(), fv_feats.data()}; }
 };
 
+// ----------------------------------------------------------------- the shims' host side
+// Stand-ins for the reference's objects with the members the shims touch.
+struct MapPointStub {
+  bool bad = false;
+  bool isBad() const { return bad; }  // MapPoint::isBad locks mMutexFeatures in the reference
+};
+typedef std::map<uint32_t, double> BowVectorMap;                   // DBoW2::BowVector
+typedef std::map<uint32_t, std::vector<unsigned int> > FeatVecMap;  // DBoW2::FeatureVector
+
+struct ShimFrame {  // a Frame / KeyFrame: mvKeysUn, mDescriptors, BoW, map points
+  int N = 0;
+  std::vector<orbx_keypoint> keys;
+  std::vector<uint8_t> desc;  // the n x 32 cv::Mat
+  BowVectorMap bow;
+  FeatVecMap fv;
+  // mvpMapPoints.  The bench's unit of work draws SearchByBoW's "valid" (60 %) and
+  // triangulation's "has a point" (40 %) independently, so the stand-in keeps one array per call
+  // to do the same work as the capi mode; the reference reads both from one array.
+  std::vector<MapPointStub*> mps, mps_tri;
+  mutable std::mutex mutex_features;
+  std::vector<MapPointStub*> GetMapPointMatches() const {
+    std::lock_guard<std::mutex> lk(mutex_features);
+    return mps;
+  }
+  MapPointStub* GetMapPoint(size_t i) const {
+    std::lock_guard<std::mutex> lk(mutex_features);
+    return mps_tri[i];
+  }
+};
+
+struct FeatVecCSR {  // ORBmatcher_orbx.cc's std::map -> CSR
+  std::vector<uint32_t> ids;
+  std::vector<int32_t> off, feats;
+  orbx_featvec view;
+  explicit FeatVecCSR(const FeatVecMap& fv) {
+    off.push_back(0);
+    for (FeatVecMap::const_iterator it = fv.begin(); it != fv.end(); ++it) {
+      ids.push_back(it->first);
+      feats.insert(feats.end(), it->second.begin(), it->second.end());
+      off.push_back((int32_t)feats.size());
+    }
+    view = orbx_featvec{(int32_t)ids.size(), ids.data(), off.data(), feats.data()};
+  }
+};
+
+std::vector<float> angles_of(const std::vector<orbx_keypoint>& k) {
+  std::vector<float> a(k.size());
+  for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
+  return a;
+}
+
+// ORBextractor::operator() as ORBextractor_orbx.cc runs it
+int shim_extract(orbx_extractor* ex, const uint8_t* img, int W, int H, int nfeatures,
+                 ShimFrame& F) {
+  int32_t cap = 4 * nfeatures + 64, n = 0;
+  std::vector<orbx_keypoint> kps(cap);
+  std::vector<uint8_t> d((size_t)cap * 32);
+  int rc = orbx_extract(ex, img, W, H, W, kps.data(), d.data(), cap, &n);
+  if (rc == ORBX_ECAPACITY) {
+    cap = n;
+    kps.resize(cap);
+    d.resize((size_t)cap * 32);
+    rc = orbx_extract(ex, img, W, H, W, kps.data(), d.data(), cap, &n);
+  }
+  if (rc != ORBX_OK) return rc;
+  kps.resize(std::max(n, 0));
+  F.keys.swap(kps);
+  F.desc.assign(d.begin(), d.begin() + (size_t)std::max(n, 0) * 32);  // create(n, 32) + copyTo
+  F.N = std::max(n, 0);
+  return ORBX_OK;
+}
+
+// Frame::ComputeBoW as Frame_orbx.cc runs it
+int shim_compute_bow(orbx_vocabulary* voc, ShimFrame& F) {
+  const int n = F.N;
+  const size_t m = (size_t)std::max(n, 1);
+  std::vector<uint32_t> bw(m), fi(m + 1);
+  std::vector<double> bv(m);
+  std::vector<int32_t> fo(m + 2), ff(m);
+  int32_t nb = 0, nf = 0;
+  const int rc = orbx_vocabulary_transform(voc, F.desc.data(), n, 4, nullptr, nullptr, bw.data(),
+                                           bv.data(), &nb, fi.data(), fo.data(), ff.data(), &nf);
+  if (rc != ORBX_OK) return rc;
+  F.bow.clear();
+  F.fv.clear();
+  for (int i = 0; i < nb; i++) F.bow.insert(F.bow.end(), std::make_pair(bw[i], bv[i]));
+  for (int j = 0; j < nf; j++)
+    F.fv.insert(F.fv.end(), std::make_pair(fi[j], std::vector<unsigned int>(ff.begin() + fo[j],
+                                                                            ff.begin() + fo[j + 1])));
+  return ORBX_OK;
+}
+
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) as ORBmatcher_orbx.cc runs it
+int shim_search_by_bow(const ShimFrame& KF, const ShimFrame& F, std::vector<MapPointStub*>& out,
+                       int32_t* nmatches) {
+  const std::vector<MapPointStub*> vpMP = KF.GetMapPointMatches();
+  std::vector<uint8_t> valid(vpMP.size());
+  for (size_t i = 0; i < vpMP.size(); i++) valid[i] = vpMP[i] && !vpMP[i]->isBad();
+  const std::vector<float> akf = angles_of(KF.keys), af = angles_of(F.keys);
+  FeatVecCSR fk(KF.fv), ff(F.fv);
+  const orbx_bow_side kf{KF.N, KF.desc.data(), akf.data(), valid.data(), fk.view};
+  const orbx_bow_side fr{F.N, F.desc.data(), af.data(), nullptr, ff.view};
+  std::vector<int32_t> match(std::max(F.N, 1));
+  const int rc = orbx_search_by_bow_kf_f(&kf, &fr, 0.7f, 1, match.data(), nmatches);
+  if (rc != ORBX_OK) return rc;
+  out.assign(F.N, nullptr);
+  for (int i = 0; i < F.N; i++)
+    if (match[i] >= 0) out[i] = vpMP[match[i]];
+  return ORBX_OK;
+}
+
+// ORBmatcher::SearchForTriangulation as ORBmatcher_orbx.cc runs it (the epipole's three cv::Mat
+// products are left out)
+int shim_search_for_triangulation(const ShimFrame& K1, const ShimFrame& K2, const float* F12,
+                                  float ex, float ey, const float* scale, const float* sigma2,
+                                  int nl, std::vector<std::pair<size_t, size_t> >& pairs_out,
+                                  int32_t* nmatches) {
+  std::vector<uint8_t> h1(K1.N), h2(K2.N);
+  for (int i = 0; i < K1.N; i++) h1[i] = K1.GetMapPoint(i) != nullptr;
+  for (int i = 0; i < K2.N; i++) h2[i] = K2.GetMapPoint(i) != nullptr;
+  FeatVecCSR f1(K1.fv), f2(K2.fv);
+  const orbx_tri_side s1{K1.N, K1.desc.data(), K1.keys.data(), nullptr, h1.data(), f1.view,
+                         scale, sigma2, nl};
+  const orbx_tri_side s2{K2.N, K2.desc.data(), K2.keys.data(), nullptr, h2.data(), f2.view,
+                         scale, sigma2, nl};
+  std::vector<int32_t> pairs(2 * std::max(K1.N, 1));
+  const int rc = orbx_search_for_triangulation(&s1, &s2, F12, ex, ey, 0, 0.6f, 0, pairs.data(),
+                                               nmatches);
+  if (rc != ORBX_OK) return rc;
+  pairs_out.clear();
+  pairs_out.reserve(*nmatches);
+  for (int i = 0; i < *nmatches; i++)
+    pairs_out.push_back(std::make_pair((size_t)pairs[2 * i], (size_t)pairs[2 * i + 1]));
+  return ORBX_OK;
+}
+
 struct Stats {
   std::vector<double> total, extract, bow, search_bow, search_tri;
   long long matches_bow = 0, matches_tri = 0, keypoints = 0;
@@ -113,9 +268,16 @@ double pct(std::vector<double> v, double p) {
 
 int main(int argc, char** argv) {
   if (argc < 10) {
-    fprintf(stderr, "usage: %s DIR W H NFEATURES N_IMG THREADS WARMUP FRAMES DEVICE\n", argv[0]);
+    fprintf(stderr, "usage: %s DIR W H NFEATURES N_IMG THREADS WARMUP FRAMES DEVICE [capi|shim]\n",
+            argv[0]);
     return 1;
   }
+  const std::string mode = argc > 10 ? argv[10] : "capi";
+  if (mode != "capi" && mode != "shim") {
+    fprintf(stderr, "MODE must be capi or shim\n");
+    return 1;
+  }
+  const bool shim = mode == "shim";
   const std::string dir = argv[1];
   const int W = atoi(argv[2]), H = atoi(argv[3]), NF = atoi(argv[4]), NIMG = atoi(argv[5]);
   const int T = atoi(argv[6]), WARM = atoi(argv[7]), FR = atoi(argv[8]), DEV = atoi(argv[9]);
@@ -179,8 +341,54 @@ int main(int argc, char** argv) {
     };
     ready++;
     while (!go.load()) std::this_thread::yield();
+    // shim mode: frames with their map points (the masks' 60 % / 40 % as stub MapPoints)
+    ShimFrame sf[2];
+    std::vector<MapPointStub> mp_pool((size_t)4 * cap);
+    std::vector<MapPointStub*> bow_out;
+    std::vector<std::pair<size_t, size_t> > tri_out;
     Clock::time_point t_start;
-    for (int f = 0; f < WARM + FR; f++) {
+    for (int f = 0; f < WARM + FR && shim; f++) {
+      if (f == WARM) t_start = Clock::now();
+      ShimFrame& cur = sf[f & 1];
+      ShimFrame& prev = sf[(f + 1) & 1];
+      const uint8_t* img = (const uint8_t*)frames.data() + ((size_t)t * NIMG + f % NIMG) * W * H;
+      const auto a = Clock::now();
+      CK(shim_extract(exr, img, W, H, NF, cur));
+      const auto b = Clock::now();
+      CK(shim_compute_bow(voc, cur));
+      // map points: SearchByBoW's "valid" (60 %), triangulation's "has a point" (40 %)
+      cur.mps.assign(cur.N, nullptr);
+      cur.mps_tri.assign(cur.N, nullptr);
+      for (int i = 0; i < cur.N; i++) {
+        MapPointStub* m = &mp_pool[(size_t)(f & 1) * 2 * cap + i];
+        m->bad = false;
+        cur.mps[i] = rnd() < 0.6f ? m : nullptr;
+        cur.mps_tri[i] = rnd() < 0.4f ? m : nullptr;
+      }
+      const auto c = Clock::now();
+      auto d = c, e = c;
+      int32_t nb = 0, nt = 0;
+      if (f > 0) {
+        CK(shim_search_by_bow(prev, cur, bow_out, &nb));
+        d = Clock::now();
+        CK(shim_search_for_triangulation(prev, cur, F12, ex, ey, scale, sigma2, nl, tri_out, &nt));
+        e = Clock::now();
+      }
+      if (f >= WARM) {
+        auto ms = [](Clock::time_point x, Clock::time_point y) {
+          return std::chrono::duration<double, std::milli>(y - x).count();
+        };
+        st.total.push_back(ms(a, e));
+        st.extract.push_back(ms(a, b));
+        st.bow.push_back(ms(b, c));
+        st.search_bow.push_back(ms(c, d));
+        st.search_tri.push_back(ms(d, e));
+        st.matches_bow += nb;
+        st.matches_tri += nt;
+        st.keypoints += cur.N;
+      }
+    }
+    for (int f = 0; f < WARM + FR && !shim; f++) {
       if (f == WARM) t_start = Clock::now();
       FrameData& cur = fd[f & 1];
       FrameData& prev = fd[(f + 1) & 1];
@@ -250,7 +458,7 @@ int main(int argc, char** argv) {
   }
   const double wall = *std::max_element(thread_wall.begin(), thread_wall.end());
   const double nfr = (double)all.total.size();
-  printf("{\"fps\": %.2f, \"frames\": %d, \"threads\": %d, \"wall_s\": %.4f, "
+  printf("{\"mode\": \"%s\", \"fps\": %.2f, \"frames\": %d, \"threads\": %d, \"wall_s\": %.4f, "
          "\"median_ms\": %.4f, \"mean_ms\": %.4f, \"p90_ms\": %.4f, "
          "\"per_call_median_ms\": {\"orbx_extract\": %.4f, \"orbx_vocabulary_transform\": %.4f, "
          "\"orbx_search_by_bow_kf_f\": %.4f, \"orbx_search_for_triangulation\": %.4f}, "
@@ -258,7 +466,7 @@ int main(int argc, char** argv) {
          "\"orbx_search_by_bow_kf_f\": %.4f, \"orbx_search_for_triangulation\": %.4f}, "
          "\"keypoints_per_frame\": %.1f, \"bow_matches_per_frame\": %.1f, "
          "\"triangulation_matches_per_frame\": %.1f}\n",
-         nfr / wall, (int)nfr, T, wall, median(all.total), mean(all.total), pct(all.total, 0.9),
+         mode.c_str(), nfr / wall, (int)nfr, T, wall, median(all.total), mean(all.total), pct(all.total, 0.9),
          median(all.extract), median(all.bow), median(all.search_bow), median(all.search_tri),
          mean(all.extract), mean(all.bow), mean(all.search_bow), mean(all.search_tri),
          all.keypoints / nfr, all.matches_bow / nfr, all.matches_tri / nfr);
