@@ -13,8 +13,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "liborbx.so")
-# experiments only: ORBX_LIB_DIR names another build directory (a variant built with EXTRA
-# defines by scripts/build_variants.sh); it needs ORBX_ALLOW_CUSTOM_BUILD=1 like any custom build
+# experiments only: ORBX_LIB_DIR names another build directory (a variant built with
+# `make -C ar_orbslam2_amd/csrc OUT=<dir> EXTRA=...`); it needs ORBX_ALLOW_CUSTOM_BUILD=1 like any
+# custom build
 if os.environ.get("ORBX_LIB_DIR") and os.environ.get("ORBX_ALLOW_CUSTOM_BUILD"):
     LIB_PATH = os.path.join(os.environ["ORBX_LIB_DIR"], "liborbx.so")
 

@@ -5,10 +5,9 @@
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
 //   k_pyramid       2 launches   row bands               (level 0 copy + cv::resize INTER_LINEAR)
 //   k_blur          x 1          64x64 tiles, all levels (GaussianBlur 7x7 s=2)
-//   k_fast_tile     x 1          64x64 tiles, all levels (FAST score + cell-local NMS at iniThFAST)
-//   k_fast_compact  x 1          4 FAST cells per wave   (ordered compaction, fallback queue)
-//   k_fast_fallback x 1-2        queued cells            (the minThFAST retry)
-//   k_octree        x 2          (image, level)          (DistributeOctTree; big levels apart)
+//   k_fast_cells    x 1-2        FAST cells, one wave    (FAST + cell-local NMS at iniThFAST, the
+//                                each                     minThFAST retry, raster compaction)
+//   k_octree        x 1-2        (image, level)          (DistributeOctTree; big levels apart)
 //   k_describe      x 1          half-wave per keypoint  (IC_Angle + rBRIEF)
 // The first k_pyramid launch copies level 0 from the caller's input into the pitched pyramid
 // block, where every level lives.  Everything is integer or bit-exact float (see orbx_math.h); compiled with
@@ -147,9 +146,9 @@ __device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
 }
 
 // ------------------------------------------------------------------ k_pyramid
-#ifndef ORBX_PY_LOADS
-#define ORBX_PY_LOADS 4  // 16-B source chunks per thread in flight while a band is staged
-#endif
+// 16-B source chunks per thread in flight while a band is staged (8 or 2 measured slower:
+// 0.426 / 0.303 vs 0.298 ms per 512 C2 frames)
+constexpr int kPyLoads = 4;
 // ComputePyramid (ORBextractor.cc:1047-1072) in a few launches (Geometry::pyr_stages): the first
 // copies level 0 into the 64-B pitched pyramid block (every later kernel reads aligned dwords)
 // and builds levels 1..3, the next ones build four levels each from the last level stored.
@@ -242,20 +241,20 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
     if ((w & 15) == 0) {  // 16-byte chunks, four per thread in flight
       const int nch = w >> 4, items = nr * nch;
       const float inv = 1.0f / (float)nch;
-      for (int i0 = tid; i0 < items; i0 += ORBX_PY_LOADS * kPyNT) {
+      for (int i0 = tid; i0 < items; i0 += kPyLoads * kPyNT) {
         // past the end a thread repeats the last chunk: identical bytes to identical places
-        uint4 v[ORBX_PY_LOADS];
-        int rr[ORBX_PY_LOADS], cc[ORBX_PY_LOADS];
+        uint4 v[kPyLoads];
+        int rr[kPyLoads], cc[kPyLoads];
 #pragma unroll
-        for (int u = 0; u < ORBX_PY_LOADS; u++) {
+        for (int u = 0; u < kPyLoads; u++) {
           py_divmod(min(i0 + kPyNT * u, items - 1), nch, inv, rr[u], cc[u]);
           v[u] = *(const uint4*)(src + (int64_t)(lo + rr[u]) * w + 16 * cc[u]);
         }
 #pragma unroll
-        for (int u = 0; u < ORBX_PY_LOADS; u++)  // pin the loads here: all four in flight together
+        for (int u = 0; u < kPyLoads; u++)  // pin the loads here: all four in flight together
           asm volatile("" : "+v"(v[u].x), "+v"(v[u].y), "+v"(v[u].z), "+v"(v[u].w));
 #pragma unroll
-        for (int u = 0; u < ORBX_PY_LOADS; u++) {
+        for (int u = 0; u < kPyLoads; u++) {
           const int y = lo + rr[u];
           *(uint4*)(sdst + __mul24(rr[u], pitch) + 16 * cc[u]) = v[u];
           if (y >= own_lo && y < own_hi) *(uint4*)(dst + (uint32_t)__mul24(y, pitch) + 16 * cc[u]) = v[u];
@@ -479,193 +478,14 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
 }
 
 // ------------------------------------------------------------------ FAST
-// One workgroup per FAST cell of ComputeKeyPointsOctTree (ORBextractor.cc:758-796): cv::FAST
-// with NMS on the cell ROI at iniThFAST, again at minThFAST when no keypoint survives, then an
-// order-preserving (raster) compaction into the cell's candidate slot.  Score = OpenCV 2.4
-// cornerScore<16>; V = score+1 clamped to [0,255] so "corner at t" is V > t.
+// cv::FAST with NMS on each cell ROI of ComputeKeyPointsOctTree (ORBextractor.cc:758-796) at
+// iniThFAST, again at minThFAST when no keypoint survives, then an order-preserving (raster)
+// compaction into the cell's candidate slot.  Score = OpenCV 2.4 cornerScore<16>;
+// V = score+1 clamped to [0,255] so "corner at t" is V > t.
 constexpr int kCellMax = 66;  // wCell, hCell < 60 (+6)
 
-// fast_score: orbx_internal.h
+// fast_score, fast_cardinal2x2: orbx_internal.h
 
-// fast_pretest, lane_rank: orbx_internal.h
-
-// ---- k_fast_tile: FAST for 64 x 64 output pixels of one level per workgroup.
-//  (1) score map V = clamp(cornerScore+1, 0, 255) on the tile plus a 1-px ring, for pixels
-//      of the detection region [19, w-19) x [19, h-19) (0 elsewhere).  A pixel failing the
-//      even-point test at iniThFAST cannot be a corner at it, so its V (<= threshold) is
-//      equivalent to 0 in the NMS: only candidates are scored, from
-//      wave-local queues (mbcnt ranks).  The test runs one pixel per lane: each circle point's
-//      darker / brighter compare is a v_cmp into a 64-bit lane mask, and the arc logic runs on
-//      those masks in the scalar unit.
-//  (2) cv::FAST's strict 8-neighbour NMS at iniThFAST, with neighbours outside the
-//      pixel's own FAST cell (or outside the detection region) counting as 0 — the cell-local
-//      NMS of FAST on each cell ROI (ORBextractor.cc:776-784).  Evaluated at the
-//      queued candidates only (one lane each); survivors set their bit in the row's 64-bit
-//      keep word in LDS (ds_or), which one thread per row and threshold then stores.
-// k_fast_fallback queue counters, [2 img + fb_big] kFbStride ints apart: one 128-B line each (the
-// queues fill with one atomic per wave; on a shared line those atomics serialize)
-constexpr int kFbStride = 32;
-constexpr int kFastT = 64;
-struct FastTile {
-  int16_t level, tx, ty, pad;
-};
-
-template <bool PAIR>
-__global__ __launch_bounds__(256) void k_fast_tile(const uint8_t* __restrict__ pyr,
-                                                   int64_t pyr_bytes, uint8_t* __restrict__ vmap,
-                                                   uint64_t* __restrict__ bitmaps,
-                                                   int64_t bm_words,
-                                                   const LevelGeom* __restrict__ lv,
-                                                   const FastTile* __restrict__ tiles,
-                                                   int ini_th, int* __restrict__ fb_count) {
-  constexpr int kInR = kFastT + 8;        // staged rows Y0-4 .. Y0+67
-  constexpr int kInD = (kFastT + 32) / 4; // staged dwords: columns X0-16 .. X0+79 (16-B pieces)
-  constexpr int kWinR = kFastT + 2;       // V rows Y0-1 .. Y0+64
-  constexpr int kWinG = (kFastT + 8) / 4; // V column groups: X0-4 .. X0+67
-  constexpr int kVS = kWinG * 4;          // V row stride (bytes)
-  constexpr int kGroups = kWinR * kWinG;
-  constexpr int kRowB = kInD * 4;         // staged row stride (bytes)
-  constexpr int kCS = 1;                  // bytes per staged column
-  // per-wave queue bound: wave w pretests the row pairs starting at 2w mod 8, i.e. at most
-  // ceil(kWinR / 8) pairs = 2 * ceil(kWinR / 8) full rows, and wave 0 also takes one ring
-  // pass of 64 pixels (waves 1 and 2 take the rest of the ring, fewer rows)
-  constexpr int kQ = 2 * ((kWinR + 7) / 8) * 64 + 64;
-  __shared__ __align__(16) uint32_t s_in[kInR * kRowB / 4];
-  __shared__ __align__(16) uint32_t s_v32[kWinR * kWinG];
-  __shared__ uint16_t s_q[4][kQ + 64];
-  int bx, img;
-  xcd_block(bx, img);
-  const FastTile T = tiles[bx];
-  const int tid = threadIdx.x, lane = tid & 63;
-  // the image's two k_fast_fallback queue counters start at 0 (read by k_fast_compact, which
-  // runs after this launch): one tile per image clears them instead of a fill launch
-  if (bx == 0 && tid < 2 * kFbStride) fb_count[2 * kFbStride * img + tid] = 0;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar row math
-  const LevelGeom& G = lv[T.level];
-  const uint8_t* src = level_base(pyr, pyr_bytes, G, img);
-  const int X0 = T.tx * kFastT, Y0 = T.ty * kFastT;
-  // staged window: rows Y0-4 .. Y0+67 clamped, 16-byte pieces of columns X0-16 .. X0+79 (zero
-  // left of the image and past the pitch, a multiple of 64 past X0 + 63)
-  for (int i = tid; i < kInR * (kInD / 4); i += 256) {
-    const int r = i / (kInD / 4), c = i - r * (kInD / 4);
-    const int y = min(max(Y0 + r - 4, 0), G.h - 1);
-    const int x = X0 - 16 + 16 * c;
-    *(uint4*)&s_in[r * kInD + 4 * c] =
-        (x >= 0 && x < G.pitch) ? *(const uint4*)(src + (uint32_t)(__mul24(y, G.pitch) + x))
-                                : make_uint4(0u, 0u, 0u, 0u);
-  }
-  for (int i = tid; i < kGroups; i += 256) s_v32[i] = 0;
-  __syncthreads();
-  const int ylo = kEdge, yhi = G.h - kEdge, xlo = kEdge, xhi = G.w - kEdge;
-  uint16_t* q = s_q[wid];
-  int nq = 0;
-  const uint8_t* sin8 = (const uint8_t*)s_in;
-  // every lane stores: failing lanes into the wave's 64 spare slots past kQ (no exec juggling)
-  auto enqueue = [&](uint64_t pass, int idx) {
-    q[(pass >> lane) & 1 ? nq + lane_rank(pass) : kQ + lane] = (uint16_t)idx;
-    nq += __popcll(pass);
-  };
-  // V window coordinates: x = X0 - 4 + vx, y = Y0 - 1 + vy; staged row vy + 3, column vx + 12
-  // holds the pixel.  Tile columns: lane = column, one wave-uniform row (pair) per pass.
-  const uint64_t col_ok = __ballot(X0 + lane >= xlo && X0 + lane < xhi);
-  if (col_ok != 0) {
-    const int vy_lo = max(0, ylo - (Y0 - 1)), vy_hi = min(kWinR, yhi - (Y0 - 1));
-    if constexpr (PAIR) {
-      // row pairs (vy, vy + 1), pair index = wid mod 4 (vy_lo is even, so vy + 1 <= 65)
-      // the lane's flag bits of interest: its column inside the detection region
-      const uint32_t fm = (X0 + lane >= xlo && X0 + lane < xhi) ? 0x80008000u : 0u;
-      for (int vy = vy_lo + 2 * wid; vy < vy_hi; vy += 8) {
-        const uint32_t f = fast_pretest2<kRowB>(sin8 + vy * kRowB + lane + 13, ini_th) &
-                           (vy + 1 < vy_hi ? fm : fm & 0x8000u);
-        wave_enqueue(q, nq, kQ, (f & 0x8000u) != 0, vy * kVS + 4 + lane, lane);
-        wave_enqueue(q, nq, kQ, (int32_t)f < 0, (vy + 1) * kVS + 4 + lane, lane);
-      }
-    } else {
-      for (int vy = vy_lo + ((wid - vy_lo) & 3); vy < vy_hi; vy += 4)  // rows = wid mod 4
-        enqueue(fast_pretest<kRowB>(sin8 + vy * kRowB + lane + 13, ini_th, col_ok),
-                vy * kVS + 4 + lane);
-    }
-  }
-  // ring columns X0-1 (vx 3) and X0+64 (vx 68): 2 * kWinR pixels, lane k = (row, side)
-  for (int k0 = wid * 64; k0 < 2 * kWinR; k0 += 256) {
-    const int k = k0 + lane;
-    const int vy = min(k >> 1, kWinR - 1), vx = k & 1 ? 4 + kFastT : 3;
-    const int x = X0 - 4 + vx, y = Y0 - 1 + vy;
-    const uint64_t ok = __ballot(k < 2 * kWinR && x >= xlo && x < xhi && y >= ylo && y < yhi);
-    if (ok != 0)
-      enqueue(fast_pretest<kRowB, kCS>(sin8 + vy * kRowB + (vx + 9) * kCS, ini_th, ok), vy * kVS + vx);
-  }
-  uint8_t* s_v = (uint8_t*)s_v32;
-  for (int j0 = 0; j0 < nq; j0 += 64) {
-    const int j = j0 + lane;
-    if (j < nq) {
-      const int i = q[j];  // = vy * kVS + vx
-      const int vy = i / kVS, vx = i - vy * kVS;
-      const int sc = fast_score<kCS>((const uint8_t*)s_in, kRowB, vx + 12, vy + 3);
-      s_v[i] = (uint8_t)min(255, max(0, sc + 1));
-    }
-  }
-  // keep words of the tile's 64 rows; cell-edge masks of its columns / rows
-  __shared__ uint64_t s_keep[kFastT];
-  __shared__ uint8_t s_cm[kFastT], s_rm[kFastT];
-  if (tid < kFastT) {
-    s_keep[tid] = 0;
-    // position inside its FAST cell (detection rows/columns 19 + i*cell ..): at the cell edges
-    // a neighbour belongs to another cell ROI and counts as 0; bit 0 = left / up allowed,
-    // bit 1 = right / down allowed
-    // (only columns / rows of the detection region matter: x - kEdge >= 0 there; the
-    // remainder by the hardware reciprocal, as py_divmod — which corrects the quotient by one
-    // either way — instead of two integer divisions)
-    const int wc = max(G.wcell, 1), x = X0 + tid;
-    int qx, rx;
-    py_divmod(max(x - kEdge, 0), wc, __builtin_amdgcn_rcpf((float)wc), qx, rx);
-    s_cm[tid] = (rx != 0 ? 1 : 0) | (rx != wc - 1 && x + 1 < xhi ? 2 : 0);
-  } else if (tid < 2 * kFastT) {
-    const int hc = max(G.hcell, 1), y = Y0 + tid - kFastT;
-    int qy, ry;
-    py_divmod(max(y - kEdge, 0), hc, __builtin_amdgcn_rcpf((float)hc), qy, ry);
-    s_rm[tid - kFastT] = (ry != 0 ? 1 : 0) | (ry != hc - 1 && y + 1 < yhi ? 2 : 0);
-  }
-  __syncthreads();
-  // cv::FAST's strict 8-neighbour NMS at iniThFAST, evaluated at the queued candidates of the
-  // tile proper (every other pixel has V = 0 and is never kept).
-  // keep at t  <=>  V > t and V-1 > (nmax > t ? nmax-1 : 0)  <=>  V > (nmax > t ? nmax : max(t,1))
-  // (a neighbour counts with its score V-1 only if it is a corner at t, V > t; the count is
-  // monotone in V, so the largest masked neighbour decides)
-  const int ini1 = max(ini_th, 1);
-  uint8_t* vout = vmap + (int64_t)img * pyr_bytes + G.pyr_off;
-  for (int j0 = 0; j0 < nq; j0 += 64) {
-    const int j = j0 + lane;
-    if (j >= nq) break;
-    const int i = q[j];
-    const int vy = i / kVS, vx = i - vy * kVS;
-    const int tx = vx - 4, ty = vy - 1;  // tile coordinates
-    if (tx < 0 || tx >= kFastT || ty < 0 || ty >= kFastT) continue;
-    const int v = s_v[i];
-    const int cm = s_cm[tx], rm = s_rm[ty];
-    const int mL = cm & 1 ? 0xFF : 0, mR = cm & 2 ? 0xFF : 0;
-    const int mU = rm & 1 ? 0xFF : 0, mD = rm & 2 ? 0xFF : 0;
-    const uint8_t* pu = s_v + i - kVS;
-    const uint8_t* pd = s_v + i + kVS;
-    const int hu = max((int)pu[0], max(pu[-1] & mL, pu[1] & mR)) & mU;
-    const int hd = max((int)pd[0], max(pd[-1] & mL, pd[1] & mR)) & mD;
-    const int nmax = max(max(hu, hd), max(s_v[i - 1] & mL, s_v[i + 1] & mR));
-    if (v > (nmax > ini_th ? nmax : ini1)) {
-      atomicOr((unsigned long long*)&s_keep[ty], 1ull << tx);
-      vout[(int64_t)(Y0 + ty) * G.pitch + X0 + tx] = (uint8_t)v;  // read at survivors only
-    }
-  }
-  __syncthreads();
-  if (tid < kFastT) {
-    const int y = Y0 + tid;
-    if (y < G.h) bitmaps[(int64_t)img * bm_words + G.bm_off + (int64_t)y * G.bm_wpr + T.tx] = s_keep[tid];
-  }
-}
-
-// ---- k_fast_compact: per FAST cell (one wave, lane = detection row): survivors at
-// iniThFAST (ORBextractor.cc:780) in raster order (row prefix sum, then ascending x) into the
-// cell's candidate slot, keys relative to minBorder = 16.  A cell without any is queued for
-// k_fast_fallback (the minThFAST retry, ORBextractor.cc:782-784).
 // Candidate keys: position in the octree frame (level coordinates - minBorder + 3) and FAST
 // score - 1.  Plans whose octree frames fit 4095 px pack x:12 y:12 score:8 into a u32; wider
 // ones (Geometry::wide_keys) use a u64 with x:16 y:16 and the score at bit 32.
@@ -691,10 +511,6 @@ struct KeyFmt<uint64_t> {
   static __device__ __forceinline__ unsigned score(uint64_t k) { return (unsigned)(k >> 32); }
 };
 
-__device__ __forceinline__ uint32_t cand_key(int x, int y, int v) {  // the legacy FAST kernels
-  return KeyFmt<uint32_t>::make(x, y, v);
-}
-
 // raster-order compaction of a cell's keep rows (lane = detection row): out slot, count
 template <class K, class VAt>
 __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int cx0,
@@ -711,286 +527,6 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
   if (lane == 0) *cnt_out = nout;
 }
 
-// survivors of a cell staged in LDS for the coalesced round 3; a cell with more (at most
-// slot_cap: cells < 60 x 60) writes its keys from the row lanes directly.  A small stage keeps
-// the workgroup's LDS at 8 KB: occupancy, not issue, bounds this latency-chained kernel.
-constexpr int kCompactCap = 256;
-constexpr int kCompactK = 4;          // cells per wave: each round of loads covers all of them
-__global__ __launch_bounds__(256) void k_fast_compact(const uint8_t* __restrict__ vmap,
-                                                      int64_t pyr_bytes,
-                                                      const uint64_t* __restrict__ bitmaps,
-                                                      int64_t bm_words,
-                                                      const CellGeom* __restrict__ cells,
-                                                      int ncells, uint32_t* __restrict__ cand,
-                                                      int cand_total,
-                                                      int* __restrict__ cell_counts,
-                                                      int* __restrict__ fb_count,
-                                                      int* __restrict__ fb_list) {
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bx, img;
-  xcd_block(bx, img);
-  const int c0 = (bx * 4 + wid) * kCompactK;  // cells c0 .. c0 + kCompactK - 1 of this wave
-  if (c0 >= ncells) return;
-  // the cell's survivors (row << 8 | column) at their raster slots
-  __shared__ uint16_t s_rc[4][kCompactK][kCompactCap];
-  // round 1: the geometry of every cell of the wave
-  CellGeom C[kCompactK];
-#pragma unroll
-  for (int j = 0; j < kCompactK; j++) C[j] = cells[min(c0 + j, ncells - 1)];
-  // round 2: every keep row (lane = detection row) of every cell
-  uint64_t bits[kCompactK];
-  int live[kCompactK];  // 1: in range with a detection region
-#pragma unroll
-  for (int j = 0; j < kCompactK; j++) {
-    const int dr = C[j].y1 - C[j].y0 - 6, cx0 = C[j].x0 + 3, width = C[j].x1 - 3 - cx0;  // <= 60
-    live[j] = c0 + j < ncells && dr > 0 && width > 0;
-    bits[j] = 0;
-    if (live[j] && lane < dr) {
-      const int sh = cx0 & 63;
-      const uint64_t* row = bitmaps + (int64_t)img * bm_words + C[j].bm_row0 + lane * C[j].bm_wpr;
-      uint64_t b = row[0] >> sh;
-      if (sh && sh + width > 64) b |= row[1] << (64 - sh);
-      bits[j] = b & (width >= 64 ? ~0ull : ((1ull << width) - 1));
-    }
-  }
-  // raster order: row prefix sum, then ascending x; an empty cell is queued for
-  // k_fast_fallback (which writes its count), a cell outside the detection region counts 0
-  int nout[kCompactK], fbq[kCompactK];  // fbq: fallback queue of an empty cell, else -1
-#pragma unroll
-  for (int j = 0; j < kCompactK; j++) {
-    nout[j] = 0;
-    fbq[j] = -1;
-    const int ci = c0 + j;
-    if (ci >= ncells) continue;
-    int* cnt_out = cell_counts + (int64_t)img * ncells + ci;
-    if (!live[j]) {
-      if (lane == 0) *cnt_out = 0;
-      continue;
-    }
-    uint64_t b = bits[j];
-    if (__ballot(b != 0) == 0) {  // no keypoint at iniThFAST: k_fast_fallback takes the cell
-      fbq[j] = C[j].fb_big;
-      continue;
-    }
-    const int cnt = __popcll(b);
-    const int incl = wave_scan_incl(cnt);
-    const int n = __shfl(incl, 63);  // <= slot_cap
-    if (lane == 0) *cnt_out = n;
-    if (n <= kCompactCap) {
-      nout[j] = n;
-      uint16_t* rc = s_rc[wid][j];
-      for (int pos = incl - cnt; b; b &= b - 1)
-        rc[pos++] = (uint16_t)((lane << 8) | __builtin_ctzll(b));
-    } else {  // rare: the row lanes write their keys themselves
-      const uint8_t* V = vmap + (int64_t)img * pyr_bytes + C[j].v_row0 + lane * C[j].pitch;
-      uint32_t* out = cand + (int64_t)img * cand_total + C[j].slot_off;
-      for (int pos = incl - cnt; b; b &= b - 1) {
-        const int k = __builtin_ctzll(b);
-        out[pos++] = cand_key(C[j].x0 + 3 + k, C[j].y0 + 3 + lane, (int)V[k]);
-      }
-    }
-  }
-  // the empty cells join queue fb_big of the image (lists of ncells entries): one atomic per
-  // queue and wave
-#pragma unroll
-  for (int bq = 0; bq < 2; bq++) {
-    int m = 0;
-#pragma unroll
-    for (int j = 0; j < kCompactK; j++) m += fbq[j] == bq;
-    if (m == 0) continue;
-    const int qi = 2 * img + bq;
-    int base = 0;
-    if (lane == 0) base = atomicAdd(fb_count + qi * kFbStride, m);
-    base = __shfl(base, 0);
-#pragma unroll
-    for (int j = 0; j < kCompactK; j++)
-      if (fbq[j] == bq) {
-        if (lane == 0) fb_list[(int64_t)qi * ncells + base] = c0 + j;
-        base++;
-      }
-  }
-  // round 3 (per 64 survivors of each LDS-staged cell): lane s takes survivor s of every cell,
-  // all V loads in flight, then the coalesced key stores
-  int nmax = 0;
-#pragma unroll
-  for (int j = 0; j < kCompactK; j++) nmax = max(nmax, nout[j]);
-  for (int s0 = 0; s0 < nmax; s0 += 64) {
-    const int si = s0 + lane;
-    uint32_t key[kCompactK];
-#pragma unroll
-    for (int j = 0; j < kCompactK; j++) {
-      key[j] = 0;
-      if (si < nout[j]) {
-        const int e = s_rc[wid][j][si], r = e >> 8, k = e & 0xFF;
-        const uint8_t* V = vmap + (int64_t)img * pyr_bytes + C[j].v_row0;
-        key[j] = cand_key(C[j].x0 + 3 + k, C[j].y0 + 3 + r, (int)V[r * C[j].pitch + k]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kCompactK; j++)
-      if (si < nout[j]) cand[(int64_t)img * cand_total + C[j].slot_off + si] = key[j];
-  }
-}
-
-// a CellGeom as dwords (moved between lanes with readlane)
-constexpr int kCellWords = (int)(sizeof(CellGeom) / 4);
-struct CellWords {
-  uint32_t w[kCellWords];
-};
-static_assert(sizeof(CellWords) == sizeof(CellGeom), "CellGeom is whole dwords");
-
-// ---- k_fast_fallback: the cells queued by k_fast_compact, one wave each (kFbWG workgroups
-// per image walk the queue): cv::FAST with NMS at minThFAST on the cell image
-// (ORBextractor.cc:782-784).  The ROI is staged in LDS; each detection row runs the even-point
-// pretest into a wave queue, the queued candidates are scored into a zero-ringed V map (pixels
-// outside the cell's detection region count as 0: the NMS is cell-local by construction) and
-// NMS'd, setting their bits in the keep rows that are compacted as above.
-// Cells at most 32 wide run two detection rows per wave step (half-wave each).
-// Instantiated for RS x MAXR staged windows: <44, 44> (cells up to 38 wide/high, the usual
-// 30-px grid) and <72, 66> (any cell, wCell / hCell < 60).
-constexpr int kFbWG = 16;  // workgroups per image
-template <int RS, int MAXR>
-__global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict__ pyr,
-                                                       int64_t pyr_bytes,
-                                                       const CellGeom* __restrict__ cells,
-                                                       int ncells, const int* __restrict__ fb_count,
-                                                       const int* __restrict__ fb_list, int min_th,
-                                                       uint32_t* __restrict__ cand, int cand_total,
-                                                       int* __restrict__ cell_counts) {
-  __shared__ __align__(16) uint8_t s_src[4][MAXR * RS + 16];
-  __shared__ __align__(16) uint8_t s_vv[4][(MAXR - 4) * RS];
-  constexpr int QCAP = (MAXR - 6) * (RS - 9);  // detection pixels of the largest cell
-  __shared__ uint16_t s_q[4][QCAP + 64];
-  __shared__ uint64_t s_rows[4][64];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int img = blockIdx.y;
-  const int qi = 2 * img + (RS > 44);  // this instance's queue (k_fast_compact)
-  const int nfb = fb_count[qi * kFbStride];
-  uint8_t* S = s_src[wid];
-  uint8_t* V = s_vv[wid];
-  uint16_t* q = s_q[wid];
-  const int t1 = max(min_th, 1);
-  const int wv = blockIdx.x * 4 + wid, nw = gridDim.x * 4;  // wave-uniform
-  for (int kb = wv; kb < nfb; kb += 64 * nw) {
-    // this wave's next (up to) 64 queued cells in one round of loads: lane j holds queue entry
-    // kb + j nw and its CellGeom; iteration `it` reads its cell's fields from lane it
-    const int kl = kb + lane * nw;
-    int cil = 0;
-    CellWords gw = {};
-    if (kl < nfb) {
-      cil = fb_list[(int64_t)qi * ncells + kl];
-      gw = ((const CellWords*)cells)[cil];
-    }
-    const int nit = min(64, (nfb - kb + nw - 1) / nw);
-    auto geom = [&](int it) {
-      CellWords cwd;
-#pragma unroll
-      for (int w = 0; w < kCellWords; w++) cwd.w[w] = __builtin_amdgcn_readlane(gw.w[w], it);
-      return __builtin_bit_cast(CellGeom, cwd);
-    };
-    // the ROI as aligned dwords (its first pixel lands at byte sh of each staged row; the 64-B
-    // pitch covers the last dword).  Lane l stages word l % kW of rows l / kW + kG u (fixed
-    // per lane: no division per item); lanes past the cell's words or rows load nothing.  When
-    // the staged window fits kPf such rounds the next cell's loads are issued before this cell
-    // is processed (their latency hides behind it) and land in LDS when it is done.
-    constexpr int kW = RS / 4, kG = 64 / kW;              // words per staged row, rows per round
-    constexpr int kPf = (MAXR + kG - 1) / kG;              // rounds for the largest ROI
-    constexpr bool kPrefetch = kPf <= 9;
-    const int lrow = lane / kW, lword = lane - lrow * kW;   // compile-time divisor
-    const bool lane_ok = lrow < kG;
-    uint32_t pv[kPrefetch ? kPf : 1];
-    int prow = 0, pmask = 0;  // rows of the staged cell; bit u: round u loaded
-    auto issue = [&](const CellGeom& C) {
-      const int cols = C.x1 - C.x0, rows = C.y1 - C.y0;
-      const int words = ((C.x0 & 3) + cols + 3) >> 2;
-      const uint8_t* srow = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - 3 * C.pitch - 3) +
-                            (C.x0 & ~3) - C.x0;  // staged row 0, word 0
-      pmask = 0;
-#pragma unroll
-      for (int u = 0; u < (kPrefetch ? kPf : 1); u++) {
-        const int r = lrow + kG * u;
-        if (lane_ok && lword < words && r < rows) {
-          pv[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(r, C.pitch) + 4 * lword);
-          pmask |= 1 << u;
-        }
-      }
-      prow = rows;
-    };
-    if (kPrefetch && nit > 0) issue(geom(0));
-    for (int it = 0; it < nit; it++) {
-      const int ci = __builtin_amdgcn_readlane(cil, it);
-      const CellGeom C = geom(it);
-      const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3 (fb_big)
-      const int dr = rows - 6, cw = cols - 6;            // > 0 (k_fast_compact)
-      const int sh = C.x0 & 3, words = (sh + cols + 3) >> 2;  // <= RS / 4
-      if constexpr (kPrefetch) {
-#pragma unroll
-        for (int u = 0; u < kPf; u++)
-          if ((pmask >> u) & 1) *(uint32_t*)(S + (lrow + kG * u) * RS + 4 * lword) = pv[u];
-        if (it + 1 < nit) issue(geom(it + 1));
-      } else {  // four rounds of loads in flight per lane
-        const uint8_t* srow = pyr + (int64_t)img * pyr_bytes + (C.v_row0 - 3 * C.pitch - 3) +
-                              (C.x0 & ~3) - C.x0;
-        for (int r0 = lrow; r0 < rows; r0 += 4 * kG) {
-          uint32_t v[4];
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            const int r = r0 + kG * u;
-            v[u] = (lane_ok && lword < words && r < rows)
-                       ? *(const uint32_t*)(srow + (uint32_t)__mul24(r, C.pitch) + 4 * lword)
-                       : 0u;
-          }
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            const int r = r0 + kG * u;
-            if (lane_ok && lword < words && r < rows) *(uint32_t*)(S + r * RS + 4 * lword) = v[u];
-          }
-        }
-      }
-      for (int i = lane; i < (dr + 2) * RS / 4; i += 64) ((uint32_t*)V)[i] = 0u;
-      const uint8_t* Sx = S + sh;  // pixel (r, c) of the ROI at Sx[r * RS + c]
-      const bool half = cw <= 32;  // wave-uniform
-      const int col = half ? lane & 31 : lane, sub = half ? 2 * (lane >> 5) : 0, step = half ? 4 : 2;
-      // every candidate of the cell stays queued (row << 6 | column): scored in batches of 64,
-      // then the NMS runs at the queued pixels only (all others have V = 0).  The pretest runs on
-      // row pairs (r, r + 1) per lane (fast_pretest2, dual-issue ops); a pair past the last
-      // detection row reads staged rows past the ROI, inside this workgroup's LDS, and is masked.
-      const uint32_t fm = col < cw ? 0x80008000u : 0u;
-      int nq = 0;
-      for (int r0 = 0; r0 < dr; r0 += step) {
-        const int r = r0 + sub;
-        const uint32_t f = fast_pretest2<RS>(Sx + r * RS + col, min_th) &
-                           fm & ((r < dr ? 0x8000u : 0u) | (r + 1 < dr ? 0x80000000u : 0u));
-        wave_enqueue(q, nq, QCAP, (f & 0x8000u) != 0, r * 64 + col, lane);
-        wave_enqueue(q, nq, QCAP, (int32_t)f < 0, (r + 1) * 64 + col, lane);
-      }
-      for (int j = lane; j < nq; j += 64) {
-        const int e = q[j], r = e >> 6, c = e & 63;
-        const int sc = fast_score(Sx, RS, c + 3, r + 3);
-        V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
-      }
-      if (lane < dr) s_rows[wid][lane] = 0;
-      // NMS at minThFAST; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
-      for (int j = lane; j < nq; j += 64) {
-        const int e = q[j], r = e >> 6, c = e & 63;
-        const uint8_t* p = V + (r + 1) * RS + c + 1;
-        const int v = p[0];
-        const int nmax = max(max(max((int)p[-RS - 1], (int)p[-RS]), max((int)p[-RS + 1], (int)p[-1])),
-                             max(max((int)p[1], (int)p[RS - 1]), max((int)p[RS], (int)p[RS + 1])));
-        if (v > (nmax > min_th ? nmax : t1))
-          atomicOr((unsigned long long*)&s_rows[wid][r], 1ull << c);
-      }
-      const uint64_t bits = lane < dr ? s_rows[wid][lane] : 0;
-      const uint8_t* Vr = V + (lane + 1) * RS + 1;
-      compact_rows(bits, lane, C.y0 + 3 + lane, C.x0 + 3,
-                   cand + (int64_t)img * cand_total + C.slot_off,
-                   cell_counts + (int64_t)img * ncells + ci, [&](int kk) { return (int)Vr[kk]; });
-    }
-  }
-}
-
 // ---- k_fast_cells: the whole per-cell FAST of ComputeKeyPointsOctTree (ORBextractor.cc:758-796)
 // in one wave per cell: the cell ROI is staged in the wave's LDS once; cv::FAST with NMS at
 // iniThFAST (:776-780) and, only if no keypoint survives, again at minThFAST on the same staged
@@ -1004,26 +540,16 @@ __global__ __launch_bounds__(256) void k_fast_fallback(const uint8_t* __restrict
 //  (2) cornerScore<16> (fast_score) of the queued pixels into a zero-ringed V map (V = score + 1
 //      clamped; every other pixel has V = 0, equivalent in the NMS to a score below t);
 //  (3) the strict 8-neighbour NMS at the queued pixels with V > t, setting keep bits per row.
-// Instantiated for RS x MAXR staged windows as k_fast_fallback: <44, 44> (cells up to 38 wide /
-// high) and <72, 66> (any cell); `list` holds the instance's cells.
+// Instantiated for RS x MAXR staged windows: <44, kFcSmallRows> (ROIs up to 41 wide with their
+// alignment slack, kFcSmallRows high: the usual ~30-px grid) and <72, kCellMax> (any cell);
+// `list` holds the instance's cells.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-#ifndef ORBX_FC_PAIR
-#define ORBX_FC_PAIR 1  // stage 1: two row-pair steps per LDS round trip
-#endif
-#ifndef ORBX_FC_MAXR
-#define ORBX_FC_MAXR 42  // rows of the small k_fast_cells instance's ROI (44: round 3's first form)
-#endif
-#ifndef ORBX_FC_ROWS_ALIAS
-#define ORBX_FC_ROWS_ALIAS 1  // keep rows in the staging buffer's slack (0: their own 512 B)
-#endif
-#ifndef ORBX_FC_SCORE2
-#define ORBX_FC_SCORE2 0  // scoring: two candidates per lane per round (measured slower: 0.637 vs 0.595 ms per 512 C2 frames)
-#endif
+constexpr int kFcSmallRows = 42;  // ROI rows of the small k_fast_cells instance (44 measured slower)
 // Stage 1 of one detection chunk (up to 8 steps of STEP rows per lane, two steps per LDS round
 // trip): the flags of step s end at bits 15 - 2 (nst - 1 - s) (row r) and 31 - 2 (...) (row
 // r + 1) of the returned word; the caller masks rows and columns outside the cell.
@@ -1032,14 +558,10 @@ __device__ __forceinline__ uint32_t cardinal_chunk(const uint8_t* c0, int nst, i
   uint32_t acc = 0;
   const uint8_t* c = c0;
   int s = 0;
-  if constexpr (ORBX_FC_PAIR) {
-    for (; s + 2 <= nst; s += 2, c += 2 * STEP * RS) {
-      uint32_t f0, f1;
-      fast_cardinal2x2<RS, STEP * RS>(c, t, f0, f1);
-      acc = (acc >> 4) | (f0 >> 2) | f1;
-    }
-  } else {
-    for (; s + 1 < nst; s++, c += STEP * RS) acc = (acc >> 2) | fast_cardinal2<RS>(c, t);
+  for (; s + 2 <= nst; s += 2, c += 2 * STEP * RS) {
+    uint32_t f0, f1;
+    fast_cardinal2x2<RS, STEP * RS>(c, t, f0, f1);
+    acc = (acc >> 4) | (f0 >> 2) | f1;
   }
   if (s < nst) acc = (acc >> 2) | fast_cardinal2<RS>(c, t);
   return acc;
@@ -1071,22 +593,14 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
   __shared__ __align__(16) uint8_t s_vv[4][(MAXR - 4) * RS];
   constexpr int QCAP = (MAXR - 6) * (RS - 9);  // detection pixels of the largest cell
   __shared__ uint16_t s_q[4][QCAP];
-#if ORBX_FC_ROWS_ALIAS
   // the keep bits per detection row live in the last 512 B of the wave's staging buffer: slack
   // rows past any ROI (the pretest reads them only masked; a cell is staged before its NMS and
   // its bits are in registers before the next cell is staged)
   static_assert((MAXR + 12) * RS - 512 >= MAXR * RS, "keep rows past every ROI row");
   static_assert(((MAXR + 12) * RS - 512) % 8 == 0, "keep rows 8-B aligned");
-#else
-  __shared__ uint64_t s_rows_sep[4][64];
-#endif
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if ORBX_FC_ROWS_ALIAS
   uint64_t* const krows = (uint64_t*)(s_src[wid] + (MAXR + 12) * RS - 512);
-#else
-  uint64_t* const krows = s_rows_sep[wid];
-#endif
   int bx, img;
   xcd_block(bx, img);
   const int l0 = (bx * 4 + wid) * cpw;
@@ -1172,22 +686,19 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         }
       }
       wave_sync();
-      // (2) scores of the queued pixels, two per lane per round so their loads overlap (a
-      // fallback pass rescores the iniThFAST ones: same value)
-      for (int j = lane; j < nq; j += ORBX_FC_SCORE2 ? 128 : 64) {
-        const int j2 = ORBX_FC_SCORE2 && j + 64 < nq ? j + 64 : j;
-        const int e0 = q[j], e1 = q[j2];
-        const int r0 = e0 >> 6, c0 = e0 & 63, r1 = e1 >> 6, c1 = e1 & 63;
-        const int sc0 = fast_score(Sx, RS, c0 + 3, r0 + 3);
-        V[(r0 + 1) * RS + c0 + 1] = (uint8_t)min(255, max(0, sc0 + 1));
-        if (ORBX_FC_SCORE2) {
-          const int sc1 = fast_score(Sx, RS, c1 + 3, r1 + 3);
-          V[(r1 + 1) * RS + c1 + 1] = (uint8_t)min(255, max(0, sc1 + 1));
-        }
+      // (2) scores of the queued pixels (a fallback pass rescores the iniThFAST ones: same
+      // value; two candidates per lane per round measured slower, 0.637 vs 0.595 ms per 512 C2
+      // frames)
+      for (int j = lane; j < nq; j += 64) {
+        const int e = q[j], r = e >> 6, c = e & 63;
+        const int sc = fast_score(Sx, RS, c + 3, r + 3);
+        V[(r + 1) * RS + c + 1] = (uint8_t)min(255, max(0, sc + 1));
       }
       krows[lane] = 0;
       wave_sync();
-      // (3) NMS at t; keep <=> V > (nmax > t ? nmax : max(t,1)) (see k_fast_tile)
+      // (3) cv::FAST's strict 8-neighbour NMS at t: a neighbour counts with its score V-1 only
+      // if it is a corner at t (V > t), and the count is monotone in V, so the largest
+      // neighbour decides: keep <=> V > (nmax > t ? nmax : max(t,1))
       const int t1 = max(t, 1);
       for (int j = lane; j < nq; j += 64) {
         const int e = q[j], r = e >> 6, c = e & 63;
@@ -1223,10 +734,7 @@ constexpr int kOctNTBig = 1024;       // for frames whose level-0 octree frame e
 constexpr int kOctBigArea = 1 << 20;  // kOctBigArea px: a workgroup holds ~100 KB of LDS there
                                       // (one per CU), so 1024 threads run its key passes 4x wide
 constexpr int kOctRegKeys = 16;       // keys per thread per register chunk
-#ifndef ORBX_OCT_BATCH
-#define ORBX_OCT_BATCH 8
-#endif
-constexpr int kOctBatch = ORBX_OCT_BATCH;  // node-info loads in flight per key pass round
+constexpr int kOctBatch = 8;          // node-info loads in flight per key pass round
 constexpr size_t kOctMaxSmem = 150 * 1024;  // dynamic LDS of one octree workgroup
 
 struct OctNodes {
@@ -1640,13 +1148,11 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
 // 256-thread instances: at least 6 waves per SIMD (the compiler's choice was 104 VGPRs, 4 waves;
 // 6 costs a few spilled registers and took C2's octree 0.154 -> 0.124 ms per 512 frames; 7 / 8
 // spill more and were slower); the 1024-thread instance keeps its registers (a cap slowed C5's
-// level-0 trees).  ORBX_OCT_WAVES overrides the floor for experiments.
-#ifndef ORBX_OCT_WAVES
-#define ORBX_OCT_WAVES 6
-#endif
+// level-0 trees).
+constexpr int kOctWaves = 6;
 template <int NT, class K>
 __global__ __launch_bounds__(NT)
-__attribute__((amdgpu_waves_per_eu(NT <= 256 ? ORBX_OCT_WAVES : 1)))
+__attribute__((amdgpu_waves_per_eu(NT <= 256 ? kOctWaves : 1)))
 void k_octree(
     const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
     const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
@@ -1921,15 +1427,10 @@ struct orbx_plan {
   BlurTile* d_tiles = nullptr;
   int ntiles = 0;
   PyrBand* d_bands = nullptr;
-  FastTile* d_ftiles = nullptr;
-  int nftiles = 0;
-  uint8_t* d_vmap = nullptr;
-  uint64_t* d_bitmaps = nullptr;
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
   // candidate keys, the octree's gathered keys and the retained keys: u32 or u64 (wide_keys)
   void *d_cand = nullptr, *d_lin = nullptr, *d_okey = nullptr;
   int *d_cell_counts = nullptr, *d_label = nullptr, *d_ocount = nullptr, *d_counts = nullptr;
-  int *d_fb_count = nullptr, *d_fb_list = nullptr;  // k_fast_fallback queue per image
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   // counts, keypoints and descriptors share one allocation (d_counts is its base) so the
@@ -1942,15 +1443,10 @@ struct orbx_plan {
   size_t oct_smem = 0, oct_smem_big = 0;
   int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;  // oct_cc* 0: cells in d_cell_scr
   int* d_cell_scr = nullptr;
-  int oct_nt = kOctNT;  // threads of the levels below oct_split (ORBX_OCT_NT_FEW: 512 for few-image plans)
   int cell_cap = 0;
-  bool has_fb_big = false;  // some cell's ROI needs k_fast_fallback<72, kCellMax>
-  // k_fast_cells: the cells of its <44, 44> and <72, kCellMax> instances
+  // k_fast_cells: the cells of its <44, kFcSmallRows> and <72, kCellMax> instances
   int *d_cells_small = nullptr, *d_cells_big = nullptr;
   int n_cells_small = 0, n_cells_big = 0;
-  bool fast_legacy = false;  // ORBX_FAST_LEGACY=1: k_fast_tile + k_fast_compact + k_fast_fallback
-  int fc_cpw = 0;            // ORBX_FC_CPW: k_fast_cells cells per wave (experiments; 0 = auto)
-  bool fast_pair = true;  // k_fast_tile pretest on row pairs (ORBX_FAST_PAIR=0: one row per lane)
   const uint8_t* last_in = nullptr;
   int last_n = 0;
   // graph cache keyed by (input pointer, batch)
@@ -2062,12 +1558,11 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
   const int L = g.nlevels;
   const int ncells = (int)g.cells.size();
   K *cand = (K*)P->d_cand, *lin = (K*)P->d_lin, *okey = (K*)P->d_okey;
-  if (ncells > 0 && !P->fast_legacy) {
+  if (ncells > 0) {
     // cells per wave: up to kCellsPerWave while the launch keeps >= 16 k waves in flight
-    int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
-    if (P->fc_cpw > 0) cpw = P->fc_cpw;
+    const int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
     if (P->n_cells_small > 0)
-      hipLaunchKernelGGL((k_fast_cells<44, ORBX_FC_MAXR, K>),
+      hipLaunchKernelGGL((k_fast_cells<44, kFcSmallRows, K>),
                          dim3((P->n_cells_small + 4 * cpw - 1) / (4 * cpw), n), dim3(256), 0,
                          P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
                          P->n_cells_small, ncells, g.ini_th, g.min_th, cand, g.cand_total,
@@ -2087,8 +1582,7 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
                        cand, g.cand_total, lin, P->d_label, okey, P->d_ocount,
                        g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0, P->d_cell_scr);
   if (P->oct_split < L) {
-    auto kern = P->oct_nt == 512 ? k_octree<512, K> : k_octree<kOctNT, K>;
-    hipLaunchKernelGGL(kern, dim3(n, L - P->oct_split), dim3(P->oct_nt), P->oct_smem,
+    hipLaunchKernelGGL((k_octree<kOctNT, K>), dim3(n, L - P->oct_split), dim3(kOctNT), P->oct_smem,
                        P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, cand,
                        g.cand_total, lin, P->d_label, okey, P->d_ocount, g.kp_total, L,
                        P->oct_nc, P->oct_cc, P->oct_split, P->d_cell_scr);
@@ -2106,9 +1600,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   const Geometry& g = P->g;
   Profiler dummy;
   Profiler& pr = prof ? *prof : dummy;
-  const int st_pyr = pr.stage("k_pyramid"),
-            st_blur = pr.stage("k_blur"), st_fs = pr.stage("k_fast_tile"),
-            st_fast = pr.stage("k_fast_compact"), st_fb = pr.stage("k_fast_fallback"),
+  const int st_pyr = pr.stage("k_pyramid"), st_blur = pr.stage("k_blur"),
             st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe"),
             st_fcell = pr.stage("k_fast_cells");
   pr.mark(P->stream, -1);
@@ -2121,28 +1613,6 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
     hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles);
     pr.mark(P->stream, st_blur);
-  }
-  const int ncells = (int)g.cells.size();
-  if (ncells > 0 && P->fast_legacy) {
-    uint32_t* cand = (uint32_t*)P->d_cand;  // (legacy plans are never wide_keys)
-    hipLaunchKernelGGL(P->fast_pair ? k_fast_tile<true> : k_fast_tile<false>, dim3(P->nftiles, n), dim3(256), 0, P->stream, P->d_pyr,
-                       g.pyr_bytes, P->d_vmap, P->d_bitmaps, g.bm_words, P->d_lv, P->d_ftiles,
-                       g.ini_th, P->d_fb_count);
-    pr.mark(P->stream, st_fs);
-    hipLaunchKernelGGL(k_fast_compact, dim3((ncells + 4 * kCompactK - 1) / (4 * kCompactK), n),
-                       dim3(256), 0, P->stream,
-                       P->d_vmap, g.pyr_bytes, P->d_bitmaps, g.bm_words, P->d_cells, ncells, cand, g.cand_total, P->d_cell_counts, P->d_fb_count,
-                       P->d_fb_list);
-    pr.mark(P->stream, st_fast);
-    hipLaunchKernelGGL((k_fast_fallback<44, 44>), dim3(kFbWG, n), dim3(256), 0, P->stream,
-                       P->d_pyr, g.pyr_bytes, P->d_cells, ncells, P->d_fb_count,
-                       P->d_fb_list, g.min_th, cand, g.cand_total, P->d_cell_counts);
-    if (P->has_fb_big)  // (a plan without such cells would launch waves that find the queue empty)
-      hipLaunchKernelGGL((k_fast_fallback<72, kCellMax>), dim3(kFbWG / 4, n), dim3(256), 0,
-                       P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, ncells,
-                       P->d_fb_count, P->d_fb_list, g.min_th, cand, g.cand_total,
-                       P->d_cell_counts);
-    pr.mark(P->stream, st_fb);
   }
   if (g.wide_keys)
     enqueue_keyed<uint64_t>(P, n, pr, st_fcell, st_oct, st_desc);
@@ -2175,13 +1645,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->params = *params;
   P->max_batch = max_batch;
   P->device = hip_device;
-  if (const char* e = getenv("ORBX_FAST_PAIR")) P->fast_pair = atoi(e) != 0;
-  if (const char* e = getenv("ORBX_FAST_LEGACY")) P->fast_legacy = atoi(e) != 0;
-  if (const char* e = getenv("ORBX_FC_CPW")) P->fc_cpw = std::max(0, std::min(kCellsPerWave, atoi(e)));
-  if (const char* e = getenv("ORBX_OCT_NT_FEW"))
-    if (max_batch <= kPyFewImages && atoi(e) == 512) P->oct_nt = 512;
   const Geometry& g = P->g;
-  for (const CellGeom& c : g.cells) P->has_fb_big |= c.fb_big != 0;
   auto fail = [&](int code) {
     orbx_plan_destroy(P);
     return code;
@@ -2200,48 +1664,29 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   for (const CellGeom& c : g.cells)
     if (c.x1 - c.x0 > kCellMax || c.y1 - c.y0 > kCellMax) return fail(ORBX_EUNSUPPORTED);
   P->ntiles = (int)tiles.size();
-  // FAST score tiles: those intersecting the detection region [19, w-19) x [19, h-19)
-  std::vector<FastTile> ftiles;
-  for (int l = 0; l < g.nlevels; l++) {
-    const LevelGeom& G = g.lv[l];
-    if (!G.ncells) continue;
-    for (int ty = 0; ty * kFastT < G.h; ty++)
-      for (int tx = 0; tx * kFastT < G.w; tx++) {
-        const int X0 = tx * kFastT, Y0 = ty * kFastT;
-        if (X0 + kFastT <= kEdge || X0 >= G.w - kEdge || Y0 + kFastT <= kEdge ||
-            Y0 >= G.h - kEdge)
-          continue;
-        ftiles.push_back({(int16_t)l, (int16_t)tx, (int16_t)ty, 0});
-      }
-  }
-  P->nftiles = (int)ftiles.size();
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
   std::vector<int> cells_small, cells_big;
   // a few-image plan runs every cell in the <72, kCellMax> instance: one launch instead of two
   // on the drop-in path's one-frame chain (either instance handles any cell)
   const bool one_fast_launch = max_batch <= kPyFewImages;
-  // the <44, ORBX_FC_MAXR> instance takes ROIs up to 41 + its alignment slack wide and
-  // ORBX_FC_MAXR rows high
+  // the <44, kFcSmallRows> instance takes ROIs up to 41 + its alignment slack wide and
+  // kFcSmallRows rows high
   for (int c = 0; c < (int)g.cells.size(); c++) {
     const CellGeom& C = g.cells[c];
-    const bool small = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= ORBX_FC_MAXR;
+    const bool small = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= kFcSmallRows;
     (small && !one_fast_launch ? cells_small : cells_big).push_back(c);
   }
   P->n_cells_small = (int)cells_small.size();
   P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;
-  if (g.wide_keys && P->fast_legacy) return fail(ORBX_EUNSUPPORTED);  // 32-bit keys only
   const size_t ksz = g.wide_keys ? 8 : 4;  // bytes per candidate key
   if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, g.cells.size()) ||
       dalloc(&P->d_xtap, g.xtap.size() / 2) || dalloc(&P->d_ytap, g.ytap.size() / 2) ||
-      dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_bands, g.bands.size()) || dalloc(&P->d_ftiles, ftiles.size()) ||
-      dalloc(&P->d_vmap, P->fast_legacy ? B * g.pyr_bytes : 1) ||
-      dalloc(&P->d_bitmaps, P->fast_legacy ? B * g.bm_words : 1) ||
+      dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_bands, g.bands.size()) ||
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
       dalloc((char**)&P->d_cand, B * g.cand_total * ksz) ||
       dalloc((char**)&P->d_lin, B * g.cand_total * ksz) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
-      dalloc(&P->d_fb_count, 2 * kFbStride * B) || dalloc(&P->d_fb_list, 2 * B * g.cells.size()) ||
       dalloc((char**)&P->d_okey, B * g.kp_total * ksz) || dalloc(&P->d_ocount, B * g.nlevels) ||
       dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_big, cells_big.size()))
     return fail(ORBX_ENOMEM);
@@ -2265,7 +1710,6 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       up(P->d_ytap, g.ytap.data(), 4 * g.ytap.size()) ||
       up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
       up(P->d_bands, g.bands.data(), sizeof(PyrBand) * g.bands.size()) ||
-      up(P->d_ftiles, ftiles.data(), sizeof(FastTile) * ftiles.size()) ||
       up(P->d_cells_small, cells_small.data(), 4 * cells_small.size()) ||
       up(P->d_cells_big, cells_big.data(), 4 * cells_big.size()))
     return fail(ORBX_EDEVICE);
@@ -2304,8 +1748,6 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   };
   if (P->oct_smem > attr_small) {
     if (!raise((const void*)k_octree<kOctNT, uint32_t>, (const void*)k_octree<kOctNT, uint64_t>,
-               P->oct_smem) ||
-        !raise((const void*)k_octree<512, uint32_t>, (const void*)k_octree<512, uint64_t>,
                P->oct_smem))
       return fail(ORBX_EDEVICE);
     attr_small = P->oct_smem;
@@ -2324,8 +1766,9 @@ int orbx_plan_destroy(orbx_plan* P) {
   ORBX_RESOURCE_LOCK;
   if (!P) return ORBX_OK;
   P->graphs.clear(P->stream);
-  void* ptrs[] = {P->d_lv,  P->d_cells, P->d_xtap,   P->d_ytap,  P->d_tiles, P->d_bands, P->d_ftiles, P->d_vmap, P->d_bitmaps, P->d_pyr,  P->d_blur,
-                  P->d_cand, P->d_lin,   P->d_okey,   P->d_cell_counts, P->d_label, P->d_fb_count, P->d_fb_list,
+  void* ptrs[] = {P->d_lv,   P->d_cells, P->d_xtap, P->d_ytap,        P->d_tiles, P->d_bands,
+                  P->d_pyr,  P->d_blur,  P->d_cand, P->d_lin,         P->d_okey,  P->d_cell_counts,
+                  P->d_label,
                   P->d_ocount, P->d_cells_small, P->d_cells_big, P->d_cell_scr,
                   P->d_counts /* base of kps and desc too */};
   for (void* p : ptrs)

@@ -188,12 +188,7 @@ int build_pyramid(Geometry* g, std::string* why) {
   // ~2 rows per level below the top, so stages stay short.
   g->pyr_stages.clear();
   g->bands.clear();
-  // LDS bound of a band's two level buffers (ORBX_PY_MAX_SMEM overrides, for tuning only)
-  static const int py_max_smem = [] {
-    const char* e = getenv("ORBX_PY_MAX_SMEM");
-    const int v = e ? atoi(e) : 0;
-    return v >= 4096 && v <= kPyMaxSmemLimit ? v : kPyMaxSmem;
-  }();
+  const int py_max_smem = kPyMaxSmem;  // LDS bound of a band's two level buffers
   for (int l0 = 1; l0 < nl;) {
     PyrStage st;
     st.l0 = l0;
@@ -268,7 +263,6 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
   g->ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
   g->min_th = std::min(std::max(p.min_th_fast, 0), 255);
   g->cells.clear();
-  g->bm_words = 0;
   g->wide_keys = false;
   for (int l = 0; l < p.nlevels; l++) {
     LevelGeom& L = g->lv[l];
@@ -293,9 +287,6 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
     const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
     L.cell_begin = (int)g->cells.size();
     L.cand_off = cand;
-    L.bm_wpr = L.pitch / 64;
-    L.bm_off = g->bm_words;
-    g->bm_words += (int64_t)L.bm_wpr * L.h;
     if (nCols > 0 && nRows > 0) {
       const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
       L.wcell = wCell;
@@ -318,16 +309,12 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
           c.offx = (int16_t)(j * wCell);
           c.offy = (int16_t)(i * hCell);
           c.level = (int16_t)l;
-          // k_fast_fallback instance: 0 = <44, 44>, 1 = <72, kCellMax>
-          c.fb_big = (int16_t)(c.x1 - c.x0 + 3 > 44 || c.y1 - c.y0 > 44);
           const int dc = c.x1 - c.x0 - 6, dr = c.y1 - c.y0 - 6;
           // strict 8-neighbour NMS survivors form an independent set of the king graph
           c.slot_cap = (dc > 0 && dr > 0) ? ((dc + 1) / 2) * ((dr + 1) / 2) : 0;
           c.slot_off = cand;
           cand += c.slot_cap;
-          c.bm_row0 = (int)(L.bm_off + (int64_t)(c.y0 + 3) * L.bm_wpr + ((c.x0 + 3) >> 6));
           c.v_row0 = (int)(L.pyr_off + (int64_t)(c.y0 + 3) * L.pitch + c.x0 + 3);
-          c.bm_wpr = (int16_t)L.bm_wpr;
           c.pitch = L.pitch;
           g->cells.push_back(c);
         }

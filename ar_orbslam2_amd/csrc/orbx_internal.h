@@ -26,39 +26,21 @@ constexpr int kHalfPatch = 15;  // HALF_PATCH_SIZE (:70)
 // k_pyramid: the levels are built in a few stages (one launch each); a stage splits every
 // image into row bands, one workgroup per (image, band) builds the stage's levels of its band
 // with the band's previous level held in LDS (two ping-pong buffers)
-#ifndef ORBX_PY_BANDH
-#define ORBX_PY_BANDH 32
-#endif
-#ifndef ORBX_PY_NT
-#define ORBX_PY_NT 512
-#endif
-#ifndef ORBX_PY_STAGE0
-#define ORBX_PY_STAGE0 3
-#endif
-#ifndef ORBX_PY_STAGEN
-#define ORBX_PY_STAGEN 4
-#endif
-constexpr int kPyBandH = ORBX_PY_BANDH;  // source-level rows per band (more if LDS is short)
-#ifndef ORBX_PY_BANDH_SMALL
-#define ORBX_PY_BANDH_SMALL 8
-#endif
+constexpr int kPyBandH = 32;  // source-level rows per band (more if LDS is short)
 // plans of at most kPyFewImages images (the drop-in extractor's batch of 1) use short bands:
 // more workgroups for one image's latency-chained level builds
-constexpr int kPyBandHSmall = ORBX_PY_BANDH_SMALL;
+constexpr int kPyBandHSmall = 8;
 constexpr int kPyFewImages = 4;
-constexpr int kPyNT = ORBX_PY_NT;        // k_pyramid threads per workgroup
-constexpr int kPyStage0 = ORBX_PY_STAGE0;  // levels built by the first stage (from the input)
-constexpr int kPyStageN = ORBX_PY_STAGEN;  // levels per later stage (from the pyramid)
+constexpr int kPyNT = 512;     // k_pyramid threads per workgroup
+constexpr int kPyStage0 = 3;   // levels built by the first stage (from the input)
+constexpr int kPyStageN = 4;   // levels per later stage (from the pyramid)
 // k_pyramid dynamic LDS bound (both buffers): bands are narrowed until they fit.  40 KB keeps
 // four workgroups per CU; the 64 KB this was measured C4's pyramid at 0.76 vs 0.62 ms per 256
 // frames (wide 1241-px rows: two workgroups per CU), C2 0.31 vs 0.30 ms (32 KB: C4 0.65,
 // 24 KB: more recomputed band cones, C4 0.76)
 constexpr int kPyMaxSmem = 40 * 1024;
 constexpr int kPyMaxSmemLimit = 64 * 1024;
-#ifndef ORBX_PY_STRIP
-#define ORBX_PY_STRIP 4
-#endif
-constexpr int kPyStrip = ORBX_PY_STRIP;  // k_pyramid output rows per work item
+constexpr int kPyStrip = 4;    // k_pyramid output rows per work item (2: 170, 8: 184 vs 166 us)
 struct PyrBand {
   int lo[kMaxLevels], hi[kMaxLevels];      // rows of each level this band computes (with halo)
   int own_lo[kMaxLevels], own_hi[kMaxLevels];  // rows it writes to the pyramid (a partition)
@@ -79,8 +61,6 @@ struct LevelGeom {
   int bxs;             // SymmColumnVec_32s8u region: x < 4*floor(w/4)
   int cell_begin, ncells;  // range in the cell table
   int wcell, hcell;        // FAST cell size (ORBextractor.cc:755-756)
-  int64_t bm_off;          // FAST keep bitmaps (u64 words) inside one image's bitmap block
-  int bm_wpr;              // bitmap words per row (pitch / 64)
   int cand_off, cand_cap;  // candidate region (keys) inside one image's candidate block
   int nfeat;               // mnFeaturesPerLevel
   int nini;                // DistributeOctTree initial columns
@@ -96,16 +76,14 @@ struct LevelGeom {
 struct CellGeom {
   int16_t x0, y0, x1, y1;  // cell image ROI in level coordinates [x0,x1) x [y0,y1)
   int16_t offx, offy;      // j*wCell, i*hCell (ORBextractor.cc:789-790)
-  int16_t level, fb_big;   // fb_big: ROI too large for k_fast_fallback<44, 44>
+  int16_t level, pad16;
   int slot_off, slot_cap;  // candidate slot inside the image's candidate block
-  // k_fast_compact addressing of the first detection row (per image): its keep-bitmap word
-  // holding column x0 + 3, and its V byte at column x0 + 3; with the level's row strides
-  int bm_row0, v_row0;
-  int16_t bm_wpr, pad16;
+  int v_row0;              // offset of the ROI's first detection pixel (x0 + 3, y0 + 3) in the
+                           // image's pyramid block
   int pitch;  // a whole aligned dword: k_fast_cells reads the next cell's geometry with scalar
               // loads (an int16 field here became a vector load whose wait it exposed per cell)
 };
-static_assert(sizeof(CellGeom) == 40, "CellGeom layout");
+static_assert(sizeof(CellGeom) == 32, "CellGeom layout");
 
 struct Geometry {
   int w = 0, h = 0, nlevels = 0;
@@ -121,7 +99,6 @@ struct Geometry {
   int64_t pyr_bytes = 0;              // per image
   std::vector<PyrStage> pyr_stages;   // k_pyramid launches, in order
   std::vector<PyrBand> bands;         // every stage's row bands
-  int64_t bm_words = 0;               // per image: the iniThFAST keep plane of every level
   int cand_total = 0;                 // per image candidate keys
   int kp_total = 0;                   // per image final keypoint slots
   int node_cap_max = 0;

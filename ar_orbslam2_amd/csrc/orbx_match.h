@@ -93,11 +93,9 @@ constexpr int ORBX_DEVERR_INDEX = 2;
 // candidates per vocabulary node whose vbMatched2 flags k_bow_nodes keeps in a per-lane register
 // bitmap (64 chunks of 64); larger nodes keep them in global memory
 constexpr int kBowRegCands = 64 * 64;
-// k_bow_nodes: candidate chunks of 64 kept in registers for a whole node (8 VGPRs each)
-#ifndef ORBX_BOW_CHUNKS
-#define ORBX_BOW_CHUNKS 2
-#endif
-constexpr int kBowDescChunks = ORBX_BOW_CHUNKS;
+// k_bow_nodes: candidate chunks of 64 kept in registers for a whole node (8 VGPRs each; 1 or 4
+// measured no faster at C2, and the wide-node instance keeps 4)
+constexpr int kBowDescChunks = 2;
 // SearchByBoW's wave merge packs (best distance, node position) into 32 bits: side 2 of a
 // problem holds fewer than 2^23 features (the entry points reject more)
 constexpr int kBowMaxSide2 = 1 << 23;

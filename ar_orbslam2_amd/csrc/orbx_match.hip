@@ -1014,18 +1014,10 @@ constexpr int kBowWgProbs = 4;
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
                bool fused_finish, int feats_per_node) {
   if (nprob <= 0) return ORBX_OK;
-  static const int wg_probs = [] {
-    const char* e = getenv("ORBX_BOW_WG_PROBS");
-    return e ? atoi(e) : kBowWgProbs;
-  }();
-  static const int wide_node = [] {  // ORBX_BOW_WIDE_NODE overrides kBowWideNode (experiments)
-    const char* e = getenv("ORBX_BOW_WIDE_NODE");
-    return e ? atoi(e) : kBowWideNode;
-  }();
-  const bool wg = max_nodes1 > 0 && nprob <= wg_probs;
+  const bool wg = max_nodes1 > 0 && nprob <= kBowWgProbs;
   if (wg)
     hipLaunchKernelGGL(k_bow_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
-  else if (max_nodes1 > 0 && feats_per_node >= wide_node)
+  else if (max_nodes1 > 0 && feats_per_node >= kBowWideNode)
     hipLaunchKernelGGL(k_bow_nodes<4>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
   else if (max_nodes1 > 0)
     hipLaunchKernelGGL(k_bow_nodes<kBowDescChunks>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256),
@@ -1043,11 +1035,7 @@ constexpr int kTriWgProbs = 4;
 int launch_tri(const TriProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
                bool fused_finish) {
   if (nprob <= 0) return ORBX_OK;
-  static const int wg_probs = [] {
-    const char* e = getenv("ORBX_TRI_WG_PROBS");
-    return e ? atoi(e) : kTriWgProbs;
-  }();
-  const bool wg = max_nodes1 > 0 && nprob <= wg_probs;
+  const bool wg = max_nodes1 > 0 && nprob <= kTriWgProbs;
   if (wg)
     hipLaunchKernelGGL(k_tri_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
   else if (max_nodes1 > 0)

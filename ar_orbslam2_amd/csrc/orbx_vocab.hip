@@ -668,11 +668,7 @@ int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word
                  int64_t out_stride, int* d_nwords, int nb, const uint32_t* d_rank_ids,
                  uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride, int* d_nn,
                  int nimg, hipStream_t s) {
-  static const bool enabled = [] {
-    const char* e = getenv("ORBX_BOWFV");
-    return !e || atoi(e) != 0;
-  }();
-  if (!enabled || !d_rank_ids || nb < 1) return ORBX_EUNSUPPORTED;
+  if (!d_rank_ids || nb < 1) return ORBX_EUNSUPPORTED;
   if (nimg <= 0) return ORBX_OK;
   const int must = scoring != ORBX_SCORE_DOT_PRODUCT;
   const int l1 = scoring != ORBX_SCORE_L2;

@@ -83,9 +83,6 @@ def algorithmic_bytes(levels, n_kp, n_img):
         # SURVEY §8d's FAST term: every level pixel read once (the per-cell kernel writes only
         # the cells' keys, 4 B per candidate, ~1 % of the pixels: not counted)
         "k_fast_cells": sum(P) * n_img,
-        # the round-2 tile path (ORBX_FAST_LEGACY=1), same model
-        "k_fast_tile": sum(P) * n_img,
-        "k_fast_compact": sum(P) * n_img / 8,                   # 1 NMS bit per pixel
         "k_describe": 60 * n_kp,
         "k_voc_transform": 52 * n_kp,                          # desc in; word, rank, node, weight out
         "k_bowvec": 24 * n_kp,
@@ -94,9 +91,9 @@ def algorithmic_bytes(levels, n_kp, n_img):
 
 
 # bytes per lane of the global loads of the kernels bench.py can name as roofline kernel (the
-# staged windows of k_fast_tile and k_cvfast: 16-B pieces per lane; k_fast_cells: the cell ROI
-# as aligned dwords); the stores are 8-B bitmap words / 1-B scores (tile) and 4-B keys (cells)
-LOAD_WIDTH = {"k_fast_tile": 16, "k_cvfast": 16, "k_fast_cells": 4}
+# staged windows of k_cvfast: 16-B pieces per lane; k_fast_cells: the cell ROI as aligned
+# dwords); the stores are 8-B bitmap words (k_cvfast) and 4-B keys (k_fast_cells)
+LOAD_WIDTH = {"k_cvfast": 16, "k_fast_cells": 4}
 
 
 def _load_json(name):
@@ -107,7 +104,8 @@ def _load_json(name):
 
 
 def _kname_is(name, kernel):
-    """rocprofv3 Kernel_Name 'void orbx::k_fast_tile<true>(...)' is kernel 'k_fast_tile'."""
+    """rocprofv3 Kernel_Name 'void orbx::k_fast_cells<44, 42, unsigned int>(...)' is kernel
+    'k_fast_cells'."""
     return name.split("(")[0].split("<")[0].endswith("::" + kernel)
 
 
@@ -242,9 +240,7 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     return out
 
 
-EXTRACT_STAGES = ("k_pyramid", "k_blur", "k_fast_cells", "k_fast_tile", "k_fast_compact",
-                  "k_fast_fallback",
-                  "k_octree", "k_describe", "k_cvfast", "k_cvselect", "k_cvdescribe")
+EXTRACT_STAGES = ("k_pyramid", "k_blur", "k_fast_cells", "k_octree", "k_describe", "k_cvfast", "k_cvselect", "k_cvdescribe")
 
 
 def phase_split(stages, steps, B):

@@ -104,7 +104,7 @@ def test_level_counts_and_scales(nlevels, scale, w, h):
 @pytest.mark.parametrize("contrast", [3, 5, 8])
 def test_min_threshold_fallback_cells(contrast):
     """Low-contrast texture (left half) next to full contrast: many cells find nothing at
-    iniThFAST and retry at minThFAST (k_fast_fallback), the others do not."""
+    iniThFAST and retry at minThFAST (k_fast_cells' second pass), the others do not."""
     img = synth.frame(640, 480, t=1, stream=2).astype(np.int32)
     img[:, :320] = 128 + (img[:, :320] - 128) // contrast
     kps = _compare(img.astype(np.uint8), 1000)
@@ -159,9 +159,9 @@ def test_blur_every_pixel_matches_oracle(w, h, kind):
 
 @pytest.mark.parametrize("w,h", [(640, 480), (1241, 376)])
 def test_dense_corner_pattern_fills_pretest_queues(w, h):
-    """Every level-0 pixel of the detection region is a pretest candidate, so each wave of
-    k_fast_tile enqueues every pixel of its rows plus its ring share: the per-wave queue bound
-    must hold that (the row-pair schedule puts 18 rows + 64 ring pixels on wave 0)."""
+    """Every level-0 pixel of the detection region is a pretest candidate, so k_fast_cells
+    queues every detection pixel of a cell: the per-wave queue bound (the cell's detection
+    pixels) must hold that."""
     img = synth.dense_corners(w, h)
     _compare(img, 1000)
     # the same texture on half the frame next to a flat region (fallback cells beside full ones)

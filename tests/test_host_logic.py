@@ -129,7 +129,7 @@ def test_bench_extract_vs_match_split():
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    st = {"k_pyramid": (1.0, 5), "k_fast_tile": (2.0, 5), "k_describe": (1.0, 5),
+    st = {"k_pyramid": (1.0, 5), "k_fast_cells": (2.0, 5), "k_describe": (1.0, 5),
           "k_voc_transform": (0.5, 5), "k_bow": (0.5, 5), "k_stereo": (1.0, 5)}
     s = bench.phase_split(st, 5, 256)
     assert s["extract_ms_per_batch"] == pytest.approx(0.8)
