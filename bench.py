@@ -199,9 +199,11 @@ AGGREGATE_STAGES = ("k_stereo", "k_bow", "k_tri")
 
 def roofline_of(stages, alg, pmc_dir, steps, B):
     """Roofline object of the dominant kernel (largest total time in the per-kernel HIP-event
-    pass).  The path is integer stencil / gather / popcount work: VALU issue bounds it, so
-    `bound` is "valu" and frac is the VALU-issue fraction when the SQ pass of this command
-    exists; the HBM fraction (algorithmic bytes / launch time vs 8 TB/s) is reported beside it."""
+    pass), in the contract's terms: `bound` "hbm", `achieved` = SURVEY §8d's algorithmic bytes
+    per launch / the average launch time, `peak` 8 TB/s, `frac` = achieved / peak.  The path is
+    integer stencil / gather / popcount work whose binding ceiling is instruction issue, not
+    bytes: that roofline (VALU / SALU quad-cycles per launch from the SQ counters of this command
+    against the issue rate of 1024 SIMDs) is reported beside it in `issue_roofline`."""
     # stages not launched in this configuration (the other FAST path) are dropped
     stages = {k: v for k, v in stages.items() if v[1] > 0}
     # stages that time several kernels (the stereo copy + 3 kernels, the matchers' node and
@@ -223,15 +225,13 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     out = {"bound": "hbm", "kernel": dom, **hbm, "traffic": traffic, "traffic_note": tnote,
            "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": a_bytes}
     if issue:
-        # issue-rate roofline in the contract's fields (achieved / peak in SIMD quad-cycles of
-        # the binding unit per second); the HBM one kept under "hbm"
+        # the issue-rate roofline (achieved / peak in SIMD quad-cycles of the binding unit per
+        # second)
         qc = (issue["valu_quad_cycles_per_launch"] if issue["issue_bound"] == "valu"
               else issue["salu_instr_per_launch"])
         peak_gqc = VALU_SIMDS * CLOCK_GHZ / 4  # G SIMD quad-cycles per second
-        out.update({"bound": issue["issue_bound"], "achieved": round(qc / avg_s / 1e9, 3),
-                    "peak": round(peak_gqc, 3),
-                    "unit": f"G {issue['issue_bound'].upper()} issue quad-cycles/s",
-                    "frac": issue["frac"], "hbm": hbm})
+        issue = dict(issue, achieved=round(qc / avg_s / 1e9, 3), peak=round(peak_gqc, 3),
+                     unit=f"G {issue['issue_bound'].upper()} issue quad-cycles/s")
     out["issue_roofline"] = issue
     out["stages_ms_per_step"] = {k: round(v[0] / steps, 4) for k, v in stages.items()}
     out["stages_of"] = (f"roofline pass: camera stream 0 alone, {steps} steps of {B} frames "
