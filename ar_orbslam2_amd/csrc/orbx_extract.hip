@@ -721,6 +721,230 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
   }
 }
 
+// ---- k_fast_pairs: two horizontally adjacent FAST cells of one cell row per wave.  Cell j's
+// ROI ends 3 px past its detection columns, where cell j + 1's detection columns begin
+// (ORBextractor.cc:766-773: iniX = minBorderX + j wCell, maxX = iniX + wCell + 6), so the two
+// cells' detection columns are contiguous and one staged ROI of up to 70 x 42 px serves both:
+// the cardinal pretest runs on all 64 lanes (one detection column each, cwA + cwB <= 64) instead
+// of the 31-32 lanes of a single ~31-px cell, the candidates of both cells share the scoring and
+// NMS rounds, and staging, the V map, the scans and the compaction are paid once per pair.  The
+// NMS stays cell-local: the V map holds a zero column between the two cells' columns (and the
+// zero ring around them), so a neighbour across the cell edge counts as 0, as on the reference's
+// per-cell ROI.  A cell without a keypoint at iniThFAST runs FAST again at minThFAST on its own
+// columns (:782-784); each cell's survivors go to its own slot in raster order.
+// Queue entries: (detection row r) << 6 | column c.  A pass whose candidates outgrow the queue
+// (dense texture) scores the rest in place, lane by lane, and then runs the NMS over the V map
+// instead of the queue (same result: the NMS candidates are the pixels with V > t).
+constexpr int kPairRS = 76;                          // staged ROI row: <= 70 px + 3 alignment
+constexpr int kPairRows = kFcSmallRows;              // ROI rows (detection rows <= 36)
+constexpr int kPairStage = 13;                       // staging rounds of 64 dwords (43.8 rows)
+constexpr int kPairSrc = kPairRS * (kPairRows + 6);  // + the keep rows (krows)
+constexpr int kPairKeepRows = 40;                    // >= detection rows
+constexpr int kPairVS = 72;                          // V row: ring, cwA, gap, cwB, ring
+constexpr int kPairVRows = kPairRows - 4;            // detection rows + 2 ring rows
+constexpr int kPairQ = 768;                          // queue entries
+constexpr int kPairsPerWave = 4;
+static_assert(kPairStage * 256 >= kPairRows * kPairRS, "staging covers the ROI");
+static_assert(kPairStage * 256 <= kPairSrc - 8 * kPairKeepRows, "keep rows past the staged bytes");
+static_assert(kPairKeepRows >= kPairRows - 6, "a keep row per detection row");
+static_assert((kPairVS * kPairVRows) % 16 == 0, "V map in 16-B pieces");
+
+// Stage 1 of one detection chunk on all 64 lanes: rows r0 + 2 s and r0 + 2 s + 1 for steps
+// s < nst <= 16, two steps per LDS round trip; the flags of step s end at bit s (row r0 + 2 s)
+// and bit 16 + s (row r0 + 2 s + 1).
+template <int RS>
+__device__ __forceinline__ uint32_t cardinal_chunk16(const uint8_t* c0, int nst, int t) {
+  uint32_t acc = 0;
+  const uint8_t* c = c0;
+  int s = 0;
+  for (; s + 2 <= nst; s += 2, c += 4 * RS) {
+    uint32_t f0, f1;
+    fast_cardinal2x2<RS, 2 * RS>(c, t, f0, f1);
+    acc = (acc >> 2) | (f0 >> 1) | f1;
+  }
+  if (s < nst) acc = (acc >> 1) | fast_cardinal2<RS>(c, t);
+  return acc >> (16 - nst);
+}
+
+template <class K>
+__global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ pyr,
+                                                    int64_t pyr_bytes,
+                                                    const CellGeom* __restrict__ cells,
+                                                    const int2* __restrict__ pairs, int npairs,
+                                                    int ncells, int ini_th, int min_th,
+                                                    K* __restrict__ cand, int cand_total,
+                                                    int* __restrict__ cell_counts, int ppw) {
+  __shared__ __align__(16) uint8_t s_src[4][kPairSrc];
+  __shared__ __align__(16) uint8_t s_vv[4][kPairVS * kPairVRows];
+  __shared__ uint16_t s_q[4][kPairQ];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bx, img;
+  xcd_block(bx, img);
+  const int p0 = (bx * 4 + wid) * ppw;
+  if (p0 >= npairs) return;  // wave-uniform; no workgroup barrier below
+  const int p1 = min(p0 + ppw, npairs);
+  uint8_t* S = s_src[wid];
+  uint8_t* V = s_vv[wid];
+  uint16_t* q = s_q[wid];
+  // keep bits per detection row: the end of the staging buffer, past every staged byte (the
+  // pretest reads rows up to dr + 6 <= 42: inside the staged bytes)
+  uint64_t* const krows = (uint64_t*)(S + kPairSrc - 8 * kPairKeepRows);
+  const uint8_t* pimg = pyr + (int64_t)img * pyr_bytes;
+  // ROI staging: dword lane + 64 u of the staged rows (row (lane + 64 u) / 19, word % 19), so
+  // every lane loads and stores every round; rows past the ROI read its last row (clamped),
+  // words past the ROI's last one read on into the pitch (never used: stage 1 masks their
+  // flags, scores read detection pixels' windows only)
+  constexpr int kW = kPairRS / 4;
+  int srow[kPairStage], swof[kPairStage];
+#pragma unroll
+  for (int u = 0; u < kPairStage; u++) {
+    const int i = lane + 64 * u;
+    srow[u] = i / kW;
+    swof[u] = 4 * (i - kW * srow[u]);
+  }
+  uint32_t pv[kPairStage];
+  auto issue = [&](const CellGeom& A) {
+    const int last = A.y1 - A.y0 - 1;
+    const uint8_t* src = pimg + (A.v_row0 - 3 * A.pitch - 3) + (A.x0 & ~3) - A.x0;
+#pragma unroll
+    for (int u = 0; u < kPairStage; u++)
+      pv[u] = *(const uint32_t*)(src + (uint32_t)(__mul24(min(srow[u], last), A.pitch) + swof[u]));
+  };
+  int2 pr = pairs[p0];
+  CellGeom A = cells[pr.x], B = cells[pr.y];
+  issue(A);
+  for (int pi = p0; pi < p1; pi++) {
+    wave_sync();  // the previous pair's reads of S are done
+#pragma unroll
+    for (int u = 0; u < kPairStage; u++) *(uint32_t*)(S + 256 * u + 4 * lane) = pv[u];
+    const CellGeom Ac = A, Bc = B;
+    const int2 pc = pr;
+    if (pi + 1 < p1) {  // the next pair's loads in flight while this one is processed
+      pr = pairs[pi + 1];
+      A = cells[pr.x];
+      B = cells[pr.y];
+      issue(A);
+    }
+    const int dr = Ac.y1 - Ac.y0 - 6;                      // detection rows, both cells
+    const int cwA = Ac.x1 - Ac.x0 - 6, cw = cwA + (Bc.x1 - Bc.x0 - 6);  // detection columns
+    for (int i = lane; i < (dr + 2) * (kPairVS / 16); i += 64) ((uint4*)V)[i] = make_uint4(0u, 0u, 0u, 0u);
+    wave_sync();
+    const uint8_t* Sx = S + (Ac.x0 & 3);  // pixel (r, c) of the ROI at Sx[r * RS + c]
+    const uint64_t mA = (1ull << cwA) - 1;  // cwA <= 60
+    const uint64_t mB = (cw >= 64 ? ~0ull : (1ull << cw) - 1) & ~mA;
+    // V byte of detection pixel (r, c): one ring row and column, the gap column after cell A
+    auto vofs = [&](int r, int c) { return __mul24(r + 1, kPairVS) + c + 1 + (c >= cwA ? 1 : 0); };
+    auto score_at = [&](int r, int c) {
+      const int sc = fast_score(Sx, kPairRS, c + 3, r + 3);
+      V[vofs(r, c)] = (uint8_t)min(255, max(0, sc + 1));
+    };
+    uint64_t allow = mA | mB;  // the columns this pass detects on
+    uint64_t bits1 = 0, keep1 = 0;
+    uint64_t bits = 0;  // this lane's keep row (lane = detection row)
+    int t = ini_th;
+    for (int pass = 0; pass < 2; pass++) {
+      // (1) cardinal pretest at t, the flagged pixels queued (or scored in place past kPairQ)
+      const bool col_ok = (allow >> lane) & 1;
+      int nq = 0;
+      bool dense = false;
+      for (int rc = 0; rc < dr; rc += 32) {
+        const int nst = min(16, (dr - rc + 1) >> 1);  // wave-uniform
+        const int nodd = min(16, (dr - rc) >> 1);     // steps whose second row is a detection row
+        uint32_t acc = cardinal_chunk16<kPairRS>(Sx + rc * kPairRS + lane, nst, t);
+        acc &= col_ok ? (((1u << nst) - 1u) | (((1u << nodd) - 1u) << 16)) : 0u;
+        const int cnt = __popc(acc);
+        const int incl = wave_scan_incl(cnt);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        if (nq + tot > kPairQ) {  // wave-uniform, rare: score this chunk's pixels in place
+          dense = true;
+          while (acc) {
+            const int b = __builtin_ctz(acc);
+            acc &= acc - 1;
+            score_at(rc + 2 * (b & 15) + (b >> 4), lane);
+          }
+          continue;
+        }
+        int pos = nq + incl - cnt;
+        nq += tot;
+        while (acc) {
+          const int b = __builtin_ctz(acc);
+          acc &= acc - 1;
+          q[pos++] = (uint16_t)(((rc + 2 * (b & 15) + (b >> 4)) << 6) | lane);
+        }
+      }
+      wave_sync();
+      // (2) cornerScore of the queued pixels (a fallback pass rescores its cell's iniThFAST
+      // candidates: same value)
+      for (int j = lane; j < nq; j += 64) {
+        const int e = q[j];
+        score_at(e >> 6, e & 63);
+      }
+      if (lane < kPairKeepRows) krows[lane] = 0;
+      wave_sync();
+      // (3) the strict 8-neighbour NMS at t: keep <=> V > (nmax > t ? nmax : max(t,1)), the
+      // largest neighbour deciding (k_fast_cells)
+      const int t1 = max(t, 1);
+      auto keep_at = [&](int r, int c) -> bool {
+        const uint8_t* p = V + vofs(r, c);
+        const int v = p[0];
+        if (v <= t1) return false;
+        const int nmax =
+            max(max(max((int)p[-kPairVS - 1], (int)p[-kPairVS]), max((int)p[-kPairVS + 1], (int)p[-1])),
+                max(max((int)p[1], (int)p[kPairVS - 1]), max((int)p[kPairVS], (int)p[kPairVS + 1])));
+        return v > (nmax > t ? nmax : t1);
+      };
+      if (!dense) {
+        for (int j = lane; j < nq; j += 64) {
+          const int e = q[j], r = e >> 6, c = e & 63;
+          if (keep_at(r, c)) atomicOr((unsigned long long*)&krows[r], 1ull << c);
+        }
+        wave_sync();
+        bits = lane < dr ? krows[lane] : 0;
+      } else {  // some candidates were not queued: every pixel of this lane's row (rare)
+        bits = 0;
+        if (lane < dr)
+          for (int c = 0; c < cw; c++)
+            if (((allow >> c) & 1) && keep_at(lane, c)) bits |= 1ull << c;
+      }
+      bits &= allow;
+      if (pass == 1) {
+        bits |= bits1 & keep1;
+        break;
+      }
+      const bool hasA = __ballot((bits & mA) != 0) != 0, hasB = __ballot((bits & mB) != 0) != 0;
+      if ((hasA && hasB) || t == min_th) break;  // every cell has keypoints, or no retry left
+      // a cell without keypoints at iniThFAST: FAST again at minThFAST on its columns
+      bits1 = bits;
+      keep1 = (hasA ? mA : 0) | (hasB ? mB : 0);
+      allow = (hasA ? 0 : mA) | (hasB ? 0 : mB);
+      t = min_th;
+    }
+    // (4) each cell's survivors to its slot in raster order: one packed scan of the two counts
+    const int nA = __popcll(bits & mA), nB = __popcll(bits & mB);
+    const int packed = nA | (nB << 16);
+    const int incl = wave_scan_incl(packed);
+    const int tot = __builtin_amdgcn_readlane(incl, 63);
+    if (lane == 0) {
+      cell_counts[(int64_t)img * ncells + pc.x] = tot & 0xFFFF;
+      cell_counts[(int64_t)img * ncells + pc.y] = tot >> 16;
+    }
+    int posA = (incl - packed) & 0xFFFF, posB = (incl - packed) >> 16;
+    K* outA = cand + (int64_t)img * cand_total + Ac.slot_off;
+    K* outB = cand + (int64_t)img * cand_total + Bc.slot_off;
+    const int y = Ac.y0 + 3 + lane, x0 = Ac.x0 + 3;
+    const uint8_t* Vr = V + __mul24(lane + 1, kPairVS) + 1;
+    while (bits) {
+      const int c = __builtin_ctzll(bits);
+      bits &= bits - 1;
+      const bool inA = c < cwA;
+      const K key = KeyFmt<K>::make(x0 + c, y, (int)Vr[c + (inA ? 0 : 1)]);
+      if (inA) outA[posA++] = key;
+      else outB[posB++] = key;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ k_octree
 // ORBextractor::DistributeOctTree (ORBextractor.cc:525-733) for one (image, level) per
 // workgroup.  The std::list is represented by node arrays kept in list order in LDS:
@@ -1444,7 +1668,10 @@ struct orbx_plan {
   int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;  // oct_cc* 0: cells in d_cell_scr
   int* d_cell_scr = nullptr;
   int cell_cap = 0;
-  // k_fast_cells: the cells of its <44, kFcSmallRows> and <72, kCellMax> instances
+  // k_fast_pairs: adjacent cell pairs; k_fast_cells: the other cells, in its <44,
+  // kFcSmallRows> and <72, kCellMax> instances
+  int2* d_pairs = nullptr;
+  int n_pairs = 0;
   int *d_cells_small = nullptr, *d_cells_big = nullptr;
   int n_cells_small = 0, n_cells_big = 0;
   const uint8_t* last_in = nullptr;
@@ -1559,7 +1786,15 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
   const int ncells = (int)g.cells.size();
   K *cand = (K*)P->d_cand, *lin = (K*)P->d_lin, *okey = (K*)P->d_okey;
   if (ncells > 0) {
-    // cells per wave: up to kCellsPerWave while the launch keeps >= 16 k waves in flight
+    // pairs (cells) per wave: up to kPairsPerWave (kCellsPerWave) while the launch keeps
+    // >= 16 k waves in flight
+    if (P->n_pairs > 0) {
+      const int ppw = std::max(1, std::min(kPairsPerWave, P->n_pairs * n / 16384));
+      hipLaunchKernelGGL((k_fast_pairs<K>), dim3((P->n_pairs + 4 * ppw - 1) / (4 * ppw), n),
+                         dim3(256), 0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_pairs,
+                         P->n_pairs, ncells, g.ini_th, g.min_th, cand, g.cand_total,
+                         P->d_cell_counts, ppw);
+    }
     const int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
     if (P->n_cells_small > 0)
       hipLaunchKernelGGL((k_fast_cells<44, kFcSmallRows, K>),
@@ -1666,16 +1901,35 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->ntiles = (int)tiles.size();
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
   std::vector<int> cells_small, cells_big;
+  std::vector<int2> pairs;
   // a few-image plan runs every cell in the <72, kCellMax> instance: one launch instead of two
   // on the drop-in path's one-frame chain (either instance handles any cell)
   const bool one_fast_launch = max_batch <= kPyFewImages;
-  // the <44, kFcSmallRows> instance takes ROIs up to 41 + its alignment slack wide and
-  // kFcSmallRows rows high
+  // k_fast_pairs takes two consecutive cells of one cell row whose detection columns are
+  // contiguous and fill at most 64 lanes, ROI at most kPairRows rows; the <44, kFcSmallRows>
+  // instance takes ROIs up to 41 + its alignment slack wide and kFcSmallRows rows high
+  auto det = [](const CellGeom& C, int* dc, int* dr) {
+    *dc = C.x1 - C.x0 - 6;
+    *dr = C.y1 - C.y0 - 6;
+    return *dc > 0 && *dr > 0;
+  };
   for (int c = 0; c < (int)g.cells.size(); c++) {
     const CellGeom& C = g.cells[c];
+    if (!one_fast_launch && c + 1 < (int)g.cells.size()) {
+      const CellGeom& D = g.cells[c + 1];
+      int dca, dra, dcb, drb;
+      if (det(C, &dca, &dra) && det(D, &dcb, &drb) && D.level == C.level && D.y0 == C.y0 &&
+          D.y1 == C.y1 && D.x0 + 3 == C.x1 - 3 && dca + dcb <= 64 && C.y1 - C.y0 <= kPairRows &&
+          D.x1 - C.x0 + 3 <= kPairRS) {
+        pairs.push_back(make_int2(c, c + 1));
+        c++;
+        continue;
+      }
+    }
     const bool small = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= kFcSmallRows;
     (small && !one_fast_launch ? cells_small : cells_big).push_back(c);
   }
+  P->n_pairs = (int)pairs.size();
   P->n_cells_small = (int)cells_small.size();
   P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;
@@ -1688,7 +1942,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc((char**)&P->d_lin, B * g.cand_total * ksz) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
       dalloc((char**)&P->d_okey, B * g.kp_total * ksz) || dalloc(&P->d_ocount, B * g.nlevels) ||
-      dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_big, cells_big.size()))
+      dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_big, cells_big.size()) ||
+      dalloc(&P->d_pairs, pairs.size()))
     return fail(ORBX_ENOMEM);
   {
     auto r256 = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1711,7 +1966,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
       up(P->d_bands, g.bands.data(), sizeof(PyrBand) * g.bands.size()) ||
       up(P->d_cells_small, cells_small.data(), 4 * cells_small.size()) ||
-      up(P->d_cells_big, cells_big.data(), 4 * cells_big.size()))
+      up(P->d_cells_big, cells_big.data(), 4 * cells_big.size()) ||
+      up(P->d_pairs, pairs.data(), sizeof(int2) * pairs.size()))
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
@@ -1769,7 +2025,7 @@ int orbx_plan_destroy(orbx_plan* P) {
   void* ptrs[] = {P->d_lv,   P->d_cells, P->d_xtap, P->d_ytap,        P->d_tiles, P->d_bands,
                   P->d_pyr,  P->d_blur,  P->d_cand, P->d_lin,         P->d_okey,  P->d_cell_counts,
                   P->d_label,
-                  P->d_ocount, P->d_cells_small, P->d_cells_big, P->d_cell_scr,
+                  P->d_ocount, P->d_cells_small, P->d_cells_big, P->d_pairs, P->d_cell_scr,
                   P->d_counts /* base of kps and desc too */};
   for (void* p : ptrs)
     if (p) hipFree(p);

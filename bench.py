@@ -103,10 +103,16 @@ def _load_json(name):
         return None
 
 
+# stages whose launch spans several kernels of different names: the per-cell FAST stage runs
+# k_fast_pairs (adjacent cell pairs) and k_fast_cells (the other cells)
+STAGE_KERNELS = {"k_fast_cells": ("k_fast_cells", "k_fast_pairs")}
+
+
 def _kname_is(name, kernel):
-    """rocprofv3 Kernel_Name 'void orbx::k_fast_cells<44, 42, unsigned int>(...)' is kernel
-    'k_fast_cells'."""
-    return name.split("(")[0].split("<")[0].endswith("::" + kernel)
+    """rocprofv3 Kernel_Name 'void orbx::k_fast_cells<44, 42, unsigned int>(...)' belongs to
+    stage 'k_fast_cells' (as does 'void orbx::k_fast_pairs<unsigned int>(...)')."""
+    base = name.split("(")[0].split("<")[0]
+    return any(base.endswith("::" + k) for k in STAGE_KERNELS.get(kernel, (kernel,)))
 
 
 def pmc_traffic(pmc_dir, kernel):

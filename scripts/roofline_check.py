@@ -18,8 +18,9 @@ b = json.loads(open(bench_file).read().strip().splitlines()[-1])
 kern = b["roofline"]["kernel"]
 import os
 path = trace_dir if trace_dir.endswith(".csv") else os.path.join(trace_dir, "run_kernel_trace.csv")
+names = {"k_fast_cells": ("k_fast_cells", "k_fast_pairs")}.get(kern, (kern,))
 rows = [r for r in csv.DictReader(open(path))
-        if r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + kern)]
+        if any(r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + nm) for nm in names)]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
 solo = dur[-steps:]

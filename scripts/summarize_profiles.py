@@ -102,7 +102,10 @@ def main(tag="r02"):
         k = rf["kernel"]
         # every instance of the kernel (k_fast_cells runs a <44, 44> and a <72, 66> launch per
         # step; bench.py's stage, one "launch", spans both): durations summed per step
-        inst = [v for kk, v in sorted(durs.items()) if kk == k or kk.startswith(k + "<")]
+        # (and k_fast_pairs, the pair kernel of the same stage)
+        names = {"k_fast_cells": ("k_fast_cells", "k_fast_pairs")}.get(k, (k,))
+        inst = [v for kk, v in sorted(durs.items())
+                if any(kk == nm or kk.startswith(nm + "<") for nm in names)]
         check.append(f"{cfg} ({line['config']['workload']}): {line['value']:.1f} frames/s")
         check.append(f"  kernel {k}: {sum(len(v) for v in inst)} dispatches"
                      + (f" ({len(inst)} instances, summed per step)" if len(inst) > 1 else ""))

@@ -22,11 +22,50 @@ CONFIGS = {
 }
 
 
+def _batch_extract(img, nfeatures, scale, nlevels, ini, mn, n=5):
+    """The image through a batch plan (orbx_plan_*, the throughput path: batches above 4 images
+    run the FAST cell pairs in k_fast_pairs, the drop-in extractor's batch of 1 does not),
+    replicated n times; returns the keypoints and descriptors of images 0 and n - 1."""
+    import ctypes as C
+    import torch
+    from ar_orbslam2_amd import KEYPOINT_DTYPE
+    from ar_orbslam2_amd._ffi import Params, check, lib
+    h, w = img.shape
+    prm = Params(int(nfeatures), float(scale), int(nlevels), int(ini), int(mn))
+    plan = C.c_void_p()
+    check("orbx_plan_create", lib().orbx_plan_create(C.byref(prm), w, h, n, 0, C.byref(plan)))
+    try:
+        d = torch.from_numpy(np.ascontiguousarray(np.stack([img] * n))).cuda()
+        check("orbx_plan_extract", lib().orbx_plan_extract(plan, C.c_void_p(d.data_ptr()), n))
+        check("orbx_plan_sync", lib().orbx_plan_sync(plan))
+        cap = C.c_int32()
+        check("orbx_plan_capacity", lib().orbx_plan_capacity(plan, C.byref(cap)))
+        kp, ds, ct = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        check("orbx_plan_outputs", lib().orbx_plan_outputs(plan, C.byref(kp), C.byref(ds),
+                                                            C.byref(ct)))
+        hip = C.CDLL("libamdhip64.so")
+
+        def d2h(ptr, nbytes):
+            out = np.zeros(nbytes, np.uint8)
+            assert hip.hipMemcpy(C.c_void_p(out.ctypes.data), C.c_void_p(ptr), C.c_size_t(nbytes), 2) == 0
+            return out
+        k = cap.value
+        counts = d2h(ct.value, 4 * n).view(np.int32)
+        kps = d2h(kp.value, n * k * 28).view(KEYPOINT_DTYPE).reshape(n, k)
+        desc = d2h(ds.value, n * k * 32).reshape(n, k, 32)
+        return [(kps[i, :counts[i]], desc[i, :counts[i]]) for i in (0, n - 1)]
+    finally:
+        lib().orbx_plan_destroy(plan)
+
+
 def _compare(img, nfeatures, scale=1.2, nlevels=8, ini=20, mn=7):
     ex = ORBextractor(nfeatures, scale, nlevels, ini, mn)
     kps, desc = ex(img)
     okps, odesc, olevels, _ = O.extract(img, O.params(nfeatures, scale, nlevels, ini, mn),
                                         want_pyramid=True)
+    for bk, bd in _batch_extract(img, nfeatures, scale, nlevels, ini, mn):
+        assert np.array_equal(bk, okps), (len(bk), len(okps))
+        assert np.array_equal(bd, odesc)
     pyr = ex.mvImagePyramid
     for l, (a, b) in enumerate(zip(pyr, olevels)):
         assert a.shape == b.shape, l
