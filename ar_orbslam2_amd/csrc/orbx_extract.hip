@@ -828,7 +828,7 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
     }
     const int dr = Ac.y1 - Ac.y0 - 6;                      // detection rows, both cells
     const int cwA = Ac.x1 - Ac.x0 - 6, cw = cwA + (Bc.x1 - Bc.x0 - 6);  // detection columns
-    for (int i = lane; i < (dr + 2) * (kPairVS / 16); i += 64) ((uint4*)V)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = lane; i < ((dr + 2) * kPairVS + 15) / 16; i += 64) ((uint4*)V)[i] = make_uint4(0u, 0u, 0u, 0u);
     wave_sync();
     const uint8_t* Sx = S + (Ac.x0 & 3);  // pixel (r, c) of the ROI at Sx[r * RS + c]
     const uint64_t mA = (1ull << cwA) - 1;  // cwA <= 60
