@@ -13,10 +13,11 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "liborbx.so")
-# experiments only: ORBX_LIB_DIR names another build directory (a variant built with
-# `make -C ar_orbslam2_amd/csrc OUT=<dir> EXTRA=...`); it needs ORBX_ALLOW_CUSTOM_BUILD=1 like any
-# custom build
-if os.environ.get("ORBX_LIB_DIR") and os.environ.get("ORBX_ALLOW_CUSTOM_BUILD"):
+# experiments only: ORBX_LIB_DIR names another build directory (a variant built from an
+# experiment copy of the sources, `make OUT=<dir>`); it needs ORBX_ALLOW_CUSTOM_BUILD=1 like any
+# custom build, and such a library is not checked against the tree's sources
+EXPERIMENT_LIB = bool(os.environ.get("ORBX_LIB_DIR") and os.environ.get("ORBX_ALLOW_CUSTOM_BUILD"))
+if EXPERIMENT_LIB:
     LIB_PATH = os.path.join(os.environ["ORBX_LIB_DIR"], "liborbx.so")
 
 KEYPOINT_DTYPE = np.dtype(
@@ -155,7 +156,7 @@ def lib():
                 f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; "
                 "g.build()'` (hipcc, gfx950). There is no CPU fallback.")
         now, built, flags = source_hash()
-        if now is None or now != built:
+        if not EXPERIMENT_LIB and (now is None or now != built):
             raise ImportError(
                 f"{LIB_PATH} is stale or its sources are missing: it was built from other "
                 f"sources than ar_orbslam2_amd/csrc (hash {built} vs {now}); rebuild with "
