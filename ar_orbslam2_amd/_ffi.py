@@ -49,6 +49,7 @@ EXPORTS = [
     "orbx_marker_results", "orbx_marker_outputs", "orbx_marker_stream", "orbx_marker_profile",
     "orbx_marker_profile_read", "orbx_debug_cvorb_cossin", "orbx_debug_retain_best",
     "orbx_debug_match_finish", "orbx_debug_sincosf", "orbx_debug_extractor_blur",
+    "orbx_debug_plan_level",
 ]
 
 # == cv::DMatch (OpenCV 2.4): queryIdx, trainIdx, imgIdx, distance

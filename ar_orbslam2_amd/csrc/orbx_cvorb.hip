@@ -1036,7 +1036,7 @@ int enqueue(Plan* P, const uint8_t* d_in, int n) {
             st_desc = pr.stage("k_cvdescribe");
   hipStream_t s = P->stream;
   pr.mark(s, -1);
-  int rc = launch_pyramid(g, P->pd, d_in, P->d_pyr, n, s);
+  int rc = launch_pyramid(g, P->pd, d_in, P->d_pyr, P->d_blur, n, s);
   if (rc) return rc;
   pr.mark(s, st_pyr);
   if (P->ntiles > 0)
@@ -1048,9 +1048,9 @@ int enqueue(Plan* P, const uint8_t* d_in, int n) {
                      P->cand_total, (int)(P->p.score_type == ORBX_HARRIS_SCORE), P->d_okey,
                      P->kp_total, P->d_ocount);
   pr.mark(s, st_sel);
-  rc = launch_blur(g, P->pd, P->d_pyr, P->d_blur, n, s);
+  rc = launch_blur(g, P->pd, P->d_pyr, P->d_blur, n, s);  // (no-op with the blur fused)
   if (rc) return rc;
-  pr.mark(s, st_blur);
+  if (!g.blur_fused) pr.mark(s, st_blur);
   KpOff ko{};
   for (int l = 0; l < L; l++) ko.off[l] = P->lv[l].kp_off;
   ko.off[L] = P->kp_total;

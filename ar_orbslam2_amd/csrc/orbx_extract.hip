@@ -194,50 +194,167 @@ __device__ __forceinline__ void py_horiz(const uint8_t* row, const int (&xs)[4],
 
 // Vertical pass for the 4 pixels from the horizontal sums of their two source rows.  SSE2
 // region: _mm_mulhi_epi16(H >> 4, b) = ((H >> 4) * b) >> 16 = mulhi_u24((H >> 4) << 8, b << 8)
-// with (H >> 4) << 8 = g & ~0xFF, the mulhi sum <= 1020, result (m + 2) >> 2; past vxs the
-// scalar (H0*b0 + H1*b1 + 2^21) >> 22.  Results are in [0, 255].
+// with (H >> 4) << 8 = g & ~0xFF, the mulhi sum <= 1020, result (m + 2) >> 2; past vxs (a
+// column whose tap carries bit 30, `sc` holds those bits at 0..3) the scalar
+// (H0*b0 + H1*b1 + 2^21) >> 22.  Results are in [0, 255].
 __device__ __forceinline__ uint32_t py_vert(const uint32_t (&g0)[4], const uint32_t (&g1)[4],
-                                           uint32_t yb, int dx0, int vxs) {
+                                           uint32_t yb, uint32_t sc) {
   const uint32_t b0 = yb & 0xFFFF, b1 = yb >> 16;
   uint32_t out = 0;
-  if (dx0 + 3 < vxs) {  // VResizeLinearVec_32s8u: the whole group in the SSE2 region
+  if (sc == 0) {  // VResizeLinearVec_32s8u: the whole group in the SSE2 region
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t m = mulhi_u24(g0[k] & 0x7FFF00, b0 << 8) + mulhi_u24(g1[k] & 0x7FFF00, b1 << 8);
       out |= ((m + 2) >> 2) << (8 * k);
     }
-  } else {  // the row end: SSE2 up to vxs, then the scalar form
+  } else {  // the row end (or a reflected column): SSE2 up to vxs, then the scalar form
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t m = mulhi_u24(g0[k] & 0x7FFF00, b0 << 8) + mulhi_u24(g1[k] & 0x7FFF00, b1 << 8);
       const uint32_t vsc = (__umul24(g0[k] >> 4, b0) + __umul24(g1[k] >> 4, b1) + (1u << 21)) >> 22;
-      out |= (dx0 + k < vxs ? (m + 2) >> 2 : vsc) << (8 * k);
+      out |= ((sc >> k) & 1 ? vsc : (m + 2) >> 2) << (8 * k);
     }
   }
   return out;
 }
 
+typedef unsigned short blur_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ blur_u16x2 byte_pair(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_bit_cast(blur_u16x2, __builtin_amdgcn_perm(hi, lo, sel));
+}
+
+// GaussianBlur 7x7 sigma 2 of 4 output pixels from the column sums of their
+// 4-column dword (c, d: column pairs (x, x+1), (x+2, x+3)) and of the dwords left (a, b: x-4 ..
+// x-1) and right (e, f: x+4 .. x+7): four v_dot2_u32_u16 per output with the taps laid over the
+// pairs, m / 65536 rounded half-even for x < bxs (the SSE2 region) and half-up in the scalar
+// tail, two results per dword by one v_perm of the high halves, clamped by v_pk_min_u16, the four
+// low bytes gathered by one more v_perm.
+__device__ __forceinline__ uint32_t blur_row4(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                              uint32_t e, uint32_t f, uint32_t tail) {
+  constexpr unsigned short k0 = 18, k1 = 34, k2 = 49, k3 = 55;
+  const blur_u16x2 W0k0 = {0, k0}, Wk1k2 = {k1, k2}, Wk3k2 = {k3, k2}, Wk1k0 = {k1, k0},
+                   Wk0k1 = {k0, k1}, Wk2k3 = {k2, k3}, Wk2k1 = {k2, k1}, Wk00 = {k0, 0};
+  const blur_u16x2 P0 = __builtin_bit_cast(blur_u16x2, a), P1 = __builtin_bit_cast(blur_u16x2, b),
+                   P2 = __builtin_bit_cast(blur_u16x2, c), P3 = __builtin_bit_cast(blur_u16x2, d),
+                   P4 = __builtin_bit_cast(blur_u16x2, e), P5 = __builtin_bit_cast(blur_u16x2, f);
+  auto d2 = [](blur_u16x2 p, blur_u16x2 k, uint32_t acc) { return __builtin_amdgcn_udot2(p, k, acc, false); };
+  const uint32_t m[4] = {d2(P3, Wk1k0, d2(P2, Wk3k2, d2(P1, Wk1k2, d2(P0, W0k0, 0u)))),
+                         d2(P4, Wk00, d2(P3, Wk2k1, d2(P2, Wk2k3, d2(P1, Wk0k1, 0u)))),
+                         d2(P4, Wk1k0, d2(P3, Wk3k2, d2(P2, Wk1k2, d2(P1, W0k0, 0u)))),
+                         d2(P5, Wk00, d2(P4, Wk2k1, d2(P3, Wk2k3, d2(P2, Wk0k1, 0u))))};
+  uint32_t rq[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) rq[k] = m[k] + (0x7FFFu + tail) + __builtin_amdgcn_ubfe(m[k], 16, 1u - tail);
+  const blur_u16x2 lim = {255, 255};
+  const blur_u16x2 h01 = __builtin_elementwise_min(byte_pair(rq[1], rq[0], 0x07060302u), lim),
+                   h23 = __builtin_elementwise_min(byte_pair(rq[3], rq[2], 0x07060302u), lim);
+  return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, h23), __builtin_bit_cast(uint32_t, h01),
+                               0x06040200u);
+}
+
+// Column sums (taps [18, 34, 49, 55, 49, 34, 18], packed u16: at most 255 * 257) of one dword
+// column's two byte pairs over 7 consecutive rows starting at j.
+template <int N>
+__device__ __forceinline__ blur_u16x2 blur_col(const blur_u16x2 (&U)[N], int j) {
+  const blur_u16x2 K0 = {18, 18}, K1 = {34, 34}, K2 = {49, 49}, K3 = {55, 55};
+  return (U[j] + U[j + 6]) * K0 + (U[j + 1] + U[j + 5]) * K1 + (U[j + 2] + U[j + 4]) * K2 +
+         U[j + 3] * K3;
+}
+
+// The fused blur (k_pyramid<true>) of one level's own band rows [own_lo, own_hi), all columns,
+// from the band's rows [lo, hi) of the level in LDS (row stride lp, column 0 at byte 16; the
+// reflected columns -4..-1 and w..w+2 are in the row's pads, so no lane handles a column border).
+// A lane holds one dword column (-1 .. gl+1, gl = the last column group with a pixel) over a
+// strip of S output rows: it unpacks its S + 6 input dwords into byte pairs once, and per output
+// row forms the column sums of its 4 columns and takes its neighbours' by DPP wave shifts (lanes
+// are consecutive columns of a strip; each wave's first and last lane only lend their sums, so
+// consecutive waves overlap by two columns).  Rows outside the level reflect (BORDER_REFLECT_101).
+template <int S>
+__device__ __forceinline__ void py_blur_band(const uint8_t* __restrict__ sb, int lp, int lo, int hi,
+                                             const LevelGeom& G, int own_lo, int own_hi,
+                                             uint8_t* __restrict__ dst) {
+  const int R = own_hi - own_lo;
+  if (R <= 0) return;
+  const int w = G.w, h = G.h, pitch = G.pitch, bxs = G.bxs;
+  const int gl = (w - 1) >> 2, ngp = gl + 3;
+  const int nitems = ((R + S - 1) / S) * ngp;
+  const int lane = threadIdx.x & 63;
+  const float inv = 1.0f / (float)ngp;
+  for (int base = (threadIdx.x >> 6) * 62; base < nitems; base += (kPyNT / 64) * 62) {
+    const int iu = base + lane - 1;
+    int st, c;
+    py_divmod(min(max(iu, 0), nitems - 1), ngp, inv, st, c);
+    const int cc = c - 1, y0 = own_lo + st * S;
+    const uint8_t* col = sb + 16 + 4 * cc;
+    blur_u16x2 U[S + 6], V[S + 6];
+    if (__all(y0 - 3 >= lo && y0 + S + 2 < hi)) {  // the strip's rows lie in the band
+      const uint8_t* p = col + __mul24(y0 - 3 - lo, lp);
+#pragma unroll
+      for (int k = 0; k < S + 6; k++) {
+        const uint32_t d = *(const uint32_t*)(p + __mul24(k, lp));
+        U[k] = byte_pair(d, d, 0x0c010c00u);
+        V[k] = byte_pair(d, d, 0x0c030c02u);
+      }
+    } else {  // the level's top / bottom rows (reflected), or a strip past the band's last row
+#pragma unroll
+      for (int k = 0; k < S + 6; k++) {
+        const int y = min(max(reflect101(y0 + k - 3, h), lo), hi - 1);
+        const uint32_t d = *(const uint32_t*)(col + __mul24(y - lo, lp));
+        U[k] = byte_pair(d, d, 0x0c010c00u);
+        V[k] = byte_pair(d, d, 0x0c030c02u);
+      }
+    }
+    const bool out = lane >= 1 && lane <= 62 && iu < nitems && cc >= 0 && cc <= gl;
+    const uint32_t tail = 4 * cc < bxs ? 0u : 1u;
+    uint8_t* drow = dst + __mul24(y0, pitch) + 4 * cc;
+#pragma unroll
+    for (int j = 0; j < S; j++) {
+      const uint32_t su = __builtin_bit_cast(uint32_t, blur_col(U, j)),
+                     sv = __builtin_bit_cast(uint32_t, blur_col(V, j));
+      // wave_shr:1 (lane n reads lane n - 1) and wave_shl:1 (lane n + 1)
+      const uint32_t lu = __builtin_amdgcn_mov_dpp(su, 0x138, 0xf, 0xf, true),
+                     lv = __builtin_amdgcn_mov_dpp(sv, 0x138, 0xf, 0xf, true),
+                     ru = __builtin_amdgcn_mov_dpp(su, 0x130, 0xf, 0xf, true),
+                     rv = __builtin_amdgcn_mov_dpp(sv, 0x130, 0xf, 0xf, true);
+      const uint32_t o = blur_row4(lu, lv, su, sv, ru, rv, tail);
+      if (out && y0 + j < own_hi) *(uint32_t*)(drow + __mul24(j, pitch)) = o;  // bytes past w: row pad
+    }
+  }
+}
+
+// With BLUR (the fused GaussianBlur, kPyFused), the band also blurs its own rows of every level
+// it builds, and of level 0 in the first stage, into `blur` (py_blur_band) from the rows it holds
+// in LDS: the bands carry the blur's 3-row halo, every level is kept in LDS, and the resize also
+// computes each row's reflected pad columns (-4..-1 and past w, the tap table's reflected
+// entries) into LDS only.  A level's blur runs in the phase that builds the next level from it
+// (both only read its buffer), so the blur adds no barrier but the stage's last.
+template <bool BLUR>
 __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ in,
                                                   uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                                   const LevelGeom* __restrict__ lv, int l0, int l1,
                                                   const PyrBand* __restrict__ bands,
                                                   const int2* __restrict__ xtap,
-                                                  const int2* __restrict__ ytap, int buf_b) {
+                                                  const int2* __restrict__ ytap, int buf_b,
+                                                  uint8_t* __restrict__ blur) {
   extern __shared__ __align__(16) uint8_t s_pyr[];
+  constexpr int kPad = BLUR ? 16 : 0;  // column 0 of a level row in LDS (py_lds_pitch)
   int band, img;
   xcd_block(band, img);
   const PyrBand& B = bands[band];
   const int tid = threadIdx.x;
   uint8_t* base = pyr + (int64_t)img * pyr_bytes;
+  uint8_t* bbase = BLUR ? blur + (int64_t)img * pyr_bytes : nullptr;
   {  // the source level's band rows into LDS (buffer of parity l0 - 1)
     const LevelGeom& G = lv[l0 - 1];
-    const int lo = B.lo[l0 - 1], nr = B.hi[l0 - 1] - lo, pitch = G.pitch;
-    uint8_t* sdst = s_pyr + ((l0 - 1) & 1 ? buf_b : 0);
+    const int lo = B.lo[l0 - 1], nr = B.hi[l0 - 1] - lo, pitch = G.pitch, lp = py_lds_pitch(G, BLUR);
+    uint8_t* sdst = s_pyr + ((l0 - 1) & 1 ? buf_b : 0) + kPad;
     const bool input = l0 == 1;  // level 0 comes from the input (ORBextractor.cc:1066-1068)
     const int w = input ? G.w : pitch;  // a pyramid row is copied pad and all
     const uint8_t* src = input ? in + (int64_t)img * G.h * G.w : base + G.pyr_off;
     const int own_lo = input ? B.own_lo[0] : 0, own_hi = input ? B.own_hi[0] : 0;
     uint8_t* dst = base + G.pyr_off;
+    const bool pads = BLUR && input;  // level 0 is blurred: its rows' reflected pad columns
     if ((w & 15) == 0) {  // 16-byte chunks, four per thread in flight
       const int nch = w >> 4, items = nr * nch;
       const float inv = 1.0f / (float)nch;
@@ -256,8 +373,13 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
 #pragma unroll
         for (int u = 0; u < kPyLoads; u++) {
           const int y = lo + rr[u];
-          *(uint4*)(sdst + __mul24(rr[u], pitch) + 16 * cc[u]) = v[u];
+          uint8_t* srow = sdst + __mul24(rr[u], lp);
+          *(uint4*)(srow + 16 * cc[u]) = v[u];
           if (y >= own_lo && y < own_hi) *(uint4*)(dst + (uint32_t)__mul24(y, pitch) + 16 * cc[u]) = v[u];
+          if (pads) {  // columns -4..-1 = 4, 3, 2, 1; w..w+3 = w-2 .. w-5 (w >= 16 here)
+            if (cc[u] == 0) *(uint32_t*)(srow - 4) = __builtin_amdgcn_perm(v[u].y, v[u].x, 0x01020304u);
+            if (cc[u] == nch - 1) *(uint32_t*)(srow + w) = __builtin_amdgcn_perm(v[u].w, v[u].z, 0x03040506u);
+          }
         }
       }
     } else {  // any input width: dwords assembled from bytes
@@ -267,12 +389,31 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
         int r, c;
         py_divmod(i, q4, inv, r, c);
         const int x4 = 4 * c, y = lo + r;
-        const uint8_t* s = src + (int64_t)y * w + x4;
-        uint32_t v = s[0];
-        if (x4 + 1 < w) v |= (uint32_t)s[1] << 8;
-        if (x4 + 2 < w) v |= (uint32_t)s[2] << 16;
-        if (x4 + 3 < w) v |= (uint32_t)s[3] << 24;
-        *(uint32_t*)(sdst + __mul24(r, pitch) + x4) = v;
+        const uint8_t* s = src + (int64_t)y * w;
+        uint8_t* srow = sdst + __mul24(r, lp);
+        uint32_t v;
+        if (pads && c == q4 - 1) {  // the last dword: columns past w reflected, and the next one
+          uint32_t pv = 0;
+          v = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            v |= (uint32_t)s[reflect101(x4 + k, w)] << (8 * k);
+            pv |= (uint32_t)s[reflect101(x4 + 4 + k, w)] << (8 * k);
+          }
+          *(uint32_t*)(srow + x4 + 4) = pv;
+        } else {
+          v = s[x4];
+          if (x4 + 1 < w) v |= (uint32_t)s[x4 + 1] << 8;
+          if (x4 + 2 < w) v |= (uint32_t)s[x4 + 2] << 16;
+          if (x4 + 3 < w) v |= (uint32_t)s[x4 + 3] << 24;
+        }
+        if (pads && c == 0) {
+          uint32_t pv = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) pv |= (uint32_t)s[reflect101(k - 4, w)] << (8 * k);
+          *(uint32_t*)(srow - 4) = pv;
+        }
+        *(uint32_t*)(srow + x4) = v;
         if (y >= own_lo && y < own_hi) *(uint32_t*)(dst + (uint32_t)__mul24(y, pitch) + x4) = v;
       }
     }
@@ -282,47 +423,64 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
     const LevelGeom& D = lv[l];
     const LevelGeom& S = lv[l - 1];
     const uint8_t* sb = s_pyr + ((l - 1) & 1 ? buf_b : 0);
-    uint8_t* db = s_pyr + (l & 1 ? buf_b : 0);
+    uint8_t* db = s_pyr + (l & 1 ? buf_b : 0) + kPad;
     uint8_t* dp = base + D.pyr_off;
-    const int slo = B.lo[l - 1], dlo = B.lo[l], ng = (D.w + 3) >> 2;
+    const int slo = B.lo[l - 1], dlo = B.lo[l];
+    const int gl = (D.w - 1) >> 2;
+    // column groups: 0 .. gl, and with BLUR the pad groups -1 and gl + 1 (LDS only)
+    const int g0 = BLUR ? -1 : 0, ng = BLUR ? gl + 3 : gl + 1;
     const int nr = max(0, B.hi[l] - dlo), nstrip = (nr + kPyStrip - 1) / kPyStrip;
     const int items = nstrip * ng;
     const float inv_ng = 1.0f / (float)ng;
-    const bool keep = l < l1;  // the stage's last level is not read back
-    const int dpitch = D.pitch, spitch = S.pitch, sh1 = S.h - 1, vxs = D.vxs;
+    const bool keep = BLUR || l < l1;  // without the blur the stage's last level is not read back
+    const int dpitch = D.pitch, dlp = py_lds_pitch(D, BLUR), slp = py_lds_pitch(S, BLUR), sh1 = S.h - 1;
     const int own_lo = B.own_lo[l], own_hi = B.own_hi[l];
     const int2* xt = xtap + D.coef_x;
     const int2* yt = ytap + D.coef_y + dlo;
+    const uint8_t* sb16 = sb + kPad;
     // work item = (strip of kPyStrip output rows, 4-pixel column group): the taps are loaded
     // once per item, and a source row's horizontal sums carry over to the next output row
     // that reads it (scale 1.2: 1.2 horizontal passes per output row instead of 2)
     for (int i = tid; i < items; i += kPyNT) {
       int st, gi;
       py_divmod(i, ng, inv_ng, st, gi);
+      gi += g0;
       const int dx0 = 4 * gi;
-      const int4 t01 = *(const int4*)(xt + dx0);  // coef_x % 4 == 0, runs padded: aligned, in range
-      const int4 t23 = *(const int4*)(xt + dx0 + 2);
-      const int xs[4] = {t01.x, t01.z, t23.x, t23.z};
+      const int4 t01 = *(const int4*)(xt + dx0);  // every run starts 4 entries before column 0 and
+      const int4 t23 = *(const int4*)(xt + dx0 + 2);  // is a multiple of 4: aligned, in range
+      const uint32_t sc = ((uint32_t)t01.x >> 30) | ((uint32_t)t01.z >> 29) |
+                          ((uint32_t)t23.x >> 28) | ((uint32_t)t23.z >> 27);  // bit 30: scalar form
+      const int xs[4] = {t01.x & 0xFFFFF, t01.z & 0xFFFFF, t23.x & 0xFFFFF, t23.z & 0xFFFFF};
       const uint32_t as[4] = {(uint32_t)t01.y, (uint32_t)t01.w, (uint32_t)t23.y, (uint32_t)t23.w};
       const int r0 = st * kPyStrip, r1 = min(nr, r0 + kPyStrip);
+      const bool gwrite = gi >= 0 && gi <= gl;
       int prev = -1;
       uint32_t gp[4] = {0u, 0u, 0u, 0u};
       for (int r = r0; r < r1; r++) {
         const int2 ty = yt[r];
         const int ya = min(max(ty.x, 0), sh1), yb = min(max(ty.x + 1, 0), sh1);
-        if (ya != prev) py_horiz(sb + __mul24(ya - slo, spitch), xs, as, gp);
+        if (ya != prev) py_horiz(sb16 + __mul24(ya - slo, slp), xs, as, gp);
         uint32_t g1[4];
-        py_horiz(sb + __mul24(yb - slo, spitch), xs, as, g1);
-        const uint32_t o = py_vert(gp, g1, (uint32_t)ty.y, dx0, vxs);
+        py_horiz(sb16 + __mul24(yb - slo, slp), xs, as, g1);
+        const uint32_t o = py_vert(gp, g1, (uint32_t)ty.y, sc);
         // pitch >= w + 4: bytes past w of the last group land in the row's pad
-        if (keep) *(uint32_t*)(db + __mul24(r, dpitch) + dx0) = o;
-        if (dlo + r >= own_lo && dlo + r < own_hi)
+        if (keep) *(uint32_t*)(db + __mul24(r, dlp) + dx0) = o;
+        if (gwrite && dlo + r >= own_lo && dlo + r < own_hi)
           *(uint32_t*)(dp + (uint32_t)__mul24(dlo + r, dpitch) + dx0) = o;
 #pragma unroll
         for (int k = 0; k < 4; k++) gp[k] = g1[k];
         prev = yb;
       }
     }
+    if (BLUR && (l > l0 || l0 == 1))  // level l-1 is blurred from the same buffer
+      py_blur_band<kPyBlurStrip>(sb, slp, slo, B.hi[l - 1], S, B.own_lo[l - 1], B.own_hi[l - 1],
+                                 bbase + S.pyr_off);
+  }
+  if (BLUR) {  // the stage's last level (level 0 alone for a one-level pyramid)
+    __syncthreads();
+    const LevelGeom& D = lv[l1];
+    py_blur_band<kPyBlurStrip>(s_pyr + (l1 & 1 ? buf_b : 0), py_lds_pitch(D, true), B.lo[l1], B.hi[l1], D,
+                               B.own_lo[l1], B.own_hi[l1], bbase + D.pyr_off);
   }
 }
 
@@ -343,12 +501,6 @@ constexpr int kBlurTW = 64, kBlurTH = 64;
 struct BlurTile {
   int16_t level, tx, ty, interior;
 };
-
-typedef unsigned short blur_u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ blur_u16x2 byte_pair(uint32_t hi, uint32_t lo, uint32_t sel) {
-  return __builtin_bit_cast(blur_u16x2, __builtin_amdgcn_perm(hi, lo, sel));
-}
 
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                               uint8_t* __restrict__ blur,
@@ -441,38 +593,16 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
   }
   __syncthreads();
   // row pass: 4 adjacent outputs per thread from the 6 column-sum pairs P_j = (c[4q + 2j],
-  // c[4q + 2j + 1]) around them (window column i = x - X0 + 4), 4 v_dot2_u32_u16 per output with
-  // the taps laid over the pairs (even outputs start mid-pair)
-  const blur_u16x2 W0k0 = {0, k0}, Wk1k2 = {k1, k2}, Wk3k2 = {k3, k2}, Wk1k0 = {k1, k0},
-                   Wk0k1 = {k0, k1}, Wk2k3 = {k2, k3}, Wk2k1 = {k2, k1}, Wk00 = {k0, 0};
+  // c[4q + 2j + 1]) around them (window column i = x - X0 + 4); m / 65536 rounded half-even in
+  // the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up in the scalar tail (m + 0x8000); x is a
+  // multiple of 4, as is bxs: one test per group (blur_row4)
   for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
     const int r = i >> 4, q = i & 15;
     const int x = X0 + 4 * q, y = Y0 + r;
     if (x >= w || y >= h) continue;
     const uint2 A = *(const uint2*)&s_col[r][2 * q], B = *(const uint2*)&s_col[r][2 * q + 2],
                 C = *(const uint2*)&s_col[r][2 * q + 4];
-    const blur_u16x2 P0 = __builtin_bit_cast(blur_u16x2, A.x), P1 = __builtin_bit_cast(blur_u16x2, A.y),
-                     P2 = __builtin_bit_cast(blur_u16x2, B.x), P3 = __builtin_bit_cast(blur_u16x2, B.y),
-                     P4 = __builtin_bit_cast(blur_u16x2, C.x), P5 = __builtin_bit_cast(blur_u16x2, C.y);
-    auto d2 = [](blur_u16x2 p, blur_u16x2 k, uint32_t acc) { return __builtin_amdgcn_udot2(p, k, acc, false); };
-    const uint32_t m[4] = {d2(P3, Wk1k0, d2(P2, Wk3k2, d2(P1, Wk1k2, d2(P0, W0k0, 0u)))),
-                           d2(P4, Wk00, d2(P3, Wk2k1, d2(P2, Wk2k3, d2(P1, Wk0k1, 0u)))),
-                           d2(P4, Wk1k0, d2(P3, Wk3k2, d2(P2, Wk1k2, d2(P1, W0k0, 0u)))),
-                           d2(P5, Wk00, d2(P4, Wk2k1, d2(P3, Wk2k3, d2(P2, Wk0k1, 0u))))};
-    // m / 65536 rounded half-even in the SSE2 region (m + 0x7FFF + lsb(m >> 16)), half-up in
-    // the scalar tail (m + 0x8000); x is a multiple of 4, as is bxs: one test per group.
-    // Quotients <= 257: two per dword by one v_perm of the high halves, clamped by v_pk_min_u16,
-    // then the four low bytes gathered by one more v_perm
-    // (bit field of width 1 in the SSE2 region, 0 in the tail: v_bfe + v_add3 per output)
-    const uint32_t tail = x < bxs ? 0u : 1u;
-    uint32_t rq[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) rq[k] = m[k] + (0x7FFFu + tail) + __builtin_amdgcn_ubfe(m[k], 16, 1u - tail);
-    const blur_u16x2 lim = {255, 255};
-    const blur_u16x2 h01 = __builtin_elementwise_min(byte_pair(rq[1], rq[0], 0x07060302u), lim),
-                     h23 = __builtin_elementwise_min(byte_pair(rq[3], rq[2], 0x07060302u), lim);
-    const uint32_t out = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, h23),
-                                               __builtin_bit_cast(uint32_t, h01), 0x06040200u);
+    const uint32_t out = blur_row4(A.x, A.y, B.x, B.y, C.x, C.y, x < bxs ? 0u : 1u);
     *(uint32_t*)(dst + (uint32_t)(y * pitch + x)) = out;  // bytes past w land in the row pad
   }
 }
@@ -1721,8 +1851,23 @@ static std::vector<BlurTile> blur_tiles(const Geometry& g) {
   return tiles;
 }
 
+// k_pyramid's dynamic LDS bound (bands of up to kPyMaxSmemLimit bytes); under the resource lock
+int orbx::pyr_kernel_init() {
+  static bool done = false;
+  if (!done) {
+    if (hipFuncSetAttribute((const void*)k_pyramid<true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kPyMaxSmemLimit) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_pyramid<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kPyMaxSmemLimit) != hipSuccess)
+      return ORBX_EDEVICE;
+    done = true;
+  }
+  return ORBX_OK;
+}
+
 int orbx::pyr_dev_create(const Geometry& g, PyrDev* d) {
   *d = PyrDev{};
+  if (pyr_kernel_init() != ORBX_OK) return ORBX_EDEVICE;
   const std::vector<BlurTile> tiles = blur_tiles(g);
   d->ntiles = (int)tiles.size();
   BlurTile* dt = nullptr;
@@ -1757,19 +1902,32 @@ void orbx::pyr_dev_destroy(PyrDev* d) {
   *d = PyrDev{};
 }
 
+// k_pyramid's stages, and with the blur fused (Geometry::blur_fused) the blurred pyramid too
+static void enqueue_pyramid(const Geometry& g, const LevelGeom* d_lv, const PyrBand* d_bands,
+                            const int2* d_xtap, const int2* d_ytap, const uint8_t* d_in,
+                            uint8_t* d_pyr, uint8_t* d_blur, int n, hipStream_t s) {
+  for (const PyrStage& st : g.pyr_stages) {
+    if (g.blur_fused)
+      hipLaunchKernelGGL(k_pyramid<true>, dim3(st.nbands, n), dim3(kPyNT), st.smem, s, d_in,
+                         d_pyr, g.pyr_bytes, d_lv, st.l0, st.l1, d_bands + st.band0, d_xtap,
+                         d_ytap, st.buf_b, d_blur);
+    else
+      hipLaunchKernelGGL(k_pyramid<false>, dim3(st.nbands, n), dim3(kPyNT), st.smem, s, d_in,
+                         d_pyr, g.pyr_bytes, d_lv, st.l0, st.l1, d_bands + st.band0, d_xtap,
+                         d_ytap, st.buf_b, nullptr);
+  }
+}
+
 int orbx::launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint8_t* d_pyr,
-                         int n, hipStream_t s) {
-  for (const PyrStage& st : g.pyr_stages)
-    hipLaunchKernelGGL(k_pyramid, dim3(st.nbands, n), dim3(kPyNT), st.smem, s, d_in, d_pyr,
-                       g.pyr_bytes, d.d_lv, st.l0, st.l1, d.d_bands + st.band0, d.d_xtap,
-                       d.d_ytap, st.buf_b);
+                         uint8_t* d_blur, int n, hipStream_t s) {
+  enqueue_pyramid(g, d.d_lv, d.d_bands, d.d_xtap, d.d_ytap, d_in, d_pyr, d_blur, n, s);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_pyramid");
 }
 
 int orbx::launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur,
                       int n, hipStream_t s) {
-  if (d.ntiles > 0)
+  if (!g.blur_fused && d.ntiles > 0)
     hipLaunchKernelGGL(k_blur, dim3(d.ntiles, n), dim3(256), 0, s, d_pyr, g.pyr_bytes, d_blur,
                        d.d_lv, (const BlurTile*)d.d_tiles);
   hipError_t e = hipGetLastError();
@@ -1839,12 +1997,10 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
             st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe"),
             st_fcell = pr.stage("k_fast_cells");
   pr.mark(P->stream, -1);
-  for (const PyrStage& st : g.pyr_stages)
-    hipLaunchKernelGGL(k_pyramid, dim3(st.nbands, n), dim3(kPyNT), st.smem, P->stream, d_in,
-                       P->d_pyr, g.pyr_bytes, P->d_lv, st.l0, st.l1, P->d_bands + st.band0,
-                       P->d_xtap, P->d_ytap, st.buf_b);
+  enqueue_pyramid(g, P->d_lv, P->d_bands, P->d_xtap, P->d_ytap, d_in, P->d_pyr, P->d_blur, n,
+                  P->stream);
   pr.mark(P->stream, st_pyr);
-  if (P->ntiles > 0) {
+  if (!g.blur_fused && P->ntiles > 0) {
     hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles);
     pr.mark(P->stream, st_blur);
@@ -1888,6 +2044,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (hipSetDevice(hip_device) != hipSuccess) return fail(ORBX_EDEVICE);
   if (hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(ORBX_EDEVICE);
+  if (pyr_kernel_init() != ORBX_OK) return fail(ORBX_EDEVICE);
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)));
   ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), g.umax, sizeof(g.umax)));
   {
@@ -2112,6 +2269,12 @@ int orbx_plan_level_download_buf(orbx_plan* P, int img, int level, uint8_t* out,
 
 int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int64_t stride) {
   return orbx_plan_level_download_buf(P, img, level, out, stride, 0);
+}
+
+int orbx_debug_plan_level(orbx_plan* P, int32_t img, int32_t level, int32_t blurred, uint8_t* out,
+                          int64_t stride) {
+  if (!out) return ORBX_EINVAL;
+  return orbx_plan_level_download_buf(P, img, level, out, stride, blurred != 0);
 }
 
 // Test hook: the device sincosf port over a range of float bit patterns (orbx.h).

@@ -118,11 +118,28 @@ static bool resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom
     g->yb.push_back((int16_t)std::min(32767, std::max(-32768, cv_round(c1 * 2048))));
   }
   L->xmax = xmax;
-  for (int dx = 0; dx < (dw + 3) / 4 * 4; dx++) {
-    const int i = 2 * (g->xofs.size() - dw + std::min(dx, dw - 1));
-    const int a0 = std::min(dx, dw - 1) >= xmax ? 2048 : g->xa[i];
-    const int a1 = std::min(dx, dw - 1) >= xmax ? 0 : g->xa[i + 1];
-    g->xtap.push_back(g->xofs[i / 2]);
+  int xs = 0;  // VResizeLinearVec_32s8u: 16-wide while x <= W-16, 4-wide while x < W-4
+  while (xs <= dw - 16) xs += 16;
+  while (xs < dw - 4) xs += 4;
+  L->vxs = xs;
+  // k_pyramid taps: columns -4 .. 4*(gl+2)-1 (gl = (dw-1)/4, the last 4-column group holding a
+  // pixel); coef_x indexes column 0.  A column outside [0, dw) carries the taps of its
+  // BORDER_REFLECT_101 image, so the level rows k_pyramid keeps in LDS hold GaussianBlur's
+  // 3-column halo on both sides (the fused blur reads it), and a column at or past vxs is marked
+  // by bit 30 of its source offset (the scalar vertical form, per column).
+  auto reflect = [](int p, int len) {
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+  };
+  const int gl = (dw - 1) / 4;
+  for (int dx = -4; dx < 4 * (gl + 2); dx++) {
+    if (dx == 0) L->coef_x = (int)g->xtap.size() / 2;
+    const int r = reflect(dx, dw);
+    const int i = 2 * ((int)g->xofs.size() - dw + r);
+    const int a0 = r >= xmax ? 2048 : g->xa[i];
+    const int a1 = r >= xmax ? 0 : g->xa[i + 1];
+    g->xtap.push_back(g->xofs[i / 2] | (r >= xs ? 1 << 30 : 0));
     g->xtap.push_back((int32_t)((uint32_t)(a0 << 4) | ((uint32_t)(a1 << 4) << 16)));  // Q15
   }
   for (int dy = 0; dy < dh; dy++) {
@@ -137,11 +154,102 @@ static bool resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom
     if (g->xa[i] < 0 || g->xa[i + 1] < 0 || g->xa[i] + g->xa[i + 1] > 2049) ok = false;
   for (size_t i = 2 * (g->yofs.size() - dh); i < g->yb.size(); i += 2)
     if (g->yb[i] < 0 || g->yb[i + 1] < 0 || g->yb[i] + g->yb[i + 1] > 2049) ok = false;
-  int xs = 0;  // VResizeLinearVec_32s8u: 16-wide while x <= W-16, 4-wide while x < W-4
-  while (xs <= dw - 16) xs += 16;
-  while (xs < dw - 4) xs += 4;
-  L->vxs = xs;
   return ok;
+}
+
+// k_pyramid's stages and row bands (the comment in build_pyramid); false when a one-row band
+// does not fit kPyMaxSmemLimit bytes of LDS
+static bool build_stages(Geometry* g, bool fused) {
+  const int nl = g->nlevels;
+  g->pyr_stages.clear();
+  g->bands.clear();
+  const int py_max_smem = fused ? kPyMaxSmemFused : kPyMaxSmem;  // a band's two level buffers
+  const int stage0 = fused ? kPyStage0Fused : kPyStage0, stage_n = fused ? kPyStageNFused : kPyStageN;
+  for (int l0 = 1; l0 < nl;) {
+    PyrStage st;
+    st.l0 = l0;
+    st.l1 = std::min(nl - 1, l0 + (l0 == 1 ? stage0 : stage_n) - 1);
+    const int hs = g->lv[l0 - 1].h;
+    std::vector<PyrBand> bands;
+    int smem_cap = py_max_smem;  // raised to kPyMaxSmemLimit for rows too wide for it
+    for (int nb = std::max(1, hs / g->py_band_h);; nb++) {
+      bands.assign(nb, PyrBand{});
+      int need[2] = {0, 0};
+      for (int b = 0; b < nb; b++) {
+        PyrBand& B = bands[b];
+        for (int l = st.l0 - 1; l <= st.l1; l++) {
+          const int h = g->lv[l].h;
+          B.own_lo[l] = B.lo[l] = (int)((int64_t)b * h / nb);
+          B.own_hi[l] = B.hi[l] = (int)((int64_t)(b + 1) * h / nb);
+          if (fused && (l >= st.l0 || st.l0 == 1) && B.own_hi[l] > B.own_lo[l]) {
+            B.lo[l] = std::max(0, B.own_lo[l] - 3);
+            B.hi[l] = std::min(h, B.own_hi[l] + 3);
+          }
+        }
+        for (int l = st.l1; l >= st.l0; l--) {
+          const LevelGeom& D = g->lv[l];
+          const LevelGeom& S = g->lv[l - 1];
+          if (B.hi[l] <= B.lo[l]) continue;
+          const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
+          const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
+          B.lo[l - 1] = std::min(B.lo[l - 1], slo);
+          B.hi[l - 1] = std::max(B.hi[l - 1], shi);
+        }
+        for (int l = st.l0 - 1; l <= st.l1; l++)
+          need[l & 1] = std::max(need[l & 1], std::max(0, B.hi[l] - B.lo[l]) * py_lds_pitch(g->lv[l], fused));
+      }
+      st.buf_b = (need[0] + 15) & ~15;
+      st.smem = st.buf_b + need[1];
+      if (st.smem <= smem_cap) break;
+      if (nb >= hs) {
+        if (smem_cap < kPyMaxSmemLimit) {  // one-row bands still too large: the larger carve
+          smem_cap = kPyMaxSmemLimit;
+          nb = std::max(1, hs / g->py_band_h) - 1;
+          continue;
+        }
+        return false;
+      }
+    }
+    st.band0 = (int)g->bands.size();
+    st.nbands = (int)bands.size();
+    g->bands.insert(g->bands.end(), bands.begin(), bands.end());
+    g->pyr_stages.push_back(st);
+    l0 = st.l1 + 1;
+  }
+  if (nl == 1) {  // level 0 alone: one copy stage (and its blur)
+    PyrStage st{1, 0, 0, 0, 0, 0};
+    const int h = g->lv[0].h, nb = std::max(1, h / g->py_band_h);
+    int rows = 0;
+    for (int b = 0; b < nb; b++) {
+      PyrBand B{};
+      B.own_lo[0] = B.lo[0] = (int)((int64_t)b * h / nb);
+      B.own_hi[0] = B.hi[0] = (int)((int64_t)(b + 1) * h / nb);
+      if (fused) {
+        B.lo[0] = std::max(0, B.own_lo[0] - 3);
+        B.hi[0] = std::min(h, B.own_hi[0] + 3);
+      }
+      rows = std::max(rows, B.hi[0] - B.lo[0]);
+      g->bands.push_back(B);
+    }
+    st.nbands = nb;
+    st.smem = std::max(16, rows * py_lds_pitch(g->lv[0], fused));
+    if (st.smem > kPyMaxSmemLimit) return false;
+    g->pyr_stages.push_back(st);
+  }
+  return true;
+}
+
+// Pixels the bands' resize passes compute (owned rows, halo rows and the cone rows the next
+// level needs) over the pixels of the levels they build.
+static double band_recompute(const Geometry& g) {
+  double comp = 0, own = 0;
+  for (const PyrStage& st : g.pyr_stages)
+    for (int b = st.band0; b < st.band0 + st.nbands; b++)
+      for (int l = st.l0; l <= st.l1; l++) {
+        comp += (double)std::max(0, g.bands[b].hi[l] - g.bands[b].lo[l]) * g.lv[l].w;
+        own += (double)(g.bands[b].own_hi[l] - g.bands[b].own_lo[l]) * g.lv[l].w;
+      }
+  return own > 0 ? comp / own : 1.0;
 }
 
 // The pyramid part of a plan for the level sizes already in g->lv[0 .. g->nlevels): cv::resize
@@ -186,68 +294,15 @@ int build_pyramid(Geometry* g, std::string* why) {
   // are computed by both, identically; only the owner stores them).  Its level l rows stay in
   // LDS for level l+1: even levels in buffer A, odd ones in B.  The recomputed cone grows by
   // ~2 rows per level below the top, so stages stay short.
-  g->pyr_stages.clear();
-  g->bands.clear();
-  const int py_max_smem = kPyMaxSmem;  // LDS bound of a band's two level buffers
-  for (int l0 = 1; l0 < nl;) {
-    PyrStage st;
-    st.l0 = l0;
-    st.l1 = std::min(nl - 1, l0 + (l0 == 1 ? kPyStage0 : kPyStageN) - 1);
-    const int hs = g->lv[l0 - 1].h;
-    std::vector<PyrBand> bands;
-    int smem_cap = py_max_smem;  // raised to kPyMaxSmemLimit for rows too wide for it
-    for (int nb = std::max(1, hs / g->py_band_h);; nb++) {
-      bands.assign(nb, PyrBand{});
-      int need[2] = {0, 0};
-      for (int b = 0; b < nb; b++) {
-        PyrBand& B = bands[b];
-        for (int l = st.l0 - 1; l <= st.l1; l++) {
-          B.own_lo[l] = B.lo[l] = (int)((int64_t)b * g->lv[l].h / nb);
-          B.own_hi[l] = B.hi[l] = (int)((int64_t)(b + 1) * g->lv[l].h / nb);
-        }
-        for (int l = st.l1; l >= st.l0; l--) {
-          const LevelGeom& D = g->lv[l];
-          const LevelGeom& S = g->lv[l - 1];
-          if (B.hi[l] <= B.lo[l]) continue;
-          const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
-          const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
-          B.lo[l - 1] = std::min(B.lo[l - 1], slo);
-          B.hi[l - 1] = std::max(B.hi[l - 1], shi);
-        }
-        for (int l = st.l0 - 1; l <= st.l1; l++)
-          need[l & 1] = std::max(need[l & 1], std::max(0, B.hi[l] - B.lo[l]) * g->lv[l].pitch);
-      }
-      st.buf_b = (need[0] + 15) & ~15;
-      st.smem = st.buf_b + need[1];
-      if (st.smem <= smem_cap) break;
-      if (nb >= hs) {
-        if (smem_cap < kPyMaxSmemLimit) {  // one-row bands still too large: the larger carve
-          smem_cap = kPyMaxSmemLimit;
-          nb = std::max(1, hs / g->py_band_h) - 1;
-          continue;
-        }
-        if (why) *why = "image too wide for the pyramid bands";
-        return ORBX_EUNSUPPORTED;
-      }
-    }
-    st.band0 = (int)g->bands.size();
-    st.nbands = (int)bands.size();
-    g->bands.insert(g->bands.end(), bands.begin(), bands.end());
-    g->pyr_stages.push_back(st);
-    l0 = st.l1 + 1;
-  }
-  if (nl == 1) {  // level 0 alone: one copy stage
-    PyrStage st{1, 0, 0, 0, 0, 0};
-    const int nb = std::max(1, g->lv[0].h / g->py_band_h);
-    for (int b = 0; b < nb; b++) {
-      PyrBand B{};
-      B.own_lo[0] = B.lo[0] = (int)((int64_t)b * g->lv[0].h / nb);
-      B.own_hi[0] = B.hi[0] = (int)((int64_t)(b + 1) * g->lv[0].h / nb);
-      g->bands.push_back(B);
-    }
-    st.nbands = nb;
-    st.smem = std::max(16, (g->lv[0].h / nb + 1) * g->lv[0].pitch);
-    g->pyr_stages.push_back(st);
+  // With the blur fused (kPyFused), a band blurs its own rows of every level it builds (and of
+  // level 0 in the first stage) from the rows it holds in LDS: those levels' row ranges carry
+  // GaussianBlur's 3-row halo, clipped to the level (the reflected rows lie inside the range).
+  // The blur is fused where the bands fit (every configuration the benchmarks run); frames too
+  // wide for its halo rows keep the separate k_blur launch.
+  g->blur_fused = kPyFused && build_stages(g, true) && band_recompute(*g) <= kPyFuseMaxRecompute;
+  if (!g->blur_fused && !build_stages(g, false)) {
+    if (why) *why = "image too wide for the pyramid bands";
+    return ORBX_EUNSUPPORTED;
   }
   return ORBX_OK;
 }

@@ -32,15 +32,28 @@ constexpr int kPyBandH = 32;  // source-level rows per band (more if LDS is shor
 constexpr int kPyBandHSmall = 8;
 constexpr int kPyFewImages = 4;
 constexpr int kPyNT = 512;     // k_pyramid threads per workgroup
-constexpr int kPyStage0 = 3;   // levels built by the first stage (from the input)
-constexpr int kPyStageN = 4;   // levels per later stage (from the pyramid)
+// levels per stage (launch): the first from the input, the others from the last level stored;
+// with the blur fused, shorter stages (each blurred level's 3-row halo widens the band cones)
+constexpr int kPyStage0 = 3, kPyStageN = 4, kPyStage0Fused = 2, kPyStageNFused = 3;
 // k_pyramid dynamic LDS bound (both buffers): bands are narrowed until they fit.  40 KB keeps
 // four workgroups per CU; the 64 KB this was measured C4's pyramid at 0.76 vs 0.62 ms per 256
 // frames (wide 1241-px rows: two workgroups per CU), C2 0.31 vs 0.30 ms (32 KB: C4 0.65,
-// 24 KB: more recomputed band cones, C4 0.76)
+// 24 KB: more recomputed band cones, C4 0.76).  With the blur fused: 53 KB, three per CU.
 constexpr int kPyMaxSmem = 40 * 1024;
+constexpr int kPyMaxSmemFused = 53 * 1024;
 constexpr int kPyMaxSmemLimit = 64 * 1024;
 constexpr int kPyStrip = 4;    // k_pyramid output rows per work item (2: 170, 8: 184 vs 166 us)
+// GaussianBlur 7x7 fused into k_pyramid (each band blurs its own rows of the levels it holds in
+// LDS) where the bands' recomputed rows stay below kPyFuseMaxRecompute x the level rows (C2, C3
+// and the AR path's 640-px frames: 1.27-1.31); wider frames and the drop-in extractor's short
+// bands (C4 1.69, C5 3.12, 8-row bands 2.1-2.4) keep the separate k_blur launch.  ORBX_PY_FUSED=0
+// builds never fuse (experiment builds only).
+#ifndef ORBX_PY_FUSED
+#define ORBX_PY_FUSED 1
+#endif
+constexpr bool kPyFused = ORBX_PY_FUSED != 0;
+constexpr double kPyFuseMaxRecompute = 1.4;
+constexpr int kPyBlurStrip = 4;  // fused blur: output rows per lane
 struct PyrBand {
   int lo[kMaxLevels], hi[kMaxLevels];      // rows of each level this band computes (with halo)
   int own_lo[kMaxLevels], own_hi[kMaxLevels];  // rows it writes to the pyramid (a partition)
@@ -72,6 +85,11 @@ struct LevelGeom {
   float size;              // (float)(int)(PATCH_SIZE * scale)
   float inv_scale;         // mvInvScaleFactor
 };
+// a level row's stride in k_pyramid's LDS: with the blur fused, 16 bytes of pad on both sides
+// (column 0 at byte 16: the reflected columns -4..-1 at 12..15, those past w after it)
+__host__ __device__ inline int py_lds_pitch(const LevelGeom& L, bool fused) {
+  return fused ? L.pitch + 32 : L.pitch;
+}
 
 struct CellGeom {
   int16_t x0, y0, x1, y1;  // cell image ROI in level coordinates [x0,x1) x [y0,y1)
@@ -103,6 +121,7 @@ struct Geometry {
   int kp_total = 0;                   // per image final keypoint slots
   int node_cap_max = 0;
   bool wide_keys = false;             // an octree frame >= 4096 px: 64-bit candidate keys
+  bool blur_fused = false;            // k_pyramid blurs the levels (else the k_blur launch)
   int py_band_h = kPyBandH;           // k_pyramid source rows per band (set before building)
   float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
   int feats[kMaxLevels];
@@ -132,10 +151,12 @@ struct PyrDev {
   void* d_tiles = nullptr;  // BlurTile[ntiles]
   int ntiles = 0;
 };
+int pyr_kernel_init();
 int pyr_dev_create(const Geometry& g, PyrDev* d);
 void pyr_dev_destroy(PyrDev* d);
-int launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint8_t* d_pyr, int n,
-                   hipStream_t s);
+// the pyramid, and with kPyFused its blurred copy (launch_blur is then a no-op)
+int launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint8_t* d_pyr,
+                   uint8_t* d_blur, int n, hipStream_t s);
 int launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur, int n,
                 hipStream_t s);
 

@@ -212,6 +212,10 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     against the issue rate of 1024 SIMDs) is reported beside it in `issue_roofline`."""
     # stages not launched in this configuration (the other FAST path) are dropped
     stages = {k: v for k, v in stages.items() if v[1] > 0}
+    if "k_pyramid" in stages and "k_blur" not in stages and "k_blur" in alg:
+        # the blur fused into k_pyramid's bands (Geometry::blur_fused): its read + write of every
+        # level (SURVEY §8d's 2 sum(P)) belong to the pyramid's two launches
+        alg = dict(alg, k_pyramid=alg["k_pyramid"] + alg["k_blur"] / 2)
     # stages that time several kernels (the stereo copy + 3 kernels, the matchers' node and
     # finish kernels) cannot be matched to one kernel's counters: the roofline kernel is the
     # largest single-kernel stage

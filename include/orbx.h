@@ -540,6 +540,12 @@ int orbx_debug_sincosf(uint32_t lo, int64_t n, float* s, float* c);
  * orbx_extract call (ORBextractor.cc:1024-1026, computeDescriptors' working image), w x h of
  * orbx_extractor_pyramid, into out with row stride `stride`.  Used by tests/test_extract_gpu.py. */
 int orbx_debug_extractor_blur(orbx_extractor* ex, int32_t level, uint8_t* out, int64_t stride);
+/* Level `level` of image `img` of the batch the last orbx_plan_extract call ran: the pyramid level
+ * (blurred = 0, ORBextractor.cc:1047-1072) or its GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) image
+ * (blurred = 1, :1024-1026), into out with row stride `stride`.  Used by tests/test_extract_gpu.py
+ * (batch plans' row bands: the blur fused into k_pyramid, or k_blur for frames too wide). */
+int orbx_debug_plan_level(orbx_plan* plan, int32_t img, int32_t level, int32_t blurred, uint8_t* out,
+                          int64_t stride);
 
 #ifdef __cplusplus
 }

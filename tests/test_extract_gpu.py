@@ -196,6 +196,44 @@ def test_blur_every_pixel_matches_oracle(w, h, kind):
         assert bad.size == 0, f"level {l} ({lv.shape}): {len(bad)} blurred px differ, first {bad[:5]}"
 
 
+@pytest.mark.parametrize("w,h,kind", [(640, 480, "synth"), (752, 480, "noise"), (1241, 376, "synth"),
+                                      (1920, 1080, "synth"), (643, 361, "noise"), (37, 29, "noise"),
+                                      (4000, 70, "noise")])
+def test_blur_every_pixel_batch_plans(w, h, kind):
+    """Batch plans (the throughput path: 32-row pyramid bands) build the pyramid and its
+    GaussianBlur in k_pyramid itself — each band blurs its own rows of every level from the rows
+    it holds in LDS, halo rows and reflected pad columns included — except for frames whose bands
+    do not fit LDS with the blur's halo (4000 x 70 here), which keep the separate k_blur launch.
+    Every pixel of every level of three distinct images against the oracle (ORBextractor.cc:
+    1024-1026, 1047-1072)."""
+    import ctypes as C
+    import torch
+    from ar_orbslam2_amd._ffi import Params, check, lib, ptr
+    rng = np.random.default_rng(w * 7 + h)
+    imgs = [synth.frame(w, h, 2, i) if kind == "synth" else rng.integers(0, 256, (h, w), dtype=np.uint8)
+            for i in range(3)]
+    n = len(imgs)
+    prm = Params(1000, 1.2, 8, 20, 7)
+    plan = C.c_void_p()
+    check("orbx_plan_create", lib().orbx_plan_create(C.byref(prm), w, h, 8, 0, C.byref(plan)))
+    try:
+        d = torch.from_numpy(np.ascontiguousarray(np.stack(imgs))).cuda()
+        check("orbx_plan_extract", lib().orbx_plan_extract(plan, C.c_void_p(d.data_ptr()), n))
+        check("orbx_plan_sync", lib().orbx_plan_sync(plan))
+        for i, img in enumerate(imgs):
+            _, _, olevels, _ = O.extract(img, O.params(1000, 1.2, 8, 20, 7), want_pyramid=True)
+            for l, lv in enumerate(olevels):
+                for blurred, ref in ((0, lv), (1, O.gaussian7(lv))):
+                    got = np.zeros_like(lv)
+                    check("orbx_debug_plan_level",
+                          lib().orbx_debug_plan_level(plan, i, l, blurred, ptr(got), C.c_int64(lv.shape[1])))
+                    bad = np.argwhere(got != ref)
+                    assert bad.size == 0, (f"image {i} level {l} {'blurred' if blurred else 'pyramid'} "
+                                           f"({lv.shape}): {len(bad)} px differ, first {bad[:5]}")
+    finally:
+        lib().orbx_plan_destroy(plan)
+
+
 @pytest.mark.parametrize("w,h", [(640, 480), (1241, 376)])
 def test_dense_corner_pattern_fills_pretest_queues(w, h):
     """Every level-0 pixel of the detection region is a pretest candidate, so k_fast_cells
