@@ -1036,9 +1036,8 @@ int enqueue(Plan* P, const uint8_t* d_in, int n) {
             st_desc = pr.stage("k_cvdescribe");
   hipStream_t s = P->stream;
   pr.mark(s, -1);
-  int rc = launch_pyramid(g, P->pd, d_in, P->d_pyr, P->d_blur, n, s);
+  int rc = launch_pyramid(g, P->pd, d_in, P->d_pyr, P->d_blur, n, s, &pr, st_pyr);
   if (rc) return rc;
-  pr.mark(s, st_pyr);
   if (P->ntiles > 0)
     hipLaunchKernelGGL(k_cvfast, dim3(P->ntiles, n), dim3(256), 0, s, P->d_pyr, g.pyr_bytes,
                        P->d_lv, P->d_tiles, P->d_bm, P->bm_words, P->d_smap);

@@ -1903,9 +1903,11 @@ void orbx::pyr_dev_destroy(PyrDev* d) {
 }
 
 // k_pyramid's stages, and with the blur fused (Geometry::blur_fused) the blurred pyramid too
+// (a profiler marks every launch: the stage's launch count is its dispatches)
 static void enqueue_pyramid(const Geometry& g, const LevelGeom* d_lv, const PyrBand* d_bands,
                             const int2* d_xtap, const int2* d_ytap, const uint8_t* d_in,
-                            uint8_t* d_pyr, uint8_t* d_blur, int n, hipStream_t s) {
+                            uint8_t* d_pyr, uint8_t* d_blur, int n, hipStream_t s,
+                            Profiler* pr = nullptr, int stage = -1) {
   for (const PyrStage& st : g.pyr_stages) {
     if (g.blur_fused)
       hipLaunchKernelGGL(k_pyramid<true>, dim3(st.nbands, n), dim3(kPyNT), st.smem, s, d_in,
@@ -1915,12 +1917,13 @@ static void enqueue_pyramid(const Geometry& g, const LevelGeom* d_lv, const PyrB
       hipLaunchKernelGGL(k_pyramid<false>, dim3(st.nbands, n), dim3(kPyNT), st.smem, s, d_in,
                          d_pyr, g.pyr_bytes, d_lv, st.l0, st.l1, d_bands + st.band0, d_xtap,
                          d_ytap, st.buf_b, nullptr);
+    if (pr) pr->mark(s, stage);
   }
 }
 
 int orbx::launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint8_t* d_pyr,
-                         uint8_t* d_blur, int n, hipStream_t s) {
-  enqueue_pyramid(g, d.d_lv, d.d_bands, d.d_xtap, d.d_ytap, d_in, d_pyr, d_blur, n, s);
+                         uint8_t* d_blur, int n, hipStream_t s, Profiler* pr, int stage) {
+  enqueue_pyramid(g, d.d_lv, d.d_bands, d.d_xtap, d.d_ytap, d_in, d_pyr, d_blur, n, s, pr, stage);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_pyramid");
 }
@@ -1998,8 +2001,7 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
             st_fcell = pr.stage("k_fast_cells");
   pr.mark(P->stream, -1);
   enqueue_pyramid(g, P->d_lv, P->d_bands, P->d_xtap, P->d_ytap, d_in, P->d_pyr, P->d_blur, n,
-                  P->stream);
-  pr.mark(P->stream, st_pyr);
+                  P->stream, &pr, st_pyr);
   if (!g.blur_fused && P->ntiles > 0) {
     hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles);

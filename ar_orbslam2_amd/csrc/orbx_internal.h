@@ -155,8 +155,9 @@ int pyr_kernel_init();
 int pyr_dev_create(const Geometry& g, PyrDev* d);
 void pyr_dev_destroy(PyrDev* d);
 // the pyramid, and with kPyFused its blurred copy (launch_blur is then a no-op)
+struct Profiler;
 int launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in, uint8_t* d_pyr,
-                   uint8_t* d_blur, int n, hipStream_t s);
+                   uint8_t* d_blur, int n, hipStream_t s, Profiler* pr = nullptr, int stage = -1);
 int launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur, int n,
                 hipStream_t s);
 

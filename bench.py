@@ -77,8 +77,9 @@ def algorithmic_bytes(levels, n_kp, n_img):
     P = [w * h for w, h in levels]
     per_resize = [(P[l - 1] + P[l]) * n_img for l in range(1, len(P))]
     return {
-        # two launches (levels 1-3 from the input, 4-7 from level 3): average launch
-        "k_pyramid": (2 * P[0] * n_img + sum(per_resize)) / 2,
+        # per step; a stage's launch is one dispatch (roofline_of divides by the dispatches per
+        # step: k_pyramid runs one per pyramid stage)
+        "k_pyramid": 2 * P[0] * n_img + sum(per_resize),
         "k_blur": 2 * sum(P) * n_img,
         # SURVEY §8d's FAST term: every level pixel read once (the per-cell kernel writes only
         # the cells' keys, 4 B per candidate, ~1 % of the pixels: not counted)
@@ -214,8 +215,8 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     stages = {k: v for k, v in stages.items() if v[1] > 0}
     if "k_pyramid" in stages and "k_blur" not in stages and "k_blur" in alg:
         # the blur fused into k_pyramid's bands (Geometry::blur_fused): its read + write of every
-        # level (SURVEY §8d's 2 sum(P)) belong to the pyramid's two launches
-        alg = dict(alg, k_pyramid=alg["k_pyramid"] + alg["k_blur"] / 2)
+        # level (SURVEY §8d's 2 sum(P)) belong to the pyramid's launches
+        alg = dict(alg, k_pyramid=alg["k_pyramid"] + alg["k_blur"])
     # stages that time several kernels (the stereo copy + 3 kernels, the matchers' node and
     # finish kernels) cannot be matched to one kernel's counters: the roofline kernel is the
     # largest single-kernel stage
@@ -225,7 +226,10 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     dom = max(single, key=lambda k: single[k][0])
     ms, launches = stages[dom]
     avg_s = ms / 1e3 / max(launches, 1)
-    a_bytes = alg.get(dom)
+    # algorithmic bytes are per step; a stage with several dispatches per step (k_pyramid: one
+    # per pyramid stage) splits them over its launches, as the PMC readers average per dispatch
+    per_step = max(launches, 1) / max(steps, 1)
+    a_bytes = alg.get(dom) / per_step if alg.get(dom) is not None else None
     achieved = (a_bytes / avg_s / 1e9) if a_bytes is not None else None
     traffic, tnote = pmc_traffic(pmc_dir, dom)
     issue = pmc_issue(pmc_dir, dom, avg_s * 1e6)
@@ -233,7 +237,8 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
            "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None}
     out = {"bound": "hbm", "kernel": dom, **hbm, "traffic": traffic, "traffic_note": tnote,
-           "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": a_bytes}
+           "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": a_bytes,
+           "launches_per_step": round(per_step, 3)}
     if issue:
         # the issue-rate roofline (achieved / peak in SIMD quad-cycles of the binding unit per
         # second)
@@ -498,7 +503,7 @@ def marker_bytes(levels, n_kp, n_img, n_target):
     matcher reads both descriptor sets once per frame)."""
     P = [w * h for w, h in levels]
     per_resize = [(P[l - 1] + P[l]) * n_img for l in range(1, len(P))]
-    return {"k_pyramid": (2 * P[0] * n_img + sum(per_resize)) / 2,
+    return {"k_pyramid": 2 * P[0] * n_img + sum(per_resize),
             "k_cvfast": sum(P) * n_img, "k_blur": 2 * sum(P) * n_img,
             "k_cvselect": sum(P) * n_img / 8 + 8 * n_kp, "k_cvdescribe": 60 * n_kp,
             "k_bfmatch": 32 * (n_kp + n_target * n_img) + 8 * n_target * n_img,

@@ -23,10 +23,15 @@ rows = [r for r in csv.DictReader(open(path))
         if any(r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + nm) for nm in names)]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
-solo = dur[-steps:]
-print(f"kernel {kern}: {len(dur)} dispatches")
+# the roofline pass's dispatches: every instance of the stage's kernels (k_fast_cells: the pair
+# kernel and two cell instances) times its launches per step (k_pyramid: one per pyramid stage)
+lps = b["roofline"].get("launches_per_step", 1) or 1
+ninst = len({r["Kernel_Name"] for r in rows})
+solo = dur[-int(round(steps * lps * ninst)):]
+per_launch = sum(solo) / (steps * lps)
+print(f"kernel {kern}: {len(dur)} dispatches ({ninst} instance(s), {lps} launch(es) per step)")
 print(f"  trace average, all dispatches (timed region with concurrent streams + roofline pass): "
       f"{sum(dur) / len(dur):.2f} us")
-print(f"  trace average, last {steps} dispatches (roofline pass, stream 0 alone): "
-      f"{sum(solo) / len(solo):.2f} us")
+print(f"  trace, last {len(solo)} dispatches (roofline pass, stream 0 alone), per launch: "
+      f"{per_launch:.2f} us")
 print(f"  bench.py roofline avg_launch_us (HIP events, same pass): {b['roofline']['avg_launch_us']} us")
