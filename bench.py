@@ -93,8 +93,9 @@ def algorithmic_bytes(levels, n_kp, n_img):
 
 # bytes per lane of the global loads of the kernels bench.py can name as roofline kernel (the
 # staged windows of k_cvfast: 16-B pieces per lane; k_fast_cells: the cell ROI as aligned
-# dwords); the stores are 8-B bitmap words (k_cvfast) and 4-B keys (k_fast_cells)
-LOAD_WIDTH = {"k_cvfast": 16, "k_fast_cells": 4}
+# dwords; k_pyramid: the source band's 16-B chunks); the stores are 8-B bitmap words (k_cvfast),
+# 4-B keys (k_fast_cells) and 4-B pixel groups (k_pyramid)
+LOAD_WIDTH = {"k_cvfast": 16, "k_fast_cells": 4, "k_pyramid": 16}
 
 
 def _load_json(name):

@@ -110,11 +110,14 @@ def main(tag="r02"):
         check.append(f"  kernel {k}: {sum(len(v) for v in inst)} dispatches"
                      + (f" ({len(inst)} instances, summed per step)" if len(inst) > 1 else ""))
         if inst:
-            solo = [sum(x) for x in zip(*(solo_run(v) for v in inst))]
+            # a stage with several dispatches per step (k_pyramid: one per pyramid stage) is
+            # averaged per dispatch, as bench.py's avg_launch_us
+            lps = int(round(rf.get("launches_per_step", 1) or 1))
+            solo = [sum(x) for x in zip(*(solo_run(v, 5 * lps) for v in inst))]
             alld = sum(sum(dur for dur, _ in v) / len(v) for v in inst)
             check.append(f"    trace average, all dispatches (timed region with concurrent streams"
                          f" + roofline pass + PCIe pass): {alld / 1e3:.2f} us")
-            check.append(f"    trace average, roofline pass (5 consecutive dispatches on one "
+            check.append(f"    trace average, roofline pass ({len(solo)} consecutive dispatches on one "
                          f"stream, camera stream 0 alone): {sum(solo) / len(solo) / 1e3:.2f} us")
         under = os.path.join(P, f"{tag}_bench{sfx}_under_rocprof.jsonl")
         if os.path.exists(under):
