@@ -671,8 +671,9 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
 //      clamped; every other pixel has V = 0, equivalent in the NMS to a score below t);
 //  (3) the strict 8-neighbour NMS at the queued pixels with V > t, setting keep bits per row.
 // Instantiated for RS x MAXR staged windows: <44, kFcSmallRows> (ROIs up to 41 wide with their
-// alignment slack, kFcSmallRows high: the usual ~30-px grid) and <72, kCellMax> (any cell);
-// `list` holds the instance's cells.
+// alignment slack, kFcSmallRows high: the usual ~30-px grid), <44, kCellMax> (as narrow, up to
+// kCellMax high: levels with 2-3 cell rows, 41 KB of LDS per workgroup instead of 70) and
+// <72, kCellMax> (any cell); `list` holds the instance's cells.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1802,8 +1803,8 @@ struct orbx_plan {
   // kFcSmallRows> and <72, kCellMax> instances
   int2* d_pairs = nullptr;
   int n_pairs = 0;
-  int *d_cells_small = nullptr, *d_cells_big = nullptr;
-  int n_cells_small = 0, n_cells_big = 0;
+  int *d_cells_small = nullptr, *d_cells_tall = nullptr, *d_cells_big = nullptr;
+  int n_cells_small = 0, n_cells_tall = 0, n_cells_big = 0;
   const uint8_t* last_in = nullptr;
   int last_n = 0;
   // graph cache keyed by (input pointer, batch)
@@ -1963,6 +1964,15 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
                          P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
                          P->n_cells_small, ncells, g.ini_th, g.min_th, cand, g.cand_total,
                          P->d_cell_counts, cpw);
+    // cells up to 41 px wide and kCellMax rows (levels with 2-3 cell rows, e.g. C4's levels 5
+    // and 7): several per wave on the narrow staging, not one per wave on <72, kCellMax>'s
+    const int cpt = std::max(1, std::min(kCellsPerWave, P->n_cells_tall * n / 16384));
+    if (P->n_cells_tall > 0)
+      hipLaunchKernelGGL((k_fast_cells<44, kCellMax, K>),
+                         dim3((P->n_cells_tall + 4 * cpt - 1) / (4 * cpt), n), dim3(256), 0,
+                         P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_tall,
+                         P->n_cells_tall, ncells, g.ini_th, g.min_th, cand, g.cand_total,
+                         P->d_cell_counts, cpt);
     if (P->n_cells_big > 0)
       hipLaunchKernelGGL((k_fast_cells<72, kCellMax, K>), dim3((P->n_cells_big + 3) / 4, n), dim3(256),
                          0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_big,
@@ -2059,7 +2069,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     if (c.x1 - c.x0 > kCellMax || c.y1 - c.y0 > kCellMax) return fail(ORBX_EUNSUPPORTED);
   P->ntiles = (int)tiles.size();
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
-  std::vector<int> cells_small, cells_big;
+  std::vector<int> cells_small, cells_tall, cells_big;
   std::vector<int2> pairs;
   // a few-image plan runs every cell in the <72, kCellMax> instance: one launch instead of two
   // on the drop-in path's one-frame chain (either instance handles any cell)
@@ -2086,10 +2096,12 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       }
     }
     const bool small = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= kFcSmallRows;
-    (small && !one_fast_launch ? cells_small : cells_big).push_back(c);
+    const bool tall = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= kCellMax;
+    (one_fast_launch ? cells_big : small ? cells_small : tall ? cells_tall : cells_big).push_back(c);
   }
   P->n_pairs = (int)pairs.size();
   P->n_cells_small = (int)cells_small.size();
+  P->n_cells_tall = (int)cells_tall.size();
   P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;
   const size_t ksz = g.wide_keys ? 8 : 4;  // bytes per candidate key
@@ -2101,7 +2113,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc((char**)&P->d_lin, B * g.cand_total * ksz) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
       dalloc((char**)&P->d_okey, B * g.kp_total * ksz) || dalloc(&P->d_ocount, B * g.nlevels) ||
-      dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_big, cells_big.size()) ||
+      dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_tall, cells_tall.size()) ||
+      dalloc(&P->d_cells_big, cells_big.size()) ||
       dalloc(&P->d_pairs, pairs.size()))
     return fail(ORBX_ENOMEM);
   {
@@ -2125,6 +2138,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
       up(P->d_bands, g.bands.data(), sizeof(PyrBand) * g.bands.size()) ||
       up(P->d_cells_small, cells_small.data(), 4 * cells_small.size()) ||
+      up(P->d_cells_tall, cells_tall.data(), 4 * cells_tall.size()) ||
       up(P->d_cells_big, cells_big.data(), 4 * cells_big.size()) ||
       up(P->d_pairs, pairs.data(), sizeof(int2) * pairs.size()))
     return fail(ORBX_EDEVICE);
@@ -2184,7 +2198,8 @@ int orbx_plan_destroy(orbx_plan* P) {
   void* ptrs[] = {P->d_lv,   P->d_cells, P->d_xtap, P->d_ytap,        P->d_tiles, P->d_bands,
                   P->d_pyr,  P->d_blur,  P->d_cand, P->d_lin,         P->d_okey,  P->d_cell_counts,
                   P->d_label,
-                  P->d_ocount, P->d_cells_small, P->d_cells_big, P->d_pairs, P->d_cell_scr,
+                  P->d_ocount, P->d_cells_small, P->d_cells_tall, P->d_cells_big, P->d_pairs,
+                  P->d_cell_scr,
                   P->d_counts /* base of kps and desc too */};
   for (void* p : ptrs)
     if (p) hipFree(p);
