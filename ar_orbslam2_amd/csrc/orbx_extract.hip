@@ -671,8 +671,8 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
 //      clamped; every other pixel has V = 0, equivalent in the NMS to a score below t);
 //  (3) the strict 8-neighbour NMS at the queued pixels with V > t, setting keep bits per row.
 // Instantiated for RS x MAXR staged windows: <44, kFcSmallRows> (ROIs up to 41 wide with their
-// alignment slack, kFcSmallRows high: the usual ~30-px grid), <44, kCellMax> (as narrow, up to
-// kCellMax high: levels with 2-3 cell rows, 41 KB of LDS per workgroup instead of 70) and
+// alignment slack, kFcSmallRows high: the usual ~30-px grid), <48, kCellMax> (up to 45 wide and
+// kCellMax high: levels with 2-3 cell rows, 46 KB of LDS per workgroup instead of 70) and
 // <72, kCellMax> (any cell); `list` holds the instance's cells.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -681,6 +681,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 constexpr int kFcSmallRows = 42;  // ROI rows of the small k_fast_cells instance (44 measured slower)
+constexpr int kFcTallRS = 48;     // staged row of the tall instance: ROIs up to 45 px wide
 // Stage 1 of one detection chunk (up to 8 steps of STEP rows per lane, two steps per LDS round
 // trip): the flags of step s end at bits 15 - 2 (nst - 1 - s) (row r) and 31 - 2 (...) (row
 // r + 1) of the returned word; the caller masks rows and columns outside the cell.
@@ -1964,11 +1965,12 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
                          P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_small,
                          P->n_cells_small, ncells, g.ini_th, g.min_th, cand, g.cand_total,
                          P->d_cell_counts, cpw);
-    // cells up to 41 px wide and kCellMax rows (levels with 2-3 cell rows, e.g. C4's levels 5
-    // and 7): several per wave on the narrow staging, not one per wave on <72, kCellMax>'s
+    // cells up to 45 px wide and kCellMax rows (levels with 2-3 cell rows, e.g. C4's levels 5
+    // and 7, C2's level 7): several per wave on the narrow staging, not one per wave on <72,
+    // kCellMax>'s
     const int cpt = std::max(1, std::min(kCellsPerWave, P->n_cells_tall * n / 16384));
     if (P->n_cells_tall > 0)
-      hipLaunchKernelGGL((k_fast_cells<44, kCellMax, K>),
+      hipLaunchKernelGGL((k_fast_cells<kFcTallRS, kCellMax, K>),
                          dim3((P->n_cells_tall + 4 * cpt - 1) / (4 * cpt), n), dim3(256), 0,
                          P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_tall,
                          P->n_cells_tall, ncells, g.ini_th, g.min_th, cand, g.cand_total,
@@ -2096,7 +2098,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       }
     }
     const bool small = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= kFcSmallRows;
-    const bool tall = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= kCellMax;
+    const bool tall = C.x1 - C.x0 + 3 <= kFcTallRS && C.y1 - C.y0 <= kCellMax;
     (one_fast_launch ? cells_big : small ? cells_small : tall ? cells_tall : cells_big).push_back(c);
   }
   P->n_pairs = (int)pairs.size();
