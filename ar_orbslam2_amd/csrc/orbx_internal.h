@@ -40,7 +40,10 @@ constexpr int kPyStage0 = 3, kPyStageN = 4, kPyStage0Fused = 2, kPyStageNFused =
 // frames (wide 1241-px rows: two workgroups per CU), C2 0.31 vs 0.30 ms (32 KB: C4 0.65,
 // 24 KB: more recomputed band cones, C4 0.76).  With the blur fused: 53 KB, three per CU.
 constexpr int kPyMaxSmem = 40 * 1024;
-constexpr int kPyMaxSmemFused = 53 * 1024;
+#ifndef ORBX_PY_SMEM_FUSED
+#define ORBX_PY_SMEM_FUSED 53
+#endif
+constexpr int kPyMaxSmemFused = ORBX_PY_SMEM_FUSED * 1024;
 constexpr int kPyMaxSmemLimit = 64 * 1024;
 constexpr int kPyStrip = 4;    // k_pyramid output rows per work item (2: 170, 8: 184 vs 166 us)
 // GaussianBlur 7x7 fused into k_pyramid (each band blurs its own rows of the levels it holds in

@@ -167,7 +167,7 @@ def pmc_issue(pmc_dir, kernel, avg_launch_us):
     and the larger floor is the bound.  Older passes without SQ_ACTIVE_INST_VALU2 price every
     VALU instruction at 4 cycles (the calibrated cost of all but the dual-issue ops)."""
     import csv
-    path = os.path.join(pmc_dir, "sq_counters.csv")
+    path = os.path.join(pmc_dir, "sq_counters.csv") if pmc_dir else ""
     if not os.path.exists(path) or not avg_launch_us:
         return None
     per = {}  # counter -> instance (full kernel name) -> values per dispatch

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Fused pyramid + blur: parity of the default build on the extraction / AR / stereo tests, then
 # the C2 and C4 bench lines of the default build and of experiment builds in ar_orbslam2_amd/_lib_exp/
-# (make OUT=../_lib_exp/<name> EXTRA=...).  Usage: bash scripts/gpu_pyr_ab.sh TAG "variant ..."
+# (make OUT=../_lib_exp/<name> EXTRA=...).  Usage: bash scripts/gpu_pyr_ab.sh TAG "variant ..." ["C2 C4"]
 set -o pipefail
 T=${1:-pyr}
 mkdir -p gpurun_out/$T
@@ -10,7 +10,7 @@ timeout -k 10 500 python -u -m pytest tests/test_extract_gpu.py tests/test_cvorb
 tail -1 gpurun_out/$T/tests.txt
 for round in 1 2; do
   for v in default $2; do
-    for C in C2 C4; do
+    for C in ${3:-C2 C4}; do
       if [ $v = default ]; then env=""; else env="ORBX_LIB_DIR=ar_orbslam2_amd/_lib_exp/$v ORBX_ALLOW_CUSTOM_BUILD=1"; fi
       env $env timeout -k 10 200 python bench.py --config $C --steps 20 --warmup 3 --no-cpu-baseline --no-upload \
         > gpurun_out/$T/${v}_$C.$round.jsonl 2> gpurun_out/$T/${v}_$C.$round.err || { tail -5 gpurun_out/$T/${v}_$C.$round.err; exit 2; }

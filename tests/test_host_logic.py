@@ -200,3 +200,25 @@ def test_pmc_compaction_keeps_bench_readings(tmp_path):
     for k in a1:
         for c in a1[k]:
             assert a1[k][c] == pytest.approx(a2[k][c]) and len(c1[(k, c)]) == len(c2[(k, c)])
+
+
+def test_roofline_bytes_split_over_a_stages_dispatches():
+    """bench.py's algorithmic bytes are per step; a stage with several dispatches per step (the
+    pyramid: one per pyramid stage) gets them split over its launches, as avg_launch_us and the
+    PMC readers (mean per dispatch) are per launch; with the blur fused (no k_blur stage) the
+    blur's bytes count under k_pyramid."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    alg = {"k_pyramid": 600.0, "k_blur": 300.0, "k_describe": 10.0}
+    # 5 steps, 3 pyramid dispatches each, 2 ms in total: 15 launches of 2/15 ms
+    st = {"k_pyramid": (2.0, 15), "k_describe": (0.5, 5)}
+    r = bench.roofline_of(st, alg, None, 5, 512)
+    assert r["kernel"] == "k_pyramid" and r["launches_per_step"] == 3.0
+    assert r["algorithmic_bytes_per_launch"] == pytest.approx(900.0 / 3)
+    assert r["avg_launch_us"] == pytest.approx(2000.0 / 15, rel=1e-3)
+    # separate blur: the pyramid's own bytes only
+    st = {"k_pyramid": (2.0, 10), "k_blur": (1.0, 5), "k_describe": (0.5, 5)}
+    r = bench.roofline_of(st, alg, None, 5, 512)
+    assert r["algorithmic_bytes_per_launch"] == pytest.approx(600.0 / 2)
