@@ -983,7 +983,8 @@ def run_dropin(args, cfg, rank, world, local):
     import tempfile
     from ar_orbslam2_amd import synth
     from ar_orbslam2_amd.vocabulary import complete_tree
-    exe = os.path.join(ROOT, "ar_orbslam2_amd", "_lib", "orbx_dropin")
+    from ar_orbslam2_amd import _ffi  # the library directory (an experiment build's with ORBX_LIB_DIR)
+    exe = os.path.join(os.path.dirname(_ffi.LIB_PATH), "orbx_dropin")
     if not os.path.exists(exe):
         raise FileNotFoundError(f"{exe} missing: build with __graft_entry__.build()")
     w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
