@@ -40,21 +40,14 @@ constexpr int kPyStage0 = 3, kPyStageN = 4, kPyStage0Fused = 2, kPyStageNFused =
 // frames (wide 1241-px rows: two workgroups per CU), C2 0.31 vs 0.30 ms (32 KB: C4 0.65,
 // 24 KB: more recomputed band cones, C4 0.76).  With the blur fused: 53 KB, three per CU.
 constexpr int kPyMaxSmem = 40 * 1024;
-#ifndef ORBX_PY_SMEM_FUSED
-#define ORBX_PY_SMEM_FUSED 53
-#endif
-constexpr int kPyMaxSmemFused = ORBX_PY_SMEM_FUSED * 1024;
+constexpr int kPyMaxSmemFused = 53 * 1024;
 constexpr int kPyMaxSmemLimit = 64 * 1024;
 constexpr int kPyStrip = 4;    // k_pyramid output rows per work item (2: 170, 8: 184 vs 166 us)
 // GaussianBlur 7x7 fused into k_pyramid (each band blurs its own rows of the levels it holds in
 // LDS) where the bands' recomputed rows stay below kPyFuseMaxRecompute x the level rows (C2, C3
 // and the AR path's 640-px frames: 1.27-1.31); wider frames and the drop-in extractor's short
-// bands (C4 1.69, C5 3.12, 8-row bands 2.1-2.4) keep the separate k_blur launch.  ORBX_PY_FUSED=0
-// builds never fuse (experiment builds only).
-#ifndef ORBX_PY_FUSED
-#define ORBX_PY_FUSED 1
-#endif
-constexpr bool kPyFused = ORBX_PY_FUSED != 0;
+// bands (C4 1.69, C5 3.12, 8-row bands 2.1-2.4) keep the separate k_blur launch.
+constexpr bool kPyFused = true;
 constexpr double kPyFuseMaxRecompute = 1.4;
 constexpr int kPyBlurStrip = 4;  // fused blur: output rows per lane
 struct PyrBand {
