@@ -3,10 +3,12 @@
 //
 // One plan = one image size + one parameter set + a maximum batch.  A batch of images runs
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
-//   k_pyramid       2 launches   row bands               (level 0 copy + cv::resize INTER_LINEAR)
-//   k_blur          x 1          64x64 tiles, all levels (GaussianBlur 7x7 s=2)
-//   k_fast_cells    x 1-2        FAST cells, one wave    (FAST + cell-local NMS at iniThFAST, the
-//                                each                     minThFAST retry, raster compaction)
+//   k_pyramid       2-3 launches row bands               (level 0 copy + cv::resize INTER_LINEAR;
+//                                                         k_pyramid<true> also GaussianBlur 7x7
+//                                                         s=2 of its rows, Geometry::blur_fused)
+//   k_blur          x 0-1        64x64 tiles, all levels (GaussianBlur 7x7 s=2, unfused plans)
+//   k_fast_pairs    x 0-1        two FAST cells, a wave  (FAST + cell-local NMS at iniThFAST, the
+//   k_fast_cells    x 1-3        up to 4 cells, a wave    minThFAST retry, raster compaction)
 //   k_octree        x 1-2        (image, level)          (DistributeOctTree; big levels apart)
 //   k_describe      x 1          half-wave per keypoint  (IC_Angle + rBRIEF)
 // The first k_pyramid launch copies level 0 from the caller's input into the pitched pyramid
