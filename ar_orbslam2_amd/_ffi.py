@@ -31,7 +31,8 @@ EXPORTS = [
     "orbx_extractor_create", "orbx_extractor_destroy", "orbx_extractor_tables", "orbx_extract",
     "orbx_extractor_pyramid", "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_capacity",
     "orbx_plan_extract", "orbx_plan_outputs", "orbx_plan_sync", "orbx_plan_stream",
-    "orbx_plan_profile", "orbx_plan_profile_read", "orbx_descriptor_distance",
+    "orbx_plan_profile", "orbx_plan_profile_read", "orbx_plan_profile_kernels",
+    "orbx_descriptor_distance",
     "orbx_search_by_bow_kf_f", "orbx_search_by_bow_kf_kf", "orbx_search_for_triangulation",
     "orbx_epipole", "orbx_search_by_projection", "orbx_search_by_projection_last",
     "orbx_search_for_initialization", "orbx_fuse", "orbx_fuse_sim3",
@@ -42,12 +43,13 @@ EXPORTS = [
     "orbx_frames_capacity", "orbx_frames_set_masks", "orbx_frames_set_matching",
     "orbx_frames_run", "orbx_frames_sync", "orbx_frames_results", "orbx_frames_outputs",
     "orbx_frames_bow", "orbx_frames_stereo", "orbx_frames_stream", "orbx_frames_profile", "orbx_frames_profile_read",
+    "orbx_frames_profile_kernels",
     "orbx_cvorb_create", "orbx_cvorb_destroy", "orbx_cvorb_capacity", "orbx_cvorb_detect",
     "orbx_cvorb_run", "orbx_cvorb_outputs", "orbx_cvorb_sync", "orbx_cvorb_stream",
     "orbx_bf_match", "orbx_good_matches", "orbx_nn_match", "orbx_marker_create",
     "orbx_marker_destroy", "orbx_marker_set_target", "orbx_marker_run", "orbx_marker_sync",
     "orbx_marker_results", "orbx_marker_outputs", "orbx_marker_stream", "orbx_marker_profile",
-    "orbx_marker_profile_read", "orbx_debug_cvorb_cossin", "orbx_debug_retain_best",
+    "orbx_marker_profile_read", "orbx_marker_profile_kernels", "orbx_debug_cvorb_cossin", "orbx_debug_retain_best",
     "orbx_debug_match_finish", "orbx_debug_sincosf", "orbx_debug_extractor_blur",
     "orbx_debug_plan_level",
 ]
@@ -183,3 +185,14 @@ def check(fn, rc):
 
 def ptr(a):
     return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def profile_kernels(fn, handle, stage_names):
+    """{stage: [kernel instance names]} of a profiled pipeline (orbx_*_profile_kernels: the
+    instances launched for each stage, named as rocprofv3 reports them)."""
+    out = {}
+    buf = C.create_string_buffer(4096)
+    for i, name in enumerate(stage_names):
+        check(fn, getattr(lib(), fn)(handle, C.c_int32(i), buf, C.c_int32(len(buf))))
+        out[name] = [k for k in buf.value.decode().split(";") if k]
+    return out

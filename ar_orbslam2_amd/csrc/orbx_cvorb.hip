@@ -1035,13 +1035,16 @@ int enqueue(Plan* P, const uint8_t* d_in, int n) {
             st_sel = pr.stage("k_cvselect"), st_blur = pr.stage("k_blur"),
             st_desc = pr.stage("k_cvdescribe");
   hipStream_t s = P->stream;
+  ProfScope scope(pr);
   pr.mark(s, -1);
   int rc = launch_pyramid(g, P->pd, d_in, P->d_pyr, P->d_blur, n, s, &pr, st_pyr);
   if (rc) return rc;
+  if (P->ntiles > 0) note_kernel("k_cvfast");
   if (P->ntiles > 0)
     hipLaunchKernelGGL(k_cvfast, dim3(P->ntiles, n), dim3(256), 0, s, P->d_pyr, g.pyr_bytes,
                        P->d_lv, P->d_tiles, P->d_bm, P->bm_words, P->d_smap);
   pr.mark(s, st_fast);
+  note_kernel("k_cvselect");
   hipLaunchKernelGGL(k_cvselect, dim3(L, n), dim3(64), 12 * kSelCap, s, P->d_pyr, g.pyr_bytes,
                      P->d_lv, L, P->d_bm, P->bm_words, P->d_smap, P->d_cand, P->d_pos,
                      P->cand_total, (int)(P->p.score_type == ORBX_HARRIS_SCORE), P->d_okey,
@@ -1053,6 +1056,7 @@ int enqueue(Plan* P, const uint8_t* d_in, int n) {
   KpOff ko{};
   for (int l = 0; l < L; l++) ko.off[l] = P->lv[l].kp_off;
   ko.off[L] = P->kp_total;
+  note_kernel("k_cvdescribe");
   hipLaunchKernelGGL(k_cvdescribe, dim3((P->kp_total + 7) / 8, n), dim3(256), 0, s, P->d_pyr,
                      g.pyr_bytes, P->d_blur, P->d_lv, L, ko, P->d_okey, P->d_ocount, P->kp_total,
                      P->d_kps, P->d_desc, P->d_counts);
@@ -1079,6 +1083,7 @@ int launch_bf(const uint8_t* d_query, int nq, const uint8_t* d_train, int64_t tr
               const int* d_tcount, int nprob, int2* d_best, int* d_second, int* d_extremes,
               hipStream_t s) {
   if (nq <= 0 || nprob <= 0) return ORBX_OK;
+  note_kernel("k_bfmatch");
   hipLaunchKernelGGL(k_bfmatch, dim3((nq + kBfQ - 1) / kBfQ, nprob), dim3(kBfQ), 0, s, d_query,
                      nq, d_train, train_stride, d_tcount, d_best, d_second, d_extremes);
   hipError_t e = hipGetLastError();
@@ -1136,11 +1141,13 @@ int marker_enqueue(orbx_marker* M, int n) {
   Profiler dummy;
   Profiler& pr = P->prof ? *P->prof : dummy;
   const int st_bf = pr.stage("k_bfmatch"), st_good = pr.stage("k_good");
+  ProfScope scope(pr);
   hipStream_t s = P->stream;
   int rc = launch_bf(M->d_target, M->n_target, (const uint8_t*)P->d_desc, P->kp_total,
                      P->d_counts, n, M->d_best, nullptr, nullptr, s);
   if (rc) return rc;
   pr.mark(s, st_bf);
+  note_kernel("k_good");
   hipLaunchKernelGGL(k_good, dim3(n), dim3(64), 0, s, M->d_best, M->n_target, P->d_counts,
                      M->d_matches, M->d_good, M->d_good_count);
   pr.mark(s, st_good);
@@ -1501,6 +1508,11 @@ int orbx_marker_profile_read(orbx_marker* M, int32_t cap, char (*names)[32], dou
                              int64_t* launches, int32_t* n_stages) {
   if (!M) return ORBX_EINVAL;
   return profile_read(M->prof, cap, names, total_ms, launches, n_stages);
+}
+
+int orbx_marker_profile_kernels(orbx_marker* M, int32_t stage, char* buf, int32_t cap) {
+  if (!M) return ORBX_EINVAL;
+  return M->prof.kernels_of(stage, buf, cap) == 0 ? ORBX_OK : ORBX_EINVAL;
 }
 
 }  // extern "C"

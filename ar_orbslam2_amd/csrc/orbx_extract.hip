@@ -1912,6 +1912,7 @@ static void enqueue_pyramid(const Geometry& g, const LevelGeom* d_lv, const PyrB
                             const int2* d_xtap, const int2* d_ytap, const uint8_t* d_in,
                             uint8_t* d_pyr, uint8_t* d_blur, int n, hipStream_t s,
                             Profiler* pr = nullptr, int stage = -1) {
+  note_kernel(g.blur_fused ? "k_pyramid<true>" : "k_pyramid<false>");
   for (const PyrStage& st : g.pyr_stages) {
     if (g.blur_fused)
       hipLaunchKernelGGL(k_pyramid<true>, dim3(st.nbands, n), dim3(kPyNT), st.smem, s, d_in,
@@ -1934,6 +1935,7 @@ int orbx::launch_pyramid(const Geometry& g, const PyrDev& d, const uint8_t* d_in
 
 int orbx::launch_blur(const Geometry& g, const PyrDev& d, const uint8_t* d_pyr, uint8_t* d_blur,
                       int n, hipStream_t s) {
+  if (!g.blur_fused && d.ntiles > 0) note_kernel("k_blur");
   if (!g.blur_fused && d.ntiles > 0)
     hipLaunchKernelGGL(k_blur, dim3(d.ntiles, n), dim3(256), 0, s, d_pyr, g.pyr_bytes, d_blur,
                        d.d_lv, (const BlurTile*)d.d_tiles);
@@ -1955,12 +1957,15 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
     // >= 16 k waves in flight
     if (P->n_pairs > 0) {
       const int ppw = std::max(1, std::min(kPairsPerWave, P->n_pairs * n / 16384));
+      note_kernel<K>("k_fast_pairs");
       hipLaunchKernelGGL((k_fast_pairs<K>), dim3((P->n_pairs + 4 * ppw - 1) / (4 * ppw), n),
                          dim3(256), 0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_pairs,
                          P->n_pairs, ncells, g.ini_th, g.min_th, cand, g.cand_total,
                          P->d_cell_counts, ppw);
     }
     const int cpw = std::max(1, std::min(kCellsPerWave, P->n_cells_small * n / 16384));
+    if (P->n_cells_small > 0) note_kernel<K>("k_fast_cells", "44, 42, ");
+    static_assert(kFcSmallRows == 42 && kFcTallRS == 48 && kCellMax == 66, "instance names");
     if (P->n_cells_small > 0)
       hipLaunchKernelGGL((k_fast_cells<44, kFcSmallRows, K>),
                          dim3((P->n_cells_small + 4 * cpw - 1) / (4 * cpw), n), dim3(256), 0,
@@ -1971,12 +1976,14 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
     // and 7, C2's level 7): several per wave on the narrow staging, not one per wave on <72,
     // kCellMax>'s
     const int cpt = std::max(1, std::min(kCellsPerWave, P->n_cells_tall * n / 16384));
+    if (P->n_cells_tall > 0) note_kernel<K>("k_fast_cells", "48, 66, ");
     if (P->n_cells_tall > 0)
       hipLaunchKernelGGL((k_fast_cells<kFcTallRS, kCellMax, K>),
                          dim3((P->n_cells_tall + 4 * cpt - 1) / (4 * cpt), n), dim3(256), 0,
                          P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_tall,
                          P->n_cells_tall, ncells, g.ini_th, g.min_th, cand, g.cand_total,
                          P->d_cell_counts, cpt);
+    if (P->n_cells_big > 0) note_kernel<K>("k_fast_cells", "72, 66, ");
     if (P->n_cells_big > 0)
       hipLaunchKernelGGL((k_fast_cells<72, kCellMax, K>), dim3((P->n_cells_big + 3) / 4, n), dim3(256),
                          0, P->stream, P->d_pyr, g.pyr_bytes, P->d_cells, P->d_cells_big,
@@ -1986,6 +1993,9 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
   }
   // levels [0, oct_split) on 1024-thread workgroups with the large LDS carve, the others on
   // 256-thread ones sized for themselves (several per CU)
+  static_assert(kOctNTBig == 1024 && kOctNT == 256, "instance names");
+  if (P->oct_split > 0) note_kernel<K>("k_octree", "1024, ");
+  if (P->oct_split < L) note_kernel<K>("k_octree", "256, ");
   if (P->oct_split > 0)
     hipLaunchKernelGGL((k_octree<kOctNTBig, K>), dim3(n, P->oct_split), dim3(kOctNTBig),
                        P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
@@ -2000,6 +2010,7 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
+  note_kernel<K>("k_describe");
   hipLaunchKernelGGL(k_describe<K>, dim3((g.kp_total + 7) / 8, n), dim3(256), 0, P->stream,
                      P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, ko, okey, P->d_ocount,
                      g.kp_total, P->d_kps, P->d_desc, P->d_counts);
@@ -2013,10 +2024,12 @@ int enqueue(orbx_plan* P, const uint8_t* d_in, int n, Profiler* prof) {
   const int st_pyr = pr.stage("k_pyramid"), st_blur = pr.stage("k_blur"),
             st_oct = pr.stage("k_octree"), st_desc = pr.stage("k_describe"),
             st_fcell = pr.stage("k_fast_cells");
+  ProfScope scope(pr);
   pr.mark(P->stream, -1);
   enqueue_pyramid(g, P->d_lv, P->d_bands, P->d_xtap, P->d_ytap, d_in, P->d_pyr, P->d_blur, n,
                   P->stream, &pr, st_pyr);
   if (!g.blur_fused && P->ntiles > 0) {
+    note_kernel("k_blur");
     hipLaunchKernelGGL(k_blur, dim3(P->ntiles, n), dim3(256), 0, P->stream, P->d_pyr,
                        g.pyr_bytes, P->d_blur, P->d_lv, P->d_tiles);
     pr.mark(P->stream, st_blur);
@@ -2266,6 +2279,11 @@ int orbx_plan_profile_read(orbx_plan* P, int32_t cap, char (*names)[32], double*
     if (launches) launches[i] = P->prof.launches[i];
   }
   return ORBX_OK;
+}
+
+int orbx_plan_profile_kernels(orbx_plan* P, int32_t stage, char* buf, int32_t cap) {
+  if (!P) return ORBX_EINVAL;
+  return P->prof.kernels_of(stage, buf, cap) == 0 ? ORBX_OK : ORBX_EINVAL;
 }
 
 // Internal accessors used by the single-image extractor (orbx_api.hip).

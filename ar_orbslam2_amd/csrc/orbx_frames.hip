@@ -186,6 +186,7 @@ int enqueue(orbx_frames* F, const uint8_t* d_in, int n, Profiler* prof) {
   const int st_fv = pr.stage("k_voc_transform"), st_bv = pr.stage("k_bowvec"),
             st_csr = pr.stage("k_csr"),
             st_bow = pr.stage("k_bow"), st_tri = pr.stage("k_tri");
+  ProfScope scope(pr);
   hipStream_t s = F->v.stream;
   int rc = plan_enqueue(F->plan, d_in, F->stereo ? 2 * n : n, prof);
   if (rc) return rc;
@@ -456,6 +457,11 @@ int orbx_frames_profile_read(orbx_frames* F, int32_t cap, char (*names)[32], dou
     if (launches) launches[i] = F->prof.launches[i];
   }
   return ORBX_OK;
+}
+
+int orbx_frames_profile_kernels(orbx_frames* F, int32_t stage, char* buf, int32_t cap) {
+  if (!F) return ORBX_EINVAL;
+  return F->prof.kernels_of(stage, buf, cap) == 0 ? ORBX_OK : ORBX_EINVAL;
 }
 
 }  // extern "C"

@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -501,11 +503,21 @@ __device__ __forceinline__ int fast_score(const uint8_t* s, int stride, int x, i
 
 // Stage timing with HIP events recorded on the launching stream between kernels.  Marks are
 // only read back in collect(), so profiling adds no host synchronisation to the timed loop.
+// A stage also records the kernel instances launched for it, under the names rocprofv3 reports
+// ("k_pyramid<true>", "k_fast_cells<44, 42, unsigned int>"): launch helpers call note_kernel(),
+// which reaches the profiler active on the calling thread (ProfScope), and mark() files the
+// names noted since the previous mark under its stage.  bench.py binds a stage's PMC counters to
+// exactly these instances.
+struct Profiler;
+inline thread_local Profiler* t_prof = nullptr;
+
 struct Profiler {
   bool on = false;
   std::vector<std::string> names;
   std::vector<double> ms;
   std::vector<long long> launches;
+  std::vector<std::vector<std::string>> kernels;  // per stage: instances launched
+  std::vector<std::string> pending;               // noted since the last mark
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   std::vector<std::pair<int, hipEvent_t>> marks;  // stage -1 = segment start
@@ -515,10 +527,23 @@ struct Profiler {
     names.push_back(name);
     ms.push_back(0);
     launches.push_back(0);
+    kernels.emplace_back();
     return (int)names.size() - 1;
+  }
+  void note(const std::string& k) {
+    for (const auto& p : pending)
+      if (p == k) return;
+    pending.push_back(k);
   }
   void mark(hipStream_t s, int st) {
     if (!on) return;
+    if (st >= 0 && st < (int)kernels.size())
+      for (const auto& k : pending) {
+        bool have = false;
+        for (const auto& e : kernels[st]) have = have || e == k;
+        if (!have) kernels[st].push_back(k);
+      }
+    pending.clear();
     if (used == pool.size()) {
       hipEvent_t e;
       if (hipEventCreate(&e) != hipSuccess) return;
@@ -552,13 +577,45 @@ struct Profiler {
   void reset() {
     marks.clear();
     used = 0;
+    pending.clear();
     for (auto& m : ms) m = 0;
     for (auto& l : launches) l = 0;
+    for (auto& k : kernels) k.clear();
+  }
+  // the stage's instances, ';'-separated, into buf (cap bytes, NUL-terminated, truncated)
+  int kernels_of(int st, char* buf, int cap) const {
+    if (st < 0 || st >= (int)kernels.size() || !buf || cap <= 0) return -1;
+    std::string j;
+    for (const auto& k : kernels[st]) j += (j.empty() ? "" : ";") + k;
+    const size_t n = std::min(j.size(), (size_t)cap - 1);
+    memcpy(buf, j.data(), n);
+    buf[n] = 0;
+    return 0;
   }
   ~Profiler() {
     for (auto e : pool) hipEventDestroy(e);
   }
 };
+
+// Makes `pr` the thread's active profiler for the enclosing enqueue (nested enqueues of the same
+// or another profiler restore the outer one); inactive unless pr.on.
+struct ProfScope {
+  Profiler* prev;
+  explicit ProfScope(Profiler& pr) : prev(t_prof) {
+    if (pr.on) t_prof = &pr;
+  }
+  ~ProfScope() { t_prof = prev; }
+};
+inline void note_kernel(const char* k) {
+  if (t_prof) t_prof->note(k);
+}
+template <class K>
+inline void note_kernel(const char* base, const char* args_before = "") {
+  if (!t_prof) return;
+  // rocprofv3's demangled template arguments: uint32_t "unsigned int", uint64_t "unsigned long"
+  const char* kt = sizeof(K) == 8 ? "unsigned long" : "unsigned int";
+  t_prof->note(std::string(base) + "<" + args_before + kt + ">");
+}
 
 #define ORBX_HIP(call)                                       \
   do {                                                       \

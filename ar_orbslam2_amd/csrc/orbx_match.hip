@@ -1056,6 +1056,7 @@ int launch_csr(const uint32_t* d_node_of, int64_t node_stride, const int* d_coun
   const int64_t per_img = std::max<int64_t>(feats_stride, n_fixed);  // features per image, at most
   const int stage_cap = smem + (size_t)per_img * 4 <= 32 * 1024 ? (int)per_img : 0;
   smem += (size_t)stage_cap * 4;
+  note_kernel("k_csr");
   hipLaunchKernelGGL(k_csr, dim3(nimg), dim3(256), smem, s, d_node_of, node_stride, d_counts,
                      n_fixed, id_lo, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride, d_nn,
                      stage_cap);

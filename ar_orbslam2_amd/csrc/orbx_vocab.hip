@@ -328,10 +328,12 @@ int launch_voc_transform(const VocView& V, int nid_level, const uint32_t* d_rank
                          int nimg, hipStream_t s) {
   if (max_n <= 0 || nimg <= 0) return ORBX_OK;
   if (V.k <= 16) {
+    note_kernel("k_voc_transform<16>");
     hipLaunchKernelGGL(k_voc_transform<16>, dim3((max_n + 15) / 16, nimg), dim3(256), 0, s, V,
                        nid_level, d_rank_of_node, d_desc, desc_stride_img, d_counts, n_fixed,
                        d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img);
   } else if (V.k <= 32) {
+    note_kernel("k_voc_transform<32>");
     hipLaunchKernelGGL(k_voc_transform<32>, dim3((max_n + 7) / 8, nimg), dim3(256), 0, s, V,
                        nid_level, d_rank_of_node, d_desc, desc_stride_img, d_counts, n_fixed,
                        d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img);
@@ -368,6 +370,7 @@ int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
     });
     if (attr != hipSuccess) return report_hip(attr, "hipFuncSetAttribute(k_bowvec)");
   }
+  note_kernel("k_bowvec");
   hipLaunchKernelGGL(k_bowvec, dim3(nimg), dim3(256), smem, s, must, l1, tf, d_word_of,
                      d_weight_of, in_stride, d_counts, n_fixed, cap, d_words, d_values,
                      out_stride, d_nwords);
@@ -654,6 +657,7 @@ static int launch_bowfv_t(int must, int l1, int tf, const uint32_t* d_word_of,
     });
     if (attr != hipSuccess) return report_hip(attr, "hipFuncSetAttribute(k_bowfv)");
   }
+  note_kernel(("k_bowfv<" + std::to_string(NPL) + ">").c_str());
   hipLaunchKernelGGL(k_bowfv<NPL>, dim3(nimg), dim3(256), smem, s, must, l1, tf, d_word_of,
                      d_rank_of, d_weight_of, in_stride, d_counts, n_fixed, d_words, d_values,
                      out_stride, d_nwords, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride,

@@ -262,3 +262,8 @@ class MarkerBatch:
                                              ptr(launches), C.byref(n)))
         return {bytes(names[i]).split(b"\0")[0].decode(): (float(ms[i]), int(launches[i]))
                 for i in range(n.value)}
+
+    def profile_kernels(self):
+        """{stage: kernel instances the profiled runs launched for it} (profile_read's stages)."""
+        return _ffi.profile_kernels("orbx_marker_profile_kernels", self._h,
+                                    list(self.profile_read()))

@@ -105,44 +105,102 @@ def _load_json(name):
         return None
 
 
-# stages whose launch spans several kernels of different names: the per-cell FAST stage runs
-# k_fast_pairs (adjacent cell pairs) and k_fast_cells (the other cells)
-STAGE_KERNELS = {"k_fast_cells": ("k_fast_cells", "k_fast_pairs")}
+# The PMC passes of a round (scripts/refresh_profiles.sh): profiles/<PMC_ROUND>_pmc[_<config>]
+PMC_ROUND = "r05"
 
 
-def _kname_is(name, kernel):
-    """rocprofv3 Kernel_Name 'void orbx::k_fast_cells<44, 42, unsigned int>(...)' belongs to
-    stage 'k_fast_cells' (as does 'void orbx::k_fast_pairs<unsigned int>(...)')."""
-    base = name.split("(")[0].split("<")[0]
-    return any(base.endswith("::" + k) for k in STAGE_KERNELS.get(kernel, (kernel,)))
+def kernel_instance(name):
+    """rocprofv3 Kernel_Name -> the instance name the library's profiler records:
+    'void orbx::k_fast_cells<44, 42, unsigned int>(unsigned char const*, ...)' ->
+    'k_fast_cells<44, 42, unsigned int>'; 'orbx::k_tri_nodes(...)' -> 'k_tri_nodes'."""
+    s = name.replace("(anonymous namespace)::", "")
+    if s.startswith("void "):
+        s = s[5:]
+    depth = 0
+    for i, ch in enumerate(s):  # the signature's '(' outside template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            s = s[:i]
+            break
+    head, sep, args = s.partition("<")
+    return head.split("::")[-1] + sep + args
 
 
-def pmc_traffic(pmc_dir, kernel):
-    """HBM-side bytes per launch of `kernel` from separate rocprofv3 --pmc passes
-    (FETCH_SIZE, WRITE_SIZE, both in KB).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2->fabric
+def library_hash():
+    """(source hash recorded by the loaded library's build, whether it is an experiment build
+    (ORBX_LIB_DIR + ORBX_ALLOW_CUSTOM_BUILD), its directory)."""
+    from ar_orbslam2_amd import _ffi
+    return _ffi.source_hash()[1], _ffi.EXPERIMENT_LIB, os.path.dirname(_ffi.LIB_PATH)
+
+
+def library_info():
+    """The library build behind a bench line: its recorded source hash, and whether it is an
+    experiment build (ORBX_LIB_DIR + ORBX_ALLOW_CUSTOM_BUILD: not checked against the tree's
+    sources, so never evidence for the tree)."""
+    built, exp, lib_dir = library_hash()
+    return {"srchash": built, "experiment_build": bool(exp),
+            "lib_dir": os.path.relpath(lib_dir, ROOT) if exp else None}
+
+
+def pmc_binding(pmc_dir, instances):
+    """Checks that the PMC passes in pmc_dir were collected from the library this process runs
+    (meta.json's lib_srchash, written by scripts/pmc_compact.py next to the passes) and hold
+    every kernel instance the timed stage launched.  Returns a reason string when they do not
+    (the counter fields are then null), else None."""
+    rel = os.path.relpath(pmc_dir, ROOT) if pmc_dir else None
+    if not pmc_dir or not os.path.isdir(pmc_dir):
+        return f"no PMC passes for this command ({rel})"
+    try:
+        meta = json.load(open(os.path.join(pmc_dir, "meta.json")))
+    except (OSError, ValueError):
+        return f"PMC passes without meta.json: not bound to a library build ({rel})"
+    built, _, _ = library_hash()
+    if not built or meta.get("lib_srchash") != built:
+        return (f"PMC passes of another library build ({rel}: {meta.get('lib_srchash')}; "
+                f"this run: {built})")
+    if not instances:
+        return "the stage's kernel instances are unknown (no profiled run)"
+    have = set(meta.get("kernels", []))
+    missing = [k for k in instances if k not in have]
+    if missing:
+        return f"kernel instance(s) {missing} not in the PMC passes ({rel})"
+    return None
+
+
+def pmc_traffic(pmc_dir, instances):
+    """HBM-side bytes per launch of a stage (its kernel `instances`, exact rocprofv3 names) from
+    separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE, both in KB) of the same library
+    build (pmc_binding).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2->fabric
     requests (Infinity-Cache hits included) and reads 1/2 of the bytes of 16-B-per-lane streaming
     loads; other widths are to be calibrated in one's own access pattern, which
     profiles/pmc_calibration.json holds (tools/pmc_calib.hip).  Returns (bytes, note):
     FETCH_SIZE x 1024 / read factor of the kernel's load width + WRITE_SIZE x 1024 / the 8-B
-    store factor, or the uncorrected sum without a calibration."""
+    store factor, or the uncorrected sum without a calibration; (None, reason) when the passes
+    do not belong to this build or lack one of the instances."""
     import csv
+    why = pmc_binding(pmc_dir, instances)
+    if why:
+        return None, why
     tot = {}
-    rel = os.path.relpath(pmc_dir, ROOT) if pmc_dir else None
+    rel = os.path.relpath(pmc_dir, ROOT)
     for name, counter in (("fetch_size.csv", "FETCH_SIZE"), ("write_size.csv", "WRITE_SIZE")):
-        path = os.path.join(pmc_dir, name) if pmc_dir else ""
+        path = os.path.join(pmc_dir, name)
         if not os.path.exists(path):
-            return None, f"no PMC passes for this command ({rel})"
-        # one "launch" of a stage spans every instance of the kernel (k_fast_cells<44, 44> and
-        # <72, 66> per step): mean per instance over its dispatches, summed over the instances
+            return None, f"no {counter} pass ({rel})"
+        # one "launch" of a stage spans every instance it launched (k_fast_pairs and the
+        # k_fast_cells instances per step): mean per instance over its dispatches, summed
         per = {}
         for r in csv.DictReader(open(path)):
-            if _kname_is(r["Kernel_Name"], kernel) and r["Counter_Name"] == counter:
-                per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
-        if not per:
-            return None, f"kernel not in the PMC passes ({rel})"
+            if kernel_instance(r["Kernel_Name"]) in instances and r["Counter_Name"] == counter:
+                per.setdefault(kernel_instance(r["Kernel_Name"]), []).append(float(r["Counter_Value"]))
+        if set(per) != set(instances):
+            return None, f"{counter} lacks {sorted(set(instances) - set(per))} ({rel})"
         tot[counter] = sum(sum(v) / len(v) for v in per.values()) * 1024
     cal = _load_json("pmc_calibration.json")
-    w = LOAD_WIDTH.get(kernel)
+    w = LOAD_WIDTH.get(instances[0].split("<")[0])
     rf = (cal or {}).get("read", {}).get(f"{w}B_per_lane") if w else None
     wf = (cal or {}).get("write", {}).get("8B_per_lane")
     if rf and wf:
@@ -154,7 +212,7 @@ def pmc_traffic(pmc_dir, kernel):
             f"this kernel's access width)")
 
 
-def pmc_issue(pmc_dir, kernel, avg_launch_us):
+def pmc_issue(pmc_dir, instances, avg_launch_us):
     """Issue-rate roofline of `kernel` from the SQ counter pass of this bench command
     (sq_counters.csv, per-dispatch sums over the chip's SIMDs).  Measured on this MI355X with
     tools/valu_calib.hip (profiles/valu_calibration.json): a wave64 VALU instruction occupies
@@ -167,16 +225,19 @@ def pmc_issue(pmc_dir, kernel, avg_launch_us):
     and the larger floor is the bound.  Older passes without SQ_ACTIVE_INST_VALU2 price every
     VALU instruction at 4 cycles (the calibrated cost of all but the dual-issue ops)."""
     import csv
+    why = pmc_binding(pmc_dir, instances)
     path = os.path.join(pmc_dir, "sq_counters.csv") if pmc_dir else ""
-    if not os.path.exists(path) or not avg_launch_us:
-        return None
-    per = {}  # counter -> instance (full kernel name) -> values per dispatch
+    if why or not os.path.exists(path) or not avg_launch_us:
+        return {"valu_floor_us": None, "frac": None,
+                "note": why or f"no SQ counter pass ({os.path.relpath(path, ROOT) if path else None})"}
+    per = {}  # counter -> instance -> values per dispatch
     for r in csv.DictReader(open(path)):
-        if _kname_is(r["Kernel_Name"], kernel):
-            per.setdefault(r["Counter_Name"], {}).setdefault(r["Kernel_Name"], []).append(
-                float(r["Counter_Value"]))
-    if "SQ_INSTS_VALU" not in per:
-        return None
+        k = kernel_instance(r["Kernel_Name"])
+        if k in instances:
+            per.setdefault(r["Counter_Name"], {}).setdefault(k, []).append(float(r["Counter_Value"]))
+    if "SQ_INSTS_VALU" not in per or set(per["SQ_INSTS_VALU"]) != set(instances):
+        return {"valu_floor_us": None, "frac": None,
+                "note": f"the SQ pass lacks an instance of {instances}"}
     # per stage launch: mean per instance, summed over the kernel's instances
     avg = {k: sum(sum(v) / len(v) for v in inst.values()) for k, inst in per.items()}
     us_per_qc = 4 / VALU_SIMDS / (CLOCK_GHZ * 1e3)
@@ -190,7 +251,7 @@ def pmc_issue(pmc_dir, kernel, avg_launch_us):
     salu_us = avg.get("SQ_INSTS_SALU", 0.0) * us_per_qc
     bound = "valu" if valu_us >= salu_us else "salu"
     floor = max(valu_us, salu_us)
-    return {"valu_instr_per_launch": round(avg["SQ_INSTS_VALU"]),
+    return {"kernels": list(instances), "valu_instr_per_launch": round(avg["SQ_INSTS_VALU"]),
             "valu_quad_cycles_per_launch": round(valu_qc),
             "salu_instr_per_launch": round(avg.get("SQ_INSTS_SALU", 0.0)),
             "valu_floor_us": round(valu_us, 2), "salu_floor_us": round(salu_us, 2),
@@ -205,7 +266,7 @@ def pmc_issue(pmc_dir, kernel, avg_launch_us):
 AGGREGATE_STAGES = ("k_stereo", "k_bow", "k_tri")
 
 
-def roofline_of(stages, alg, pmc_dir, steps, B):
+def roofline_of(stages, alg, pmc_dir, steps, B, kernels=None):
     """Roofline object of the dominant kernel (largest total time in the per-kernel HIP-event
     pass), in the contract's terms: `bound` "hbm", `achieved` = SURVEY §8d's algorithmic bytes
     per launch / the average launch time, `peak` 8 TB/s, `frac` = achieved / peak.  The path is
@@ -232,15 +293,19 @@ def roofline_of(stages, alg, pmc_dir, steps, B):
     per_step = max(launches, 1) / max(steps, 1)
     a_bytes = alg.get(dom) / per_step if alg.get(dom) is not None else None
     achieved = (a_bytes / avg_s / 1e9) if a_bytes is not None else None
-    traffic, tnote = pmc_traffic(pmc_dir, dom)
-    issue = pmc_issue(pmc_dir, dom, avg_s * 1e6)
+    # the kernel instances the roofline pass launched for this stage (the library's profiler):
+    # the PMC fields are those instances' counters from passes of this same library build
+    inst = (kernels or {}).get(dom) or []
+    traffic, tnote = pmc_traffic(pmc_dir, inst)
+    issue = pmc_issue(pmc_dir, inst, avg_s * 1e6)
     hbm = {"achieved": round(achieved, 3) if achieved is not None else None,
            "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None}
-    out = {"bound": "hbm", "kernel": dom, **hbm, "traffic": traffic, "traffic_note": tnote,
+    out = {"bound": "hbm", "kernel": dom, "kernel_instances": inst, **hbm, "traffic": traffic,
+           "traffic_note": tnote,
            "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": a_bytes,
            "launches_per_step": round(per_step, 3)}
-    if issue:
+    if issue and issue.get("frac") is not None:
         # the issue-rate roofline (achieved / peak in SIMD quad-cycles of the binding unit per
         # second)
         qc = (issue["valu_quad_cycles_per_launch"] if issue["issue_bound"] == "valu"
@@ -712,7 +777,7 @@ def run_marker(args, cfg, rank, world, local, streams, dist):
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    stages = {}
+    stages, kernels = {}, {}
     pipe = pipes[0]
     if not args.no_profile:
         pipe.profile(True)
@@ -720,6 +785,7 @@ def run_marker(args, cfg, rank, world, local, streams, dist):
             pipe.run(pools[0][i % len(pools[0])].data_ptr(), B)
         pipe.sync()
         stages = pipe.profile_read()
+        kernels = pipe.profile_kernels()
         pipe.profile(False)
     kp_counts, good_counts = pipe.results(B)
     if (kp_counts < 0).any():
@@ -730,7 +796,7 @@ def run_marker(args, cfg, rank, world, local, streams, dist):
     levels = cvorb_level_sizes(cvorb_params(nf), w, h)
     n_kp = int(kp_counts.sum())
     alg = marker_bytes(levels, n_kp, B, len(target_desc))
-    roofline = roofline_of(stages, alg, args.pmc_dir, args.roofline_steps, B)
+    roofline = roofline_of(stages, alg, args.pmc_dir, args.roofline_steps, B, kernels)
     out = {
         "metric": MARKER_METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -749,6 +815,7 @@ def run_marker(args, cfg, rank, world, local, streams, dist):
                    "timing": "hipGraph replay of the extraction + 2 matcher launches per batch"},
         "roofline": roofline,
     }
+    out["config"]["library"] = library_info()
     return out, target_desc
 
 
@@ -905,13 +972,14 @@ def run_frames(args, cfg, rank, world, local, streams, dist):
     # roofline pass (after timing): stream 0 alone with HIP events around every kernel on the
     # stream it launches on, so a kernel's event interval is its own duration (as rocprofv3
     # reports it) rather than a share of the concurrent streams
-    stages = {}
+    stages, kernels = {}, {}
     if not args.no_profile:
         pipe.profile(True)
         for i in range(args.roofline_steps):
             pipe.run(pools[0][i % len(pools[0])].data_ptr(), B)
         pipe.sync()
         stages = pipe.profile_read()
+        kernels = pipe.profile_kernels()
         pipe.profile(False)
     kp_counts, bow, tri, err = pipe.results(B)
     if err:
@@ -933,7 +1001,7 @@ def run_frames(args, cfg, rank, world, local, streams, dist):
     n_kp = int(kp_counts.sum())
     # stereo: both images of a frame are extracted (right keypoint count ~ left)
     alg = algorithmic_bytes(levels, 2 * n_kp if stereo else n_kp, 2 * B if stereo else B)
-    roofline = roofline_of(stages, alg, args.pmc_dir, args.roofline_steps, B)
+    roofline = roofline_of(stages, alg, args.pmc_dir, args.roofline_steps, B, kernels)
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -957,6 +1025,7 @@ def run_frames(args, cfg, rank, world, local, streams, dist):
                              "before the warm-up); per-kernel HIP events only in the roofline pass"},
         "roofline": roofline,
     }
+    out["config"]["library"] = library_info()
     if upload:
         out["pcie_upload_included"] = upload
     return out
@@ -1021,7 +1090,7 @@ def run_dropin(args, cfg, rank, world, local):
                                                   ", drop-in through the reference-side shims' "
                                                   "per-call marshalling, one frame per call"),
                    "host_threads": args.threads, "image": f"{w}x{h}", "nfeatures": nf,
-                   "dropin_mode": args.dropin_mode},
+                   "dropin_mode": args.dropin_mode, "library": library_info()},
         "dropin": d,
     }
 
@@ -1082,11 +1151,12 @@ def parse_args(argv=None):
     args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = CONFIGS[args.config].get("batch", 256)
-    if args.pmc_dir is None:  # the committed PMC passes of this config's default command
-        # (never another config's: a missing directory reports traffic / VALU floor as null)
+    if args.pmc_dir is None:  # this round's committed PMC passes of the config's default command
+        # (never another config's; passes of another library build or without the timed kernel
+        # instances give null counter fields with the reason, pmc_binding)
         args.pmc_dir = os.path.join(ROOT, "profiles",
-                                    "r03_pmc" if args.config == "C2" else
-                                    "r03_pmc_" + args.config.lower())
+                                    f"{PMC_ROUND}_pmc" if args.config == "C2" else
+                                    f"{PMC_ROUND}_pmc_" + args.config.lower())
     return args
 
 

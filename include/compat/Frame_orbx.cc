@@ -56,20 +56,22 @@ bool orbx_compute_bow(const cv::Mat& descriptors, DBoW2::BowVector& bow, DBoW2::
 bool orbx_compute_stereo_matches(Frame& F) {
   orbx_extractor* l = orbx_context_of(F.mpORBextractorLeft);
   orbx_extractor* r = orbx_context_of(F.mpORBextractorRight);
-  if (!l || !r) {
-    // an extraction served by the host: the reference's body runs on mvImagePyramid, which the
-    // device extraction (if any) exports now
-    orbx_materialize_pyramid(F.mpORBextractorLeft);
-    orbx_materialize_pyramid(F.mpORBextractorRight);
-    return false;
-  }
+  // the reference's body reads mvImagePyramid: the device extraction (if any) exports it first;
+  // should that fail, no stereo match is made rather than one on another frame's levels
+  // (mvuRight / mvDepth -1: "no depth", as the reference leaves unmatched keypoints)
+  auto host_body_or_no_depth = [&F] {
+    const bool okl = orbx_materialize_pyramid(F.mpORBextractorLeft);
+    const bool okr = orbx_materialize_pyramid(F.mpORBextractorRight);
+    if (okl && okr) return false;  // run the reference's body
+    F.mvuRight.assign(F.N, -1.0f);
+    F.mvDepth.assign(F.N, -1.0f);
+    return true;
+  };
+  if (!l || !r) return host_body_or_no_depth();  // an extraction served by the host
   std::vector<float> ur(std::max(F.N, 1)), depth(std::max(F.N, 1));
   int32_t n = 0;
-  if (orbx_stereo_matches(l, r, F.mb, F.mbf, ur.data(), depth.data(), &n) != ORBX_OK || n != F.N) {
-    orbx_materialize_pyramid(F.mpORBextractorLeft);  // the host body reads mvImagePyramid
-    orbx_materialize_pyramid(F.mpORBextractorRight);
-    return false;
-  }
+  if (orbx_stereo_matches(l, r, F.mb, F.mbf, ur.data(), depth.data(), &n) != ORBX_OK || n != F.N)
+    return host_body_or_no_depth();
   F.mvuRight.assign(ur.begin(), ur.begin() + F.N);
   F.mvDepth.assign(depth.begin(), depth.begin() + F.N);
   return true;

@@ -36,6 +36,9 @@ struct ExtractorCtx {
   bool create_failed = false;        // no device context: every call goes to the host
   bool last_on_device = false;       // the last call's results are resident on the GPU
   bool pyramid_exported = false;     // mvImagePyramid holds the last device call's levels
+  // the last device call's input (a header sharing the caller's refcounted image): if the
+  // pyramid export fails, the host extractor rebuilds mvImagePyramid from it
+  cv::Mat last_image;
 };
 
 std::mutex g_mutex;
@@ -58,7 +61,10 @@ ExtractorCtx& ctx_of(const ORBextractor* self, const orbx_params& p) {
     delete c.host;
     c = ExtractorCtx{};
   }
-  if (c.create_failed && !same_params(c.p, p)) c = ExtractorCtx{};
+  if (c.create_failed && !same_params(c.p, p)) {
+    delete c.host;  // built by the constructor's fallback for the earlier parameters
+    c = ExtractorCtx{};
+  }
   if (!c.ex && !c.create_failed) {  // one attempt per (object, parameters), not one per frame
     c.p = p;
     if (orbx_extractor_create(&p, /*hip_device*/ 0, &c.ex) != ORBX_OK) {
@@ -155,10 +161,12 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask,
       // runs on the device: it is exported on demand (orbx_materialize_pyramid), not per call
       c.last_on_device = true;
       c.pyramid_exported = false;
+      c.last_image = image;
       return;
     }
   }
   c.last_on_device = false;
+  c.last_image = cv::Mat();
   // device error: the reference's own code on the host, same outputs
   log_once("orbx_extract", rc);
   ORBextractorHost* host;
@@ -184,18 +192,35 @@ orbx_extractor* orbx_context_of(const ORBextractor* self) {
 bool orbx_materialize_pyramid(ORBextractor* self) {
   if (!self) return false;
   orbx_extractor* ex;
+  cv::Mat image;
   {
     std::lock_guard<std::mutex> lock(g_mutex);
     auto it = g_ctx.find(self);
     if (it == g_ctx.end() || !it->second.last_on_device || it->second.pyramid_exported)
       return true;  // host-served call (levels already there) or already exported
     ex = it->second.ex;
+    image = it->second.last_image;
   }
   // the extractor is not reentrant (ORBextractor.h), so its owner's thread is the only writer
-  const int rc = export_pyramid(ex, self->GetLevels(), self->mvImagePyramid);
+  int rc = export_pyramid(ex, self->GetLevels(), self->mvImagePyramid);
   if (rc != ORBX_OK) {
+    // never leave the previous frame's (or partly exported) levels for the reader: rebuild them
+    // with the reference's own ComputePyramid through the host extractor on the same input
     log_once("orbx_extractor_pyramid", rc);
-    return false;
+    for (cv::Mat& m : self->mvImagePyramid) m.release();
+    if (image.empty()) return false;
+    ORBextractorHost* host;
+    {
+      std::lock_guard<std::mutex> lock(g_mutex);
+      ExtractorCtx& c = g_ctx[self];
+      if (!c.host) c.host = new ORBextractorHost(c.p.nfeatures, c.p.scale_factor, c.p.nlevels,
+                                                 c.p.ini_th_fast, c.p.min_th_fast);
+      host = c.host;
+    }
+    std::vector<cv::KeyPoint> kps;
+    cv::Mat desc;
+    (*host)(image, cv::Mat(), kps, desc);  // the keypoints equal the device call's (unused)
+    self->mvImagePyramid = host->mvImagePyramid;
   }
   std::lock_guard<std::mutex> lock(g_mutex);
   g_ctx[self].pyramid_exported = true;

@@ -164,6 +164,11 @@ void* orbx_plan_stream(orbx_plan* plan);
 int orbx_plan_profile(orbx_plan* plan, int32_t enable);
 int orbx_plan_profile_read(orbx_plan* plan, int32_t cap, char (*names)[32], double* total_ms,
                            int64_t* launches, int32_t* n_stages);
+/* The kernel instances the profiled runs launched for stage `stage` (profile_read order), under
+ * the names rocprofv3 reports ("k_pyramid<true>", "k_fast_cells<44, 42, unsigned int>"),
+ * ';'-separated into buf (cap bytes, NUL-terminated).  Lets a benchmark bind a stage's time to
+ * the counters of exactly those kernels. */
+int orbx_plan_profile_kernels(orbx_plan* plan, int32_t stage, char* buf, int32_t cap);
 
 /* ------------------------------------------------------------------ projection searches
  * The current Frame as the tracking searches see it: mvKeysUn, mDescriptors, mvuRight, the
@@ -405,6 +410,7 @@ void* orbx_frames_stream(orbx_frames* fr);
 int orbx_frames_profile(orbx_frames* fr, int32_t enable);
 int orbx_frames_profile_read(orbx_frames* fr, int32_t cap, char (*names)[32], double* total_ms,
                              int64_t* launches, int32_t* n_stages);
+int orbx_frames_profile_kernels(orbx_frames* fr, int32_t stage, char* buf, int32_t cap);
 
 /* ------------------------------------------------------------------ matcher */
 /* ORBmatcher::DescriptorDistance on n row pairs (host pointers). */
@@ -516,6 +522,7 @@ void* orbx_marker_stream(orbx_marker* mk);
 int orbx_marker_profile(orbx_marker* mk, int32_t enable);
 int orbx_marker_profile_read(orbx_marker* mk, int32_t cap, char (*names)[32], double* total_ms,
                              int64_t* launches, int32_t* n_stages);
+int orbx_marker_profile_kernels(orbx_marker* mk, int32_t stage, char* buf, int32_t cap);
 
 /* ------------------------------------------------------------------ test hooks (not product API) */
 /* The device computeOrbDescriptor rotation (float)cos/sin((double)(deg * (float)(CV_PI/180.f)))

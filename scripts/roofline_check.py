@@ -18,9 +18,11 @@ b = json.loads(open(bench_file).read().strip().splitlines()[-1])
 kern = b["roofline"]["kernel"]
 import os
 path = trace_dir if trace_dir.endswith(".csv") else os.path.join(trace_dir, "run_kernel_trace.csv")
-names = {"k_fast_cells": ("k_fast_cells", "k_fast_pairs")}.get(kern, (kern,))
-rows = [r for r in csv.DictReader(open(path))
-        if any(r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + nm) for nm in names)]
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_instance  # noqa: E402
+# the exact instances the bench line's roofline pass launched for the stage
+inst = set(b["roofline"].get("kernel_instances") or [])
+rows = [r for r in csv.DictReader(open(path)) if kernel_instance(r["Kernel_Name"]) in inst]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
 # the roofline pass's dispatches: every instance of the stage's kernels (k_fast_cells: the pair
@@ -29,7 +31,7 @@ lps = b["roofline"].get("launches_per_step", 1) or 1
 ninst = len({r["Kernel_Name"] for r in rows})
 solo = dur[-int(round(steps * lps * ninst)):]
 per_launch = sum(solo) / (steps * lps)
-print(f"kernel {kern}: {len(dur)} dispatches ({ninst} instance(s), {lps} launch(es) per step)")
+print(f"kernel {kern} ({', '.join(sorted(inst))}): {len(dur)} dispatches ({ninst} instance(s), {lps} launch(es) per step)")
 print(f"  trace average, all dispatches (timed region with concurrent streams + roofline pass): "
       f"{sum(dur) / len(dur):.2f} us")
 print(f"  trace, last {len(solo)} dispatches (roofline pass, stream 0 alone), per launch: "

@@ -1,5 +1,7 @@
 """Host-side logic of the mirrors and of the matcher semantics, on the CPU oracle with
 hand-built inputs (ORBmatcher.cc rules of SURVEY §8a M1-M5)."""
+import json
+
 import numpy as np
 import pytest
 
@@ -156,7 +158,7 @@ def test_summarizer_finds_roofline_pass():
     assert m.solo_run(timed) == [700] * 5  # no solo run: the last dispatches
 
 
-def test_pmc_compaction_keeps_bench_readings(tmp_path):
+def test_pmc_compaction_keeps_bench_readings(tmp_path, monkeypatch):
     """scripts/pmc_compact.py rewrites a --pmc pass to one row per (kernel, counter) holding the
     mean per dispatch: bench.py's traffic and issue readings and the summarizer's per-dispatch
     sums are unchanged (the committed round-3 passes are compact)."""
@@ -190,7 +192,12 @@ def test_pmc_compaction_keeps_bench_readings(tmp_path):
     assert len(list(csv.DictReader(open(comp / "fetch_size.csv")))) == 3
     sys.path.insert(0, root)
     import bench
-    assert bench.pmc_traffic(str(full), "k_fast_cells")[0] == bench.pmc_traffic(str(comp), "k_fast_cells")[0]
+    inst = ["k_fast_cells<44, 44, unsigned int>", "k_fast_cells<72, 66, unsigned int>"]
+    for d in (full, comp):
+        (d / "meta.json").write_text(json.dumps({"lib_srchash": "h0", "kernels": inst + ["k_blur"]}))
+    monkeypatch.setattr(bench, "library_hash", lambda: ("h0", False, root))
+    tf, tc = bench.pmc_traffic(str(full), inst)[0], bench.pmc_traffic(str(comp), inst)[0]
+    assert tf is not None and tf == tc
     spec = importlib.util.spec_from_file_location("summarize_profiles",
                                                   os.path.join(root, "scripts", "summarize_profiles.py"))
     sm = importlib.util.module_from_spec(spec)
@@ -222,3 +229,76 @@ def test_roofline_bytes_split_over_a_stages_dispatches():
     st = {"k_pyramid": (2.0, 10), "k_blur": (1.0, 5), "k_describe": (0.5, 5)}
     r = bench.roofline_of(st, alg, None, 5, 512)
     assert r["algorithmic_bytes_per_launch"] == pytest.approx(600.0 / 2)
+
+
+def test_pmc_fields_bound_to_library_and_instances(tmp_path, monkeypatch):
+    """bench.py's counter fields (roofline.traffic, issue_roofline) come only from PMC passes of
+    the library build that ran (meta.json's lib_srchash) and only from the exact kernel
+    instances the roofline pass launched for the stage: k_pyramid<true> never reads
+    k_pyramid<false>'s (or another build's) counters; otherwise the fields are null with the
+    reason."""
+    import csv
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    d = tmp_path / "pmc"
+    d.mkdir()
+    names = {"void orbx::k_pyramid<false>(unsigned char const*)": 100.0,
+             "void orbx::k_pyramid<true>(unsigned char const*)": 300.0}
+    for fn, c in (("fetch_size.csv", "FETCH_SIZE"), ("write_size.csv", "WRITE_SIZE")):
+        with open(d / fn, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Kernel_Name", "Counter_Name", "Counter_Value", "Dispatches"])
+            for k, v in names.items():
+                w.writerow([k, c, v, 3])
+    with open(d / "sq_counters.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Counter_Name", "Counter_Value", "Dispatches"])
+        for k, v in names.items():
+            for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_INSTS_SALU"):
+                w.writerow([k, c, v * (0 if c.endswith("VALU2") else 1000), 3])
+    (d / "meta.json").write_text(json.dumps({"lib_srchash": "abc",
+                                             "kernels": ["k_pyramid<false>", "k_pyramid<true>"]}))
+    monkeypatch.setattr(bench, "library_hash", lambda: ("abc", False, root))
+    t_true, _ = bench.pmc_traffic(str(d), ["k_pyramid<true>"])
+    t_false, _ = bench.pmc_traffic(str(d), ["k_pyramid<false>"])
+    assert t_true is not None and t_false is not None and t_true == 3 * t_false
+    it = bench.pmc_issue(str(d), ["k_pyramid<true>"], 100.0)
+    iff = bench.pmc_issue(str(d), ["k_pyramid<false>"], 100.0)
+    assert it["valu_instr_per_launch"] == 300000 and iff["valu_instr_per_launch"] == 100000
+    # an instance the passes do not hold: null, with the reason
+    t, why = bench.pmc_traffic(str(d), ["k_fast_pairs<unsigned int>"])
+    assert t is None and "k_fast_pairs<unsigned int>" in why
+    assert bench.pmc_issue(str(d), ["k_fast_pairs<unsigned int>"], 100.0)["frac"] is None
+    # passes of another build: null, with the reason
+    monkeypatch.setattr(bench, "library_hash", lambda: ("other", False, root))
+    t, why = bench.pmc_traffic(str(d), ["k_pyramid<true>"])
+    assert t is None and "another library build" in why
+    assert bench.pmc_issue(str(d), ["k_pyramid<true>"], 100.0)["frac"] is None
+    # no meta.json: not bound to a build
+    (d / "meta.json").unlink()
+    monkeypatch.setattr(bench, "library_hash", lambda: ("abc", False, root))
+    t, why = bench.pmc_traffic(str(d), ["k_pyramid<true>"])
+    assert t is None and "meta.json" in why
+    # roofline_of carries the instances and nulls the counter fields
+    r = bench.roofline_of({"k_pyramid": (2.0, 15)}, {"k_pyramid": 600.0}, str(d), 5, 512,
+                          {"k_pyramid": ["k_pyramid<true>"]})
+    assert r["kernel_instances"] == ["k_pyramid<true>"] and r["traffic"] is None
+    assert r["issue_roofline"]["frac"] is None
+
+
+def test_kernel_instance_names():
+    """rocprofv3 Kernel_Name -> the library profiler's instance name."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    ki = bench.kernel_instance
+    assert ki("void orbx::k_fast_cells<44, 42, unsigned int>(unsigned char const*, long)") == \
+        "k_fast_cells<44, 42, unsigned int>"
+    assert ki("void orbx::k_octree<1024, unsigned long>(orbx::LevelGeom const*, int)") == \
+        "k_octree<1024, unsigned long>"
+    assert ki("orbx::k_tri_nodes(orbx::TriProblem const*)") == "k_tri_nodes"
+    assert ki("(anonymous namespace)::k_fill_u32(unsigned int*, unsigned long)") == "k_fill_u32"

@@ -49,6 +49,24 @@ def test_search_by_projection_last_frame_vo_points(stereo, th, fwd, bwd, ori):
     assert (om >= len(L["valid"])).any()  # some copies took their feature over
 
 
+@pytest.mark.parametrize("stereo,th,fwd", [(True, 7.0, 0), (False, 15.0, 1)])
+def test_search_by_projection_last_frame_split_takeovers(stereo, th, fwd):
+    """A feature taken over by a point whose rotation bin is on the other side of the top-3 cut
+    (ORBmatcher.cc:1440-1468, advisor round 4): k_proj_resolve's log-based removal nulls it and
+    counts each removed entry once, as the oracle and its Python restatement do."""
+    from test_projection_oracle import last_with_split_takeovers, py_last, split_takeover_features
+    F, _, L = scene(stereo=stereo, seed=int(th) + fwd)
+    L2 = last_with_split_takeovers(L, int(th))
+    n, m = ORBmatcher(0.9, True).SearchByProjection(F, L2, th, forward=fwd, backward=0)
+    on, om = O.search_by_projection_last(F, L2, th, fwd, 0, True)
+    assert n == on and np.array_equal(m, om)
+    st = {}
+    py_last(F, L2, th, fwd, 0, True, st)
+    split, removed = split_takeover_features(st["hist"], st["kept"])
+    assert len(split) >= 10 and (m[split] == -1).all()
+    assert n == sum(len(b) for b in st["hist"]) - removed
+
+
 def test_projection_edge_cases():
     F, P, L = scene(w=376, h=240, nf=400)
     # no points

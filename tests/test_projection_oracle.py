@@ -170,6 +170,8 @@ def py_last(F, L, th, fwd, bwd, ori, stats=None):
                     nm -= 1
     if stats is not None:
         stats["takeovers"] = takeovers
+        stats["hist"] = hist
+        stats["kept"] = {i1, i2, i3} - {-1} if ori else set(range(30))
     return nm, np.array(match, np.int32)
 
 
@@ -232,6 +234,45 @@ def test_search_by_projection_last_frame_vo_points(stereo, th, fwd, bwd, ori):
     n1, m1 = O.search_by_projection_last(F, L2, th, fwd, bwd, ori)
     n0, m0 = O.search_by_projection_last(F, dict(L2, blocks=None), th, fwd, bwd, ori)
     assert n1 == n0 and np.array_equal(m1, m0)
+
+
+def last_with_split_takeovers(L, seed):
+    """last_with_vo_points with the copies' angles turned by 150 degrees: a copy that takes a
+    feature over lands in a rotation bin 5 away from the original's, so the feature has one
+    histogram entry inside the three maxima and one outside (ORBmatcher.cc:1440-1468).  The
+    reference nulls mvpMapPoints[feature] for the entry outside — whichever point holds it by
+    then — and decrements nmatches once per such entry."""
+    L2 = last_with_vo_points(L, seed)
+    n0 = len(L["valid"])
+    L2["angle"] = L2["angle"].copy()
+    L2["angle"][n0:] = np.mod(L2["angle"][n0:] + np.float32(150), np.float32(360)).astype(np.float32)
+    L2["blocks"][:n0] = 0  # every original is a visual-odometry point: its copy may take over
+    return L2
+
+
+def split_takeover_features(hist, kept):
+    """Features with one rotation-histogram entry in a kept bin and one in a removed bin."""
+    inside = {i for b in kept for i in hist[b]}
+    outside = {i for b in range(30) if b not in kept for i in hist[b]}
+    return sorted(inside & outside), sum(len(hist[b]) for b in range(30) if b not in kept)
+
+
+@pytest.mark.parametrize("stereo,th,fwd", [(True, 7.0, 0), (False, 15.0, 1)])
+def test_search_by_projection_last_frame_split_takeovers(stereo, th, fwd):
+    """A feature taken over (advisor, round 4): its two rotHist entries straddle the top-3 cut.
+    The oracle's log-based removal equals the Python restatement, every such feature ends
+    unmatched, and nmatches = assignments - entries in the removed bins."""
+    F, _, L = scene(stereo=stereo, seed=int(th) + fwd)
+    L2 = last_with_split_takeovers(L, int(th))
+    n, m = O.search_by_projection_last(F, L2, th, fwd, 0, True)
+    st = {}
+    pn, pm = py_last(F, L2, th, fwd, 0, True, st)
+    assert n == pn and np.array_equal(m, pm)
+    split, removed = split_takeover_features(st["hist"], st["kept"])
+    assert len(split) >= 10
+    assert (m[split] == -1).all()
+    assigned = sum(len(b) for b in st["hist"])
+    assert n == assigned - removed
 
 
 def three_maxima(counts):
