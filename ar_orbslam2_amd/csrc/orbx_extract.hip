@@ -264,22 +264,23 @@ __device__ __forceinline__ blur_u16x2 blur_col(const blur_u16x2 (&U)[N], int j) 
          U[j + 3] * K3;
 }
 
-// The fused blur (k_pyramid<true>) of one level's own band rows [own_lo, own_hi), all columns,
-// from the band's rows [lo, hi) of the level in LDS (row stride lp, column 0 at byte 16; the
-// reflected columns -4..-1 and w..w+2 are in the row's pads, so no lane handles a column border).
-// A lane holds one dword column (-1 .. gl+1, gl = the last column group with a pixel) over a
-// strip of S output rows: it unpacks its S + 6 input dwords into byte pairs once, and per output
-// row forms the column sums of its 4 columns and takes its neighbours' by DPP wave shifts (lanes
-// are consecutive columns of a strip; each wave's first and last lane only lend their sums, so
-// consecutive waves overlap by two columns).  Rows outside the level reflect (BORDER_REFLECT_101).
+// The fused blur (k_pyramid<true>) of one level's own tile: rows [own_lo, own_hi), groups
+// [own_glo, own_ghi), from the tile's rows [lo, hi) of the level in LDS (row stride lp, column c
+// at byte c - cb; the tile holds the group left and right of its own ones, at the level's edges
+// the reflected columns -4..-1 and w..: no lane handles a column border).
+// A lane holds one dword column (own_glo - 1 .. own_ghi) over a strip of S output rows: it
+// unpacks its S + 6 input dwords into byte pairs once, and per output row forms the column sums
+// of its 4 columns and takes its neighbours' by DPP wave shifts (lanes are consecutive columns
+// of a strip; each wave's first and last lane only lend their sums, so consecutive waves overlap
+// by two columns).  Rows outside the level reflect (BORDER_REFLECT_101).
 template <int S>
-__device__ __forceinline__ void py_blur_band(const uint8_t* __restrict__ sb, int lp, int lo, int hi,
-                                             const LevelGeom& G, int own_lo, int own_hi,
-                                             uint8_t* __restrict__ dst) {
+__device__ __forceinline__ void py_blur_band(const uint8_t* __restrict__ sb, int lp, int cb, int lo,
+                                             int hi, const LevelGeom& G, int own_lo, int own_hi,
+                                             int own_glo, int own_ghi, uint8_t* __restrict__ dst) {
   const int R = own_hi - own_lo;
-  if (R <= 0) return;
-  const int w = G.w, h = G.h, pitch = G.pitch, bxs = G.bxs;
-  const int gl = (w - 1) >> 2, ngp = gl + 3;
+  if (R <= 0 || own_ghi <= own_glo) return;
+  const int h = G.h, pitch = G.pitch, bxs = G.bxs;
+  const int ngp = own_ghi - own_glo + 2;
   const int nitems = ((R + S - 1) / S) * ngp;
   const int lane = threadIdx.x & 63;
   const float inv = 1.0f / (float)ngp;
@@ -287,8 +288,8 @@ __device__ __forceinline__ void py_blur_band(const uint8_t* __restrict__ sb, int
     const int iu = base + lane - 1;
     int st, c;
     py_divmod(min(max(iu, 0), nitems - 1), ngp, inv, st, c);
-    const int cc = c - 1, y0 = own_lo + st * S;
-    const uint8_t* col = sb + 16 + 4 * cc;
+    const int cc = own_glo - 1 + c, y0 = own_lo + st * S;
+    const uint8_t* col = sb + 4 * cc - cb;
     blur_u16x2 U[S + 6], V[S + 6];
     if (__all(y0 - 3 >= lo && y0 + S + 2 < hi)) {  // the strip's rows lie in the band
       const uint8_t* p = col + __mul24(y0 - 3 - lo, lp);
@@ -307,7 +308,7 @@ __device__ __forceinline__ void py_blur_band(const uint8_t* __restrict__ sb, int
         V[k] = byte_pair(d, d, 0x0c030c02u);
       }
     }
-    const bool out = lane >= 1 && lane <= 62 && iu < nitems && cc >= 0 && cc <= gl;
+    const bool out = lane >= 1 && lane <= 62 && iu < nitems && cc >= own_glo && cc < own_ghi;
     const uint32_t tail = 4 * cc < bxs ? 0u : 1u;
     uint8_t* drow = dst + __mul24(y0, pitch) + 4 * cc;
 #pragma unroll
@@ -340,26 +341,29 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
                                                   const int2* __restrict__ ytap, int buf_b,
                                                   uint8_t* __restrict__ blur) {
   extern __shared__ __align__(16) uint8_t s_pyr[];
-  constexpr int kPad = BLUR ? 16 : 0;  // column 0 of a level row in LDS (py_lds_pitch)
   int band, img;
   xcd_block(band, img);
   const PyrBand& B = bands[band];
   const int tid = threadIdx.x;
   uint8_t* base = pyr + (int64_t)img * pyr_bytes;
   uint8_t* bbase = BLUR ? blur + (int64_t)img * pyr_bytes : nullptr;
-  {  // the source level's band rows into LDS (buffer of parity l0 - 1)
+  {  // the source level's tile (rows lo..hi-1, columns cb .. cb + lp - 1) into LDS (buffer of
+     // parity l0 - 1); level 0 is copied into the pyramid by the tile that owns it
     const LevelGeom& G = lv[l0 - 1];
-    const int lo = B.lo[l0 - 1], nr = B.hi[l0 - 1] - lo, pitch = G.pitch, lp = py_lds_pitch(G, BLUR);
-    uint8_t* sdst = s_pyr + ((l0 - 1) & 1 ? buf_b : 0) + kPad;
+    const int lo = B.lo[l0 - 1], nr = B.hi[l0 - 1] - lo, pitch = G.pitch;
+    const int cb = B.cb[l0 - 1], lp = B.lp[l0 - 1];
+    uint8_t* sdst = s_pyr + ((l0 - 1) & 1 ? buf_b : 0);
     const bool input = l0 == 1;  // level 0 comes from the input (ORBextractor.cc:1066-1068)
     const int w = input ? G.w : pitch;  // a pyramid row is copied pad and all
     const uint8_t* src = input ? in + (int64_t)img * G.h * G.w : base + G.pyr_off;
     const int own_lo = input ? B.own_lo[0] : 0, own_hi = input ? B.own_hi[0] : 0;
+    const int own_x0 = 4 * B.own_glo[0], own_x1 = 4 * B.own_ghi[0];
     uint8_t* dst = base + G.pyr_off;
     const bool pads = BLUR && input;  // level 0 is blurred: its rows' reflected pad columns
+    const int c0 = max(cb, 0) >> 4, c1 = min((cb + lp) >> 4, (w + 15) >> 4);  // 16-B chunks
     if ((w & 15) == 0) {  // 16-byte chunks, four per thread in flight
-      const int nch = w >> 4, items = nr * nch;
-      const float inv = 1.0f / (float)nch;
+      const int nch = c1 - c0, items = nr * nch;
+      const float inv = 1.0f / (float)max(nch, 1);
       for (int i0 = tid; i0 < items; i0 += kPyLoads * kPyNT) {
         // past the end a thread repeats the last chunk: identical bytes to identical places
         uint4 v[kPyLoads];
@@ -367,6 +371,7 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
 #pragma unroll
         for (int u = 0; u < kPyLoads; u++) {
           py_divmod(min(i0 + kPyNT * u, items - 1), nch, inv, rr[u], cc[u]);
+          cc[u] += c0;
           v[u] = *(const uint4*)(src + (int64_t)(lo + rr[u]) * w + 16 * cc[u]);
         }
 #pragma unroll
@@ -374,72 +379,64 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
           asm volatile("" : "+v"(v[u].x), "+v"(v[u].y), "+v"(v[u].z), "+v"(v[u].w));
 #pragma unroll
         for (int u = 0; u < kPyLoads; u++) {
-          const int y = lo + rr[u];
-          uint8_t* srow = sdst + __mul24(rr[u], lp);
-          *(uint4*)(srow + 16 * cc[u]) = v[u];
-          if (y >= own_lo && y < own_hi) *(uint4*)(dst + (uint32_t)__mul24(y, pitch) + 16 * cc[u]) = v[u];
+          const int y = lo + rr[u], x = 16 * cc[u];
+          uint8_t* srow = sdst + __mul24(rr[u], lp) - cb;  // column c at srow + c
+          *(uint4*)(srow + x) = v[u];
+          if (y >= own_lo && y < own_hi && x >= own_x0 && x < own_x1)
+            *(uint4*)(dst + (uint32_t)__mul24(y, pitch) + x) = v[u];
           if (pads) {  // columns -4..-1 = 4, 3, 2, 1; w..w+3 = w-2 .. w-5 (w >= 16 here)
-            if (cc[u] == 0) *(uint32_t*)(srow - 4) = __builtin_amdgcn_perm(v[u].y, v[u].x, 0x01020304u);
-            if (cc[u] == nch - 1) *(uint32_t*)(srow + w) = __builtin_amdgcn_perm(v[u].w, v[u].z, 0x03040506u);
+            if (x == 0 && cb < 0) *(uint32_t*)(srow - 4) = __builtin_amdgcn_perm(v[u].y, v[u].x, 0x01020304u);
+            if (x == w - 16 && cb + lp > w) *(uint32_t*)(srow + w) = __builtin_amdgcn_perm(v[u].w, v[u].z, 0x03040506u);
           }
         }
       }
-    } else {  // any input width: dwords assembled from bytes
-      const int q4 = (w + 3) >> 2, items = nr * q4;
+    } else {  // any input width: dwords assembled from bytes, the columns outside the level
+              // reflected (only the blurred level 0 reads them)
+      const int q0 = cb >> 2, q4 = lp >> 2, items = nr * q4;
       const float inv = 1.0f / (float)q4;
       for (int i = tid; i < items; i += kPyNT) {
         int r, c;
         py_divmod(i, q4, inv, r, c);
-        const int x4 = 4 * c, y = lo + r;
+        const int x4 = 4 * (q0 + c), y = lo + r;
         const uint8_t* s = src + (int64_t)y * w;
-        uint8_t* srow = sdst + __mul24(r, lp);
-        uint32_t v;
-        if (pads && c == q4 - 1) {  // the last dword: columns past w reflected, and the next one
-          uint32_t pv = 0;
-          v = 0;
+        uint32_t v = 0;
+        if (x4 >= 0 && x4 + 3 < w) {
+          v = s[x4] | (uint32_t)s[x4 + 1] << 8 | (uint32_t)s[x4 + 2] << 16 | (uint32_t)s[x4 + 3] << 24;
+        } else if (pads) {
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
-            v |= (uint32_t)s[reflect101(x4 + k, w)] << (8 * k);
-            pv |= (uint32_t)s[reflect101(x4 + 4 + k, w)] << (8 * k);
-          }
-          *(uint32_t*)(srow + x4 + 4) = pv;
+          for (int k = 0; k < 4; k++) v |= (uint32_t)s[reflect101(x4 + k, w)] << (8 * k);
         } else {
-          v = s[x4];
-          if (x4 + 1 < w) v |= (uint32_t)s[x4 + 1] << 8;
-          if (x4 + 2 < w) v |= (uint32_t)s[x4 + 2] << 16;
-          if (x4 + 3 < w) v |= (uint32_t)s[x4 + 3] << 24;
-        }
-        if (pads && c == 0) {
-          uint32_t pv = 0;
 #pragma unroll
-          for (int k = 0; k < 4; k++) pv |= (uint32_t)s[reflect101(k - 4, w)] << (8 * k);
-          *(uint32_t*)(srow - 4) = pv;
+          for (int k = 0; k < 4; k++)
+            if (x4 + k >= 0 && x4 + k < w) v |= (uint32_t)s[x4 + k] << (8 * k);
         }
-        *(uint32_t*)(srow + x4) = v;
-        if (y >= own_lo && y < own_hi) *(uint32_t*)(dst + (uint32_t)__mul24(y, pitch) + x4) = v;
+        *(uint32_t*)(sdst + __mul24(r, lp) + 4 * c) = v;
+        if (y >= own_lo && y < own_hi && x4 >= own_x0 && x4 < own_x1)
+          *(uint32_t*)(dst + (uint32_t)__mul24(y, pitch) + x4) = v;
       }
     }
   }
   for (int l = l0; l <= l1; l++) {
-    __syncthreads();  // level l-1 of this band is in LDS
+    __syncthreads();  // level l-1 of this tile is in LDS
     const LevelGeom& D = lv[l];
     const LevelGeom& S = lv[l - 1];
     const uint8_t* sb = s_pyr + ((l - 1) & 1 ? buf_b : 0);
-    uint8_t* db = s_pyr + (l & 1 ? buf_b : 0) + kPad;
+    uint8_t* db = s_pyr + (l & 1 ? buf_b : 0) - B.cb[l];  // column c of a row at + c
     uint8_t* dp = base + D.pyr_off;
     const int slo = B.lo[l - 1], dlo = B.lo[l];
-    const int gl = (D.w - 1) >> 2;
-    // column groups: 0 .. gl, and with BLUR the pad groups -1 and gl + 1 (LDS only)
-    const int g0 = BLUR ? -1 : 0, ng = BLUR ? gl + 3 : gl + 1;
+    const int scb = B.cb[l - 1];
+    // column groups glo .. ghi - 1: with BLUR the pad groups -1 and gl + 1 at the level's edges
+    // (LDS only)
+    const int g0 = B.glo[l], ng = max(0, B.ghi[l] - g0);
     const int nr = max(0, B.hi[l] - dlo), nstrip = (nr + kPyStrip - 1) / kPyStrip;
     const int items = nstrip * ng;
-    const float inv_ng = 1.0f / (float)ng;
+    const float inv_ng = 1.0f / (float)max(ng, 1);
     const bool keep = BLUR || l < l1;  // without the blur the stage's last level is not read back
-    const int dpitch = D.pitch, dlp = py_lds_pitch(D, BLUR), slp = py_lds_pitch(S, BLUR), sh1 = S.h - 1;
-    const int own_lo = B.own_lo[l], own_hi = B.own_hi[l];
+    const int dpitch = D.pitch, dlp = B.lp[l], slp = B.lp[l - 1], sh1 = S.h - 1;
+    const int own_lo = B.own_lo[l], own_hi = B.own_hi[l], own_glo = B.own_glo[l], own_ghi = B.own_ghi[l];
     const int2* xt = xtap + D.coef_x;
     const int2* yt = ytap + D.coef_y + dlo;
-    const uint8_t* sb16 = sb + kPad;
+    const uint8_t* sbx = sb - scb;  // column c of a source row at + c
     // work item = (strip of kPyStrip output rows, 4-pixel column group): the taps are loaded
     // once per item, and a source row's horizontal sums carry over to the next output row
     // that reads it (scale 1.2: 1.2 horizontal passes per output row instead of 2)
@@ -455,15 +452,15 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
       const int xs[4] = {t01.x & 0xFFFFF, t01.z & 0xFFFFF, t23.x & 0xFFFFF, t23.z & 0xFFFFF};
       const uint32_t as[4] = {(uint32_t)t01.y, (uint32_t)t01.w, (uint32_t)t23.y, (uint32_t)t23.w};
       const int r0 = st * kPyStrip, r1 = min(nr, r0 + kPyStrip);
-      const bool gwrite = gi >= 0 && gi <= gl;
+      const bool gwrite = gi >= own_glo && gi < own_ghi;
       int prev = -1;
       uint32_t gp[4] = {0u, 0u, 0u, 0u};
       for (int r = r0; r < r1; r++) {
         const int2 ty = yt[r];
         const int ya = min(max(ty.x, 0), sh1), yb = min(max(ty.x + 1, 0), sh1);
-        if (ya != prev) py_horiz(sb16 + __mul24(ya - slo, slp), xs, as, gp);
+        if (ya != prev) py_horiz(sbx + __mul24(ya - slo, slp), xs, as, gp);
         uint32_t g1[4];
-        py_horiz(sb16 + __mul24(yb - slo, slp), xs, as, g1);
+        py_horiz(sbx + __mul24(yb - slo, slp), xs, as, g1);
         const uint32_t o = py_vert(gp, g1, (uint32_t)ty.y, sc);
         // pitch >= w + 4: bytes past w of the last group land in the row's pad
         if (keep) *(uint32_t*)(db + __mul24(r, dlp) + dx0) = o;
@@ -475,14 +472,15 @@ __global__ __launch_bounds__(kPyNT) void k_pyramid(const uint8_t* __restrict__ i
       }
     }
     if (BLUR && (l > l0 || l0 == 1))  // level l-1 is blurred from the same buffer
-      py_blur_band<kPyBlurStrip>(sb, slp, slo, B.hi[l - 1], S, B.own_lo[l - 1], B.own_hi[l - 1],
-                                 bbase + S.pyr_off);
+      py_blur_band<kPyBlurStrip>(sb, slp, scb, slo, B.hi[l - 1], S, B.own_lo[l - 1], B.own_hi[l - 1],
+                                 B.own_glo[l - 1], B.own_ghi[l - 1], bbase + S.pyr_off);
   }
   if (BLUR) {  // the stage's last level (level 0 alone for a one-level pyramid)
     __syncthreads();
     const LevelGeom& D = lv[l1];
-    py_blur_band<kPyBlurStrip>(s_pyr + (l1 & 1 ? buf_b : 0), py_lds_pitch(D, true), B.lo[l1], B.hi[l1], D,
-                               B.own_lo[l1], B.own_hi[l1], bbase + D.pyr_off);
+    py_blur_band<kPyBlurStrip>(s_pyr + (l1 & 1 ? buf_b : 0), B.lp[l1], B.cb[l1], B.lo[l1], B.hi[l1], D,
+                               B.own_lo[l1], B.own_hi[l1], B.own_glo[l1], B.own_ghi[l1],
+                               bbase + D.pyr_off);
   }
 }
 
@@ -643,6 +641,27 @@ struct KeyFmt<uint64_t> {
   static __device__ __forceinline__ unsigned score(uint64_t k) { return (unsigned)(k >> 32); }
 };
 
+// A cell's geometry by whole dwords from a wave-uniform index: two 16-B scalar loads (a field
+// read as int16 became a vector load, and the wait for it exposed a memory latency per cell)
+__device__ __forceinline__ CellGeom load_cell(const CellGeom* __restrict__ cells, int i) {
+  const int4* p = (const int4*)(cells + i);
+  const int4 a = p[0], b = p[1];
+  CellGeom c;
+  c.x0 = (int16_t)(a.x & 0xFFFF);
+  c.y0 = (int16_t)(a.x >> 16);
+  c.x1 = (int16_t)(a.y & 0xFFFF);
+  c.y1 = (int16_t)(a.y >> 16);
+  c.offx = (int16_t)(a.z & 0xFFFF);
+  c.offy = (int16_t)(a.z >> 16);
+  c.level = (int16_t)(a.w & 0xFFFF);
+  c.pad16 = (int16_t)(a.w >> 16);
+  c.slot_off = b.x;
+  c.slot_cap = b.y;
+  c.v_row0 = b.z;
+  c.pitch = b.w;
+  return c;
+}
+
 // raster-order compaction of a cell's keep rows (lane = detection row): out slot, count
 template <class K, class VAt>
 __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int cx0,
@@ -761,7 +780,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
       pv[u] = *(const uint32_t*)(srow + (uint32_t)__mul24(min(lrow + kG * u, rows - 1), C.pitch));
   };
   int ci = list[l0];
-  CellGeom C = cells[ci];
+  CellGeom C = load_cell(cells, ci);
   issue(C);
   for (int li = l0; li < l1; li++) {
     const int rows = C.y1 - C.y0, cols = C.x1 - C.x0;  // <= MAXR, <= RS - 3
@@ -776,7 +795,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     const int cic = ci;
     if (li + 1 < l1) {
       ci = list[li + 1];
-      C = cells[ci];
+      C = load_cell(cells, ci);
       issue(C);
     }
     if (dr <= 0 || cw <= 0) {
@@ -858,47 +877,57 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
 // ---- k_fast_pairs: two horizontally adjacent FAST cells of one cell row per wave.  Cell j's
 // ROI ends 3 px past its detection columns, where cell j + 1's detection columns begin
 // (ORBextractor.cc:766-773: iniX = minBorderX + j wCell, maxX = iniX + wCell + 6), so the two
-// cells' detection columns are contiguous and one staged ROI of up to 70 x 42 px serves both:
-// the cardinal pretest runs on all 64 lanes (one detection column each, cwA + cwB <= 64) instead
-// of the 31-32 lanes of a single ~31-px cell, the candidates of both cells share the scoring and
-// NMS rounds, and staging, the V map, the scans and the compaction are paid once per pair.  The
-// NMS stays cell-local: the V map holds a zero column between the two cells' columns (and the
-// zero ring around them), so a neighbour across the cell edge counts as 0, as on the reference's
-// per-cell ROI.  A cell without a keypoint at iniThFAST runs FAST again at minThFAST on its own
-// columns (:782-784); each cell's survivors go to its own slot in raster order.
-// Queue entries: (detection row r) << 6 | column c.  A pass whose candidates outgrow the queue
+// cells' detection columns are contiguous and one staged ROI of up to 70 x 40 px serves both:
+// the cardinal pretest runs on all 64 lanes (one detection column each, cwA + cwB <= 64), the
+// candidates of both cells share the scoring and NMS rounds, and staging, the V map, the scans
+// and the compaction are paid once per pair.  The NMS stays cell-local: the V map holds a zero
+// column between the two cells' columns (and the zero ring around them), so a neighbour across
+// the cell edge counts as 0, as on the reference's per-cell ROI.  A cell without a keypoint at
+// iniThFAST runs FAST again at minThFAST on its own columns (:782-784); each cell's survivors go
+// to its own slot in raster order.
+//
+// The staged ROI is a column-major plane of u16 pairs: word k of a column holds ROI rows k and
+// k + kPairD (low / high halves, one byte each), k < kPairD + 6.  A pretest step takes
+// detection rows s and s + kPairD of the lane's column in the two halves of one register, and
+// each of its five inputs — the centre and the circle points (0, -3), (3, 0), (0, 3), (-3, 0) —
+// is ONE aligned ds_read_b32: words s + 3 (centre; columns +-3 for the side points), s and s + 6.
+// The arc test runs on packed u16 maxima / minima:
+//   brighter candidate  min(max(x0, x8), max(x4, x12)) > v + t
+//   darker candidate    max(min(x0, x8), min(x4, x12)) < v - t
+// (any arc of 9 holds two adjacent cardinal points), 12 VALU per two pixels with the flag
+// word's shift, against round 4's 22 on byte rows (five d16 merges per two pixels).  Staging
+// is two 16-B loads per lane per round (rows k and k + 17 of a 16-column chunk, exactly the ROI's
+// rows and dwords: no clamped re-reads) and a v_perm per stored word.  A candidate's 7 x 7
+// window lies in one copy (low halves for detection rows < kPairD, high ones after), so the
+// scorer reads uniform offsets.
+// Queue entries: (detection row) << 6 | column.  A pass whose candidates outgrow the queue
 // (dense texture) scores the rest in place, lane by lane, and then runs the NMS over the V map
 // instead of the queue (same result: the NMS candidates are the pixels with V > t).
-constexpr int kPairRS = 76;                          // staged ROI row: <= 70 px + 3 alignment
-constexpr int kPairRows = kFcSmallRows;              // ROI rows (detection rows <= 36)
-constexpr int kPairStage = 13;                       // staging rounds of 64 dwords (43.8 rows)
-constexpr int kPairSrc = kPairRS * (kPairRows + 6);  // + the keep rows (krows)
-constexpr int kPairKeepRows = 40;                    // >= detection rows
-constexpr int kPairVS = 72;                          // V row: ring, cwA, gap, cwB, ring
-constexpr int kPairVRows = kPairRows - 4;            // detection rows + 2 ring rows
-constexpr int kPairQ = 768;                          // queue entries
+constexpr int kPairRS = 76;        // host eligibility: ROI width + its dword slack <= 76 bytes
+constexpr int kPairRows = 40;      // ROI rows (detection rows <= 34)
+constexpr int kPairD = 17;         // the second row of a lane step: detection row s + kPairD
+constexpr int kPairWords = kPairD + 6;   // plane words per column: ROI rows (k, k + kPairD)
+constexpr int kPairCS = 4 * kPairWords;  // 92 B per staged column: 23 dwords, odd (no conflicts)
+constexpr int kPairCols = 70;            // staged ROI columns (cwA + cwB + 6)
+constexpr int kPairQ = 384;              // queue entries
+constexpr int kPairKeepRows = 2 * kPairD;  // keep row per detection row
+constexpr int kPairVS = 40;        // V map: column-major, a column of ring + 34 rows + ring
+constexpr int kPairVCols = 67;     // ring, cwA, gap, cwB, ring
+// a wave's LDS: [queue][keep rows][plane][V map].  Staging writes whole 16-column chunks: up to
+// 3 columns before the plane (into the keep rows / queue, dead while a pair is staged) and up
+// to 10 past it (into the V map, zeroed after staging)
+constexpr int kPairOffK = 2 * kPairQ;
+constexpr int kPairOffP = kPairOffK + 8 * kPairKeepRows;
+constexpr int kPairOffV = (kPairOffP + kPairCS * kPairCols + 15) & ~15;
+constexpr int kPairVBytes = (kPairVS * kPairVCols + 15) & ~15;
+constexpr int kPairLds = kPairOffV + kPairVBytes;
 constexpr int kPairsPerWave = 4;
-static_assert(kPairStage * 256 >= kPairRows * kPairRS, "staging covers the ROI");
-static_assert(kPairStage * 256 <= kPairSrc - 8 * kPairKeepRows, "keep rows past the staged bytes");
-static_assert(kPairKeepRows >= kPairRows - 6, "a keep row per detection row");
-static_assert((kPairVS * kPairVRows) % 16 == 0, "V map in 16-B pieces");
-
-// Stage 1 of one detection chunk on all 64 lanes: rows r0 + 2 s and r0 + 2 s + 1 for steps
-// s < nst <= 16, two steps per LDS round trip; the flags of step s end at bit s (row r0 + 2 s)
-// and bit 16 + s (row r0 + 2 s + 1).
-template <int RS>
-__device__ __forceinline__ uint32_t cardinal_chunk16(const uint8_t* c0, int nst, int t) {
-  uint32_t acc = 0;
-  const uint8_t* c = c0;
-  int s = 0;
-  for (; s + 2 <= nst; s += 2, c += 4 * RS) {
-    uint32_t f0, f1;
-    fast_cardinal2x2<RS, 2 * RS>(c, t, f0, f1);
-    acc = (acc >> 2) | (f0 >> 1) | f1;
-  }
-  if (s < nst) acc = (acc >> 1) | fast_cardinal2<RS>(c, t);
-  return acc >> (16 - nst);
-}
+static_assert(kPairOffK % 8 == 0 && kPairOffP % 4 == 0 && kPairOffV % 16 == 0, "LDS alignment");
+static_assert(3 * kPairCS <= kPairOffP, "left staging spill stays in the wave's LDS");
+static_assert(10 * kPairCS <= kPairVBytes, "right staging spill stays in the V map");
+static_assert(kPairRows <= kPairWords + kPairD, "plane rows cover the ROI");
+static_assert(kPairVS >= kPairKeepRows + 2, "V column holds the ring rows");
+static_assert(4 * kPairLds <= 40 * 1024, "four workgroups per CU");
 
 template <class K>
 __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ pyr,
@@ -908,9 +937,7 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
                                                     int ncells, int ini_th, int min_th,
                                                     K* __restrict__ cand, int cand_total,
                                                     int* __restrict__ cell_counts, int ppw) {
-  __shared__ __align__(16) uint8_t s_src[4][kPairSrc];
-  __shared__ __align__(16) uint8_t s_vv[4][kPairVS * kPairVRows];
-  __shared__ uint16_t s_q[4][kPairQ];
+  __shared__ __align__(16) uint8_t s_lds[4][kPairLds];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bx, img;
@@ -918,93 +945,153 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
   const int p0 = (bx * 4 + wid) * ppw;
   if (p0 >= npairs) return;  // wave-uniform; no workgroup barrier below
   const int p1 = min(p0 + ppw, npairs);
-  uint8_t* S = s_src[wid];
-  uint8_t* V = s_vv[wid];
-  uint16_t* q = s_q[wid];
-  // keep bits per detection row: the end of the staging buffer, past every staged byte (the
-  // pretest reads rows up to dr + 6 <= 42: inside the staged bytes)
-  uint64_t* const krows = (uint64_t*)(S + kPairSrc - 8 * kPairKeepRows);
+  uint8_t* const W = s_lds[wid];
+  uint16_t* const q = (uint16_t*)W;
+  uint64_t* const krows = (uint64_t*)(W + kPairOffK);
+  uint8_t* const Pl = W + kPairOffP;  // plane: column x, word k at Pl + x * kPairCS + 4 k
+  uint8_t* const V = W + kPairOffV;
   const uint8_t* pimg = pyr + (int64_t)img * pyr_bytes;
-  // ROI staging: dword lane + 64 u of the staged rows (row (lane + 64 u) / 19, word % 19), so
-  // every lane loads and stores every round; rows past the ROI read its last row (clamped),
-  // words past the ROI's last one read on into the pitch (never used: stage 1 masks their
-  // flags, scores read detection pixels' windows only)
-  constexpr int kW = kPairRS / 4;
-  int srow[kPairStage], swof[kPairStage];
+  // staging tasks of this lane, rounds u = 0, 1: plane word k of a 16-column chunk ch (lanes
+  // take consecutive words of a chunk: conflict-free LDS stores)
+  int tk[2], tch[2];
 #pragma unroll
-  for (int u = 0; u < kPairStage; u++) {
+  for (int u = 0; u < 2; u++) {
     const int i = lane + 64 * u;
-    srow[u] = i / kW;
-    swof[u] = 4 * (i - kW * srow[u]);
+    tch[u] = i / kPairWords;
+    tk[u] = i - kPairWords * tch[u];
   }
-  uint32_t pv[kPairStage];
-  auto issue = [&](const CellGeom& A) {
-    const int last = A.y1 - A.y0 - 1;
-    const uint8_t* src = pimg + (A.v_row0 - 3 * A.pitch - 3) + (A.x0 & ~3) - A.x0;
+  // 16-B loads at dword alignment (global_load_dwordx4 needs only that on gfx950)
+  typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+  u32x4_a4 pv[2][2];
+  int xoff = 0, nch = 0;
+  auto issue = [&](const CellGeom& A, const CellGeom& B) {
+    const int rows = A.y1 - A.y0;
+    xoff = A.x0 & 3;
+    nch = (xoff + (B.x1 - A.x0) + 15) >> 4;
+    const uint8_t* src = pimg + (A.v_row0 - 3 * A.pitch - 3) - xoff;  // ROI row 0, dword aligned
+    // every lane loads, branch-free: a task past the ROI's rows or chunks reads the last row /
+    // chunk (lines the wave's other lanes request anyway; its words are never used)
 #pragma unroll
-    for (int u = 0; u < kPairStage; u++)
-      pv[u] = *(const uint32_t*)(src + (uint32_t)(__mul24(min(srow[u], last), A.pitch) + swof[u]));
+    for (int u = 0; u < 2; u++) {
+      const int ch = min(tch[u], nch - 1);
+      const int r0 = min(tk[u], rows - 1), r1 = min(tk[u] + kPairD, rows - 1);
+      pv[u][0] = *(const u32x4_a4*)(src + (uint32_t)(__mul24(r0, A.pitch) + 16 * ch));
+      pv[u][1] = *(const u32x4_a4*)(src + (uint32_t)(__mul24(r1, A.pitch) + 16 * ch));
+    }
   };
   int2 pr = pairs[p0];
-  CellGeom A = cells[pr.x], B = cells[pr.y];
-  issue(A);
+  CellGeom A = load_cell(cells, pr.x), B = load_cell(cells, pr.y);
+  issue(A, B);
   for (int pi = p0; pi < p1; pi++) {
-    wave_sync();  // the previous pair's reads of S are done
+    wave_sync();  // the previous pair's reads of the wave's LDS are done
+    // the staged ROI as the plane: word (lo byte j of row k, hi byte j of row k + kPairD) of
+    // column 16 ch + j - xoff, one v_perm each
 #pragma unroll
-    for (int u = 0; u < kPairStage; u++) *(uint32_t*)(S + 256 * u + 4 * lane) = pv[u];
+    for (int u = 0; u < 2; u++) {
+      if (tch[u] < nch) {
+        uint8_t* dst = Pl + (16 * tch[u] - xoff) * kPairCS + 4 * tk[u];
+        const uint32_t lo[4] = {pv[u][0].x, pv[u][0].y, pv[u][0].z, pv[u][0].w};
+        const uint32_t hi[4] = {pv[u][1].x, pv[u][1].y, pv[u][1].z, pv[u][1].w};
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          const uint32_t b = j & 3;
+          const uint32_t sel = 0x0c000c00u | ((4 + b) << 16) | b;
+          *(uint32_t*)(dst + j * kPairCS) = __builtin_amdgcn_perm(hi[j >> 2], lo[j >> 2], sel);
+        }
+      }
+    }
     const CellGeom Ac = A, Bc = B;
     const int2 pc = pr;
     if (pi + 1 < p1) {  // the next pair's loads in flight while this one is processed
       pr = pairs[pi + 1];
-      A = cells[pr.x];
-      B = cells[pr.y];
-      issue(A);
+      A = load_cell(cells, pr.x);
+      B = load_cell(cells, pr.y);
+      issue(A, B);
     }
     const int dr = Ac.y1 - Ac.y0 - 6;                      // detection rows, both cells
     const int cwA = Ac.x1 - Ac.x0 - 6, cw = cwA + (Bc.x1 - Bc.x0 - 6);  // detection columns
-    for (int i = lane; i < ((dr + 2) * kPairVS + 15) / 16; i += 64) ((uint4*)V)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = lane; i < kPairVBytes / 16; i += 64) ((uint4*)V)[i] = make_uint4(0u, 0u, 0u, 0u);
     wave_sync();
-    const uint8_t* Sx = S + (Ac.x0 & 3);  // pixel (r, c) of the ROI at Sx[r * RS + c]
     const uint64_t mA = (1ull << cwA) - 1;  // cwA <= 60
     const uint64_t mB = (cw >= 64 ? ~0ull : (1ull << cw) - 1) & ~mA;
-    // V byte of detection pixel (r, c): one ring row and column, the gap column after cell A
-    auto vofs = [&](int r, int c) { return __mul24(r + 1, kPairVS) + c + 1 + (c >= cwA ? 1 : 0); };
+    // V byte of detection pixel (r, c): column-major, one ring row and column, the gap column
+    // after cell A
+    auto vofs = [&](int r, int c) { return __mul24(c + 1 + (c >= cwA ? 1 : 0), kPairVS) + r + 1; };
+    // cornerScore of detection pixel (r, c) from the copy holding its whole 7 x 7 window
     auto score_at = [&](int r, int c) {
-      const int sc = fast_score(Sx, kPairRS, c + 3, r + 3);
+      const bool hi = r >= kPairD;
+      const int sc = fast_score<kPairCS>(Pl + (hi ? 2 : 0), 4, c + 3, (hi ? r - kPairD : r) + 3);
       V[vofs(r, c)] = (uint8_t)min(255, max(0, sc + 1));
     };
     uint64_t allow = mA | mB;  // the columns this pass detects on
     uint64_t bits1 = 0, keep1 = 0;
     uint64_t bits = 0;  // this lane's keep row (lane = detection row)
     int t = ini_th;
+    // the lane's column in the plane (detection column lane: ROI column lane + 3)
+    const uint32_t* colw = (const uint32_t*)(Pl + (lane + 3) * kPairCS);
     for (int pass = 0; pass < 2; pass++) {
-      // (1) cardinal pretest at t, the flagged pixels queued (or scored in place past kPairQ)
+      // (1) cardinal pretest at t: steps 0..15 into acc (bit s: row s, bit 16 + s: row s + 17),
+      // step 16 into acc2 (bit 0: row 16, bit 1: row 33); every step runs (rows past dr read
+      // plane words that exist and are masked below: branch-free, the loads issued together)
+      const uint32_t T = (uint32_t)t * 0x10001u;
+      uint32_t acc = 0, acc2 = 0;
       const bool col_ok = (allow >> lane) & 1;
+#pragma unroll
+      for (int s = 0; s < kPairD; s++) {
+        {
+          const uint32_t x0 = colw[s], c = colw[s + 3], x8 = colw[s + 6];
+          const uint32_t x4 = colw[s + 3 + 3 * kPairWords], x12 = colw[s + 3 - 3 * kPairWords];
+          typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+          typedef short i16x2 __attribute__((ext_vector_type(2)));
+          auto U = [](uint32_t v) { return __builtin_bit_cast(u16x2, v); };
+          const u16x2 br = __builtin_elementwise_min(__builtin_elementwise_max(U(x0), U(x8)),
+                                                     __builtin_elementwise_max(U(x4), U(x12)));
+          const u16x2 dk = __builtin_elementwise_max(__builtin_elementwise_min(U(x0), U(x8)),
+                                                     __builtin_elementwise_min(U(x4), U(x12)));
+          // saturating differences (v_pk_sub_u16 clamp): brighter / darker margins, then their
+          // maximum against t: negative halves of t - m are the candidates
+          const u16x2 ub = __builtin_elementwise_sub_sat(br, U(c));
+          const u16x2 ud = __builtin_elementwise_sub_sat(U(c), dk);
+          const u16x2 m = __builtin_elementwise_max(ub, ud);
+          const uint32_t sg = __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2, U(T)) -
+                                                               __builtin_bit_cast(i16x2, m));
+          if (s < 16) acc = (acc >> 1) | (sg & 0x80008000u);
+          else acc2 = ((sg >> 15) & 1u) | ((sg >> 30) & 2u);
+        }
+      }
+      // step s: bit s (row s), bit 16 + s (row s + 17)
+      {
+        const int nlo = min(16, dr), nhi = min(16, max(0, dr - kPairD));
+        acc &= col_ok ? ((1u << nlo) - 1u) | (((1u << nhi) - 1u) << 16) : 0u;
+        acc2 &= col_ok ? (dr > 16 ? 1u : 0u) | (dr > 16 + kPairD ? 2u : 0u) : 0u;
+      }
       int nq = 0;
       bool dense = false;
-      for (int rc = 0; rc < dr; rc += 32) {
-        const int nst = min(16, (dr - rc + 1) >> 1);  // wave-uniform
-        const int nodd = min(16, (dr - rc) >> 1);     // steps whose second row is a detection row
-        uint32_t acc = cardinal_chunk16<kPairRS>(Sx + rc * kPairRS + lane, nst, t);
-        acc &= col_ok ? (((1u << nst) - 1u) | (((1u << nodd) - 1u) << 16)) : 0u;
-        const int cnt = __popc(acc);
+      {
+        const int cnt = __popc(acc) + __popc(acc2);
         const int incl = wave_scan_incl(cnt);
         const int tot = __builtin_amdgcn_readlane(incl, 63);
-        if (nq + tot > kPairQ) {  // wave-uniform, rare: score this chunk's pixels in place
+        if (tot > kPairQ) {  // wave-uniform, rare: score every flagged pixel in place
           dense = true;
           while (acc) {
             const int b = __builtin_ctz(acc);
             acc &= acc - 1;
-            score_at(rc + 2 * (b & 15) + (b >> 4), lane);
+            score_at(b < 16 ? b : b + 1, lane);
           }
-          continue;
-        }
-        int pos = nq + incl - cnt;
-        nq += tot;
-        while (acc) {
-          const int b = __builtin_ctz(acc);
-          acc &= acc - 1;
-          q[pos++] = (uint16_t)(((rc + 2 * (b & 15) + (b >> 4)) << 6) | lane);
+          if (acc2 & 1u) score_at(16, lane);
+          if (acc2 & 2u) score_at(16 + kPairD, lane);
+        } else {
+          nq = tot;
+          uint16_t* qp = q + (incl - cnt);
+          // bit b < 16: row b; b >= 16: row b + 1 (= (b - 16) + kPairD)
+          const uint32_t e0 = (uint32_t)lane;
+          while (acc) {
+            const uint32_t b = (uint32_t)__builtin_ctz(acc);
+            acc &= acc - 1;
+            *qp++ = (uint16_t)(((b + (b >> 4)) << 6) | e0);
+          }
+          if (acc2 & 1u) *qp++ = (uint16_t)((16 << 6) | e0);
+          if (acc2 & 2u) *qp++ = (uint16_t)(((16 + kPairD) << 6) | e0);
         }
       }
       wave_sync();
@@ -1054,8 +1141,11 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
       allow = (hasA ? 0 : mA) | (hasB ? 0 : mB);
       t = min_th;
     }
-    // (4) each cell's survivors to its slot in raster order: one packed scan of the two counts
-    const int nA = __popcll(bits & mA), nB = __popcll(bits & mB);
+    // (4) each cell's survivors to its slot in raster order: one packed scan of the two counts,
+    // then each lane (detection row) writes its row's keys, cell A's and cell B's in two loops
+    // (uniform slot pointers, no per-key select)
+    uint64_t bA = bits & mA, bB = bits >> cwA;
+    const int nA = __popcll(bA), nB = __popcll(bB);
     const int packed = nA | (nB << 16);
     const int incl = wave_scan_incl(packed);
     const int tot = __builtin_amdgcn_readlane(incl, 63);
@@ -1063,18 +1153,19 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
       cell_counts[(int64_t)img * ncells + pc.x] = tot & 0xFFFF;
       cell_counts[(int64_t)img * ncells + pc.y] = tot >> 16;
     }
-    int posA = (incl - packed) & 0xFFFF, posB = (incl - packed) >> 16;
-    K* outA = cand + (int64_t)img * cand_total + Ac.slot_off;
-    K* outB = cand + (int64_t)img * cand_total + Bc.slot_off;
+    K* outA = cand + (int64_t)img * cand_total + Ac.slot_off + ((incl - packed) & 0xFFFF);
+    K* outB = cand + (int64_t)img * cand_total + Bc.slot_off + ((incl - packed) >> 16);
     const int y = Ac.y0 + 3 + lane, x0 = Ac.x0 + 3;
-    const uint8_t* Vr = V + __mul24(lane + 1, kPairVS) + 1;
-    while (bits) {
-      const int c = __builtin_ctzll(bits);
-      bits &= bits - 1;
-      const bool inA = c < cwA;
-      const K key = KeyFmt<K>::make(x0 + c, y, (int)Vr[c + (inA ? 0 : 1)]);
-      if (inA) outA[posA++] = key;
-      else outB[posB++] = key;
+    const uint8_t* Vr = V + lane + 1;  // detection row `lane` of V column 0
+    while (bA) {
+      const int c = __builtin_ctzll(bA);
+      bA &= bA - 1;
+      *outA++ = KeyFmt<K>::make(x0 + c, y, (int)Vr[__mul24(c + 1, kPairVS)]);
+    }
+    while (bB) {
+      const int c = __builtin_ctzll(bB);
+      bB &= bB - 1;
+      *outB++ = KeyFmt<K>::make(x0 + cwA + c, y, (int)Vr[__mul24(cwA + c + 2, kPairVS)]);
     }
   }
 }
@@ -1093,6 +1184,7 @@ constexpr int kOctBigArea = 1 << 20;  // kOctBigArea px: a workgroup holds ~100 
                                       // (one per CU), so 1024 threads run its key passes 4x wide
 constexpr int kOctRegKeys = 16;       // keys per thread per register chunk
 constexpr int kOctBatch = 8;          // node-info loads in flight per key pass round
+constexpr int kOctBatchRl = 4;        // the relabel + count sweep's (more registers per key)
 constexpr size_t kOctMaxSmem = 150 * 1024;  // dynamic LDS of one octree workgroup
 
 struct OctNodes {
@@ -1118,7 +1210,9 @@ __device__ __forceinline__ int quad_of(K key, uint32_t info) {
 struct OctCtx {
   OctNodes A, B;
   int *cc, *t1, *t2, *t3, *t4, *s_tmp, *s_misc;
-  uint32_t* ninfo;  // node_info() of the current nodes
+  int* cc2;          // the next pass's quadrant counts (counted during this pass's relabel)
+  uint32_t* ninfo;   // node_info() of the current nodes
+  uint32_t* ninfo2;  // node_info() of the next pass's nodes (written with them)
   uint64_t *pk, *s_tmp64;
   void* outk;  // K[] of the level's retained keys
   int* oc;
@@ -1201,11 +1295,12 @@ __device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, 
 
 // What a key of node i becomes after a pass: its new label is base - pre[q], pre[q] = the node's
 // non-empty quadrants before the key's quadrant q (children are pushed in quadrant order); bits
-// 2q..2q+1 hold pre[q] (pre[0] = 0), zero for a node that is not divided, and bits 8- the base
+// 2q..2q+1 hold pre[q] (pre[0] = 0), zero for a node that is not divided, bit 8 is set for a
+// divided node and bits 9- hold the base
 __device__ __forceinline__ int relabel_info(int base, int divided, const int* ccn) {
-  if (!divided) return base << 8;
+  if (!divided) return base << 9;
   const int p1 = ccn[0] > 0, p2 = p1 + (ccn[1] > 0), p3 = p2 + (ccn[2] > 0);
-  return (base << 8) | (p1 << 2) | (p2 << 4) | (p3 << 6);
+  return (base << 9) | 0x100 | (p1 << 2) | (p2 << 4) | (p3 << 6);
 }
 
 template <int NT, class KS>
@@ -1255,54 +1350,58 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   int seqc = nini;
   bool final_mode = false;
   const int N = G.nfeat;
-  for (int iter = 0; iter < 4096; iter++) {
-    const int prevSize = size;
-    for (int i = tid; i < 4 * size; i += NT) cc[i] = 0;
-    for (int i = tid; i < size; i += NT)
-      X.ninfo[i] = node_info(cur.cnt[i], cur.x0[i], cur.x1[i], cur.y0[i], cur.y1[i]);
-    __syncthreads();
-    // quadrant counts; keys are in cell order, so a wave's keys usually share one node and the
-    // four counts are added with one atomic each instead of one per key
-    const int lane = tid & 63;
-    auto count_one = [&](int j, int k, uint32_t info) {
-      int nd = -1, q = -1;
-      if (k < n) {
-        nd = ks.get_lab(j);
-        if (info >> 31) {
-          q = quad_of(ks.get_key(j), info);
-          ks.set_q(j, q);
-        }
+  // quadrant count of key slot j (label nd, node info `info`) into counts[4 nd + q]; keys are in
+  // cell order, so a wave's keys usually share one node and the four counts are added with one
+  // atomic each instead of one per key.  Every lane of the wave calls it (ballots).
+  const int lane = tid & 63;
+  auto count_one = [&](int* counts, int j, bool valid, int nd, uint32_t info) {
+    int q = -1;
+    if (valid && (info >> 31)) {
+      q = quad_of(ks.get_key(j), info);
+      ks.set_q(j, q);
+    }
+    const uint64_t act = __ballot(q >= 0);
+    if (!act) return;
+    const int first = __builtin_ctzll(act);
+    const int ndf = __shfl(nd, first);
+    if (__ballot(q >= 0 && nd != ndf) == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        const int c = __popcll(__ballot(q == jj));
+        if (lane == first && c) atomicAdd(&counts[4 * ndf + jj], c);
       }
-      const uint64_t act = __ballot(q >= 0);
-      if (!act) return;
-      const int first = __builtin_ctzll(act);
-      const int ndf = __shfl(nd, first);
-      if (__ballot(q >= 0 && nd != ndf) == 0) {
+    } else if (q >= 0) {
+      atomicAdd(&counts[4 * nd + q], 1);
+    }
+  };
+  // the first pass's quadrant counts: one sweep over the keys; later passes count during the
+  // previous pass's relabel (below), so each pass sweeps the keys once
+  for (int i = tid; i < 4 * size; i += NT) cc[i] = 0;
+  for (int i = tid; i < size; i += NT)
+    X.ninfo[i] = node_info(cur.cnt[i], cur.x0[i], cur.x1[i], cur.y0[i], cur.y1[i]);
+  __syncthreads();
+  // every lane runs every slot (the ballots need the whole wave); a chunk's node infos are
+  // loaded together before its first atomic, one LDS latency per chunk instead of per key
+  for (int c = 0; c < ks.nchunks(); c++) {
+    ks.load(c, true);
 #pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-          const int c = __popcll(__ballot(q == jj));
-          if (lane == first && c) atomicAdd(&cc[4 * ndf + jj], c);
-        }
-      } else if (q >= 0) {
-        atomicAdd(&cc[4 * nd + q], 1);
-      }
-    };
-    // every lane runs every slot (the ballots need the whole wave); a chunk's node infos are
-    // loaded together before its first atomic, one LDS latency per chunk instead of per key
-    for (int c = 0; c < ks.nchunks(); c++) {
-      ks.load(c, true);
+    for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
+      uint32_t inf[kOctBatch];
 #pragma unroll
-      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
-        uint32_t inf[kOctBatch];
+      for (int j = 0; j < kOctBatch; j++)
+        inf[j] = tid + NT * (c * kOctRegKeys + j0 + j) < n ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
 #pragma unroll
-        for (int j = 0; j < kOctBatch; j++)
-          inf[j] = tid + NT * (c * kOctRegKeys + j0 + j) < n ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
-#pragma unroll
-        for (int j = 0; j < kOctBatch; j++)
-          count_one(j0 + j, tid + NT * (c * kOctRegKeys + j0 + j), inf[j]);
+      for (int j = 0; j < kOctBatch; j++) {
+        const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
+        count_one(cc, j0 + j, v, v ? ks.get_lab(j0 + j) : -1, inf[j]);
       }
     }
-    __syncthreads();
+  }
+  __syncthreads();
+  int* ccn = X.cc2;
+  uint32_t *ninfo = X.ninfo, *ninfo_n = X.ninfo2;
+  for (int iter = 0; iter < 4096; iter++) {
+    const int prevSize = size;
     int T, newSize, nToExpand;
     if (!final_mode) {
       // outer pass (list order): one packed scan gives childPre (bits 0-19), the rank among
@@ -1423,7 +1522,9 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       }
       __syncthreads();
     }
-    // write next node arrays: t2 = divided, t1 = childPre, t4 = base, t3 = relabel_info
+    // write next node arrays: t2 = divided, t1 = childPre, t4 = base, t3 = relabel_info; with
+    // them the next pass's node infos and counts: a child's counts start at zero (its keys are
+    // counted by the relabel sweep below), an undivided node keeps this pass's counts
     for (int i = tid; i < size; i += NT) {
       if (t2[i]) {
         const int x0 = cur.x0[i], x1 = cur.x1[i], y0 = cur.y0[i], y1 = cur.y1[i];
@@ -1434,12 +1535,16 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
           const int c = cc[4 * i + q];
           if (c > 0) {
             const int pos = t4[i] - j;
-            nxt.x0[pos] = (int16_t)((q & 1) ? xm : x0);
-            nxt.x1[pos] = (int16_t)((q & 1) ? x1 : xm);
-            nxt.y0[pos] = (int16_t)((q & 2) ? ym : y0);
-            nxt.y1[pos] = (int16_t)((q & 2) ? y1 : ym);
+            const int cx0 = (q & 1) ? xm : x0, cx1 = (q & 1) ? x1 : xm;
+            const int cy0 = (q & 2) ? ym : y0, cy1 = (q & 2) ? y1 : ym;
+            nxt.x0[pos] = (int16_t)cx0;
+            nxt.x1[pos] = (int16_t)cx1;
+            nxt.y0[pos] = (int16_t)cy0;
+            nxt.y1[pos] = (int16_t)cy1;
             nxt.cnt[pos] = c;
             nxt.seq[pos] = seqc + t1[i] + j;
+            ninfo_n[pos] = node_info(c, cx0, cx1, cy0, cy1);
+            *(int4*)&ccn[4 * pos] = make_int4(0, 0, 0, 0);
             j++;
           }
         }
@@ -1448,26 +1553,40 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         nxt.x0[pos] = cur.x0[i]; nxt.x1[pos] = cur.x1[i];
         nxt.y0[pos] = cur.y0[i]; nxt.y1[pos] = cur.y1[i];
         nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
+        ninfo_n[pos] = ninfo[i];
+        *(int4*)&ccn[4 * pos] = *(const int4*)&cc[4 * i];  // zero unless counted (cnt > 1)
       }
     }
-    // relabel keys: a chunk's relabel infos (and, for keys in memory, node infos) in one round
+    __syncthreads();
+    // relabel keys and count the divided nodes' keys into their children's quadrants for the
+    // next pass (a key's child and that child's split point are now known): a chunk's relabel
+    // infos (and, for keys in memory, node infos), then the children's infos, each in one round
     // of loads
     for (int c = 0; c < ks.nchunks(); c++) {
       ks.load(c, true);
 #pragma unroll
-      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
-        uint32_t rl[kOctBatch], inf[kOctBatch];
+      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatchRl) {
+        uint32_t rl[kOctBatchRl], inf[kOctBatchRl];
 #pragma unroll
-        for (int j = 0; j < kOctBatch; j++) {
+        for (int j = 0; j < kOctBatchRl; j++) {
           const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
           rl[j] = v ? (uint32_t)t3[ks.get_lab(j0 + j)] : 0u;
-          inf[j] = (!KS::kRegs && v) ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
+          inf[j] = (!KS::kRegs && v) ? ninfo[ks.get_lab(j0 + j)] : 0u;
+        }
+        int nl[kOctBatchRl];
+#pragma unroll
+        for (int j = 0; j < kOctBatchRl; j++) {
+          const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
+          // rl bits 2..7 are zero for an undivided node: its keys keep their node (base)
+          nl[j] = (int)(rl[j] >> 9) - (int)((rl[j] >> (2 * ks.get_q(j0 + j, inf[j]))) & 3u);
+          if (v) ks.set_lab(j0 + j, nl[j]);
+          inf[j] = v && (rl[j] & 0x100u) ? ninfo_n[nl[j]] : 0u;  // a divided node's child
         }
 #pragma unroll
-        for (int j = 0; j < kOctBatch; j++)
-          if (tid + NT * (c * kOctRegKeys + j0 + j) < n)
-            ks.set_lab(j0 + j, (int)(rl[j] >> 8) -
-                                   (int)((rl[j] >> (2 * ks.get_q(j0 + j, inf[j]))) & 3u));
+        for (int j = 0; j < kOctBatchRl; j++) {
+          const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
+          count_one(ccn, j0 + j, v, nl[j], inf[j]);
+        }
       }
       ks.store_labs(c);
     }
@@ -1476,6 +1595,12 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       OctNodes tmp = cur;
       cur = nxt;
       nxt = tmp;
+      int* tc = cc;
+      cc = ccn;
+      ccn = tc;
+      uint32_t* ti = ninfo;
+      ninfo = ninfo_n;
+      ninfo_n = ti;
     }
     size = newSize;
     seqc += T;
@@ -1550,6 +1675,8 @@ void k_octree(
   int* t3 = (int*)take(4 * NC);
   int* t4 = (int*)take(4 * NC);
   uint32_t* ninfo = (uint32_t*)take(4 * NC);
+  int* cc2 = (int*)take(16 * NC);
+  uint32_t* ninfo2 = (uint32_t*)take(4 * NC);
   // per-cell key starts and slots: in LDS, or (cell_cap == 0: levels with too many cells for
   // it) in this (image, level)'s part of cell_scr, [2 (ncells + nlevels)] ints per image
   int* cpre = cell_cap > 0 ? (int*)take(4 * (cell_cap + 1))
@@ -1599,7 +1726,7 @@ void k_octree(
       v[j] = k < n ? cb[s_slot[c] + k - cpre[c]] : K(0);
     }
   };
-  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, ninfo, pk, s_tmp64, outk, oc};
+  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, cc2, ninfo, ninfo2, pk, s_tmp64, outk, oc};
   if (n <= kOctRegKeys * NT) {  // keys + labels in registers: every pass stays on-chip
     RegKeys<NT, K> ks;
     ks.n = n;
@@ -2162,7 +2289,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   auto oct_bytes = [&](size_t NC, size_t CC) {
-    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 5 * r16(4 * NC) +
+    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + 2 * r16(16 * NC) + 6 * r16(4 * NC) +
            (CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0) + r16(8 * NC);
   };
   while (P->oct_split < g.nlevels && (int64_t)g.lv[P->oct_split].W * g.lv[P->oct_split].H > kOctBigArea)

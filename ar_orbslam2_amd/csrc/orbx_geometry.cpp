@@ -157,99 +157,143 @@ static bool resize_tables(int sw, int sh, int dw, int dh, Geometry* g, LevelGeom
   return ok;
 }
 
-// k_pyramid's stages and row bands (the comment in build_pyramid); false when a one-row band
-// does not fit kPyMaxSmemLimit bytes of LDS
-static bool build_stages(Geometry* g, bool fused) {
+// Stage `st` as nb row bands x ncol column tiles (PyrBand).  Every level's rows split into nb
+// bands and its 4-column groups into ncol tiles on 16-column boundaries; a tile computes, going
+// down from the stage's last level, the rows and groups its levels' cones need (rows and groups
+// shared by two tiles are computed by both, identically; only the owner stores them), and with
+// the blur fused its blurred levels carry GaussianBlur's 3-row / one-group halo (clipped rows:
+// the reflected rows lie inside; the groups -1 and gl + 1 hold the reflected pad columns).
+// Returns the LDS bytes of the stage (st.smem, st.buf_b set) and the pixels the resize passes
+// compute and own (levels l0 .. l1).
+static int stage_tiles(const Geometry& g, PyrStage& st, int nb, int ncol, bool fused,
+                       std::vector<PyrBand>& tiles, double& comp, double& own) {
+  tiles.assign((size_t)nb * ncol, PyrBand{});
+  int need[2] = {0, 0};
+  comp = own = 0;
+  constexpr int kEmpty = 1 << 30;
+  for (int b = 0; b < nb; b++)
+    for (int t = 0; t < ncol; t++) {
+      PyrBand& B = tiles[(size_t)b * ncol + t];
+      for (int l = st.l0 - 1; l <= st.l1; l++) {
+        const LevelGeom& L = g.lv[l];
+        const int h = L.h, ng = ((L.w - 1) >> 2) + 1, n16 = (ng + 3) / 4;
+        B.own_lo[l] = (int)((int64_t)b * h / nb);
+        B.own_hi[l] = (int)((int64_t)(b + 1) * h / nb);
+        B.own_glo[l] = std::min(ng, 4 * (int)((int64_t)t * n16 / ncol));
+        B.own_ghi[l] = std::min(ng, 4 * (int)((int64_t)(t + 1) * n16 / ncol));
+        const bool owns = B.own_hi[l] > B.own_lo[l] && B.own_ghi[l] > B.own_glo[l];
+        const bool blurred = fused && (l >= st.l0 || st.l0 == 1);
+        // the source level is computed only for the cone of the level above it
+        if (!owns || (l == st.l0 - 1 && st.l0 > 1)) {
+          B.lo[l] = B.glo[l] = kEmpty;
+          B.hi[l] = B.ghi[l] = -kEmpty;
+        } else if (blurred) {
+          B.lo[l] = std::max(0, B.own_lo[l] - 3);
+          B.hi[l] = std::min(h, B.own_hi[l] + 3);
+          B.glo[l] = B.own_glo[l] - 1;
+          B.ghi[l] = B.own_ghi[l] + 1;
+        } else {
+          B.lo[l] = B.own_lo[l];
+          B.hi[l] = B.own_hi[l];
+          B.glo[l] = B.own_glo[l];
+          B.ghi[l] = B.own_ghi[l];
+        }
+      }
+      for (int l = st.l1; l >= st.l0; l--) {  // the source rows and columns of level l's ranges
+        const LevelGeom& D = g.lv[l];
+        const LevelGeom& S = g.lv[l - 1];
+        if (B.hi[l] <= B.lo[l] || B.ghi[l] <= B.glo[l]) continue;
+        const int slo = std::min(std::max(g.yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
+        const int shi = std::min(std::max(g.yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
+        int xmin = kEmpty, xmax = -1;
+        for (int dx = 4 * B.glo[l]; dx < 4 * B.ghi[l]; dx++) {
+          const int xs = g.xtap[2 * (D.coef_x + dx)] & 0xFFFFF;
+          xmin = std::min(xmin, xs);
+          xmax = std::max(xmax, xs + 1);  // py_horiz reads S0 and S1
+        }
+        B.lo[l - 1] = std::min(B.lo[l - 1], slo);
+        B.hi[l - 1] = std::max(B.hi[l - 1], shi);
+        B.glo[l - 1] = std::min(B.glo[l - 1], xmin >> 2);
+        B.ghi[l - 1] = std::max(B.ghi[l - 1], (xmax >> 2) + 1);
+      }
+      for (int l = st.l0 - 1; l <= st.l1; l++) {
+        if (B.hi[l] <= B.lo[l] || B.ghi[l] <= B.glo[l]) {
+          B.lo[l] = B.hi[l] = B.own_lo[l];
+          B.glo[l] = B.ghi[l] = std::max(0, B.own_glo[l]);
+          B.cb[l] = 0;
+          B.lp[l] = 16;
+          continue;
+        }
+        // LDS row: columns cb .. cb + lp - 1, cb = 4 glo rounded down to 16 bytes
+        B.cb[l] = (4 * B.glo[l]) & ~15;
+        B.lp[l] = (4 * B.ghi[l] - B.cb[l] + 15) & ~15;
+        need[l & 1] = std::max(need[l & 1], (B.hi[l] - B.lo[l]) * B.lp[l]);
+        if (l >= st.l0) {
+          comp += (double)(B.hi[l] - B.lo[l]) * 4 * (B.ghi[l] - B.glo[l]);
+          own += (double)(B.own_hi[l] - B.own_lo[l]) * 4 * (B.own_ghi[l] - B.own_glo[l]);
+        }
+      }
+    }
+  st.buf_b = (need[0] + 15) & ~15;
+  st.smem = std::max(16, st.buf_b + need[1]);
+  return st.smem;
+}
+
+// k_pyramid's stages and tiles (the comment in build_pyramid); false when no tiling of a stage
+// fits kPyMaxSmemLimit bytes of LDS.  Per stage, for every column split 1 .. kPyMaxCols, the
+// tallest bands (down to py_band_h / kPyBandHMin source rows) whose two LDS buffers fit the
+// bound, then the split whose tiles compute the fewest pixels.
+static bool build_stages(Geometry* g, bool fused, double* recompute) {
   const int nl = g->nlevels;
   g->pyr_stages.clear();
   g->bands.clear();
-  const int py_max_smem = fused ? kPyMaxSmemFused : kPyMaxSmem;  // a band's two level buffers
+  const int py_max_smem = fused ? kPyMaxSmemFused : kPyMaxSmem;  // a tile's two level buffers
   const int stage0 = fused ? kPyStage0Fused : kPyStage0, stage_n = fused ? kPyStageNFused : kPyStageN;
-  for (int l0 = 1; l0 < nl;) {
-    PyrStage st;
+  double comp_all = 0, own_all = 0;
+  for (int l0 = 1; l0 <= std::max(nl - 1, 1); ) {
+    PyrStage st{};
     st.l0 = l0;
-    st.l1 = std::min(nl - 1, l0 + (l0 == 1 ? stage0 : stage_n) - 1);
+    st.l1 = nl == 1 ? 0 : std::min(nl - 1, l0 + (l0 == 1 ? stage0 : stage_n) - 1);
     const int hs = g->lv[l0 - 1].h;
-    std::vector<PyrBand> bands;
-    int smem_cap = py_max_smem;  // raised to kPyMaxSmemLimit for rows too wide for it
-    for (int nb = std::max(1, hs / g->py_band_h);; nb++) {
-      bands.assign(nb, PyrBand{});
-      int need[2] = {0, 0};
-      for (int b = 0; b < nb; b++) {
-        PyrBand& B = bands[b];
-        for (int l = st.l0 - 1; l <= st.l1; l++) {
-          const int h = g->lv[l].h;
-          B.own_lo[l] = B.lo[l] = (int)((int64_t)b * h / nb);
-          B.own_hi[l] = B.hi[l] = (int)((int64_t)(b + 1) * h / nb);
-          if (fused && (l >= st.l0 || st.l0 == 1) && B.own_hi[l] > B.own_lo[l]) {
-            B.lo[l] = std::max(0, B.own_lo[l] - 3);
-            B.hi[l] = std::min(h, B.own_hi[l] + 3);
+    std::vector<PyrBand> best, tiles;
+    PyrStage best_st{};
+    double best_comp = 0, best_own = 0;
+    bool found = false;
+    for (int cap : {py_max_smem, kPyMaxSmemLimit}) {
+      // the few-image plans keep their short bands (more workgroups for one image's chain)
+      const int ncmax = g->py_band_h < kPyBandH ? 1 : kPyMaxCols;
+      for (int ncol = 1; ncol <= ncmax; ncol++) {
+        const int band_h = g->py_band_h < kPyBandH ? g->py_band_h : g->py_band_h * kPyBandHMul;
+        const int nb_lo = std::max(1, hs / std::max(1, band_h));
+        const int nb_hi = std::max(nb_lo, hs);
+        for (int nb = nb_lo; nb <= nb_hi; nb++) {
+          PyrStage s2 = st;
+          double comp, own;
+          if (stage_tiles(*g, s2, nb, ncol, fused, tiles, comp, own) > cap) continue;
+          if (!found || comp < best_comp) {
+            found = true;
+            best.swap(tiles);
+            best_st = s2;
+            best_comp = comp;
+            best_own = own;
           }
+          break;  // taller bands than the first that fits do not fit
         }
-        for (int l = st.l1; l >= st.l0; l--) {
-          const LevelGeom& D = g->lv[l];
-          const LevelGeom& S = g->lv[l - 1];
-          if (B.hi[l] <= B.lo[l]) continue;
-          const int slo = std::min(std::max(g->yofs[D.coef_y + B.lo[l]], 0), S.h - 1);
-          const int shi = std::min(std::max(g->yofs[D.coef_y + B.hi[l] - 1] + 1, 0), S.h - 1) + 1;
-          B.lo[l - 1] = std::min(B.lo[l - 1], slo);
-          B.hi[l - 1] = std::max(B.hi[l - 1], shi);
-        }
-        for (int l = st.l0 - 1; l <= st.l1; l++)
-          need[l & 1] = std::max(need[l & 1], std::max(0, B.hi[l] - B.lo[l]) * py_lds_pitch(g->lv[l], fused));
       }
-      st.buf_b = (need[0] + 15) & ~15;
-      st.smem = st.buf_b + need[1];
-      if (st.smem <= smem_cap) break;
-      if (nb >= hs) {
-        if (smem_cap < kPyMaxSmemLimit) {  // one-row bands still too large: the larger carve
-          smem_cap = kPyMaxSmemLimit;
-          nb = std::max(1, hs / g->py_band_h) - 1;
-          continue;
-        }
-        return false;
-      }
+      if (found) break;  // the larger carve only when nothing fits the bound
     }
-    st.band0 = (int)g->bands.size();
-    st.nbands = (int)bands.size();
-    g->bands.insert(g->bands.end(), bands.begin(), bands.end());
-    g->pyr_stages.push_back(st);
+    if (!found) return false;
+    best_st.band0 = (int)g->bands.size();
+    best_st.nbands = (int)best.size();
+    g->bands.insert(g->bands.end(), best.begin(), best.end());
+    g->pyr_stages.push_back(best_st);
+    comp_all += best_comp;
+    own_all += best_own;
     l0 = st.l1 + 1;
+    if (nl == 1) break;
   }
-  if (nl == 1) {  // level 0 alone: one copy stage (and its blur)
-    PyrStage st{1, 0, 0, 0, 0, 0};
-    const int h = g->lv[0].h, nb = std::max(1, h / g->py_band_h);
-    int rows = 0;
-    for (int b = 0; b < nb; b++) {
-      PyrBand B{};
-      B.own_lo[0] = B.lo[0] = (int)((int64_t)b * h / nb);
-      B.own_hi[0] = B.hi[0] = (int)((int64_t)(b + 1) * h / nb);
-      if (fused) {
-        B.lo[0] = std::max(0, B.own_lo[0] - 3);
-        B.hi[0] = std::min(h, B.own_hi[0] + 3);
-      }
-      rows = std::max(rows, B.hi[0] - B.lo[0]);
-      g->bands.push_back(B);
-    }
-    st.nbands = nb;
-    st.smem = std::max(16, rows * py_lds_pitch(g->lv[0], fused));
-    if (st.smem > kPyMaxSmemLimit) return false;
-    g->pyr_stages.push_back(st);
-  }
+  if (recompute) *recompute = own_all > 0 ? comp_all / own_all : 1.0;
   return true;
-}
-
-// Pixels the bands' resize passes compute (owned rows, halo rows and the cone rows the next
-// level needs) over the pixels of the levels they build.
-static double band_recompute(const Geometry& g) {
-  double comp = 0, own = 0;
-  for (const PyrStage& st : g.pyr_stages)
-    for (int b = st.band0; b < st.band0 + st.nbands; b++)
-      for (int l = st.l0; l <= st.l1; l++) {
-        comp += (double)std::max(0, g.bands[b].hi[l] - g.bands[b].lo[l]) * g.lv[l].w;
-        own += (double)(g.bands[b].own_hi[l] - g.bands[b].own_lo[l]) * g.lv[l].w;
-      }
-  return own > 0 ? comp / own : 1.0;
 }
 
 // The pyramid part of a plan for the level sizes already in g->lv[0 .. g->nlevels): cv::resize
@@ -299,8 +343,9 @@ int build_pyramid(Geometry* g, std::string* why) {
   // GaussianBlur's 3-row halo, clipped to the level (the reflected rows lie inside the range).
   // The blur is fused where the bands fit (every configuration the benchmarks run); frames too
   // wide for its halo rows keep the separate k_blur launch.
-  g->blur_fused = kPyFused && build_stages(g, true) && band_recompute(*g) <= kPyFuseMaxRecompute;
-  if (!g->blur_fused && !build_stages(g, false)) {
+  double rc = 0;
+  g->blur_fused = kPyFused && build_stages(g, true, &rc) && rc <= kPyFuseMaxRecompute;
+  if (!g->blur_fused && !build_stages(g, false, nullptr)) {
     if (why) *why = "image too wide for the pyramid bands";
     return ORBX_EUNSUPPORTED;
   }

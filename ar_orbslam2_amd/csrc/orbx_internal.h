@@ -52,9 +52,21 @@ constexpr int kPyStrip = 4;    // k_pyramid output rows per work item (2: 170, 8
 constexpr bool kPyFused = true;
 constexpr double kPyFuseMaxRecompute = 1.4;
 constexpr int kPyBlurStrip = 4;  // fused blur: output rows per lane
+// column tiles: up to kPyMaxCols per row band, and batch plans' bands up to kPyBandHMul x
+// kPyBandH source rows (the tallest that fit the LDS bound)
+constexpr int kPyMaxCols = 8;
+constexpr int kPyBandHMul = 4;
+// A band is a tile: a range of rows and of 4-column groups of every level of its stage.  Wide
+// frames split their rows into several column tiles, so a tile's rows can be many without its
+// LDS outgrowing the bound, and the rows and columns the tile recomputes for the next level's
+// cone (and the blur's halo) stay a small share of what it owns.
 struct PyrBand {
   int lo[kMaxLevels], hi[kMaxLevels];      // rows of each level this band computes (with halo)
   int own_lo[kMaxLevels], own_hi[kMaxLevels];  // rows it writes to the pyramid (a partition)
+  int glo[kMaxLevels], ghi[kMaxLevels];    // column groups it computes (-1 / gl + 1: blur pads)
+  int own_glo[kMaxLevels], own_ghi[kMaxLevels];  // groups it writes (a partition of 0 .. gl)
+  int cb[kMaxLevels];                      // LDS row byte 0 = column cb (a multiple of 16)
+  int lp[kMaxLevels];                      // LDS row pitch (a multiple of 16)
 };
 struct PyrStage {
   int l0, l1;          // builds levels l0..l1 from level l0 - 1 (the input when l0 == 1)
@@ -83,11 +95,6 @@ struct LevelGeom {
   float size;              // (float)(int)(PATCH_SIZE * scale)
   float inv_scale;         // mvInvScaleFactor
 };
-// a level row's stride in k_pyramid's LDS: with the blur fused, 16 bytes of pad on both sides
-// (column 0 at byte 16: the reflected columns -4..-1 at 12..15, those past w after it)
-__host__ __device__ inline int py_lds_pitch(const LevelGeom& L, bool fused) {
-  return fused ? L.pitch + 32 : L.pitch;
-}
 
 struct CellGeom {
   int16_t x0, y0, x1, y1;  // cell image ROI in level coordinates [x0,x1) x [y0,y1)

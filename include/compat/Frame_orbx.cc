@@ -37,19 +37,29 @@ bool orbx_compute_bow(const cv::Mat& descriptors, DBoW2::BowVector& bow, DBoW2::
   if (!voc) return false;
   const int n = descriptors.rows;
   const size_t m = (size_t)std::max(n, 1);
-  std::vector<uint32_t> bw(m), fi(m + 1);
-  std::vector<double> bv(m);
-  std::vector<int32_t> fo(m + 2), ff(m);
+  // the transform's raw outputs, per thread and reused (Tracking and LocalMapping run ComputeBoW)
+  struct Scratch {
+    std::vector<uint32_t> bw, fi;
+    std::vector<double> bv;
+    std::vector<int32_t> fo, ff;
+  };
+  static thread_local Scratch S;
+  S.bw.resize(m);
+  S.fi.resize(m + 1);
+  S.bv.resize(m);
+  S.fo.resize(m + 2);
+  S.ff.resize(m);
   int32_t nb = 0, nf = 0;
-  if (orbx_vocabulary_transform(voc.get(), descriptors.data, n, 4, nullptr, nullptr, bw.data(), bv.data(),
-                                &nb, fi.data(), fo.data(), ff.data(), &nf) != ORBX_OK)
+  if (orbx_vocabulary_transform(voc.get(), descriptors.data, n, 4, nullptr, nullptr, S.bw.data(),
+                                S.bv.data(), &nb, S.fi.data(), S.fo.data(), S.ff.data(), &nf) != ORBX_OK)
     return false;
   bow.clear();
   fv.clear();
-  for (int i = 0; i < nb; i++) bow.insert(bow.end(), std::make_pair(bw[i], bv[i]));  // ascending
+  // ascending ids: every entry placed at the end by hint, no tree search
+  for (int i = 0; i < nb; i++) bow.emplace_hint(bow.end(), S.bw[i], S.bv[i]);
   for (int j = 0; j < nf; j++)
-    fv.insert(fv.end(), std::make_pair(fi[j], std::vector<unsigned int>(ff.begin() + fo[j],
-                                                                        ff.begin() + fo[j + 1])));
+    fv.emplace_hint(fv.end(), S.fi[j],
+                    std::vector<unsigned int>(S.ff.begin() + S.fo[j], S.ff.begin() + S.fo[j + 1]));
   return true;
 }
 

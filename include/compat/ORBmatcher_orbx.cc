@@ -48,12 +48,16 @@ void log_fallback(const char* what, int rc) {
     fprintf(stderr, "[orbx] %s failed (%d): falling back to the host ORBmatcher\n", what, rc);
 }
 
-// DBoW2::FeatureVector (std::map, node ids ascending) as CSR
+// DBoW2::FeatureVector (std::map, node ids ascending) as CSR, refilled in place (the vectors
+// keep their capacity from call to call)
 struct FeatVecCSR {
   std::vector<uint32_t> ids;
   std::vector<int32_t> off, feats;
   orbx_featvec view;
-  explicit FeatVecCSR(const DBoW2::FeatureVector& fv) {
+  void assign(const DBoW2::FeatureVector& fv) {
+    ids.clear();
+    off.clear();
+    feats.clear();
     off.push_back(0);
     for (DBoW2::FeatureVector::const_iterator it = fv.begin(); it != fv.end(); ++it) {
       ids.push_back(it->first);
@@ -64,10 +68,22 @@ struct FeatVecCSR {
   }
 };
 
-std::vector<float> angles_of(const std::vector<cv::KeyPoint>& k) {
-  std::vector<float> a(k.size());
+// The per-call host buffers of SearchByBoW / SearchForTriangulation, kept per thread (Tracking,
+// LocalMapping and LoopClosing call at once) and reused: no allocation per call once warm.
+struct CallScratch {
+  FeatVecCSR f1, f2;
+  std::vector<uint8_t> m1, m2;
+  std::vector<float> a1, a2;
+  std::vector<int32_t> idx;
+};
+CallScratch& scratch() {
+  static thread_local CallScratch s;
+  return s;
+}
+
+void angles_of(const std::vector<cv::KeyPoint>& k, std::vector<float>& a) {
+  a.resize(k.size());
   for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
-  return a;
 }
 
 const orbx_keypoint* keys_of(const std::vector<cv::KeyPoint>& k) {
@@ -123,16 +139,20 @@ int ORBmatcher::DescriptorDistance(const cv::Mat& a, const cv::Mat& b) {
 
 // ------------------------------------------------------------------ SearchByBoW (:159-288)
 int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
+  CallScratch& S = scratch();
   const std::vector<MapPoint*> vpMP = pKF->GetMapPointMatches();
-  std::vector<uint8_t> valid(vpMP.size());
-  for (size_t i = 0; i < vpMP.size(); i++) valid[i] = vpMP[i] && !vpMP[i]->isBad();
-  const std::vector<float> akf = angles_of(pKF->mvKeysUn), af = angles_of(F.mvKeys);
-  FeatVecCSR fk(pKF->mFeatVec), ff(F.mFeatVec);
-  const orbx_bow_side kf{pKF->N, pKF->mDescriptors.data, akf.data(), valid.data(), fk.view};
-  const orbx_bow_side fr{F.N, F.mDescriptors.data, af.data(), nullptr, ff.view};
-  std::vector<int32_t> match(std::max(F.N, 1));
+  S.m1.resize(vpMP.size());
+  for (size_t i = 0; i < vpMP.size(); i++) S.m1[i] = vpMP[i] && !vpMP[i]->isBad();
+  angles_of(pKF->mvKeysUn, S.a1);
+  angles_of(F.mvKeys, S.a2);
+  S.f1.assign(pKF->mFeatVec);
+  S.f2.assign(F.mFeatVec);
+  const orbx_bow_side kf{pKF->N, pKF->mDescriptors.data, S.a1.data(), S.m1.data(), S.f1.view};
+  const orbx_bow_side fr{F.N, F.mDescriptors.data, S.a2.data(), nullptr, S.f2.view};
+  S.idx.resize(std::max(F.N, 1));
+  const std::vector<int32_t>& match = S.idx;
   int32_t n = 0;
-  const int rc = orbx_search_by_bow_kf_f(&kf, &fr, mfNNratio, mbCheckOrientation, match.data(), &n);
+  const int rc = orbx_search_by_bow_kf_f(&kf, &fr, mfNNratio, mbCheckOrientation, S.idx.data(), &n);
   if (rc != ORBX_OK) {
     log_fallback("orbx_search_by_bow_kf_f", rc);
     return ORBmatcherHost(mfNNratio, mbCheckOrientation).SearchByBoW(pKF, F, vpMapPointMatches);
@@ -145,17 +165,22 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpM
 
 // (:525-658)
 int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12) {
+  CallScratch& S = scratch();
   const std::vector<MapPoint*> vp1 = pKF1->GetMapPointMatches(), vp2 = pKF2->GetMapPointMatches();
-  std::vector<uint8_t> v1(vp1.size()), v2(vp2.size());
-  for (size_t i = 0; i < vp1.size(); i++) v1[i] = vp1[i] && !vp1[i]->isBad();
-  for (size_t i = 0; i < vp2.size(); i++) v2[i] = vp2[i] && !vp2[i]->isBad();
-  const std::vector<float> a1 = angles_of(pKF1->mvKeysUn), a2 = angles_of(pKF2->mvKeysUn);
-  FeatVecCSR f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
-  const orbx_bow_side s1{pKF1->N, pKF1->mDescriptors.data, a1.data(), v1.data(), f1.view};
-  const orbx_bow_side s2{pKF2->N, pKF2->mDescriptors.data, a2.data(), v2.data(), f2.view};
-  std::vector<int32_t> match(std::max(pKF1->N, 1));
+  S.m1.resize(vp1.size());
+  S.m2.resize(vp2.size());
+  for (size_t i = 0; i < vp1.size(); i++) S.m1[i] = vp1[i] && !vp1[i]->isBad();
+  for (size_t i = 0; i < vp2.size(); i++) S.m2[i] = vp2[i] && !vp2[i]->isBad();
+  angles_of(pKF1->mvKeysUn, S.a1);
+  angles_of(pKF2->mvKeysUn, S.a2);
+  S.f1.assign(pKF1->mFeatVec);
+  S.f2.assign(pKF2->mFeatVec);
+  const orbx_bow_side s1{pKF1->N, pKF1->mDescriptors.data, S.a1.data(), S.m1.data(), S.f1.view};
+  const orbx_bow_side s2{pKF2->N, pKF2->mDescriptors.data, S.a2.data(), S.m2.data(), S.f2.view};
+  S.idx.resize(std::max(pKF1->N, 1));
+  const std::vector<int32_t>& match = S.idx;
   int32_t n = 0;
-  const int rc = orbx_search_by_bow_kf_kf(&s1, &s2, mfNNratio, mbCheckOrientation, match.data(), &n);
+  const int rc = orbx_search_by_bow_kf_kf(&s1, &s2, mfNNratio, mbCheckOrientation, S.idx.data(), &n);
   if (rc != ORBX_OK) {
     log_fallback("orbx_search_by_bow_kf_kf", rc);
     return ORBmatcherHost(mfNNratio, mbCheckOrientation).SearchByBoW(pKF1, pKF2, vpMatches12);
@@ -178,23 +203,27 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
   const float invz = 1.0f / C2.at<float>(2);
   const float ex = pKF2->fx * C2.at<float>(0) * invz + pKF2->cx;
   const float ey = pKF2->fy * C2.at<float>(1) * invz + pKF2->cy;
-  std::vector<uint8_t> h1(pKF1->N), h2(pKF2->N);
-  for (int i = 0; i < pKF1->N; i++) h1[i] = pKF1->GetMapPoint(i) != NULL;
-  for (int i = 0; i < pKF2->N; i++) h2[i] = pKF2->GetMapPoint(i) != NULL;
-  FeatVecCSR f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
+  CallScratch& S = scratch();
+  S.m1.resize(pKF1->N);
+  S.m2.resize(pKF2->N);
+  for (int i = 0; i < pKF1->N; i++) S.m1[i] = pKF1->GetMapPoint(i) != NULL;
+  for (int i = 0; i < pKF2->N; i++) S.m2[i] = pKF2->GetMapPoint(i) != NULL;
+  S.f1.assign(pKF1->mFeatVec);
+  S.f2.assign(pKF2->mFeatVec);
   const orbx_tri_side s1{pKF1->N, pKF1->mDescriptors.data, keys_of(pKF1->mvKeysUn),
-                         pKF1->mvuRight.data(), h1.data(), f1.view, pKF1->mvScaleFactors.data(),
+                         pKF1->mvuRight.data(), S.m1.data(), S.f1.view, pKF1->mvScaleFactors.data(),
                          pKF1->mvLevelSigma2.data(), (int32_t)pKF1->mvScaleFactors.size()};
   const orbx_tri_side s2{pKF2->N, pKF2->mDescriptors.data, keys_of(pKF2->mvKeysUn),
-                         pKF2->mvuRight.data(), h2.data(), f2.view, pKF2->mvScaleFactors.data(),
+                         pKF2->mvuRight.data(), S.m2.data(), S.f2.view, pKF2->mvScaleFactors.data(),
                          pKF2->mvLevelSigma2.data(), (int32_t)pKF2->mvScaleFactors.size()};
   float F[9];
   for (int r = 0; r < 3; r++)
     for (int c = 0; c < 3; c++) F[3 * r + c] = F12.at<float>(r, c);
-  std::vector<int32_t> pairs(2 * std::max(pKF1->N, 1));
+  S.idx.resize(2 * std::max(pKF1->N, 1));
+  const std::vector<int32_t>& pairs = S.idx;
   int32_t n = 0;
   const int rc = orbx_search_for_triangulation(&s1, &s2, F, ex, ey, bOnlyStereo, mfNNratio,
-                                               mbCheckOrientation, pairs.data(), &n);
+                                               mbCheckOrientation, S.idx.data(), &n);
   if (rc != ORBX_OK) {
     log_fallback("orbx_search_for_triangulation", rc);
     return ORBmatcherHost(mfNNratio, mbCheckOrientation)

@@ -6,7 +6,7 @@ TAG=${1:-pmc}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-BENCH="bench.py --steps 4 --warmup 2 --no-cpu-baseline ${2:-}"
+BENCH="bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-upload ${2:-}"
 cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \

@@ -25,6 +25,13 @@
 //                          vector back to MapPoint pointers; SearchForTriangulation's
 //                          GetMapPoint(i) per feature under the keyframe's feature mutex and the
 //                          vector<pair<size_t, size_t>> result
+// The shims' scratch (CSR, masks, angles, the transform's and matchers' raw outputs) is kept per
+// thread and reused from call to call, as the shims keep it (CallScratch).
+// In shim mode thread 0 also writes its first and last timed frames to DIR/dump_first.bin and
+// DIR/dump_last.bin (what the shims hand back to Frame / ORBmatcher's callers: keypoints,
+// descriptors, the std::map BowVector and FeatureVector, SearchByBoW's MapPoint pointers as
+// point indices, SearchForTriangulation's pairs, with the masks and the geometry the calls used)
+// for tests/test_dropin_gpu.py to check against the CPU oracle.
 //
 // usage: orbx_dropin DIR W H NFEATURES N_IMG THREADS WARMUP FRAMES DEVICE [MODE]
 //   DIR/frames.u8       THREADS x N_IMG x H x W u8 images
@@ -136,11 +143,14 @@ struct ShimFrame {  // a Frame / KeyFrame: mvKeysUn, mDescriptors, BoW, map poin
   }
 };
 
-struct FeatVecCSR {  // ORBmatcher_orbx.cc's std::map -> CSR
+struct FeatVecCSR {  // ORBmatcher_orbx.cc's std::map -> CSR (capacity kept between calls)
   std::vector<uint32_t> ids;
   std::vector<int32_t> off, feats;
   orbx_featvec view;
-  explicit FeatVecCSR(const FeatVecMap& fv) {
+  void assign(const FeatVecMap& fv) {
+    ids.clear();
+    off.clear();
+    feats.clear();
     off.push_back(0);
     for (FeatVecMap::const_iterator it = fv.begin(); it != fv.end(); ++it) {
       ids.push_back(it->first);
@@ -151,10 +161,23 @@ struct FeatVecCSR {  // ORBmatcher_orbx.cc's std::map -> CSR
   }
 };
 
-std::vector<float> angles_of(const std::vector<orbx_keypoint>& k) {
-  std::vector<float> a(k.size());
+// the shims' per-thread scratch (ORBmatcher_orbx.cc, Frame_orbx.cc: CallScratch)
+struct CallScratch {
+  FeatVecCSR f1, f2;
+  std::vector<uint8_t> m1, m2;
+  std::vector<float> a1, a2;
+  std::vector<int32_t> idx, fo, ff;
+  std::vector<uint32_t> bw, fi;
+  std::vector<double> bv;
+};
+CallScratch& scratch() {
+  static thread_local CallScratch s;
+  return s;
+}
+
+void angles_of(const std::vector<orbx_keypoint>& k, std::vector<float>& a) {
+  a.resize(k.size());
   for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
-  return a;
 }
 
 // ORBextractor::operator() as ORBextractor_orbx.cc runs it
@@ -178,42 +201,49 @@ int shim_extract(orbx_extractor* ex, const uint8_t* img, int W, int H, int nfeat
   return ORBX_OK;
 }
 
-// Frame::ComputeBoW as Frame_orbx.cc runs it
+// Frame::ComputeBoW as Frame_orbx.cc runs it: ascending ids, so every map entry is placed at
+// the end by hint (no tree search)
 int shim_compute_bow(orbx_vocabulary* voc, ShimFrame& F) {
+  CallScratch& S = scratch();
   const int n = F.N;
   const size_t m = (size_t)std::max(n, 1);
-  std::vector<uint32_t> bw(m), fi(m + 1);
-  std::vector<double> bv(m);
-  std::vector<int32_t> fo(m + 2), ff(m);
+  S.bw.resize(m);
+  S.fi.resize(m + 1);
+  S.bv.resize(m);
+  S.fo.resize(m + 2);
+  S.ff.resize(m);
   int32_t nb = 0, nf = 0;
-  const int rc = orbx_vocabulary_transform(voc, F.desc.data(), n, 4, nullptr, nullptr, bw.data(),
-                                           bv.data(), &nb, fi.data(), fo.data(), ff.data(), &nf);
+  const int rc = orbx_vocabulary_transform(voc, F.desc.data(), n, 4, nullptr, nullptr, S.bw.data(),
+                                           S.bv.data(), &nb, S.fi.data(), S.fo.data(), S.ff.data(), &nf);
   if (rc != ORBX_OK) return rc;
   F.bow.clear();
   F.fv.clear();
-  for (int i = 0; i < nb; i++) F.bow.insert(F.bow.end(), std::make_pair(bw[i], bv[i]));
+  for (int i = 0; i < nb; i++) F.bow.emplace_hint(F.bow.end(), S.bw[i], S.bv[i]);
   for (int j = 0; j < nf; j++)
-    F.fv.insert(F.fv.end(), std::make_pair(fi[j], std::vector<unsigned int>(ff.begin() + fo[j],
-                                                                            ff.begin() + fo[j + 1])));
+    F.fv.emplace_hint(F.fv.end(), S.fi[j],
+                      std::vector<unsigned int>(S.ff.begin() + S.fo[j], S.ff.begin() + S.fo[j + 1]));
   return ORBX_OK;
 }
 
 // ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) as ORBmatcher_orbx.cc runs it
 int shim_search_by_bow(const ShimFrame& KF, const ShimFrame& F, std::vector<MapPointStub*>& out,
                        int32_t* nmatches) {
+  CallScratch& S = scratch();
   const std::vector<MapPointStub*> vpMP = KF.GetMapPointMatches();
-  std::vector<uint8_t> valid(vpMP.size());
-  for (size_t i = 0; i < vpMP.size(); i++) valid[i] = vpMP[i] && !vpMP[i]->isBad();
-  const std::vector<float> akf = angles_of(KF.keys), af = angles_of(F.keys);
-  FeatVecCSR fk(KF.fv), ff(F.fv);
-  const orbx_bow_side kf{KF.N, KF.desc.data(), akf.data(), valid.data(), fk.view};
-  const orbx_bow_side fr{F.N, F.desc.data(), af.data(), nullptr, ff.view};
-  std::vector<int32_t> match(std::max(F.N, 1));
-  const int rc = orbx_search_by_bow_kf_f(&kf, &fr, 0.7f, 1, match.data(), nmatches);
+  S.m1.resize(vpMP.size());
+  for (size_t i = 0; i < vpMP.size(); i++) S.m1[i] = vpMP[i] && !vpMP[i]->isBad();
+  angles_of(KF.keys, S.a1);
+  angles_of(F.keys, S.a2);
+  S.f1.assign(KF.fv);
+  S.f2.assign(F.fv);
+  const orbx_bow_side kf{KF.N, KF.desc.data(), S.a1.data(), S.m1.data(), S.f1.view};
+  const orbx_bow_side fr{F.N, F.desc.data(), S.a2.data(), nullptr, S.f2.view};
+  S.idx.resize(std::max(F.N, 1));
+  const int rc = orbx_search_by_bow_kf_f(&kf, &fr, 0.7f, 1, S.idx.data(), nmatches);
   if (rc != ORBX_OK) return rc;
   out.assign(F.N, nullptr);
   for (int i = 0; i < F.N; i++)
-    if (match[i] >= 0) out[i] = vpMP[match[i]];
+    if (S.idx[i] >= 0) out[i] = vpMP[S.idx[i]];
   return ORBX_OK;
 }
 
@@ -223,24 +253,59 @@ int shim_search_for_triangulation(const ShimFrame& K1, const ShimFrame& K2, cons
                                   float ex, float ey, const float* scale, const float* sigma2,
                                   int nl, std::vector<std::pair<size_t, size_t> >& pairs_out,
                                   int32_t* nmatches) {
-  std::vector<uint8_t> h1(K1.N), h2(K2.N);
-  for (int i = 0; i < K1.N; i++) h1[i] = K1.GetMapPoint(i) != nullptr;
-  for (int i = 0; i < K2.N; i++) h2[i] = K2.GetMapPoint(i) != nullptr;
-  FeatVecCSR f1(K1.fv), f2(K2.fv);
-  const orbx_tri_side s1{K1.N, K1.desc.data(), K1.keys.data(), nullptr, h1.data(), f1.view,
+  CallScratch& S = scratch();
+  S.m1.resize(K1.N);
+  S.m2.resize(K2.N);
+  for (int i = 0; i < K1.N; i++) S.m1[i] = K1.GetMapPoint(i) != nullptr;
+  for (int i = 0; i < K2.N; i++) S.m2[i] = K2.GetMapPoint(i) != nullptr;
+  S.f1.assign(K1.fv);
+  S.f2.assign(K2.fv);
+  const orbx_tri_side s1{K1.N, K1.desc.data(), K1.keys.data(), nullptr, S.m1.data(), S.f1.view,
                          scale, sigma2, nl};
-  const orbx_tri_side s2{K2.N, K2.desc.data(), K2.keys.data(), nullptr, h2.data(), f2.view,
+  const orbx_tri_side s2{K2.N, K2.desc.data(), K2.keys.data(), nullptr, S.m2.data(), S.f2.view,
                          scale, sigma2, nl};
-  std::vector<int32_t> pairs(2 * std::max(K1.N, 1));
-  const int rc = orbx_search_for_triangulation(&s1, &s2, F12, ex, ey, 0, 0.6f, 0, pairs.data(),
+  S.idx.resize(2 * std::max(K1.N, 1));
+  const int rc = orbx_search_for_triangulation(&s1, &s2, F12, ex, ey, 0, 0.6f, 0, S.idx.data(),
                                                nmatches);
   if (rc != ORBX_OK) return rc;
   pairs_out.clear();
   pairs_out.reserve(*nmatches);
   for (int i = 0; i < *nmatches; i++)
-    pairs_out.push_back(std::make_pair((size_t)pairs[2 * i], (size_t)pairs[2 * i + 1]));
+    pairs_out.push_back(std::make_pair((size_t)S.idx[2 * i], (size_t)S.idx[2 * i + 1]));
   return ORBX_OK;
 }
+
+// One frame's shim outputs for the oracle check (tests/test_dropin_gpu.py reads this layout)
+struct Dump {
+  FILE* f;
+  explicit Dump(const std::string& path) : f(fopen(path.c_str(), "wb")) {}
+  ~Dump() {
+    if (f) fclose(f);
+  }
+  void raw(const void* p, size_t n) {
+    if (f && n) fwrite(p, 1, n, f);
+  }
+  void i32(int32_t v) { raw(&v, 4); }
+  void u8(bool v) {
+    const uint8_t b = v ? 1 : 0;
+    raw(&b, 1);
+  }
+  void frame(const ShimFrame& F) {
+    i32(F.N);
+    raw(F.keys.data(), sizeof(orbx_keypoint) * F.N);
+    raw(F.desc.data(), (size_t)32 * F.N);
+    i32((int32_t)F.bow.size());
+    for (const auto& e : F.bow) i32((int32_t)e.first);
+    for (const auto& e : F.bow) raw(&e.second, 8);
+    i32((int32_t)F.fv.size());
+    for (const auto& e : F.fv) i32((int32_t)e.first);
+    int32_t o = 0;
+    i32(o);
+    for (const auto& e : F.fv) i32(o += (int32_t)e.second.size());
+    for (const auto& e : F.fv)
+      for (unsigned v : e.second) i32((int32_t)v);
+  }
+};
 
 struct Stats {
   std::vector<double> total, extract, bow, search_bow, search_tri;
@@ -386,6 +451,33 @@ int main(int argc, char** argv) {
         st.matches_bow += nb;
         st.matches_tri += nt;
         st.keypoints += cur.N;
+      }
+      if (t == 0 && f > 0 && (f == std::max(WARM, 1) || f == WARM + FR - 1)) {
+        // after the timing of this frame: the first and last timed frames of thread 0
+        Dump D(dir + (f == WARM + FR - 1 ? "/dump_last.bin" : "/dump_first.bin"));
+        D.raw("ORBXDMP1", 8);
+        D.i32(f);
+        D.i32(f % NIMG);
+        D.i32((f - 1) % NIMG);
+        D.raw(F12, 36);
+        D.raw(&ex, 4);
+        D.raw(&ey, 4);
+        D.i32(nl);
+        D.raw(scale, 4 * nl);
+        D.raw(sigma2, 4 * nl);
+        D.frame(prev);
+        D.frame(cur);
+        const MapPointStub* pbase = &mp_pool[(size_t)((f + 1) & 1) * 2 * cap];
+        for (int i = 0; i < prev.N; i++) D.u8(prev.mps[i] && !prev.mps[i]->isBad());
+        for (int i = 0; i < prev.N; i++) D.u8(prev.mps_tri[i] != nullptr);
+        for (int i = 0; i < cur.N; i++) D.u8(cur.mps_tri[i] != nullptr);
+        D.i32(nb);
+        for (int i = 0; i < cur.N; i++) D.i32(bow_out[i] ? (int32_t)(bow_out[i] - pbase) : -1);
+        D.i32(nt);
+        for (const auto& pr : tri_out) {
+          D.i32((int32_t)pr.first);
+          D.i32((int32_t)pr.second);
+        }
       }
     }
     for (int f = 0; f < WARM + FR && !shim; f++) {
