@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -877,57 +878,47 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
 // ---- k_fast_pairs: two horizontally adjacent FAST cells of one cell row per wave.  Cell j's
 // ROI ends 3 px past its detection columns, where cell j + 1's detection columns begin
 // (ORBextractor.cc:766-773: iniX = minBorderX + j wCell, maxX = iniX + wCell + 6), so the two
-// cells' detection columns are contiguous and one staged ROI of up to 70 x 40 px serves both:
-// the cardinal pretest runs on all 64 lanes (one detection column each, cwA + cwB <= 64), the
-// candidates of both cells share the scoring and NMS rounds, and staging, the V map, the scans
-// and the compaction are paid once per pair.  The NMS stays cell-local: the V map holds a zero
-// column between the two cells' columns (and the zero ring around them), so a neighbour across
-// the cell edge counts as 0, as on the reference's per-cell ROI.  A cell without a keypoint at
-// iniThFAST runs FAST again at minThFAST on its own columns (:782-784); each cell's survivors go
-// to its own slot in raster order.
-//
-// The staged ROI is a column-major plane of u16 pairs: word k of a column holds ROI rows k and
-// k + kPairD (low / high halves, one byte each), k < kPairD + 6.  A pretest step takes
-// detection rows s and s + kPairD of the lane's column in the two halves of one register, and
-// each of its five inputs — the centre and the circle points (0, -3), (3, 0), (0, 3), (-3, 0) —
-// is ONE aligned ds_read_b32: words s + 3 (centre; columns +-3 for the side points), s and s + 6.
-// The arc test runs on packed u16 maxima / minima:
-//   brighter candidate  min(max(x0, x8), max(x4, x12)) > v + t
-//   darker candidate    max(min(x0, x8), min(x4, x12)) < v - t
-// (any arc of 9 holds two adjacent cardinal points), 12 VALU per two pixels with the flag
-// word's shift, against round 4's 22 on byte rows (five d16 merges per two pixels).  Staging
-// is two 16-B loads per lane per round (rows k and k + 17 of a 16-column chunk, exactly the ROI's
-// rows and dwords: no clamped re-reads) and a v_perm per stored word.  A candidate's 7 x 7
-// window lies in one copy (low halves for detection rows < kPairD, high ones after), so the
-// scorer reads uniform offsets.
-// Queue entries: (detection row) << 6 | column.  A pass whose candidates outgrow the queue
+// cells' detection columns are contiguous and one staged ROI of up to 70 x 42 px serves both:
+// the cardinal pretest runs on all 64 lanes (one detection column each, cwA + cwB <= 64) instead
+// of the 31-32 lanes of a single ~31-px cell, the candidates of both cells share the scoring and
+// NMS rounds, and staging, the V map, the scans and the compaction are paid once per pair.  The
+// NMS stays cell-local: the V map holds a zero column between the two cells' columns (and the
+// zero ring around them), so a neighbour across the cell edge counts as 0, as on the reference's
+// per-cell ROI.  A cell without a keypoint at iniThFAST runs FAST again at minThFAST on its own
+// columns (:782-784); each cell's survivors go to its own slot in raster order.
+// Queue entries: (detection row r) << 6 | column c.  A pass whose candidates outgrow the queue
 // (dense texture) scores the rest in place, lane by lane, and then runs the NMS over the V map
 // instead of the queue (same result: the NMS candidates are the pixels with V > t).
-constexpr int kPairRS = 76;        // host eligibility: ROI width + its dword slack <= 76 bytes
-constexpr int kPairRows = 40;      // ROI rows (detection rows <= 34)
-constexpr int kPairD = 17;         // the second row of a lane step: detection row s + kPairD
-constexpr int kPairWords = kPairD + 6;   // plane words per column: ROI rows (k, k + kPairD)
-constexpr int kPairCS = 4 * kPairWords;  // 92 B per staged column: 23 dwords, odd (no conflicts)
-constexpr int kPairCols = 70;            // staged ROI columns (cwA + cwB + 6)
-constexpr int kPairQ = 384;              // queue entries
-constexpr int kPairKeepRows = 2 * kPairD;  // keep row per detection row
-constexpr int kPairVS = 40;        // V map: column-major, a column of ring + 34 rows + ring
-constexpr int kPairVCols = 67;     // ring, cwA, gap, cwB, ring
-// a wave's LDS: [queue][keep rows][plane][V map].  Staging writes whole 16-column chunks: up to
-// 3 columns before the plane (into the keep rows / queue, dead while a pair is staged) and up
-// to 10 past it (into the V map, zeroed after staging)
-constexpr int kPairOffK = 2 * kPairQ;
-constexpr int kPairOffP = kPairOffK + 8 * kPairKeepRows;
-constexpr int kPairOffV = (kPairOffP + kPairCS * kPairCols + 15) & ~15;
-constexpr int kPairVBytes = (kPairVS * kPairVCols + 15) & ~15;
-constexpr int kPairLds = kPairOffV + kPairVBytes;
+constexpr int kPairRS = 76;                          // staged ROI row: <= 70 px + 3 alignment
+constexpr int kPairRows = kFcSmallRows;              // ROI rows (detection rows <= 36)
+constexpr int kPairStage = 13;                       // staging rounds of 64 dwords (43.8 rows)
+constexpr int kPairSrc = kPairRS * (kPairRows + 6);  // + the keep rows (krows)
+constexpr int kPairKeepRows = 40;                    // >= detection rows
+constexpr int kPairVS = 72;                          // V row: ring, cwA, gap, cwB, ring
+constexpr int kPairVRows = kPairRows - 4;            // detection rows + 2 ring rows
+constexpr int kPairQ = 768;                          // queue entries
 constexpr int kPairsPerWave = 4;
-static_assert(kPairOffK % 8 == 0 && kPairOffP % 4 == 0 && kPairOffV % 16 == 0, "LDS alignment");
-static_assert(3 * kPairCS <= kPairOffP, "left staging spill stays in the wave's LDS");
-static_assert(10 * kPairCS <= kPairVBytes, "right staging spill stays in the V map");
-static_assert(kPairRows <= kPairWords + kPairD, "plane rows cover the ROI");
-static_assert(kPairVS >= kPairKeepRows + 2, "V column holds the ring rows");
-static_assert(4 * kPairLds <= 40 * 1024, "four workgroups per CU");
+static_assert(kPairStage * 256 >= kPairRows * kPairRS, "staging covers the ROI");
+static_assert(kPairStage * 256 <= kPairSrc - 8 * kPairKeepRows, "keep rows past the staged bytes");
+static_assert(kPairKeepRows >= kPairRows - 6, "a keep row per detection row");
+static_assert((kPairVS * kPairVRows) % 16 == 0, "V map in 16-B pieces");
+
+// Stage 1 of one detection chunk on all 64 lanes: rows r0 + 2 s and r0 + 2 s + 1 for steps
+// s < nst <= 16, two steps per LDS round trip; the flags of step s end at bit s (row r0 + 2 s)
+// and bit 16 + s (row r0 + 2 s + 1).
+template <int RS>
+__device__ __forceinline__ uint32_t cardinal_chunk16(const uint8_t* c0, int nst, int t) {
+  uint32_t acc = 0;
+  const uint8_t* c = c0;
+  int s = 0;
+  for (; s + 2 <= nst; s += 2, c += 4 * RS) {
+    uint32_t f0, f1;
+    fast_cardinal2x2<RS, 2 * RS>(c, t, f0, f1);
+    acc = (acc >> 2) | (f0 >> 1) | f1;
+  }
+  if (s < nst) acc = (acc >> 1) | fast_cardinal2<RS>(c, t);
+  return acc >> (16 - nst);
+}
 
 template <class K>
 __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ pyr,
@@ -937,7 +928,9 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
                                                     int ncells, int ini_th, int min_th,
                                                     K* __restrict__ cand, int cand_total,
                                                     int* __restrict__ cell_counts, int ppw) {
-  __shared__ __align__(16) uint8_t s_lds[4][kPairLds];
+  __shared__ __align__(16) uint8_t s_src[4][kPairSrc];
+  __shared__ __align__(16) uint8_t s_vv[4][kPairVS * kPairVRows];
+  __shared__ uint16_t s_q[4][kPairQ];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bx, img;
@@ -945,61 +938,44 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
   const int p0 = (bx * 4 + wid) * ppw;
   if (p0 >= npairs) return;  // wave-uniform; no workgroup barrier below
   const int p1 = min(p0 + ppw, npairs);
-  uint8_t* const W = s_lds[wid];
-  uint16_t* const q = (uint16_t*)W;
-  uint64_t* const krows = (uint64_t*)(W + kPairOffK);
-  uint8_t* const Pl = W + kPairOffP;  // plane: column x, word k at Pl + x * kPairCS + 4 k
-  uint8_t* const V = W + kPairOffV;
+  uint8_t* S = s_src[wid];
+  uint8_t* V = s_vv[wid];
+  uint16_t* q = s_q[wid];
+  // keep bits per detection row: the end of the staging buffer, past every staged byte (the
+  // pretest reads rows up to dr + 6 <= 42: inside the staged bytes)
+  uint64_t* const krows = (uint64_t*)(S + kPairSrc - 8 * kPairKeepRows);
   const uint8_t* pimg = pyr + (int64_t)img * pyr_bytes;
-  // staging tasks of this lane, rounds u = 0, 1: plane word k of a 16-column chunk ch (lanes
-  // take consecutive words of a chunk: conflict-free LDS stores)
-  int tk[2], tch[2];
+  // ROI staging: dword lane + 64 u of the staged rows (row (lane + 64 u) / 19, word % 19).  A
+  // lane loads exactly the ROI's dwords: rows past its last row and words past its last dword
+  // are not read (their staged bytes are stale and never used: stage 1 masks their flags, scores
+  // read detection pixels' windows only), and a round wholly past the ROI issues nothing.
+  constexpr int kW = kPairRS / 4;
+  int srow[kPairStage], swof[kPairStage];
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
+  for (int u = 0; u < kPairStage; u++) {
     const int i = lane + 64 * u;
-    tch[u] = i / kPairWords;
-    tk[u] = i - kPairWords * tch[u];
+    srow[u] = i / kW;
+    swof[u] = 4 * (i - kW * srow[u]);
   }
-  // 16-B loads at dword alignment (global_load_dwordx4 needs only that on gfx950)
-  typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-  u32x4_a4 pv[2][2];
-  int xoff = 0, nch = 0;
+  uint32_t pv[kPairStage];
+#pragma unroll
+  for (int u = 0; u < kPairStage; u++) pv[u] = 0u;
   auto issue = [&](const CellGeom& A, const CellGeom& B) {
     const int rows = A.y1 - A.y0;
-    xoff = A.x0 & 3;
-    nch = (xoff + (B.x1 - A.x0) + 15) >> 4;
-    const uint8_t* src = pimg + (A.v_row0 - 3 * A.pitch - 3) - xoff;  // ROI row 0, dword aligned
-    // every lane loads, branch-free: a task past the ROI's rows or chunks reads the last row /
-    // chunk (lines the wave's other lanes request anyway; its words are never used)
+    const int wb = (A.x0 & 3) + (B.x1 - A.x0);  // staged bytes per row (from the aligned start)
+    const uint8_t* src = pimg + (A.v_row0 - 3 * A.pitch - 3) + (A.x0 & ~3) - A.x0;
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
-      const int ch = min(tch[u], nch - 1);
-      const int r0 = min(tk[u], rows - 1), r1 = min(tk[u] + kPairD, rows - 1);
-      pv[u][0] = *(const u32x4_a4*)(src + (uint32_t)(__mul24(r0, A.pitch) + 16 * ch));
-      pv[u][1] = *(const u32x4_a4*)(src + (uint32_t)(__mul24(r1, A.pitch) + 16 * ch));
-    }
+    for (int u = 0; u < kPairStage; u++)
+      if (srow[u] < rows && swof[u] < wb)
+        pv[u] = *(const uint32_t*)(src + (uint32_t)(__mul24(srow[u], A.pitch) + swof[u]));
   };
   int2 pr = pairs[p0];
   CellGeom A = load_cell(cells, pr.x), B = load_cell(cells, pr.y);
   issue(A, B);
   for (int pi = p0; pi < p1; pi++) {
-    wave_sync();  // the previous pair's reads of the wave's LDS are done
-    // the staged ROI as the plane: word (lo byte j of row k, hi byte j of row k + kPairD) of
-    // column 16 ch + j - xoff, one v_perm each
+    wave_sync();  // the previous pair's reads of S are done
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
-      if (tch[u] < nch) {
-        uint8_t* dst = Pl + (16 * tch[u] - xoff) * kPairCS + 4 * tk[u];
-        const uint32_t lo[4] = {pv[u][0].x, pv[u][0].y, pv[u][0].z, pv[u][0].w};
-        const uint32_t hi[4] = {pv[u][1].x, pv[u][1].y, pv[u][1].z, pv[u][1].w};
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-          const uint32_t b = j & 3;
-          const uint32_t sel = 0x0c000c00u | ((4 + b) << 16) | b;
-          *(uint32_t*)(dst + j * kPairCS) = __builtin_amdgcn_perm(hi[j >> 2], lo[j >> 2], sel);
-        }
-      }
-    }
+    for (int u = 0; u < kPairStage; u++) *(uint32_t*)(S + 256 * u + 4 * lane) = pv[u];
     const CellGeom Ac = A, Bc = B;
     const int2 pc = pr;
     if (pi + 1 < p1) {  // the next pair's loads in flight while this one is processed
@@ -1010,102 +986,76 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
     }
     const int dr = Ac.y1 - Ac.y0 - 6;                      // detection rows, both cells
     const int cwA = Ac.x1 - Ac.x0 - 6, cw = cwA + (Bc.x1 - Bc.x0 - 6);  // detection columns
-    for (int i = lane; i < kPairVBytes / 16; i += 64) ((uint4*)V)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = lane; i < ((dr + 2) * kPairVS + 15) / 16; i += 64) ((uint4*)V)[i] = make_uint4(0u, 0u, 0u, 0u);
     wave_sync();
+    const uint8_t* Sx = S + (Ac.x0 & 3);  // pixel (r, c) of the ROI at Sx[r * RS + c]
     const uint64_t mA = (1ull << cwA) - 1;  // cwA <= 60
     const uint64_t mB = (cw >= 64 ? ~0ull : (1ull << cw) - 1) & ~mA;
-    // V byte of detection pixel (r, c): column-major, one ring row and column, the gap column
-    // after cell A
-    auto vofs = [&](int r, int c) { return __mul24(c + 1 + (c >= cwA ? 1 : 0), kPairVS) + r + 1; };
-    // cornerScore of detection pixel (r, c) from the copy holding its whole 7 x 7 window
+    // V byte of detection pixel (r, c): one ring row and column, the gap column after cell A
+    auto vofs = [&](int r, int c) { return __mul24(r + 1, kPairVS) + c + 1 + (c >= cwA ? 1 : 0); };
     auto score_at = [&](int r, int c) {
-      const bool hi = r >= kPairD;
-      const int sc = fast_score<kPairCS>(Pl + (hi ? 2 : 0), 4, c + 3, (hi ? r - kPairD : r) + 3);
-      V[vofs(r, c)] = (uint8_t)min(255, max(0, sc + 1));
+      const int sc = fast_score(Sx, kPairRS, c + 3, r + 3);
+      const int v = min(255, max(0, sc + 1));
+      V[vofs(r, c)] = (uint8_t)v;
+      return v;
     };
     uint64_t allow = mA | mB;  // the columns this pass detects on
     uint64_t bits1 = 0, keep1 = 0;
     uint64_t bits = 0;  // this lane's keep row (lane = detection row)
     int t = ini_th;
-    // the lane's column in the plane (detection column lane: ROI column lane + 3)
-    const uint32_t* colw = (const uint32_t*)(Pl + (lane + 3) * kPairCS);
     for (int pass = 0; pass < 2; pass++) {
-      // (1) cardinal pretest at t: steps 0..15 into acc (bit s: row s, bit 16 + s: row s + 17),
-      // step 16 into acc2 (bit 0: row 16, bit 1: row 33); every step runs (rows past dr read
-      // plane words that exist and are masked below: branch-free, the loads issued together)
-      const uint32_t T = (uint32_t)t * 0x10001u;
-      uint32_t acc = 0, acc2 = 0;
+      // (1) cardinal pretest at t, the flagged pixels queued (or scored in place past kPairQ)
       const bool col_ok = (allow >> lane) & 1;
-#pragma unroll
-      for (int s = 0; s < kPairD; s++) {
-        {
-          const uint32_t x0 = colw[s], c = colw[s + 3], x8 = colw[s + 6];
-          const uint32_t x4 = colw[s + 3 + 3 * kPairWords], x12 = colw[s + 3 - 3 * kPairWords];
-          typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-          typedef short i16x2 __attribute__((ext_vector_type(2)));
-          auto U = [](uint32_t v) { return __builtin_bit_cast(u16x2, v); };
-          const u16x2 br = __builtin_elementwise_min(__builtin_elementwise_max(U(x0), U(x8)),
-                                                     __builtin_elementwise_max(U(x4), U(x12)));
-          const u16x2 dk = __builtin_elementwise_max(__builtin_elementwise_min(U(x0), U(x8)),
-                                                     __builtin_elementwise_min(U(x4), U(x12)));
-          // saturating differences (v_pk_sub_u16 clamp): brighter / darker margins, then their
-          // maximum against t: negative halves of t - m are the candidates
-          const u16x2 ub = __builtin_elementwise_sub_sat(br, U(c));
-          const u16x2 ud = __builtin_elementwise_sub_sat(U(c), dk);
-          const u16x2 m = __builtin_elementwise_max(ub, ud);
-          const uint32_t sg = __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2, U(T)) -
-                                                               __builtin_bit_cast(i16x2, m));
-          if (s < 16) acc = (acc >> 1) | (sg & 0x80008000u);
-          else acc2 = ((sg >> 15) & 1u) | ((sg >> 30) & 2u);
-        }
-      }
-      // step s: bit s (row s), bit 16 + s (row s + 17)
-      {
-        const int nlo = min(16, dr), nhi = min(16, max(0, dr - kPairD));
-        acc &= col_ok ? ((1u << nlo) - 1u) | (((1u << nhi) - 1u) << 16) : 0u;
-        acc2 &= col_ok ? (dr > 16 ? 1u : 0u) | (dr > 16 + kPairD ? 2u : 0u) : 0u;
-      }
       int nq = 0;
       bool dense = false;
-      {
-        const int cnt = __popc(acc) + __popc(acc2);
+      for (int rc = 0; rc < dr; rc += 32) {
+        const int nst = min(16, (dr - rc + 1) >> 1);  // wave-uniform
+        const int nodd = min(16, (dr - rc) >> 1);     // steps whose second row is a detection row
+        uint32_t acc = cardinal_chunk16<kPairRS>(Sx + rc * kPairRS + lane, nst, t);
+        acc &= col_ok ? (((1u << nst) - 1u) | (((1u << nodd) - 1u) << 16)) : 0u;
+        const int cnt = __popc(acc);
         const int incl = wave_scan_incl(cnt);
         const int tot = __builtin_amdgcn_readlane(incl, 63);
-        if (tot > kPairQ) {  // wave-uniform, rare: score every flagged pixel in place
+        if (nq + tot > kPairQ) {  // wave-uniform, rare: score this chunk's pixels in place
           dense = true;
           while (acc) {
             const int b = __builtin_ctz(acc);
             acc &= acc - 1;
-            score_at(b < 16 ? b : b + 1, lane);
+            score_at(rc + 2 * (b & 15) + (b >> 4), lane);
           }
-          if (acc2 & 1u) score_at(16, lane);
-          if (acc2 & 2u) score_at(16 + kPairD, lane);
-        } else {
-          nq = tot;
-          uint16_t* qp = q + (incl - cnt);
-          // bit b < 16: row b; b >= 16: row b + 1 (= (b - 16) + kPairD)
-          const uint32_t e0 = (uint32_t)lane;
-          while (acc) {
-            const uint32_t b = (uint32_t)__builtin_ctz(acc);
-            acc &= acc - 1;
-            *qp++ = (uint16_t)(((b + (b >> 4)) << 6) | e0);
-          }
-          if (acc2 & 1u) *qp++ = (uint16_t)((16 << 6) | e0);
-          if (acc2 & 2u) *qp++ = (uint16_t)(((16 + kPairD) << 6) | e0);
+          continue;
+        }
+        int pos = nq + incl - cnt;
+        nq += tot;
+        while (acc) {
+          const int b = __builtin_ctz(acc);
+          acc &= acc - 1;
+          q[pos++] = (uint16_t)(((rc + 2 * (b & 15) + (b >> 4)) << 6) | lane);
         }
       }
       wave_sync();
       // (2) cornerScore of the queued pixels (a fallback pass rescores its cell's iniThFAST
-      // candidates: same value)
-      for (int j = lane; j < nq; j += 64) {
-        const int e = q[j];
-        score_at(e >> 6, e & 63);
+      // candidates: same value); the corners at t (V > max(t, 1): the NMS candidates, about a
+      // quarter of the queue) are compacted in place to the queue's front (a round reads its
+      // entries before any lane writes, and writes only below the next round's)
+      const int t1 = max(t, 1);
+      int nc = 0;
+      for (int j0 = 0; j0 < nq; j0 += 64) {
+        const int j = j0 + lane;
+        int e = 0;
+        bool corner = false;
+        if (j < nq) {
+          e = q[j];
+          corner = score_at(e >> 6, e & 63) > t1;
+        }
+        const uint64_t m = __ballot(corner);
+        if (corner) q[nc + lane_rank(m)] = (uint16_t)e;
+        nc += __popcll(m);
       }
       if (lane < kPairKeepRows) krows[lane] = 0;
       wave_sync();
-      // (3) the strict 8-neighbour NMS at t: keep <=> V > (nmax > t ? nmax : max(t,1)), the
-      // largest neighbour deciding (k_fast_cells)
-      const int t1 = max(t, 1);
+      // (3) the strict 8-neighbour NMS at t over the corners: keep <=> V > (nmax > t ? nmax :
+      // max(t,1)), the largest neighbour deciding (k_fast_cells)
       auto keep_at = [&](int r, int c) -> bool {
         const uint8_t* p = V + vofs(r, c);
         const int v = p[0];
@@ -1116,7 +1066,7 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
         return v > (nmax > t ? nmax : t1);
       };
       if (!dense) {
-        for (int j = lane; j < nq; j += 64) {
+        for (int j = lane; j < nc; j += 64) {
           const int e = q[j], r = e >> 6, c = e & 63;
           if (keep_at(r, c)) atomicOr((unsigned long long*)&krows[r], 1ull << c);
         }
@@ -1156,16 +1106,17 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
     K* outA = cand + (int64_t)img * cand_total + Ac.slot_off + ((incl - packed) & 0xFFFF);
     K* outB = cand + (int64_t)img * cand_total + Bc.slot_off + ((incl - packed) >> 16);
     const int y = Ac.y0 + 3 + lane, x0 = Ac.x0 + 3;
-    const uint8_t* Vr = V + lane + 1;  // detection row `lane` of V column 0
+    const uint8_t* Vr = V + __mul24(lane + 1, kPairVS) + 1;
     while (bA) {
       const int c = __builtin_ctzll(bA);
       bA &= bA - 1;
-      *outA++ = KeyFmt<K>::make(x0 + c, y, (int)Vr[__mul24(c + 1, kPairVS)]);
+      *outA++ = KeyFmt<K>::make(x0 + c, y, (int)Vr[c]);
     }
+    const uint8_t* VrB = Vr + cwA + 1;  // cell B's columns, past the gap column
     while (bB) {
       const int c = __builtin_ctzll(bB);
       bB &= bB - 1;
-      *outB++ = KeyFmt<K>::make(x0 + cwA + c, y, (int)Vr[__mul24(cwA + c + 2, kPairVS)]);
+      *outB++ = KeyFmt<K>::make(x0 + cwA + c, y, (int)VrB[c]);
     }
   }
 }
@@ -1184,7 +1135,6 @@ constexpr int kOctBigArea = 1 << 20;  // kOctBigArea px: a workgroup holds ~100 
                                       // (one per CU), so 1024 threads run its key passes 4x wide
 constexpr int kOctRegKeys = 16;       // keys per thread per register chunk
 constexpr int kOctBatch = 8;          // node-info loads in flight per key pass round
-constexpr int kOctBatchRl = 4;        // the relabel + count sweep's (more registers per key)
 constexpr size_t kOctMaxSmem = 150 * 1024;  // dynamic LDS of one octree workgroup
 
 struct OctNodes {
@@ -1210,9 +1160,7 @@ __device__ __forceinline__ int quad_of(K key, uint32_t info) {
 struct OctCtx {
   OctNodes A, B;
   int *cc, *t1, *t2, *t3, *t4, *s_tmp, *s_misc;
-  int* cc2;          // the next pass's quadrant counts (counted during this pass's relabel)
-  uint32_t* ninfo;   // node_info() of the current nodes
-  uint32_t* ninfo2;  // node_info() of the next pass's nodes (written with them)
+  uint32_t* ninfo;  // node_info() of the current nodes
   uint64_t *pk, *s_tmp64;
   void* outk;  // K[] of the level's retained keys
   int* oc;
@@ -1295,12 +1243,11 @@ __device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, 
 
 // What a key of node i becomes after a pass: its new label is base - pre[q], pre[q] = the node's
 // non-empty quadrants before the key's quadrant q (children are pushed in quadrant order); bits
-// 2q..2q+1 hold pre[q] (pre[0] = 0), zero for a node that is not divided, bit 8 is set for a
-// divided node and bits 9- hold the base
+// 2q..2q+1 hold pre[q] (pre[0] = 0), zero for a node that is not divided, and bits 8- the base
 __device__ __forceinline__ int relabel_info(int base, int divided, const int* ccn) {
-  if (!divided) return base << 9;
+  if (!divided) return base << 8;
   const int p1 = ccn[0] > 0, p2 = p1 + (ccn[1] > 0), p3 = p2 + (ccn[2] > 0);
-  return (base << 9) | 0x100 | (p1 << 2) | (p2 << 4) | (p3 << 6);
+  return (base << 8) | (p1 << 2) | (p2 << 4) | (p3 << 6);
 }
 
 template <int NT, class KS>
@@ -1350,58 +1297,54 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
   int seqc = nini;
   bool final_mode = false;
   const int N = G.nfeat;
-  // quadrant count of key slot j (label nd, node info `info`) into counts[4 nd + q]; keys are in
-  // cell order, so a wave's keys usually share one node and the four counts are added with one
-  // atomic each instead of one per key.  Every lane of the wave calls it (ballots).
-  const int lane = tid & 63;
-  auto count_one = [&](int* counts, int j, bool valid, int nd, uint32_t info) {
-    int q = -1;
-    if (valid && (info >> 31)) {
-      q = quad_of(ks.get_key(j), info);
-      ks.set_q(j, q);
-    }
-    const uint64_t act = __ballot(q >= 0);
-    if (!act) return;
-    const int first = __builtin_ctzll(act);
-    const int ndf = __shfl(nd, first);
-    if (__ballot(q >= 0 && nd != ndf) == 0) {
-#pragma unroll
-      for (int jj = 0; jj < 4; jj++) {
-        const int c = __popcll(__ballot(q == jj));
-        if (lane == first && c) atomicAdd(&counts[4 * ndf + jj], c);
-      }
-    } else if (q >= 0) {
-      atomicAdd(&counts[4 * nd + q], 1);
-    }
-  };
-  // the first pass's quadrant counts: one sweep over the keys; later passes count during the
-  // previous pass's relabel (below), so each pass sweeps the keys once
-  for (int i = tid; i < 4 * size; i += NT) cc[i] = 0;
-  for (int i = tid; i < size; i += NT)
-    X.ninfo[i] = node_info(cur.cnt[i], cur.x0[i], cur.x1[i], cur.y0[i], cur.y1[i]);
-  __syncthreads();
-  // every lane runs every slot (the ballots need the whole wave); a chunk's node infos are
-  // loaded together before its first atomic, one LDS latency per chunk instead of per key
-  for (int c = 0; c < ks.nchunks(); c++) {
-    ks.load(c, true);
-#pragma unroll
-    for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
-      uint32_t inf[kOctBatch];
-#pragma unroll
-      for (int j = 0; j < kOctBatch; j++)
-        inf[j] = tid + NT * (c * kOctRegKeys + j0 + j) < n ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
-#pragma unroll
-      for (int j = 0; j < kOctBatch; j++) {
-        const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
-        count_one(cc, j0 + j, v, v ? ks.get_lab(j0 + j) : -1, inf[j]);
-      }
-    }
-  }
-  __syncthreads();
-  int* ccn = X.cc2;
-  uint32_t *ninfo = X.ninfo, *ninfo_n = X.ninfo2;
   for (int iter = 0; iter < 4096; iter++) {
     const int prevSize = size;
+    for (int i = tid; i < 4 * size; i += NT) cc[i] = 0;
+    for (int i = tid; i < size; i += NT)
+      X.ninfo[i] = node_info(cur.cnt[i], cur.x0[i], cur.x1[i], cur.y0[i], cur.y1[i]);
+    __syncthreads();
+    // quadrant counts; keys are in cell order, so a wave's keys usually share one node and the
+    // four counts are added with one atomic each instead of one per key
+    const int lane = tid & 63;
+    auto count_one = [&](int j, int k, uint32_t info) {
+      int nd = -1, q = -1;
+      if (k < n) {
+        nd = ks.get_lab(j);
+        if (info >> 31) {
+          q = quad_of(ks.get_key(j), info);
+          ks.set_q(j, q);
+        }
+      }
+      const uint64_t act = __ballot(q >= 0);
+      if (!act) return;
+      const int first = __builtin_ctzll(act);
+      const int ndf = __shfl(nd, first);
+      if (__ballot(q >= 0 && nd != ndf) == 0) {
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+          const int c = __popcll(__ballot(q == jj));
+          if (lane == first && c) atomicAdd(&cc[4 * ndf + jj], c);
+        }
+      } else if (q >= 0) {
+        atomicAdd(&cc[4 * nd + q], 1);
+      }
+    };
+    // every lane runs every slot (the ballots need the whole wave); a chunk's node infos are
+    // loaded together before its first atomic, one LDS latency per chunk instead of per key
+    for (int c = 0; c < ks.nchunks(); c++) {
+      ks.load(c, true);
+#pragma unroll
+      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
+        uint32_t inf[kOctBatch];
+#pragma unroll
+        for (int j = 0; j < kOctBatch; j++)
+          inf[j] = tid + NT * (c * kOctRegKeys + j0 + j) < n ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
+#pragma unroll
+        for (int j = 0; j < kOctBatch; j++)
+          count_one(j0 + j, tid + NT * (c * kOctRegKeys + j0 + j), inf[j]);
+      }
+    }
+    __syncthreads();
     int T, newSize, nToExpand;
     if (!final_mode) {
       // outer pass (list order): one packed scan gives childPre (bits 0-19), the rank among
@@ -1522,9 +1465,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       }
       __syncthreads();
     }
-    // write next node arrays: t2 = divided, t1 = childPre, t4 = base, t3 = relabel_info; with
-    // them the next pass's node infos and counts: a child's counts start at zero (its keys are
-    // counted by the relabel sweep below), an undivided node keeps this pass's counts
+    // write next node arrays: t2 = divided, t1 = childPre, t4 = base, t3 = relabel_info
     for (int i = tid; i < size; i += NT) {
       if (t2[i]) {
         const int x0 = cur.x0[i], x1 = cur.x1[i], y0 = cur.y0[i], y1 = cur.y1[i];
@@ -1535,16 +1476,12 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
           const int c = cc[4 * i + q];
           if (c > 0) {
             const int pos = t4[i] - j;
-            const int cx0 = (q & 1) ? xm : x0, cx1 = (q & 1) ? x1 : xm;
-            const int cy0 = (q & 2) ? ym : y0, cy1 = (q & 2) ? y1 : ym;
-            nxt.x0[pos] = (int16_t)cx0;
-            nxt.x1[pos] = (int16_t)cx1;
-            nxt.y0[pos] = (int16_t)cy0;
-            nxt.y1[pos] = (int16_t)cy1;
+            nxt.x0[pos] = (int16_t)((q & 1) ? xm : x0);
+            nxt.x1[pos] = (int16_t)((q & 1) ? x1 : xm);
+            nxt.y0[pos] = (int16_t)((q & 2) ? ym : y0);
+            nxt.y1[pos] = (int16_t)((q & 2) ? y1 : ym);
             nxt.cnt[pos] = c;
             nxt.seq[pos] = seqc + t1[i] + j;
-            ninfo_n[pos] = node_info(c, cx0, cx1, cy0, cy1);
-            *(int4*)&ccn[4 * pos] = make_int4(0, 0, 0, 0);
             j++;
           }
         }
@@ -1553,40 +1490,26 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         nxt.x0[pos] = cur.x0[i]; nxt.x1[pos] = cur.x1[i];
         nxt.y0[pos] = cur.y0[i]; nxt.y1[pos] = cur.y1[i];
         nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
-        ninfo_n[pos] = ninfo[i];
-        *(int4*)&ccn[4 * pos] = *(const int4*)&cc[4 * i];  // zero unless counted (cnt > 1)
       }
     }
-    __syncthreads();
-    // relabel keys and count the divided nodes' keys into their children's quadrants for the
-    // next pass (a key's child and that child's split point are now known): a chunk's relabel
-    // infos (and, for keys in memory, node infos), then the children's infos, each in one round
+    // relabel keys: a chunk's relabel infos (and, for keys in memory, node infos) in one round
     // of loads
     for (int c = 0; c < ks.nchunks(); c++) {
       ks.load(c, true);
 #pragma unroll
-      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatchRl) {
-        uint32_t rl[kOctBatchRl], inf[kOctBatchRl];
+      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
+        uint32_t rl[kOctBatch], inf[kOctBatch];
 #pragma unroll
-        for (int j = 0; j < kOctBatchRl; j++) {
+        for (int j = 0; j < kOctBatch; j++) {
           const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
           rl[j] = v ? (uint32_t)t3[ks.get_lab(j0 + j)] : 0u;
-          inf[j] = (!KS::kRegs && v) ? ninfo[ks.get_lab(j0 + j)] : 0u;
-        }
-        int nl[kOctBatchRl];
-#pragma unroll
-        for (int j = 0; j < kOctBatchRl; j++) {
-          const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
-          // rl bits 2..7 are zero for an undivided node: its keys keep their node (base)
-          nl[j] = (int)(rl[j] >> 9) - (int)((rl[j] >> (2 * ks.get_q(j0 + j, inf[j]))) & 3u);
-          if (v) ks.set_lab(j0 + j, nl[j]);
-          inf[j] = v && (rl[j] & 0x100u) ? ninfo_n[nl[j]] : 0u;  // a divided node's child
+          inf[j] = (!KS::kRegs && v) ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < kOctBatchRl; j++) {
-          const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
-          count_one(ccn, j0 + j, v, nl[j], inf[j]);
-        }
+        for (int j = 0; j < kOctBatch; j++)
+          if (tid + NT * (c * kOctRegKeys + j0 + j) < n)
+            ks.set_lab(j0 + j, (int)(rl[j] >> 8) -
+                                   (int)((rl[j] >> (2 * ks.get_q(j0 + j, inf[j]))) & 3u));
       }
       ks.store_labs(c);
     }
@@ -1595,12 +1518,6 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       OctNodes tmp = cur;
       cur = nxt;
       nxt = tmp;
-      int* tc = cc;
-      cc = ccn;
-      ccn = tc;
-      uint32_t* ti = ninfo;
-      ninfo = ninfo_n;
-      ninfo_n = ti;
     }
     size = newSize;
     seqc += T;
@@ -1675,8 +1592,6 @@ void k_octree(
   int* t3 = (int*)take(4 * NC);
   int* t4 = (int*)take(4 * NC);
   uint32_t* ninfo = (uint32_t*)take(4 * NC);
-  int* cc2 = (int*)take(16 * NC);
-  uint32_t* ninfo2 = (uint32_t*)take(4 * NC);
   // per-cell key starts and slots: in LDS, or (cell_cap == 0: levels with too many cells for
   // it) in this (image, level)'s part of cell_scr, [2 (ncells + nlevels)] ints per image
   int* cpre = cell_cap > 0 ? (int*)take(4 * (cell_cap + 1))
@@ -1726,7 +1641,7 @@ void k_octree(
       v[j] = k < n ? cb[s_slot[c] + k - cpre[c]] : K(0);
     }
   };
-  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, cc2, ninfo, ninfo2, pk, s_tmp64, outk, oc};
+  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, ninfo, pk, s_tmp64, outk, oc};
   if (n <= kOctRegKeys * NT) {  // keys + labels in registers: every pass stays on-chip
     RegKeys<NT, K> ks;
     ks.n = n;
@@ -2183,6 +2098,9 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (!P) return ORBX_ENOMEM;
   std::string why;
   P->g.py_band_h = max_batch <= kPyFewImages ? kPyBandHSmall : kPyBandH;
+  // batch plans: a k_pyramid launch of at least kPyMinGrid workgroups (4 rounds of the chip's
+  // ~768 resident tiles), however few tiles a stage's small levels need
+  P->g.py_min_tiles = max_batch <= kPyFewImages ? 1 : std::max(1, (kPyMinGrid + max_batch - 1) / max_batch);
   int rc = build_geometry(*params, w, h, &P->g, &why);
   if (rc != ORBX_OK) {
     fprintf(stderr, "[orbx] plan %dx%d unsupported: %s\n", w, h, why.c_str());
@@ -2289,7 +2207,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   auto oct_bytes = [&](size_t NC, size_t CC) {
-    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + 2 * r16(16 * NC) + 6 * r16(4 * NC) +
+    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 5 * r16(4 * NC) +
            (CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0) + r16(8 * NC);
   };
   while (P->oct_split < g.nlevels && (int64_t)g.lv[P->oct_split].W * g.lv[P->oct_split].H > kOctBigArea)

@@ -241,8 +241,9 @@ static int stage_tiles(const Geometry& g, PyrStage& st, int nb, int ncol, bool f
 
 // k_pyramid's stages and tiles (the comment in build_pyramid); false when no tiling of a stage
 // fits kPyMaxSmemLimit bytes of LDS.  Per stage, for every column split 1 .. kPyMaxCols, the
-// tallest bands (down to py_band_h / kPyBandHMin source rows) whose two LDS buffers fit the
-// bound, then the split whose tiles compute the fewest pixels.
+// tallest bands (at most kPyBandHMul x py_band_h source rows, at least py_min_tiles tiles per
+// image) whose two LDS buffers fit the bound, then the split whose tiles compute the fewest
+// pixels.
 static bool build_stages(Geometry* g, bool fused, double* recompute) {
   const int nl = g->nlevels;
   g->pyr_stages.clear();
@@ -264,7 +265,8 @@ static bool build_stages(Geometry* g, bool fused, double* recompute) {
       const int ncmax = g->py_band_h < kPyBandH ? 1 : kPyMaxCols;
       for (int ncol = 1; ncol <= ncmax; ncol++) {
         const int band_h = g->py_band_h < kPyBandH ? g->py_band_h : g->py_band_h * kPyBandHMul;
-        const int nb_lo = std::max(1, hs / std::max(1, band_h));
+        // enough tiles per image that a batch's launch fills the chip several times over
+        const int nb_lo = std::max({1, hs / std::max(1, band_h), (g->py_min_tiles + ncol - 1) / ncol});
         const int nb_hi = std::max(nb_lo, hs);
         for (int nb = nb_lo; nb <= nb_hi; nb++) {
           PyrStage s2 = st;

@@ -56,6 +56,7 @@ constexpr int kPyBlurStrip = 4;  // fused blur: output rows per lane
 // kPyBandH source rows (the tallest that fit the LDS bound)
 constexpr int kPyMaxCols = 8;
 constexpr int kPyBandHMul = 4;
+constexpr int kPyMinGrid = 3072;
 // A band is a tile: a range of rows and of 4-column groups of every level of its stage.  Wide
 // frames split their rows into several column tiles, so a tile's rows can be many without its
 // LDS outgrowing the bound, and the rows and columns the tile recomputes for the next level's
@@ -128,6 +129,7 @@ struct Geometry {
   bool wide_keys = false;             // an octree frame >= 4096 px: 64-bit candidate keys
   bool blur_fused = false;            // k_pyramid blurs the levels (else the k_blur launch)
   int py_band_h = kPyBandH;           // k_pyramid source rows per band (set before building)
+  int py_min_tiles = 1;               // k_pyramid tiles per image and stage, at least (idem)
   float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
   int feats[kMaxLevels];
   int umax[kHalfPatch + 1];
