@@ -39,6 +39,9 @@ struct ExtractorCtx {
   // the last device call's input (a header sharing the caller's refcounted image): if the
   // pyramid export fails, the host extractor rebuilds mvImagePyramid from it
   cv::Mat last_image;
+  // the library's raw outputs, kept between calls (one extractor runs on one thread)
+  std::vector<orbx_keypoint> kps;
+  cv::Mat desc;
 };
 
 std::mutex g_mutex;
@@ -135,27 +138,28 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask,
   int rc = c.ex ? ORBX_OK : ORBX_EDEVICE;
   int32_t n = 0;
   if (c.ex) {
-    int32_t cap = 4 * nfeatures + 64;
-    _keypoints.resize(cap);
-    cv::Mat d(cap, 32, CV_8U);
-    rc = orbx_extract(c.ex, image.data, image.cols, image.rows, (int64_t)image.step,
-                      reinterpret_cast<orbx_keypoint*>(_keypoints.data()), d.data, cap, &n);
+    int32_t cap = std::max<int32_t>(4 * nfeatures + 64, (int32_t)c.kps.size());
+    if ((int32_t)c.kps.size() < cap) c.kps.resize(cap);
+    if (c.desc.rows < cap) c.desc.create(cap, 32, CV_8U);
+    rc = orbx_extract(c.ex, image.data, image.cols, image.rows, (int64_t)image.step, c.kps.data(),
+                      c.desc.data, cap, &n);
     if (rc == ORBX_ECAPACITY) {  // more keypoints than the first guess: grow once, repeat
       cap = n;
-      _keypoints.resize(cap);
-      d.create(cap, 32, CV_8U);
+      c.kps.resize(cap);
+      c.desc.create(cap, 32, CV_8U);
       rc = orbx_extract(c.ex, image.data, image.cols, image.rows, (int64_t)image.step,
-                        reinterpret_cast<orbx_keypoint*>(_keypoints.data()), d.data, cap, &n);
+                        c.kps.data(), c.desc.data, cap, &n);
     }
     if (rc == ORBX_OK) {
       if (n <= 0) {  // :1005-1006 (no keypoints: descriptors released)
         _keypoints.clear();
         _descriptors.release();
       } else {
-        _keypoints.resize(n);
+        const cv::KeyPoint* k = reinterpret_cast<const cv::KeyPoint*>(c.kps.data());
+        _keypoints.assign(k, k + n);
         _descriptors.create(n, 32, CV_8U);  // as ORBextractor.cc:1008-1009
         cv::Mat out = _descriptors.getMat();
-        d.rowRange(0, n).copyTo(out);
+        c.desc.rowRange(0, n).copyTo(out);
       }
       // mvImagePyramid (ORBextractor.h:88) is read by Frame::ComputeStereoMatches only, which
       // runs on the device: it is exported on demand (orbx_materialize_pyramid), not per call

@@ -206,8 +206,14 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
   CallScratch& S = scratch();
   S.m1.resize(pKF1->N);
   S.m2.resize(pKF2->N);
-  for (int i = 0; i < pKF1->N; i++) S.m1[i] = pKF1->GetMapPoint(i) != NULL;
-  for (int i = 0; i < pKF2->N; i++) S.m2[i] = pKF2->GetMapPoint(i) != NULL;
+  // the reference reads GetMapPoint(idx) per candidate (:702, :725), one lock each; one snapshot
+  // per keyframe (one lock) reads the same pointers
+  {
+    const std::vector<MapPoint*> vp1 = pKF1->GetMapPointMatches();
+    const std::vector<MapPoint*> vp2 = pKF2->GetMapPointMatches();
+    for (int i = 0; i < pKF1->N; i++) S.m1[i] = vp1[i] != NULL;
+    for (int i = 0; i < pKF2->N; i++) S.m2[i] = vp2[i] != NULL;
+  }
   S.f1.assign(pKF1->mFeatVec);
   S.f2.assign(pKF2->mFeatVec);
   const orbx_tri_side s1{pKF1->N, pKF1->mDescriptors.data, keys_of(pKF1->mvKeysUn),

@@ -14,16 +14,16 @@
 // "shim" replays what the reference-side shims (include/compat/*.cc) do around each call, so the
 // number is what Frame.cc:252-258 / Tracking.cc:1132-1136 / LocalMapping.cc:238-241 would see
 // with the shims linked in — everything but OpenCV itself, which is not in this image:
-//   ORBextractor_orbx.cc   a fresh keypoint vector and a cap x 32 descriptor block per call
-//                          (cv::Mat d), then descriptors.create(n, 32) + the row copy; no pyramid
-//                          export (mvImagePyramid is materialised on demand, mono never does)
+//   ORBextractor_orbx.cc   the library writes into the extractor's kept keypoint / descriptor
+//                          blocks, then the keypoint vector of n and descriptors.create(n, 32) +
+//                          the row copy; no pyramid export (mvImagePyramid is materialised on demand, mono never does)
 //   Frame_orbx.cc          per-call output vectors, then BowVector / FeatureVector as the
 //                          reference's std::maps (map<WordId, double>, map<NodeId,
 //                          vector<unsigned>>)
 //   ORBmatcher_orbx.cc     GetMapPointMatches() copies, the validity masks (isBad per point),
 //                          angles, the std::map FeatureVectors -> CSR for both sides, the match
 //                          vector back to MapPoint pointers; SearchForTriangulation's
-//                          GetMapPoint(i) per feature under the keyframe's feature mutex and the
+//                          one GetMapPointMatches() snapshot per keyframe and the
 //                          vector<pair<size_t, size_t>> result
 // The shims' scratch (CSR, masks, angles, the transform's and matchers' raw outputs) is kept per
 // thread and reused from call to call, as the shims keep it (CallScratch).
@@ -137,9 +137,9 @@ struct ShimFrame {  // a Frame / KeyFrame: mvKeysUn, mDescriptors, BoW, map poin
     std::lock_guard<std::mutex> lk(mutex_features);
     return mps;
   }
-  MapPointStub* GetMapPoint(size_t i) const {
+  std::vector<MapPointStub*> GetMapPointMatchesTri() const {  // triangulation's draw
     std::lock_guard<std::mutex> lk(mutex_features);
-    return mps_tri[i];
+    return mps_tri;
   }
 };
 
@@ -169,6 +169,8 @@ struct CallScratch {
   std::vector<int32_t> idx, fo, ff;
   std::vector<uint32_t> bw, fi;
   std::vector<double> bv;
+  std::vector<orbx_keypoint> kps;  // ORBextractor_orbx.cc's ExtractorCtx::kps / desc
+  std::vector<uint8_t> desc;
 };
 CallScratch& scratch() {
   static thread_local CallScratch s;
@@ -183,21 +185,22 @@ void angles_of(const std::vector<orbx_keypoint>& k, std::vector<float>& a) {
 // ORBextractor::operator() as ORBextractor_orbx.cc runs it
 int shim_extract(orbx_extractor* ex, const uint8_t* img, int W, int H, int nfeatures,
                  ShimFrame& F) {
-  int32_t cap = 4 * nfeatures + 64, n = 0;
-  std::vector<orbx_keypoint> kps(cap);
-  std::vector<uint8_t> d((size_t)cap * 32);
-  int rc = orbx_extract(ex, img, W, H, W, kps.data(), d.data(), cap, &n);
+  CallScratch& S = scratch();
+  int32_t cap = std::max<int32_t>(4 * nfeatures + 64, (int32_t)S.kps.size()), n = 0;
+  if ((int32_t)S.kps.size() < cap) S.kps.resize(cap);
+  if (S.desc.size() < (size_t)cap * 32) S.desc.resize((size_t)cap * 32);
+  int rc = orbx_extract(ex, img, W, H, W, S.kps.data(), S.desc.data(), cap, &n);
   if (rc == ORBX_ECAPACITY) {
     cap = n;
-    kps.resize(cap);
-    d.resize((size_t)cap * 32);
-    rc = orbx_extract(ex, img, W, H, W, kps.data(), d.data(), cap, &n);
+    S.kps.resize(cap);
+    S.desc.resize((size_t)cap * 32);
+    rc = orbx_extract(ex, img, W, H, W, S.kps.data(), S.desc.data(), cap, &n);
   }
   if (rc != ORBX_OK) return rc;
-  kps.resize(std::max(n, 0));
-  F.keys.swap(kps);
-  F.desc.assign(d.begin(), d.begin() + (size_t)std::max(n, 0) * 32);  // create(n, 32) + copyTo
-  F.N = std::max(n, 0);
+  n = std::max(n, 0);
+  F.keys.assign(S.kps.begin(), S.kps.begin() + n);
+  F.desc.assign(S.desc.begin(), S.desc.begin() + (size_t)n * 32);  // create(n, 32) + copyTo
+  F.N = n;
   return ORBX_OK;
 }
 
@@ -256,8 +259,11 @@ int shim_search_for_triangulation(const ShimFrame& K1, const ShimFrame& K2, cons
   CallScratch& S = scratch();
   S.m1.resize(K1.N);
   S.m2.resize(K2.N);
-  for (int i = 0; i < K1.N; i++) S.m1[i] = K1.GetMapPoint(i) != nullptr;
-  for (int i = 0; i < K2.N; i++) S.m2[i] = K2.GetMapPoint(i) != nullptr;
+  {
+    const std::vector<MapPointStub*> vp1 = K1.GetMapPointMatchesTri(), vp2 = K2.GetMapPointMatchesTri();
+    for (int i = 0; i < K1.N; i++) S.m1[i] = vp1[i] != nullptr;
+    for (int i = 0; i < K2.N; i++) S.m2[i] = vp2[i] != nullptr;
+  }
   S.f1.assign(K1.fv);
   S.f2.assign(K2.fv);
   const orbx_tri_side s1{K1.N, K1.desc.data(), K1.keys.data(), nullptr, S.m1.data(), S.f1.view,
