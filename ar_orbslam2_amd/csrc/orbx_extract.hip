@@ -3,13 +3,13 @@
 //
 // One plan = one image size + one parameter set + a maximum batch.  A batch of images runs
 // as a fixed launch sequence on the plan's stream (captured once into a hipGraph):
-//   k_pyramid       2-3 launches row bands               (level 0 copy + cv::resize INTER_LINEAR;
+//   k_pyramid       2-3 launches band x column tiles     (level 0 copy + cv::resize INTER_LINEAR;
 //                                                         k_pyramid<true> also GaussianBlur 7x7
 //                                                         s=2 of its rows, Geometry::blur_fused)
 //   k_blur          x 0-1        64x64 tiles, all levels (GaussianBlur 7x7 s=2, unfused plans)
 //   k_fast_pairs    x 0-1        two FAST cells, a wave  (FAST + cell-local NMS at iniThFAST, the
 //   k_fast_cells    x 1-3        up to 4 cells, a wave    minThFAST retry, raster compaction)
-//   k_octree        x 1-2        (image, level)          (DistributeOctTree; big levels apart)
+//   k_octree        x 1-2        (image, level)          (DistributeOctTree on quadrant-path bins)
 //   k_describe      x 1          half-wave per keypoint  (IC_Angle + rBRIEF)
 // The first k_pyramid launch copies level 0 from the caller's input into the pitched pyramid
 // block, where every level lives.  Everything is integer or bit-exact float (see orbx_math.h); compiled with
@@ -66,6 +66,12 @@ __device__ __forceinline__ int reflect101(int p, int len) {
   return p;
 }
 
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int NT>
 __device__ int block_sum(int v, int* s_tmp) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -80,36 +86,40 @@ __device__ int block_sum(int v, int* s_tmp) {
   return t;
 }
 
+// exclusive prefix over the threads of one value each (and the total)
+template <int NT>
+__device__ __forceinline__ int grp_excl(int v, int* s_tmp, int& total) {
+  const int inc = wave_scan_incl(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 63) s_tmp[wid] = inc;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; w++) {
+    const int x = s_tmp[w];
+    pre += w < wid ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return pre + inc - v;
+}
+
 // Exclusive scan of a[0..M) in place (LDS array), chunked per thread so the scan is stable.
 template <int NT>
 __device__ int block_scan_excl(int* a, int M, int* s_tmp) {
   const int per = (M + NT - 1) / NT;
-  const int t = threadIdx.x;
-  const int beg = min(t * per, M), end = min(beg + per, M);
+  const int beg = min((int)threadIdx.x * per, M), end = min(beg + per, M);
   int sum = 0;
   for (int i = beg; i < end; i++) sum += a[i];
-  const int lane = t & 63, wid = t >> 6;
-  const int v = wave_scan_incl(sum);
-  __syncthreads();
-  if (lane == 63) s_tmp[wid] = v;
-  __syncthreads();
-  if (t == 0) {
-    int acc = 0;
-    for (int w = 0; w < NT / 64; w++) {
-      const int x = s_tmp[w];
-      s_tmp[w] = acc;
-      acc += x;
-    }
-    s_tmp[NT / 64] = acc;
-  }
-  __syncthreads();
-  int run = s_tmp[wid] + v - sum;
+  int total;
+  int run = grp_excl<NT>(sum, s_tmp, total);
   for (int i = beg; i < end; i++) {
     const int x = a[i];
     a[i] = run;
     run += x;
   }
-  const int total = s_tmp[NT / 64];
   __syncthreads();
   return total;
 }
@@ -146,6 +156,28 @@ __device__ uint64_t block_scan_excl64(uint64_t* a, int M, uint64_t* s_tmp) {
   const uint64_t total = s_tmp[NT / 64];
   __syncthreads();
   return total;
+}
+
+// exclusive max-scan of one value >= -1 per thread (-1 below the first): DPP row shifts and
+// row broadcasts as wave_scan_incl, on v + 1 so that a missing source (0) is neutral
+template <int NT>
+__device__ int block_max_excl(int v, int* s_tmp) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t u = (uint32_t)(v + 1);
+  u = max(u, dpp0<0x111, 0xF, true>(u));
+  u = max(u, dpp0<0x112, 0xF, true>(u));
+  u = max(u, dpp0<0x114, 0xF, true>(u));
+  u = max(u, dpp0<0x118, 0xF, true>(u));
+  u = max(u, dpp0<0x142, 0xA, false>(u));
+  u = max(u, dpp0<0x143, 0xC, false>(u));
+  const int ex = (int)dpp0<0x138, 0xF, true>(u) - 1;  // wave_shr:1 (lane 0: none)
+  __syncthreads();
+  if (lane == 63) s_tmp[wid] = (int)u - 1;
+  __syncthreads();
+  int pre = -1;
+  for (int w = 0; w < wid; w++) pre = max(pre, s_tmp[w]);
+  __syncthreads();
+  return max(pre, ex);
 }
 
 // ------------------------------------------------------------------ k_pyramid
@@ -696,12 +728,6 @@ __device__ __forceinline__ void compact_rows(uint64_t bits, int lane, int y, int
 // alignment slack, kFcSmallRows high: the usual ~30-px grid), <48, kCellMax> (up to 45 wide and
 // kCellMax high: levels with 2-3 cell rows, 46 KB of LDS per workgroup instead of 70) and
 // <72, kCellMax> (any cell); `list` holds the instance's cells.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 constexpr int kFcSmallRows = 42;  // ROI rows of the small k_fast_cells instance (44 measured slower)
 constexpr int kFcTallRS = 48;     // staged row of the tall instance: ROIs up to 45 px wide
 // Stage 1 of one detection chunk (up to 8 steps of STEP rows per lane, two steps per LDS round
@@ -1125,63 +1151,43 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
 // ORBextractor::DistributeOctTree (ORBextractor.cc:525-733) for one (image, level) per
 // workgroup.  The std::list is represented by node arrays kept in list order in LDS:
 // a division pass pushes children to the front, so after each step the order is
-// [children, newest seq first] + [undivided nodes, previous order].  Keys keep
-// candidate order inside every node (DivideNode is a stable partition), so a node's retained
-// key is its max response with the lowest candidate index.  The final-refinement sort uses the
+// [children, newest seq first] + [undivided nodes, previous order].  A node's
+// retained key is its max response with the lowest candidate index (DivideNode is a stable
+// partition, so a node's keys stay in candidate order).  The final-refinement sort uses the
 // canonical (size, creation sequence) tie-break.
-constexpr int kOctNT = 256;           // threads per (image, level) workgroup, and
-constexpr int kOctNTBig = 1024;       // for frames whose level-0 octree frame exceeds
-constexpr int kOctBigArea = 1 << 20;  // kOctBigArea px: a workgroup holds ~100 KB of LDS there
-                                      // (one per CU), so 1024 threads run its key passes 4x wide
-constexpr int kOctRegKeys = 16;       // keys per thread per register chunk
-constexpr int kOctBatch = 8;          // node-info loads in flight per key pass round
+//
+// Counting by bins instead of key passes.  A node's division is fixed by its rectangle (the
+// ceil midpoints of DivideNode, ORBextractor.cc:472-473), so every key's path down the tree —
+// its quadrant digit at each depth below a node — is known in advance.  A refine sweep gives
+// every node that may still divide (> 1 key) a block of 4^R bins, one per R-digit path below
+// it, and every other node one bin; each key adds itself to the bin of its path, and the bins'
+// prefix sums then give the key count of every descendant down to R levels as the difference
+// of two sums (a node's bin range splits into four quarters, one per child).  Passes only touch
+// node arrays; the keys are swept again only when a node that may divide has no digit left
+// (at most a few times per level, usually once), and once at the end to retain the best key of
+// each node (a key's node = the node whose bin range holds the key's bin).
+// Threads per (image, level) workgroup: 256, or 1024 for levels whose octree frame exceeds
+// kOctBigArea px (a workgroup holds ~130 KB of LDS there, one per CU, and its key sweeps run 16
+// waves wide).
+constexpr int kOctNT = 256, kOctNTBig = 1024;
+constexpr int64_t kOctBigArea = 1 << 20;
+constexpr int kOctRegKeys = 8;        // keys per thread per register chunk
+constexpr int kOctBins = 1024;        // bins per (image, level) at least: batch plans,
+constexpr int kOctBinsFew = 8192;     // few-image plans and the 1024-thread instance
 constexpr size_t kOctMaxSmem = 150 * 1024;  // dynamic LDS of one octree workgroup
 
-struct OctNodes {
-  int16_t *x0, *x1, *y0, *y1;
-  int *cnt, *seq;
-};
-
-// A node's split point packed for the key passes (one LDS load per key): xm in bits 0-15, ym in
-// 16-30 (levels are < 32768 px), bit 31 set when the node holds more than one key
-__device__ __forceinline__ uint32_t node_info(int cnt, int x0, int x1, int y0, int y1) {
-  const int xm = x0 + (x1 - x0 + 1) / 2;  // ceil((float)(UR.x-UL.x)/2)
-  const int ym = y0 + (y1 - y0 + 1) / 2;
-  return (cnt > 1 ? 0x80000000u : 0u) | (uint32_t)xm | ((uint32_t)ym << 16);
-}
-
-// quadrant of a key in its node: 0 UL, 1 UR, 2 BL, 3 BR (DivideNode, ORBextractor.cc:487-522)
-template <class K>
-__device__ __forceinline__ int quad_of(K key, uint32_t info) {
-  const int x = KeyFmt<K>::x(key), y = KeyFmt<K>::y(key);
-  return (x >= (int)(info & 0xFFFFu)) | ((y >= (int)((info >> 16) & 0x7FFFu)) << 1);
-}
-
-struct OctCtx {
-  OctNodes A, B;
-  int *cc, *t1, *t2, *t3, *t4, *s_tmp, *s_misc;
-  uint32_t* ninfo;  // node_info() of the current nodes
-  uint64_t *pk, *s_tmp64;
-  void* outk;  // K[] of the level's retained keys
-  int* oc;
-};
-
-// Where the octree keeps its keys (KeyFmt<K>) and their node labels.  Thread t
-// owns keys t, t + NT, t + 2 NT, ... (NT threads); they are processed in chunks of kOctRegKeys
-// held in registers, slot r of chunk c being key t + NT (c kOctRegKeys + r).
-//   RegKeys<NT>: one chunk (n <= kOctRegKeys NT): keys and labels stay in registers for the
-//                whole tree, and the quadrant of each key is kept from the count pass to the
-//                relabel pass;
-//   MemKeys<NT>: larger levels, keys and labels in global scratch (L2-resident): every pass
-//                loads a chunk with all its loads in flight, works on the registers and stores
-//                the labels back (one load latency per chunk instead of one per key).
+// Where the octree keeps its keys (KeyFmt<K>) and their bins.  Thread t owns keys t, t + NT,
+// t + 2 NT, ... (NT threads); they are processed in chunks of kOctRegKeys held in registers,
+// slot r of chunk c being key t + NT (c kOctRegKeys + r).
+//   RegKeys<NT>: one chunk (n <= kOctRegKeys NT): keys and bins stay in registers;
+//   MemKeys<NT>: larger levels, keys and bins in global scratch (L2-resident): a sweep loads a
+//                chunk with all its loads in flight, works on the registers and stores the bins
+//                back (one load latency per chunk instead of one per key).
 template <int NT, class K>
 struct RegKeys {
   using Key = K;
-  static constexpr bool kRegs = true;
   K key[kOctRegKeys];
   int lab[kOctRegKeys];
-  uint32_t q2 = 0;  // 2 bits per key: quadrant inside its node (valid when the node splits)
   int n;
   __device__ int nchunks() const { return 1; }
   __device__ void load(int, bool) {}
@@ -1189,14 +1195,11 @@ struct RegKeys {
   __device__ K get_key(int r) const { return key[r]; }
   __device__ int get_lab(int r) const { return lab[r]; }
   __device__ void set_lab(int r, int v) { lab[r] = v; }
-  __device__ void set_q(int r, int q) { q2 = (q2 & ~(3u << (2 * r))) | ((uint32_t)q << (2 * r)); }
-  __device__ int get_q(int r, uint32_t) const { return (q2 >> (2 * r)) & 3; }
 };
 
 template <int NT, class K>
 struct MemKeys {
   using Key = K;
-  static constexpr bool kRegs = false;
   K* keys;
   int* labs;
   int n;
@@ -1221,14 +1224,15 @@ struct MemKeys {
   __device__ K get_key(int r) const { return key[r]; }
   __device__ int get_lab(int r) const { return lab[r]; }
   __device__ void set_lab(int r, int v) { lab[r] = v; }
-  __device__ void set_q(int, int) {}
-  __device__ int get_q(int r, uint32_t info) const { return quad_of(key[r], info); }
 };
 
-// every key of this thread: f(r, k) for key k < n in register slot r; `want_labs` loads a
-// chunk's labels with its keys, `labs_out` stores them back after it (MemKeys only)
-template <int NT, class KS, class F>
-__device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, F f) {
+// every key of this thread: f(r, k) for key k < n in register slot r, then g(r, k) for every
+// such key of the chunk.  f only reads LDS (the loads of all slots overlap); g holds the LDS
+// atomics, which would otherwise order every slot's loads behind the previous slot's atomic.
+// `want_labs` loads a chunk's bins with its keys, `labs_out` stores them back after it
+// (MemKeys only).
+template <int NT, class KS, class F, class G>
+__device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, F f, G g) {
   const int nc = ks.nchunks();
   for (int c = 0; c < nc; c++) {
     ks.load(c, want_labs);
@@ -1237,115 +1241,283 @@ __device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, 
       const int k = threadIdx.x + NT * (c * kOctRegKeys + r);
       if (k < ks.n) f(r, k);
     }
+#pragma unroll
+    for (int r = 0; r < kOctRegKeys; r++) {
+      const int k = threadIdx.x + NT * (c * kOctRegKeys + r);
+      if (k < ks.n) g(r, k);
+    }
     if (labs_out) ks.store_labs(c);
   }
 }
 
-// What a key of node i becomes after a pass: its new label is base - pre[q], pre[q] = the node's
-// non-empty quadrants before the key's quadrant q (children are pushed in quadrant order); bits
-// 2q..2q+1 hold pre[q] (pre[0] = 0), zero for a node that is not divided, and bits 8- the base
-__device__ __forceinline__ int relabel_info(int base, int divided, const int* ccn) {
-  if (!divided) return base << 8;
-  const int p1 = ccn[0] > 0, p2 = p1 + (ccn[1] > 0), p3 = p2 + (ccn[2] > 0);
-  return (base << 8) | (p1 << 2) | (p2 << 4) | (p3 << 6);
+// ---- node storage, shared steps
+struct OctNodes {
+  int *rx, *ry;  // x0 | x1 << 16 and y0 | y1 << 16: the node's [x0, x1) x [y0, y1) (< 32768 px)
+  int *cnt, *seq;
+  // first bin << 9 | depth << 4 | digits left: the node's bins are [first, first + 4^digits)
+  int* bl;
+};
+__device__ __forceinline__ int lo16(int v) { return v & 0xFFFF; }
+__device__ __forceinline__ int hi16(int v) { return (int)((uint32_t)v >> 16); }
+
+struct OctCtx {
+  OctNodes A, B;
+  int *cc, *t1, *t2, *t3, *t4, *s_tmp, *s_misc;
+  int* bins;   // [bin_cap + 8]: keys per bin, then their exclusive prefix sums
+  int* table;  // [bin_cap + 8]: bin -> node position (forward-filled from each node's first bin)
+  int bin_cap;
+  uint64_t *pk, *s_tmp64;
+  void* outk;  // K[] of the level's retained keys
+  int* oc;
+  const uint32_t *px, *py;  // the level's quadrant paths (Geometry::octpath)
+};
+
+// Per-thread chunks of whole int4s over [0, M) (bin arrays are 16-B aligned): [beg, end)
+template <int NT>
+__device__ __forceinline__ void int4_chunk(int M, int& beg, int& end) {
+  const int per = ((M + NT - 1) / NT + 3) & ~3;
+  beg = min((int)threadIdx.x * per, M);
+  end = min(beg + per, M);
 }
 
+// exclusive scan of a bin array a[0..M) in place, four bins per LDS access
+template <int NT>
+__device__ int bins_scan_excl(int* a, int M, int* s_tmp) {
+  int beg, end;
+  int4_chunk<NT>(M, beg, end);
+  int sum = 0, i = beg;
+  for (; i + 4 <= end; i += 4) {
+    const int4 v = *(const int4*)(a + i);
+    sum += v.x + v.y + v.z + v.w;
+  }
+  for (; i < end; i++) sum += a[i];
+  int total;
+  int run = grp_excl<NT>(sum, s_tmp, total);
+  for (i = beg; i + 4 <= end; i += 4) {
+    const int4 v = *(const int4*)(a + i);
+    int4 o;
+    o.x = run; run += v.x;
+    o.y = run; run += v.y;
+    o.z = run; run += v.z;
+    o.w = run; run += v.w;
+    *(int4*)(a + i) = o;
+  }
+  for (; i < end; i++) {
+    const int x = a[i];
+    a[i] = run;
+    run += x;
+  }
+  __syncthreads();
+  return total;
+}
+
+// table[b] = the node whose bin range holds bin b: each node's first bin marked, then every
+// thread's chunk forward-filled from the last mark before it (bins of dropped empty children
+// take their predecessor's node; no key lies in them)
+template <int NT>
+__device__ void oct_fill_table(int* table, const OctNodes& cur, int size, int gen_total,
+                               int* s_tmp) {
+  int beg, end;
+  int4_chunk<NT>(gen_total, beg, end);
+  int i = beg;
+  for (; i + 4 <= end; i += 4) *(int4*)(table + i) = make_int4(-1, -1, -1, -1);
+  for (; i < end; i++) table[i] = -1;
+  __syncthreads();
+  for (int k = threadIdx.x; k < size; k += NT) table[cur.bl[k] >> 9] = k;
+  __syncthreads();
+  int last = -1;
+  for (i = beg; i + 4 <= end; i += 4) {
+    const int4 v = *(const int4*)(table + i);
+    last = v.w >= 0 ? i + 3 : v.z >= 0 ? i + 2 : v.y >= 0 ? i + 1 : v.x >= 0 ? i : last;
+  }
+  for (; i < end; i++)
+    if (table[i] >= 0) last = i;
+  const int carry = block_max_excl<NT>(last, s_tmp);
+  int nd = carry >= 0 ? table[carry] : -1;
+  for (i = beg; i + 4 <= end; i += 4) {
+    int4 v = *(const int4*)(table + i);
+    v.x = v.x >= 0 ? (nd = v.x) : nd;
+    v.y = v.y >= 0 ? (nd = v.y) : nd;
+    v.z = v.z >= 0 ? (nd = v.z) : nd;
+    v.w = v.w >= 0 ? (nd = v.w) : nd;
+    *(int4*)(table + i) = v;
+  }
+  for (; i < end; i++) {
+    const int v = table[i];
+    if (v >= 0) nd = v;
+    else table[i] = nd;
+  }
+  __syncthreads();
+}
+
+// initial nodes (ORBextractor.cc:530-567): the keys' first bins are their initial node
+// indices; the non-empty nodes go to X.B in order with one bin each.  Returns their count.
 template <int NT, class KS>
-__device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, KS& ks,
-                                            const typename KS::Key* keys_mem) {
+__device__ int oct_initial(const LevelGeom& G, const OctCtx& X, KS& ks) {
   using K = typename KS::Key;
-  const int tid = threadIdx.x;
-  const int n = ks.n;
-  OctNodes A = X.A, B = X.B;
-  int *cc = X.cc, *t1 = X.t1, *t2 = X.t2, *t3 = X.t3, *t4 = X.t4, *s_tmp = X.s_tmp,
-      *s_misc = X.s_misc;
-  K* outk = (K*)X.outk;
-  int* oc = X.oc;
-  // 2. initial nodes (ORBextractor.cc:530-567)
-  const int nini = G.nini;
+  const int tid = threadIdx.x, nini = G.nini;
+  const OctNodes A = X.A, B = X.B;
   for (int i = tid; i < nini; i += NT) {
     // ni.UL / ni.UR = cv::Point2i(hX * (float)i, 0): the float product truncated (:540-544)
-    A.x0[i] = (int16_t)(int)(G.hx * static_cast<float>(i));
-    A.x1[i] = (int16_t)(int)(G.hx * static_cast<float>(i + 1));
-    A.y0[i] = 0;
-    A.y1[i] = (int16_t)G.H;
+    A.rx[i] = (int)(G.hx * static_cast<float>(i)) | ((int)(G.hx * static_cast<float>(i + 1)) << 16);
+    A.ry[i] = G.H << 16;
     A.cnt[i] = 0;
     A.seq[i] = i;
   }
   __syncthreads();
-  each_key<NT>(ks, false, true, [&](int j, int) {
-    const float x = (float)KeyFmt<K>::x(ks.get_key(j));
-    const int ni = min((int)(x / G.hx), nini - 1);
-    ks.set_lab(j, ni);
-    atomicAdd(&A.cnt[ni], 1);
-  });
+  each_key<NT>(
+      ks, false, true,
+      [&](int j, int) {
+        const float x = (float)KeyFmt<K>::x(ks.get_key(j));
+        ks.set_lab(j, min((int)(x / G.hx), nini - 1));
+      },
+      [&](int j, int) { atomicAdd(&A.cnt[ks.get_lab(j)], 1); });
   __syncthreads();
   // drop empty initial nodes, keep order
-  for (int i = tid; i < nini; i += NT) t1[i] = A.cnt[i] > 0;
+  for (int i = tid; i < nini; i += NT) X.t1[i] = A.cnt[i] > 0;
   __syncthreads();
-  int size = block_scan_excl<NT>(t1, nini, s_tmp);
+  const int size = block_scan_excl<NT>(X.t1, nini, X.s_tmp);
   for (int i = tid; i < nini; i += NT)
     if (A.cnt[i] > 0) {
-      const int j = t1[i];
-      B.x0[j] = A.x0[i]; B.x1[j] = A.x1[i]; B.y0[j] = A.y0[i]; B.y1[j] = A.y1[i];
+      const int j = X.t1[i];
+      B.rx[j] = A.rx[i]; B.ry[j] = A.ry[i];
       B.cnt[j] = A.cnt[i]; B.seq[j] = A.seq[i];
+      B.bl[j] = i << 9;
     }
   __syncthreads();
-  each_key<NT>(ks, true, true, [&](int j, int) { ks.set_lab(j, t1[ks.get_lab(j)]); });
+  return size;
+}
+
+// A new generation of bins: R digits below every node with > 1 key, one bin for the others
+// (R as large as the bin capacity allows, capped near the key count: the bins are scanned and
+// filled per refine, so a refine costs O(bins + keys)).
+template <int NT, class KS>
+__device__ void oct_refine(const OctCtx& X, KS& ks, const OctNodes& cur, int size,
+                           int& gen_total) {
+  using K = typename KS::Key;
+  const int tid = threadIdx.x;
+  int *t2 = X.t2, *t3 = X.t3, *bins = X.bins, *table = X.table;
+  oct_fill_table<NT>(table, cur, size, gen_total, X.s_tmp);
+  int act = 0;
+  for (int i = tid; i < size; i += NT) {
+    const int a = cur.cnt[i] > 1;
+    t2[i] = a;
+    act += a;
+  }
+  const int nact = block_sum<NT>(act, X.s_tmp);
+  const int nin = size - nact;
+  const int lim = min(X.bin_cap, max(4 * size, ks.n));
+  int R = 1;
+  while (R < 15 && nin + ((int64_t)nact << (2 * (R + 1))) <= lim) R++;
+  for (int i = tid; i < size; i += NT) t3[i] = t2[i] ? 1 << (2 * R) : 1;
   __syncthreads();
-  OctNodes cur = B, nxt = A;
-  int seqc = nini;
+  gen_total = block_scan_excl<NT>(t3, size, X.s_tmp);  // t3: each node's first new bin
+  for (int i = 4 * tid; i <= gen_total; i += 4 * NT) *(int4*)(bins + i) = make_int4(0, 0, 0, 0);
+  __syncthreads();
+  each_key<NT>(
+      ks, true, true,
+      [&](int j, int) {
+        const int nd = table[ks.get_lab(j)];
+        int b = t3[nd];
+        if (t2[nd]) {  // the key's quadrant digits below its node (DivideNode, :487-522)
+          const K key = ks.get_key(j);
+          const uint64_t path =
+              (uint64_t)(X.px[KeyFmt<K>::x(key)] | X.py[KeyFmt<K>::y(key)]) << 32;
+          const int sh = 2 * (32 - ((cur.bl[nd] >> 4) & 31) - R);  // < 0: below depth 32, 0s
+          b += sh >= 0 ? (int)((path >> sh) & ((1u << (2 * R)) - 1)) : 0;
+        }
+        ks.set_lab(j, b);
+      },
+      [&](int j, int) { atomicAdd(&bins[ks.get_lab(j)], 1); });
+  __syncthreads();
+  bins_scan_excl<NT>(bins, gen_total + 1, X.s_tmp);
+  for (int i = tid; i < size; i += NT)
+    cur.bl[i] = (t3[i] << 9) | (cur.bl[i] & (31 << 4)) | (t2[i] ? R : 0);
+  __syncthreads();
+}
+
+// 3. retain the best key per node (max response, first in candidate order)
+template <int NT, class KS>
+__device__ void oct_retain(const OctCtx& X, KS& ks, const OctNodes& cur, int size,
+                           int gen_total, const typename KS::Key* keys_mem) {
+  using K = typename KS::Key;
+  const int tid = threadIdx.x;
+  oct_fill_table<NT>(X.table, cur, size, gen_total, X.s_tmp);
+  unsigned* best = (unsigned*)X.t1;
+  for (int i = tid; i < size; i += NT) best[i] = 0;
+  __syncthreads();
+  each_key<NT>(
+      ks, true, false, [&](int j, int) { ks.set_lab(j, X.table[ks.get_lab(j)]); },
+      [&](int j, int k) {
+        atomicMax(&best[ks.get_lab(j)],
+                  (KeyFmt<K>::score(ks.get_key(j)) << 24) | (0xFFFFFFu - (unsigned)k));
+      });
+  __syncthreads();
+  K* outk = (K*)X.outk;
+  for (int i = tid; i < size; i += NT) {
+    // every node holds a key; the clamp only keeps a broken invariant from reading past them
+    const int k = min((int)(0xFFFFFFu - (best[i] & 0xFFFFFFu)), ks.n - 1);
+    outk[i] = keys_mem[k];
+  }
+  if (tid == 0) *X.oc = size;
+}
+
+// A divided node's children into the next list (nxt): the non-empty quadrants in order at
+// base, base - 1, ..., sequence numbers seq0, seq0 + 1, ..., each with its quarter of the
+// parent's bin range
+__device__ __forceinline__ void oct_push_children(const OctNodes& nxt, int rx, int ry, int bl,
+                                                  const int (&c)[4], int base, int seq0) {
+  const int x0 = lo16(rx), x1 = hi16(rx), y0 = lo16(ry), y1 = hi16(ry);
+  const int xm = x0 + (x1 - x0 + 1) / 2, ym = y0 + (y1 - y0 + 1) / 2;
+  const int ls = (bl & 15) - 1, s4 = 1 << (2 * ls);
+  int j = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    if (c[q] > 0) {
+      const int pos = base - j;
+      nxt.rx[pos] = (q & 1) ? (xm | (x1 << 16)) : (x0 | (xm << 16));
+      nxt.ry[pos] = (q & 2) ? (ym | (y1 << 16)) : (y0 | (ym << 16));
+      nxt.cnt[pos] = c[q];
+      nxt.seq[pos] = seq0 + j;
+      nxt.bl[pos] = (((bl >> 9) + q * s4) << 9) | min((bl & (31 << 4)) + (1 << 4), 31 << 4) | ls;
+      j++;
+    }
+  }
+}
+
+// ---- the passes, workgroup form (256 / 1024 threads): node arrays in LDS, one barrier per step
+template <int NT, class KS>
+__device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, KS& ks,
+                                            const typename KS::Key* keys_mem) {
+  const int tid = threadIdx.x;
+  int *cc = X.cc, *t1 = X.t1, *t2 = X.t2, *t3 = X.t3, *t4 = X.t4, *s_tmp = X.s_tmp,
+      *s_misc = X.s_misc, *bins = X.bins;
+  int size = oct_initial<NT>(G, X, ks);
+  OctNodes cur = X.B, nxt = X.A;
+  int gen_total = G.nini;  // bins of the current generation
+  int seqc = G.nini;
   bool final_mode = false;
   const int N = G.nfeat;
   for (int iter = 0; iter < 4096; iter++) {
     const int prevSize = size;
-    for (int i = tid; i < 4 * size; i += NT) cc[i] = 0;
-    for (int i = tid; i < size; i += NT)
-      X.ninfo[i] = node_info(cur.cnt[i], cur.x0[i], cur.x1[i], cur.y0[i], cur.y1[i]);
-    __syncthreads();
-    // quadrant counts; keys are in cell order, so a wave's keys usually share one node and the
-    // four counts are added with one atomic each instead of one per key
-    const int lane = tid & 63;
-    auto count_one = [&](int j, int k, uint32_t info) {
-      int nd = -1, q = -1;
-      if (k < n) {
-        nd = ks.get_lab(j);
-        if (info >> 31) {
-          q = quad_of(ks.get_key(j), info);
-          ks.set_q(j, q);
-        }
-      }
-      const uint64_t act = __ballot(q >= 0);
-      if (!act) return;
-      const int first = __builtin_ctzll(act);
-      const int ndf = __shfl(nd, first);
-      if (__ballot(q >= 0 && nd != ndf) == 0) {
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-          const int c = __popcll(__ballot(q == jj));
-          if (lane == first && c) atomicAdd(&cc[4 * ndf + jj], c);
-        }
-      } else if (q >= 0) {
-        atomicAdd(&cc[4 * nd + q], 1);
-      }
-    };
-    // every lane runs every slot (the ballots need the whole wave); a chunk's node infos are
-    // loaded together before its first atomic, one LDS latency per chunk instead of per key
-    for (int c = 0; c < ks.nchunks(); c++) {
-      ks.load(c, true);
-#pragma unroll
-      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
-        uint32_t inf[kOctBatch];
-#pragma unroll
-        for (int j = 0; j < kOctBatch; j++)
-          inf[j] = tid + NT * (c * kOctRegKeys + j0 + j) < n ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
-#pragma unroll
-        for (int j = 0; j < kOctBatch; j++)
-          count_one(j0 + j, tid + NT * (c * kOctRegKeys + j0 + j), inf[j]);
+    // a node that may divide with no digit left in its bin block: new bins first
+    int need = 0;
+    for (int i = tid; i < size; i += NT) need |= cur.cnt[i] > 1 && (cur.bl[i] & 15) == 0;
+    if (block_sum<NT>(need, s_tmp)) oct_refine<NT>(X, ks, cur, size, gen_total);
+    // quadrant counts of the nodes that may divide: the four quarters of their bin ranges
+    for (int i = tid; i < size; i += NT) {
+      if (cur.cnt[i] > 1) {
+        const int bl = cur.bl[i], b = bl >> 9, s4 = 1 << (2 * ((bl & 15) - 1));
+        const int e0 = bins[b], e1 = bins[b + s4], e2 = bins[b + 2 * s4], e3 = bins[b + 3 * s4],
+                  e4 = bins[b + 4 * s4];
+        cc[4 * i] = e1 - e0;
+        cc[4 * i + 1] = e2 - e1;
+        cc[4 * i + 2] = e3 - e2;
+        cc[4 * i + 3] = e4 - e3;
       }
     }
     __syncthreads();
-    int T, newSize, nToExpand;
+    int T, newSize, nToExpand = 0;
     if (!final_mode) {
       // outer pass (list order): one packed scan gives childPre (bits 0-19), the rank among
       // undivided nodes (20-39) and the total of children with > 1 key (40-)
@@ -1373,13 +1545,10 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         const uint64_t e = pk[i];
         const int pre = (int)(e & 0xFFFFF), ndr = (int)((e >> 20) & 0xFFFFF);
         t1[i] = pre;
-        const int base = t2[i] ? T - 1 - pre : T + ndr;
-        t4[i] = base;
-        t3[i] = relabel_info(base, t2[i], cc + 4 * i);
+        t4[i] = t2[i] ? T - 1 - pre : T + ndr;
       }
       __syncthreads();
     } else {
-      int nexp_local = 0;
       for (int i = tid; i < size; i += NT) {
         const bool e = cur.cnt[i] > 1;
         int ne = 0;
@@ -1389,7 +1558,6 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         }
         t1[i] = ne;
       }
-      nToExpand = block_sum<NT>(nexp_local, s_tmp);
       // final refinement: visit expandable nodes by (size desc, seq desc).  A node's rank is
       // the number of expandable nodes with a larger (size, seq) key; the keys are packed once
       // into pk (size << 32 | seq, 0 for nodes that do not expand) so the all-pairs count is one
@@ -1420,8 +1588,7 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       __syncthreads();
       if (tid == 0) s_misc[0] = E > 0 ? E - 1 : -1;
       __syncthreads();
-      const int Tall = block_scan_excl<NT>(t2, E, s_tmp);
-      (void)Tall;
+      block_scan_excl<NT>(t2, E, s_tmp);
       // cut = first v with size + childPre_v + ne_v - (v+1) >= N
       for (int v = tid; v < E; v += NT) {
         const int ne = t1[t3[v]];
@@ -1437,9 +1604,8 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         newSize = size;
       }
       __syncthreads();
-      // divided flag & childPre per node: reuse t1 (keep nonEmpty in cc) -> store childPre
-      // in t1 for divided nodes; t2 becomes divided flag per node (indexed by node).
-      // First move childPre (indexed by v) into a per-node array (t4 holds rank).
+      // divided flag & childPre per node: t4 holds the rank; childPre (indexed by rank in t2)
+      // moves to a per-node array in t1, t2 becomes the divided flag per node
       for (int i = tid; i < size; i += NT) {
         const bool e = cur.cnt[i] > 1;
         const int r = e ? t4[i] : -1;
@@ -1456,62 +1622,21 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         t3[i] = !(t4[i] >= 0);
       }
       __syncthreads();
-      const int nd_total = block_scan_excl<NT>(t3, size, s_tmp);
-      (void)nd_total;
-      for (int i = tid; i < size; i += NT) {
-        const int base = t2[i] ? T - 1 - t1[i] : T + t3[i];
-        t4[i] = base;
-        t3[i] = relabel_info(base, t2[i], cc + 4 * i);
-      }
+      block_scan_excl<NT>(t3, size, s_tmp);
+      for (int i = tid; i < size; i += NT) t4[i] = t2[i] ? T - 1 - t1[i] : T + t3[i];
       __syncthreads();
     }
-    // write next node arrays: t2 = divided, t1 = childPre, t4 = base, t3 = relabel_info
+    // write next node arrays: t2 = divided, t1 = childPre, t4 = base
     for (int i = tid; i < size; i += NT) {
       if (t2[i]) {
-        const int x0 = cur.x0[i], x1 = cur.x1[i], y0 = cur.y0[i], y1 = cur.y1[i];
-        const int xm = x0 + (x1 - x0 + 1) / 2, ym = y0 + (y1 - y0 + 1) / 2;
-        int j = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int c = cc[4 * i + q];
-          if (c > 0) {
-            const int pos = t4[i] - j;
-            nxt.x0[pos] = (int16_t)((q & 1) ? xm : x0);
-            nxt.x1[pos] = (int16_t)((q & 1) ? x1 : xm);
-            nxt.y0[pos] = (int16_t)((q & 2) ? ym : y0);
-            nxt.y1[pos] = (int16_t)((q & 2) ? y1 : ym);
-            nxt.cnt[pos] = c;
-            nxt.seq[pos] = seqc + t1[i] + j;
-            j++;
-          }
-        }
+        const int c[4] = {cc[4 * i], cc[4 * i + 1], cc[4 * i + 2], cc[4 * i + 3]};
+        oct_push_children(nxt, cur.rx[i], cur.ry[i], cur.bl[i], c, t4[i], seqc + t1[i]);
       } else {
         const int pos = t4[i];
-        nxt.x0[pos] = cur.x0[i]; nxt.x1[pos] = cur.x1[i];
-        nxt.y0[pos] = cur.y0[i]; nxt.y1[pos] = cur.y1[i];
+        nxt.rx[pos] = cur.rx[i]; nxt.ry[pos] = cur.ry[i];
         nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
+        nxt.bl[pos] = cur.bl[i];
       }
-    }
-    // relabel keys: a chunk's relabel infos (and, for keys in memory, node infos) in one round
-    // of loads
-    for (int c = 0; c < ks.nchunks(); c++) {
-      ks.load(c, true);
-#pragma unroll
-      for (int j0 = 0; j0 < kOctRegKeys; j0 += kOctBatch) {
-        uint32_t rl[kOctBatch], inf[kOctBatch];
-#pragma unroll
-        for (int j = 0; j < kOctBatch; j++) {
-          const bool v = tid + NT * (c * kOctRegKeys + j0 + j) < n;
-          rl[j] = v ? (uint32_t)t3[ks.get_lab(j0 + j)] : 0u;
-          inf[j] = (!KS::kRegs && v) ? X.ninfo[ks.get_lab(j0 + j)] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kOctBatch; j++)
-          if (tid + NT * (c * kOctRegKeys + j0 + j) < n)
-            ks.set_lab(j0 + j, (int)(rl[j] >> 8) -
-                                   (int)((rl[j] >> (2 * ks.get_q(j0 + j, inf[j]))) & 3u));
-      }
-      ks.store_labs(c);
     }
     __syncthreads();
     {
@@ -1528,27 +1653,12 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
       if (size >= N || size == prevSize) break;
     }
   }
-  // 3. retain the best key per node (max response, first in candidate order)
-  unsigned* best = (unsigned*)t1;
-  for (int i = tid; i < size; i += NT) best[i] = 0;
-  __syncthreads();
-  each_key<NT>(ks, true, false, [&](int j, int k) {
-    const K key = ks.get_key(j);
-    atomicMax(&best[ks.get_lab(j)], (KeyFmt<K>::score(key) << 24) | (0xFFFFFFu - (unsigned)k));
-  });
-  __syncthreads();
-  for (int i = tid; i < size; i += NT) {
-    const int k = (int)(0xFFFFFFu - (best[i] & 0xFFFFFFu));
-    outk[i] = keys_mem[k];
-  }
-  if (tid == 0) *oc = size;
+  oct_retain<NT>(X, ks, cur, size, gen_total, keys_mem);
 }
 
-
-// 256-thread instances: at least 6 waves per SIMD (the compiler's choice was 104 VGPRs, 4 waves;
-// 6 costs a few spilled registers and took C2's octree 0.154 -> 0.124 ms per 512 frames; 7 / 8
-// spill more and were slower); the 1024-thread instance keeps its registers (a cap slowed C5's
-// level-0 trees).
+// 256-thread instances: 6 waves per SIMD (80 VGPRs; a few spill, but C2's octree took 0.120
+// vs 0.128 ms per 512 frames against 4 waves without spills); the 1024-thread instance keeps
+// its registers.
 constexpr int kOctWaves = 6;
 template <int NT, class K>
 __global__ __launch_bounds__(NT)
@@ -1558,7 +1668,7 @@ void k_octree(
     const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
     K* __restrict__ lin, int* __restrict__ label, K* __restrict__ okey,
     int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
-    int level_base, int* __restrict__ cell_scr) {
+    int bin_cap, int level_base, int* __restrict__ cell_scr, const uint32_t* __restrict__ octpath) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_tmp[NT / 64 + 1];
   __shared__ int s_misc[8];
@@ -1580,23 +1690,25 @@ void k_octree(
     return r;
   };
   OctNodes A, B;
-  A.x0 = (int16_t*)take(2 * NC); A.x1 = (int16_t*)take(2 * NC);
-  A.y0 = (int16_t*)take(2 * NC); A.y1 = (int16_t*)take(2 * NC);
-  A.cnt = (int*)take(4 * NC); A.seq = (int*)take(4 * NC);
-  B.x0 = (int16_t*)take(2 * NC); B.x1 = (int16_t*)take(2 * NC);
-  B.y0 = (int16_t*)take(2 * NC); B.y1 = (int16_t*)take(2 * NC);
-  B.cnt = (int*)take(4 * NC); B.seq = (int*)take(4 * NC);
+  for (OctNodes* L : {&A, &B}) {
+    L->rx = (int*)take(4 * NC); L->ry = (int*)take(4 * NC);
+    L->cnt = (int*)take(4 * NC); L->seq = (int*)take(4 * NC); L->bl = (int*)take(4 * NC);
+  }
   int* cc = (int*)take(16 * NC);
   int* t1 = (int*)take(4 * NC);
   int* t2 = (int*)take(4 * NC);
   int* t3 = (int*)take(4 * NC);
   int* t4 = (int*)take(4 * NC);
-  uint32_t* ninfo = (uint32_t*)take(4 * NC);
-  // per-cell key starts and slots: in LDS, or (cell_cap == 0: levels with too many cells for
-  // it) in this (image, level)'s part of cell_scr, [2 (ncells + nlevels)] ints per image
+  uint64_t* pk = (uint64_t*)take(8 * (NC + 1));
+  // one region for the gather's per-cell key starts and slots and, after it, the bins and
+  // their node table.  Cells: in LDS, or (cell_cap == 0: levels with too many cells for it)
+  // in this (image, level)'s part of cell_scr, [2 (ncells + nlevels)] ints per image
+  unsigned char* region = p;
+  int* bins = (int*)take(4 * (bin_cap + 8));
+  int* table = (int*)take(4 * (bin_cap + 8));
+  p = region;
   int* cpre = cell_cap > 0 ? (int*)take(4 * (cell_cap + 1))
                            : cell_scr + (int64_t)img * 2 * (ncells + nlevels) + 2 * (G.cell_begin + level);
-  uint64_t* pk = (uint64_t*)take(8 * NC);
   int* s_slot = cell_cap > 0 ? (int*)take(4 * cell_cap) : cpre + G.ncells + 1;
   __shared__ uint64_t s_tmp64[NT / 64 + 1];
 
@@ -1641,8 +1753,10 @@ void k_octree(
       v[j] = k < n ? cb[s_slot[c] + k - cpre[c]] : K(0);
     }
   };
-  OctCtx X{A, B, cc, t1, t2, t3, t4, s_tmp, s_misc, ninfo, pk, s_tmp64, outk, oc};
-  if (n <= kOctRegKeys * NT) {  // keys + labels in registers: every pass stays on-chip
+  // (the bins are first written by octree_core's refine, several barriers after the gather)
+  OctCtx X{A,    B,       cc,   t1, t2, t3, t4, s_tmp, s_misc, bins, table, bin_cap,
+           pk,   s_tmp64, outk, oc, octpath + G.path_x, octpath + G.path_y};
+  if (n <= kOctRegKeys * NT) {  // keys + bins in registers: every sweep stays on-chip
     RegKeys<NT, K> ks;
     ks.n = n;
     load_keys(0, ks.key);
@@ -1653,7 +1767,7 @@ void k_octree(
       if (k < n) keys[k] = ks.key[j];
     }
     octree_core<NT>(G, X, ks, keys);
-  } else {  // keys + labels in global scratch, processed in register chunks
+  } else {  // keys + bins in global scratch, swept in register chunks
     for (int k0 = 0; k0 < n; k0 += NT * kOctRegKeys) {
       K v[kOctRegKeys];
       load_keys(k0, v);
@@ -1822,6 +1936,7 @@ struct orbx_plan {
   int device = 0;
   hipStream_t stream = nullptr;
   LevelGeom* d_lv = nullptr;
+  uint32_t* d_octpath = nullptr;  // Geometry::octpath
   CellGeom* d_cells = nullptr;
   int2 *d_xtap = nullptr, *d_ytap = nullptr;
   BlurTile* d_tiles = nullptr;
@@ -1836,12 +1951,12 @@ struct orbx_plan {
   // counts, keypoints and descriptors share one allocation (d_counts is its base) so the
   // drop-in path brings a frame's results back with one copy
   size_t out_kps_off = 0, out_desc_off = 0, out_bytes = 0;
-  // k_octree: levels below oct_split (level area > kOctBigArea) run 1024-thread workgroups
-  // with LDS for oct_nc_big nodes / oct_cc_big cells, the rest 256-thread ones sized for
-  // theirs, so small levels no longer hold a whole CU each
-  int oct_split = 0;
-  size_t oct_smem = 0, oct_smem_big = 0;
-  int oct_nc = 1, oct_cc = 1, oct_nc_big = 1, oct_cc_big = 1;  // oct_cc* 0: cells in d_cell_scr
+  // k_octree instances (kOctNTBig, kOctNT threads): levels [lo, hi) each, with LDS for nc
+  // nodes, cc cells (0: the cell tables in d_cell_scr) and `bins` bins
+  struct OctInst {
+    int lo = 0, hi = 0, nc = 1, cc = 1, bins = 1;
+    size_t smem = 0;
+  } oct[2];
   int* d_cell_scr = nullptr;
   int cell_cap = 0;
   // k_fast_pairs: adjacent cell pairs; k_fast_cells: the other cells, in its <44,
@@ -2033,22 +2148,18 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
                          P->d_cell_counts, 1);
     pr.mark(P->stream, st_fcell);
   }
-  // levels [0, oct_split) on 1024-thread workgroups with the large LDS carve, the others on
-  // 256-thread ones sized for themselves (several per CU)
+  // levels by octree frame area: 1024-thread and 256-thread workgroups
   static_assert(kOctNTBig == 1024 && kOctNT == 256, "instance names");
-  if (P->oct_split > 0) note_kernel<K>("k_octree", "1024, ");
-  if (P->oct_split < L) note_kernel<K>("k_octree", "256, ");
-  if (P->oct_split > 0)
-    hipLaunchKernelGGL((k_octree<kOctNTBig, K>), dim3(n, P->oct_split), dim3(kOctNTBig),
-                       P->oct_smem_big, P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells,
-                       cand, g.cand_total, lin, P->d_label, okey, P->d_ocount,
-                       g.kp_total, L, P->oct_nc_big, P->oct_cc_big, 0, P->d_cell_scr);
-  if (P->oct_split < L) {
-    hipLaunchKernelGGL((k_octree<kOctNT, K>), dim3(n, L - P->oct_split), dim3(kOctNT), P->oct_smem,
-                       P->stream, P->d_lv, P->d_cell_counts, ncells, P->d_cells, cand,
-                       g.cand_total, lin, P->d_label, okey, P->d_ocount, g.kp_total, L,
-                       P->oct_nc, P->oct_cc, P->oct_split, P->d_cell_scr);
-  }
+  auto launch_oct = [&](auto kern, int nt, const orbx_plan::OctInst& o, const char* name) {
+    if (o.hi <= o.lo) return;
+    note_kernel<K>("k_octree", name);
+    hipLaunchKernelGGL(kern, dim3(n, o.hi - o.lo), dim3(nt), o.smem, P->stream, P->d_lv,
+                       P->d_cell_counts, ncells, P->d_cells, cand, g.cand_total, lin, P->d_label,
+                       okey, P->d_ocount, g.kp_total, L, o.nc, o.cc, o.bins, o.lo, P->d_cell_scr,
+                       P->d_octpath);
+  };
+  launch_oct(k_octree<kOctNTBig, K>, kOctNTBig, P->oct[0], "1024, ");
+  launch_oct(k_octree<kOctNT, K>, kOctNT, P->oct[1], "256, ");
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
@@ -2177,7 +2288,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc((char**)&P->d_okey, B * g.kp_total * ksz) || dalloc(&P->d_ocount, B * g.nlevels) ||
       dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_tall, cells_tall.size()) ||
       dalloc(&P->d_cells_big, cells_big.size()) ||
-      dalloc(&P->d_pairs, pairs.size()))
+      dalloc(&P->d_pairs, pairs.size()) || dalloc(&P->d_octpath, g.octpath.size()))
     return fail(ORBX_ENOMEM);
   {
     auto r256 = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -2194,6 +2305,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     return bytes ? hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) : hipSuccess;
   };
   if (up(P->d_lv, g.lv, sizeof(LevelGeom) * g.nlevels) ||
+      up(P->d_octpath, g.octpath.data(), 4 * g.octpath.size()) ||
       up(P->d_cells, g.cells.data(), sizeof(CellGeom) * g.cells.size()) ||
       up(P->d_xtap, g.xtap.data(), 4 * g.xtap.size()) ||
       up(P->d_ytap, g.ytap.data(), 4 * g.ytap.size()) ||
@@ -2206,48 +2318,52 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  auto oct_bytes = [&](size_t NC, size_t CC) {
-    return 2 * (4 * r16(2 * NC) + 2 * r16(4 * NC)) + r16(16 * NC) + 5 * r16(4 * NC) +
-           (CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0) + r16(8 * NC);
+  // node arrays (two lists of x0 x1 y0 y1 cnt seq bl), quadrant counts, four scratch arrays and
+  // the rank keys, then one region for the gather's cell tables or the bins + node table
+  auto oct_bytes = [&](size_t NC, size_t CC, size_t BC) {
+    return 2 * 5 * r16(4 * NC) + r16(16 * NC) + 4 * r16(4 * NC) + r16(8 * (NC + 1)) +
+           std::max(CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0, 2 * r16(4 * (BC + 8)));
   };
-  while (P->oct_split < g.nlevels && (int64_t)g.lv[P->oct_split].W * g.lv[P->oct_split].H > kOctBigArea)
-    P->oct_split++;
-  for (int l = 0; l < g.nlevels; l++) {
-    int& nc = l < P->oct_split ? P->oct_nc_big : P->oct_nc;
-    int& cc = l < P->oct_split ? P->oct_cc_big : P->oct_cc;
-    nc = std::max(nc, g.lv[l].node_cap);
-    cc = std::max(cc, g.lv[l].ncells);
+  // levels are in decreasing area: each instance takes a contiguous range
+  int inst_of[kMaxLevels];
+  for (int l = 0; l < g.nlevels; l++)
+    inst_of[l] = (int64_t)g.lv[l].W * g.lv[l].H > kOctBigArea ? 0 : 1;
+  for (int i = 0, l = 0; i < 2; i++) {
+    orbx_plan::OctInst& o = P->oct[i];
+    o.lo = l;
+    while (l < g.nlevels && inst_of[l] == i) {
+      o.nc = std::max(o.nc, g.lv[l].node_cap);
+      o.cc = std::max(o.cc, g.lv[l].ncells);
+      l++;
+    }
+    o.hi = l;
+    // bins: every refine gives each node with > 1 key at least one digit (4 bins) and needs
+    // the initial nodes' bins first, so at least 4 x the node capacity; more bins, fewer refine
+    // sweeps (few-image plans and the 1024-thread instance are not bound by LDS occupancy)
+    o.bins = std::max(4 * o.nc + 4, (i == 0 || max_batch <= kPyFewImages) ? kOctBinsFew : kOctBins);
+    // a level with more cells than fit beside its nodes keeps its cell table in global scratch
+    if (oct_bytes(o.nc, o.cc, o.bins) > kOctMaxSmem) o.cc = 0;
+    o.smem = o.hi > o.lo ? oct_bytes(o.nc, o.cc, o.bins) : 0;
+    if (o.smem > kOctMaxSmem) return fail(ORBX_EUNSUPPORTED);
   }
-  // a level with more cells than fit beside its nodes keeps its cell table in global scratch
-  if (oct_bytes(P->oct_nc, P->oct_cc) > kOctMaxSmem) P->oct_cc = 0;
-  if (oct_bytes(P->oct_nc_big, P->oct_cc_big) > kOctMaxSmem) P->oct_cc_big = 0;
-  if ((P->oct_cc == 0 || (P->oct_split && P->oct_cc_big == 0)) &&
-      dalloc(&P->d_cell_scr, B * 2 * (g.cells.size() + g.nlevels)))
+  bool cell_scr = false;
+  for (const orbx_plan::OctInst& o : P->oct) cell_scr |= o.hi > o.lo && o.cc == 0;
+  if (cell_scr && dalloc(&P->d_cell_scr, B * 2 * (g.cells.size() + g.nlevels)))
     return fail(ORBX_ENOMEM);
-  P->oct_smem = oct_bytes(P->oct_nc, P->oct_cc);
-  P->oct_smem_big = P->oct_split ? oct_bytes(P->oct_nc_big, P->oct_cc_big) : 0;
-  if (std::max(P->oct_smem, P->oct_smem_big) > kOctMaxSmem) return fail(ORBX_EUNSUPPORTED);
-  // keys and labels live in registers (up to kOctRegKeys * threads per level) or in global
+  // keys and their bins live in registers (up to kOctRegKeys * threads per level) or in global
   // scratch.  The dynamic-LDS attribute is per function and shared by every plan of the
   // process: only ever raised.
-  static size_t attr_small = 0, attr_big = 0;  // guarded by the resource lock
-  auto raise = [](const void* f32, const void* f64, size_t bytes) {
-    return hipFuncSetAttribute(f32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
-               hipSuccess &&
-           hipFuncSetAttribute(f64, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
-               hipSuccess;
-  };
-  if (P->oct_smem > attr_small) {
-    if (!raise((const void*)k_octree<kOctNT, uint32_t>, (const void*)k_octree<kOctNT, uint64_t>,
-               P->oct_smem))
-      return fail(ORBX_EDEVICE);
-    attr_small = P->oct_smem;
-  }
-  if (P->oct_smem_big > attr_big) {
-    if (!raise((const void*)k_octree<kOctNTBig, uint32_t>,
-               (const void*)k_octree<kOctNTBig, uint64_t>, P->oct_smem_big))
-      return fail(ORBX_EDEVICE);
-    attr_big = P->oct_smem_big;
+  static size_t attr[2] = {0, 0};  // guarded by the resource lock
+  const void* fns[2][2] = {
+      {(const void*)k_octree<kOctNTBig, uint32_t>, (const void*)k_octree<kOctNTBig, uint64_t>},
+      {(const void*)k_octree<kOctNT, uint32_t>, (const void*)k_octree<kOctNT, uint64_t>}};
+  for (int i = 0; i < 2; i++) {
+    if (P->oct[i].smem <= attr[i]) continue;
+    for (const void* f : fns[i])
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)P->oct[i].smem) != hipSuccess)
+        return fail(ORBX_EDEVICE);
+    attr[i] = P->oct[i].smem;
   }
   *out = P;
   return ORBX_OK;
@@ -2261,7 +2377,7 @@ int orbx_plan_destroy(orbx_plan* P) {
                   P->d_pyr,  P->d_blur,  P->d_cand, P->d_lin,         P->d_okey,  P->d_cell_counts,
                   P->d_label,
                   P->d_ocount, P->d_cells_small, P->d_cells_tall, P->d_cells_big, P->d_pairs,
-                  P->d_cell_scr,
+                  P->d_cell_scr, P->d_octpath,
                   P->d_counts /* base of kps and desc too */};
   for (void* p : ptrs)
     if (p) hipFree(p);

@@ -365,6 +365,7 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
   g->ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
   g->min_th = std::min(std::max(p.min_th_fast, 0), 255);
   g->cells.clear();
+  g->octpath.clear();
   g->wide_keys = false;
   for (int l = 0; l < p.nlevels; l++) {
     LevelGeom& L = g->lv[l];
@@ -437,6 +438,38 @@ int build_geometry(const orbx_params& p, int w, int h, Geometry* g, std::string*
         return ORBX_EUNSUPPORTED;
       }
       g->wide_keys |= L.W >= 4096 || L.H >= 4096;
+      // quadrant paths (ORBextractor.cc:472-522: halfX = ceil((UR.x - UL.x) / 2), a key goes
+      // right when x >= UL.x + halfX); below depth 16 every node is at most 1 px wide and high,
+      // so every key of it stays in quadrant 0 and the path is all zeros there
+      auto spread = [](uint32_t v) {
+        v = (v | (v << 8)) & 0x00FF00FFu;
+        v = (v | (v << 4)) & 0x0F0F0F0Fu;
+        v = (v | (v << 2)) & 0x33333333u;
+        return (v | (v << 1)) & 0x55555555u;
+      };
+      auto path = [&](int c, int lo, int hi) {
+        uint32_t bits = 0;
+        for (int t = 0; t < 16; t++) {
+          const int m = lo + (hi - lo + 1) / 2;
+          if (c >= m) {
+            bits |= 1u << (15 - t);
+            lo = m;
+          } else {
+            hi = m;
+          }
+        }
+        return spread(bits);
+      };
+      L.path_x = (int)g->octpath.size();
+      for (int x = 0; x < L.W; x++) {
+        // the key's initial node as k_octree and DistributeOctTree take it ((int)(x / hX),
+        // :555), the node's columns from the truncated products (:540-544)
+        const int i = std::min((int)(static_cast<float>(x) / L.hx), L.nini - 1);
+        g->octpath.push_back(path(x, (int)(L.hx * static_cast<float>(i)),
+                                  (int)(L.hx * static_cast<float>(i + 1))));
+      }
+      L.path_y = (int)g->octpath.size();
+      for (int y = 0; y < L.H; y++) g->octpath.push_back(path(y, 0, L.H) << 1);
     }
     L.ncells = (int)g->cells.size() - L.cell_begin;
     L.cand_cap = cand - L.cand_off;

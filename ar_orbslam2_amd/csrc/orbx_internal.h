@@ -91,6 +91,8 @@ struct LevelGeom {
   float hx;                // (float)(maxX-minX)/nIni; node i spans [(int)(hx*i), (int)(hx*(i+1)))
   int W, H;                // maxX-minX, maxY-minY (octree frame, origin at minBorder=16)
   int node_cap;            // max alive octree nodes: max(N+3, 4*nIni+4)
+  int path_x, path_y;      // k_octree's quadrant paths of x in [0, W) and y in [0, H): offsets
+                           // into Geometry::octpath
   int kp_off, kp_cap;      // per-image final keypoint slots for this level
   float scale;             // mvScaleFactor
   float size;              // (float)(int)(PATCH_SIZE * scale)
@@ -114,6 +116,10 @@ struct Geometry {
   int ini_th = 20, min_th = 7;
   LevelGeom lv[kMaxLevels];
   std::vector<CellGeom> cells;
+  // per level, the DivideNode path of every octree-frame column and row below its initial node
+  // (LevelGeom::path_x / path_y): bit 2 (15 - t) (x) or 2 (15 - t) + 1 (y) set when the
+  // coordinate lies at or past the depth-t midpoint, so a key's path is path_x[x] | path_y[y]
+  std::vector<uint32_t> octpath;
   std::vector<int> xofs, yofs;        // resize source offsets
   std::vector<int16_t> xa, yb;        // resize fixed-point coefficients (pairs)
   // k_pyramid taps, one int32 pair per output column / row: {x0, a0 << 4 | a1 << 20} (past

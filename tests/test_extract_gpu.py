@@ -159,6 +159,28 @@ def test_noise_octree_chunked_levels(w, h, nf):
     _compare(rng.integers(0, 256, (h, w), dtype=np.uint8), nf)
 
 
+@pytest.mark.parametrize("kind", ["patch", "dots", "pairs"])
+def test_octree_deep_divisions(kind):
+    """Keypoints packed into a small region or spread as a few isolated pairs: the octree
+    divides far below the first refine's bin depth (k_octree refines its bins several times per
+    level, and levels with fewer keys than features divide down to single keys)."""
+    rng = np.random.default_rng(11)
+    img = np.full((480, 640), 90, np.uint8)
+    if kind == "patch":    # one 56 x 56 noise patch: every level's keys in one corner of a node
+        img[200:256, 300:356] = rng.integers(0, 256, (56, 56), dtype=np.uint8)
+    elif kind == "dots":   # isolated 3 x 3 bright squares, some 5-8 px apart
+        for _ in range(40):
+            y, x = rng.integers(40, 440), rng.integers(40, 600)
+            img[y:y + 3, x:x + 3] = 250
+            img[y + 6:y + 9, x + 5:x + 8] = 250
+    else:                  # a few tight pairs: keys 2-4 px apart, many levels deep
+        for _ in range(12):
+            y, x = rng.integers(40, 440), rng.integers(40, 600)
+            img[y, x] = 255
+            img[y + 2, x + 3] = 0
+    _compare(img, 1000)
+
+
 def _blurred_levels(ex):
     import ctypes as C
     from ar_orbslam2_amd._ffi import lib, check, ptr
