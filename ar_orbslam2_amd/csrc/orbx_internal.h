@@ -33,6 +33,7 @@ constexpr int kPyBandH = 32;  // source-level rows per band (more if LDS is shor
 // more workgroups for one image's latency-chained level builds
 constexpr int kPyBandHSmall = 8;
 constexpr int kPyFewImages = 4;
+constexpr int kPyFewTiles = 128;  // k_pyramid tiles per image at least, few-image plans
 constexpr int kPyNT = 512;     // k_pyramid threads per workgroup
 // levels per stage (launch): the first from the input, the others from the last level stored;
 // with the blur fused, shorter stages (each blurred level's 3-row halo widens the band cones)
