@@ -11,10 +11,11 @@
 # tests; the two parts fit one gpurun call each.
 # PMC passes are compacted to one row per (kernel, counter) (scripts/pmc_compact.py); the
 # kernel traces stay under gpurun_out/$TAG/traces (scripts/summarize_profiles.py reads them there).
-# Usage: bash scripts/refresh_profiles.sh r03 [configs]
+# Usage: bash scripts/refresh_profiles.sh r05 [configs ["C3 C4"]]
 set -e -o pipefail
-TAG=${1:-r03}
+TAG=${1:-r05}
 PART=${2:-main}
+CFGS=${3:-C3 C4 C5}
 # issue-rate counters (8 SQ counters, one pass): dual-issued VALU quad-cycles and SALU
 # instructions give bench.py's issue floors (profiles/valu_calibration.json)
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS"
@@ -23,7 +24,7 @@ O=$R/gpurun_out/$TAG
 cd $R
 if [ "$PART" = configs ]; then
   mkdir -p $O
-  for C in C3 C4 C5; do
+  for C in $CFGS; do
     c=$(echo $C | tr A-Z a-z)
     (cd /tmp && export TMPDIR=/tmp && D=$O/${TAG}_pmc_$c && mkdir -p $D &&
      timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/f -o run -- \
