@@ -1251,14 +1251,13 @@ __device__ __forceinline__ void each_key(KS& ks, bool want_labs, bool labs_out, 
 }
 
 // ---- node storage, shared steps
+// A node is its bin range: its rectangle never needs storing, since a key's digits below the
+// node come from the path tables and the node's depth, and its children's counts from the bins.
 struct OctNodes {
-  int *rx, *ry;  // x0 | x1 << 16 and y0 | y1 << 16: the node's [x0, x1) x [y0, y1) (< 32768 px)
   int *cnt, *seq;
   // first bin << 9 | depth << 4 | digits left: the node's bins are [first, first + 4^digits)
   int* bl;
 };
-__device__ __forceinline__ int lo16(int v) { return v & 0xFFFF; }
-__device__ __forceinline__ int hi16(int v) { return (int)((uint32_t)v >> 16); }
 
 struct OctCtx {
   OctNodes A, B;
@@ -1357,10 +1356,9 @@ __device__ int oct_initial(const LevelGeom& G, const OctCtx& X, KS& ks) {
   using K = typename KS::Key;
   const int tid = threadIdx.x, nini = G.nini;
   const OctNodes A = X.A, B = X.B;
+  // (the initial nodes' columns, ni.UL / ni.UR = cv::Point2i(hX * (float)i, 0), :540-544, are
+  // in the path tables)
   for (int i = tid; i < nini; i += NT) {
-    // ni.UL / ni.UR = cv::Point2i(hX * (float)i, 0): the float product truncated (:540-544)
-    A.rx[i] = (int)(G.hx * static_cast<float>(i)) | ((int)(G.hx * static_cast<float>(i + 1)) << 16);
-    A.ry[i] = G.H << 16;
     A.cnt[i] = 0;
     A.seq[i] = i;
   }
@@ -1380,7 +1378,6 @@ __device__ int oct_initial(const LevelGeom& G, const OctCtx& X, KS& ks) {
   for (int i = tid; i < nini; i += NT)
     if (A.cnt[i] > 0) {
       const int j = X.t1[i];
-      B.rx[j] = A.rx[i]; B.ry[j] = A.ry[i];
       B.cnt[j] = A.cnt[i]; B.seq[j] = A.seq[i];
       B.bl[j] = i << 9;
     }
@@ -1464,22 +1461,19 @@ __device__ void oct_retain(const OctCtx& X, KS& ks, const OctNodes& cur, int siz
 
 // A divided node's children into the next list (nxt): the non-empty quadrants in order at
 // base, base - 1, ..., sequence numbers seq0, seq0 + 1, ..., each with its quarter of the
-// parent's bin range
-__device__ __forceinline__ void oct_push_children(const OctNodes& nxt, int rx, int ry, int bl,
-                                                  const int (&c)[4], int base, int seq0) {
-  const int x0 = lo16(rx), x1 = hi16(rx), y0 = lo16(ry), y1 = hi16(ry);
-  const int xm = x0 + (x1 - x0 + 1) / 2, ym = y0 + (y1 - y0 + 1) / 2;
+// parent's bin range, one level deeper
+__device__ __forceinline__ void oct_push_children(const OctNodes& nxt, int bl, const int (&c)[4],
+                                                  int base, int seq0) {
   const int ls = (bl & 15) - 1, s4 = 1 << (2 * ls);
+  const int depth = min((bl & (31 << 4)) + (1 << 4), 31 << 4);
   int j = 0;
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     if (c[q] > 0) {
       const int pos = base - j;
-      nxt.rx[pos] = (q & 1) ? (xm | (x1 << 16)) : (x0 | (xm << 16));
-      nxt.ry[pos] = (q & 2) ? (ym | (y1 << 16)) : (y0 | (ym << 16));
       nxt.cnt[pos] = c[q];
       nxt.seq[pos] = seq0 + j;
-      nxt.bl[pos] = (((bl >> 9) + q * s4) << 9) | min((bl & (31 << 4)) + (1 << 4), 31 << 4) | ls;
+      nxt.bl[pos] = (((bl >> 9) + q * s4) << 9) | depth | ls;
       j++;
     }
   }
@@ -1630,10 +1624,9 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
     for (int i = tid; i < size; i += NT) {
       if (t2[i]) {
         const int c[4] = {cc[4 * i], cc[4 * i + 1], cc[4 * i + 2], cc[4 * i + 3]};
-        oct_push_children(nxt, cur.rx[i], cur.ry[i], cur.bl[i], c, t4[i], seqc + t1[i]);
+        oct_push_children(nxt, cur.bl[i], c, t4[i], seqc + t1[i]);
       } else {
         const int pos = t4[i];
-        nxt.rx[pos] = cur.rx[i]; nxt.ry[pos] = cur.ry[i];
         nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
         nxt.bl[pos] = cur.bl[i];
       }
@@ -1691,7 +1684,6 @@ void k_octree(
   };
   OctNodes A, B;
   for (OctNodes* L : {&A, &B}) {
-    L->rx = (int*)take(4 * NC); L->ry = (int*)take(4 * NC);
     L->cnt = (int*)take(4 * NC); L->seq = (int*)take(4 * NC); L->bl = (int*)take(4 * NC);
   }
   // the quadrant counts (counts step to the next list) and the bin -> node table (refine and
@@ -2323,10 +2315,10 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     return fail(ORBX_EDEVICE);
   if (hipMemset(P->d_counts, 0, 4 * B) != hipSuccess) return fail(ORBX_EDEVICE);
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  // node arrays (two lists of x0 x1 y0 y1 cnt seq bl), quadrant counts, four scratch arrays and
+  // node arrays (two lists of cnt seq bl), quadrant counts, four scratch arrays and
   // the rank keys, then one region for the gather's cell tables or the bins + node table
   auto oct_bytes = [&](size_t NC, size_t CC, size_t BC) {
-    return 2 * 5 * r16(4 * NC) + r16(4 * std::max(4 * NC, BC + 8)) + 4 * r16(4 * NC) +
+    return 2 * 3 * r16(4 * NC) + r16(4 * std::max(4 * NC, BC + 8)) + 4 * r16(4 * NC) +
            r16(8 * (NC + 1)) + std::max(CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0, r16(4 * (BC + 8)));
   };
   // levels are in decreasing area: each instance takes a contiguous range
