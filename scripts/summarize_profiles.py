@@ -35,30 +35,44 @@ def short(name: str) -> str:
 
 
 def trace_durations(path):
-    """kernel -> [(duration ns, stream id)] in dispatch-time order"""
+    """kernel -> [(duration ns, stream id, solo)] in dispatch-time order; `solo`: no dispatch of
+    another stream (any kernel) overlaps it in time"""
     d = collections.defaultdict(list)
+    allr = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            d[short(r["Kernel_Name"])].append(
-                (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
-                 r.get("Stream_Id", "")))
-    return {k: [(dur, st) for _, dur, st in sorted(v)] for k, v in d.items()}
+            t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            st = r.get("Stream_Id", "")
+            allr.append((t0, t1, st))
+            d[short(r["Kernel_Name"])].append((t0, t1, st))
+    allr.sort()
+    starts = [a[0] for a in allr]
+
+    def solo(t0, t1, st):
+        # dispatches starting before t1; any of another stream still running after t0 overlaps
+        import bisect
+        k = bisect.bisect_left(starts, t1)
+        for a0, a1, ast in allr[max(0, k - 64):k]:
+            if ast != st and a1 > t0:
+                return False
+        return True
+
+    return {k: [(t1 - t0, st, solo(t0, t1, st)) for t0, t1, st in sorted(v)] for k, v in d.items()}
 
 
 def solo_run(d, steps=5):
-    """The roofline pass's dispatches: the first `steps` of the longest run of consecutive
-    dispatches on one stream.  The timed region before it and the PCIe pass after it rotate
-    over the camera streams (1, 2, 3, ...), so the run is the pass itself plus, at its end, the
-    PCIe pass's first dispatch when that lands on the same stream."""
+    """The roofline pass's dispatches: stream 0 alone after the timed region, so the longest run
+    of consecutive dispatches on one stream that no other stream's dispatch overlaps (the timed
+    region before it and the PCIe pass after it run the camera streams concurrently)."""
     best, i = [], 0
     while i < len(d):
         j = i
-        while j < len(d) and d[j][1] == d[i][1]:
+        while j < len(d) and d[j][1] == d[i][1] and d[j][2]:
             j += 1
         if j - i >= steps and j - i > len(best):
-            best = [dur for dur, _ in d[i:j]]
-        i = j
-    return best[:steps] or [dur for dur, _ in d[-steps:]]
+            best = [x[0] for x in d[i:j]]
+        i = max(j, i + 1)
+    return best[:steps] or [x[0] for x in d[-steps:]]
 
 
 def counters(pmc_dir):
@@ -114,7 +128,7 @@ def main(tag="r02"):
             # averaged per dispatch, as bench.py's avg_launch_us
             lps = int(round(rf.get("launches_per_step", 1) or 1))
             solo = [sum(x) for x in zip(*(solo_run(v, 5 * lps) for v in inst))]
-            alld = sum(sum(dur for dur, _ in v) / len(v) for v in inst)
+            alld = sum(sum(x[0] for x in v) / len(v) for v in inst)
             check.append(f"    trace average, all dispatches (timed region with concurrent streams"
                          f" + roofline pass + PCIe pass): {alld / 1e3:.2f} us")
             check.append(f"    trace average, roofline pass ({len(solo)} consecutive dispatches on one "
@@ -141,7 +155,7 @@ def main(tag="r02"):
                     f"{'lds/w':>7s}{'wait%':>6s}{'valu_us':>9s}{'salu_us':>9s}{'fetchMB':>9s}"
                     f"{'writeMB':>9s}")
         rows = []
-        for kn, dd in ((kn, [dur for dur, _ in v]) for kn, v in durs.items()):
+        for kn, dd in ((kn, [x[0] for x in v]) for kn, v in durs.items()):
             a = agg.get(kn, {})
 
             def per(c):
