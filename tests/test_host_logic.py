@@ -140,10 +140,12 @@ def test_bench_extract_vs_match_split():
     assert s["match_stages"] == ["k_bow", "k_stereo", "k_voc_transform"]
 
 
-def test_summarizer_finds_roofline_pass():
-    """scripts/summarize_profiles.py: the roofline pass is the start of the longest run of
-    dispatches on one stream (the timed region and the PCIe pass rotate over the streams, and
-    the PCIe pass's first dispatch may extend the run)."""
+def test_summarizer_finds_roofline_pass(tmp_path):
+    """scripts/summarize_profiles.py: the roofline pass is the longest run of dispatches on one
+    stream that no other stream's dispatch overlaps (the timed region and the PCIe pass run the
+    camera streams concurrently; the timed region's tail may leave one stream's last dispatches
+    in a row, overlapped by the others' — the round-5 C5 trace did)."""
+    import csv
     import importlib.util
     import os
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
@@ -151,11 +153,21 @@ def test_summarizer_finds_roofline_pass():
     spec = importlib.util.spec_from_file_location("summarize_profiles", path)
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
-    timed = [(700, s) for _ in range(4) for s in "123"]
-    solo = [(650 + i, "1") for i in range(5)]
-    pcie = [(720, s) for _ in range(3) for s in "123"]
-    assert m.solo_run(timed + solo + pcie) == [650, 651, 652, 653, 654]
+    timed = [(700, s, False) for _ in range(4) for s in "123"]
+    tail = [(900, "1", False) for _ in range(6)]  # stream 1 ahead, the others still running
+    solo = [(650 + i, "1", True) for i in range(5)]
+    pcie = [(720, s, False) for _ in range(3) for s in "123"]
+    assert m.solo_run(timed + tail + solo + pcie) == [650, 651, 652, 653, 654]
     assert m.solo_run(timed) == [700] * 5  # no solo run: the last dispatches
+    # the overlap test on a trace: k on stream 1 overlapped by stream 2's dispatch, then alone
+    rows = [("k", 0, 100, "1"), ("j", 50, 150, "2"), ("k", 200, 300, "1"), ("k", 300, 400, "1")]
+    f = tmp_path / "t.csv"
+    with open(f, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Stream_Id"])
+        w.writerows(rows)
+    d = m.trace_durations(str(f))
+    assert d["k"] == [(100, "1", False), (100, "1", True), (100, "1", True)]
 
 
 def test_pmc_compaction_keeps_bench_readings(tmp_path, monkeypatch):
