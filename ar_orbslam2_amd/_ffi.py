@@ -26,6 +26,7 @@ KEYPOINT_DTYPE = np.dtype(
 
 ERRORS = {-1: "ORBX_EINVAL", -2: "ORBX_ENOMEM", -3: "ORBX_EDEVICE", -4: "ORBX_ECAPACITY",
           -5: "ORBX_EUNSUPPORTED"}
+ORBX_ECAPACITY = -4
 
 EXPORTS = [
     "orbx_extractor_create", "orbx_extractor_destroy", "orbx_extractor_tables", "orbx_extract",
@@ -191,8 +192,14 @@ def profile_kernels(fn, handle, stage_names):
     """{stage: [kernel instance names]} of a profiled pipeline (orbx_*_profile_kernels: the
     instances launched for each stage, named as rocprofv3 reports them)."""
     out = {}
-    buf = C.create_string_buffer(4096)
+    cap = 4096
     for i, name in enumerate(stage_names):
-        check(fn, getattr(lib(), fn)(handle, C.c_int32(i), buf, C.c_int32(len(buf))))
+        while True:  # ORBX_ECAPACITY: the list does not fit (never returned cut): a larger buffer
+            buf = C.create_string_buffer(cap)
+            rc = getattr(lib(), fn)(handle, C.c_int32(i), buf, C.c_int32(cap))
+            if rc != ORBX_ECAPACITY or cap >= 1 << 20:
+                break
+            cap *= 4
+        check(fn, rc)
         out[name] = [k for k in buf.value.decode().split(";") if k]
     return out

@@ -1512,7 +1512,8 @@ int orbx_marker_profile_read(orbx_marker* M, int32_t cap, char (*names)[32], dou
 
 int orbx_marker_profile_kernels(orbx_marker* M, int32_t stage, char* buf, int32_t cap) {
   if (!M) return ORBX_EINVAL;
-  return M->prof.kernels_of(stage, buf, cap) == 0 ? ORBX_OK : ORBX_EINVAL;
+  const int r = M->prof.kernels_of(stage, buf, cap);
+  return r == 0 ? ORBX_OK : r > 0 ? ORBX_ECAPACITY : ORBX_EINVAL;
 }
 
 }  // extern "C"

@@ -2441,7 +2441,8 @@ int orbx_plan_profile_read(orbx_plan* P, int32_t cap, char (*names)[32], double*
 
 int orbx_plan_profile_kernels(orbx_plan* P, int32_t stage, char* buf, int32_t cap) {
   if (!P) return ORBX_EINVAL;
-  return P->prof.kernels_of(stage, buf, cap) == 0 ? ORBX_OK : ORBX_EINVAL;
+  const int r = P->prof.kernels_of(stage, buf, cap);
+  return r == 0 ? ORBX_OK : r > 0 ? ORBX_ECAPACITY : ORBX_EINVAL;
 }
 
 // Internal accessors used by the single-image extractor (orbx_api.hip).

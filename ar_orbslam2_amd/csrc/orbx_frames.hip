@@ -461,7 +461,8 @@ int orbx_frames_profile_read(orbx_frames* F, int32_t cap, char (*names)[32], dou
 
 int orbx_frames_profile_kernels(orbx_frames* F, int32_t stage, char* buf, int32_t cap) {
   if (!F) return ORBX_EINVAL;
-  return F->prof.kernels_of(stage, buf, cap) == 0 ? ORBX_OK : ORBX_EINVAL;
+  const int r = F->prof.kernels_of(stage, buf, cap);
+  return r == 0 ? ORBX_OK : r > 0 ? ORBX_ECAPACITY : ORBX_EINVAL;
 }
 
 }  // extern "C"

@@ -598,14 +598,19 @@ struct Profiler {
     for (auto& l : launches) l = 0;
     for (auto& k : kernels) k.clear();
   }
-  // the stage's instances, ';'-separated, into buf (cap bytes, NUL-terminated, truncated)
+  // the stage's instances, ';'-separated, into buf (cap bytes, NUL-terminated): 0, -1 on a
+  // bad argument, 1 when the list does not fit (buf then holds the empty string, never a cut
+  // name)
   int kernels_of(int st, char* buf, int cap) const {
     if (st < 0 || st >= (int)kernels.size() || !buf || cap <= 0) return -1;
     std::string j;
     for (const auto& k : kernels[st]) j += (j.empty() ? "" : ";") + k;
-    const size_t n = std::min(j.size(), (size_t)cap - 1);
-    memcpy(buf, j.data(), n);
-    buf[n] = 0;
+    if (j.size() + 1 > (size_t)cap) {
+      buf[0] = 0;
+      return 1;
+    }
+    memcpy(buf, j.data(), j.size());
+    buf[j.size()] = 0;
     return 0;
   }
   ~Profiler() {

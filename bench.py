@@ -78,8 +78,11 @@ def algorithmic_bytes(levels, n_kp, n_img):
     per_resize = [(P[l - 1] + P[l]) * n_img for l in range(1, len(P))]
     return {
         # per step; a stage's launch is one dispatch (roofline_of divides by the dispatches per
-        # step: k_pyramid runs one per pyramid stage)
-        "k_pyramid": 2 * P[0] * n_img + sum(per_resize),
+        # step: k_pyramid runs one per pyramid stage).  SURVEY §8d counts the input once (P0
+        # read); the kernel also writes level 0 into the pitched pyramid (one more P0), which
+        # is reported beside the §8d figure as the builder's model, never used for `frac`
+        "k_pyramid": P[0] * n_img + sum(per_resize),
+        "k_pyramid_level0_write": P[0] * n_img,
         "k_blur": 2 * sum(P) * n_img,
         # SURVEY §8d's FAST term: every level pixel read once (the per-cell kernel writes only
         # the cells' keys, 4 B per candidate, ~1 % of the pixels: not counted)
@@ -95,7 +98,7 @@ def algorithmic_bytes(levels, n_kp, n_img):
 # staged windows of k_cvfast: 16-B pieces per lane; k_fast_cells: the cell ROI as aligned
 # dwords; k_pyramid: the source band's 16-B chunks); the stores are 8-B bitmap words (k_cvfast),
 # 4-B keys (k_fast_cells) and 4-B pixel groups (k_pyramid)
-LOAD_WIDTH = {"k_cvfast": 16, "k_fast_cells": 4, "k_pyramid": 16}
+LOAD_WIDTH = {"k_cvfast": 16, "k_fast_cells": 4, "k_fast_pairs": 4, "k_pyramid": 16}
 
 
 def _load_json(name):
@@ -170,7 +173,7 @@ def pmc_binding(pmc_dir, instances):
     return None
 
 
-def pmc_traffic(pmc_dir, instances):
+def pmc_traffic(pmc_dir, instances, stage=None):
     """HBM-side bytes per launch of a stage (its kernel `instances`, exact rocprofv3 names) from
     separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE, both in KB) of the same library
     build (pmc_binding).  MI355X_MICROARCH.md §HBM: FETCH_SIZE counts L2->fabric
@@ -200,7 +203,12 @@ def pmc_traffic(pmc_dir, instances):
             return None, f"{counter} lacks {sorted(set(instances) - set(per))} ({rel})"
         tot[counter] = sum(sum(v) / len(v) for v in per.values()) * 1024
     cal = _load_json("pmc_calibration.json")
-    w = LOAD_WIDTH.get(instances[0].split("<")[0])
+    # the load width of the stage (its instances may be different kernels: the k_fast_cells
+    # stage launches k_fast_pairs first); instances of different widths get no correction
+    widths = {LOAD_WIDTH.get(i.split("<")[0]) for i in instances}
+    w = LOAD_WIDTH.get(stage) if stage else (widths.pop() if len(widths) == 1 else None)
+    if stage and len(widths - {None}) > 1:
+        w = None
     rf = (cal or {}).get("read", {}).get(f"{w}B_per_lane") if w else None
     wf = (cal or {}).get("write", {}).get("8B_per_lane")
     if rf and wf:
@@ -296,7 +304,7 @@ def roofline_of(stages, alg, pmc_dir, steps, B, kernels=None):
     # the kernel instances the roofline pass launched for this stage (the library's profiler):
     # the PMC fields are those instances' counters from passes of this same library build
     inst = (kernels or {}).get(dom) or []
-    traffic, tnote = pmc_traffic(pmc_dir, inst)
+    traffic, tnote = pmc_traffic(pmc_dir, inst, dom)
     issue = pmc_issue(pmc_dir, inst, avg_s * 1e6)
     hbm = {"achieved": round(achieved, 3) if achieved is not None else None,
            "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -304,7 +312,14 @@ def roofline_of(stages, alg, pmc_dir, steps, B, kernels=None):
     out = {"bound": "hbm", "kernel": dom, "kernel_instances": inst, **hbm, "traffic": traffic,
            "traffic_note": tnote,
            "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": a_bytes,
+           "algorithmic_bytes_model": "SURVEY §8d",
            "launches_per_step": round(per_step, 3)}
+    if dom == "k_pyramid" and alg.get("k_pyramid_level0_write") and a_bytes is not None:
+        # the builder's model adds the level-0 write into the pitched pyramid (not a §8d term)
+        b_bytes = a_bytes + alg["k_pyramid_level0_write"] / per_step
+        out["builder_model"] = {"algorithmic_bytes_per_launch": b_bytes,
+                                "extra_term": "level-0 write into the pyramid, P0 per image",
+                                "frac": round(b_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 6)}
     if issue and issue.get("frac") is not None:
         # the issue-rate roofline (achieved / peak in SIMD quad-cycles of the binding unit per
         # second)

@@ -40,7 +40,10 @@ bool orbx_compute_stereo_matches(Frame& F);
 // only reader, Frame::ComputeStereoMatches, runs on the device (orbx_compute_stereo_matches).
 // This copies the last device extraction's levels into mvImagePyramid; it is a no-op when they
 // are already there (or the last call ran on the host, which fills them itself).  Returns false
-// on a device error.  Code reading mvImagePyramid elsewhere calls it first.
+// on a device error.  Code reading mvImagePyramid elsewhere calls it first.  If the export fails,
+// the levels are rebuilt on the host from the extraction's input image, so call it while that
+// image is alive and unchanged (Frame's stereo constructor does: ComputeStereoMatches runs right
+// after the two extractions, Frame.cc:52-80); the input is released once the levels are out.
 bool orbx_materialize_pyramid(ORBextractor* self);
 
 }  // namespace ORB_SLAM2

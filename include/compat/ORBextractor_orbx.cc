@@ -36,8 +36,10 @@ struct ExtractorCtx {
   bool create_failed = false;        // no device context: every call goes to the host
   bool last_on_device = false;       // the last call's results are resident on the GPU
   bool pyramid_exported = false;     // mvImagePyramid holds the last device call's levels
-  // the last device call's input (a header sharing the caller's refcounted image): if the
-  // pyramid export fails, the host extractor rebuilds mvImagePyramid from it
+  // the last device call's input (a header sharing the caller's image): if the pyramid export
+  // fails, the host extractor rebuilds mvImagePyramid from it.  Valid only while the caller's
+  // pixels are (Frame's constructor, where ComputeStereoMatches runs; Frame_orbx.h), and
+  // released once orbx_materialize_pyramid has consumed it
   cv::Mat last_image;
   // the library's raw outputs, kept between calls (one extractor runs on one thread)
   std::vector<orbx_keypoint> kps;
@@ -227,7 +229,9 @@ bool orbx_materialize_pyramid(ORBextractor* self) {
     self->mvImagePyramid = host->mvImagePyramid;
   }
   std::lock_guard<std::mutex> lock(g_mutex);
-  g_ctx[self].pyramid_exported = true;
+  ExtractorCtx& c = g_ctx[self];
+  c.pyramid_exported = true;
+  c.last_image = cv::Mat();  // consumed: no header on the caller's buffer past this frame
   return true;
 }
 

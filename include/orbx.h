@@ -167,7 +167,8 @@ int orbx_plan_profile_read(orbx_plan* plan, int32_t cap, char (*names)[32], doub
 /* The kernel instances the profiled runs launched for stage `stage` (profile_read order), under
  * the names rocprofv3 reports ("k_pyramid<true>", "k_fast_cells<44, 42, unsigned int>"),
  * ';'-separated into buf (cap bytes, NUL-terminated).  Lets a benchmark bind a stage's time to
- * the counters of exactly those kernels. */
+ * the counters of exactly those kernels.  ORBX_ECAPACITY (buf = "") when the list needs more than
+ * cap bytes: the list is never returned cut. */
 int orbx_plan_profile_kernels(orbx_plan* plan, int32_t stage, char* buf, int32_t cap);
 
 /* ------------------------------------------------------------------ projection searches

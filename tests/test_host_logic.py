@@ -314,3 +314,24 @@ def test_kernel_instance_names():
         "k_octree<1024, unsigned long>"
     assert ki("orbx::k_tri_nodes(orbx::TriProblem const*)") == "k_tri_nodes"
     assert ki("(anonymous namespace)::k_fill_u32(unsigned int*, unsigned long)") == "k_fill_u32"
+
+
+def test_roofline_bytes_follow_survey_8d():
+    """The per-kernel algorithmic bytes add up to SURVEY §8d's B per image (4,788,674 B at
+    C1/C2), with the input counted once; the level-0 write of the pitched pyramid is carried
+    beside it as the builder's model and never enters `frac`."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    levels = bench.level_sizes(640, 480, [1 / 1.2 ** l for l in range(8)])
+    alg = bench.algorithmic_bytes(levels, 1000, 1)
+    assert alg["k_pyramid"] + alg["k_blur"] + alg["k_fast_cells"] + alg["k_describe"] == 4788674
+    assert alg["total_per_frame"] == 4788674
+    st = {"k_pyramid": (3.0, 3)}
+    r = bench.roofline_of(st, alg, None, 1, 1)
+    assert r["algorithmic_bytes_per_launch"] == pytest.approx((alg["k_pyramid"] + alg["k_blur"]) / 3)
+    assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, abs=1e-6)
+    b = r["builder_model"]
+    assert b["algorithmic_bytes_per_launch"] == pytest.approx(r["algorithmic_bytes_per_launch"] + 307200 / 3)
+    assert b["frac"] > r["frac"]
