@@ -917,34 +917,50 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
 // instead of the queue (same result: the NMS candidates are the pixels with V > t).
 constexpr int kPairRS = 76;                          // staged ROI row: <= 70 px + 3 alignment
 constexpr int kPairRows = kFcSmallRows;              // ROI rows (detection rows <= 36)
-constexpr int kPairStage = 13;                       // staging rounds of 64 dwords (43.8 rows)
+constexpr int kPairStage = 14;                       // staging rounds of three 19-dword rows
 constexpr int kPairSrc = kPairRS * (kPairRows + 6);  // + the keep rows (krows)
 constexpr int kPairKeepRows = 40;                    // >= detection rows
 constexpr int kPairVS = 72;                          // V row: ring, cwA, gap, cwB, ring
 constexpr int kPairVRows = kPairRows - 4;            // detection rows + 2 ring rows
 constexpr int kPairQ = 768;                          // queue entries
 constexpr int kPairsPerWave = 4;
-static_assert(kPairStage * 256 >= kPairRows * kPairRS, "staging covers the ROI");
-static_assert(kPairStage * 256 <= kPairSrc - 8 * kPairKeepRows, "keep rows past the staged bytes");
+#ifndef ORBX_EXP_NO_SINGLES
+constexpr bool SINGLES_IN_PAIRS = true;   // unpaired cells through k_fast_pairs
+#else
+constexpr bool SINGLES_IN_PAIRS = false;
+#endif
+static_assert(kPairStage * 3 >= kPairRows, "staging covers the ROI");
+static_assert(kPairStage * 3 * kPairRS <= kPairSrc - 8 * kPairKeepRows, "keep rows past the staged bytes");
 static_assert(kPairKeepRows >= kPairRows - 6, "a keep row per detection row");
 static_assert((kPairVS * kPairVRows) % 16 == 0, "V map in 16-B pieces");
 
-// Stage 1 of one detection chunk on all 64 lanes: rows r0 + 2 s and r0 + 2 s + 1 for steps
-// s < nst <= 16, two steps per LDS round trip; the flags of step s end at bit s (row r0 + 2 s)
-// and bit 16 + s (row r0 + 2 s + 1).
-template <int RS>
+// Stage 1 of one detection chunk on all 64 lanes: rows r0 + STEP s and r0 + STEP s + 1 for
+// steps s < nst <= 16, two steps per LDS round trip; the flags of step s end at bit s (row
+// r0 + STEP s) and bit 16 + s (row r0 + STEP s + 1).  STEP 2: a lane's column over 32 rows;
+// STEP 4: the half-wave form (each half-wave takes two of every four rows of one cell at most
+// 32 wide, so a single cell's retry pass keeps all 64 lanes busy).
+template <int RS, int STEP>
 __device__ __forceinline__ uint32_t cardinal_chunk16(const uint8_t* c0, int nst, int t) {
   uint32_t acc = 0;
   const uint8_t* c = c0;
   int s = 0;
-  for (; s + 2 <= nst; s += 2, c += 4 * RS) {
+  for (; s + 2 <= nst; s += 2, c += 2 * STEP * RS) {
     uint32_t f0, f1;
-    fast_cardinal2x2<RS, 2 * RS>(c, t, f0, f1);
+    fast_cardinal2x2<RS, STEP * RS>(c, t, f0, f1);
     acc = (acc >> 2) | (f0 >> 1) | f1;
   }
   if (s < nst) acc = (acc >> 1) | fast_cardinal2<RS>(c, t);
   return acc >> (16 - nst);
 }
+
+#ifdef ORBX_FAST_PROF  // experiment builds only: per-phase wave time of k_fast_pairs (s_memtime)
+__device__ unsigned long long g_fast_prof[16];
+#define FP_NOW() __builtin_amdgcn_s_memtime()
+#define FP_ADD(i, x) (pf[i] += (x))
+#else
+#define FP_NOW() 0ull
+#define FP_ADD(i, x) ((void)(x))
+#endif
 
 template <class K>
 __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ pyr,
@@ -970,38 +986,49 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
   // keep bits per detection row: the end of the staging buffer, past every staged byte (the
   // pretest reads rows up to dr + 6 <= 42: inside the staged bytes)
   uint64_t* const krows = (uint64_t*)(S + kPairSrc - 8 * kPairKeepRows);
+  // per-row output bases of the emit (2 ints a row): the start of the staging buffer, whose ROI
+  // bytes are dead once both passes are done
+  int* const rbase = (int*)S;
+  static_assert(8 * kPairKeepRows <= kPairSrc - 8 * kPairKeepRows, "row bases below the keep rows");
   const uint8_t* pimg = pyr + (int64_t)img * pyr_bytes;
-  // ROI staging: dword lane + 64 u of the staged rows (row (lane + 64 u) / 19, word % 19).  A
-  // lane loads exactly the ROI's dwords: rows past its last row and words past its last dword
-  // are not read (their staged bytes are stale and never used: stage 1 masks their flags, scores
-  // read detection pixels' windows only), and a round wholly past the ROI issues nothing.
+  // ROI staging: lane = (row lane / 19 of three, dword lane % 19 of the 76-B staged row; lanes
+  // 57-63 idle), round u adds three rows: the per-round offsets are uniform.  A lane loads
+  // exactly the ROI's dwords: rows past its last row and words past its last dword are not read
+  // (their staged bytes are stale and never used: stage 1 masks their flags, scores read
+  // detection pixels' windows only), and a round wholly past the ROI issues nothing.
   constexpr int kW = kPairRS / 4;
-  int srow[kPairStage], swof[kPairStage];
-#pragma unroll
-  for (int u = 0; u < kPairStage; u++) {
-    const int i = lane + 64 * u;
-    srow[u] = i / kW;
-    swof[u] = 4 * (i - kW * srow[u]);
-  }
+  const int lrow = lane / kW, lwof = 4 * (lane - kW * lrow);
+  const bool sl = lane < 3 * kW;
   uint32_t pv[kPairStage];
 #pragma unroll
   for (int u = 0; u < kPairStage; u++) pv[u] = 0u;
   auto issue = [&](const CellGeom& A, const CellGeom& B) {
     const int rows = A.y1 - A.y0;
     const int wb = (A.x0 & 3) + (B.x1 - A.x0);  // staged bytes per row (from the aligned start)
-    const uint8_t* src = pimg + (A.v_row0 - 3 * A.pitch - 3) + (A.x0 & ~3) - A.x0;
+    const uint8_t* src = pimg + (A.v_row0 - 3 * A.pitch - 3) + (A.x0 & ~3) - A.x0 +
+                         (uint32_t)(__mul24(lrow, A.pitch) + lwof);
+    const bool ok = sl && lwof < wb;
 #pragma unroll
     for (int u = 0; u < kPairStage; u++)
-      if (srow[u] < rows && swof[u] < wb)
-        pv[u] = *(const uint32_t*)(src + (uint32_t)(__mul24(srow[u], A.pitch) + swof[u]));
+      if (ok && lrow + 3 * u < rows) pv[u] = *(const uint32_t*)(src + (uint32_t)(3 * u * A.pitch));
   };
+  // a single cell runs as a pair with an empty cell B (pr.y >= ncells: a geometry entry past
+  // the level cells with no detection columns, ending where cell A ends)
   int2 pr = pairs[p0];
   CellGeom A = load_cell(cells, pr.x), B = load_cell(cells, pr.y);
   issue(A, B);
+#ifdef ORBX_FAST_PROF
+  uint64_t pf[16] = {};
+  const uint64_t tk0 = FP_NOW();
+#endif
   for (int pi = p0; pi < p1; pi++) {
+    uint64_t tp = FP_NOW();
+    FP_ADD(8, 1);
     wave_sync();  // the previous pair's reads of S are done
+    if (sl) {
 #pragma unroll
-    for (int u = 0; u < kPairStage; u++) *(uint32_t*)(S + 256 * u + 4 * lane) = pv[u];
+      for (int u = 0; u < kPairStage; u++) *(uint32_t*)(S + (lrow + 3 * u) * kPairRS + lwof) = pv[u];
+    }
     const CellGeom Ac = A, Bc = B;
     const int2 pc = pr;
     if (pi + 1 < p1) {  // the next pair's loads in flight while this one is processed
@@ -1029,16 +1056,50 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
     uint64_t bits1 = 0, keep1 = 0;
     uint64_t bits = 0;  // this lane's keep row (lane = detection row)
     int t = ini_th;
+    bool any_dense = false;
+    // a pass over one cell at most 32 wide (a single cell, or a pair's retry pass) takes the
+    // half-wave form
+    bool half = cw == cwA && cwA <= 32;
+    int c_off = 0, cw_r = cw; // the half-wave pass's cell: first detection column and width
+    int qbase = 0;            // pass 2 queues past pass 1's corners (kept for the emit)
+    int nc = 0;               // corners (decoded (r << 6) | c) at q[0, nc)
+    { const uint64_t t2 = FP_NOW(); FP_ADD(0, t2 - tp); tp = t2; }
+#if defined(ORBX_EXP_FAST_STAGE_ONLY)  // timing experiments only (wrong output: no keys)
+    if (lane == 0) cell_counts[(int64_t)img * ncells + pc.x] = 0;
+    if (lane == 0 && pc.y < ncells) cell_counts[(int64_t)img * ncells + pc.y] = 0;
+    continue;
+#endif
     for (int pass = 0; pass < 2; pass++) {
-      // (1) cardinal pretest at t, the flagged pixels queued (or scored in place past kPairQ)
-      const bool col_ok = (allow >> lane) & 1;
-      int nq = 0;
+      // (1) cardinal pretest at t, the flagged pixels queued as raw flag bits (b << 6 | column,
+      // bit 11 = the 32-row chunk, or the half-wave in the half form; decoded when scored), or
+      // scored in place past kPairQ
+      // full form: lane = column, rows rc + 2 (b & 15) + (b >> 4); half form: lane & 31 = the
+      // cell's column, rows 2 (lane >> 5) + 4 (b & 15) + (b >> 4)
+      const int hsub = lane >> 5;
+      const int lcol = half ? c_off + min(lane & 31, cw_r - 1) : lane;
+      const bool col_ok = half ? (lane & 31) < cw_r : ((allow >> lane) & 1) != 0;
+      const int hsh = half ? 1 : 5, bsh = half ? 2 : 1;  // r = (hb << hsh) + ((b & 15) << bsh) + (b >> 4)
+      int nq = qbase;
       bool dense = false;
-      for (int rc = 0; rc < dr; rc += 32) {
-        const int nst = min(16, (dr - rc + 1) >> 1);  // wave-uniform
-        const int nodd = min(16, (dr - rc) >> 1);     // steps whose second row is a detection row
-        uint32_t acc = cardinal_chunk16<kPairRS>(Sx + rc * kPairRS + lane, nst, t);
-        acc &= col_ok ? (((1u << nst) - 1u) | (((1u << nodd) - 1u) << 16)) : 0u;
+      const int nchunks = half ? 1 : (dr + 31) >> 5;
+      for (int ch = 0; ch < nchunks; ch++) {
+        uint32_t acc;
+        int hb;
+        if (half) {
+          const int sub = 2 * hsub;
+          const int nst = (dr + 3) >> 2;  // wave-uniform
+          acc = cardinal_chunk16<kPairRS, 4>(Sx + sub * kPairRS + lcol, nst, t);
+          const int nlo = min(nst, max(0, dr - sub + 3) >> 2), nhi = min(nst, max(0, dr - sub + 2) >> 2);
+          acc &= col_ok ? (((1u << nlo) - 1u) | (((1u << nhi) - 1u) << 16)) : 0u;
+          hb = hsub;
+        } else {
+          const int rc = ch << 5;
+          const int nst = min(16, (dr - rc + 1) >> 1);  // wave-uniform
+          const int nodd = min(16, (dr - rc) >> 1);     // steps whose second row is a detection row
+          acc = cardinal_chunk16<kPairRS, 2>(Sx + rc * kPairRS + lane, nst, t);
+          acc &= col_ok ? (((1u << nst) - 1u) | (((1u << nodd) - 1u) << 16)) : 0u;
+          hb = ch;
+        }
         const int cnt = __popc(acc);
         const int incl = wave_scan_incl(cnt);
         const int tot = __builtin_amdgcn_readlane(incl, 63);
@@ -1047,41 +1108,52 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
           while (acc) {
             const int b = __builtin_ctz(acc);
             acc &= acc - 1;
-            score_at(rc + 2 * (b & 15) + (b >> 4), lane);
+            score_at((hb << hsh) + ((b & 15) << bsh) + (b >> 4), lcol);
           }
           continue;
         }
+        const int ebase = (hb << 11) | lcol;
         int pos = nq + incl - cnt;
         nq += tot;
         while (acc) {
           const int b = __builtin_ctz(acc);
           acc &= acc - 1;
-          q[pos++] = (uint16_t)(((rc + 2 * (b & 15) + (b >> 4)) << 6) | lane);
+          q[pos++] = (uint16_t)((b << 6) | ebase);
         }
       }
+      any_dense = any_dense || dense;
       wave_sync();
+#if defined(ORBX_EXP_FAST_PRETEST_ONLY)
+      break;
+#endif
+      { const uint64_t t2 = FP_NOW(); FP_ADD(1 + 3 * pass, t2 - tp); tp = t2; FP_ADD(11, nq - qbase); FP_ADD(10, half ? 1 : 0); }
       // (2) cornerScore of the queued pixels (a fallback pass rescores its cell's iniThFAST
       // candidates: same value); the corners at t (V > max(t, 1): the NMS candidates, about a
-      // quarter of the queue) are compacted in place to the queue's front (a round reads its
-      // entries before any lane writes, and writes only below the next round's)
+      // quarter of the queue) are compacted in place, decoded to (r << 6) | c, after the corners
+      // already kept (a round reads its entries before any lane writes, and writes only below
+      // the next round's)
       const int t1 = max(t, 1);
-      int nc = 0;
-      for (int j0 = 0; j0 < nq; j0 += 64) {
+      const int cbase = qbase;
+      nc = qbase;
+      for (int j0 = qbase; j0 < nq; j0 += 64) {
         const int j = j0 + lane;
-        int e = 0;
+        int rcode = 0;
         bool corner = false;
         if (j < nq) {
-          e = q[j];
-          corner = score_at(e >> 6, e & 63) > t1;
+          const int e = q[j], hbb = e >> 6, c = e & 63;
+          const int r = ((hbb >> 5) << hsh) + ((hbb & 15) << bsh) + ((hbb >> 4) & 1);
+          rcode = (r << 6) | c;
+          corner = score_at(r, c) > t1;
         }
         const uint64_t m = __ballot(corner);
-        if (corner) q[nc + lane_rank(m)] = (uint16_t)e;
+        if (corner) q[nc + lane_rank(m)] = (uint16_t)rcode;
         nc += __popcll(m);
       }
       if (lane < kPairKeepRows) krows[lane] = 0;
       wave_sync();
-      // (3) the strict 8-neighbour NMS at t over the corners: keep <=> V > (nmax > t ? nmax :
-      // max(t,1)), the largest neighbour deciding (k_fast_cells)
+      { const uint64_t t2 = FP_NOW(); FP_ADD(2 + 3 * pass, t2 - tp); tp = t2; FP_ADD(12, nc - cbase); }
+      // (3) the strict 8-neighbour NMS at t over this pass's corners: keep <=> V > (nmax > t ?
+      // nmax : max(t,1)), the largest neighbour deciding (k_fast_cells)
       auto keep_at = [&](int r, int c) -> bool {
         const uint8_t* p = V + vofs(r, c);
         const int v = p[0];
@@ -1092,7 +1164,7 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
         return v > (nmax > t ? nmax : t1);
       };
       if (!dense) {
-        for (int j = lane; j < nc; j += 64) {
+        for (int j = cbase + lane; j < nc; j += 64) {
           const int e = q[j], r = e >> 6, c = e & 63;
           if (keep_at(r, c)) atomicOr((unsigned long long*)&krows[r], 1ull << c);
         }
@@ -1105,21 +1177,36 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
             if (((allow >> c) & 1) && keep_at(lane, c)) bits |= 1ull << c;
       }
       bits &= allow;
+      { const uint64_t t2 = FP_NOW(); FP_ADD(3 + 3 * pass, t2 - tp); tp = t2; FP_ADD(9, pass); }
       if (pass == 1) {
         bits |= bits1 & keep1;
         break;
       }
-      const bool hasA = __ballot((bits & mA) != 0) != 0, hasB = __ballot((bits & mB) != 0) != 0;
-      if ((hasA && hasB) || t == min_th) break;  // every cell has keypoints, or no retry left
-      // a cell without keypoints at iniThFAST: FAST again at minThFAST on its columns
+      // a cell without keypoints at iniThFAST (an empty cell B has nothing to retry)
+      const bool needA = __ballot((bits & mA) != 0) == 0;
+      const bool needB = mB != 0 && __ballot((bits & mB) != 0) == 0;
+#if defined(ORBX_EXP_FAST_NO_RETRY)
+      break;
+#endif
+      if ((!needA && !needB) || t == min_th) break;  // every cell has keypoints, or no retry left
+      // FAST again at minThFAST on the columns of the cells without keypoints
       bits1 = bits;
-      keep1 = (hasA ? mA : 0) | (hasB ? mB : 0);
-      allow = (hasA ? 0 : mA) | (hasB ? 0 : mB);
+      keep1 = (needA ? 0 : mA) | (needB ? 0 : mB);
+      allow = (needA ? mA : 0) | (needB ? mB : 0);
       t = min_th;
+      if (needA != needB) {  // one cell: the half-wave form when it is at most 32 wide
+        c_off = needA ? 0 : cwA;
+        cw_r = needA ? cwA : cw - cwA;
+        half = cw_r <= 32;
+      }
+      qbase = nc;
     }
-    // (4) each cell's survivors to its slot in raster order: one packed scan of the two counts,
-    // then each lane (detection row) writes its row's keys, cell A's and cell B's in two loops
-    // (uniform slot pointers, no per-key select)
+    // (4) each cell's survivors to its slot in raster order
+#if defined(ORBX_EXP_FAST_PRETEST_ONLY) || defined(ORBX_EXP_FAST_NO_EMIT)
+    if (lane == 0) cell_counts[(int64_t)img * ncells + pc.x] = __popcll(bits) & 0;
+    if (lane == 0 && pc.y < ncells) cell_counts[(int64_t)img * ncells + pc.y] = 0;
+    continue;
+#endif
     uint64_t bA = bits & mA, bB = bits >> cwA;
     const int nA = __popcll(bA), nB = __popcll(bB);
     const int packed = nA | (nB << 16);
@@ -1127,24 +1214,57 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
     const int tot = __builtin_amdgcn_readlane(incl, 63);
     if (lane == 0) {
       cell_counts[(int64_t)img * ncells + pc.x] = tot & 0xFFFF;
-      cell_counts[(int64_t)img * ncells + pc.y] = tot >> 16;
+      if (pc.y < ncells) cell_counts[(int64_t)img * ncells + pc.y] = tot >> 16;
     }
-    K* outA = cand + (int64_t)img * cand_total + Ac.slot_off + ((incl - packed) & 0xFFFF);
-    K* outB = cand + (int64_t)img * cand_total + Bc.slot_off + ((incl - packed) >> 16);
-    const int y = Ac.y0 + 3 + lane, x0 = Ac.x0 + 3;
-    const uint8_t* Vr = V + __mul24(lane + 1, kPairVS) + 1;
-    while (bA) {
-      const int c = __builtin_ctzll(bA);
-      bA &= bA - 1;
-      *outA++ = KeyFmt<K>::make(x0 + c, y, (int)Vr[c]);
+    K* const candA = cand + (int64_t)img * cand_total + Ac.slot_off;
+    K* const candB = cand + (int64_t)img * cand_total + Bc.slot_off;
+    const int x0 = Ac.x0 + 3;
+    if (!any_dense) {
+      // by rank, one lane per corner: a kept corner (r, c) goes to its cell's keys of the rows
+      // above r plus the kept bits left of c in row r; every kept pixel is a corner of the pass
+      // that kept it, queued in q[0, nc) (pass 1's corners stay in front of pass 2's; a pixel
+      // queued by both passes writes the same key to the same place twice)
+      if (lane < dr) {
+        const int ex = incl - packed;
+        rbase[2 * lane] = ex & 0xFFFF;
+        rbase[2 * lane + 1] = (ex >> 16) - nA;  // cell B: its rank counts cell A's bits of the row
+        krows[lane] = bits;
+      }
+      wave_sync();
+      for (int j = lane; j < nc; j += 64) {
+        const int e = q[j], r = e >> 6, c = e & 63;
+        const uint64_t kr = krows[r];
+        if ((kr >> c) & 1) {
+          const bool isB = c >= cwA;
+          const int pos = rbase[2 * r + (isB ? 1 : 0)] + __popcll(kr & ((1ull << c) - 1));
+          (isB ? candB : candA)[pos] = KeyFmt<K>::make(x0 + c, Ac.y0 + 3 + r, (int)V[vofs(r, c)]);
+        }
+      }
+    } else {
+      // each lane (detection row) writes its row's keys, cell A's and cell B's in two loops
+      K* outA = candA + ((incl - packed) & 0xFFFF);
+      K* outB = candB + ((incl - packed) >> 16);
+      const int y = Ac.y0 + 3 + lane;
+      const uint8_t* Vr = V + __mul24(lane + 1, kPairVS) + 1;
+      while (bA) {
+        const int c = __builtin_ctzll(bA);
+        bA &= bA - 1;
+        *outA++ = KeyFmt<K>::make(x0 + c, y, (int)Vr[c]);
+      }
+      const uint8_t* VrB = Vr + cwA + 1;  // cell B's columns, past the gap column
+      while (bB) {
+        const int c = __builtin_ctzll(bB);
+        bB &= bB - 1;
+        *outB++ = KeyFmt<K>::make(x0 + cwA + c, y, (int)VrB[c]);
+      }
     }
-    const uint8_t* VrB = Vr + cwA + 1;  // cell B's columns, past the gap column
-    while (bB) {
-      const int c = __builtin_ctzll(bB);
-      bB &= bB - 1;
-      *outB++ = KeyFmt<K>::make(x0 + cwA + c, y, (int)VrB[c]);
-    }
+    { const uint64_t t2 = FP_NOW(); FP_ADD(7, t2 - tp); }
   }
+#ifdef ORBX_FAST_PROF
+  pf[13] = FP_NOW() - tk0;
+  if (lane == 0)
+    for (int i = 0; i < 16; i++) atomicAdd(&g_fast_prof[i], (unsigned long long)pf[i]);
+#endif
 }
 
 // ------------------------------------------------------------------ k_octree
@@ -2240,7 +2360,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   P->ntiles = (int)tiles.size();
   for (int l = 0; l < g.nlevels; l++) P->cell_cap = std::max(P->cell_cap, g.lv[l].ncells);
   std::vector<int> cells_small, cells_tall, cells_big;
-  std::vector<int2> pairs;
+  std::vector<int2> pairs, singles;
+  std::vector<CellGeom> empties;  // k_fast_pairs' empty partners, past the level cells
   // a few-image plan runs every cell in the <72, kCellMax> instance: one launch instead of two
   // on the drop-in path's one-frame chain (either instance handles any cell)
   const bool one_fast_launch = max_batch <= kPyFewImages;
@@ -2265,17 +2386,31 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
         continue;
       }
     }
+    // a single cell whose ROI fits the pair staging runs in k_fast_pairs with an empty partner
+    // (half-wave form when it is at most 32 wide): one launch instead of a k_fast_cells one
+    int dcs, drs;
+    if (SINGLES_IN_PAIRS && !one_fast_launch && det(C, &dcs, &drs) && C.y1 - C.y0 <= kPairRows &&
+        C.x1 - C.x0 + 3 <= kPairRS) {
+      CellGeom e = C;  // the empty partner: no detection columns, ending where C ends
+      e.x0 = (int16_t)(C.x1 - 6);
+      singles.push_back(make_int2(c, (int)g.cells.size() + (int)empties.size()));
+      empties.push_back(e);
+      continue;
+    }
     const bool small = C.x1 - C.x0 + 3 <= 44 && C.y1 - C.y0 <= kFcSmallRows;
     const bool tall = C.x1 - C.x0 + 3 <= kFcTallRS && C.y1 - C.y0 <= kCellMax;
     (one_fast_launch ? cells_big : small ? cells_small : tall ? cells_tall : cells_big).push_back(c);
   }
+  pairs.insert(pairs.end(), singles.begin(), singles.end());  // singles after the pairs
   P->n_pairs = (int)pairs.size();
   P->n_cells_small = (int)cells_small.size();
   P->n_cells_tall = (int)cells_tall.size();
   P->n_cells_big = (int)cells_big.size();
   const size_t B = (size_t)max_batch;
   const size_t ksz = g.wide_keys ? 8 : 4;  // bytes per candidate key
-  if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, g.cells.size()) ||
+  std::vector<CellGeom> cells_dev(g.cells);  // + the empty partners of single cells
+  cells_dev.insert(cells_dev.end(), empties.begin(), empties.end());
+  if (dalloc(&P->d_lv, g.nlevels) || dalloc(&P->d_cells, cells_dev.size()) ||
       dalloc(&P->d_xtap, g.xtap.size() / 2) || dalloc(&P->d_ytap, g.ytap.size() / 2) ||
       dalloc(&P->d_tiles, tiles.size()) || dalloc(&P->d_bands, g.bands.size()) ||
       dalloc(&P->d_pyr, B * g.pyr_bytes) || dalloc(&P->d_blur, B * g.pyr_bytes) ||
@@ -2303,7 +2438,7 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   };
   if (up(P->d_lv, g.lv, sizeof(LevelGeom) * g.nlevels) ||
       up(P->d_octpath, g.octpath.data(), 4 * g.octpath.size()) ||
-      up(P->d_cells, g.cells.data(), sizeof(CellGeom) * g.cells.size()) ||
+      up(P->d_cells, cells_dev.data(), sizeof(CellGeom) * cells_dev.size()) ||
       up(P->d_xtap, g.xtap.data(), 4 * g.xtap.size()) ||
       up(P->d_ytap, g.ytap.data(), 4 * g.ytap.size()) ||
       up(P->d_tiles, tiles.data(), sizeof(BlurTile) * tiles.size()) ||
@@ -2468,6 +2603,18 @@ int orbx_plan_level_download_buf(orbx_plan* P, int img, int level, uint8_t* out,
 int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int64_t stride) {
   return orbx_plan_level_download_buf(P, img, level, out, stride, 0);
 }
+
+#ifdef ORBX_FAST_PROF
+int orbx_debug_fast_prof(uint64_t* out, int32_t reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_prof), sizeof(g_fast_prof)) != hipSuccess)
+    return ORBX_EDEVICE;
+  if (reset) {
+    static const unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_fast_prof), z, sizeof(z)) != hipSuccess) return ORBX_EDEVICE;
+  }
+  return ORBX_OK;
+}
+#endif
 
 int orbx_debug_plan_level(orbx_plan* P, int32_t img, int32_t level, int32_t blurred, uint8_t* out,
                           int64_t stride) {
