@@ -290,11 +290,16 @@ __device__ __forceinline__ uint32_t blur_row4(uint32_t a, uint32_t b, uint32_t c
 
 // Column sums (taps [18, 34, 49, 55, 49, 34, 18], packed u16: at most 255 * 257) of one dword
 // column's two byte pairs over 7 consecutive rows starting at j.
+// The symmetric pair sums (at most 510 a half: no carry crosses into the high half) as plain
+// 32-bit adds, which dual-issue (profiles/valu_calibration.json), where v_pk_add_u16 does not.
+__device__ __forceinline__ blur_u16x2 blur_pair_add(blur_u16x2 a, blur_u16x2 b) {
+  return __builtin_bit_cast(blur_u16x2, __builtin_bit_cast(uint32_t, a) + __builtin_bit_cast(uint32_t, b));
+}
 template <int N>
 __device__ __forceinline__ blur_u16x2 blur_col(const blur_u16x2 (&U)[N], int j) {
   const blur_u16x2 K0 = {18, 18}, K1 = {34, 34}, K2 = {49, 49}, K3 = {55, 55};
-  return (U[j] + U[j + 6]) * K0 + (U[j + 1] + U[j + 5]) * K1 + (U[j + 2] + U[j + 4]) * K2 +
-         U[j + 3] * K3;
+  return blur_pair_add(U[j], U[j + 6]) * K0 + blur_pair_add(U[j + 1], U[j + 5]) * K1 +
+         blur_pair_add(U[j + 2], U[j + 4]) * K2 + U[j + 3] * K3;
 }
 
 // The fused blur (k_pyramid<true>) of one level's own tile: rows [own_lo, own_hi), groups
@@ -597,13 +602,11 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
     }
   }
   __syncthreads();
-  constexpr unsigned short k0 = 18, k1 = 34, k2 = 49, k3 = 55;
   // column pass (the sum is separable and exact, so columns first gives the same m): a thread
   // takes one window dword column and 4 output rows; its 10 input dwords unpack once into byte
   // pairs (b0, b1) and (b2, b3), each output row is 7 packed u16 ops per pair (a column sum is
   // at most 255 * 257 = 65535)
   {
-    const blur_u16x2 K0 = {k0, k0}, K1 = {k1, k1}, K2 = {k2, k2}, K3 = {k3, k3};
     for (int i = tid; i < kWords * (kBlurTH / 4); i += 256) {
       const int rb = i / kWords, c = i - rb * kWords, r0 = 4 * rb;
       blur_u16x2 U[10], V[10];
@@ -615,10 +618,7 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, i
       }
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const blur_u16x2 su = (U[j] + U[j + 6]) * K0 + (U[j + 1] + U[j + 5]) * K1 +
-                              (U[j + 2] + U[j + 4]) * K2 + U[j + 3] * K3;
-        const blur_u16x2 sv = (V[j] + V[j + 6]) * K0 + (V[j + 1] + V[j + 5]) * K1 +
-                              (V[j + 2] + V[j + 4]) * K2 + V[j + 3] * K3;
+        const blur_u16x2 su = blur_col(U, j), sv = blur_col(V, j);
         *(uint2*)&s_col[r0 + j][2 * c] =
             make_uint2(__builtin_bit_cast(uint32_t, su), __builtin_bit_cast(uint32_t, sv));
       }
@@ -1125,6 +1125,12 @@ __global__ __launch_bounds__(256) void k_fast_pairs(const uint8_t* __restrict__ 
       wave_sync();
 #if defined(ORBX_EXP_FAST_PRETEST_ONLY)
       break;
+#endif
+#if defined(ORBX_EXP_FAST_RETRY_PRETEST_ONLY)
+      if (pass == 1) {
+        bits = bits1 & keep1;
+        break;
+      }
 #endif
       { const uint64_t t2 = FP_NOW(); FP_ADD(1 + 3 * pass, t2 - tp); tp = t2; FP_ADD(11, nq - qbase); FP_ADD(10, half ? 1 : 0); }
       // (2) cornerScore of the queued pixels (a fallback pass rescores its cell's iniThFAST
