@@ -47,6 +47,11 @@ struct BowProblem {
   int mode;
   float nnratio;
   int check_ori;
+  // nullable (the resident per-frame calls): the finish writes the match array to match_host
+  // and (count, error) to ctrl_host in pinned host memory, then returns match / matched2 /
+  // error / done to their clean state (-1, 0, 0, 0) for the next call: no copy launches
+  int* match_host;
+  int* ctrl_host;
 };
 
 struct DevFeatVec {
@@ -85,6 +90,14 @@ struct TriProblem {
   int* count;
   int* error;  // bit 1 (ORBX_DEVERR_INDEX): a match index outside KF2
   int* done;   // nullable, zeroed: k_tri_nodes_wg's finished-workgroup counter (as BowProblem)
+  // nullable (resident calls, as BowProblem): pairs go to pairs_host, (count, error) to
+  // ctrl_host, and m12 / error / done return to their clean state
+  int* pairs_host;
+  int* ctrl_host;
+  // tab_inline: the sides' scale_factors / level_sigma2 are tab[0..1] / tab[2..3] (the kernels
+  // point them at their LDS copy of the problem), not device arrays
+  int tab_inline;
+  float tab[4][16];
 };
 
 // device error bits of the matcher problems: a finish kernel read a match index outside the
@@ -219,6 +232,74 @@ struct Workspace {
   }
 };
 extern thread_local Workspace tls_ws;
+
+// ------------------------------------------------------------------ resident frames
+// The per-frame drop-in chain (Frame::ComputeBoW, SearchByBoW(KF, F), SearchForTriangulation)
+// hands the library the same frame's arrays call after call, and a keyframe's for many frames
+// (the reference keyframe of TrackReferenceKeyFrame, Tracking.cc:1127-1136; KeyFrame copies the
+// Frame's descriptors, KeyFrame.cc:31).  A frame's descriptors and FeatureVector stay in HBM in
+// an entry of this cache, found by content (feature count, then the descriptor bytes compared
+// with the entry's host copy: an address or an id could name another frame after a free or a
+// Tracking::Reset).  Entries are claimed least-recently-used; one in use by a call in flight is
+// never reclaimed.
+constexpr int kResEntries = 16;
+constexpr int kResMaxFeatures = 8192;
+struct ResEntry {
+  int device = -1;
+  int cap = 0;          // features the device block holds
+  int n = -1;           // descriptors held (-1: free)
+  bool ready = false;   // the device descriptors are filled (a claiming call set them)
+  int fv_n = -1;        // FeatureVector nodes held (-1: none)
+  bool has_keys = false;  // keypoints (mvKeysUn) held
+  uint64_t stamp = 0;
+  int refs = 0;
+  // device block: desc [cap][32] | fv ids [cap] | fv offsets [cap + 1] | fv feats [cap] |
+  // keypoints [cap] (28 B)
+  char* d = nullptr;
+  std::vector<uint8_t> h_desc;
+  std::vector<uint32_t> h_ids;
+  std::vector<int> h_off, h_feats;
+  std::vector<orbx_keypoint> h_keys;
+  uint8_t* d_desc() const { return (uint8_t*)d; }
+  uint32_t* d_ids() const { return (uint32_t*)(d + (size_t)cap * 32); }
+  int* d_off() const { return (int*)(d + (size_t)cap * 36); }
+  int* d_feats() const { return (int*)(d + (size_t)cap * 40 + 4); }
+  orbx_keypoint* d_keys() const { return (orbx_keypoint*)(d + (size_t)cap * 44 + 16); }  // 16-B aligned
+  static size_t fv_bytes(int cap) { return (size_t)cap * 12 + 4; }  // ids | offsets | feats
+  static size_t bytes(int cap) { return (size_t)cap * 72 + 16; }
+};
+// The entry holding these n descriptors on the current device (*hit), or a reclaimed one now
+// assigned to them whose device copy the caller must fill (!*hit).  nullptr: n out of range or
+// no entry free (every one in use).  Every non-null return is released by res_release.
+ResEntry* res_acquire(int n, const uint8_t* desc, bool* hit);
+void res_release(ResEntry* e);
+// whether the entry's device FeatureVector / keypoints equal these host arrays
+bool res_fv_matches(const ResEntry* e, const orbx_featvec& fv);
+bool res_keys_match(const ResEntry* e, const orbx_keypoint* keys);
+// after the call that filled them has completed: the entry's device descriptors, FeatureVector
+// and keypoints equal these host arrays (nullptr: that part unchanged)
+void res_mark_filled(ResEntry* e, bool desc, const orbx_featvec* fv, const orbx_keypoint* keys);
+// drops the entry's contents (a failed fill)
+void res_invalidate(ResEntry* e);
+// the caller is the entry's only user and it holds no FeatureVector yet
+bool res_exclusive_without_fv(const ResEntry* e);
+
+// Per-thread device scratch of the resident calls, kept in its clean state between calls (the
+// finish kernels restore it): bow match [cap] = -1, matched2 [cap] = 0, tri m12 [cap] = -1,
+// control words (bow done / error, tri done / error) = 0.
+struct ResScratch {
+  int device = -1;
+  int cap = 0;
+  bool dirty = true;  // a call failed between launch and finish: re-initialise first
+  char* d = nullptr;
+  int* match() const { return (int*)d; }
+  int* matched2() const { return (int*)d + cap; }
+  int* m12() const { return (int*)d + 2 * (size_t)cap; }
+  int* ctrl() const { return (int*)d + 3 * (size_t)cap; }  // [0] bow done [1] bow error [2] tri done [3] tri error [4..7] device counts
+};
+// the calling thread's scratch for at least cap features (re-initialised when grown or dirty,
+// synchronously on the thread's stream); nullptr on an allocation failure
+ResScratch* res_scratch(int cap);
 
 // Packs host arrays into one staging buffer, uploaded with one copy.  The buffer is the
 // calling thread's pinned arena (one Stager per thread at a time: every entry point stages,

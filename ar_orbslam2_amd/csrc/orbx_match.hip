@@ -300,8 +300,8 @@ __device__ __forceinline__ bool claimed(uint64_t m0, uint64_t m1, int pos) {
   return ((pos < 64 ? m0 >> pos : m1 >> (pos - 64)) & 1) != 0;
 }
 
-__device__ __forceinline__ void bow_nodes_wg(const BowProblem* __restrict__ probs) {
-  const BowProblem& P = probs[blockIdx.y];
+__device__ __forceinline__ void bow_nodes_wg(const BowProblem* __restrict__ probs, const int pi) {
+  const BowProblem& P = probs[pi];
   const int a = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -322,7 +322,7 @@ __device__ __forceinline__ void bow_nodes_wg(const BowProblem* __restrict__ prob
   if (b < 0) return;  // workgroup-uniform
   const int f0 = P.s2.node_offsets[b], m = P.s2.node_offsets[b + 1] - f0;
   if (m > kBwgCands) {  // the wave form (no candidate limit)
-    if (wid == 0) bow_node_wave<kBowDescChunks>(probs, blockIdx.y, a, lane);
+    if (wid == 0) bow_node_wave<kBowDescChunks>(probs, pi, a, lane);
     return;
   }
   const bool kfkf = P.mode == 1;
@@ -444,9 +444,21 @@ __device__ __forceinline__ void bow_nodes_wg(const BowProblem* __restrict__ prob
   }
 }
 
+// The workgroup's problem into LDS: the kernels read its fields throughout, and a resident
+// call's problem lives in pinned host memory (one PCIe read per workgroup, not one per use).
+template <class T>
+__device__ __forceinline__ void stage_problem(T* dst, const T* __restrict__ src) {
+  static_assert(sizeof(T) % 4 == 0, "problem in dwords");
+  for (int i = threadIdx.x; i < (int)(sizeof(T) / 4); i += blockDim.x)
+    ((int*)dst)[i] = ((const int*)src)[i];
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_bow_nodes_wg(const BowProblem* __restrict__ probs) {
-  bow_nodes_wg(probs);
-  if (probs[blockIdx.y].done && last_workgroup(probs[blockIdx.y].done)) bow_finish(probs, blockIdx.y);
+  __shared__ BowProblem s_p;
+  stage_problem(&s_p, probs + blockIdx.y);
+  bow_nodes_wg(&s_p, 0);
+  if (s_p.done && last_workgroup(s_p.done)) bow_finish(&s_p, 0);
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:1604-1645)
@@ -564,10 +576,25 @@ __device__ __forceinline__ void bow_finish(const BowProblem* __restrict__ probs,
   atomicAdd(&s_cnt, local);
   __syncthreads();
   if (tid == 0) *P.count = s_cnt;
+  if (P.match_host) {  // a resident call: results to pinned host memory, scratch back to clean
+    for (int i = tid; i < n; i += 256) {
+      P.match_host[i] = P.match[i];
+      P.match[i] = -1;
+    }
+    if (kfkf && P.matched2)
+      for (int i = tid; i < n_other; i += 256) P.matched2[i] = 0;
+    if (tid == 0) {
+      P.ctrl_host[0] = s_cnt;
+      P.ctrl_host[1] = atomicExch(P.error, 0);
+      if (P.done) atomicExch(P.done, 0);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_bow_finish(const BowProblem* __restrict__ probs) {
-  bow_finish(probs, blockIdx.x);
+  __shared__ BowProblem s_p;
+  stage_problem(&s_p, probs + blockIdx.x);
+  bow_finish(&s_p, 0);
 }
 
 // The last workgroup of a node kernel to finish (counted in *done, zeroed by the host) runs the
@@ -716,8 +743,8 @@ __global__ __launch_bounds__(256) void k_tri_nodes(const TriProblem* __restrict_
 // node, the KF2 node staged 256 features at a time for the whole workgroup and G = 256 / n1
 // lanes per KF1 feature, so a node's scan is spread over four times as many lanes.  Same keys,
 // same LDS minimum, same result.
-__device__ __forceinline__ void tri_nodes_wg(const TriProblem* __restrict__ probs) {
-  const TriProblem& P = probs[blockIdx.y];
+__device__ __forceinline__ void tri_nodes_wg(const TriProblem* __restrict__ probs, const int pi) {
+  const TriProblem& P = probs[pi];
   const int a = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   if (a >= tri_nodes(P.s1)) return;
@@ -815,9 +842,24 @@ __device__ __forceinline__ void tri_nodes_wg(const TriProblem* __restrict__ prob
   }
 }
 
+// a resident call's level tables travel inside the problem: point the sides at the LDS copy
+__device__ __forceinline__ void tri_inline_tables(TriProblem& p) {
+  if (!p.tab_inline) return;
+  if (threadIdx.x == 0) {
+    p.s1.scale_factors = p.tab[0];
+    p.s1.level_sigma2 = p.tab[1];
+    p.s2.scale_factors = p.tab[2];
+    p.s2.level_sigma2 = p.tab[3];
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_tri_nodes_wg(const TriProblem* __restrict__ probs) {
-  tri_nodes_wg(probs);
-  if (probs[blockIdx.y].done && last_workgroup(probs[blockIdx.y].done)) tri_finish(probs, blockIdx.y);
+  __shared__ TriProblem s_p;
+  stage_problem(&s_p, probs + blockIdx.y);
+  tri_inline_tables(s_p);
+  tri_nodes_wg(&s_p, 0);
+  if (s_p.done && last_workgroup(s_p.done)) tri_finish(&s_p, 0);
 }
 
 __device__ __forceinline__ void tri_finish(const TriProblem* __restrict__ probs, const int pi) {
@@ -897,6 +939,7 @@ __device__ __forceinline__ void tri_finish(const TriProblem* __restrict__ probs,
     pos += w < wid ? s_scan[w] : 0;
     total += s_scan[w];
   }
+  int* const pairs = P.pairs_host ? P.pairs_host : P.pairs;  // resident calls: pinned host
   for (int b0 = beg; b0 < end; b0 += kFinishRegs) {
     int m[kFinishRegs];
 #pragma unroll
@@ -904,17 +947,29 @@ __device__ __forceinline__ void tri_finish(const TriProblem* __restrict__ probs,
 #pragma unroll
     for (int r = 0; r < kFinishRegs; r++) {
       if (m[r] >= 0) {
-        P.pairs[2 * pos] = b0 + r;
-        P.pairs[2 * pos + 1] = m[r];
+        pairs[2 * pos] = b0 + r;
+        pairs[2 * pos + 1] = m[r];
         pos++;
       }
     }
   }
   if (tid == 0) *P.count = total;
+  if (P.pairs_host) {  // scratch back to clean for the next resident call
+    __syncthreads();   // every m12 read above is done
+    for (int i = tid; i < n; i += 256) P.m12[i] = -1;
+    if (tid == 0) {
+      P.ctrl_host[0] = total;
+      P.ctrl_host[1] = P.error ? atomicExch(P.error, 0) : 0;
+      if (P.done) atomicExch(P.done, 0);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_tri_finish(const TriProblem* __restrict__ probs) {
-  tri_finish(probs, blockIdx.x);
+  __shared__ TriProblem s_p;
+  stage_problem(&s_p, probs + blockIdx.x);
+  tri_inline_tables(s_p);
+  tri_finish(&s_p, 0);
 }
 
 // ------------------------------------------------------------------ vocabulary + FeatureVector
@@ -1092,6 +1147,152 @@ hipError_t queue_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
 thread_local Workspace tls_ws;
 thread_local PinnedBuf tls_stage;
 
+// ------------------------------------------------------------------ resident frames
+namespace {
+std::mutex g_res_mutex;
+ResEntry g_res[kResEntries];
+uint64_t g_res_clock = 0;
+}  // namespace
+
+ResEntry* res_acquire(int n, const uint8_t* desc, bool* hit) {
+  if (n <= 0 || n > kResMaxFeatures || !desc || !hit) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(g_res_mutex);
+  const size_t bytes = (size_t)n * 32;
+  ResEntry* victim = nullptr;
+  for (ResEntry& e : g_res) {
+    if (e.ready && e.device == dev && e.n == n && memcmp(e.h_desc.data(), desc, bytes) == 0) {
+      e.refs++;
+      e.stamp = ++g_res_clock;
+      *hit = true;
+      return &e;
+    }
+    if (e.refs == 0 && (!victim || e.stamp < victim->stamp)) victim = &e;  // free ones: stamp 0
+  }
+  if (!victim) return nullptr;  // every entry in use by a call in flight
+  if (victim->device != dev || victim->cap < n) {
+    ORBX_RESOURCE_LOCK;
+    if (victim->d) (void)hipFree(victim->d);
+    victim->d = nullptr;
+    victim->cap = 0;
+    const int cap = std::max(1024, (n + 255) & ~255);
+    if (hipMalloc(&victim->d, ResEntry::bytes(cap)) != hipSuccess) {
+      victim->d = nullptr;
+      victim->device = -1;
+      victim->n = -1;
+      return nullptr;
+    }
+    victim->cap = cap;
+    victim->device = dev;
+  }
+  victim->n = n;
+  victim->ready = false;
+  victim->fv_n = -1;
+  victim->has_keys = false;
+  victim->h_desc.assign(desc, desc + bytes);
+  victim->refs = 1;
+  victim->stamp = ++g_res_clock;
+  *hit = false;
+  return victim;
+}
+
+void res_release(ResEntry* e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> lock(g_res_mutex);
+  e->refs--;
+}
+
+bool res_fv_matches(const ResEntry* e, const orbx_featvec& fv) {
+  std::lock_guard<std::mutex> lock(g_res_mutex);
+  if (e->fv_n != fv.n_nodes) return false;
+  const int nn = fv.n_nodes;
+  if (nn == 0) return true;
+  const int m = fv.node_offsets[nn];
+  return memcmp(e->h_ids.data(), fv.node_ids, (size_t)nn * 4) == 0 &&
+         memcmp(e->h_off.data(), fv.node_offsets, ((size_t)nn + 1) * 4) == 0 &&
+         (int)e->h_feats.size() == m && memcmp(e->h_feats.data(), fv.node_feats, (size_t)m * 4) == 0;
+}
+
+bool res_keys_match(const ResEntry* e, const orbx_keypoint* keys) {
+  std::lock_guard<std::mutex> lock(g_res_mutex);
+  return e->has_keys && memcmp(e->h_keys.data(), keys, sizeof(orbx_keypoint) * e->n) == 0;
+}
+
+void res_mark_filled(ResEntry* e, bool desc, const orbx_featvec* fv, const orbx_keypoint* keys) {
+  std::lock_guard<std::mutex> lock(g_res_mutex);
+  if (desc) e->ready = true;
+  if (fv) {
+    const int nn = fv->n_nodes, m = nn ? fv->node_offsets[nn] : 0;
+    e->h_ids.assign(fv->node_ids, fv->node_ids + nn);
+    e->h_off.assign(fv->node_offsets, fv->node_offsets + nn + 1);
+    if (nn == 0) e->h_off.assign(1, 0);
+    e->h_feats.assign(fv->node_feats, fv->node_feats + m);
+    e->fv_n = nn;
+  }
+  if (keys) {
+    e->h_keys.assign(keys, keys + e->n);
+    e->has_keys = true;
+  }
+}
+
+bool res_exclusive_without_fv(const ResEntry* e) {
+  std::lock_guard<std::mutex> lock(g_res_mutex);
+  return e->refs == 1 && e->fv_n < 0;
+}
+
+void res_invalidate(ResEntry* e) {
+  std::lock_guard<std::mutex> lock(g_res_mutex);
+  e->ready = false;
+  e->n = -1;
+  e->fv_n = -1;
+  e->has_keys = false;
+  e->stamp = 0;
+}
+
+namespace {
+struct ResScratchHolder {
+  ResScratch r;
+  ~ResScratchHolder() {
+    ORBX_RESOURCE_LOCK;
+    if (r.d) (void)hipFree(r.d);
+  }
+};
+thread_local ResScratchHolder tls_res;
+}  // namespace
+
+ResScratch* res_scratch(int cap) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (tls_ws.reserve(256) != ORBX_OK) return nullptr;  // the thread's stream
+  ResScratch& r = tls_res.r;
+  if (r.device != dev || r.cap < cap) {
+    ORBX_RESOURCE_LOCK;
+    if (r.d) (void)hipFree(r.d);
+    r.d = nullptr;
+    r.cap = 0;
+    const int c = std::max(4096, (cap + 1023) & ~1023);
+    if (hipMalloc(&r.d, ((size_t)3 * c + 16) * 4) != hipSuccess) {
+      r.d = nullptr;
+      r.device = -1;
+      return nullptr;
+    }
+    r.cap = c;
+    r.device = dev;
+    r.dirty = true;
+  }
+  if (r.dirty) {
+    hipStream_t s = tls_ws.stream;
+    if (hipMemsetAsync(r.match(), 0xFF, (size_t)r.cap * 4, s) != hipSuccess ||
+        hipMemsetAsync(r.matched2(), 0, (size_t)r.cap * 4, s) != hipSuccess ||
+        hipMemsetAsync(r.m12(), 0xFF, (size_t)r.cap * 4, s) != hipSuccess ||
+        hipMemsetAsync(r.ctrl(), 0, 16 * 4, s) != hipSuccess || wait_stream(s) != hipSuccess)
+      return nullptr;
+    r.dirty = false;
+  }
+  return &r;
+}
+
 }  // namespace orbx
 
 using namespace orbx;
@@ -1146,11 +1347,165 @@ DevSide dev_side(char* base, const SideOffs& o, const orbx_bow_side* s) {
   return d;
 }
 
+// A frame-cache entry held for the duration of a call, with what the call must still upload
+// into it (a whole block image staged at `up`: descriptors, FeatureVector and, for
+// SearchForTriangulation, keypoints).
+struct Held {
+  ResEntry* e = nullptr;
+  bool need_desc = false, need_fv = false, need_keys = false, committed = false;
+  size_t up = (size_t)-1, up_bytes = 0;
+  char* up_dst = nullptr;
+  Held() = default;
+  Held(const Held&) = delete;
+  ~Held() {
+    if (e && need() && !committed) res_invalidate(e);  // an upload that may not have landed
+    res_release(e);
+  }
+  bool need() const { return need_desc || need_fv || need_keys; }
+};
+
+bool res_enabled() {  // ORBX_NO_RESIDENT=1: every call takes the staged path (A/B runs)
+  static const bool on = getenv("ORBX_NO_RESIDENT") == nullptr;
+  return on;
+}
+
+// Finds (or claims) the entry of a side's descriptors and decides what to upload.  false: the
+// resident path does not apply (no entry free, or the FeatureVector / keypoints differ from an
+// entry another call is using).
+bool res_side(Held& h, int n, const uint8_t* desc, const orbx_featvec& fv, const orbx_keypoint* keys) {
+  bool hit = false;
+  h.e = res_acquire(n, desc, &hit);
+  if (!h.e) return false;
+  h.need_desc = !hit;
+  h.need_fv = !hit || !res_fv_matches(h.e, fv);
+  h.need_keys = keys && (!hit || !res_keys_match(h.e, keys));
+  if (hit && (h.need_fv || h.need_keys)) {  // rewriting a part another call may be reading
+    bool shared;
+    {
+      std::lock_guard<std::mutex> lock(g_res_mutex);
+      shared = h.e->refs > 1;
+    }
+    if (shared) return false;
+  }
+  return true;
+}
+
+// The block image of a side for an entry upload (desc | fv ids | offsets | feats | keypoints,
+// at the entry's capacity offsets).
+void stage_block(Stager& st, Held& h, int n, const uint8_t* desc, const orbx_featvec& fv,
+                 const orbx_keypoint* keys) {
+  if (!h.need()) return;
+  const int cap = h.e->cap;
+  if (!h.need_desc && !h.need_fv) {  // the keypoints alone (the current frame's first triangulation)
+    h.up_bytes = sizeof(orbx_keypoint) * n;
+    h.up = st.add(keys, h.up_bytes);
+    h.up_dst = (char*)h.e->d_keys();
+    return;
+  }
+  h.up_bytes = keys ? ResEntry::bytes(cap) : (size_t)cap * 32 + ResEntry::fv_bytes(cap);
+  h.up = st.add(nullptr, h.up_bytes);
+  h.up_dst = h.e->d;
+  char* b = st.host.data() + h.up;
+  memcpy(b, desc, (size_t)n * 32);
+  const int nn = fv.n_nodes, m = nn ? fv.node_offsets[nn] : 0;
+  if (nn) memcpy(b + (size_t)cap * 32, fv.node_ids, (size_t)nn * 4);
+  if (nn) memcpy(b + (size_t)cap * 36, fv.node_offsets, ((size_t)nn + 1) * 4);
+  if (m) memcpy(b + (size_t)cap * 40 + 4, fv.node_feats, (size_t)m * 4);
+  if (keys) memcpy(b + (size_t)cap * 44 + 16, keys, sizeof(orbx_keypoint) * n);
+}
+
+// after a successful call: the uploaded parts are now resident
+void commit_block(Held& h, const orbx_featvec& fv, const orbx_keypoint* keys) {
+  if (h.need()) res_mark_filled(h.e, h.need_desc, &fv, keys);
+  h.committed = true;
+}
+
+// SearchByBoW with both sides' descriptors and FeatureVectors resident in the frame cache (a side
+// seen for the first time is uploaded into its entry, one copy), the per-call arrays (angles,
+// validity, the problem) read by the kernels from the thread's pinned stager and the results
+// written by the finish into it: in the per-frame chain no copy kernel runs at all.
+// ORBX_EUNSUPPORTED: not applicable, the caller takes the staged path.
+int run_bow_resident(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int check_ori,
+                     int mode, int32_t* match_out, int32_t* nmatches) {
+  if (s1->n <= 0 || s2->n <= 0 || s1->n > kResMaxFeatures || s2->n > kResMaxFeatures)
+    return ORBX_EUNSUPPORTED;
+  const int nout = mode == 1 ? s1->n : s2->n;
+  Held h1, h2;
+  if (!res_side(h1, s1->n, s1->desc, s1->fv, nullptr) || !res_side(h2, s2->n, s2->desc, s2->fv, nullptr))
+    return ORBX_EUNSUPPORTED;
+  if (h1.e == h2.e) return ORBX_EUNSUPPORTED;  // the same frame on both sides
+  ResScratch* rs = res_scratch(std::max(s1->n, s2->n));
+  if (!rs) return ORBX_EUNSUPPORTED;
+  Stager st;
+  stage_block(st, h1, s1->n, s1->desc, s1->fv, nullptr);
+  stage_block(st, h2, s2->n, s2->desc, s2->fv, nullptr);
+  // the per-call arrays and the problem: one upload into the workspace (read by every
+  // workgroup: over PCIe from the stager they put a round trip on each one's critical path)
+  const size_t osmall = (st.host.size() + 15) & ~size_t(15);
+  const size_t oa1 = st.add(s1->angle, (size_t)s1->n * 4), oa2 = st.add(s2->angle, (size_t)s2->n * 4);
+  const size_t ov1 = s1->valid ? st.add(s1->valid, (size_t)s1->n) : (size_t)-1;
+  const size_t ov2 = s2->valid ? st.add(s2->valid, (size_t)s2->n) : (size_t)-1;
+  const size_t oprob = st.add(nullptr, sizeof(BowProblem));
+  const size_t osmall_end = st.host.size();
+  const size_t omatch = st.add(nullptr, (size_t)nout * 4), octrl = st.add(nullptr, 16);
+  char* hb = st.host.data();  // final: every add is done
+  if (!st.host.pinned) return ORBX_EUNSUPPORTED;
+  if (tls_ws.reserve(osmall_end - osmall) != ORBX_OK) return ORBX_EUNSUPPORTED;
+  char* db = tls_ws.d - osmall;  // device address of stager offset o: db + o
+  auto side = [&](const orbx_bow_side* sd, const Held& h, size_t oa, size_t ov) {
+    DevSide d{};
+    d.n = sd->n;
+    d.desc = h.e->d_desc();
+    d.angle = (const float*)(db + oa);
+    d.angle_stride = 1;
+    d.valid = ov == (size_t)-1 ? nullptr : (const uint8_t*)(db + ov);
+    d.n_nodes = sd->fv.n_nodes;
+    d.node_ids = h.e->d_ids();
+    d.node_offsets = h.e->d_off();
+    d.node_feats = h.e->d_feats();
+    return d;
+  };
+  BowProblem P{};
+  P.s1 = side(s1, h1, oa1, ov1);
+  P.s2 = side(s2, h2, oa2, ov2);
+  P.match = rs->match();
+  P.matched2 = rs->matched2();
+  P.done = rs->ctrl() + 0;
+  P.error = rs->ctrl() + 1;
+  P.count = rs->ctrl() + 4;
+  P.mode = mode;
+  P.nnratio = nnratio;
+  P.check_ori = check_ori;
+  P.match_host = (int*)(hb + omatch);
+  P.ctrl_host = (int*)(hb + octrl);
+  memcpy(hb + oprob, &P, sizeof(P));
+  hipStream_t s = tls_ws.stream;
+  rs->dirty = true;  // until the finish has restored it
+  for (Held* h : {&h1, &h2})
+    if (h->need()) ORBX_HIP(queue_copy(h->up_dst, hb + h->up, h->up_bytes, s));
+  ORBX_HIP(queue_copy(db + osmall, hb + osmall, osmall_end - osmall, s));
+  int rc = launch_bow((const BowProblem*)(db + oprob), 1, s1->fv.n_nodes, s, true);
+  if (rc) return rc;
+  ORBX_HIP(orbx::wait_stream(s));
+  rs->dirty = false;
+  commit_block(h1, s1->fv, nullptr);
+  commit_block(h2, s2->fv, nullptr);
+  const int* res = (const int*)(hb + octrl);
+  if (res[1]) return report(ORBX_EDEVICE, "SearchByBoW: a match index outside the keyframe");
+  memcpy(match_out, hb + omatch, (size_t)nout * 4);
+  *nmatches = res[0];
+  return ORBX_OK;
+}
+
 int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int check_ori,
             int mode, int32_t* match_out, int32_t* nmatches) {
   if (!side_ok(s1) || !side_ok(s2) || !match_out || !nmatches) return ORBX_EINVAL;
   if (!fv_ok(s1->fv, s1->n) || !fv_ok(s2->fv, s2->n)) return ORBX_EINVAL;
   if (s2->n >= kBowMaxSide2) return report(ORBX_EUNSUPPORTED, "SearchByBoW: side 2 above 2^23 features");
+  if (res_enabled()) {
+    const int rr = run_bow_resident(s1, s2, nnratio, check_ori, mode, match_out, nmatches);
+    if (rr != ORBX_EUNSUPPORTED) return rr;
+  }
   const int nout = mode == 1 ? s1->n : s2->n;
   Stager st;
   SideOffs o1 = stage_side(st, s1), o2 = stage_side(st, s2);
@@ -1189,6 +1544,91 @@ int run_bow(const orbx_bow_side* s1, const orbx_bow_side* s2, float nnratio, int
   return ORBX_OK;
 }
 
+// SearchForTriangulation with both keyframes' descriptors, FeatureVectors and keypoints
+// resident in the frame cache (run_bow_resident's scheme; the level tables travel inside the
+// problem, mvuRight and the map-point flags are read from the pinned stager).
+int tri_resident(const orbx_tri_side* k1, const orbx_tri_side* k2, const float F12[9], float ex,
+                 float ey, int only_stereo, int check_ori, int32_t* pairs, int32_t* nmatches) {
+  if (k1->n <= 0 || k2->n <= 0 || k1->n > kResMaxFeatures || k2->n > kResMaxFeatures ||
+      k1->nlevels > 16 || k2->nlevels > 16)
+    return ORBX_EUNSUPPORTED;
+  Held h1, h2;
+  if (!res_side(h1, k1->n, k1->desc, k1->fv, nullptr) || !res_side(h2, k2->n, k2->desc, k2->fv, nullptr))
+    return ORBX_EUNSUPPORTED;
+  if (h1.e == h2.e) return ORBX_EUNSUPPORTED;
+  ResScratch* rs = res_scratch(std::max(k1->n, k2->n));
+  if (!rs) return ORBX_EUNSUPPORTED;
+  Stager st;
+  stage_block(st, h1, k1->n, k1->desc, k1->fv, nullptr);
+  stage_block(st, h2, k2->n, k2->desc, k2->fv, nullptr);
+  const orbx_tri_side* ks[2] = {k1, k2};
+  // the per-call arrays (keypoints, mvuRight, map-point flags) and the problem: one upload
+  const size_t osmall = (st.host.size() + 15) & ~size_t(15);
+  size_t okeys[2], our[2], omp[2];
+  for (int i = 0; i < 2; i++) {
+    okeys[i] = st.add(ks[i]->keys_un, sizeof(orbx_keypoint) * ks[i]->n);
+    our[i] = ks[i]->u_right ? st.add(ks[i]->u_right, (size_t)ks[i]->n * 4) : (size_t)-1;
+    omp[i] = ks[i]->has_mp ? st.add(ks[i]->has_mp, (size_t)ks[i]->n) : (size_t)-1;
+  }
+  const size_t oprob = st.add(nullptr, sizeof(TriProblem));
+  const size_t osmall_end = st.host.size();
+  const size_t opairs = st.add(nullptr, (size_t)k1->n * 8), octrl = st.add(nullptr, 16);
+  if (!st.host.pinned) return ORBX_EUNSUPPORTED;
+  if (tls_ws.reserve(osmall_end - osmall) != ORBX_OK) return ORBX_EUNSUPPORTED;
+  char* hb = st.host.data();
+  char* db = tls_ws.d - osmall;
+  TriProblem P{};
+  DevTriSide* ds[2] = {&P.s1, &P.s2};
+  const Held* hs[2] = {&h1, &h2};
+  for (int i = 0; i < 2; i++) {
+    const orbx_tri_side* k = ks[i];
+    const ResEntry* e = hs[i]->e;
+    DevTriSide& d = *ds[i];
+    d.n = k->n;
+    d.desc = e->d_desc();
+    d.keys_un = (const orbx_keypoint*)(db + okeys[i]);
+    d.u_right = our[i] == (size_t)-1 ? nullptr : (const float*)(db + our[i]);
+    d.has_mp = omp[i] == (size_t)-1 ? nullptr : (const uint8_t*)(db + omp[i]);
+    d.fv.n_nodes = k->fv.n_nodes;
+    d.fv.node_ids = e->d_ids();
+    d.fv.node_offsets = e->d_off();
+    d.fv.node_feats = e->d_feats();
+    for (int l = 0; l < k->nlevels; l++) {
+      P.tab[2 * i][l] = k->scale_factors[l];
+      P.tab[2 * i + 1][l] = k->level_sigma2[l];
+    }
+  }
+  P.tab_inline = 1;
+  memcpy(P.F, F12, 36);
+  P.ex = ex;
+  P.ey = ey;
+  P.only_stereo = only_stereo;
+  P.check_ori = check_ori;
+  P.m12 = rs->m12();
+  P.done = rs->ctrl() + 2;
+  P.error = rs->ctrl() + 3;
+  P.count = rs->ctrl() + 5;
+  P.pairs_host = (int*)(hb + opairs);
+  P.ctrl_host = (int*)(hb + octrl);
+  memcpy(hb + oprob, &P, sizeof(P));
+  hipStream_t s = tls_ws.stream;
+  rs->dirty = true;
+  for (Held* h : {&h1, &h2})
+    if (h->need()) ORBX_HIP(queue_copy(h->up_dst, hb + h->up, h->up_bytes, s));
+  ORBX_HIP(queue_copy(db + osmall, hb + osmall, osmall_end - osmall, s));
+  int rc = launch_tri((const TriProblem*)(db + oprob), 1, k1->fv.n_nodes, s, true);
+  if (rc) return rc;
+  ORBX_HIP(orbx::wait_stream(s));
+  rs->dirty = false;
+  commit_block(h1, k1->fv, nullptr);
+  commit_block(h2, k2->fv, nullptr);
+  const int* res = (const int*)(hb + octrl);
+  if (res[1]) return report(ORBX_EDEVICE, "SearchForTriangulation: a match index outside KF2");
+  if (res[0] > 0) memcpy(pairs, hb + opairs, (size_t)res[0] * 8);
+  *nmatches = res[0];
+  return ORBX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1218,6 +1658,10 @@ int orbx_search_for_triangulation(const orbx_tri_side* k1, const orbx_tri_side* 
       if (k->keys_un[i].octave < 0 || k->keys_un[i].octave >= k->nlevels) return ORBX_EINVAL;
   }
   if (!F12 || !pairs || !nmatches) return ORBX_EINVAL;
+  if (res_enabled()) {
+    const int rr = tri_resident(k1, k2, F12, ex, ey, only_stereo, check_ori, pairs, nmatches);
+    if (rr != ORBX_EUNSUPPORTED) return rr;
+  }
   Stager st;
   size_t o[2][9];
   for (int s = 0; s < 2; s++) {

@@ -27,6 +27,21 @@ struct VocRanks {
   uint32_t* d_rank_ids = nullptr;      // [nb] node id of rank b
 };
 
+// Pinned-host mirrors of a one-image call's outputs (the resident drop-in transform): the
+// kernels write them beside their device outputs, so no download copy runs.  All nullable.
+struct VocHostOut {
+  uint8_t* desc_copy;                     // k_voc_transform: the descriptors it read (device)
+  uint32_t* word_of;                      // k_voc_transform: word id, FeatureVector node id
+  uint32_t* node_of;
+  uint32_t* words;                        // k_bowfv: BowVector
+  double* values;
+  int* nwords;
+  uint32_t* ids;                          // k_bowfv: FeatureVector CSR
+  int* off;
+  int* feats;
+  int* nn;
+};
+
 int vocab_view(const orbx_vocabulary* voc, VocView* v, int* device);
 int vocab_ranks(const orbx_vocabulary* voc, int levelsup, const VocRanks** out);
 
@@ -36,7 +51,7 @@ int launch_voc_transform(const VocView& V, int nid_level, const uint32_t* d_rank
                          const uint8_t* d_desc, int64_t desc_stride_img, const int* d_counts,
                          int n_fixed, int max_n, uint32_t* d_word_of, uint32_t* d_rank_of,
                          uint32_t* d_node_of, double* d_weight_of, int64_t out_stride_img,
-                         int nimg, hipStream_t s);
+                         int nimg, hipStream_t s, const VocHostOut& ho = VocHostOut{});
 // BowVector of every image from the word ids and weights (TemplatedVocabulary.h:1144-1197).
 // max_n <= 8192.
 int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
@@ -52,6 +67,6 @@ int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word
                  const int* d_counts, int n_fixed, int max_n, uint32_t* d_words, double* d_values,
                  int64_t out_stride, int* d_nwords, int nb, const uint32_t* d_rank_ids,
                  uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride, int* d_nn,
-                 int nimg, hipStream_t s);
+                 int nimg, hipStream_t s, const VocHostOut& ho = VocHostOut{});
 
 }  // namespace orbx

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void k_voc_transform(VocView V, int nid_level,
                                                        uint32_t* __restrict__ rank_out,
                                                        uint32_t* __restrict__ node_out,
                                                        double* __restrict__ weight_out,
-                                                       int64_t out_stride) {
+                                                       int64_t out_stride, VocHostOut ho) {
   const int img = blockIdx.y, tid = threadIdx.x;
   const int c = tid & (G - 1);
   const int f = blockIdx.x * (256 / G) + tid / G;
@@ -125,12 +125,19 @@ __global__ __launch_bounds__(256) void k_voc_transform(VocView V, int nid_level,
     }
   }
   if (!active || c != 0) return;
+  if (ho.desc_copy) {  // one-image calls: the descriptors into the frame cache's entry
+    uint4* q = (uint4*)(ho.desc_copy + (int64_t)f * 32);
+    q[0] = make_uint4((uint32_t)d[0], (uint32_t)(d[0] >> 32), (uint32_t)d[1], (uint32_t)(d[1] >> 32));
+    q[1] = make_uint4((uint32_t)d[2], (uint32_t)(d[2] >> 32), (uint32_t)d[3], (uint32_t)(d[3] >> 32));
+  }
   const int64_t o = img * out_stride + f;
   if (V.n_words == 0) {  // transform: if(empty()) return;
     word_out[o] = 0xFFFFFFFFu;
     rank_out[o] = 0xFFFFFFFFu;
     if (node_out) node_out[o] = 0xFFFFFFFFu;
     weight_out[o] = 0;
+    if (ho.word_of) ho.word_of[f] = 0xFFFFFFFFu;
+    if (ho.node_of) ho.node_of[f] = 0xFFFFFFFFu;
     return;
   }
   if (nid == 0xFFFFFFFFu) nid = (uint32_t)node;  // leaf above L - levelsup (header)
@@ -140,6 +147,8 @@ __global__ __launch_bounds__(256) void k_voc_transform(VocView V, int nid_level,
   word_out[o] = keep ? (uint32_t)word : 0xFFFFFFFFu;
   rank_out[o] = keep ? rank_of_node[nid] : 0xFFFFFFFFu;
   if (node_out) node_out[o] = keep ? nid : 0xFFFFFFFFu;
+  if (ho.word_of) ho.word_of[f] = keep ? (uint32_t)word : 0xFFFFFFFFu;
+  if (ho.node_of) ho.node_of[f] = keep ? nid : 0xFFFFFFFFu;
 }
 
 // ------------------------------------------------------------------ k_bowvec
@@ -325,18 +334,18 @@ int launch_voc_transform(const VocView& V, int nid_level, const uint32_t* d_rank
                          const uint8_t* d_desc, int64_t desc_stride_img, const int* d_counts,
                          int n_fixed, int max_n, uint32_t* d_word_of, uint32_t* d_rank_of,
                          uint32_t* d_node_of, double* d_weight_of, int64_t out_stride_img,
-                         int nimg, hipStream_t s) {
+                         int nimg, hipStream_t s, const VocHostOut& ho) {
   if (max_n <= 0 || nimg <= 0) return ORBX_OK;
   if (V.k <= 16) {
     note_kernel("k_voc_transform<16>");
     hipLaunchKernelGGL(k_voc_transform<16>, dim3((max_n + 15) / 16, nimg), dim3(256), 0, s, V,
                        nid_level, d_rank_of_node, d_desc, desc_stride_img, d_counts, n_fixed,
-                       d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img);
+                       d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img, ho);
   } else if (V.k <= 32) {
     note_kernel("k_voc_transform<32>");
     hipLaunchKernelGGL(k_voc_transform<32>, dim3((max_n + 7) / 8, nimg), dim3(256), 0, s, V,
                        nid_level, d_rank_of_node, d_desc, desc_stride_img, d_counts, n_fixed,
-                       d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img);
+                       d_word_of, d_rank_of, d_node_of, d_weight_of, out_stride_img, ho);
   } else {
     return ORBX_EUNSUPPORTED;
   }
@@ -467,7 +476,8 @@ __global__ __launch_bounds__(256) void k_bowfv(int must, int l1, int tf,
                                                const uint32_t* __restrict__ rank_ids,
                                                uint32_t* __restrict__ node_ids,
                                                int* __restrict__ offsets, int* __restrict__ feats,
-                                               int64_t feats_stride, int* __restrict__ n_nodes) {
+                                               int64_t feats_stride, int* __restrict__ n_nodes,
+                                               VocHostOut ho) {
   constexpr int R = 64 * NPL, CAP = 4 * R;
   constexpr int IB = __builtin_ctz(CAP);
   constexpr uint32_t IMASK = (1u << IB) - 1u;
@@ -585,10 +595,13 @@ __global__ __launch_bounds__(256) void k_bowfv(int must, int l1, int tf,
       for (int j = s0 + 1; j < s1; j++) v += s_wt[mA[j] & IMASK];  // addWeight, feature order
     if (tf && !must) v /= (double)nu;  // TemplatedVocabulary.h:1165-1172
     ow[o] = x >> IB;
-    if (must)
+    if (ho.words) ho.words[o] = x >> IB;
+    if (must) {
       s_val[o] = v;
-    else
+    } else {
       ov[o] = v;
+      if (ho.values) ho.values[o] = v;
+    }
   }
   {
     uint32_t* oid = node_ids + (int64_t)img * nb;
@@ -596,14 +609,25 @@ __global__ __launch_bounds__(256) void k_bowfv(int must, int l1, int tf,
     int* of = feats + img * feats_stride;
     for (int q = tid; q < nn; q += 256) {
       const int j = s_nstart[q];
-      oid[q] = rank_ids[mB[j] >> IB];
+      const uint32_t id = rank_ids[mB[j] >> IB];
+      oid[q] = id;
       ooff[q] = j;
+      if (ho.ids) {
+        ho.ids[q] = id;
+        ho.off[q] = j;
+      }
     }
-    for (int j = tid; j < m_b; j += 256) of[j] = (int)(mB[j] & IMASK);
+    for (int j = tid; j < m_b; j += 256) {
+      of[j] = (int)(mB[j] & IMASK);
+      if (ho.feats) ho.feats[j] = (int)(mB[j] & IMASK);
+    }
     if (tid == 0) {
       ooff[nn] = m_b;
       n_nodes[img] = nn;
       out_n[img] = nu;
+      if (ho.off) ho.off[nn] = m_b;
+      if (ho.nn) *ho.nn = nn;
+      if (ho.nwords) *ho.nwords = nu;
     }
   }
   if (!must) return;
@@ -636,7 +660,11 @@ __global__ __launch_bounds__(256) void k_bowfv(int must, int l1, int tf,
   }
   __syncthreads();
   const double norm = s_norm;
-  for (int o = tid; o < nu; o += 256) ov[o] = norm > 0.0 ? s_val[o] / norm : s_val[o];
+  for (int o = tid; o < nu; o += 256) {
+    const double v = norm > 0.0 ? s_val[o] / norm : s_val[o];
+    ov[o] = v;
+    if (ho.values) ho.values[o] = v;
+  }
 }
 
 template <int NPL>
@@ -645,7 +673,7 @@ static int launch_bowfv_t(int must, int l1, int tf, const uint32_t* d_word_of,
                           const int* d_counts, int n_fixed, uint32_t* d_words, double* d_values,
                           int64_t out_stride, int* d_nwords, int nb, const uint32_t* d_rank_ids,
                           uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride,
-                          int* d_nn, int nimg, hipStream_t s) {
+                          int* d_nn, int nimg, hipStream_t s, const VocHostOut& ho) {
   constexpr int CAP = 256 * NPL;
   constexpr size_t smem = (size_t)CAP * 32 + 32;  // runs, merged orders, weights, run starts
   if constexpr (smem > 64 * 1024) {
@@ -661,7 +689,7 @@ static int launch_bowfv_t(int must, int l1, int tf, const uint32_t* d_word_of,
   hipLaunchKernelGGL(k_bowfv<NPL>, dim3(nimg), dim3(256), smem, s, must, l1, tf, d_word_of,
                      d_rank_of, d_weight_of, in_stride, d_counts, n_fixed, d_words, d_values,
                      out_stride, d_nwords, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride,
-                     d_nn);
+                     d_nn, ho);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ORBX_OK : report_hip(e, "launch_bowfv");
 }
@@ -671,7 +699,7 @@ int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word
                  const int* d_counts, int n_fixed, int max_n, uint32_t* d_words, double* d_values,
                  int64_t out_stride, int* d_nwords, int nb, const uint32_t* d_rank_ids,
                  uint32_t* d_ids, int* d_off, int* d_feats, int64_t feats_stride, int* d_nn,
-                 int nimg, hipStream_t s) {
+                 int nimg, hipStream_t s, const VocHostOut& ho) {
   if (!d_rank_ids || nb < 1) return ORBX_EUNSUPPORTED;
   if (nimg <= 0) return ORBX_OK;
   const int must = scoring != ORBX_SCORE_DOT_PRODUCT;
@@ -685,7 +713,7 @@ int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word
 #define ORBX_BOWFV_ARGS                                                                        \
   must, l1, tf, d_word_of, d_rank_of, d_weight_of, in_stride, d_counts, n_fixed, d_words,     \
       d_values, out_stride, d_nwords, nb, d_rank_ids, d_ids, d_off, d_feats, feats_stride, d_nn, \
-      nimg, s
+      nimg, s, ho
   if (fits(1024, 10)) return launch_bowfv_t<4>(ORBX_BOWFV_ARGS);
   if (fits(2048, 11)) return launch_bowfv_t<8>(ORBX_BOWFV_ARGS);
   if (fits(4096, 12)) return launch_bowfv_t<16>(ORBX_BOWFV_ARGS);
@@ -954,6 +982,107 @@ int orbx_vocabulary_info(const orbx_vocabulary* V, int32_t* k, int32_t* L, int32
   return ORBX_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Frame::ComputeBoW of the per-frame chain on the frame cache (orbx_match.h): the descriptors are
+// read by k_voc_transform from the thread's pinned stager and copied into the frame's entry as
+// they are read (a frame seen before reads them from HBM), the FeatureVector is written into the
+// entry for the matchers that follow, and every output the caller wants is written by the kernels
+// into the pinned stager as well: no copy kernel.  ORBX_EUNSUPPORTED: the staged path applies.
+int transform_resident(const orbx_vocabulary* V, const VocView& view, const VocRanks* R,
+                       const uint8_t* desc, int n, int levelsup, uint32_t* word_of,
+                       uint32_t* node_of, uint32_t* bow_words, double* bow_values, int32_t* bow_n,
+                       uint32_t* fv_node_ids, int32_t* fv_offsets, int32_t* fv_feats,
+                       int32_t* fv_n) {
+  if (n <= 0 || n > 4096 || getenv("ORBX_NO_RESIDENT")) return ORBX_EUNSUPPORTED;
+  bool hit = false;
+  ResEntry* e = res_acquire(n, desc, &hit);
+  if (!e) return ORBX_EUNSUPPORTED;
+  struct Guard {
+    ResEntry* e;
+    bool ok = false, fill = false;
+    ~Guard() {
+      if (fill && !ok) res_invalidate(e);
+      res_release(e);
+    }
+  } g{e};
+  g.fill = !hit;
+  // the FeatureVector goes into the entry when no other call can be reading it there
+  const bool own_fv = !hit || res_exclusive_without_fv(e);
+  const int nn = std::max(n, 1);
+  Stager st;
+  const size_t od = hit ? (size_t)-1 : st.add(desc, (size_t)n * 32);
+  const size_t ohw = word_of ? st.add(nullptr, (size_t)nn * 4) : (size_t)-1;
+  const size_t ohn = node_of ? st.add(nullptr, (size_t)nn * 4) : (size_t)-1;
+  const size_t obw = st.add(nullptr, (size_t)nn * 4), obv = st.add(nullptr, (size_t)nn * 8),
+               obn = st.add(nullptr, 4), ofi = st.add(nullptr, (size_t)nn * 4),
+               ofo = st.add(nullptr, ((size_t)nn + 1) * 4), off = st.add(nullptr, (size_t)nn * 4),
+               ofn = st.add(nullptr, 4);
+  if (!st.host.pinned) return ORBX_EUNSUPPORTED;
+  char* hb = st.host.data();
+  // device scratch: word, rank, weight per feature, the BowVector and, when the entry's is
+  // not ours to write, the FeatureVector
+  const size_t dw = 0, dr = dw + (size_t)nn * 4, dwt = (dr + (size_t)nn * 4 + 15) & ~size_t(15),
+               dbw = dwt + (size_t)nn * 8, dbv = (dbw + (size_t)nn * 4 + 15) & ~size_t(15),
+               dbn = dbv + (size_t)nn * 8, dfi = dbn + 16, dfo = dfi + (size_t)nn * 4,
+               dff = dfo + ((size_t)nn + 1) * 4 + 12, dfn = dff + (size_t)nn * 4, dend = dfn + 16;
+  int rc = tls_ws.reserve(dend);
+  if (rc) return rc;
+  char* base = tls_ws.d;
+  hipStream_t s = tls_ws.stream;
+  VocHostOut ho{};
+  ho.desc_copy = hit ? nullptr : e->d_desc();
+  ho.word_of = ohw == (size_t)-1 ? nullptr : (uint32_t*)(hb + ohw);
+  ho.node_of = ohn == (size_t)-1 ? nullptr : (uint32_t*)(hb + ohn);
+  rc = launch_voc_transform(view, V->L - levelsup, R->d_rank_of_node,
+                            hit ? e->d_desc() : (const uint8_t*)(hb + od), 0, nullptr, n, n,
+                            dptr<uint32_t>(base, dw), dptr<uint32_t>(base, dr), nullptr,
+                            dptr<double>(base, dwt), 0, 1, s, ho);
+  if (rc) return rc;
+  VocHostOut hb2{};
+  hb2.words = (uint32_t*)(hb + obw);
+  hb2.values = (double*)(hb + obv);
+  hb2.nwords = (int*)(hb + obn);
+  hb2.ids = (uint32_t*)(hb + ofi);
+  hb2.off = (int*)(hb + ofo);
+  hb2.feats = (int*)(hb + off);
+  hb2.nn = (int*)(hb + ofn);
+  rc = launch_bowfv(V->scoring, V->weighting, V->n_words, dptr<uint32_t>(base, dw),
+                    dptr<uint32_t>(base, dr), dptr<double>(base, dwt), 0, nullptr, n, n,
+                    dptr<uint32_t>(base, dbw), dptr<double>(base, dbv), 0, dptr<int>(base, dbn),
+                    R->nb, R->d_rank_ids, own_fv ? e->d_ids() : dptr<uint32_t>(base, dfi),
+                    own_fv ? e->d_off() : dptr<int>(base, dfo),
+                    own_fv ? e->d_feats() : dptr<int>(base, dff), 0, dptr<int>(base, dfn), 1, s,
+                    hb2);
+  if (rc == ORBX_EUNSUPPORTED) {  // the descriptor copy may be in flight: let it land
+    ORBX_HIP(orbx::wait_stream(s));
+    return ORBX_EUNSUPPORTED;
+  }
+  if (rc) return rc;
+  ORBX_HIP(orbx::wait_stream(s));
+  const int nb = *(const int*)(hb + obn), nf = *(const int*)(hb + ofn);
+  memcpy(bow_words, hb + obw, (size_t)nb * 4);
+  memcpy(bow_values, hb + obv, (size_t)nb * 8);
+  *bow_n = nb;
+  memcpy(fv_node_ids, hb + ofi, (size_t)nf * 4);
+  memcpy(fv_offsets, hb + ofo, ((size_t)nf + 1) * 4);
+  const int nfeat = ((const int*)(hb + ofo))[nf];
+  memcpy(fv_feats, hb + off, (size_t)nfeat * 4);
+  *fv_n = nf;
+  if (word_of) memcpy(word_of, hb + ohw, (size_t)n * 4);
+  if (node_of) memcpy(node_of, hb + ohn, (size_t)n * 4);
+  orbx_featvec fv{nf, fv_node_ids, fv_offsets, fv_feats};
+  res_mark_filled(e, !hit, own_fv ? &fv : nullptr, nullptr);
+  g.ok = true;
+  return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int orbx_vocabulary_transform(const orbx_vocabulary* V, const uint8_t* desc, int32_t n,
                               int32_t levelsup, uint32_t* word_of, uint32_t* node_of,
                               uint32_t* bow_words, double* bow_values, int32_t* bow_n,
@@ -969,6 +1098,11 @@ int orbx_vocabulary_transform(const orbx_vocabulary* V, const uint8_t* desc, int
   if (R->nb > 8192) return ORBX_EUNSUPPORTED;  // k_csr buckets live in LDS
   VocView view;
   vocab_view(V, &view, nullptr);
+  {
+    const int rr = transform_resident(V, view, R, desc, n, levelsup, word_of, node_of, bow_words,
+                                      bow_values, bow_n, fv_node_ids, fv_offsets, fv_feats, fv_n);
+    if (rr != ORBX_EUNSUPPORTED) return rr;
+  }
   const int nn = std::max(n, 1);
   Stager st;
   const size_t od = st.add(desc, (size_t)n * 32);
