@@ -243,6 +243,8 @@ extern thread_local Workspace tls_ws;
 // Tracking::Reset).  Entries are claimed least-recently-used; one in use by a call in flight is
 // never reclaimed.
 constexpr int kResEntries = 16;
+// false when ORBX_NO_RESIDENT is set: every call takes the staged per-call copies (A/B runs)
+bool res_enabled();
 constexpr int kResMaxFeatures = 8192;
 struct ResEntry {
   int device = -1;

@@ -1154,6 +1154,11 @@ ResEntry g_res[kResEntries];
 uint64_t g_res_clock = 0;
 }  // namespace
 
+bool res_enabled() {  // ORBX_NO_RESIDENT=1: every call takes the staged path (A/B runs)
+  static const bool on = getenv("ORBX_NO_RESIDENT") == nullptr;
+  return on;
+}
+
 ResEntry* res_acquire(int n, const uint8_t* desc, bool* hit) {
   if (n <= 0 || n > kResMaxFeatures || !desc || !hit) return nullptr;
   int dev = 0;
@@ -1364,10 +1369,7 @@ struct Held {
   bool need() const { return need_desc || need_fv || need_keys; }
 };
 
-bool res_enabled() {  // ORBX_NO_RESIDENT=1: every call takes the staged path (A/B runs)
-  static const bool on = getenv("ORBX_NO_RESIDENT") == nullptr;
-  return on;
-}
+
 
 // Finds (or claims) the entry of a side's descriptors and decides what to upload.  false: the
 // resident path does not apply (no entry free, or the FeatureVector / keypoints differ from an

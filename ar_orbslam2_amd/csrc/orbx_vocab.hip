@@ -996,7 +996,7 @@ int transform_resident(const orbx_vocabulary* V, const VocView& view, const VocR
                        uint32_t* node_of, uint32_t* bow_words, double* bow_values, int32_t* bow_n,
                        uint32_t* fv_node_ids, int32_t* fv_offsets, int32_t* fv_feats,
                        int32_t* fv_n) {
-  if (n <= 0 || n > 4096 || getenv("ORBX_NO_RESIDENT")) return ORBX_EUNSUPPORTED;
+  if (n <= 0 || n > 4096 || !res_enabled()) return ORBX_EUNSUPPORTED;
   bool hit = false;
   ResEntry* e = res_acquire(n, desc, &hit);
   if (!e) return ORBX_EUNSUPPORTED;

@@ -23,8 +23,7 @@ SHIFT_F = np.array([[0, 0, -1], [0, 0, 1], [1, -1, 0]], np.float32)
 N_ENTRIES = 16  # kResEntries
 
 
-@pytest.fixture(scope="module")
-def chain():
+def _chain():
     p = O.params(1000)
     voc = vocab_desc()
     v = Vocabulary.complete(10, 6, voc)
@@ -40,6 +39,11 @@ def chain():
             valid=(rng.random(n) < 0.6).astype(np.uint8), has_mp=(rng.random(n) < 0.4).astype(np.uint8),
             mvuRight=np.full(n, -1.0, np.float32), mvScaleFactors=t["scale"], mvLevelSigma2=t["sigma2"]))
     return frames, v
+
+
+@pytest.fixture(scope="module")
+def chain():
+    return _chain()
 
 
 def _bow_side(kf, valid=True):

@@ -1,11 +1,13 @@
-"""The library's two remaining environment switches, each run in a process of its own and checked
-against the oracle (every other kernel selector was removed in round 4: `grep getenv
-ar_orbslam2_amd/csrc` lists exactly these two).
+"""The library's environment switches, each run in a process of its own and checked against the
+oracle (every other kernel selector was removed in round 4: `grep getenv ar_orbslam2_amd/csrc`
+lists exactly these).
   ORBX_SPIN_US      how long a one-call (drop-in) wait polls its stream before blocking; 0 blocks
                     at once (orbx_geometry.cpp wait_stream)
   ORBX_SYNC_STAGES  debugging: a frame pipeline runs eagerly (no captured graph), synchronising
                     after every stage to name the stage of an asynchronous fault
-                    (orbx_frames.hip, orbx_internal.h Profiler::mark)"""
+                    (orbx_frames.hip, orbx_internal.h Profiler::mark)
+  ORBX_NO_RESIDENT  the per-frame drop-in calls take the staged per-call copies instead of the
+                    resident frame cache (orbx_match.h; A/B runs of bench.py --dropin)"""
 import os
 import re
 import subprocess
@@ -68,7 +70,7 @@ def test_switch_list_is_exactly_the_tested_ones():
         for f in files:
             if f.endswith((".hip", ".h", ".cpp")):
                 found |= set(re.findall(r'getenv\("(\w+)"\)', open(os.path.join(root, f)).read()))
-    assert found == {"ORBX_SPIN_US", "ORBX_SYNC_STAGES"}
+    assert found == {"ORBX_SPIN_US", "ORBX_SYNC_STAGES", "ORBX_NO_RESIDENT"}
 
 
 @pytest.mark.gpu
@@ -82,3 +84,20 @@ def test_spin_us_drop_in_extraction(spin):
 @pytest.mark.timeout(300)
 def test_sync_stages_pipeline():
     _run(_PIPELINE, {"ORBX_SYNC_STAGES": "1"})
+
+
+_CHAIN = r"""
+import sys
+sys.path.insert(0, "tests")
+import test_resident_gpu as T
+frames, v = T._chain()
+T.test_chain_with_reference_keyframes_and_evictions((frames, v))
+T.test_other_featurevector_and_keypoints_for_resident_descriptors((frames, v))
+print("SWITCH-OK", len(frames))
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_no_resident_drop_in_chain():
+    _run(_CHAIN, {"ORBX_NO_RESIDENT": "1"})
