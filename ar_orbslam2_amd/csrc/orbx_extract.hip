@@ -1302,6 +1302,22 @@ constexpr int kOctBins = 1024;        // bins per (image, level) at least: batch
 constexpr int kOctBinsFew = 8192;     // few-image plans and the 1024-thread instance
 constexpr size_t kOctMaxSmem = 150 * 1024;  // dynamic LDS of one octree workgroup
 
+#ifdef ORBX_OCT_PROF  // experiment builds only: per-phase workgroup time of k_octree (s_memtime)
+__device__ unsigned long long g_oct_prof[8 * 16];
+#define OP_NOW() __builtin_amdgcn_s_memtime()
+#define OP_ADD(i, x) (opf[i] += (x))
+#else
+#define OP_NOW() 0ull
+#define OP_ADD(i, x) ((void)(x))
+#endif
+
+#ifdef ORBX_OCT_PROF
+__device__ unsigned long long g_oct_sub[8];  // oct_refine's steps, level 0 only
+#define OS_MARK(i) do { if (X.level0) { const uint64_t t_ = OP_NOW(); if (threadIdx.x == 0) atomicAdd(&g_oct_sub[i], (unsigned long long)(t_ - ts_)); ts_ = t_; } } while (0)
+#else
+#define OS_MARK(i) ((void)0)
+#endif
+
 // Where the octree keeps its keys (KeyFmt<K>) and their bins.  Thread t owns keys t, t + NT,
 // t + 2 NT, ... (NT threads); they are processed in chunks of kOctRegKeys held in registers,
 // slot r of chunk c being key t + NT (c kOctRegKeys + r).
@@ -1395,6 +1411,7 @@ struct OctCtx {
   void* outk;  // K[] of the level's retained keys
   int* oc;
   const uint32_t *px, *py;  // the level's quadrant paths (Geometry::octpath)
+  int level0;               // profiling builds: this workgroup runs level 0
 };
 
 // Per-thread chunks of whole int4s over [0, M) (bin arrays are 16-B aligned): [beg, end)
@@ -1520,7 +1537,11 @@ __device__ void oct_refine(const OctCtx& X, KS& ks, const OctNodes& cur, int siz
   using K = typename KS::Key;
   const int tid = threadIdx.x;
   int *t2 = X.t2, *t3 = X.t3, *bins = X.bins, *table = X.table;
+#ifdef ORBX_OCT_PROF
+  uint64_t ts_ = OP_NOW();
+#endif
   oct_fill_table<NT>(table, cur, size, gen_total, X.s_tmp);
+  OS_MARK(0);
   int act = 0;
   for (int i = tid; i < size; i += NT) {
     const int a = cur.cnt[i] > 1;
@@ -1535,8 +1556,10 @@ __device__ void oct_refine(const OctCtx& X, KS& ks, const OctNodes& cur, int siz
   for (int i = tid; i < size; i += NT) t3[i] = t2[i] ? 1 << (2 * R) : 1;
   __syncthreads();
   gen_total = block_scan_excl<NT>(t3, size, X.s_tmp);  // t3: each node's first new bin
+  OS_MARK(1);
   for (int i = 4 * tid; i <= gen_total; i += 4 * NT) *(int4*)(bins + i) = make_int4(0, 0, 0, 0);
   __syncthreads();
+  OS_MARK(2);
   each_key<NT>(
       ks, true, true,
       [&](int j, int) {
@@ -1553,10 +1576,13 @@ __device__ void oct_refine(const OctCtx& X, KS& ks, const OctNodes& cur, int siz
       },
       [&](int j, int) { atomicAdd(&bins[ks.get_lab(j)], 1); });
   __syncthreads();
+  OS_MARK(3);
   bins_scan_excl<NT>(bins, gen_total + 1, X.s_tmp);
+  OS_MARK(4);
   for (int i = tid; i < size; i += NT)
     cur.bl[i] = (t3[i] << 9) | (cur.bl[i] & (31 << 4)) | (t2[i] ? R : 0);
   __syncthreads();
+  OS_MARK(5);
 }
 
 // 3. retain the best key per node (max response, first in candidate order)
@@ -1608,113 +1634,181 @@ __device__ __forceinline__ void oct_push_children(const OctNodes& nxt, int bl, c
 // ---- the passes, workgroup form (256 / 1024 threads): node arrays in LDS, one barrier per step
 template <int NT, class KS>
 __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X, KS& ks,
-                                            const typename KS::Key* keys_mem) {
+                                            const typename KS::Key* keys_mem, int level = 0) {
   const int tid = threadIdx.x;
+#ifdef ORBX_OCT_PROF
+  uint64_t opf[16] = {};
+#endif
+  uint64_t tq = OP_NOW();
   int *cc = X.cc, *t1 = X.t1, *t2 = X.t2, *t3 = X.t3, *t4 = X.t4, *s_tmp = X.s_tmp,
       *s_misc = X.s_misc, *bins = X.bins;
   int size = oct_initial<NT>(G, X, ks);
+  { const uint64_t t2 = OP_NOW(); OP_ADD(0, t2 - tq); tq = t2; }
   OctNodes cur = X.B, nxt = X.A;
   int gen_total = G.nini;  // bins of the current generation
   int seqc = G.nini;
   bool final_mode = false;
   const int N = G.nfeat;
+  // -1: the next pass checks its nodes for a refine itself; else the previous outer pass's
+  // verdict (a child without digits left that may divide)
+  int need_known = -1;
+  const int lane = tid & 63, wid = tid >> 6;
   for (int iter = 0; iter < 4096; iter++) {
     const int prevSize = size;
     // a node that may divide with no digit left in its bin block: new bins first
-    int need = 0;
-    for (int i = tid; i < size; i += NT) need |= cur.cnt[i] > 1 && (cur.bl[i] & 15) == 0;
-    if (block_sum<NT>(need, s_tmp)) oct_refine<NT>(X, ks, cur, size, gen_total);
-    // quadrant counts of the nodes that may divide: the four quarters of their bin ranges
-    for (int i = tid; i < size; i += NT) {
-      if (cur.cnt[i] > 1) {
-        const int bl = cur.bl[i], b = bl >> 9, s4 = 1 << (2 * ((bl & 15) - 1));
-        const int e0 = bins[b], e1 = bins[b + s4], e2 = bins[b + 2 * s4], e3 = bins[b + 3 * s4],
-                  e4 = bins[b + 4 * s4];
-        cc[4 * i] = e1 - e0;
-        cc[4 * i + 1] = e2 - e1;
-        cc[4 * i + 2] = e3 - e2;
-        cc[4 * i + 3] = e4 - e3;
-      }
+    int need = need_known;
+    if (need < 0) {
+      need = 0;
+      for (int i = tid; i < size; i += NT) need |= cur.cnt[i] > 1 && (cur.bl[i] & 15) == 0;
+      need = block_sum<NT>(need, s_tmp);
     }
-    __syncthreads();
+    if (need) oct_refine<NT>(X, ks, cur, size, gen_total);
+    { const uint64_t t2 = OP_NOW(); OP_ADD(1, t2 - tq); tq = t2; OP_ADD(7, need ? 1 : 0); }
     int T, newSize, nToExpand = 0;
     if (!final_mode) {
-      // outer pass (list order): one packed scan gives childPre (bits 0-19), the rank among
-      // undivided nodes (20-39) and the total of children with > 1 key (40-)
+      // Outer pass (list order) in two steps, one barrier each.  Every thread owns a contiguous
+      // chunk of nodes for the whole pass (the scan's chunks), so a node's quadrant counts,
+      // flags and chunk-local prefix never cross threads before the scan: (1) quadrant counts
+      // (the four quarters of the node's bin range) and the packed per-node terms — childPre
+      // (bits 0-19), rank among undivided nodes (20-39), children with > 1 key (40-) — summed
+      // along the chunk, one wave scan, the wave totals in LDS; (2) every node to the next
+      // list (children pushed to the front, newest first; the undivided after them in order),
+      // and whether a child without digits left may divide (the next pass's refine check).
+      const int par = iter & 1;
+      if (tid == 0) s_misc[2 + (par ^ 1)] = 0;
+      const int per = (size + NT - 1) / NT;
+      const int beg = min(tid * per, size), end = min(beg + per, size);
       uint64_t* pk = X.pk;
-      for (int i = tid; i < size; i += NT) {
-        const bool e = cur.cnt[i] > 1;
-        uint64_t ne = 0, nx = 0;
-        if (e) {
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            ne += cc[4 * i + q] > 0;
-            nx += cc[4 * i + q] > 1;
-          }
+      uint64_t run = 0;
+      for (int i = beg; i < end; i++) {
+        uint64_t v = (uint64_t)1 << 20;  // undivided
+        if (cur.cnt[i] > 1) {
+          const int bl = cur.bl[i], b = bl >> 9, s4 = 1 << (2 * ((bl & 15) - 1));
+          const int e0 = bins[b], e1 = bins[b + s4], e2 = bins[b + 2 * s4], e3 = bins[b + 3 * s4],
+                    e4 = bins[b + 4 * s4];
+          const int c0 = e1 - e0, c1 = e2 - e1, c2 = e3 - e2, c3 = e4 - e3;
+          cc[4 * i] = c0;
+          cc[4 * i + 1] = c1;
+          cc[4 * i + 2] = c2;
+          cc[4 * i + 3] = c3;
+          v = (uint64_t)((c0 > 0) + (c1 > 0) + (c2 > 0) + (c3 > 0)) |
+              ((uint64_t)((c0 > 1) + (c1 > 1) + (c2 > 1) + (c3 > 1)) << 40);
         }
-        t2[i] = e;  // divided flag (the outer pass divides every expandable node)
-        pk[i] = ne | ((uint64_t)!e << 20) | (nx << 40);
+        pk[i] = run;
+        run += v;
       }
+      const uint64_t incl = wave_scan_incl64(run);
+      if (lane == 63) X.s_tmp64[wid] = incl;
       __syncthreads();
-      const uint64_t tot = block_scan_excl64<NT>(pk, size, X.s_tmp64);
+      uint64_t off = incl - run, tot = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; w++) {
+        const uint64_t x = X.s_tmp64[w];
+        off += w < wid ? x : 0;
+        tot += x;
+      }
       T = (int)(tot & 0xFFFFF);
       newSize = T + (int)((tot >> 20) & 0xFFFFF);
       nToExpand = (int)(tot >> 40);
-      // base: divided -> T-1-childPre (child j at base-j); else newpos
-      for (int i = tid; i < size; i += NT) {
-        const uint64_t e = pk[i];
-        const int pre = (int)(e & 0xFFFFF), ndr = (int)((e >> 20) & 0xFFFFF);
-        t1[i] = pre;
-        t4[i] = t2[i] ? T - 1 - pre : T + ndr;
+      bool nd = false;
+      for (int i = beg; i < end; i++) {
+        const uint64_t pre = off + pk[i];
+        const int childPre = (int)(pre & 0xFFFFF), ndr = (int)((pre >> 20) & 0xFFFFF);
+        if (cur.cnt[i] > 1) {
+          const int bl = cur.bl[i];
+          const int c[4] = {cc[4 * i], cc[4 * i + 1], cc[4 * i + 2], cc[4 * i + 3]};
+          oct_push_children(nxt, bl, c, T - 1 - childPre, seqc + childPre);
+          nd |= (bl & 15) == 1 && (c[0] > 1 || c[1] > 1 || c[2] > 1 || c[3] > 1);
+        } else {
+          const int pos = T + ndr;
+          nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
+          nxt.bl[pos] = cur.bl[i];
+        }
       }
+      if (nd) s_misc[2 + (par ^ 1)] = 1;
       __syncthreads();
+      need_known = s_misc[2 + (par ^ 1)];
+      { const uint64_t t2 = OP_NOW(); OP_ADD(2, t2 - tq); tq = t2; OP_ADD(5, 1); }
     } else {
-      for (int i = tid; i < size; i += NT) {
-        const bool e = cur.cnt[i] > 1;
+      // Final refinement (ORBextractor.cc:687-727): the expandable nodes are visited by (size,
+      // seq) descending, each adding its children until the list would reach N.  Six barrier
+      // steps, every thread owning a contiguous chunk of nodes (and of visiting ranks):
+      //  A  quadrant counts, children per node, the rank keys, the expandable count E;
+      //  B  each expandable node's visiting rank (all-pairs count of larger keys), the visiting
+      //     order;
+      //  C  children per visiting rank, prefix-summed in visiting order (childPre);
+      //  D  the cut: the first rank whose children reach N (a minimum over the ranks);
+      //  E  the undivided nodes' ranks in list order;
+      //  F  the next list: children of the ranks up to the cut at the front, the rest in order.
+      need_known = -1;
+      const int per = (size + NT - 1) / NT;
+      const int beg = min(tid * per, size), end = min(beg + per, size);
+      uint64_t* pk = X.pk;
+      int e_local = 0;
+      for (int i = beg; i < end; i++) {
+        uint64_t key = 0;
         int ne = 0;
-        if (e) {
-#pragma unroll
-          for (int q = 0; q < 4; q++) ne += cc[4 * i + q] > 0;
+        if (cur.cnt[i] > 1) {
+          const int bl = cur.bl[i], b = bl >> 9, s4 = 1 << (2 * ((bl & 15) - 1));
+          const int e0 = bins[b], e1 = bins[b + s4], e2 = bins[b + 2 * s4], e3 = bins[b + 3 * s4],
+                    e4 = bins[b + 4 * s4];
+          const int c0 = e1 - e0, c1 = e2 - e1, c2 = e3 - e2, c3 = e4 - e3;
+          cc[4 * i] = c0;
+          cc[4 * i + 1] = c1;
+          cc[4 * i + 2] = c2;
+          cc[4 * i + 3] = c3;
+          ne = (c0 > 0) + (c1 > 0) + (c2 > 0) + (c3 > 0);
+          key = ((uint64_t)cur.cnt[i] << 32) | (uint32_t)cur.seq[i];
+          e_local++;
         }
         t1[i] = ne;
+        pk[i] = key;
       }
-      // final refinement: visit expandable nodes by (size desc, seq desc).  A node's rank is
-      // the number of expandable nodes with a larger (size, seq) key; the keys are packed once
-      // into pk (size << 32 | seq, 0 for nodes that do not expand) so the all-pairs count is one
-      // broadcast 64-bit load and compare per node pair
-      uint64_t* pk = X.pk;
-      for (int i = tid; i < size; i += NT)
-        pk[i] = cur.cnt[i] > 1 ? ((uint64_t)cur.cnt[i] << 32) | (uint32_t)cur.seq[i] : 0;
-      __syncthreads();
-      int E_local = 0;
-      for (int i = tid; i < size; i += NT) {
+      {
+        const int ew = wave_scan_incl(e_local);
+        if (lane == 63) s_tmp[wid] = ew;
+      }
+      __syncthreads();  // A
+      int E = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; w++) E += s_tmp[w];
+      for (int i = beg; i < end; i++) {
         const uint64_t ki = pk[i];
+        int rank = -1;
         if (ki != 0) {
-          int r = 0;
-          int j = 0;
+          int r = 0, j = 0;
           for (; j + 4 <= size; j += 4) {
             const uint64_t a = pk[j], b = pk[j + 1], c = pk[j + 2], d = pk[j + 3];
             r += (a > ki) + (b > ki) + (c > ki) + (d > ki);
           }
           for (; j < size; j++) r += pk[j] > ki;
-          t3[r] = i;  // vis[r] = node
-          t4[i] = r;  // rank
-          E_local++;
+          t3[r] = i;  // visiting order
+          rank = r;
         }
+        t4[i] = rank;
       }
-      const int E = block_sum<NT>(E_local, s_tmp);
-      // per visiting rank: nonEmpty -> childPre (exclusive scan over visiting order); t2 reused
-      for (int v = tid; v < E; v += NT) t2[v] = t1[t3[v]];
-      __syncthreads();
+      __syncthreads();  // B
+      const int vper = (E + NT - 1) / NT;
+      const int vb = min(tid * vper, E), ve = min(vb + vper, E);
+      int run = 0;
+      for (int v = vb; v < ve; v++) {
+        t2[v] = run;  // chunk-local exclusive prefix of the children in visiting order
+        run += t1[t3[v]];
+      }
+      const int vincl = wave_scan_incl(run);
+      if (lane == 63) s_tmp[wid] = vincl;
       if (tid == 0) s_misc[0] = E > 0 ? E - 1 : -1;
-      __syncthreads();
-      block_scan_excl<NT>(t2, E, s_tmp);
-      // cut = first v with size + childPre_v + ne_v - (v+1) >= N
-      for (int v = tid; v < E; v += NT) {
-        const int ne = t1[t3[v]];
-        if (size + t2[v] + ne - (v + 1) >= N) atomicMin(&s_misc[0], v);
+      __syncthreads();  // C
+      int voff = vincl - run;
+#pragma unroll
+      for (int w = 0; w < NT / 64; w++) voff += w < wid ? s_tmp[w] : 0;
+      for (int v = vb; v < ve; v++) {
+        const int childPre = voff + t2[v];
+        t2[v] = childPre;
+        // cut = the first v with size + childPre_v + ne_v - (v + 1) >= N
+        if (size + childPre + t1[t3[v]] - (v + 1) >= N) atomicMin(&s_misc[0], v);
       }
-      __syncthreads();
+      __syncthreads();  // D
       const int cut = s_misc[0];
       if (cut >= 0) {
         T = t2[cut] + t1[t3[cut]];
@@ -1723,41 +1817,29 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
         T = 0;
         newSize = size;
       }
-      __syncthreads();
-      // divided flag & childPre per node: t4 holds the rank; childPre (indexed by rank in t2)
-      // moves to a per-node array in t1, t2 becomes the divided flag per node
-      for (int i = tid; i < size; i += NT) {
-        const bool e = cur.cnt[i] > 1;
-        const int r = e ? t4[i] : -1;
-        t4[i] = (e && r <= cut) ? r : -1;  // rank if divided, else -1
-      }
-      __syncthreads();
-      for (int i = tid; i < size; i += NT) {
+      int und = 0;
+      for (int i = beg; i < end; i++) und += !(t4[i] >= 0 && t4[i] <= cut);
+      const int uincl = wave_scan_incl(und);
+      if (lane == 63) s_tmp[wid] = uincl;
+      __syncthreads();  // E
+      int upos = uincl - und;
+#pragma unroll
+      for (int w = 0; w < NT / 64; w++) upos += w < wid ? s_tmp[w] : 0;
+      for (int i = beg; i < end; i++) {
         const int r = t4[i];
-        t1[i] = r >= 0 ? t2[r] : 0;  // childPre
+        if (r >= 0 && r <= cut) {
+          const int childPre = t2[r];
+          const int c[4] = {cc[4 * i], cc[4 * i + 1], cc[4 * i + 2], cc[4 * i + 3]};
+          oct_push_children(nxt, cur.bl[i], c, T - 1 - childPre, seqc + childPre);
+        } else {
+          const int pos = T + upos++;
+          nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
+          nxt.bl[pos] = cur.bl[i];
+        }
       }
-      __syncthreads();
-      for (int i = tid; i < size; i += NT) {
-        t2[i] = t4[i] >= 0;
-        t3[i] = !(t4[i] >= 0);
-      }
-      __syncthreads();
-      block_scan_excl<NT>(t3, size, s_tmp);
-      for (int i = tid; i < size; i += NT) t4[i] = t2[i] ? T - 1 - t1[i] : T + t3[i];
-      __syncthreads();
+      __syncthreads();  // F
+      { const uint64_t t2 = OP_NOW(); OP_ADD(3, t2 - tq); tq = t2; OP_ADD(6, 1); }
     }
-    // write next node arrays: t2 = divided, t1 = childPre, t4 = base
-    for (int i = tid; i < size; i += NT) {
-      if (t2[i]) {
-        const int c[4] = {cc[4 * i], cc[4 * i + 1], cc[4 * i + 2], cc[4 * i + 3]};
-        oct_push_children(nxt, cur.bl[i], c, t4[i], seqc + t1[i]);
-      } else {
-        const int pos = t4[i];
-        nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
-        nxt.bl[pos] = cur.bl[i];
-      }
-    }
-    __syncthreads();
     {
       OctNodes tmp = cur;
       cur = nxt;
@@ -1773,13 +1855,20 @@ __device__ __forceinline__ void octree_core(const LevelGeom& G, const OctCtx& X,
     }
   }
   oct_retain<NT>(X, ks, cur, size, gen_total, keys_mem);
+  { const uint64_t t2 = OP_NOW(); OP_ADD(4, t2 - tq); tq = t2; OP_ADD(8, size); OP_ADD(9, ks.n); }
+#ifdef ORBX_OCT_PROF
+  if (tid == 0)
+    for (int i = 0; i < 16; i++) atomicAdd(&g_oct_prof[(level & 7) * 16 + i], (unsigned long long)opf[i]);
+#endif
 }
 
 // 256-thread instances: 6 waves per SIMD (80 VGPRs; a few spill, but C2's octree took 0.120
 // vs 0.128 ms per 512 frames against 4 waves without spills); the 1024-thread instance keeps
 // its registers.
 constexpr int kOctWaves = 6;
-template <int NT, class K>
+// PLDS: the level's quadrant paths staged in LDS (ds_read in the refine sweeps; a pointer that
+// may be either kind would compile to flat loads, which measured as slow as global ones)
+template <int NT, bool PLDS, class K>
 __global__ __launch_bounds__(NT)
 __attribute__((amdgpu_waves_per_eu(NT <= 256 ? kOctWaves : 1)))
 void k_octree(
@@ -1787,7 +1876,8 @@ void k_octree(
     const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
     K* __restrict__ lin, int* __restrict__ label, K* __restrict__ okey,
     int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
-    int bin_cap, int level_base, int* __restrict__ cell_scr, const uint32_t* __restrict__ octpath) {
+    int bin_cap, int level_base, int* __restrict__ cell_scr, const uint32_t* __restrict__ octpath,
+    int path_cap) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_tmp[NT / 64 + 1];
   __shared__ int s_misc[8];
@@ -1821,6 +1911,15 @@ void k_octree(
   int* t3 = (int*)take(4 * NC);
   int* t4 = (int*)take(4 * NC);
   uint64_t* pk = (uint64_t*)take(8 * (NC + 1));
+  // the level's quadrant paths (x then y: one contiguous run of Geometry::octpath) in LDS: the
+  // refine sweeps look them up per key (loaded here beside the gather's loads)
+  // (path_cap 0: the plan keeps them in global memory, where the LDS would cost occupancy)
+  const uint32_t* pxy = octpath + G.path_x;
+  if constexpr (PLDS) {
+    uint32_t* s_path = (uint32_t*)take(4 * (size_t)path_cap);
+    for (int i = tid; i < G.W + G.H; i += NT) s_path[i] = pxy[i];
+    pxy = s_path;
+  }
   // one region for the gather's per-cell key starts and slots and, after it, the bins and
   // their node table.  Cells: in LDS, or (cell_cap == 0: levels with too many cells for it)
   // in this (image, level)'s part of cell_scr, [2 (ncells + nlevels)] ints per image
@@ -1875,7 +1974,7 @@ void k_octree(
   };
   // (the bins are first written by octree_core's refine, several barriers after the gather)
   OctCtx X{A,    B,       cc,   t1, t2, t3, t4, s_tmp, s_misc, bins, table, bin_cap,
-           pk,   s_tmp64, outk, oc, octpath + G.path_x, octpath + G.path_y};
+           pk,   s_tmp64, outk, oc, pxy, pxy + G.W, level == 0};
   if (n <= kOctRegKeys * NT) {  // keys + bins in registers: every sweep stays on-chip
     RegKeys<NT, K> ks;
     ks.n = n;
@@ -1886,7 +1985,7 @@ void k_octree(
       ks.lab[j] = 0;
       if (k < n) keys[k] = ks.key[j];
     }
-    octree_core<NT>(G, X, ks, keys);
+    octree_core<NT>(G, X, ks, keys, level);
   } else {  // keys + bins in global scratch, swept in register chunks
     for (int k0 = 0; k0 < n; k0 += NT * kOctRegKeys) {
       K v[kOctRegKeys];
@@ -1901,7 +2000,7 @@ void k_octree(
     ks.keys = keys;
     ks.labs = lab;
     ks.n = n;
-    octree_core<NT>(G, X, ks, keys);
+    octree_core<NT>(G, X, ks, keys, level);
   }
 }
 
@@ -2074,6 +2173,7 @@ struct orbx_plan {
   // k_octree instances (kOctNTBig, kOctNT threads): levels [lo, hi) each, with LDS for nc
   // nodes, cc cells (0: the cell tables in d_cell_scr) and `bins` bins
   struct OctInst {
+    int paths = 0;  // quadrant-path entries of the instance's largest level (W + H)
     int lo = 0, hi = 0, nc = 1, cc = 1, bins = 1;
     size_t smem = 0;
   } oct[2];
@@ -2276,10 +2376,16 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
     hipLaunchKernelGGL(kern, dim3(n, o.hi - o.lo), dim3(nt), o.smem, P->stream, P->d_lv,
                        P->d_cell_counts, ncells, P->d_cells, cand, g.cand_total, lin, P->d_label,
                        okey, P->d_ocount, g.kp_total, L, o.nc, o.cc, o.bins, o.lo, P->d_cell_scr,
-                       P->d_octpath);
+                       P->d_octpath, o.paths);
   };
-  launch_oct(k_octree<kOctNTBig, K>, kOctNTBig, P->oct[0], "1024, ");
-  launch_oct(k_octree<kOctNT, K>, kOctNT, P->oct[1], "256, ");
+  if (P->oct[0].paths > 0)
+    launch_oct(k_octree<kOctNTBig, true, K>, kOctNTBig, P->oct[0], "1024, true, ");
+  else
+    launch_oct(k_octree<kOctNTBig, false, K>, kOctNTBig, P->oct[0], "1024, false, ");
+  if (P->oct[1].paths > 0)
+    launch_oct(k_octree<kOctNT, true, K>, kOctNT, P->oct[1], "256, true, ");
+  else
+    launch_oct(k_octree<kOctNT, false, K>, kOctNT, P->oct[1], "256, false, ");
   pr.mark(P->stream, st_oct);
   KpOffsets ko{};
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
@@ -2458,9 +2564,10 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   auto r16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   // node arrays (two lists of cnt seq bl), quadrant counts, four scratch arrays and
   // the rank keys, then one region for the gather's cell tables or the bins + node table
-  auto oct_bytes = [&](size_t NC, size_t CC, size_t BC) {
+  auto oct_bytes = [&](size_t NC, size_t CC, size_t BC, size_t PC) {
     return 2 * 3 * r16(4 * NC) + r16(4 * std::max(4 * NC, BC + 8)) + 4 * r16(4 * NC) +
-           r16(8 * (NC + 1)) + std::max(CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0, r16(4 * (BC + 8)));
+           r16(8 * (NC + 1)) + r16(4 * PC) +
+           std::max(CC ? r16(4 * (CC + 1)) + r16(4 * CC) : 0, r16(4 * (BC + 8)));
   };
   // levels are in decreasing area: each instance takes a contiguous range
   int inst_of[kMaxLevels];
@@ -2472,6 +2579,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     while (l < g.nlevels && inst_of[l] == i) {
       o.nc = std::max(o.nc, g.lv[l].node_cap);
       o.cc = std::max(o.cc, g.lv[l].ncells);
+      o.paths = std::max(o.paths, g.lv[l].W + g.lv[l].H);
+      if (g.lv[l].path_y != g.lv[l].path_x + g.lv[l].W) return fail(ORBX_EUNSUPPORTED);
       l++;
     }
     o.hi = l;
@@ -2480,8 +2589,25 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
     // sweeps (few-image plans and the 1024-thread instance are not bound by LDS occupancy)
     o.bins = std::max(4 * o.nc + 4, (i == 0 || max_batch <= kPyFewImages) ? kOctBinsFew : kOctBins);
     // a level with more cells than fit beside its nodes keeps its cell table in global scratch
-    if (oct_bytes(o.nc, o.cc, o.bins) > kOctMaxSmem) o.cc = 0;
-    o.smem = o.hi > o.lo ? oct_bytes(o.nc, o.cc, o.bins) : 0;
+    if (oct_bytes(o.nc, o.cc, o.bins, 0) > kOctMaxSmem) o.cc = 0;
+    // the quadrant paths in LDS only where that keeps the workgroups per CU and the LDS bound
+    // (C2: octree 0.115 -> 0.101 ms per 512 frames; C5's 256-thread levels lost a workgroup per
+    // CU to them and took longer)
+    const int nt = i == 0 ? kOctNTBig : kOctNT;
+    const int wave_cap = i == 0 ? 1 : 4 * kOctWaves / (nt / 64);  // workgroups per CU by waves
+    auto per_cu = [&](size_t b) { return std::min<int>(wave_cap, (int)((160 * 1024) / std::max<size_t>(b, 1))); };
+#ifdef ORBX_EXP_OCT_DEBUG
+    fprintf(stderr, "[oct] inst %d levels %d..%d nc %d cc %d bins %d paths %d bytes %zu / %zu per_cu %d / %d\n",
+            i, o.lo, o.hi, o.nc, o.cc, o.bins, o.paths, oct_bytes(o.nc, o.cc, o.bins, 0),
+            oct_bytes(o.nc, o.cc, o.bins, o.paths), per_cu(oct_bytes(o.nc, o.cc, o.bins, 0)),
+            per_cu(oct_bytes(o.nc, o.cc, o.bins, o.paths)));
+#endif
+#ifndef ORBX_EXP_OCT_PATHS_ALWAYS
+    if (oct_bytes(o.nc, o.cc, o.bins, o.paths) > kOctMaxSmem ||
+        per_cu(oct_bytes(o.nc, o.cc, o.bins, o.paths)) < per_cu(oct_bytes(o.nc, o.cc, o.bins, 0)))
+      o.paths = 0;
+#endif
+    o.smem = o.hi > o.lo ? oct_bytes(o.nc, o.cc, o.bins, o.paths) : 0;
     if (o.smem > kOctMaxSmem) return fail(ORBX_EUNSUPPORTED);
   }
   bool cell_scr = false;
@@ -2492,9 +2618,11 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
   // scratch.  The dynamic-LDS attribute is per function and shared by every plan of the
   // process: only ever raised.
   static size_t attr[2] = {0, 0};  // guarded by the resource lock
-  const void* fns[2][2] = {
-      {(const void*)k_octree<kOctNTBig, uint32_t>, (const void*)k_octree<kOctNTBig, uint64_t>},
-      {(const void*)k_octree<kOctNT, uint32_t>, (const void*)k_octree<kOctNT, uint64_t>}};
+  const void* fns[2][4] = {
+      {(const void*)k_octree<kOctNTBig, false, uint32_t>, (const void*)k_octree<kOctNTBig, false, uint64_t>,
+       (const void*)k_octree<kOctNTBig, true, uint32_t>, (const void*)k_octree<kOctNTBig, true, uint64_t>},
+      {(const void*)k_octree<kOctNT, false, uint32_t>, (const void*)k_octree<kOctNT, false, uint64_t>,
+       (const void*)k_octree<kOctNT, true, uint32_t>, (const void*)k_octree<kOctNT, true, uint64_t>}};
   for (int i = 0; i < 2; i++) {
     if (P->oct[i].smem <= attr[i]) continue;
     for (const void* f : fns[i])
@@ -2609,6 +2737,21 @@ int orbx_plan_level_download_buf(orbx_plan* P, int img, int level, uint8_t* out,
 int orbx_plan_level_download(orbx_plan* P, int img, int level, uint8_t* out, int64_t stride) {
   return orbx_plan_level_download_buf(P, img, level, out, stride, 0);
 }
+
+#ifdef ORBX_OCT_PROF
+int orbx_debug_oct_prof(uint64_t* out, int32_t reset) {
+  if (out && (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_prof), sizeof(g_oct_prof)) != hipSuccess ||
+              hipMemcpyFromSymbol(out + 8 * 16, HIP_SYMBOL(g_oct_sub), sizeof(g_oct_sub)) != hipSuccess))
+    return ORBX_EDEVICE;
+  if (reset) {
+    static const unsigned long long z[8 * 16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_oct_prof), z, sizeof(z)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_oct_sub), z, 8 * 8) != hipSuccess)
+      return ORBX_EDEVICE;
+  }
+  return ORBX_OK;
+}
+#endif
 
 #ifdef ORBX_FAST_PROF
 int orbx_debug_fast_prof(uint64_t* out, int32_t reset) {
