@@ -1422,8 +1422,9 @@ __device__ __forceinline__ void int4_chunk(int M, int& beg, int& end) {
   end = min(beg + per, M);
 }
 
-// exclusive scan of a bin array a[0..M) in place, four bins per LDS access
-template <int NT>
+// exclusive scan of a bin array a[0..M) in place, four bins per LDS access (GUARD false: the
+// caller knows s_tmp has no pending reader, so the scan skips grp_excl's leading barrier)
+template <int NT, bool GUARD = true>
 __device__ int bins_scan_excl(int* a, int M, int* s_tmp) {
   int beg, end;
   int4_chunk<NT>(M, beg, end);
@@ -1434,7 +1435,24 @@ __device__ int bins_scan_excl(int* a, int M, int* s_tmp) {
   }
   for (; i < end; i++) sum += a[i];
   int total;
-  int run = grp_excl<NT>(sum, s_tmp, total);
+  int run;
+  if constexpr (GUARD) {
+    run = grp_excl<NT>(sum, s_tmp, total);
+  } else {
+    const int inc = wave_scan_incl(sum);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 63) s_tmp[wid] = inc;
+    __syncthreads();
+    int pre = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+      const int x = s_tmp[w];
+      pre += w < wid ? x : 0;
+      total += x;
+    }
+    run = pre + inc - sum;
+  }
   for (i = beg; i + 4 <= end; i += 4) {
     const int4 v = *(const int4*)(a + i);
     int4 o;
@@ -1542,20 +1560,46 @@ __device__ void oct_refine(const OctCtx& X, KS& ks, const OctNodes& cur, int siz
 #endif
   oct_fill_table<NT>(table, cur, size, gen_total, X.s_tmp);
   OS_MARK(0);
+  // the nodes that may divide and the digits R, then each node's first new bin (t3): every
+  // thread owns a contiguous chunk of nodes, so one wave scan and one barrier per total
+  const int lane = tid & 63, wid = tid >> 6;
+  const int per = (size + NT - 1) / NT;
+  const int beg = min(tid * per, size), end = min(beg + per, size);
   int act = 0;
-  for (int i = tid; i < size; i += NT) {
+  for (int i = beg; i < end; i++) {
     const int a = cur.cnt[i] > 1;
     t2[i] = a;
     act += a;
   }
-  const int nact = block_sum<NT>(act, X.s_tmp);
+  {
+    const int ai = wave_scan_incl(act);
+    if (lane == 63) X.s_tmp[wid] = ai;
+  }
+  __syncthreads();
+  int nact = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; w++) nact += X.s_tmp[w];
   const int nin = size - nact;
   const int lim = min(X.bin_cap, max(4 * size, ks.n));
   int R = 1;
   while (R < 15 && nin + ((int64_t)nact << (2 * (R + 1))) <= lim) R++;
-  for (int i = tid; i < size; i += NT) t3[i] = t2[i] ? 1 << (2 * R) : 1;
+  int run = 0;
+  for (int i = beg; i < end; i++) {
+    t3[i] = run;
+    run += t2[i] ? 1 << (2 * R) : 1;
+  }
+  const int ri = wave_scan_incl(run);
+  if (lane == 63) X.s_tmp64[wid] = (uint64_t)ri;
   __syncthreads();
-  gen_total = block_scan_excl<NT>(t3, size, X.s_tmp);  // t3: each node's first new bin
+  int off = ri - run;
+  gen_total = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; w++) {
+    const int x = (int)X.s_tmp64[w];
+    off += w < wid ? x : 0;
+    gen_total += x;
+  }
+  for (int i = beg; i < end; i++) t3[i] += off;  // t3: each node's first new bin
   OS_MARK(1);
   for (int i = 4 * tid; i <= gen_total; i += 4 * NT) *(int4*)(bins + i) = make_int4(0, 0, 0, 0);
   __syncthreads();
@@ -1577,7 +1621,7 @@ __device__ void oct_refine(const OctCtx& X, KS& ks, const OctNodes& cur, int siz
       [&](int j, int) { atomicAdd(&bins[ks.get_lab(j)], 1); });
   __syncthreads();
   OS_MARK(3);
-  bins_scan_excl<NT>(bins, gen_total + 1, X.s_tmp);
+  bins_scan_excl<NT, false>(bins, gen_total + 1, X.s_tmp);
   OS_MARK(4);
   for (int i = tid; i < size; i += NT)
     cur.bl[i] = (t3[i] << 9) | (cur.bl[i] & (31 << 4)) | (t2[i] ? R : 0);
