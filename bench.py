@@ -109,7 +109,7 @@ def _load_json(name):
 
 
 # The PMC passes of a round (scripts/refresh_profiles.sh): profiles/<PMC_ROUND>_pmc[_<config>]
-PMC_ROUND = "r05"
+PMC_ROUND = "r06"
 
 
 def kernel_instance(name):

@@ -174,6 +174,17 @@ def main(tag="r02"):
                 continue
             summ.append(f"{r[1][:27]:28s}{r[0]:9.1f}{r[2]:9.0f}{r[3]:8.0f}{r[4]:8.0f}{r[5]:7.0f}"
                         f"{r[6]:6.0f}{r[7]:9.1f}{r[8]:9.1f}{r[9]:9.1f}{r[10]:9.1f}")
+        # k_describe: counter traffic per keypoint against the bytes one keypoint's 37x37 blurred
+        # patch holds (the image pyramid is read once per image at batch 512, so the traffic is
+        # the pyramid's bytes spread over the keypoints, not the patches)
+        c = line["config"]
+        kp = c.get("keypoints_per_frame", 0) * c.get("frames_per_batch", 0) * c.get("images_per_frame", 1)
+        for r in rows:
+            if r[1].startswith("k_describe") and kp:
+                fb, wb = r[9] * 1024 * 1024 / kp, r[10] * 1024 * 1024 / kp
+                summ.append(f"# k_describe per keypoint ({kp:.0f} keypoints per dispatch): fetched "
+                            f"{fb:.0f} B, written {wb:.0f} B; one 37x37 patch 1369 B, algorithmic "
+                            f"(keypoint in + descriptor out) 60 B")
         summ.append("")
     open(os.path.join(P, f"{tag}_roofline_check.txt"), "w").write("\n".join(check) + "\n")
     open(os.path.join(P, f"{tag}_pmc_summary.txt"), "w").write("\n".join(summ))
