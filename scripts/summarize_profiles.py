@@ -181,10 +181,14 @@ def main(tag="r02"):
         kp = c.get("keypoints_per_frame", 0) * c.get("frames_per_batch", 0) * c.get("images_per_frame", 1)
         for r in rows:
             if r[1].startswith("k_describe") and kp:
-                fb, wb = r[9] * 1024 * 1024 / kp, r[10] * 1024 * 1024 / kp
+                # FETCH_SIZE reads 1/2 of the bytes loaded (profiles/pmc_calibration.json)
+                fb, wb = r[9] * 1024 * 1024 / 0.5 / kp, r[10] * 1024 * 1024 / kp
+                pyr = 2 * c.get("frames_per_batch", 0) * c.get("images_per_frame", 1)
                 summ.append(f"# k_describe per keypoint ({kp:.0f} keypoints per dispatch): fetched "
-                            f"{fb:.0f} B, written {wb:.0f} B; one 37x37 patch 1369 B, algorithmic "
-                            f"(keypoint in + descriptor out) 60 B")
+                            f"{fb:.0f} B (FETCH_SIZE / 0.5), written {wb:.0f} B; one keypoint's "
+                            f"31x31 raw + 37x37 blurred patches 2330 B, algorithmic (keypoint in + "
+                            f"descriptor out) 60 B; fetched per dispatch {r[9] / 0.5:.0f} MB for "
+                            f"{pyr} pyramids (raw + blurred) of {c.get('frames_per_batch')} images")
         summ.append("")
     open(os.path.join(P, f"{tag}_roofline_check.txt"), "w").write("\n".join(check) + "\n")
     open(os.path.join(P, f"{tag}_pmc_summary.txt"), "w").write("\n".join(summ))
