@@ -1408,7 +1408,9 @@ struct OctCtx {
   int* table;  // [bin_cap + 8], in cc's LDS: bin -> node position (forward-filled per node)
   int bin_cap;
   uint64_t *pk, *s_tmp64;
-  void* outk;  // K[] of the level's retained keys
+  void* outk;  // K[] of the level's retained keys, in candidate order
+  int* opos;   // their node-order (output) positions
+  int tcap;    // ints in the table's LDS
   int* oc;
   const uint32_t *px, *py;  // the level's quadrant paths (Geometry::octpath)
   int level0;               // profiling builds: this workgroup runs level 0
@@ -1647,10 +1649,46 @@ __device__ void oct_retain(const OctCtx& X, KS& ks, const OctNodes& cur, int siz
       });
   __syncthreads();
   K* outk = (K*)X.outk;
-  for (int i = tid; i < size; i += NT) {
-    // every node holds a key; the clamp only keeps a broken invariant from reading past them
-    const int k = min((int)(0xFFFFFFu - (best[i] & 0xFFFFFFu)), ks.n - 1);
-    outk[i] = keys_mem[k];
+  // every node holds a key; the clamp only keeps a broken invariant from reading past them
+  auto winner = [&](int i) { return min((int)(0xFFFFFFu - (best[i] & 0xFFFFFFu)), ks.n - 1); };
+  // The retained keys go out in candidate order (cells in raster order, raster order inside a
+  // cell) with their node-order positions, where k_describe writes each keypoint: its
+  // workgroups then take spatial neighbours, whose patches share cache lines.  A key's place is
+  // the number of retained keys before it in candidate order: a bitmap over the candidates
+  // (the bin table's LDS, free after the sweep) and its prefix popcounts.
+  const int W = (ks.n + 31) >> 5;
+  if (2 * W > X.tcap) {  // no room: node order
+    for (int i = tid; i < size; i += NT) {
+      outk[i] = keys_mem[winner(i)];
+      X.opos[i] = i;
+    }
+  } else {
+    unsigned* bm = (unsigned*)X.table;
+    int* pre = X.table + W;
+    for (int w = tid; w < W; w += NT) bm[w] = 0u;
+    __syncthreads();
+    for (int i = tid; i < size; i += NT) {
+      const int k = winner(i);
+      atomicOr(&bm[k >> 5], 1u << (k & 31));
+    }
+    __syncthreads();
+    int beg, end;
+    int4_chunk<NT>(W, beg, end);
+    int sum = 0;
+    for (int w = beg; w < end; w++) sum += __popc(bm[w]);
+    int total;
+    int run = grp_excl<NT>(sum, X.s_tmp, total);
+    for (int w = beg; w < end; w++) {
+      pre[w] = run;
+      run += __popc(bm[w]);
+    }
+    __syncthreads();
+    for (int i = tid; i < size; i += NT) {
+      const int k = winner(i);
+      const int r = pre[k >> 5] + __popc(bm[k >> 5] & ((1u << (k & 31)) - 1u));
+      outk[r] = keys_mem[k];
+      X.opos[r] = i;
+    }
   }
   if (tid == 0) *X.oc = size;
 }
@@ -1918,7 +1956,7 @@ __attribute__((amdgpu_waves_per_eu(NT <= 256 ? kOctWaves : 1)))
 void k_octree(
     const LevelGeom* __restrict__ lv, const int* __restrict__ cell_counts, int ncells,
     const CellGeom* __restrict__ cells, const K* __restrict__ cand, int cand_total,
-    K* __restrict__ lin, int* __restrict__ label, K* __restrict__ okey,
+    K* __restrict__ lin, int* __restrict__ label, K* __restrict__ okey, int* __restrict__ oidx,
     int* __restrict__ ocount, int kp_total, int nlevels, int node_cap, int cell_cap,
     int bin_cap, int level_base, int* __restrict__ cell_scr, const uint32_t* __restrict__ octpath,
     int path_cap) {
@@ -2018,7 +2056,8 @@ void k_octree(
   };
   // (the bins are first written by octree_core's refine, several barriers after the gather)
   OctCtx X{A,    B,       cc,   t1, t2, t3, t4, s_tmp, s_misc, bins, table, bin_cap,
-           pk,   s_tmp64, outk, oc, pxy, pxy + G.W, level == 0};
+           pk,   s_tmp64, outk, oidx + (int64_t)img * kp_total + G.kp_off,
+           max(4 * NC, bin_cap + 8), oc, pxy, pxy + G.W, level == 0};
   if (n <= kOctRegKeys * NT) {  // keys + bins in registers: every sweep stays on-chip
     RegKeys<NT, K> ks;
     ks.n = n;
@@ -2063,7 +2102,8 @@ template <class K>
 __global__ __launch_bounds__(256) void k_describe(
     const uint8_t* __restrict__ pyr, int64_t pyr_bytes, const uint8_t* __restrict__ blur,
     const LevelGeom* __restrict__ lv, int nlevels, KpOffsets ko, const K* __restrict__ okey,
-    const int* __restrict__ ocount, int kp_total, orbx_keypoint* __restrict__ kps,
+    const int* __restrict__ oidx, const int* __restrict__ ocount, int kp_total,
+    orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts) {
   // dwords per staged row: raw 31+3 bytes rounded up; blurred 16-B pieces from a 16-B aligned
   // start (offset <= 15 plus 37 bytes: 13 dwords) — an odd stride, so the rBRIEF samples of
@@ -2090,11 +2130,15 @@ __global__ __launch_bounds__(256) void k_describe(
   const int idx = slot - ko.off[level];
   // the count, the key and the level's fields in one round of loads, pinned in registers (a
   // rematerialised load of G per patch row would serialise the patch loads behind it)
+  // the level's keys come in candidate order (spatial neighbours together, k_octree's retain),
+  // each with the node-order position it is written to
   int noc = oc[level];
   K key = okey[(int64_t)img * kp_total + min(slot, kp_total - 1)];
+  int opos = oidx[(int64_t)img * kp_total + min(slot, kp_total - 1)];
   int pitch = G.pitch, pyr_off = (int)G.pyr_off;
   float lscale = G.scale, lsize = G.size;
-  asm volatile("" : "+v"(noc), "+v"(key), "+v"(pitch), "+v"(pyr_off), "+v"(lscale), "+v"(lsize));
+  asm volatile("" : "+v"(noc), "+v"(key), "+v"(opos), "+v"(pitch), "+v"(pyr_off), "+v"(lscale),
+               "+v"(lsize));
   const bool active = slot < kp_total && idx < noc;  // uniform within the half-wave
   if (!active) key = 0;
   const int cx = active ? KeyFmt<K>::x(key) + (kEdge - 3) : 0;
@@ -2170,7 +2214,7 @@ __global__ __launch_bounds__(256) void k_describe(
     const int t1 = bcb[sample_offset(rotate_fma(pp.z, pp.w, cs, sn, nsn), BS)];
     byte |= (uint32_t)(t0 < t1) << m;
   }
-  int outpos = idx;
+  int outpos = opos;
   for (int l = 0; l < level; l++) outpos += oc[l];
   const int64_t o = (int64_t)img * kp_total + outpos;
   desc[o * 32 + hl] = (uint8_t)byte;
@@ -2209,6 +2253,7 @@ struct orbx_plan {
   // candidate keys, the octree's gathered keys and the retained keys: u32 or u64 (wide_keys)
   void *d_cand = nullptr, *d_lin = nullptr, *d_okey = nullptr;
   int *d_cell_counts = nullptr, *d_label = nullptr, *d_ocount = nullptr, *d_counts = nullptr;
+  int* d_oidx = nullptr;  // per retained key (candidate order): its node-order position
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   // counts, keypoints and descriptors share one allocation (d_counts is its base) so the
@@ -2419,7 +2464,7 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
     note_kernel<K>("k_octree", name);
     hipLaunchKernelGGL(kern, dim3(n, o.hi - o.lo), dim3(nt), o.smem, P->stream, P->d_lv,
                        P->d_cell_counts, ncells, P->d_cells, cand, g.cand_total, lin, P->d_label,
-                       okey, P->d_ocount, g.kp_total, L, o.nc, o.cc, o.bins, o.lo, P->d_cell_scr,
+                       okey, P->d_oidx, P->d_ocount, g.kp_total, L, o.nc, o.cc, o.bins, o.lo, P->d_cell_scr,
                        P->d_octpath, o.paths);
   };
   if (P->oct[0].paths > 0)
@@ -2435,8 +2480,8 @@ void enqueue_keyed(orbx_plan* P, int n, Profiler& pr, int st_fcell, int st_oct, 
   for (int l = 0; l < L; l++) ko.off[l] = g.lv[l].kp_off;
   note_kernel<K>("k_describe");
   hipLaunchKernelGGL(k_describe<K>, dim3((g.kp_total + 7) / 8, n), dim3(256), 0, P->stream,
-                     P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, ko, okey, P->d_ocount,
-                     g.kp_total, P->d_kps, P->d_desc, P->d_counts);
+                     P->d_pyr, g.pyr_bytes, P->d_blur, P->d_lv, L, ko, okey, P->d_oidx,
+                     P->d_ocount, g.kp_total, P->d_kps, P->d_desc, P->d_counts);
   pr.mark(P->stream, st_desc);
 }
 
@@ -2573,7 +2618,8 @@ int orbx_plan_create(const orbx_params* params, int32_t w, int32_t h, int32_t ma
       dalloc((char**)&P->d_cand, B * g.cand_total * ksz) ||
       dalloc((char**)&P->d_lin, B * g.cand_total * ksz) ||
       dalloc(&P->d_label, B * g.cand_total) || dalloc(&P->d_cell_counts, B * g.cells.size()) ||
-      dalloc((char**)&P->d_okey, B * g.kp_total * ksz) || dalloc(&P->d_ocount, B * g.nlevels) ||
+      dalloc((char**)&P->d_okey, B * g.kp_total * ksz) || dalloc(&P->d_oidx, B * g.kp_total) ||
+      dalloc(&P->d_ocount, B * g.nlevels) ||
       dalloc(&P->d_cells_small, cells_small.size()) || dalloc(&P->d_cells_tall, cells_tall.size()) ||
       dalloc(&P->d_cells_big, cells_big.size()) ||
       dalloc(&P->d_pairs, pairs.size()) || dalloc(&P->d_octpath, g.octpath.size()))
@@ -2685,7 +2731,7 @@ int orbx_plan_destroy(orbx_plan* P) {
   P->graphs.clear(P->stream);
   void* ptrs[] = {P->d_lv,   P->d_cells, P->d_xtap, P->d_ytap,        P->d_tiles, P->d_bands,
                   P->d_pyr,  P->d_blur,  P->d_cand, P->d_lin,         P->d_okey,  P->d_cell_counts,
-                  P->d_label,
+                  P->d_label, P->d_oidx,
                   P->d_ocount, P->d_cells_small, P->d_cells_tall, P->d_cells_big, P->d_pairs,
                   P->d_cell_scr, P->d_octpath,
                   P->d_counts /* base of kps and desc too */};
