@@ -92,24 +92,35 @@ __global__ __launch_bounds__(256) void k_stereo_rows(const StereoProblem* __rest
   }
 }
 
-// sum over the 64 lanes, wave-uniform: 16-lane row sums on DPP, then the four rows by readlane
-// (no ds_bpermute round trips: the SAD slide's 11 reductions are on the kernel's critical path).
-// Every lane must be active.
-__device__ __forceinline__ int wave_sum(int v) {
+// Sums and minima over the 32 lanes of a half-wave, in each of its lanes: 16-lane rows on DPP,
+// then the half's two rows by a swizzle (lanes 0-15 <-> 16-31 of each half).  Every lane of the
+// half-wave must be active; the other half's lanes are never read.
+__device__ __forceinline__ int half_sum(int v) {
   v = row16_sum(v);
-  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
-         __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+  return v + __builtin_amdgcn_ds_swizzle(v, 0x401F);
+}
+__device__ __forceinline__ uint32_t half_min_u32(uint32_t v) {
+  v = row16_min(v);
+  return min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F));
 }
 
+// One half-wave per left keypoint, eight per workgroup (Frame::ComputeStereoMatches,
+// Frame.cc:471-643): the keypoint's chain of dependent loads (row band, candidates, the
+// windows) is latency, so two keypoints share a wave's issue slots; the candidate scan, the 121
+// window pixels (four per lane) and the SAD sums run on the half's 32 lanes.
 __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __restrict__ probs,
                                                       const LevelGeom* __restrict__ lv,
                                                       int nrows, float mb, float mbf) {
+  constexpr int KP = ((2 * kW + 1) * (2 * kW + 1) + 31) / 32;  // window pixels per lane (4)
   const StereoProblem& P = probs[blockIdx.y];
-  const int lane = threadIdx.x & 63;
-  const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int hw = threadIdx.x >> 5;  // the workgroup's half-wave, 0..7
+  const int iL0 = blockIdx.x * 8 + ((threadIdx.x >> 6) << 1);  // the wave's first keypoint
   const int nl = *P.nl;
-  if (iL >= nl) return;
-  const orbx_keypoint kpL = P.kl[iL];
+  if (iL0 >= nl) return;  // wave-uniform
+  const int iL = iL0 + ((lane >> 5) & 1);
+  const bool live = iL < nl;  // uniform in the half-wave
+  const orbx_keypoint kpL = P.kl[live ? iL : iL0];
   float uright = -1.0f, depth = -1.0f;
   int sad_out = -1;
   const float minZ = mb, minD = -3.0f;
@@ -117,14 +128,14 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
   const float vL = kpL.y, uL = kpL.x;
   const int levelL = kpL.octave;
   const int row = (int)vL;  // vRowIndices[vL]: float -> index truncation
-  bool ok = row >= 0 && row < nrows;
+  bool ok = live && row >= 0 && row < nrows;
   int bestDist = kTH_HIGH;
   float uR0 = 0.0f;
   const float minU = uL - maxD, maxU = uL - minD;
   if (ok && maxU < 0) ok = false;
   // the left window (IL) depends only on the left keypoint: its loads are issued here, ahead of
-  // the candidate search, so their latency overlaps it (addresses clamped into the level; the
-  // values are used only when the reference would take the window)
+  // the candidate search, so their latency overlaps it (values used only when the reference
+  // would take the window)
   const LevelGeom& G = lv[levelL];
   const float scaleFactor = G.inv_scale;
   const float scaleduL = roundf(kpL.x * scaleFactor);
@@ -134,28 +145,32 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
   const int64_t pitch = G.pitch;
   const uint8_t* PL = P.pyrL + G.pyr_off;
   const uint8_t* PR = P.pyrR + G.pyr_off;
-  int yy[2], xx[2];
-  bool has[2];
+  int yy[KP], xx[KP];
+  bool has[KP];
 #pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int p = lane + 64 * k;
+  for (int k = 0; k < KP; k++) {
+    const int p = hl + 32 * k;
     has[k] = p < (2 * kW + 1) * (2 * kW + 1);
     yy[k] = has[k] ? p / (2 * kW + 1) : 0;
     xx[k] = has[k] ? p - yy[k] * (2 * kW + 1) : 0;
   }
-  // its 11 rows x 11 columns as 4 aligned dwords per row (lane < 44), kept in a register until
-  // the window is staged in LDS for the SAD; a dword starting at or past w is not read
+  // its 11 rows x 11 columns as 4 aligned dwords per row (44: two per lane), kept in registers
+  // until the window is staged in LDS for the SAD; a dword starting at or past w is not read
   const int al = xl0 & ~3, lo = xl0 - al;
-  uint32_t lw = 0u;
-  if (ok && left_in && lane < (2 * kW + 1) * 4 && al + 4 * (lane & 3) < G.w)
-    lw = *(const uint32_t*)(PL + (int64_t)(y0 + (lane >> 2)) * pitch + al + 4 * (lane & 3));
+  uint32_t lw[2] = {0u, 0u};
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int i = hl + 32 * r;
+    if (ok && left_in && i < (2 * kW + 1) * 4 && al + 4 * (i & 3) < G.w)
+      lw[r] = *(const uint32_t*)(PL + (int64_t)(y0 + (i >> 2)) * pitch + al + 4 * (i & 3));
+  }
   if (ok) {
     const int c0 = P.row_off[row], c1 = P.row_off[row + 1];
     const uint64_t* q = (const uint64_t*)(P.dl + (int64_t)iL * 32);
     const uint64_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
     int key = INT_MAX;  // (distance << 16) | right index: first minimum in right-index order
     float ukey = 0.0f;  // the u of this lane's best key (no reload of the winner's keypoint)
-    for (int j = c0 + lane; j < c1; j += 64) {
+    for (int j = c0 + hl; j < c1; j += 32) {
       const uint2 e = P.row_ent[j];  // (index | octave << 16, x): no keypoint reload
       const int iR = (int)(e.x & 0xFFFFu), octR = (int)(e.x >> 16);
       if (octR < levelL - 1 || octR > levelL + 1) continue;
@@ -171,12 +186,11 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
         }
       }
     }
-    const int kmin = (int)wave_min_u32((uint32_t)key);  // key >= 0: the same minimum
+    const int kmin = (int)half_min_u32((uint32_t)key);  // key >= 0: the same minimum
     if (kmin != INT_MAX && (kmin >> 16) < bestDist) {
       bestDist = kmin >> 16;
-      const uint64_t who = __ballot(key == kmin);  // (distance, index) keys are unique
-      uR0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ukey),
-                                                                (int)__builtin_ctzll(who)));
+      const uint32_t who = (uint32_t)(__ballot(key == kmin) >> (lane & 32));  // unique keys
+      uR0 = __shfl(ukey, (lane & 32) + (int)__builtin_ctz(who));
     }
     ok = bestDist < kTH_HIGH;
   }
@@ -190,27 +204,29 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
     if (ok && (!left_in || xr - kL - kW < 0)) ok = false;
     if (ok) {
       // the right window's 11 rows x 21 columns (xr - 10 .. xr + 10, every shift) staged in
-      // this wave's LDS by aligned dword loads (6 per row, 66 in all), instead of 22 byte
-      // loads per lane over 11 rows each; dwords starting at or past w stay unread (the
-      // window ends at xr + 10 <= w - 2; the pitch is >= w + 4)
-      __shared__ uint32_t s_rw[4][2 * kW + 1][6];
-      __shared__ uint32_t s_lw[4][2 * kW + 1][4];
-      const int wv = threadIdx.x >> 6;
-      if (lane < (2 * kW + 1) * 4) s_lw[wv][lane >> 2][lane & 3] = lw;
+      // this half-wave's LDS by aligned dword loads (6 per row, 66 in all); dwords starting at
+      // or past w stay unread (the window ends at xr + 10 <= w - 2; the pitch is >= w + 4)
+      __shared__ uint32_t s_rw[8][2 * kW + 1][6];
+      __shared__ uint32_t s_lw[8][2 * kW + 1][4];
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const int i = hl + 32 * r;
+        if (i < (2 * kW + 1) * 4) s_lw[hw][i >> 2][i & 3] = lw[r];
+      }
       const int ar = (xr - 2 * kL) & ~3, ro = (xr - 2 * kL) - ar;  // ar >= 0: xr >= 10
-      for (int i = lane; i < (2 * kW + 1) * 6; i += 64) {  // 66 dwords: two rounds
+      for (int i = hl; i < (2 * kW + 1) * 6; i += 32) {  // 66 dwords: three rounds
         const int rr = i / 6, dw = i - rr * 6;
-        s_rw[wv][rr][dw] = ar + 4 * dw < G.w
+        s_rw[hw][rr][dw] = ar + 4 * dw < G.w
                                ? *(const uint32_t*)(PR + (int64_t)(y0 + rr) * pitch + ar + 4 * dw)
                                : 0u;
       }
       __builtin_amdgcn_wave_barrier();
-      const uint8_t* rw = (const uint8_t*)s_rw[wv];  // byte (row, c) at rw[row * 24 + c]
-      const uint8_t* lwb = (const uint8_t*)s_lw[wv];  // byte (row, c) at lwb[row * 16 + c]
+      const uint8_t* rw = (const uint8_t*)s_rw[hw];  // byte (row, c) at rw[row * 24 + c]
+      const uint8_t* lwb = (const uint8_t*)s_lw[hw];  // byte (row, c) at lwb[row * 16 + c]
       const int cL = lwb[kW * 16 + lo + kW];
-      int a[2];
+      int a[KP];
 #pragma unroll
-      for (int k = 0; k < 2; k++) a[k] = has[k] ? (int)lwb[yy[k] * 16 + lo + xx[k]] - cL : 0;
+      for (int k = 0; k < KP; k++) a[k] = has[k] ? (int)lwb[yy[k] * 16 + lo + xx[k]] - cL : 0;
       int vd[2 * kL + 1];
       int bestSad = INT_MAX, bestinc = 0;
 #pragma unroll
@@ -219,13 +235,13 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
         const int cR = rw[kW * 24 + ro + inc + 2 * kL];  // the shifted window's centre
         int acc = 0;
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < KP; k++) {
           if (has[k]) {
             const int b = (int)rw[yy[k] * 24 + ro + inc + kL + xx[k]] - cR;
             acc += abs(a[k] - b);
           }
         }
-        const int dist = wave_sum(acc);
+        const int dist = half_sum(acc);
         vd[inc + kL] = dist;
         if (dist < bestSad) {  // `(float)dist < bestDist(int)`: exact integers
           bestSad = dist;
@@ -255,7 +271,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
       }
     }
   }
-  if (lane == 0) {
+  if (live && hl == 0) {
     P.uright[iL] = uright;
     P.depth[iL] = depth;
     P.sad[iL] = sad_out;
@@ -322,7 +338,7 @@ int launch_stereo(const StereoProblem* d_probs, int nprob, const LevelGeom* d_lv
   if (nrows < 1 || (size_t)nrows * 4 > 64 * 1024 || kp_cap > 65535) return ORBX_EUNSUPPORTED;
   hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(256), (size_t)nrows * 4, s, d_probs, d_lv,
                      nrows, row_cap);
-  hipLaunchKernelGGL(k_stereo_match, dim3((kp_cap + 3) / 4, nprob), dim3(256), 0, s, d_probs,
+  hipLaunchKernelGGL(k_stereo_match, dim3((kp_cap + 7) / 8, nprob), dim3(256), 0, s, d_probs,
                      d_lv, nrows, mb, mbf);
   hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();
