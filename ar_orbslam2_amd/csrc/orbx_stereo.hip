@@ -92,34 +92,42 @@ __global__ __launch_bounds__(256) void k_stereo_rows(const StereoProblem* __rest
   }
 }
 
-// Sums and minima over the 32 lanes of a half-wave, in each of its lanes: 16-lane rows on DPP,
-// then the half's two rows by a swizzle (lanes 0-15 <-> 16-31 of each half).  Every lane of the
-// half-wave must be active; the other half's lanes are never read.
-__device__ __forceinline__ int half_sum(int v) {
+// kStG lanes per left keypoint, kStKP per workgroup (Frame::ComputeStereoMatches,
+// Frame.cc:471-643): the keypoint's chain of dependent loads (row band, candidates, the
+// windows) is latency, so several keypoints share a wave's issue slots; the candidate scan, the
+// 121 window pixels (eight per lane) and the SAD sums run on the keypoint's 16 lanes (DPP row
+// sums and minima).
+// lanes per left keypoint: 16 (C3 / C4 stereo 0.41 / 0.72 ms per 512 frames; a half-wave 0.52 /
+// 0.90, a wave 0.72 / 1.21), and keypoints per workgroup
+constexpr int kStG = 16;
+constexpr int kStKP = 256 / kStG;
+
+template <int G>
+__device__ __forceinline__ int grp_sum(int v) {
   v = row16_sum(v);
-  return v + __builtin_amdgcn_ds_swizzle(v, 0x401F);
+  if constexpr (G == 32) v += __builtin_amdgcn_ds_swizzle(v, 0x401F);
+  return v;
 }
-__device__ __forceinline__ uint32_t half_min_u32(uint32_t v) {
+template <int G>
+__device__ __forceinline__ uint32_t grp_min_u32(uint32_t v) {
   v = row16_min(v);
-  return min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F));
+  if constexpr (G == 32) v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F));
+  return v;
 }
 
-// One half-wave per left keypoint, eight per workgroup (Frame::ComputeStereoMatches,
-// Frame.cc:471-643): the keypoint's chain of dependent loads (row band, candidates, the
-// windows) is latency, so two keypoints share a wave's issue slots; the candidate scan, the 121
-// window pixels (four per lane) and the SAD sums run on the half's 32 lanes.
 __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __restrict__ probs,
                                                       const LevelGeom* __restrict__ lv,
                                                       int nrows, float mb, float mbf) {
-  constexpr int KP = ((2 * kW + 1) * (2 * kW + 1) + 31) / 32;  // window pixels per lane (4)
+  constexpr int NG = kStG;
+  constexpr int KP = ((2 * kW + 1) * (2 * kW + 1) + NG - 1) / NG;  // window pixels per lane
   const StereoProblem& P = probs[blockIdx.y];
-  const int lane = threadIdx.x & 63, hl = lane & 31;
-  const int hw = threadIdx.x >> 5;  // the workgroup's half-wave, 0..7
-  const int iL0 = blockIdx.x * 8 + ((threadIdx.x >> 6) << 1);  // the wave's first keypoint
+  const int lane = threadIdx.x & 63, hl = lane & (NG - 1);
+  const int hw = threadIdx.x / NG;  // the workgroup's keypoint group
+  const int iL0 = blockIdx.x * kStKP + (threadIdx.x >> 6) * (64 / NG);  // the wave's first keypoint
   const int nl = *P.nl;
   if (iL0 >= nl) return;  // wave-uniform
-  const int iL = iL0 + ((lane >> 5) & 1);
-  const bool live = iL < nl;  // uniform in the half-wave
+  const int iL = iL0 + (lane / NG);
+  const bool live = iL < nl;  // uniform in the keypoint's lanes
   const orbx_keypoint kpL = P.kl[live ? iL : iL0];
   float uright = -1.0f, depth = -1.0f;
   int sad_out = -1;
@@ -149,7 +157,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
   bool has[KP];
 #pragma unroll
   for (int k = 0; k < KP; k++) {
-    const int p = hl + 32 * k;
+    const int p = hl + NG * k;
     has[k] = p < (2 * kW + 1) * (2 * kW + 1);
     yy[k] = has[k] ? p / (2 * kW + 1) : 0;
     xx[k] = has[k] ? p - yy[k] * (2 * kW + 1) : 0;
@@ -157,10 +165,13 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
   // its 11 rows x 11 columns as 4 aligned dwords per row (44: two per lane), kept in registers
   // until the window is staged in LDS for the SAD; a dword starting at or past w is not read
   const int al = xl0 & ~3, lo = xl0 - al;
-  uint32_t lw[2] = {0u, 0u};
+  constexpr int KLW = ((2 * kW + 1) * 4 + NG - 1) / NG;
+  uint32_t lw[KLW];
 #pragma unroll
-  for (int r = 0; r < 2; r++) {
-    const int i = hl + 32 * r;
+  for (int r = 0; r < KLW; r++) lw[r] = 0u;
+#pragma unroll
+  for (int r = 0; r < KLW; r++) {
+    const int i = hl + NG * r;
     if (ok && left_in && i < (2 * kW + 1) * 4 && al + 4 * (i & 3) < G.w)
       lw[r] = *(const uint32_t*)(PL + (int64_t)(y0 + (i >> 2)) * pitch + al + 4 * (i & 3));
   }
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
     const uint64_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
     int key = INT_MAX;  // (distance << 16) | right index: first minimum in right-index order
     float ukey = 0.0f;  // the u of this lane's best key (no reload of the winner's keypoint)
-    for (int j = c0 + hl; j < c1; j += 32) {
+    for (int j = c0 + hl; j < c1; j += NG) {
       const uint2 e = P.row_ent[j];  // (index | octave << 16, x): no keypoint reload
       const int iR = (int)(e.x & 0xFFFFu), octR = (int)(e.x >> 16);
       if (octR < levelL - 1 || octR > levelL + 1) continue;
@@ -186,11 +197,12 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
         }
       }
     }
-    const int kmin = (int)half_min_u32((uint32_t)key);  // key >= 0: the same minimum
+    const int kmin = (int)grp_min_u32<NG>((uint32_t)key);  // key >= 0: the same minimum
     if (kmin != INT_MAX && (kmin >> 16) < bestDist) {
       bestDist = kmin >> 16;
-      const uint32_t who = (uint32_t)(__ballot(key == kmin) >> (lane & 32));  // unique keys
-      uR0 = __shfl(ukey, (lane & 32) + (int)__builtin_ctz(who));
+      const int gb = lane & ~(NG - 1);
+      const uint32_t who = (uint32_t)(__ballot(key == kmin) >> gb);  // unique keys
+      uR0 = __shfl(ukey, gb + (int)__builtin_ctz(who));
     }
     ok = bestDist < kTH_HIGH;
   }
@@ -204,17 +216,17 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
     if (ok && (!left_in || xr - kL - kW < 0)) ok = false;
     if (ok) {
       // the right window's 11 rows x 21 columns (xr - 10 .. xr + 10, every shift) staged in
-      // this half-wave's LDS by aligned dword loads (6 per row, 66 in all); dwords starting at
+      // this keypoint's LDS by aligned dword loads (6 per row, 66 in all); dwords starting at
       // or past w stay unread (the window ends at xr + 10 <= w - 2; the pitch is >= w + 4)
-      __shared__ uint32_t s_rw[8][2 * kW + 1][6];
-      __shared__ uint32_t s_lw[8][2 * kW + 1][4];
+      __shared__ uint32_t s_rw[kStKP][2 * kW + 1][6];
+      __shared__ uint32_t s_lw[kStKP][2 * kW + 1][4];
 #pragma unroll
-      for (int r = 0; r < 2; r++) {
-        const int i = hl + 32 * r;
+      for (int r = 0; r < KLW; r++) {
+        const int i = hl + NG * r;
         if (i < (2 * kW + 1) * 4) s_lw[hw][i >> 2][i & 3] = lw[r];
       }
       const int ar = (xr - 2 * kL) & ~3, ro = (xr - 2 * kL) - ar;  // ar >= 0: xr >= 10
-      for (int i = hl; i < (2 * kW + 1) * 6; i += 32) {  // 66 dwords: three rounds
+      for (int i = hl; i < (2 * kW + 1) * 6; i += NG) {  // 66 dwords
         const int rr = i / 6, dw = i - rr * 6;
         s_rw[hw][rr][dw] = ar + 4 * dw < G.w
                                ? *(const uint32_t*)(PR + (int64_t)(y0 + rr) * pitch + ar + 4 * dw)
@@ -241,7 +253,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoProblem* __res
             acc += abs(a[k] - b);
           }
         }
-        const int dist = half_sum(acc);
+        const int dist = grp_sum<NG>(acc);
         vd[inc + kL] = dist;
         if (dist < bestSad) {  // `(float)dist < bestDist(int)`: exact integers
           bestSad = dist;
@@ -338,7 +350,7 @@ int launch_stereo(const StereoProblem* d_probs, int nprob, const LevelGeom* d_lv
   if (nrows < 1 || (size_t)nrows * 4 > 64 * 1024 || kp_cap > 65535) return ORBX_EUNSUPPORTED;
   hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(256), (size_t)nrows * 4, s, d_probs, d_lv,
                      nrows, row_cap);
-  hipLaunchKernelGGL(k_stereo_match, dim3((kp_cap + 7) / 8, nprob), dim3(256), 0, s, d_probs,
+  hipLaunchKernelGGL(k_stereo_match, dim3((kp_cap + kStKP - 1) / kStKP, nprob), dim3(256), 0, s, d_probs,
                      d_lv, nrows, mb, mbf);
   hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();
