@@ -51,7 +51,7 @@ EXPORTS = [
     "orbx_marker_destroy", "orbx_marker_set_target", "orbx_marker_run", "orbx_marker_sync",
     "orbx_marker_results", "orbx_marker_outputs", "orbx_marker_stream", "orbx_marker_profile",
     "orbx_marker_profile_read", "orbx_marker_profile_kernels", "orbx_debug_cvorb_cossin", "orbx_debug_retain_best",
-    "orbx_debug_match_finish", "orbx_debug_sincosf", "orbx_debug_extractor_blur",
+    "orbx_debug_match_finish", "orbx_debug_bow_kernel", "orbx_debug_sincosf", "orbx_debug_extractor_blur",
     "orbx_debug_plan_level",
 ]
 

@@ -10,6 +10,7 @@
 //   k_tri_finish  rotation filter + ordered (idx1 ascending) pair compaction (:794-823)
 //   k_csr         FeatureVector build: stable bucket sort of feature indices by node id
 //                 (FeatureVector.cpp:31-45)
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1066,17 +1067,30 @@ __global__ void k_distance(const uint8_t* a, const uint8_t* b, int n, int* out) 
 // (ORBX_BOW_WG_PROBS overrides the limit for experiments)
 constexpr int kBowWgProbs = 4;
 
+namespace {
+std::atomic<int> g_bow_form{0};  // orbx_debug_bow_kernel: 0 = chosen per call
+}
+
 int launch_bow(const BowProblem* d_probs, int nprob, int max_nodes1, hipStream_t s,
                bool fused_finish, int feats_per_node) {
   if (nprob <= 0) return ORBX_OK;
-  const bool wg = max_nodes1 > 0 && nprob <= kBowWgProbs;
-  if (wg)
-    hipLaunchKernelGGL(k_bow_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
-  else if (max_nodes1 > 0 && feats_per_node >= kBowWideNode)
-    hipLaunchKernelGGL(k_bow_nodes<4>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
-  else if (max_nodes1 > 0)
-    hipLaunchKernelGGL(k_bow_nodes<kBowDescChunks>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256),
-                       0, s, d_probs);
+  // 1 the workgroup form (calls of few problems: the drop-in), else a wave per node with 4
+  // register chunks (2) for frames with many features per vocabulary node, or with 2 (3).
+  // (A 16- or 32-lane group per node, several nodes per wave, measured slower: 0.16-0.17 vs 0.115
+  // ms per 512 C2 frames — the group's per-feature broadcasts need ds_bpermute where the wave
+  // form's are readlanes.)
+  int form = g_bow_form.load(std::memory_order_relaxed);
+  if (form < 1 || form > 3) form = nprob <= kBowWgProbs ? 1 : feats_per_node >= kBowWideNode ? 2 : 3;
+  const bool wg = max_nodes1 > 0 && form == 1;
+  if (max_nodes1 > 0) {
+    if (form == 1)
+      hipLaunchKernelGGL(k_bow_nodes_wg, dim3(max_nodes1, nprob), dim3(256), 0, s, d_probs);
+    else if (form == 2)
+      hipLaunchKernelGGL(k_bow_nodes<4>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256), 0, s, d_probs);
+    else
+      hipLaunchKernelGGL(k_bow_nodes<kBowDescChunks>, dim3((max_nodes1 + 3) / 4, nprob), dim3(256),
+                         0, s, d_probs);
+  }
   if (!(wg && fused_finish))  // else the node kernel's last workgroup ran it
     hipLaunchKernelGGL(k_bow_finish, dim3(nprob), dim3(256), 0, s, d_probs);
   hipError_t e = hipGetLastError();
@@ -1773,6 +1787,12 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t n, int3
 // array, without the orientation check.  Out-of-range values are what a stale match array
 // would hold: the kernels must drop them (out[i] = -1) and report ORBX_EDEVICE, never read
 // through them.
+int orbx_debug_bow_kernel(int32_t form) {
+  if (form < 0 || form > 3) return ORBX_EINVAL;
+  g_bow_form.store(form, std::memory_order_relaxed);
+  return ORBX_OK;
+}
+
 int orbx_debug_match_finish(int32_t kind, int32_t n1, int32_t n2, const int32_t* match,
                             int32_t* out, int32_t* nmatches) {
   if (kind < 0 || kind > 2 || n1 < 0 || n2 < 0 || !match || !out || !nmatches) return ORBX_EINVAL;

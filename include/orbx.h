@@ -540,6 +540,11 @@ int orbx_debug_retain_best(float* resp, uint32_t* ids, int32_t n, int32_t n_poin
  * Used by tests/test_match_gpu.py. */
 int orbx_debug_match_finish(int32_t kind, int32_t n1, int32_t n2, const int32_t* match,
                             int32_t* out, int32_t* nmatches);
+/* The SearchByBoW node kernel every later call launches, process-wide: 0 chosen per call (the
+ * default: calls of at most 4 problems a workgroup per node, batches a wave per node), 1 a
+ * workgroup per node, 2 / 3 a wave per node with 4 / 2 register chunks.  Used by
+ * tests/test_match_gpu.py to run each form on the same inputs. */
+int orbx_debug_bow_kernel(int32_t form);
 /* The device glibc sincosf port of computeOrbDescriptor (ORBextractor.cc:103-104, orbx_math.h)
  * for the n floats whose bit patterns are lo, lo+1, ...; s / c host arrays of n.  Used by
  * tests/test_math_gpu.py (every float in [0, 2*pi] against the host libm). */

@@ -277,3 +277,25 @@ def test_finish_kernels_reject_stale_indices(kind):
     assert rc == -3  # ORBX_EDEVICE
     keep = np.where((bad >= 0) & (bad < other), bad, -1)
     assert np.array_equal(out, keep) and cnt.value == int((keep >= 0).sum())
+
+
+@pytest.mark.parametrize("form", [1, 2, 3])
+def test_search_by_bow_every_kernel_form(frames, form):
+    """Every SearchByBoW node kernel on the same inputs (orbx_debug_bow_kernel forces the form the
+    calls choose by problem count and features per node: 1 workgroup per node, 2 / 3 a wave with
+    4 / 2 register chunks — the batches' forms, otherwise reached only through the frame
+    pipeline): both overloads on real frames, contested small and large nodes (claim chains, ties,
+    invalid features) and a node of 1,500 candidates (register chunks and memory reads)."""
+    from ar_orbslam2_amd._ffi import check, lib
+    check("orbx_debug_bow_kernel", lib().orbx_debug_bow_kernel(form))
+    try:
+        kf, f, _ = frames
+        test_search_by_bow_kf_frame(frames, 0.7, True)
+        test_search_by_bow_kf_kf(frames, 0.75, True)
+        cases = [(10, 12, 2, False), (20, 30, 4, True), (90, 7, 2, False), (100, 128, 4, True),
+                 (130, 100, 16, False)]
+        for n1, n2, palette, chain in cases:
+            test_search_by_bow_contested_nodes(n1, n2, palette, chain)
+        test_search_by_bow_single_huge_node(1500)
+    finally:
+        lib().orbx_debug_bow_kernel(0)
