@@ -60,7 +60,8 @@ int launch_bowvec(int scoring, int weighting, const uint32_t* d_word_of,
                   int* d_nwords, int nimg, hipStream_t s);
 // BowVector (as launch_bowvec) and FeatureVector CSR (as launch_csr with id_lo 0 over
 // d_rank_ids) of every image in one launch (k_bowfv).  ORBX_EUNSUPPORTED when it does not apply
-// (more than 4096 features, ids too wide, no rank table, ORBX_BOWFV=0): the caller then runs
+// (more than 4096 features, or more than 2048 in a call of more than 4 images; ids too wide; no
+// rank table): the caller then runs
 // launch_bowvec + launch_csr.
 int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word_of,
                  const uint32_t* d_rank_of, const double* d_weight_of, int64_t in_stride,

@@ -10,7 +10,8 @@
 //                    in LDS, per-word weight sums in feature order (BowVector::addWeight /
 //                    addIfNotExist, BowVector.cpp:38-62), then the scoring's L1/L2
 //                    normalisation as one ordered pass (BowVector::normalize, :66-98)
-//   k_bowfv          one workgroup per image of up to 4096 features: the BowVector above and
+//   k_bowfv          one workgroup per image of up to 2048 features (4096 in calls of at most 4
+//                    images): the BowVector above and
 //                    the FeatureVector CSR together, from two in-register bitonic sorts merged
 //                    by rank (one launch instead of k_bowvec + k_csr)
 // Otherwise the FeatureVector CSR reuses k_csr (orbx_match.hip) over the node ranks built here.
@@ -716,7 +717,10 @@ int launch_bowfv(int scoring, int weighting, int n_words, const uint32_t* d_word
       nimg, s, ho
   if (fits(1024, 10)) return launch_bowfv_t<4>(ORBX_BOWFV_ARGS);
   if (fits(2048, 11)) return launch_bowfv_t<8>(ORBX_BOWFV_ARGS);
-  if (fits(4096, 12)) return launch_bowfv_t<16>(ORBX_BOWFV_ARGS);
+  // 16 keys per lane take every VGPR (512, and a few spilled): one wave per SIMD.  A call of a
+  // few images keeps it (a single frame's latency); batches of such frames take k_bowvec +
+  // k_csr instead (C5's line 46.7-46.8 k -> 47.4 k frames/s)
+  if (fits(4096, 12) && nimg <= 4) return launch_bowfv_t<16>(ORBX_BOWFV_ARGS);
 #undef ORBX_BOWFV_ARGS
   return ORBX_EUNSUPPORTED;
 }
